@@ -1,0 +1,254 @@
+"""oracle/oracle.py -- TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of the plain-C restatement in oracle/vrh_oracle.c (the parity checker) plus helpers
+that drive the reference harness oracle/_ref/vsnray_ref.  Only tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg import this module; the product path (visionaray_amd) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libvrh_oracle.so")
+REF_BIN = os.path.join(HERE, "_ref", "vsnray_ref")
+REF_BENCH_BIN = os.path.join(HERE, "_ref", "vsnray_ref_bench")
+
+TRI_DTYPE = np.dtype([("geom_id", "<u4"), ("prim_id", "<u4"), ("pad", "<u4", 2),
+                      ("v1", "<f4", 4), ("e1", "<f4", 4), ("e2", "<f4", 4)])
+SPHERE_DTYPE = np.dtype([("geom_id", "<u4"), ("prim_id", "<u4"), ("pad", "<u4", 2),
+                         ("center", "<f4", 4), ("radius", "<f4"), ("pad2", "<f4", 3)])
+NODE_DTYPE = np.dtype([("bmin", "<f4", 3), ("first", "<u4"), ("bmax", "<f4", 3), ("num_prims", "<u4")])
+assert TRI_DTYPE.itemsize == 64 and SPHERE_DTYPE.itemsize == 48 and NODE_DTYPE.itemsize == 32
+
+VO_TRI, VO_SPHERE = 0, 1
+VO_MODE_PRIMARY, VO_MODE_AO = 0, 1
+
+
+class _Bvh(C.Structure):
+    _fields_ = [("nodes", C.c_void_p), ("num_nodes", C.c_size_t),
+                ("indices", C.c_void_p), ("num_indices", C.c_size_t), ("max_depth", C.c_uint)]
+
+
+class _Counters(C.Structure):
+    _fields_ = [("box_tests", C.c_uint64), ("prim_tests", C.c_uint64)]
+
+
+class _Scene(C.Structure):
+    _fields_ = [("nodes", C.c_void_p), ("indices", C.c_void_p), ("prims", C.c_void_p),
+                ("kind", C.c_int), ("normals", C.c_void_p)]
+
+
+class _Camera(C.Structure):
+    _fields_ = [("eye", C.c_float * 3), ("cam_u", C.c_float * 3), ("cam_v", C.c_float * 3),
+                ("cam_w", C.c_float * 3), ("width", C.c_int), ("height", C.c_int)]
+
+
+class _Kernel(C.Structure):
+    _fields_ = [("mode", C.c_int), ("samples", C.c_int), ("radius", C.c_float), ("eps", C.c_float),
+                ("bg", C.c_float * 4)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE, "liboracle"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        vp, sz = C.c_void_p, C.c_size_t
+        L.vo_gen_cornell.argtypes = [vp]; L.vo_gen_cornell.restype = sz
+        L.vo_gen_heightfield.argtypes = [C.c_int, vp]; L.vo_gen_heightfield.restype = None
+        L.vo_gen_spheres.argtypes = [C.c_int, vp]; L.vo_gen_spheres.restype = None
+        L.vo_face_normals.argtypes = [vp, sz, vp]; L.vo_face_normals.restype = None
+        L.vo_build.argtypes = [vp, sz, C.c_int, C.POINTER(_Bvh)]; L.vo_build.restype = C.c_int
+        L.vo_bvh_free.argtypes = [C.POINTER(_Bvh)]; L.vo_bvh_free.restype = None
+        L.vo_camera_basis.argtypes = [C.POINTER(C.c_float)] * 3 + [C.c_float, C.c_float] + [C.POINTER(C.c_float)] * 3
+        L.vo_camera_basis.restype = None
+        L.vo_render_rows.argtypes = [C.POINTER(_Scene), C.POINTER(_Camera), C.POINTER(_Kernel), C.c_int, C.c_int,
+                                     vp, vp, vp, vp, vp, C.c_int, C.POINTER(_Counters)]
+        L.vo_render_rows.restype = C.c_uint64
+        L.vo_render_pixels.argtypes = [C.POINTER(_Scene), C.POINTER(_Camera), C.POINTER(_Kernel), vp, sz,
+                                       vp, vp, vp, vp, C.c_int]
+        L.vo_render_pixels.restype = C.c_uint64
+        L.vo_fnv1a.argtypes = [vp, sz, C.c_uint64]; L.vo_fnv1a.restype = C.c_uint64
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+# ---- scenes ------------------------------------------------------------
+
+SCENES = {
+    # name: (kind, param, eye, W, H)
+    "cornell12": (VO_TRI, 0, (0.0, 0.0, 3.4), 512, 512),
+    "hf1M": (VO_TRI, 708, (0.0, 0.9, 1.4), 1920, 1080),
+    "hf10M": (VO_TRI, 2236, (0.0, 0.9, 1.4), 1920, 1080),
+    "sph1M": (VO_SPHERE, 1000000, (0.0, 0.0, 3.5), 1920, 1080),
+}
+
+
+def scene_spec(name):
+    if name in SCENES:
+        return SCENES[name]
+    if name.startswith("hf"):
+        return (VO_TRI, int(name[2:]), (0.0, 0.9, 1.4), 1920, 1080)
+    if name.startswith("sph"):
+        return (VO_SPHERE, int(name[3:]), (0.0, 0.0, 3.5), 1920, 1080)
+    raise KeyError(name)
+
+
+def gen_prims(name):
+    kind, param, _, _, _ = scene_spec(name)
+    L = lib()
+    if kind == VO_TRI:
+        if param == 0:
+            a = np.zeros(12, TRI_DTYPE)
+            L.vo_gen_cornell(_p(a))
+        else:
+            a = np.zeros(2 * param * param, TRI_DTYPE)
+            L.vo_gen_heightfield(param, _p(a))
+    else:
+        a = np.zeros(param, SPHERE_DTYPE)
+        L.vo_gen_spheres(param, _p(a))
+    return kind, a
+
+
+def face_normals(tris):
+    out = np.zeros((len(tris), 4), np.float32)
+    lib().vo_face_normals(_p(tris), len(tris), _p(out))
+    return out
+
+
+def build_bvh(prims, kind):
+    b = _Bvh()
+    rc = lib().vo_build(_p(prims), len(prims), kind, C.byref(b))
+    if rc != 0:
+        raise RuntimeError("vo_build failed")
+    nodes = np.ctypeslib.as_array(C.cast(b.nodes, C.POINTER(C.c_uint32)), (b.num_nodes * 8,)).copy().view(NODE_DTYPE)
+    idx = np.ctypeslib.as_array(C.cast(b.indices, C.POINTER(C.c_uint32)), (b.num_indices,)).copy()
+    depth = b.max_depth
+    lib().vo_bvh_free(C.byref(b))
+    return nodes, idx, depth
+
+
+def camera_basis(eye, center, up, fovy, aspect):
+    f3 = C.c_float * 3
+    u, v, w = f3(), f3(), f3()
+    lib().vo_camera_basis(f3(*eye), f3(*center), f3(*up), C.c_float(fovy), C.c_float(aspect), u, v, w)
+    return (np.array(u[:], np.float32), np.array(v[:], np.float32), np.array(w[:], np.float32))
+
+
+def scene_camera(name, W=None, H=None):
+    """camera::perspective(45 deg, W/H) + look_at(eye, 0, +y), basis as simple_sched computes it."""
+    _, _, eye, W0, H0 = scene_spec(name)
+    W = W or W0
+    H = H or H0
+    fovy = np.float32(45.0) * np.float32(1.74532925199432957692369076849e-02)
+    aspect = np.float32(W) / np.float32(H)
+    u, v, w = camera_basis(eye, (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), float(fovy), float(aspect))
+    return np.array(eye, np.float32), u, v, w, W, H
+
+
+@dataclass
+class Scene:
+    name: str
+    kind: int
+    prims: np.ndarray
+    nodes: np.ndarray
+    indices: np.ndarray
+    normals: np.ndarray | None
+    max_depth: int
+
+
+def make_scene(name):
+    kind, prims = gen_prims(name)
+    nodes, idx, depth = build_bvh(prims, kind)
+    normals = face_normals(prims) if kind == VO_TRI else None
+    return Scene(name, kind, prims, nodes, idx, normals, depth)
+
+
+def _structs(scene, cam, mode, samples=8, radius=0.1, eps=1e-3, bg=(0.1, 0.2, 0.3, 1.0)):
+    s = _Scene(_p(scene.nodes).value, _p(scene.indices).value, _p(scene.prims).value, scene.kind,
+               _p(scene.normals).value if scene.normals is not None else None)
+    eye, u, v, w, W, H = cam
+    c = _Camera((C.c_float * 3)(*eye), (C.c_float * 3)(*u), (C.c_float * 3)(*v), (C.c_float * 3)(*w), W, H)
+    k = _Kernel(mode, samples, radius, eps, (C.c_float * 4)(*bg))
+    return s, c, k
+
+
+def render(scene, cam, mode=VO_MODE_AO, rows=None, threads=0, **kw):
+    """Full-image (or row range) oracle frame. Returns dict of arrays sized W*H."""
+    _, _, _, _, W, H = cam
+    y0, y1 = rows if rows else (0, H)
+    out = {
+        "color": np.zeros((H * W, 4), np.float32),
+        "prim_id": np.full(H * W, 0xFFFFFFFF, np.uint32),
+        "t": np.full(H * W, -1.0, np.float32),
+        "occ": np.zeros(H * W, np.uint8),
+        "list_index": np.full(H * W, 0xFFFFFFFF, np.uint32),
+    }
+    s, c, k = _structs(scene, cam, mode, **kw)
+    cnt = _Counters()
+    rays = lib().vo_render_rows(C.byref(s), C.byref(c), C.byref(k), y0, y1, _p(out["color"]), _p(out["prim_id"]),
+                                _p(out["t"]), _p(out["occ"]), _p(out["list_index"]), threads, C.byref(cnt))
+    out["rays"] = int(rays)
+    out["box_tests"] = int(cnt.box_tests)
+    out["prim_tests"] = int(cnt.prim_tests)
+    return out
+
+
+def render_pixels(scene, cam, pixels, mode=VO_MODE_AO, threads=0, **kw):
+    pixels = np.ascontiguousarray(pixels, np.uint32)
+    n = len(pixels)
+    out = {
+        "color": np.zeros((n, 4), np.float32),
+        "prim_id": np.zeros(n, np.uint32),
+        "t": np.zeros(n, np.float32),
+        "occ": np.zeros(n, np.uint8),
+    }
+    s, c, k = _structs(scene, cam, mode, **kw)
+    out["rays"] = int(lib().vo_render_pixels(C.byref(s), C.byref(c), C.byref(k), _p(pixels), n, _p(out["color"]),
+                                             _p(out["prim_id"]), _p(out["t"]), _p(out["occ"]), threads))
+    return out
+
+
+def fnv1a(arr):
+    a = np.ascontiguousarray(arr)
+    return "%016x" % lib().vo_fnv1a(_p(a), a.nbytes, 0)
+
+
+# ---- reference harness (oracle/_ref) -----------------------------------------------------------
+
+def ref_available():
+    return os.path.exists(REF_BIN)
+
+
+def ref_golden(name, outdir, W=None, H=None):
+    args = [REF_BIN, "golden", name, outdir] + ([str(W), str(H)] if W else [])
+    r = subprocess.run(args, check=True, capture_output=True, text=True)
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def ref_bench(name, threads, frames, W=None, H=None, samples=None, timeout=600):
+    args = [REF_BENCH_BIN, "bench", name, str(threads), str(frames)]
+    if W:
+        args += [str(W), str(H)]
+        if samples is not None:
+            args += [str(samples)]
+    r = subprocess.run(args, check=True, capture_output=True, text=True, timeout=timeout)
+    return json.loads(r.stdout.strip().splitlines()[-1])

@@ -1,0 +1,469 @@
+// oracle/ref_harness.cpp -- TEST INFRASTRUCTURE ONLY (never shipped, never measured as product).
+//
+// Drives the *reference* Visionaray headers (compiled in place from /root/reference/include by
+// oracle/Makefile; no reference source is copied into this repository) to produce:
+//
+//   golden <scene> <outdir> [W H]  : reference BVH (build<index_bvh<P>>, build.inl:165-178), the
+//                                    scalar simple_sched<basic_ray<float>> frame (simple_sched.inl:
+//                                    139-151) of primary closest_hit (traverse_linear.inl:286-329) and
+//                                    the parity version of the ao/main.cpp:183-246 kernel (SURVEY.md
+//                                    Appendix A), written as raw little-endian arrays + hashes.
+//   bench  <scene> <threads> <frames> [W H] [samples]
+//                                  : the reference SSE4 CPU path, tiled_sched<basic_ray<simd::float4>>
+//                                    (tiled_sched.inl:365-391) running the ao/main.cpp:183-246 kernel
+//                                    verbatim in behaviour (random_sampler + cosine_sample_hemisphere),
+//                                    timed; prints one JSON line (Mrays/s, rays, cores).
+//
+// The synthetic scenes follow SURVEY.md Appendix A (libm-free, fixed seeds).  This file is the only
+// place that instantiates reference code; outputs land in oracle/_ref/ or a caller-given directory.
+
+#include <visionaray/math/math.h>
+#include <visionaray/bvh.h>
+#include <visionaray/camera.h>
+#include <visionaray/get_normal.h>
+#include <visionaray/result_record.h>
+#include <visionaray/sampling.h>
+#include <visionaray/random_sampler.h>
+#include <visionaray/scheduler.h>
+#include <visionaray/simple_buffer_rt.h>
+#include <visionaray/traverse.h>
+
+#include <atomic>
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+using namespace visionaray;
+
+using tri_t = basic_triangle<3, float>;
+using sph_t = basic_sphere<float>;
+
+//-------------------------------------------------------------------------------------------------
+// Appendix A scene generators
+//
+
+static inline uint32_t wang(uint32_t a)
+{
+    a = (a ^ 61u) ^ (a >> 16);
+    a = a + (a << 3);
+    a = a ^ (a >> 4);
+    a = a * 0x27d4eb2du;
+    a = a ^ (a >> 15);
+    return a;
+}
+
+static inline float U(uint32_t k)
+{
+    return float(wang(k) >> 8) * (1.0f / 16777216.0f);
+}
+
+static vec3 hf_vertex(int grid, int i, int j)
+{
+    float x = -1.0f + 2.0f * float(i) / float(grid);
+    float z = -1.0f + 2.0f * float(j) / float(grid);
+    uint32_t k = uint32_t(j) * uint32_t(grid + 1) + uint32_t(i);
+    float y = 0.3f * x * z * (1.0f - x * x) * (1.0f - z * z) + 0.004f * (U(k) - 0.5f);
+    return vec3(x, y, z);
+}
+
+static void make_heightfield(int grid, aligned_vector<tri_t>& tris)
+{
+    tris.resize(size_t(2) * grid * grid);
+    std::vector<vec3> row0(grid + 1), row1(grid + 1);
+    for (int j = 0; j < grid; ++j)
+    {
+        for (int i = 0; i <= grid; ++i) { row0[i] = hf_vertex(grid, i, j); row1[i] = hf_vertex(grid, i, j + 1); }
+        for (int i = 0; i < grid; ++i)
+        {
+            vec3 a = row0[i], b = row0[i + 1], c = row1[i + 1], e = row1[i];
+            size_t base = size_t(2) * (size_t(j) * grid + i);
+            tri_t& t0 = tris[base];
+            t0.v1 = a; t0.e1 = b - a; t0.e2 = c - a; t0.prim_id = unsigned(base); t0.geom_id = 0;
+            tri_t& t1 = tris[base + 1];
+            t1.v1 = a; t1.e1 = c - a; t1.e2 = e - a; t1.prim_id = unsigned(base + 1); t1.geom_id = 0;
+        }
+    }
+}
+
+static void make_cornell(aligned_vector<tri_t>& tris)
+{
+    const float q[6][4][3] = {
+        {{-1,-1,-1},{ 1,-1,-1},{ 1,-1, 1},{-1,-1, 1}},
+        {{-1, 1,-1},{-1, 1, 1},{ 1, 1, 1},{ 1, 1,-1}},
+        {{-1,-1,-1},{-1, 1,-1},{ 1, 1,-1},{ 1,-1,-1}},
+        {{-1,-1,-1},{-1,-1, 1},{-1, 1, 1},{-1, 1,-1}},
+        {{ 1,-1,-1},{ 1, 1,-1},{ 1, 1, 1},{ 1,-1, 1}},
+        {{-.25f,.99f,-.25f},{-.25f,.99f,.25f},{.25f,.99f,.25f},{.25f,.99f,-.25f}},
+    };
+    tris.clear();
+    for (int f = 0; f < 6; ++f)
+    {
+        vec3 a(q[f][0]), b(q[f][1]), c(q[f][2]), d(q[f][3]);
+        tri_t t;
+        t.geom_id = 0;
+        t.v1 = a; t.e1 = b - a; t.e2 = c - a; t.prim_id = unsigned(tris.size()); tris.push_back(t);
+        t.v1 = a; t.e1 = c - a; t.e2 = d - a; t.prim_id = unsigned(tris.size()); tris.push_back(t);
+    }
+}
+
+static void make_spheres(int n, aligned_vector<sph_t>& s)
+{
+    s.resize(n);
+    for (int i = 0; i < n; ++i)
+    {
+        uint32_t k = uint32_t(6) * uint32_t(i);
+        s[i].center = vec3(2.0f * U(k) - 1.0f, 2.0f * U(k + 1) - 1.0f, 2.0f * U(k + 2) - 1.0f);
+        s[i].radius = 0.002f + 0.008f * U(k + 3);
+        s[i].prim_id = unsigned(i);
+        s[i].geom_id = 0;
+    }
+}
+
+//-------------------------------------------------------------------------------------------------
+// Hashing (FNV-1a 64; SURVEY.md Appendix B conventions)
+//
+
+struct fnv
+{
+    uint64_t h = 0xcbf29ce484222325ull;
+    void bytes(void const* p, size_t n)
+    {
+        auto b = static_cast<unsigned char const*>(p);
+        for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 0x100000001b3ull; }
+    }
+    void u32(uint32_t w) { bytes(&w, 4); }
+};
+
+static void write_file(std::string const& path, void const* p, size_t n)
+{
+    FILE* f = fopen(path.c_str(), "wb");
+    if (!f) { perror(path.c_str()); exit(2); }
+    if (n && fwrite(p, 1, n, f) != n) { perror("fwrite"); exit(2); }
+    fclose(f);
+}
+
+static uint32_t fbits(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+
+//-------------------------------------------------------------------------------------------------
+// Scene description
+//
+
+struct scene_desc
+{
+    std::string name;
+    bool spheres = false;
+    int  grid = 0;        // heightfield grid, 0 = cornell
+    int  nspheres = 0;
+    vec3 eye;
+    int  W = 1920, H = 1080;
+};
+
+static scene_desc lookup(std::string const& name)
+{
+    scene_desc d;
+    d.name = name;
+    if (name == "cornell12") { d.grid = 0; d.eye = vec3(0.0f, 0.0f, 3.4f); d.W = 512; d.H = 512; }
+    else if (name == "hf1M")  { d.grid = 708;  d.eye = vec3(0.0f, 0.9f, 1.4f); }
+    else if (name == "hf10M") { d.grid = 2236; d.eye = vec3(0.0f, 0.9f, 1.4f); }
+    else if (name == "sph1M") { d.spheres = true; d.nspheres = 1000000; d.eye = vec3(0.0f, 0.0f, 3.5f); }
+    else if (name.compare(0, 2, "hf") == 0) { d.grid = atoi(name.c_str() + 2); d.eye = vec3(0.0f, 0.9f, 1.4f); }
+    else if (name.compare(0, 3, "sph") == 0) { d.spheres = true; d.nspheres = atoi(name.c_str() + 3); d.eye = vec3(0.0f, 0.0f, 3.5f); }
+    else { fprintf(stderr, "unknown scene %s\n", name.c_str()); exit(2); }
+    return d;
+}
+
+static camera make_camera(scene_desc const& d, int W, int H)
+{
+    camera cam;
+    float aspect = W / static_cast<float>(H);
+    cam.perspective(45.0f * constants::degrees_to_radians<float>(), aspect, 0.001f, 1000.0f);
+    cam.look_at(d.eye, vec3(0.0f, 0.0f, 0.0f), vec3(0.0f, 1.0f, 0.0f));
+    return cam;
+}
+
+//-------------------------------------------------------------------------------------------------
+// golden: scalar simple_sched frame, primary closest hit + parity AO
+//
+
+template <typename P>
+static int run_golden(scene_desc const& d, aligned_vector<P>& prims, std::vector<vec3> const& normals,
+                      std::string const& outdir, int W, int H, bool do_ao)
+{
+    auto t0 = std::chrono::steady_clock::now();
+    auto bvh = build<index_bvh<P>>(prims.data(), prims.size());
+    auto t1 = std::chrono::steady_clock::now();
+
+    fnv hn, hi;
+    unsigned max_depth = 0;
+    for (auto const& n : bvh.nodes()) { uint32_t w[8]; std::memcpy(w, &n, 32); for (int k = 0; k < 8; ++k) hn.u32(w[k]); }
+    for (auto i : bvh.indices()) hi.u32(i);
+    {
+        // tree depth (root depth 0), for stack-size planning
+        std::vector<std::pair<unsigned, unsigned>> st{{0u, 0u}};
+        while (!st.empty())
+        {
+            auto e = st.back(); st.pop_back();
+            max_depth = std::max(max_depth, e.second);
+            auto const& n = bvh.nodes()[e.first];
+            if (n.num_prims == 0) { st.push_back({n.first_child, e.second + 1}); st.push_back({n.first_child + 1, e.second + 1}); }
+        }
+    }
+    write_file(outdir + "/nodes.bin", bvh.nodes().data(), bvh.nodes().size() * sizeof(bvh_node));
+    write_file(outdir + "/indices.bin", bvh.indices().data(), bvh.indices().size() * 4);
+    write_file(outdir + "/prims.bin", prims.data(), prims.size() * sizeof(P));
+
+    camera cam = make_camera(d, W, H);
+
+    // camera basis exactly as simple_sched.inl:61-89 computes it (recorded as bits)
+    auto f = normalize(cam.eye() - cam.center());
+    auto s = normalize(cross(cam.up(), f));
+    auto u = cross(f, s);
+    vec3 cam_u = s * float(tan(cam.fovy() / 2.0f) * cam.aspect());
+    vec3 cam_v = u * float(tan(cam.fovy() / 2.0f));
+    vec3 cam_w = -f;
+    vec3 basis[4] = { cam.eye(), cam_u, cam_v, cam_w };
+    write_file(outdir + "/camera.bin", basis, sizeof(basis));
+
+    size_t npx = size_t(W) * H;
+    std::vector<uint32_t> prim_id(npx, 0xFFFFFFFFu);
+    std::vector<float> tval(npx, -1.0f);
+    std::vector<uint8_t> occ(npx, 0);
+    std::vector<uint32_t> leaf_pos(npx, 0xFFFFFFFFu);
+
+    using bvh_ref = typename index_bvh<P>::bvh_ref;
+    std::vector<bvh_ref> bvhs{ bvh.ref() };
+    auto prims_begin = bvhs.data();
+    auto prims_end = bvhs.data() + bvhs.size();
+
+    simple_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> rt;
+    rt.resize(W, H);
+    auto sparams = make_sched_params(pixel_sampler::uniform_type{}, cam, rt);
+    simple_sched<ray> sched;
+
+    uint64_t ao_rays = 0, ao_occ = 0;
+    const vec4 bg(0.1f, 0.2f, 0.3f, 1.0f);
+
+    sched.frame([&](ray r, unsigned x, unsigned y) -> result_record<float>
+    {
+        result_record<float> result;
+        result.color = bg;
+        auto hr = closest_hit(r, prims_begin, prims_end);
+        result.hit = hr.hit;
+        size_t p = size_t(y) * W + x;
+        if (!hr.hit) return result;
+        prim_id[p] = hr.prim_id;
+        tval[p] = hr.t;
+        leaf_pos[p] = hr.primitive_list_index;
+        if (!do_ao) { result.color = vec4(1.0f); return result; }
+
+        hr.isect_pos = r.ori + r.dir * hr.t;
+        vec4 clr(1.0f);
+        vec3 n = normals[hr.prim_id];
+        vec3 uu, vv, w = n;
+        make_orthonormal_basis(uu, vv, w);
+        uint8_t mask = 0;
+        for (int smp = 0; smp < 8; ++smp)
+        {
+            float sx = 0.0f, sy = 0.0f;
+            for (uint32_t k = 0; k < 16; ++k)
+            {
+                uint32_t ctr = ((uint32_t(p) * 8u + uint32_t(smp)) * 16u + k) * 2u;
+                float xa = 2.0f * U(ctr) - 1.0f;
+                float ya = 2.0f * U(ctr + 1) - 1.0f;
+                if (xa * xa + ya * ya < 1.0f) { sx = xa; sy = ya; break; }
+            }
+            float sz = sqrt(std::max(0.0f, 1.0f - sx * sx - sy * sy));
+            auto dir = normalize(sx * uu + sy * vv + sz * w);
+            ray ao;
+            ao.ori = hr.isect_pos + dir * 1E-3f;
+            ao.dir = dir;
+            auto ar = any_hit(ao, prims_begin, prims_end, 0.1f);
+            ++ao_rays;
+            if (ar.hit) { clr = clr - 1.0f / 8; mask |= uint8_t(1u << smp); ++ao_occ; }
+        }
+        occ[p] = mask;
+        result.color = vec4(clr.xyz(), 1.0f);
+        return result;
+    }, sparams);
+    auto t2 = std::chrono::steady_clock::now();
+
+    write_file(outdir + "/prim_id.bin", prim_id.data(), npx * 4);
+    write_file(outdir + "/t.bin", tval.data(), npx * 4);
+    write_file(outdir + "/leaf_pos.bin", leaf_pos.data(), npx * 4);
+    write_file(outdir + "/color.bin", rt.color(), npx * 16);
+    if (do_ao) write_file(outdir + "/occ.bin", occ.data(), npx);
+
+    fnv hp, ht, ho, hc;
+    uint64_t hits = 0;
+    for (size_t p = 0; p < npx; ++p)
+    {
+        hp.u32(prim_id[p]); ht.u32(fbits(tval[p])); ho.bytes(&occ[p], 1);
+        hits += prim_id[p] != 0xFFFFFFFFu;
+    }
+    hc.bytes(rt.color(), npx * 16);
+
+    printf("{\"scene\":\"%s\",\"W\":%d,\"H\":%d,\"prims\":%zu,\"nodes\":%zu,\"max_depth\":%u,"
+           "\"bvh_hash\":\"%016llx\",\"idx_hash\":\"%016llx\",\"hits\":%llu,\"ao_rays\":%llu,\"ao_occluded\":%llu,"
+           "\"primid_hash\":\"%016llx\",\"t_hash\":\"%016llx\",\"occmask_hash\":\"%016llx\",\"color_hash\":\"%016llx\","
+           "\"cam_u\":[\"%08x\",\"%08x\",\"%08x\"],\"cam_v\":[\"%08x\",\"%08x\",\"%08x\"],\"cam_w\":[\"%08x\",\"%08x\",\"%08x\"],"
+           "\"build_s\":%.3f,\"render_s\":%.3f}\n",
+           d.name.c_str(), W, H, prims.size(), bvh.nodes().size(), max_depth,
+           (unsigned long long)hn.h, (unsigned long long)hi.h, (unsigned long long)hits,
+           (unsigned long long)ao_rays, (unsigned long long)ao_occ,
+           (unsigned long long)hp.h, (unsigned long long)ht.h, (unsigned long long)ho.h, (unsigned long long)hc.h,
+           fbits(cam_u.x), fbits(cam_u.y), fbits(cam_u.z), fbits(cam_v.x), fbits(cam_v.y), fbits(cam_v.z),
+           fbits(cam_w.x), fbits(cam_w.y), fbits(cam_w.z),
+           std::chrono::duration<double>(t1 - t0).count(), std::chrono::duration<double>(t2 - t1).count());
+    return 0;
+}
+
+//-------------------------------------------------------------------------------------------------
+// bench: reference SSE4 tiled_sched<ray4> path, ao/main.cpp kernel
+//
+
+template <typename P>
+static int run_bench(scene_desc const& d, aligned_vector<P>& prims, std::vector<vec3> const& normals,
+                     int threads, int frames, int W, int H, int samples)
+{
+    using R = basic_ray<simd::float4>;
+    using S = R::scalar_type;
+    using C = vector<4, S>;
+    using V = vector<3, S>;
+
+    auto bvh = build<index_bvh<P>>(prims.data(), prims.size());
+    camera cam = make_camera(d, W, H);
+
+    using bvh_ref = typename index_bvh<P>::bvh_ref;
+    std::vector<bvh_ref> bvhs{ bvh.ref() };
+    auto prims_begin = bvhs.data();
+    auto prims_end = bvhs.data() + bvhs.size();
+
+    simple_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> rt;
+    rt.resize(W, H);
+    auto sparams = make_sched_params(pixel_sampler::uniform_type{}, cam, rt);
+    tiled_sched<R> sched(threads);
+    // tiled_sched can lose the wakeup of a worker that is not waiting yet (tiled_sched.inl:181,386)
+    std::this_thread::sleep_for(std::chrono::milliseconds(300));
+
+    std::atomic<uint64_t> rays{0};
+    float radius = 0.1f;
+    auto kernel = [&](R ray, random_sampler<S>& samp) -> result_record<S>
+    {
+        result_record<S> result;
+        result.color = C(vec4(0.1f, 0.2f, 0.3f, 1.0f));
+        auto hit_rec = closest_hit(ray, prims_begin, prims_end);
+        result.hit = hit_rec.hit;
+        uint64_t local = 4;
+        if (samples > 0 && any(hit_rec.hit))
+        {
+            hit_rec.isect_pos = ray.ori + ray.dir * hit_rec.t;
+            C clr(1.0);
+            V n;
+            if (!d.spheres)
+                n = get_normal(normals.data(), hit_rec, index_bvh<tri_t>{}, normals_per_face_binding{});
+            else
+                n = V(vec3(0.0f, 1.0f, 0.0f));
+            V u, v, w = n;
+            make_orthonormal_basis(u, v, w);
+            alignas(16) float hf[4];
+            simd::store(hf, select(hit_rec.hit, S(1.0f), S(0.0f)));
+            int nh = int(hf[0] + hf[1] + hf[2] + hf[3]);
+            for (int i = 0; i < samples; ++i)
+            {
+                auto sp = cosine_sample_hemisphere(samp.next(), samp.next());
+                auto dir = normalize(sp.x * u + sp.y * v + sp.z * w);
+                R ao_ray;
+                ao_ray.ori = hit_rec.isect_pos + dir * S(1E-3f);
+                ao_ray.dir = dir;
+                auto ao_rec = any_hit(ao_ray, prims_begin, prims_end, S(radius));
+                clr = select(ao_rec.hit, clr - S(1.0f / samples), clr);
+            }
+            local += uint64_t(nh) * samples;
+            result.color = select(hit_rec.hit, C(clr.xyz(), S(1.0)), result.color);
+        }
+        rays.fetch_add(local, std::memory_order_relaxed);
+        return result;
+    };
+
+    sched.frame(kernel, sparams);  // warm-up
+    std::vector<double> times;
+    uint64_t rays_per_frame = 0;
+    for (int f = 0; f < frames; ++f)
+    {
+        rays = 0;
+        auto t0 = std::chrono::steady_clock::now();
+        sched.frame(kernel, sparams);
+        auto t1 = std::chrono::steady_clock::now();
+        times.push_back(std::chrono::duration<double>(t1 - t0).count());
+        rays_per_frame = rays.load();
+    }
+    std::sort(times.begin(), times.end());
+    double med = times[times.size() / 2];
+    printf("{\"kind\":\"reference\",\"path\":\"tiled_sched<basic_ray<simd::float4>> -O3 -msse4.1\",\"scene\":\"%s\","
+           "\"W\":%d,\"H\":%d,\"samples\":%d,\"threads\":%d,\"frames\":%d,\"rays_per_frame\":%llu,"
+           "\"median_s\":%.6f,\"mrays_per_s\":%.3f}\n",
+           d.name.c_str(), W, H, samples, threads, frames, (unsigned long long)rays_per_frame, med,
+           rays_per_frame / med / 1e6);
+    return 0;
+}
+
+//-------------------------------------------------------------------------------------------------
+
+template <typename F>
+static int with_scene(scene_desc const& d, F&& f)
+{
+    if (d.spheres)
+    {
+        aligned_vector<sph_t> s;
+        make_spheres(d.nspheres, s);
+        std::vector<vec3> normals;
+        return f(s, normals);
+    }
+    aligned_vector<tri_t> t;
+    if (d.grid == 0) make_cornell(t); else make_heightfield(d.grid, t);
+    std::vector<vec3> normals(t.size());
+    for (size_t i = 0; i < t.size(); ++i) normals[i] = normalize(cross(t[i].e1, t[i].e2));
+    return f(t, normals);
+}
+
+int main(int argc, char** argv)
+{
+    if (argc < 3)
+    {
+        fprintf(stderr, "usage: %s golden <scene> <outdir> [W H]\n"
+                        "       %s bench <scene> <threads> <frames> [W H] [samples]\n", argv[0], argv[0]);
+        return 2;
+    }
+    std::string mode = argv[1];
+    scene_desc d = lookup(argv[2]);
+    if (mode == "golden")
+    {
+        if (argc < 4) return 2;
+        std::string outdir = argv[3];
+        int W = argc > 5 ? atoi(argv[4]) : d.W;
+        int H = argc > 5 ? atoi(argv[5]) : d.H;
+        return with_scene(d, [&](auto& prims, std::vector<vec3> const& normals)
+        {
+            return run_golden(d, prims, normals, outdir, W, H, !d.spheres);
+        });
+    }
+    if (mode == "bench")
+    {
+        int threads = argc > 3 ? atoi(argv[3]) : int(std::thread::hardware_concurrency());
+        int frames = argc > 4 ? atoi(argv[4]) : 5;
+        int W = argc > 6 ? atoi(argv[5]) : d.W;
+        int H = argc > 6 ? atoi(argv[6]) : d.H;
+        int samples = argc > 7 ? atoi(argv[7]) : (d.spheres ? 0 : 8);
+        return with_scene(d, [&](auto& prims, std::vector<vec3> const& normals)
+        {
+            return run_bench(d, prims, normals, threads, frames, W, H, samples);
+        });
+    }
+    return 2;
+}

@@ -1,0 +1,614 @@
+/*
+ * oracle/vrh_oracle.c -- TEST INFRASTRUCTURE ONLY (see vrh_oracle.h).
+ *
+ * Plain-C restatement of the reference algorithm for the hot path.  Compiled with
+ * -O2 -ffp-contract=off (no FMA contraction: SURVEY.md §7 hard part 1), float arithmetic in
+ * exactly the reference's operation order.  Every function cites the reference file:line it
+ * restates.  Parity of this file against the reference is checked by tests/test_oracle.py
+ * (against oracle/_ref/vsnray_ref when built, and against the committed tests/golden fixtures).
+ */
+#include "vrh_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ------------------------------------------------------------------------------------------ */
+/* math/detail/math.h:48-60  min(x,y) = x<y?x:y, max(x,y) = x<y?y:x  (NaN follows the ternary)   */
+static inline float fmin_ref(float x, float y) { return x < y ? x : y; }
+static inline float fmax_ref(float x, float y) { return x < y ? y : x; }
+
+typedef struct { float x, y, z; } v3;
+static inline v3 mk(float x, float y, float z) { v3 r = { x, y, z }; return r; }
+static inline v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 mul(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline v3 muls(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+static inline v3 smul(float s, v3 a) { return mk(s * a.x, s * a.y, s * a.z); }
+/* vector3.inl:291-301 */
+static inline v3 cross(v3 u, v3 v) { return mk(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x); }
+/* vector3.inl:303-307  (x*x + y*y) + z*z */
+static inline float dot(v3 u, v3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
+/* vector3.inl:331-336 + math.h:477-481  v * (1/sqrt(dot(v,v))) */
+static inline v3 normalize(v3 v) { return muls(v, 1.0f / sqrtf(dot(v, v))); }
+static inline v3 ld(const vo_vec3* p) { return mk(p->x, p->y, p->z); }
+static inline void st(vo_vec3* p, v3 v) { p->x = v.x; p->y = v.y; p->z = v.z; p->pad = 0.0f; }
+static inline float comp(v3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+
+/* ------------------------------------------------------------------------------------------ */
+/* SURVEY.md Appendix A                                                                        */
+uint32_t vo_wang(uint32_t a)
+{
+    a = (a ^ 61u) ^ (a >> 16);
+    a = a + (a << 3);
+    a = a ^ (a >> 4);
+    a = a * 0x27d4eb2du;
+    a = a ^ (a >> 15);
+    return a;
+}
+
+float vo_uniform(uint32_t k) { return (float)(vo_wang(k) >> 8) * (1.0f / 16777216.0f); }
+
+static void set_tri(vo_tri* t, v3 a, v3 b, v3 c, uint32_t prim_id)
+{
+    memset(t, 0, sizeof(*t));
+    t->geom_id = 0;
+    t->prim_id = prim_id;
+    st(&t->v1, a);
+    st(&t->e1, sub(b, a));
+    st(&t->e2, sub(c, a));
+}
+
+size_t vo_gen_cornell(vo_tri* out)
+{
+    static const float q[6][4][3] = {
+        {{-1,-1,-1},{ 1,-1,-1},{ 1,-1, 1},{-1,-1, 1}},
+        {{-1, 1,-1},{-1, 1, 1},{ 1, 1, 1},{ 1, 1,-1}},
+        {{-1,-1,-1},{-1, 1,-1},{ 1, 1,-1},{ 1,-1,-1}},
+        {{-1,-1,-1},{-1,-1, 1},{-1, 1, 1},{-1, 1,-1}},
+        {{ 1,-1,-1},{ 1, 1,-1},{ 1, 1, 1},{ 1,-1, 1}},
+        {{-.25f,.99f,-.25f},{-.25f,.99f,.25f},{.25f,.99f,.25f},{.25f,.99f,-.25f}},
+    };
+    size_t n = 0;
+    for (int f = 0; f < 6; ++f) {
+        v3 a = mk(q[f][0][0], q[f][0][1], q[f][0][2]);
+        v3 b = mk(q[f][1][0], q[f][1][1], q[f][1][2]);
+        v3 c = mk(q[f][2][0], q[f][2][1], q[f][2][2]);
+        v3 d = mk(q[f][3][0], q[f][3][1], q[f][3][2]);
+        set_tri(&out[n], a, b, c, (uint32_t)n); ++n;
+        set_tri(&out[n], a, c, d, (uint32_t)n); ++n;
+    }
+    return n;
+}
+
+static v3 hf_vertex(int grid, int i, int j)
+{
+    float x = -1.0f + 2.0f * (float)i / (float)grid;
+    float z = -1.0f + 2.0f * (float)j / (float)grid;
+    uint32_t k = (uint32_t)j * (uint32_t)(grid + 1) + (uint32_t)i;
+    float y = 0.3f * x * z * (1.0f - x * x) * (1.0f - z * z) + 0.004f * (vo_uniform(k) - 0.5f);
+    return mk(x, y, z);
+}
+
+void vo_gen_heightfield(int grid, vo_tri* out)
+{
+    #pragma omp parallel for schedule(static)
+    for (int j = 0; j < grid; ++j) {
+        for (int i = 0; i < grid; ++i) {
+            v3 a = hf_vertex(grid, i, j), b = hf_vertex(grid, i + 1, j);
+            v3 c = hf_vertex(grid, i + 1, j + 1), e = hf_vertex(grid, i, j + 1);
+            size_t base = (size_t)2 * ((size_t)j * grid + i);
+            set_tri(&out[base], a, b, c, (uint32_t)base);
+            set_tri(&out[base + 1], a, c, e, (uint32_t)(base + 1));
+        }
+    }
+}
+
+void vo_gen_spheres(int n, vo_sphere* out)
+{
+    #pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; ++i) {
+        uint32_t k = 6u * (uint32_t)i;
+        vo_sphere* s = &out[i];
+        memset(s, 0, sizeof(*s));
+        st(&s->center, mk(2.0f * vo_uniform(k) - 1.0f, 2.0f * vo_uniform(k + 1) - 1.0f, 2.0f * vo_uniform(k + 2) - 1.0f));
+        s->radius = 0.002f + 0.008f * vo_uniform(k + 3);
+        s->prim_id = (uint32_t)i;
+        s->geom_id = 0;
+    }
+}
+
+void vo_face_normals(const vo_tri* tris, size_t n, vo_vec3* out)
+{
+    #pragma omp parallel for schedule(static)
+    for (long i = 0; i < (long)n; ++i)
+        st(&out[i], normalize(cross(ld(&tris[i].e1), ld(&tris[i].e2))));
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Builder: build.inl:28-178, sah.h:150-763, math/detail/aabb.inl                              */
+typedef struct { v3 mn, mx; } box;
+
+static inline void box_invalidate(box* b)            /* aabb.inl invalidate: max() / lowest() */
+{
+    b->mn = mk(FLT_MAX, FLT_MAX, FLT_MAX);
+    b->mx = mk(-FLT_MAX, -FLT_MAX, -FLT_MAX);
+}
+static inline void box_insert_v(box* b, v3 v)        /* aabb.inl insert(vec) */
+{
+    b->mn = mk(fmin_ref(b->mn.x, v.x), fmin_ref(b->mn.y, v.y), fmin_ref(b->mn.z, v.z));
+    b->mx = mk(fmax_ref(b->mx.x, v.x), fmax_ref(b->mx.y, v.y), fmax_ref(b->mx.z, v.z));
+}
+static inline void box_insert_b(box* b, const box* o) /* aabb.inl insert(aabb) */
+{
+    b->mn = mk(fmin_ref(b->mn.x, o->mn.x), fmin_ref(b->mn.y, o->mn.y), fmin_ref(b->mn.z, o->mn.z));
+    b->mx = mk(fmax_ref(b->mx.x, o->mx.x), fmax_ref(b->mx.y, o->mx.y), fmax_ref(b->mx.z, o->mx.z));
+}
+static inline v3 box_center(const box* b) { return muls(add(b->mx, b->mn), 0.5f); }
+static inline v3 box_size(const box* b) { return sub(b->mx, b->mn); }
+static inline float safe_hsa(const box* b)           /* aabb.inl safe_half_surface_area */
+{
+    v3 s = sub(b->mx, b->mn);
+    s.x = fmax_ref(0.0f, s.x); s.y = fmax_ref(0.0f, s.y); s.z = fmax_ref(0.0f, s.z);
+    return s.x * s.y + s.y * s.z + s.z * s.x;
+}
+
+typedef struct { box bounds; int index; } prim_ref;  /* sah.h:155-167 */
+typedef struct { box prim_bounds, cent_bounds; int enter, leave; } bin; /* sah.h:193-220 */
+typedef struct { box prim_bounds, cent_bounds; int first; } leaf_info;  /* sah.h:270-275 */
+enum { NUM_BINS = 16 };
+
+typedef struct {
+    prim_ref* refs; size_t nrefs;
+    vo_node* nodes; size_t nn, cap_n;
+    uint32_t* indices; size_t ni;
+    unsigned max_depth;
+} builder;
+
+static void bin_merge(bin* lhs, const bin* rhs)      /* sah.h:211-219 */
+{
+    box_insert_b(&lhs->prim_bounds, &rhs->prim_bounds);
+    box_insert_b(&lhs->cent_bounds, &rhs->cent_bounds);
+    lhs->enter += rhs->enter;
+    lhs->leave += rhs->leave;
+}
+
+static void set_node(vo_node* n, const box* b, uint32_t first, uint32_t count)
+{
+    n->bmin[0] = b->mn.x; n->bmin[1] = b->mn.y; n->bmin[2] = b->mn.z;
+    n->bmax[0] = b->mx.x; n->bmax[1] = b->mx.y; n->bmax[2] = b->mx.z;
+    n->first = first; n->num_prims = count;
+}
+
+static size_t push_node(builder* B)
+{
+    if (B->nn == B->cap_n) {
+        B->cap_n = B->cap_n ? B->cap_n * 2 : 64;
+        B->nodes = (vo_node*)realloc(B->nodes, B->cap_n * sizeof(vo_node));
+    }
+    memset(&B->nodes[B->nn], 0, sizeof(vo_node));
+    return B->nn++;
+}
+
+/* sah.h:678-762 (object split only: no spatial splits in any config) */
+static int sah_split(builder* B, leaf_info childs[2], const leaf_info* leaf, int max_leaf_size)
+{
+    int leaf_size = (int)(B->nrefs - (size_t)leaf->first);
+    if (leaf_size <= max_leaf_size) return 0;
+
+    v3 size = box_size(&leaf->cent_bounds);
+    /* vector.inl:811-821 max_index */
+    int axis = comp(size, 1) < comp(size, 0) ? 0 : 1;
+    axis = comp(size, 2) < comp(size, axis) ? axis : 2;
+    if (comp(size, axis) <= 0.0f) return 0;
+
+    /* sah.h:224-268 projection */
+    float k0 = comp(leaf->cent_bounds.mn, axis);
+    float k1 = (float)NUM_BINS / (comp(leaf->cent_bounds.mx, axis) - k0);
+
+    /* sah.h:387-402 find_object_split */
+    bin bins[NUM_BINS];
+    for (int i = 0; i < NUM_BINS; ++i) {
+        box_invalidate(&bins[i].prim_bounds); box_invalidate(&bins[i].cent_bounds);
+        bins[i].enter = bins[i].leave = 0;
+    }
+    for (size_t r = (size_t)leaf->first; r < B->nrefs; ++r) {
+        v3 cen = box_center(&B->refs[r].bounds);
+        int bi = (int)(k1 * (comp(cen, axis) - k0));
+        if (bi < 0) bi = 0;
+        if (bi > NUM_BINS - 1) bi = NUM_BINS - 1;
+        bin* b = &bins[bi];
+        box_insert_b(&b->prim_bounds, &B->refs[r].bounds);
+        box_insert_v(&b->cent_bounds, cen);
+        b->enter++; b->leave++;
+    }
+
+    /* sah.h:308-367 find_split */
+    float hsa_parent = safe_hsa(&leaf->prim_bounds);
+    float best_cost = FLT_MAX;
+    int best_index = -1;
+    bin acc_l[NUM_BINS], acc_r[NUM_BINS];
+    acc_l[0] = bins[0];
+    for (int i = 1; i < NUM_BINS; ++i) { acc_l[i] = acc_l[i - 1]; bin_merge(&acc_l[i], &bins[i]); }
+    acc_r[NUM_BINS - 1] = bins[NUM_BINS - 1];
+    for (int i = NUM_BINS - 1; i > 0; --i) {
+        acc_r[i - 1] = acc_r[i]; bin_merge(&acc_r[i - 1], &bins[i - 1]);
+        const bin* L = &acc_l[i - 1];
+        const bin* R = &acc_r[i];
+        /* sah.h:279-292 compute_split_cost */
+        float cost = 1.0f + (safe_hsa(&L->prim_bounds) / hsa_parent) * (3.0f * (float)L->enter)
+                          + (safe_hsa(&R->prim_bounds) / hsa_parent) * (3.0f * (float)R->leave);
+        if (cost < best_cost) { best_cost = cost; best_index = i; }
+    }
+    if (best_index <= 0) return 0; /* unreachable for finite input (reference asserts) */
+
+    /* sah.h:742-747 leaf cost check */
+    if (best_cost > 3.0f * (float)leaf_size) return 0;
+
+    const bin* L = &acc_l[best_index - 1];
+    const bin* R = &acc_r[best_index];
+
+    /* sah.h:405-424 perform_object_partition, std::partition = libstdc++ bidirectional
+     * __partition (stl_algo.h): Hoare-style swaps from both ends */
+    childs[0].prim_bounds = L->prim_bounds; childs[0].cent_bounds = L->cent_bounds;
+    childs[1].prim_bounds = R->prim_bounds; childs[1].cent_bounds = R->cent_bounds;
+    prim_ref* first = B->refs + leaf->first;
+    prim_ref* last = B->refs + B->nrefs;
+#define PRED(pr) ((int)(k1 * (comp(box_center(&(pr)->bounds), axis) - k0)) < best_index)
+    for (;;) {
+        for (;;) {
+            if (first == last) goto done;
+            else if (PRED(first)) ++first;
+            else break;
+        }
+        --last;
+        for (;;) {
+            if (first == last) goto done;
+            else if (!PRED(last)) --last;
+            else break;
+        }
+        { prim_ref tmp = *first; *first = *last; *last = tmp; }
+        ++first;
+    }
+#undef PRED
+done:
+    childs[0].first = leaf->first;
+    childs[1].first = (int)(first - B->refs);
+    return 1;
+}
+
+/* build.inl:28-81 build_tree_impl: children allocated as an adjacent pair, right subtree first */
+static void build_rec(builder* B, size_t index, const leaf_info* leaf, int max_leaf_size, unsigned depth)
+{
+    if (depth > B->max_depth) B->max_depth = depth;
+    leaf_info childs[2];
+    if (sah_split(B, childs, leaf, max_leaf_size)) {
+        size_t first_child = B->nn;
+        set_node(&B->nodes[index], &leaf->prim_bounds, (uint32_t)first_child, 0);
+        push_node(B); push_node(B);
+        build_rec(B, first_child + 1, &childs[1], max_leaf_size, depth + 1);
+        build_rec(B, first_child + 0, &childs[0], max_leaf_size, depth + 1);
+    } else {
+        /* sah.h:657-672 insert_indices */
+        uint32_t first = (uint32_t)B->ni;
+        uint32_t count = (uint32_t)(B->nrefs - (size_t)leaf->first);
+        for (size_t r = (size_t)leaf->first; r < B->nrefs; ++r) B->indices[B->ni++] = (uint32_t)B->refs[r].index;
+        B->nrefs = (size_t)leaf->first;
+        set_node(&B->nodes[index], &leaf->prim_bounds, first, count);
+    }
+}
+
+static box prim_bounds(const void* prims, int kind, size_t i)
+{
+    box b;
+    box_invalidate(&b);
+    if (kind == VO_TRI) {                  /* triangle.inl:34-44 */
+        const vo_tri* t = (const vo_tri*)prims + i;
+        v3 v1 = ld(&t->v1);
+        box_insert_v(&b, v1);
+        box_insert_v(&b, add(v1, ld(&t->e1)));
+        box_insert_v(&b, add(v1, ld(&t->e2)));
+    } else {                               /* sphere.inl:29-38: center -/+ radius */
+        const vo_sphere* s = (const vo_sphere*)prims + i;
+        v3 c = ld(&s->center);
+        float r = s->radius;
+        box_insert_v(&b, mk(c.x - r, c.y - r, c.z - r));
+        box_insert_v(&b, mk(c.x + r, c.y + r, c.z + r));
+    }
+    return b;
+}
+
+int vo_build(const void* prims, size_t n, int kind, vo_bvh* out)
+{
+    memset(out, 0, sizeof(*out));
+    if (n == 0) return 1;
+    builder B;
+    memset(&B, 0, sizeof(B));
+    B.refs = (prim_ref*)malloc(n * sizeof(prim_ref));
+    B.indices = (uint32_t*)malloc(n * sizeof(uint32_t));
+    B.nrefs = n;
+    /* sah.h:171-186 init + sah.h:643-654 */
+    leaf_info root;
+    box_invalidate(&root.prim_bounds);
+    box_invalidate(&root.cent_bounds);
+    root.first = 0;
+    for (size_t i = 0; i < n; ++i) {
+        B.refs[i].bounds = prim_bounds(prims, kind, i);
+        B.refs[i].index = (int)i;
+        box_insert_b(&root.prim_bounds, &B.refs[i].bounds);
+        box_insert_v(&root.cent_bounds, box_center(&B.refs[i].bounds));
+    }
+    B.cap_n = 2 * (n / 4) + 64;
+    B.nodes = (vo_node*)malloc(B.cap_n * sizeof(vo_node));
+    push_node(&B);                        /* build.inl:156 root node */
+    build_rec(&B, 0, &root, 4, 0);        /* build.inl:137-140 max_leaf_size = 4 */
+    free(B.refs);
+    out->nodes = B.nodes; out->num_nodes = B.nn;
+    out->indices = B.indices; out->num_indices = B.ni;
+    out->max_depth = B.max_depth;
+    return 0;
+}
+
+void vo_bvh_free(vo_bvh* b)
+{
+    free(b->nodes); free(b->indices);
+    memset(b, 0, sizeof(*b));
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* simple_sched.inl:61-89 camera basis                                                         */
+void vo_camera_basis(const float eye[3], const float center[3], const float up[3],
+                     float fovy, float aspect, float ou[3], float ov[3], float ow[3])
+{
+    v3 e = mk(eye[0], eye[1], eye[2]), c = mk(center[0], center[1], center[2]), u0 = mk(up[0], up[1], up[2]);
+    v3 f = normalize(sub(e, c));
+    v3 s = normalize(cross(u0, f));
+    v3 u = cross(f, s);
+    float th = tanf(fovy / 2.0f);
+    v3 cu = muls(s, th * aspect);
+    v3 cv = muls(u, th);
+    v3 cw = mk(-f.x, -f.y, -f.z);
+    ou[0] = cu.x; ou[1] = cu.y; ou[2] = cu.z;
+    ov[0] = cv.x; ov[1] = cv.y; ov[2] = cv.z;
+    ow[0] = cw.x; ow[1] = cw.y; ow[2] = cw.z;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Traversal                                                                                   */
+typedef struct { int hit; float t, u, v; uint32_t prim_id, geom_id; } prim_hit;
+
+/* math/intersect.h:122-179 ray/triangle (Moller-Trumbore, two-sided) */
+static inline prim_hit isect_tri(v3 ori, v3 dir, const vo_tri* tri)
+{
+    prim_hit r; r.hit = 0; r.t = -1.0f; r.u = 0.0f; r.v = 0.0f; r.prim_id = 0; r.geom_id = 0;
+    v3 v1 = ld(&tri->v1), e1 = ld(&tri->e1), e2 = ld(&tri->e2);
+    v3 s1 = cross(dir, e2);
+    float div = dot(s1, e1);
+    if (!(div != 0.0f)) return r;
+    float inv_div = 1.0f / div;
+    v3 d = sub(ori, v1);
+    float b1 = dot(d, s1) * inv_div;
+    if (!(b1 >= 0.0f && b1 <= 1.0f)) return r;
+    v3 s2 = cross(d, e1);
+    float b2 = dot(dir, s2) * inv_div;
+    if (!(b2 >= 0.0f && b1 + b2 <= 1.0f)) return r;
+    r.hit = 1;
+    r.prim_id = tri->prim_id; r.geom_id = tri->geom_id;
+    r.t = dot(e2, s2) * inv_div;
+    r.u = b1; r.v = b2;
+    return r;
+}
+
+/* math/intersect.h:186-221 ray/sphere */
+static inline prim_hit isect_sphere(v3 ori, v3 dir, const vo_sphere* s)
+{
+    prim_hit r; r.u = 0.0f; r.v = 0.0f;
+    v3 o = sub(ori, ld(&s->center));
+    float A = dot(dir, dir);
+    float B = dot(dir, o) * 2.0f;
+    float C = dot(o, o) - s->radius * s->radius;
+    float disc = B * B - 4.0f * A * C;
+    int valid = disc >= 0.0f;
+    float root_disc = valid ? sqrtf(disc) : disc;
+    float q = B < 0.0f ? -0.5f * (B - root_disc) : -0.5f * (B + root_disc);
+    float t1 = q / A;
+    float t2 = C / q;
+    r.hit = valid;
+    r.prim_id = s->prim_id; r.geom_id = s->geom_id;
+    r.t = valid ? (t1 > t2 ? t2 : t1) : -1.0f;
+    return r;
+}
+
+vo_hit vo_intersect(const float ori_[3], const float dir_[3], const vo_node* nodes, const uint32_t* indices,
+                    const void* prims, int kind, int any_hit, float max_t, vo_counters* cnt)
+{
+    v3 ori = mk(ori_[0], ori_[1], ori_[2]);
+    v3 dir = mk(dir_[0], dir_[1], dir_[2]);
+    /* hit_record ctor (intersect.h:95-103): hit false, ids 0, t = max(), u = v = 0 */
+    vo_hit res; res.hit = 0; res.prim_id = 0; res.geom_id = 0; res.list_index = 0;
+    res.t = FLT_MAX; res.u = 0.0f; res.v = 0.0f;
+    uint64_t nbox = 0, nprim = 0;
+
+    /* detail/bvh/intersect.inl:60-63; stack sized generously (reference stack<32>, stack.h) */
+    uint32_t stack[256];
+    int sp = 0;
+    stack[sp++] = 0;
+    v3 inv_dir = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+
+    while (sp > 0) {
+        const vo_node* node = &nodes[stack[--sp]];
+        int terminated = 0;
+        while (node->num_prims == 0) {
+            const vo_node* ch = &nodes[node->first];
+            float tn[2], tf[2]; int hb[2];
+            for (int c = 0; c < 2; ++c) {
+                /* math/intersect.h:52-70 slab test */
+                v3 t1 = mul(sub(mk(ch[c].bmin[0], ch[c].bmin[1], ch[c].bmin[2]), ori), inv_dir);
+                v3 t2 = mul(sub(mk(ch[c].bmax[0], ch[c].bmax[1], ch[c].bmax[2]), ori), inv_dir);
+                tn[c] = fmax_ref(fmin_ref(t1.x, t2.x), fmax_ref(fmin_ref(t1.y, t2.y), fmin_ref(t1.z, t2.z)));
+                tf[c] = fmin_ref(fmax_ref(t1.x, t2.x), fmin_ref(fmax_ref(t1.y, t2.y), fmax_ref(t1.z, t2.z)));
+                int h = tf[c] >= tn[c];
+                /* update_if.h:60-66,82-88 is_closer(box) */
+                hb[c] = h && tn[c] < res.t && tf[c] >= 0.0f && tn[c] < max_t;
+            }
+            nbox += 2;
+            if (hb[0] && hb[1]) {
+                unsigned near_addr = (tn[0] < tn[1]) ? 0u : 1u;   /* intersect.inl:86 */
+                stack[sp++] = node->first + (near_addr ^ 1u);
+                node = &nodes[node->first + near_addr];
+            } else if (hb[0]) {
+                node = &nodes[node->first];
+            } else if (hb[1]) {
+                node = &nodes[node->first + 1];
+            } else {
+                terminated = 1;
+                break;
+            }
+        }
+        if (terminated) continue;
+        for (uint32_t i = node->first; i != node->first + node->num_prims; ++i) {
+            prim_hit hr = kind == VO_TRI ? isect_tri(ori, dir, (const vo_tri*)prims + indices[i])
+                                         : isect_sphere(ori, dir, (const vo_sphere*)prims + indices[i]);
+            ++nprim;
+            /* update_if.h:48-56,73-79 is_closer + update_if.h:27-37 + hit_record.h:54-64 */
+            int closer = hr.hit && hr.t >= 0.0f && hr.t < res.t && hr.t < max_t;
+            if (!closer) continue;
+            res.hit = 1; res.t = hr.t; res.prim_id = hr.prim_id; res.geom_id = hr.geom_id;
+            res.u = hr.u; res.v = hr.v; res.list_index = i;
+            if (any_hit) goto out;          /* exit_traversal.h:49-56 */
+        }
+    }
+out:
+    if (cnt) { cnt->box_tests += nbox; cnt->prim_tests += nprim; }
+    return res;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Pixel pipeline + kernels                                                                    */
+
+/* sched_common.h:130-150 make_primary_ray_impl (pinhole) + :180-195 uniform sampler */
+static inline void primary_ray(const vo_camera* cam, unsigned x, unsigned y, v3* ori, v3* dir)
+{
+    float fx = (float)x, fy = (float)y;
+    float u = 2.0f * (fx + 0.5f) / (float)cam->width - 1.0f;
+    float v = 2.0f * (fy + 0.5f) / (float)cam->height - 1.0f;
+    v3 cu = mk(cam->cam_u[0], cam->cam_u[1], cam->cam_u[2]);
+    v3 cv = mk(cam->cam_v[0], cam->cam_v[1], cam->cam_v[2]);
+    v3 cw = mk(cam->cam_w[0], cam->cam_w[1], cam->cam_w[2]);
+    *ori = mk(cam->eye[0], cam->eye[1], cam->eye[2]);
+    *dir = normalize(add(add(muls(cu, u), muls(cv, v)), cw));
+}
+
+typedef struct { float color[4]; uint32_t prim_id; float t; uint8_t occ; uint32_t list_index; uint32_t rays; } px_out;
+
+/* ao/main.cpp:183-246 with the deterministic sampler of SURVEY.md Appendix A */
+static px_out shade_pixel(const vo_scene* s, const vo_camera* cam, const vo_kernel* k, unsigned x, unsigned y,
+                          vo_counters* cnt)
+{
+    px_out o;
+    memcpy(o.color, k->bg, sizeof(o.color));
+    o.prim_id = 0xFFFFFFFFu; o.t = -1.0f; o.occ = 0; o.list_index = 0xFFFFFFFFu; o.rays = 1;
+    v3 ori, dir;
+    primary_ray(cam, x, y, &ori, &dir);
+    float fo[3] = { ori.x, ori.y, ori.z }, fd[3] = { dir.x, dir.y, dir.z };
+    vo_hit hr = vo_intersect(fo, fd, s->nodes, s->indices, s->prims, s->kind, 0, FLT_MAX, cnt);
+    if (!hr.hit) return o;
+    o.prim_id = hr.prim_id; o.t = hr.t; o.list_index = hr.list_index;
+    if (k->mode != VO_MODE_AO) {
+        o.color[0] = o.color[1] = o.color[2] = o.color[3] = 1.0f;
+        return o;
+    }
+    v3 isect_pos = add(ori, muls(dir, hr.t));
+    v3 n = ld(&s->normals[hr.prim_id]);                                /* get_normal.h:26-37 */
+    /* vector3.inl:357-367 make_orthonormal_basis (w = n) */
+    v3 bv = fabsf(n.x) > fabsf(n.y) ? normalize(mk(-n.z, 0.0f, n.x)) : normalize(mk(0.0f, n.z, -n.y));
+    v3 bu = cross(bv, n);
+    float clr = 1.0f;
+    uint32_t p = (uint32_t)y * (uint32_t)cam->width + (uint32_t)x;
+    float step = 1.0f / (float)k->samples;
+    for (int smp = 0; smp < k->samples; ++smp) {
+        float sx = 0.0f, sy = 0.0f;
+        for (uint32_t kk = 0; kk < 16; ++kk) {
+            uint32_t ctr = ((p * 8u + (uint32_t)smp) * 16u + kk) * 2u;
+            float xa = 2.0f * vo_uniform(ctr) - 1.0f;
+            float ya = 2.0f * vo_uniform(ctr + 1) - 1.0f;
+            if (xa * xa + ya * ya < 1.0f) { sx = xa; sy = ya; break; }
+        }
+        float sz = sqrtf(fmax_ref(0.0f, 1.0f - sx * sx - sy * sy));
+        v3 d = normalize(add(add(smul(sx, bu), smul(sy, bv)), smul(sz, n)));
+        v3 ao = add(isect_pos, muls(d, k->eps));
+        float ao_o[3] = { ao.x, ao.y, ao.z }, ao_d[3] = { d.x, d.y, d.z };
+        vo_hit ar = vo_intersect(ao_o, ao_d, s->nodes, s->indices, s->prims, s->kind, 1, k->radius, cnt);
+        o.rays++;
+        if (ar.hit) { clr = clr - step; o.occ |= (uint8_t)(1u << smp); }
+    }
+    o.color[0] = o.color[1] = o.color[2] = clr;
+    o.color[3] = 1.0f;
+    return o;
+}
+
+uint64_t vo_render_rows(const vo_scene* s, const vo_camera* cam, const vo_kernel* k, int y0, int y1,
+                        float* color, uint32_t* prim_id, float* t, uint8_t* occ, uint32_t* list_index,
+                        int threads, vo_counters* cnt)
+{
+    uint64_t rays = 0, nbox = 0, nprim = 0;
+    int W = cam->width;
+#ifdef _OPENMP
+    if (threads <= 0) threads = omp_get_max_threads();
+#else
+    threads = 1;
+#endif
+    #pragma omp parallel for schedule(dynamic, 1) num_threads(threads) reduction(+:rays,nbox,nprim)
+    for (int y = y0; y < y1; ++y) {
+        vo_counters c = { 0, 0 };
+        for (int x = 0; x < W; ++x) {
+            px_out o = shade_pixel(s, cam, k, (unsigned)x, (unsigned)y, &c);
+            size_t p = (size_t)y * W + x;
+            if (color) memcpy(color + 4 * p, o.color, 16);
+            if (prim_id) prim_id[p] = o.prim_id;
+            if (t) t[p] = o.t;
+            if (occ) occ[p] = o.occ;
+            if (list_index) list_index[p] = o.list_index;
+            rays += o.rays;
+        }
+        nbox += c.box_tests; nprim += c.prim_tests;
+    }
+    if (cnt) { cnt->box_tests += nbox; cnt->prim_tests += nprim; }
+    return rays;
+}
+
+uint64_t vo_render_pixels(const vo_scene* s, const vo_camera* cam, const vo_kernel* k,
+                          const uint32_t* pixels, size_t npix,
+                          float* color, uint32_t* prim_id, float* t, uint8_t* occ, int threads)
+{
+    uint64_t rays = 0;
+    int W = cam->width;
+#ifdef _OPENMP
+    if (threads <= 0) threads = omp_get_max_threads();
+#else
+    threads = 1;
+#endif
+    #pragma omp parallel for schedule(dynamic, 64) num_threads(threads) reduction(+:rays)
+    for (long i = 0; i < (long)npix; ++i) {
+        unsigned x = pixels[i] % (unsigned)W, y = pixels[i] / (unsigned)W;
+        px_out o = shade_pixel(s, cam, k, x, y, NULL);
+        if (color) memcpy(color + 4 * i, o.color, 16);
+        if (prim_id) prim_id[i] = o.prim_id;
+        if (t) t[i] = o.t;
+        if (occ) occ[i] = o.occ;
+        rays += o.rays;
+    }
+    return rays;
+}
+
+uint64_t vo_fnv1a(const void* data, size_t n, uint64_t h)
+{
+    const unsigned char* b = (const unsigned char*)data;
+    if (h == 0) h = 0xcbf29ce484222325ull;
+    for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 0x100000001b3ull; }
+    return h;
+}

@@ -1,0 +1,101 @@
+/*
+ * oracle/vrh_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C restatement of the reference hot path (Visionaray v0.1.0), used exclusively as the
+ * parity checker by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.  The product
+ * (visionaray_amd/, include/vrh.h) never links, loads or calls anything in oracle/.
+ *
+ * Pinned against the reference itself: oracle/_ref/vsnray_ref (built by oracle/Makefile from the
+ * reference headers where they lie) emits BVHs, per-pixel prim_id / t / AO masks and hashes; the
+ * committed fixtures in tests/golden/ carry those results to the GPU box.
+ *
+ * All binary layouts are the reference's:
+ *   vo_tri    64 B : geom_id@0 prim_id@4 v1@16 e1@32 e2@48      (basic_triangle<3,float>)
+ *   vo_sphere 48 B : geom_id@0 prim_id@4 center@16 radius@32     (basic_sphere<float>)
+ *   vo_node   32 B : bbox_min[3] first_child|first_prim bbox_max[3] num_prims   (bvh.h:52-119)
+ */
+#ifndef VRH_ORACLE_H
+#define VRH_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct { float x, y, z, pad; } vo_vec3;                         /* vector<3,float>, 16 B */
+typedef struct { uint32_t geom_id, prim_id, pad0, pad1; vo_vec3 v1, e1, e2; } vo_tri;
+typedef struct { uint32_t geom_id, prim_id, pad0, pad1; vo_vec3 center; float radius, pad2, pad3, pad4; } vo_sphere;
+typedef struct { float bmin[3]; uint32_t first; float bmax[3]; uint32_t num_prims; } vo_node;
+
+enum { VO_TRI = 0, VO_SPHERE = 1 };
+enum { VO_MODE_PRIMARY = 0, VO_MODE_AO = 1 };
+
+/* ---- synthetic scenes, SURVEY.md Appendix A ---- */
+uint32_t vo_wang(uint32_t a);
+float    vo_uniform(uint32_t k);
+size_t   vo_gen_cornell(vo_tri* out);                                  /* 12 tris */
+void     vo_gen_heightfield(int grid, vo_tri* out);                    /* 2*grid*grid tris */
+void     vo_gen_spheres(int n, vo_sphere* out);
+void     vo_face_normals(const vo_tri* tris, size_t n, vo_vec3* out);  /* normalize(cross(e1,e2)) */
+
+/* ---- binned SAH builder (build.inl:28-178, sah.h:150-763), tree-identical to the reference ---- */
+typedef struct {
+    vo_node*  nodes;   size_t num_nodes;
+    uint32_t* indices; size_t num_indices;
+    unsigned  max_depth;
+} vo_bvh;
+int  vo_build(const void* prims, size_t n, int kind, vo_bvh* out);    /* 0 = ok */
+void vo_bvh_free(vo_bvh* b);
+
+/* ---- camera basis, simple_sched.inl:61-89 (tanf from the host libm) ---- */
+void vo_camera_basis(const float eye[3], const float center[3], const float up[3],
+                     float fovy, float aspect, float out_u[3], float out_v[3], float out_w[3]);
+
+/* ---- traversal: one ray against one index BVH (detail/bvh/intersect.inl:25-134) ---- */
+typedef struct {
+    int      hit;
+    uint32_t prim_id, geom_id, list_index;
+    float    t, u, v;
+} vo_hit;
+typedef struct { uint64_t box_tests, prim_tests; } vo_counters;
+
+vo_hit vo_intersect(const float ori[3], const float dir[3], const vo_node* nodes, const uint32_t* indices,
+                    const void* prims, int kind, int any_hit, float max_t, vo_counters* cnt);
+
+/* ---- a frame, simple_sched order (row-major), over rows [y0, y1) ---- */
+typedef struct {
+    const vo_node* nodes; const uint32_t* indices; const void* prims; int kind;
+    const vo_vec3* normals;               /* per prim_id, for AO */
+} vo_scene;
+typedef struct {
+    float eye[3], cam_u[3], cam_v[3], cam_w[3];
+    int   width, height;
+} vo_camera;
+typedef struct {
+    int   mode;                           /* VO_MODE_PRIMARY | VO_MODE_AO */
+    int   samples;                        /* AO samples (8) */
+    float radius;                         /* AO radius (0.1) */
+    float eps;                            /* AO origin offset (1e-3) */
+    float bg[4];                          /* miss colour */
+} vo_kernel;
+
+/* Any output pointer may be NULL.  Arrays are full-image sized (W*H), indexed y*W+x.
+ * threads <= 0: all cores (OpenMP).  Returns rays traced (primary + AO) over the rows. */
+uint64_t vo_render_rows(const vo_scene* s, const vo_camera* cam, const vo_kernel* k, int y0, int y1,
+                        float* color, uint32_t* prim_id, float* t, uint8_t* occ, uint32_t* list_index,
+                        int threads, vo_counters* cnt);
+
+/* Same, for an explicit list of pixel indices (p = y*W + x); outputs are indexed by list position. */
+uint64_t vo_render_pixels(const vo_scene* s, const vo_camera* cam, const vo_kernel* k,
+                          const uint32_t* pixels, size_t npix,
+                          float* color, uint32_t* prim_id, float* t, uint8_t* occ, int threads);
+
+/* FNV-1a 64 over bytes (hash convention used by tests/golden) */
+uint64_t vo_fnv1a(const void* data, size_t n, uint64_t h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
