@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""bench.py -- Mrays/s (primary + 8-sample AO) of the MI355X traversal backend.
+
+Workload (BASELINE.json configs[2], the config the metric is quoted on): the 1,002,528-triangle
+procedural heightfield hf1M, binned-SAH index BVH, 1920x1080, one primary
+closest-hit ray per pixel + 8 cosine-hemisphere any-hit AO rays (radius 0.1) per hit pixel.
+A "step" is one frame.  Inputs (BVH, primitives, normals) are resident in HBM before timing.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+N > 1: one process per GPU; the image is sharded by 16-row bands (band b -> rank b % N, SURVEY.md
+§8e), each rank renders its packed shard, and the framebuffer (RGBA32F + u32 prim ids) is gathered
+to rank 0 over RCCL (torch.distributed "nccl") and un-interleaved there (vrh_unshard) -- all inside
+the timed step.  Total work per frame is fixed, so scaling is strong.
+
+Rank 0 prints one JSON line (contract in the task statement) with the roofline of the traversal
+kernel (algorithmic bytes per SURVEY.md §8d from a counting pass, over the hipEvent kernel time of
+the timed frames) and the CPU baseline (the reference's own SSE4 tiled_sched path, oracle/_ref,
+timed on this host on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+TRI_BYTES, SPHERE_BYTES, INDEX_BYTES, NODE_BYTES = 64, 48, 4, 32
+OUT_BYTES_PRIMARY = 24          # RGBA32F + u32 prim_id + f32 t per primary ray
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--scene", default="hf1M", help="hf1M (C3, default) | hf10M (C4) | sph1M (C5)")
+    ap.add_argument("--kernel", default=None, choices=["ao", "primary"], help="default: ao for triangles")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="host cores for the CPU baseline")
+    return ap.parse_args()
+
+
+def cpu_baseline(scene, kernel, threads):
+    """Reference SSE4 tiled_sched<ray4> (oracle/_ref/vsnray_ref_bench) on a bounded sample:
+    the same scene and camera at full resolution, 1 warm-up + 3 timed frames (~2-10 s)."""
+    from oracle import oracle as O
+    samples = 8 if kernel == "ao" else 0
+    if os.path.exists(O.REF_BENCH_BIN):
+        r = O.ref_bench(scene, threads, 3, 1920, 1080, samples, timeout=900)
+        return {"value": round(r["mrays_per_s"], 3), "unit": "Mrays/s", "cores": threads, "kind": "reference",
+                "sample": f"{scene} 1920x1080, {samples} AO spp, tiled_sched<basic_ray<simd::float4>> -O3 -msse4.1, "
+                          f"median of 3 frames after 1 warm-up ({r['rays_per_frame']} rays/frame)"}
+    # fallback: the plain-C restatement (scalar, OpenMP rows) on 1/8 of the image rows
+    sc = O.make_scene(scene)
+    cam = O.scene_camera(scene)
+    mode = O.VO_MODE_AO if kernel == "ao" else O.VO_MODE_PRIMARY
+    H = cam[5]
+    rows = (0, H // 8)
+    t0 = time.perf_counter()
+    out = O.render(sc, cam, mode=mode, rows=rows, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(out["rays"] / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{scene} rows {rows[0]}-{rows[1]} of 1920x1080 ({out['rays']} rays), scalar C restatement"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}; using WORLD_SIZE", file=sys.stderr)
+
+    # torch first: its HIP runtime is then the one libvrh.so binds to (one runtime per process)
+    import torch
+    import torch.distributed as dist
+
+    import visionaray_amd as va
+    from visionaray_amd import _capi, scenes
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    kernel = args.kernel or ("ao" if not args.scene.startswith("sph") else "primary")
+
+    # ---- CPU baseline (rank 0, N = 1 only), before any GPU work ------------------------------
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(args.scene, kernel, args.cpu_threads)
+        except Exception as e:  # reported, never fatal for the GPU measurement
+            cpu = {"value": None, "unit": "Mrays/s", "cores": args.cpu_threads, "kind": "reference",
+                   "sample": f"failed: {e}"}
+
+    # ---- scene: host build, upload (excluded from timing) --------------------------------------
+    t0 = time.perf_counter()
+    prims = scenes.primitives(args.scene)
+    host = va.build_index_bvh(prims)
+    build_s = time.perf_counter() - t0
+    # one explicit stream shared by libvrh launches and torch/RCCL, so render -> gather -> unshard
+    # are ordered on the device without host syncs
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    ctx = va.Context(local, stream=stream.cuda_stream)
+    dev = va.hip_index_bvh(ctx, host, scenes.normals_for(prims))
+    cam, W, H = scenes.scene_camera(args.scene)
+    basis = cam.basis(W, H)
+    kern = va.ao_kernel(dev) if kernel == "ao" else va.closest_hit_kernel(dev)
+    kern_count = va.ao_kernel(dev, count_tests=True) if kernel == "ao" else va.closest_hit_kernel(dev, count_tests=True)
+
+    # ---- framebuffers: full image on rank 0, packed shard per rank for N > 1 ------------------
+    rows_max = 16 * va.shard_bands(H, 0, world)
+    if world == 1:
+        rt = va.hip_buffer_rt(ctx, W, H)
+        shard = None
+    else:
+        loc_color = torch.empty((rows_max * W, 4), dtype=torch.float32, device="cuda")
+        loc_pid = torch.empty((rows_max * W,), dtype=torch.int32, device="cuda")
+        rt = va.hip_buffer_rt(ctx, W, rows_max, wrap=(loc_color.data_ptr(), loc_pid.data_ptr(), 0, 0))
+        shard = _capi.vrh_shard(rank, world, 1, 0)
+        if rank == 0:
+            g_color = torch.empty((world, rows_max * W, 4), dtype=torch.float32, device="cuda")
+            g_pid = torch.empty((world, rows_max * W), dtype=torch.int32, device="cuda")
+            full = va.hip_buffer_rt(ctx, W, H, flags=_capi.VRH_RT_COLOR | _capi.VRH_RT_PRIM_ID)
+
+    def step():
+        va.render(ctx, dev, rt, basis, kern, shard)
+        if world > 1:
+            if rank == 0:
+                dist.gather(loc_color, gather_list=list(g_color.unbind(0)), dst=0)
+                dist.gather(loc_pid, gather_list=list(g_pid.unbind(0)), dst=0)
+                va.unshard(ctx, W, H, world, g_color.data_ptr(), g_pid.data_ptr(), full)
+            else:
+                dist.gather(loc_color, dst=0)
+                dist.gather(loc_pid, dst=0)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # ---- counting pass (untimed): box / primitive tests per ray for the algorithmic bytes ------
+    va.render(ctx, dev, rt, basis, kern_count, shard)
+    cstats = ctx.last_frame_stats()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    ctx.stats_reset()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    acc = ctx.accum_stats()
+
+    # ---- aggregate over ranks -------------------------------------------------------------------
+    local_vals = torch.tensor([elapsed, float(acc["rays"]), acc["kernel_ms_total"], float(acc["timed_frames"]),
+                               float(cstats["box_tests"]), float(cstats["prim_tests"]), float(cstats["rays"]),
+                               float(cstats["hits"])], dtype=torch.float64, device="cuda")
+    if world > 1:
+        mx = local_vals.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = local_vals.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+    else:
+        mx = sm = local_vals
+    t_max = float(mx[0])
+    total_rays = float(sm[1])
+    mrays = total_rays / t_max / 1e6
+
+    if rank == 0:
+        # algorithmic bytes: 32 B per box test (a 64-B child pair per inner visit),
+        # (S_prim + 4 index) B per primitive test, 24 B of output per primary ray
+        s_prim = TRI_BYTES if args.scene.startswith("hf") or args.scene == "cornell12" else SPHERE_BYTES
+        n_box, n_prim, n_rays = float(sm[4]), float(sm[5]), float(sm[6])
+        primary_rays = W * H
+        bytes_frame = NODE_BYTES * n_box + (s_prim + INDEX_BYTES) * n_prim + OUT_BYTES_PRIMARY * primary_rays
+        bytes_per_ray = bytes_frame / n_rays
+        # dominant kernel = the traversal kernel; per-launch algorithmic bytes over its mean hipEvent time
+        k_ms_mean = float(local_vals[2]) / max(float(local_vals[3]), 1.0)    # rank 0's launches
+        local_bytes = bytes_per_ray * float(acc["rays"]) / max(float(acc["timed_frames"]), 1.0)
+        achieved = local_bytes / (k_ms_mean * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                with open(pmc) as f:
+                    pm = json.load(f)
+                if pm.get("scene") == args.scene and pm.get("kernel") == kernel and pm.get("gpus") == 1 and world == 1:
+                    traffic = pm.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        line = {
+            "metric": "Mrays/s (primary + 8-sample AO)" if kernel == "ao" else "Mrays/s (primary)",
+            "value": round(mrays, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (SURVEY.md Appendix A procedural scene, deterministic)",
+            "config": {
+                "workload": f"{args.scene} {W}x{H} 1 spp primary" + (" + 8 AO any-hit rays/hit (r=0.1)" if kernel == "ao" else ""),
+                "scene": args.scene, "primitives": int(len(prims)), "bvh_nodes": int(len(host.nodes)),
+                "width": W, "height": H, "ao_samples": 8 if kernel == "ao" else 0,
+                "rays_per_frame": int(n_rays), "parallelism": f"image-tile shard x{world}" + (" + RCCL gather" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": "render_kernel (traversal)", "kernel_ms_mean": round(k_ms_mean, 4),
+                "bytes_per_ray": round(bytes_per_ray, 1), "box_tests_per_ray": round(n_box / n_rays, 3),
+                "prim_tests_per_ray": round(n_prim / n_rays, 3),
+            },
+            "cpu_baseline": cpu,
+            "host_build_s": round(build_s, 3),
+        }
+        print(json.dumps(line), flush=True)
+
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

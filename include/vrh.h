@@ -1,0 +1,200 @@
+/*
+ * include/vrh.h -- C-ABI of the MI355X-native Visionaray traversal backend (libvrh.so).
+ *
+ * This is the drop-in boundary.  Everything above it -- the C++ header API in
+ * include/visionaray_hip/ (hip_sched<R>, hip_buffer_rt<CF,DF>, hip_index_bvh<P>) and the Python
+ * mirror in visionaray_amd/ -- packs arguments and calls these entry points; everything below it
+ * is hand-written HIP for gfx950.  Plain pointers and sizes only; no C++ or torch types.
+ *
+ * Reference interfaces replaced (file:line in tu500/visionaray v0.1.0):
+ *   vrh_scene_upload   <- cuda_index_bvh<P>(host_bvh) copy-ctor       bvh.h:344-350, 443-448; viewer.cpp:791
+ *   vrh_rt_alloc/_free <- gpu_buffer_rt<CF,DF>::resize / dtor        gpu_buffer_rt.h:19-51, .inl:14-47
+ *   vrh_rt_clear       <- gpu_buffer_rt::clear_color_buffer (thrust::fill) gpu_buffer_rt.inl:49-76
+ *   vrh_render         <- cuda_sched<R>::frame(kernel, sparams)      cuda_sched.h:33-34, .inl:160-198, 238-320
+ *                         (render<<<grid,block>>> cuda_sched.inl:53-153 -> persistent traversal kernels)
+ *   vrh_rt_download    <- gpu_buffer_rt::display_color_buffer D2H   gpu_buffer_rt.inl:90-119
+ *   vrh_sync           <- (none: cuda_sched is async) ; called by hip_buffer_rt::end_frame()
+ *   vrh_build_bvh      <- build<index_bvh<P>>(prims, n)              detail/bvh/build.inl:165-178 (+ sah.h)
+ *
+ * Status codes: every function returns 0 on success and never throws or longjmps across the ABI;
+ * vrh_last_error() gives a thread-local message for the last failure on the calling thread.
+ */
+#ifndef VRH_H
+#define VRH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VRH_API __attribute__((visibility("default")))
+
+typedef struct vrh_ctx   vrh_ctx;    /* one per GPU: device + hipStream_t + events + work counters */
+typedef struct vrh_scene vrh_scene;  /* device-resident index BVH (+ face normals)               */
+typedef struct vrh_rt    vrh_rt;     /* device render target (colour + side buffers)             */
+
+enum vrh_status {
+    VRH_OK = 0,
+    VRH_ERR_INVALID = 1,      /* bad argument / shape                                  */
+    VRH_ERR_HIP = 2,          /* HIP runtime error (message in vrh_last_error)         */
+    VRH_ERR_OOM = 3,          /* device or host allocation failed                      */
+    VRH_ERR_UNSUPPORTED = 4,  /* e.g. BVH deeper than the device stack supports        */
+    VRH_ERR_NO_DEVICE = 5     /* no HIP device visible                                 */
+};
+
+/* primitive layouts accepted by vrh_scene_upload / vrh_build_bvh (reference binary layouts,
+ * SURVEY.md Appendix C) */
+enum vrh_prim_kind {
+    VRH_PRIM_TRI64 = 0,       /* basic_triangle<3,float>: geom_id@0 prim_id@4 v1@16 e1@32 e2@48 */
+    VRH_PRIM_SPHERE48 = 1     /* basic_sphere<float>:     geom_id@0 prim_id@4 center@16 radius@32 */
+};
+
+/* built-in kernels (a C ABI cannot carry an arbitrary C++ lambda; SURVEY.md §7 hard part 6) */
+enum vrh_kernel_kind {
+    VRH_KERNEL_PRIMARY = 0,   /* closest_hit primary visibility: colour = hit ? 1 : bg     */
+    VRH_KERNEL_AO = 1         /* ao/main.cpp:183-246 with the Appendix-A counter sampler  */
+};
+
+enum vrh_rt_flags {
+    VRH_RT_COLOR = 1u,        /* RGBA32F colour (pixel_access.h:582-604 store)             */
+    VRH_RT_PRIM_ID = 2u,      /* u32 closest-hit prim_id, 0xFFFFFFFF on miss               */
+    VRH_RT_T = 4u,            /* f32 closest-hit t, -1 on miss                             */
+    VRH_RT_OCC = 8u,          /* u8 AO occlusion mask (bit s = sample s occluded)          */
+    VRH_RT_ALL = 15u
+};
+
+/* Host-computed pinhole basis exactly as simple_sched.inl:61-89 derives it (bit-exact floats). */
+typedef struct {
+    float    eye[3];
+    float    cam_u[3];
+    float    cam_v[3];
+    float    cam_w[3];
+    uint32_t width, height;   /* full image size (primary ray u,v and the AO pixel index use it) */
+} vrh_camera;
+
+typedef struct {
+    uint32_t kind;            /* vrh_kernel_kind                                          */
+    uint32_t samples;         /* AO samples per hit pixel (ao/main.cpp default 8, <= 32)   */
+    float    radius;          /* AO any_hit max_t (default 0.1)                            */
+    float    eps;             /* AO origin offset along the sample direction (1e-3)        */
+    float    bg[4];           /* miss colour                                               */
+    uint32_t flags;           /* vrh_kernel_flags                                          */
+} vrh_kernel_desc;
+
+enum vrh_kernel_flags {
+    VRH_KERNEL_COUNT_TESTS = 1u   /* instrumented variant: count box / primitive tests (slower;
+                                     feeds the algorithmic-bytes roofline)    */
+};
+
+/* Image-tile sharding: the image is cut into bands of 16 rows (tiled_sched
+ * tile_height, tiled_sched.inl:24-25); shard g of N renders bands b with b % N == g.
+ * packed = 0: pixels land at their image position in a W x H target.
+ * packed = 1: owned bands are stored back to back (band b at local band b / N) in a target of
+ *             W x (16 * vrh_shard_bands(H, g, N)) rows -- the layout gathered over RCCL. */
+typedef struct {
+    uint32_t index, count, packed, reserved;
+} vrh_shard;
+
+typedef struct {
+    float    kernel_ms;       /* hipEvent time of the traversal launch(es) of the last render */
+    uint64_t rays;            /* primary + AO rays traced by the last render                  */
+    uint64_t hits;            /* primary hits of the last render                              */
+    uint64_t box_tests;       /* ray/box tests (only with VRH_KERNEL_COUNT_TESTS, else 0)     */
+    uint64_t prim_tests;      /* ray/primitive tests (only with VRH_KERNEL_COUNT_TESTS)       */
+    uint32_t launches;        /* kernel launches in the last render                           */
+    uint32_t grid_blocks;
+    uint32_t block_threads;
+    uint32_t stack_depth;     /* per-lane traversal stack entries used by the variant         */
+} vrh_frame_stats;
+
+typedef struct {
+    uint32_t num_nodes, num_prims, num_indices, prim_kind;
+    uint32_t max_depth;       /* root depth 0; traversal needs <= max_depth stack entries      */
+    uint64_t device_bytes;    /* node pairs + leaf-ordered primitives + normals               */
+} vrh_scene_info;
+
+/* camera::look_at + camera::perspective (camera.inl:10-57) followed by the pinhole basis that
+ * simple_sched computes on the host (simple_sched.inl:61-89): f = normalize(eye - center),
+ * s = normalize(cross(up, f)), u = cross(f, s), cam_u = s * (tanf(fovy/2) * aspect),
+ * cam_v = u * tanf(fovy/2), cam_w = -f.  fovy in radians, aspect = width / height as float. */
+VRH_API int vrh_make_camera(const float eye[3], const float center[3], const float up[3], float fovy,
+                            float aspect, uint32_t width, uint32_t height, vrh_camera* out);
+
+VRH_API const char* vrh_version(void);
+VRH_API const char* vrh_last_error(void);
+VRH_API int vrh_device_count(int* count);
+
+/* contexts: one per GPU; hip_stream may be NULL (the context creates its own stream) */
+VRH_API int vrh_ctx_create(int hip_device, vrh_ctx** out);
+VRH_API int vrh_ctx_create_on_stream(int hip_device, void* hip_stream, vrh_ctx** out);
+VRH_API int vrh_ctx_destroy(vrh_ctx* ctx);
+
+/* scene upload: copies the host arrays (reference layouts) into device memory the scene owns.
+ * indices may be NULL for a non-index BVH (prims already in leaf order).  face_normals (vec3,
+ * 16-B stride, indexed by prim_id) is required for VRH_KERNEL_AO on triangles. */
+VRH_API int vrh_scene_upload(vrh_ctx* ctx, const void* nodes, uint32_t num_nodes,
+                             const void* prims, uint32_t num_prims, uint32_t prim_kind,
+                             const uint32_t* indices, uint32_t num_indices,
+                             const void* face_normals, vrh_scene** out);
+VRH_API int vrh_scene_get_info(const vrh_scene* scene, vrh_scene_info* info);
+VRH_API int vrh_scene_free(vrh_scene* scene);
+
+/* render targets.  vrh_rt_alloc owns its buffers (flags = vrh_rt_flags); vrh_rt_wrap borrows
+ * caller device pointers (any may be NULL), e.g. torch tensors used for the RCCL gather. */
+VRH_API int vrh_rt_alloc(vrh_ctx* ctx, uint32_t width, uint32_t height, uint32_t flags, vrh_rt** out);
+VRH_API int vrh_rt_wrap(vrh_ctx* ctx, uint32_t width, uint32_t height, void* color, uint32_t* prim_id,
+                        float* t, uint8_t* occ, vrh_rt** out);
+VRH_API int vrh_rt_get_buffers(const vrh_rt* rt, void** color, uint32_t** prim_id, float** t, uint8_t** occ);
+VRH_API int vrh_rt_clear(vrh_ctx* ctx, vrh_rt* rt, const float color[4]);
+VRH_API int vrh_rt_free(vrh_rt* rt);
+
+/* one frame (asynchronous on the context stream); shard may be NULL (= whole image) */
+VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* scene, vrh_rt* rt, const vrh_camera* cam,
+                       const vrh_kernel_desc* kernel, const vrh_shard* shard, uint32_t frame_num);
+VRH_API int vrh_sync(vrh_ctx* ctx);
+VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats);   /* syncs */
+
+/* accumulation over every render since the last vrh_stats_reset (hipEvents per frame, kept in a
+ * ring of VRH_MAX_TIMED_FRAMES; frames beyond that are counted in rays/hits but not timed) */
+#define VRH_MAX_TIMED_FRAMES 1024
+typedef struct {
+    uint32_t frames;          /* renders since reset                                      */
+    uint32_t timed_frames;    /* renders whose kernel time is in the sums                 */
+    double   kernel_ms_total, kernel_ms_min, kernel_ms_max;
+    uint64_t rays, hits;
+} vrh_accum_stats;
+VRH_API int vrh_stats_reset(vrh_ctx* ctx);
+VRH_API int vrh_get_accum_stats(vrh_ctx* ctx, vrh_accum_stats* out);           /* syncs */
+
+/* device -> host copies (any destination may be NULL); synchronous */
+VRH_API int vrh_rt_download(vrh_ctx* ctx, vrh_rt* rt, void* color, uint32_t* prim_id, float* t, uint8_t* occ);
+
+/* host -> device copies into a render target (any source may be NULL); synchronous */
+VRH_API int vrh_rt_upload(vrh_ctx* ctx, vrh_rt* rt, const void* color, const uint32_t* prim_id, const float* t,
+                          const uint8_t* occ);
+
+/* multi-GPU: number of 16-row bands shard g of N owns, and the root-side un-interleave of
+ * N gathered packed shards (device pointers laid out [N][bands_max*16][W]) into a full target */
+VRH_API uint32_t vrh_shard_bands(uint32_t height, uint32_t index, uint32_t count);
+VRH_API int vrh_unshard(vrh_ctx* ctx, uint32_t width, uint32_t height, uint32_t count,
+                        const void* gathered_color, const uint32_t* gathered_prim_id,
+                        vrh_rt* dst);
+
+/* host binned-SAH builder, tree-identical to build<index_bvh<P>> (build.inl:165-178).
+ * nodes_out must hold 2*num_prims nodes (32 B each), indices_out num_prims entries. */
+VRH_API int vrh_build_bvh(const void* prims, uint32_t num_prims, uint32_t prim_kind,
+                          void* nodes_out, uint32_t* num_nodes_out, uint32_t* indices_out,
+                          uint32_t* max_depth_out);
+
+/* synthetic scenes of SURVEY.md Appendix A (bench / test inputs) */
+VRH_API int vrh_gen_heightfield(uint32_t grid, void* tris_out);        /* 2*grid*grid TRI64   */
+VRH_API int vrh_gen_cornell(void* tris_out);                           /* 12 TRI64            */
+VRH_API int vrh_gen_spheres(uint32_t n, void* spheres_out);            /* n SPHERE48          */
+VRH_API int vrh_face_normals(const void* tris, uint32_t n, float* normals_out); /* 4 floats each */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VRH_H */

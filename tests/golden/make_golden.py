@@ -1,0 +1,87 @@
+"""Regenerate tests/golden/ from the reference itself (oracle/_ref/vsnray_ref).
+
+Run in the build container (needs /root/reference to build the harness):
+
+    make -C oracle ref && python tests/golden/make_golden.py
+
+For every case the reference harness renders a full simple_sched<basic_ray<float>> frame
+(primary closest_hit + the Appendix-A AO kernel for triangle scenes) and this script stores:
+  * golden.json            : per case counts, BVH/pixel FNV-1a-64 hashes (bytes, little endian),
+                             camera basis bits, tree depth;
+  * <case>.npz             : small cases -> every pixel (prim_id, t, occ, colour) + the BVH;
+                             large cases -> a fixed sample of 4096 pixels.
+The fixtures are data (inputs are the deterministic Appendix-A generators, outputs are what the
+reference computed); no reference source is stored.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = os.path.join(ROOT, "oracle", "_ref", "vsnray_ref")
+
+# (case name, scene, W, H, full dump?)
+CASES = [
+    ("cornell12", "cornell12", 512, 512, True),
+    ("hf64_160x90", "hf64", 160, 90, True),
+    ("hf200_320x180", "hf200", 320, 180, True),
+    ("sph5000_256x144", "sph5000", 256, 144, True),
+    ("hf1M", "hf1M", 1920, 1080, False),
+    ("sph1M", "sph1M", 1920, 1080, False),
+    ("hf10M", "hf10M", 1920, 1080, False),
+]
+
+
+def fnv1a(a):
+    """FNV-1a 64 over the little-endian bytes (computed by the oracle's C helper for speed)."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O  # noqa: E402
+    return O.fnv1a(np.ascontiguousarray(a).view(np.uint8).reshape(-1))
+
+
+def main():
+    if not os.path.exists(REF):
+        sys.exit("build the reference harness first: make -C oracle ref")
+    out = {}
+    rng = np.random.default_rng(12345)
+    for case, scene, W, H, full in CASES:
+        with tempfile.TemporaryDirectory() as d:
+            r = subprocess.run([REF, "golden", scene, d, str(W), str(H)], check=True, capture_output=True, text=True)
+            info = json.loads(r.stdout.strip().splitlines()[-1])
+            pid = np.fromfile(os.path.join(d, "prim_id.bin"), np.uint32)
+            t = np.fromfile(os.path.join(d, "t.bin"), np.float32)
+            color = np.fromfile(os.path.join(d, "color.bin"), np.float32).reshape(-1, 4)
+            occp = os.path.join(d, "occ.bin")
+            occ = np.fromfile(occp, np.uint8) if os.path.exists(occp) else np.zeros(W * H, np.uint8)
+            nodes = np.fromfile(os.path.join(d, "nodes.bin"), np.uint32)
+            idx = np.fromfile(os.path.join(d, "indices.bin"), np.uint32)
+            rec = {
+                "scene": scene, "W": W, "H": H, "prims": info["prims"], "nodes": info["nodes"],
+                "max_depth": info["max_depth"], "hits": info["hits"], "ao_rays": info["ao_rays"],
+                "ao_occluded": info["ao_occluded"],
+                "bvh_hash": fnv1a(nodes), "idx_hash": fnv1a(idx),
+                "primid_hash": fnv1a(pid), "t_hash": fnv1a(t), "occ_hash": fnv1a(occ), "color_hash": fnv1a(color),
+                "cam_u": info["cam_u"], "cam_v": info["cam_v"], "cam_w": info["cam_w"],
+            }
+            if full:
+                np.savez_compressed(os.path.join(HERE, case + ".npz"), prim_id=pid, t=t, occ=occ, color=color,
+                                    nodes=nodes, indices=idx)
+            else:
+                pix = np.sort(rng.choice(W * H, 4096, replace=False)).astype(np.uint32)
+                np.savez_compressed(os.path.join(HERE, case + ".npz"), pixels=pix, prim_id=pid[pix], t=t[pix],
+                                    occ=occ[pix], color=color[pix])
+            out[case] = rec
+            print(case, rec["hits"], rec["ao_occluded"], rec["primid_hash"], flush=True)
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

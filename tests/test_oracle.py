@@ -1,0 +1,112 @@
+"""CPU: the oracle (plain-C restatement, oracle/vrh_oracle.c) against the reference's own outputs.
+
+Pins: tests/golden/* were produced by the reference headers compiled in place (oracle/_ref,
+tests/golden/make_golden.py); when the reference harness is present (build container) the oracle is
+also cross-checked live on cases that are not fixtures.  The reference's own known-answer test
+(test/unittests/get_normal.cpp:17-75) is restated here.
+"""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FULL_CASES = ["cornell12", "hf64_160x90", "hf200_320x180", "sph5000_256x144"]
+
+
+def _render_case(O, g):
+    sc = O.make_scene(g["scene"])
+    cam = O.scene_camera(g["scene"], g["W"], g["H"])
+    mode = O.VO_MODE_AO if sc.kind == O.VO_TRI else O.VO_MODE_PRIMARY
+    return sc, cam, O.render(sc, cam, mode=mode)
+
+
+@pytest.mark.parametrize("case", FULL_CASES)
+def test_oracle_matches_reference_every_pixel(oracle_mod, golden, case):
+    O = oracle_mod
+    g = golden[case]
+    ref = np.load(os.path.join(HERE, "golden", case + ".npz"))
+    sc, cam, out = _render_case(O, g)
+    assert np.array_equal(sc.nodes.view(np.uint32).reshape(-1), ref["nodes"]), "BVH nodes differ from reference build"
+    assert np.array_equal(sc.indices, ref["indices"])
+    assert sc.max_depth == g["max_depth"]
+    assert np.array_equal(out["prim_id"], ref["prim_id"])
+    assert np.array_equal(out["t"].view(np.uint32), ref["t"].view(np.uint32))
+    assert np.array_equal(out["occ"], ref["occ"])
+    assert np.array_equal(out["color"].view(np.uint32), ref["color"].view(np.uint32))
+    assert int((out["prim_id"] != 0xFFFFFFFF).sum()) == g["hits"]
+
+
+@pytest.mark.parametrize("case", ["hf1M", "sph1M", "hf10M"])
+def test_oracle_matches_reference_hashes_full_size(oracle_mod, golden, case):
+    O = oracle_mod
+    g = golden[case]
+    sc, cam, out = _render_case(O, g)
+    assert O.fnv1a(sc.nodes) == g["bvh_hash"] and O.fnv1a(sc.indices) == g["idx_hash"]
+    assert len(sc.nodes) == g["nodes"] and sc.max_depth == g["max_depth"]
+    assert O.fnv1a(out["prim_id"]) == g["primid_hash"]
+    assert O.fnv1a(out["t"]) == g["t_hash"]
+    assert O.fnv1a(out["occ"]) == g["occ_hash"]
+    assert O.fnv1a(out["color"]) == g["color_hash"]
+    hits = int((out["prim_id"] != 0xFFFFFFFF).sum())
+    assert hits == g["hits"]
+    assert out["rays"] == g["W"] * g["H"] + g["ao_rays"]
+    assert int(np.unpackbits(out["occ"]).sum()) == g["ao_occluded"]
+
+
+def test_camera_basis_bits_match_reference(oracle_mod, golden):
+    O = oracle_mod
+    for case in ("cornell12", "hf1M", "sph1M"):
+        g = golden[case]
+        _, u, v, w, _, _ = O.scene_camera(g["scene"], g["W"], g["H"])
+        for got, want in ((u, g["cam_u"]), (v, g["cam_v"]), (w, g["cam_w"])):
+            assert ["%08x" % b for b in got.view(np.uint32)] == want
+
+
+def test_get_normal_known_answer(oracle_mod):
+    """test/unittests/get_normal.cpp:17-75: two triangles, ray (0.5,-0.5,2) -> (0,0,-1)."""
+    O = oracle_mod
+    tris = np.zeros(2, O.TRI_DTYPE)
+    v1a, v1b = np.array([-1, -1, 1], np.float32), np.array([1, -1, -1], np.float32)
+    tris[0]["v1"][:3] = v1a
+    tris[0]["e1"][:3] = np.array([1, -1, 1], np.float32) - v1a
+    tris[0]["e2"][:3] = np.array([1, 1, 1], np.float32) - v1a
+    tris[0]["prim_id"], tris[0]["geom_id"] = 0, 0
+    tris[1]["v1"][:3] = v1b
+    tris[1]["e1"][:3] = np.array([-1, -1, -1], np.float32) - v1b
+    tris[1]["e2"][:3] = np.array([-1, 1, -1], np.float32) - v1b
+    tris[1]["prim_id"], tris[1]["geom_id"] = 1, 1
+    nodes, idx, _ = O.build_bvh(tris, O.VO_TRI)
+    assert len(nodes) > 0 and len(idx) == 2
+    # a 1x1 camera looking down -z from (0.5,-0.5,2): basis chosen so the single ray is (0,0,-1)
+    sc = O.Scene("kat", O.VO_TRI, tris, nodes, idx, O.face_normals(tris), 0)
+    cam = (np.array([0.5, -0.5, 2.0], np.float32), np.zeros(3, np.float32), np.zeros(3, np.float32),
+           np.array([0.0, 0.0, -1.0], np.float32), 1, 1)
+    out = O.render(sc, cam, mode=O.VO_MODE_PRIMARY)
+    assert out["prim_id"][0] == 0
+    assert out["t"][0] == np.float32(1.0)
+    n = O.face_normals(tris)[0, :3]
+    e1, e2 = tris[0]["e1"][:3], tris[0]["e2"][:3]
+    c = np.cross(e1, e2).astype(np.float32)
+    np.testing.assert_allclose(n, c / np.sqrt(np.float32((c * c).sum())), rtol=1e-6)
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(os.path.dirname(HERE), "oracle", "_ref", "vsnray_ref")),
+                    reason="reference harness not built (only in the build container)")
+@pytest.mark.parametrize("scene,W,H", [("hf37", 123, 77), ("sph777", 97, 61), ("hf5", 40, 33)])
+def test_oracle_matches_live_reference(oracle_mod, scene, W, H):
+    O = oracle_mod
+    with tempfile.TemporaryDirectory() as d:
+        info = O.ref_golden(scene, d, W, H)
+        sc = O.make_scene(scene)
+        cam = O.scene_camera(scene, W, H)
+        mode = O.VO_MODE_AO if sc.kind == O.VO_TRI else O.VO_MODE_PRIMARY
+        out = O.render(sc, cam, mode=mode)
+        assert np.array_equal(sc.nodes.view(np.uint32).reshape(-1), np.fromfile(os.path.join(d, "nodes.bin"), np.uint32))
+        assert np.array_equal(out["prim_id"], np.fromfile(os.path.join(d, "prim_id.bin"), np.uint32))
+        assert np.array_equal(out["t"].view(np.uint32), np.fromfile(os.path.join(d, "t.bin"), np.uint32))
+        assert np.array_equal(out["list_index"], np.fromfile(os.path.join(d, "leaf_pos.bin"), np.uint32))
+        if mode == O.VO_MODE_AO:
+            assert np.array_equal(out["occ"], np.fromfile(os.path.join(d, "occ.bin"), np.uint8))
+        assert int((out["prim_id"] != 0xFFFFFFFF).sum()) == info["hits"]

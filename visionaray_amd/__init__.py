@@ -1,0 +1,19 @@
+"""visionaray_amd -- MI355X-native (gfx950) backend for Visionaray's ray-traversal hot path.
+
+BVH traversal + ray/triangle and ray/sphere intersection as hand-written HIP kernels behind the
+C-ABI in include/vrh.h (libvrh.so), with a host API that mirrors the reference's
+scheduler / render_target / BVH interface (hip_sched, hip_buffer_rt, hip_index_bvh).
+"""
+from . import _capi
+from .api import (BVH_NODE_DTYPE, DEGREES_TO_RADIANS, SPHERE_DTYPE, TRIANGLE_DTYPE, Context, ao_kernel,
+                  build_index_bvh, camera, closest_hit_kernel, device_count, face_normals, hip_buffer_rt,
+                  hip_index_bvh, hip_sched, index_bvh, make_sched_params, make_spheres, make_triangles,
+                  pixel_sampler, render, shard_bands, unshard)
+from ._capi import VrhError
+
+__all__ = [
+    "BVH_NODE_DTYPE", "DEGREES_TO_RADIANS", "SPHERE_DTYPE", "TRIANGLE_DTYPE", "Context", "VrhError", "ao_kernel",
+    "build_index_bvh", "camera", "closest_hit_kernel", "device_count", "face_normals", "hip_buffer_rt",
+    "hip_index_bvh", "hip_sched", "index_bvh", "make_sched_params", "make_spheres", "make_triangles",
+    "pixel_sampler", "render", "shard_bands", "unshard", "_capi",
+]

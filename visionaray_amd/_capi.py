@@ -1,0 +1,121 @@
+"""ctypes binding of libvrh.so (include/vrh.h), the C-ABI of the MI355X traversal backend.
+
+The library is built in-tree (``make -C visionaray_amd`` or ``__graft_entry__.build()``) into
+``visionaray_amd/_lib/libvrh.so``.  There is no fallback: if the library is missing or a call fails,
+an exception is raised.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libvrh.so")
+
+# enums (vrh.h)
+VRH_OK, VRH_ERR_INVALID, VRH_ERR_HIP, VRH_ERR_OOM, VRH_ERR_UNSUPPORTED, VRH_ERR_NO_DEVICE = range(6)
+VRH_PRIM_TRI64, VRH_PRIM_SPHERE48 = 0, 1
+VRH_KERNEL_PRIMARY, VRH_KERNEL_AO = 0, 1
+VRH_RT_COLOR, VRH_RT_PRIM_ID, VRH_RT_T, VRH_RT_OCC, VRH_RT_ALL = 1, 2, 4, 8, 15
+
+
+class vrh_camera(C.Structure):
+    _fields_ = [("eye", C.c_float * 3), ("cam_u", C.c_float * 3), ("cam_v", C.c_float * 3),
+                ("cam_w", C.c_float * 3), ("width", C.c_uint32), ("height", C.c_uint32)]
+
+
+class vrh_kernel_desc(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("samples", C.c_uint32), ("radius", C.c_float), ("eps", C.c_float),
+                ("bg", C.c_float * 4), ("flags", C.c_uint32)]
+
+
+VRH_KERNEL_COUNT_TESTS = 1
+VRH_MAX_TIMED_FRAMES = 1024
+
+
+class vrh_accum_stats(C.Structure):
+    _fields_ = [("frames", C.c_uint32), ("timed_frames", C.c_uint32), ("kernel_ms_total", C.c_double),
+                ("kernel_ms_min", C.c_double), ("kernel_ms_max", C.c_double), ("rays", C.c_uint64),
+                ("hits", C.c_uint64)]
+
+
+class vrh_shard(C.Structure):
+    _fields_ = [("index", C.c_uint32), ("count", C.c_uint32), ("packed", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class vrh_frame_stats(C.Structure):
+    _fields_ = [("kernel_ms", C.c_float), ("rays", C.c_uint64), ("hits", C.c_uint64), ("box_tests", C.c_uint64),
+                ("prim_tests", C.c_uint64), ("launches", C.c_uint32),
+                ("grid_blocks", C.c_uint32), ("block_threads", C.c_uint32), ("stack_depth", C.c_uint32)]
+
+
+class vrh_scene_info(C.Structure):
+    _fields_ = [("num_nodes", C.c_uint32), ("num_prims", C.c_uint32), ("num_indices", C.c_uint32),
+                ("prim_kind", C.c_uint32), ("max_depth", C.c_uint32), ("device_bytes", C.c_uint64)]
+
+
+class VrhError(RuntimeError):
+    def __init__(self, fn, code, msg):
+        super().__init__(f"{fn} failed (status {code}): {msg}")
+        self.code = code
+
+
+# every exported symbol of include/vrh.h with its signature: name -> (restype, argtypes)
+_vp, _u32, _pf = C.c_void_p, C.c_uint32, C.POINTER(C.c_float)
+SIGNATURES = {
+    "vrh_make_camera": (C.c_int, [_pf, _pf, _pf, C.c_float, C.c_float, _u32, _u32, C.POINTER(vrh_camera)]),
+    "vrh_version": (C.c_char_p, []),
+    "vrh_last_error": (C.c_char_p, []),
+    "vrh_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "vrh_ctx_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
+    "vrh_ctx_create_on_stream": (C.c_int, [C.c_int, _vp, C.POINTER(_vp)]),
+    "vrh_ctx_destroy": (C.c_int, [_vp]),
+    "vrh_scene_upload": (C.c_int, [_vp, _vp, _u32, _vp, _u32, _u32, _vp, _u32, _vp, C.POINTER(_vp)]),
+    "vrh_scene_get_info": (C.c_int, [_vp, C.POINTER(vrh_scene_info)]),
+    "vrh_scene_free": (C.c_int, [_vp]),
+    "vrh_rt_alloc": (C.c_int, [_vp, _u32, _u32, _u32, C.POINTER(_vp)]),
+    "vrh_rt_wrap": (C.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _vp, C.POINTER(_vp)]),
+    "vrh_rt_get_buffers": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp)]),
+    "vrh_rt_clear": (C.c_int, [_vp, _vp, _pf]),
+    "vrh_rt_free": (C.c_int, [_vp]),
+    "vrh_render": (C.c_int, [_vp, _vp, _vp, C.POINTER(vrh_camera), C.POINTER(vrh_kernel_desc),
+                             C.POINTER(vrh_shard), _u32]),
+    "vrh_sync": (C.c_int, [_vp]),
+    "vrh_last_frame_stats": (C.c_int, [_vp, C.POINTER(vrh_frame_stats)]),
+    "vrh_stats_reset": (C.c_int, [_vp]),
+    "vrh_get_accum_stats": (C.c_int, [_vp, C.POINTER(vrh_accum_stats)]),
+    "vrh_rt_download": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "vrh_rt_upload": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "vrh_shard_bands": (C.c_uint32, [_u32, _u32, _u32]),
+    "vrh_unshard": (C.c_int, [_vp, _u32, _u32, _u32, _vp, _vp, _vp]),
+    "vrh_build_bvh": (C.c_int, [_vp, _u32, _u32, _vp, C.POINTER(_u32), _vp, C.POINTER(_u32)]),
+    "vrh_gen_heightfield": (C.c_int, [_u32, _vp]),
+    "vrh_gen_cornell": (C.c_int, [_vp]),
+    "vrh_gen_spheres": (C.c_int, [_u32, _vp]),
+    "vrh_face_normals": (C.c_int, [_vp, _u32, _vp]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libvrh.so (raises if it was not built -- there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `make -C {_HERE}` (or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(fn, *args):
+    """Call lib().fn(*args); raise VrhError on a non-zero status."""
+    rc = getattr(lib(), fn)(*args)
+    if rc != VRH_OK:
+        raise VrhError(fn, rc, lib().vrh_last_error().decode(errors="replace"))
+    return rc

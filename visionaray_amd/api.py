@@ -1,0 +1,384 @@
+"""Host-side mirror of Visionaray's scheduler / render-target / BVH interface for the HIP backend.
+
+Names and argument meaning follow the reference so code (and tests) read like Visionaray's own:
+
+    bvh   = build_index_bvh(prims)                          # build<index_bvh<P>>(prims, n)      build.inl:165-178
+    ctx   = Context(0)                                      # one per GPU (HIP device + stream)
+    dbvh  = hip_index_bvh(ctx, bvh, normals)                # cuda_index_bvh<P>(host_bvh)         bvh.h:344-350
+    rt    = hip_buffer_rt(ctx, w, h)                        # gpu_buffer_rt<PF_RGBA32F, ...>     gpu_buffer_rt.h:19-51
+    cam   = camera(); cam.perspective(...); cam.look_at(eye, center, up)          camera.inl:10-57
+    sched = hip_sched(ctx)                                  # cuda_sched<R>                       cuda_sched.h:25-40
+    sched.frame(ao_kernel(dbvh), make_sched_params(pixel_sampler.uniform_type, cam, rt))
+
+Every device call goes through libvrh.so (include/vrh.h).  There is no CPU fallback in this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+
+from . import _capi as capi
+
+# reference binary layouts
+TRIANGLE_DTYPE = np.dtype([("geom_id", "<u4"), ("prim_id", "<u4"), ("pad", "<u4", 2),
+                           ("v1", "<f4", 4), ("e1", "<f4", 4), ("e2", "<f4", 4)])
+SPHERE_DTYPE = np.dtype([("geom_id", "<u4"), ("prim_id", "<u4"), ("pad", "<u4", 2),
+                         ("center", "<f4", 4), ("radius", "<f4"), ("pad2", "<f4", 3)])
+BVH_NODE_DTYPE = np.dtype([("bbox_min", "<f4", 3), ("first", "<u4"), ("bbox_max", "<f4", 3), ("num_prims", "<u4")])
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _kind_of(prims):
+    if prims.dtype == TRIANGLE_DTYPE:
+        return capi.VRH_PRIM_TRI64
+    if prims.dtype == SPHERE_DTYPE:
+        return capi.VRH_PRIM_SPHERE48
+    raise TypeError(f"unsupported primitive dtype {prims.dtype}; use TRIANGLE_DTYPE or SPHERE_DTYPE")
+
+
+# ---- primitives -------------------------------------------------------------------------------
+
+def make_triangles(v1, e1, e2, prim_id=None, geom_id=None):
+    """basic_triangle<3,float> array from (N,3) vertex / edge arrays."""
+    v1, e1, e2 = (np.asarray(a, np.float32).reshape(-1, 3) for a in (v1, e1, e2))
+    n = len(v1)
+    t = np.zeros(n, TRIANGLE_DTYPE)
+    t["v1"][:, :3], t["e1"][:, :3], t["e2"][:, :3] = v1, e1, e2
+    t["prim_id"] = np.arange(n, dtype=np.uint32) if prim_id is None else prim_id
+    t["geom_id"] = 0 if geom_id is None else geom_id
+    return t
+
+
+def make_spheres(center, radius, prim_id=None, geom_id=None):
+    """basic_sphere<float> array."""
+    center = np.asarray(center, np.float32).reshape(-1, 3)
+    n = len(center)
+    s = np.zeros(n, SPHERE_DTYPE)
+    s["center"][:, :3] = center
+    s["radius"] = radius
+    s["prim_id"] = np.arange(n, dtype=np.uint32) if prim_id is None else prim_id
+    s["geom_id"] = 0 if geom_id is None else geom_id
+    return s
+
+
+def face_normals(tris):
+    """normalize(cross(e1, e2)) per triangle (get_normal normals_per_face_binding input)."""
+    out = np.zeros((len(tris), 4), np.float32)
+    capi.check("vrh_face_normals", _p(np.ascontiguousarray(tris)), len(tris), _p(out))
+    return out
+
+
+# ---- host BVH ---------------------------------------------------------------------------------
+
+class index_bvh:
+    """Host index BVH (index_bvh_t, bvh.h:317-403): prims + nodes + indices, reference layouts."""
+
+    def __init__(self, prims, nodes, indices, max_depth):
+        self.prims = prims
+        self.nodes = nodes
+        self.indices = indices
+        self.max_depth = max_depth
+        self.prim_kind = _kind_of(prims)
+
+    def num_nodes(self):
+        return len(self.nodes)
+
+    def num_primitives(self):
+        return len(self.prims)
+
+
+def build_index_bvh(prims):
+    """build<index_bvh<P>>(prims, n) -- binned SAH, tree-identical to the reference builder."""
+    prims = np.ascontiguousarray(prims)
+    n = len(prims)
+    if n == 0:
+        raise ValueError("build_index_bvh: no primitives")
+    kind = _kind_of(prims)
+    nodes = np.zeros(max(2 * n, 1), BVH_NODE_DTYPE)
+    idx = np.zeros(n, np.uint32)
+    nn, depth = C.c_uint32(0), C.c_uint32(0)
+    capi.check("vrh_build_bvh", _p(prims), n, kind, _p(nodes), C.byref(nn), _p(idx), C.byref(depth))
+    return index_bvh(prims, nodes[: nn.value].copy(), idx, depth.value)
+
+
+# ---- camera -----------------------------------------------------------------------------------
+
+class camera:
+    """camera (camera.h:46-95): perspective() + look_at(); basis computed as simple_sched does."""
+
+    def __init__(self):
+        self.fovy = float(np.float32(45.0) * np.float32(math.pi / 180.0))
+        self.aspect = 1.0
+        self.z_near, self.z_far = 0.001, 1000.0
+        self.eye = (0.0, 0.0, 1.0)
+        self.center = (0.0, 0.0, 0.0)
+        self.up = (0.0, 1.0, 0.0)
+
+    def perspective(self, fovy, aspect, z_near, z_far):
+        self.fovy, self.aspect, self.z_near, self.z_far = float(fovy), float(aspect), float(z_near), float(z_far)
+
+    def look_at(self, eye, center, up=(0.0, 1.0, 0.0)):
+        self.eye, self.center, self.up = tuple(eye), tuple(center), tuple(up)
+
+    def basis(self, width, height):
+        f3 = C.c_float * 3
+        out = capi.vrh_camera()
+        capi.check("vrh_make_camera", f3(*self.eye), f3(*self.center), f3(*self.up), C.c_float(self.fovy),
+                   C.c_float(self.aspect), width, height, C.byref(out))
+        return out
+
+
+DEGREES_TO_RADIANS = float(np.float32(1.74532925199432957692369076849e-02))
+
+
+# ---- device objects ---------------------------------------------------------------------------
+
+class Context:
+    """One HIP device + stream (vrh_ctx).  stream: optional raw hipStream_t (int) to launch on."""
+
+    def __init__(self, device=0, stream=None):
+        h = C.c_void_p()
+        if stream is None:
+            capi.check("vrh_ctx_create", int(device), C.byref(h))
+        else:
+            capi.check("vrh_ctx_create_on_stream", int(device), C.c_void_p(stream), C.byref(h))
+        self.handle = h
+        self.device = device
+
+    def sync(self):
+        capi.check("vrh_sync", self.handle)
+
+    def last_frame_stats(self):
+        s = capi.vrh_frame_stats()
+        capi.check("vrh_last_frame_stats", self.handle, C.byref(s))
+        return {k: getattr(s, k) for k, _ in s._fields_}
+
+    def stats_reset(self):
+        capi.check("vrh_stats_reset", self.handle)
+
+    def accum_stats(self):
+        s = capi.vrh_accum_stats()
+        capi.check("vrh_get_accum_stats", self.handle, C.byref(s))
+        return {k: getattr(s, k) for k, _ in s._fields_}
+
+    def close(self):
+        if self.handle:
+            capi.lib().vrh_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def device_count():
+    n = C.c_int(0)
+    rc = capi.lib().vrh_device_count(C.byref(n))
+    return n.value if rc == 0 else 0
+
+
+class hip_index_bvh:
+    """Device-resident index BVH: the cuda_index_bvh<P>(host_bvh) copy-constructor analogue."""
+
+    def __init__(self, ctx, host_bvh, normals=None):
+        self.ctx = ctx
+        h = C.c_void_p()
+        nrm = None if normals is None else np.ascontiguousarray(normals, np.float32)
+        if nrm is not None and nrm.shape != (len(host_bvh.prims), 4):
+            raise ValueError("normals must be (num_prims, 4) float32")
+        capi.check("vrh_scene_upload", ctx.handle, _p(host_bvh.nodes), len(host_bvh.nodes), _p(host_bvh.prims),
+                   len(host_bvh.prims), host_bvh.prim_kind, _p(host_bvh.indices), len(host_bvh.indices),
+                   _p(nrm), C.byref(h))
+        self.handle = h
+        info = capi.vrh_scene_info()
+        capi.check("vrh_scene_get_info", h, C.byref(info))
+        self.info = {k: getattr(info, k) for k, _ in info._fields_}
+
+    def close(self):
+        if self.handle:
+            capi.lib().vrh_scene_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class hip_buffer_rt:
+    """gpu_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> plus the integer side buffers used for parity.
+
+    wrap=(color_ptr, prim_id_ptr, t_ptr, occ_ptr) borrows caller device memory (e.g. torch tensors).
+    """
+
+    def __init__(self, ctx, width, height, flags=capi.VRH_RT_ALL, wrap=None):
+        self.ctx = ctx
+        self.handle = None
+        self.flags = flags
+        self._wrap = wrap
+        self.resize(width, height)
+
+    def resize(self, width, height):
+        self.close()
+        h = C.c_void_p()
+        if self._wrap is None:
+            capi.check("vrh_rt_alloc", self.ctx.handle, width, height, self.flags, C.byref(h))
+        else:
+            c, p, t, o = (C.c_void_p(x) if x else None for x in self._wrap)
+            capi.check("vrh_rt_wrap", self.ctx.handle, width, height, c, p, t, o, C.byref(h))
+        self.handle = h
+        self.w, self.h = width, height
+
+    def width(self):
+        return self.w
+
+    def height(self):
+        return self.h
+
+    def clear_color_buffer(self, color=(0.0, 0.0, 0.0, 0.0)):
+        capi.check("vrh_rt_clear", self.ctx.handle, self.handle, (C.c_float * 4)(*color))
+
+    def begin_frame(self):
+        pass
+
+    def end_frame(self):
+        """Blocks until the frame is done (so hip_sched::frame is synchronous like tiled_sched)."""
+        self.ctx.sync()
+
+    def device_buffers(self):
+        bufs = [C.c_void_p() for _ in range(4)]
+        capi.check("vrh_rt_get_buffers", self.handle, *[C.byref(b) for b in bufs])
+        return tuple(b.value for b in bufs)
+
+    def download(self, color=True, prim_id=True, t=True, occ=True):
+        n = self.w * self.h
+        has = self.device_buffers()
+        out = {}
+        if color and has[0]:
+            out["color"] = np.zeros((n, 4), np.float32)
+        if prim_id and has[1]:
+            out["prim_id"] = np.zeros(n, np.uint32)
+        if t and has[2]:
+            out["t"] = np.zeros(n, np.float32)
+        if occ and has[3]:
+            out["occ"] = np.zeros(n, np.uint8)
+        capi.check("vrh_rt_download", self.ctx.handle, self.handle, _p(out.get("color")), _p(out.get("prim_id")),
+                   _p(out.get("t")), _p(out.get("occ")))
+        return out
+
+    def upload(self, color=None, prim_id=None, t=None, occ=None):
+        arrs = [None if a is None else np.ascontiguousarray(a) for a in (color, prim_id, t, occ)]
+        n = self.w * self.h
+        for a, per in zip(arrs, (16, 4, 4, 1)):
+            if a is not None and a.nbytes != n * per:
+                raise ValueError("upload: array size does not match the render target")
+        capi.check("vrh_rt_upload", self.ctx.handle, self.handle, *[_p(a) for a in arrs])
+
+    def color(self):
+        return self.download(prim_id=False, t=False, occ=False)["color"]
+
+    def close(self):
+        if self.handle:
+            capi.lib().vrh_rt_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ---- scheduler ----------------------------------------------------------------------------------
+
+class pixel_sampler:
+    class uniform_type:
+        pass
+
+
+class sched_params:
+    def __init__(self, cam, rt, sampler=pixel_sampler.uniform_type, image_size=None):
+        if sampler is not pixel_sampler.uniform_type:
+            raise NotImplementedError("hip_sched supports pixel_sampler::uniform_type only")
+        self.cam = cam          # stored by value in the reference (scheduler.h:72)
+        self.rt = rt            # by reference (scheduler.h:73)
+        self.scissor_box = (0, 0, rt.width(), rt.height())
+        # full image size; differs from the rt size only for a packed image-tile shard
+        self.image_size = tuple(image_size) if image_size else (rt.width(), rt.height())
+
+
+def make_sched_params(*args, image_size=None):
+    """make_sched_params([pixel_sampler], camera, rt) -- scheduler.h:164-242."""
+    if len(args) == 3:
+        sampler, cam, rt = args
+    elif len(args) == 2:
+        sampler, (cam, rt) = pixel_sampler.uniform_type, args
+    else:
+        raise TypeError("make_sched_params([sampler,] camera, render_target)")
+    return sched_params(cam, rt, sampler, image_size)
+
+
+class _builtin_kernel:
+    def __init__(self, bvh, kind, samples, radius, eps, bg, count_tests=False):
+        self.bvh = bvh
+        self.desc = capi.vrh_kernel_desc(kind, samples, radius, eps, (C.c_float * 4)(*bg),
+                                         capi.VRH_KERNEL_COUNT_TESTS if count_tests else 0)
+
+
+def closest_hit_kernel(bvh, bg=(0.1, 0.2, 0.3, 1.0), count_tests=False):
+    """Primary visibility: closest_hit(ray, bvhs) (traverse_linear.inl:286-329); colour = hit ? 1 : bg."""
+    return _builtin_kernel(bvh, capi.VRH_KERNEL_PRIMARY, 0, 0.0, 0.0, bg, count_tests)
+
+
+def ao_kernel(bvh, samples=8, radius=0.1, eps=1e-3, bg=(0.1, 0.2, 0.3, 1.0), count_tests=False):
+    """ao/main.cpp:183-246 (closest hit + `samples` any_hit rays, radius), Appendix-A sampler."""
+    return _builtin_kernel(bvh, capi.VRH_KERNEL_AO, samples, radius, eps, bg, count_tests)
+
+
+class hip_sched:
+    """hip_sched<R>: drop-in for cuda_sched<R> (cuda_sched.h:25-40).
+
+    frame() = rt.begin_frame() -> vrh_render -> rt.end_frame() (end_frame syncs, so frame() is
+    synchronous like tiled_sched).  shard=(index, count, packed) renders only that image-tile shard.
+    """
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def frame(self, kernel, sparams, frame_num=0, shard=None, sync=True):
+        if not isinstance(kernel, _builtin_kernel):
+            raise TypeError("hip_sched runs built-in kernels only (closest_hit_kernel / ao_kernel): an arbitrary "
+                            "callable cannot cross the C ABI")
+        rt = sparams.rt
+        cam = sparams.cam.basis(*sparams.image_size)
+        sh = None
+        if shard is not None:
+            sh = capi.vrh_shard(shard[0], shard[1], 1 if shard[2] else 0, 0)
+        rt.begin_frame()
+        capi.check("vrh_render", self.ctx.handle, kernel.bvh.handle, rt.handle, C.byref(cam), C.byref(kernel.desc),
+                   C.byref(sh) if sh is not None else None, frame_num)
+        if sync:
+            rt.end_frame()
+
+
+def render(ctx, bvh, rt, cam_basis, kernel, shard=None):
+    """Low-level frame with an explicit vrh_camera (full-image size) and optional vrh_shard."""
+    capi.check("vrh_render", ctx.handle, bvh.handle, rt.handle, C.byref(cam_basis), C.byref(kernel.desc),
+               C.byref(shard) if shard is not None else None, 0)
+
+
+def shard_bands(height, index, count):
+    return capi.lib().vrh_shard_bands(height, index, count)
+
+
+def unshard(ctx, width, height, count, gathered_color_ptr, gathered_prim_id_ptr, dst_rt):
+    capi.check("vrh_unshard", ctx.handle, width, height, count, C.c_void_p(gathered_color_ptr) if gathered_color_ptr else None,
+               C.c_void_p(gathered_prim_id_ptr) if gathered_prim_id_ptr else None, dst_rt.handle)

@@ -1,0 +1,42 @@
+// visionaray_amd/csrc/vrh_kernels.h -- kernel launch interface (host side of vrh_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace vrh {
+
+struct render_params
+{
+    const float4* pairs;      // 4 float4 per inner node pair record
+    const float4* prims;      // leaf-ordered primitives (3 float4 tri, 2 float4 sphere)
+    const float4* normals;    // per prim_id
+    uint32_t root;            // root link (pair 0, or LEAF_BIT|0 for a single-leaf tree)
+
+    float eye[3], cam_u[3], cam_v[3], cam_w[3];
+    uint32_t width, height;
+
+    uint32_t samples;
+    float radius, eps;
+    float bg[4];
+
+    uint32_t shard_index, shard_count, packed;
+    uint32_t tiles_x, num_tiles;
+
+    float4* color;
+    uint32_t* prim_id;
+    float* t;
+    uint8_t* occ;
+
+    // counters (u64): [0] tile dequeue (u32), [1] frame rays, [2] frame hits, [3] frame box tests,
+    // [4] frame primitive tests, [8] total rays, [9] total hits (since vrh_stats_reset)
+    unsigned long long* counters;
+};
+
+hipError_t launch_render(const render_params& p, int kind, bool ao, bool count, int stack_cap, int grid, hipStream_t s);
+int render_blocks_per_cu(int kind, bool ao, bool count, int stack_cap);
+int render_block_threads();
+hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t count, uint32_t rows_per_shard, const void* gcolor,
+                          const uint32_t* gpid, void* color, uint32_t* pid, hipStream_t s);
+
+} // namespace vrh

@@ -1,0 +1,592 @@
+// visionaray_amd/csrc/vrh_runtime.cpp -- the C-ABI of libvrh (include/vrh.h).
+//
+// Host-side runtime: contexts (device + stream + events + counters), scene upload with the
+// MI355X layout transform (node pairs, leaf-ordered primitives), render targets, the frame launch
+// (cuda_sched<R>::frame replacement, cuda_sched.inl:238-320), multi-GPU shard helpers and the
+// host builder entry point.  Every HIP call is checked; nothing throws across the ABI.
+
+#include "vrh_internal.h"
+#include "vrh_kernels.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+namespace vrh {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+} // namespace vrh
+
+using namespace vrh;
+
+#define VRH_HIP(call)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (call);                                                                    \
+        if (e_ != hipSuccess) {                                                                    \
+            set_error(std::string(#call) + ": " + hipGetErrorString(e_));                         \
+            return e_ == hipErrorOutOfMemory ? VRH_ERR_OOM : VRH_ERR_HIP;                          \
+        }                                                                                          \
+    } while (0)
+
+#define VRH_CHECK(cond, msg)                                                                       \
+    do {                                                                                           \
+        if (!(cond)) { set_error(msg); return VRH_ERR_INVALID; }                                   \
+    } while (0)
+
+struct vrh_ctx
+{
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int num_cus = 0;
+    // device counters (u64), see render_params::counters; [0..7] reset per frame
+    unsigned long long* counters = nullptr;
+    // one hipEvent pair per frame since vrh_stats_reset (ring of VRH_MAX_TIMED_FRAMES)
+    std::vector<hipEvent_t> ev_start, ev_stop;
+    uint32_t frames = 0;
+    uint32_t last_slot = 0;
+    vrh_frame_stats last{};
+    bool have_frame = false;
+};
+
+struct vrh_scene
+{
+    vrh_ctx* ctx = nullptr;
+    float4* pairs = nullptr;
+    float4* prims = nullptr;
+    float4* normals = nullptr;
+    uint32_t root = 0;
+    vrh_scene_info info{};
+};
+
+struct vrh_rt
+{
+    vrh_ctx* ctx = nullptr;
+    uint32_t width = 0, height = 0;
+    float4* color = nullptr;
+    uint32_t* prim_id = nullptr;
+    float* t = nullptr;
+    uint8_t* occ = nullptr;
+    bool owned = false;
+};
+
+namespace {
+
+int select_device(vrh_ctx* ctx)
+{
+    VRH_HIP(hipSetDevice(ctx->device));
+    return VRH_OK;
+}
+
+uint32_t bands_of(uint32_t height) { return (height + 15u) / 16u; }
+
+} // namespace
+
+extern "C" {
+
+VRH_API const char* vrh_version(void) { return "visionaray-amd 0.1.0 (gfx950)"; }
+VRH_API const char* vrh_last_error(void) { return g_last_error.c_str(); }
+
+VRH_API int vrh_device_count(int* count)
+{
+    VRH_CHECK(count, "vrh_device_count: null");
+    *count = 0;
+    hipError_t e = hipGetDeviceCount(count);
+    if (e != hipSuccess) { *count = 0; set_error(hipGetErrorString(e)); return VRH_ERR_NO_DEVICE; }
+    return VRH_OK;
+}
+
+VRH_API int vrh_ctx_create_on_stream(int hip_device, void* hip_stream, vrh_ctx** out)
+{
+    VRH_CHECK(out, "vrh_ctx_create: null out");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) { set_error("no HIP device visible"); return VRH_ERR_NO_DEVICE; }
+    VRH_CHECK(hip_device >= 0 && hip_device < n, "vrh_ctx_create: device index out of range");
+    auto* ctx = new (std::nothrow) vrh_ctx;
+    if (!ctx) { set_error("host allocation failed"); return VRH_ERR_OOM; }
+    ctx->device = hip_device;
+    int rc = VRH_OK;
+    do {
+        if ((rc = select_device(ctx)) != VRH_OK) break;
+        hipDeviceProp_t prop;
+        hipError_t e = hipGetDeviceProperties(&prop, hip_device);
+        if (e != hipSuccess) { set_error(hipGetErrorString(e)); rc = VRH_ERR_HIP; break; }
+        ctx->num_cus = prop.multiProcessorCount;
+        if (hip_stream) ctx->stream = static_cast<hipStream_t>(hip_stream);
+        else
+        {
+            e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+            if (e != hipSuccess) { set_error(hipGetErrorString(e)); rc = VRH_ERR_HIP; break; }
+            ctx->own_stream = true;
+        }
+        e = hipMalloc(&ctx->counters, 16 * sizeof(unsigned long long));
+        if (e != hipSuccess) { set_error(hipGetErrorString(e)); rc = VRH_ERR_OOM; break; }
+        e = hipMemset(ctx->counters, 0, 16 * sizeof(unsigned long long));
+        if (e != hipSuccess) { set_error(hipGetErrorString(e)); rc = VRH_ERR_HIP; break; }
+    } while (0);
+    if (rc != VRH_OK) { vrh_ctx_destroy(ctx); return rc; }
+    *out = ctx;
+    return VRH_OK;
+}
+
+VRH_API int vrh_ctx_create(int hip_device, vrh_ctx** out) { return vrh_ctx_create_on_stream(hip_device, nullptr, out); }
+
+VRH_API int vrh_ctx_destroy(vrh_ctx* ctx)
+{
+    if (!ctx) return VRH_OK;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->counters) (void)hipFree(ctx->counters);
+    for (auto e : ctx->ev_start) (void)hipEventDestroy(e);
+    for (auto e : ctx->ev_stop) (void)hipEventDestroy(e);
+    if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return VRH_OK;
+}
+
+// ---- scene upload -------------------------------------------------------------------------------
+
+VRH_API int vrh_scene_upload(vrh_ctx* ctx, const void* nodes_v, uint32_t num_nodes, const void* prims_v,
+                             uint32_t num_prims, uint32_t prim_kind, const uint32_t* indices, uint32_t num_indices,
+                             const void* face_normals, vrh_scene** out)
+{
+    VRH_CHECK(ctx && out && nodes_v && prims_v, "vrh_scene_upload: null argument");
+    VRH_CHECK(num_nodes >= 1 && num_prims >= 1, "vrh_scene_upload: empty BVH");
+    VRH_CHECK(prim_kind == VRH_PRIM_TRI64 || prim_kind == VRH_PRIM_SPHERE48, "vrh_scene_upload: unknown prim_kind");
+    VRH_CHECK(num_nodes % 2 == 1, "vrh_scene_upload: node count must be odd (root + child pairs)");
+    *out = nullptr;
+    if (!indices) num_indices = num_prims;
+    auto nodes = static_cast<const node32*>(nodes_v);
+
+    // -- node pairs + topology validation + depth
+    const uint32_t npairs = (num_nodes - 1) / 2;
+    std::vector<float4> pairs(4 * std::max<uint32_t>(npairs, 1), make_float4(0, 0, 0, 0));
+    std::vector<uint8_t> end_flag(num_indices, 0);
+    auto link_of = [&](const node32& c, uint32_t& link) -> bool {
+        if (c.num_prims != 0)
+        {
+            if (uint64_t(c.first) + c.num_prims > num_indices || c.first >= 0x80000000u) return false;
+            end_flag[c.first + c.num_prims - 1] = 1;
+            link = 0x80000000u | c.first;
+            return true;
+        }
+        if (c.first == 0 || c.first % 2 != 1 || uint64_t(c.first) + 1 >= num_nodes) return false;
+        link = (c.first - 1) / 2;
+        return true;
+    };
+    uint32_t root = 0;
+    if (!link_of(nodes[0], root)) { set_error("vrh_scene_upload: malformed root node"); return VRH_ERR_INVALID; }
+    if (nodes[0].num_prims == 0 && nodes[0].first != 1) { set_error("vrh_scene_upload: root children must be nodes 1,2"); return VRH_ERR_INVALID; }
+    for (uint32_t k = 0; k < npairs; ++k)
+    {
+        const node32& c0 = nodes[2 * k + 1];
+        const node32& c1 = nodes[2 * k + 2];
+        uint32_t l0, l1;
+        if (!link_of(c0, l0) || !link_of(c1, l1)) { set_error("vrh_scene_upload: malformed node pair " + std::to_string(k)); return VRH_ERR_INVALID; }
+        float4* q = &pairs[4 * k];
+        q[0] = make_float4(c0.bmin[0], c0.bmin[1], c0.bmin[2], c0.bmax[0]);
+        q[1] = make_float4(c0.bmax[1], c0.bmax[2], c1.bmin[0], c1.bmin[1]);
+        q[2] = make_float4(c1.bmin[2], c1.bmax[0], c1.bmax[1], c1.bmax[2]);
+        uint32_t w[4] = { l0, l1, 0u, 0u };
+        std::memcpy(&q[3], w, 16);
+    }
+    // depth (root depth 0) by iterative DFS over links
+    uint32_t max_depth = 0;
+    {
+        std::vector<std::pair<uint32_t, uint32_t>> st;
+        if (!(root & 0x80000000u)) st.push_back({ root, 1u });
+        size_t visited = 0;
+        while (!st.empty())
+        {
+            auto e = st.back(); st.pop_back();
+            if (++visited > npairs) { set_error("vrh_scene_upload: BVH is not a tree"); return VRH_ERR_INVALID; }
+            max_depth = std::max(max_depth, e.second);
+            uint32_t w[4];
+            std::memcpy(w, &pairs[4 * e.first + 3], 16);
+            for (int c = 0; c < 2; ++c)
+                if (!(w[c] & 0x80000000u))
+                {
+                    if (w[c] >= npairs) { set_error("vrh_scene_upload: child pair out of range"); return VRH_ERR_INVALID; }
+                    st.push_back({ w[c], e.second + 1 });
+                }
+        }
+    }
+
+    // -- leaf-ordered primitives with END flags
+    const uint32_t f4_per = prim_kind == VRH_PRIM_TRI64 ? 3u : 2u;
+    std::vector<float4> lp(size_t(f4_per) * num_indices);
+    for (uint32_t i = 0; i < num_indices; ++i)
+    {
+        uint32_t src = indices ? indices[i] : i;
+        if (src >= num_prims) { set_error("vrh_scene_upload: index out of range"); return VRH_ERR_INVALID; }
+        uint32_t flags = end_flag[i] ? 1u : 0u;
+        float4* q = &lp[size_t(f4_per) * i];
+        if (prim_kind == VRH_PRIM_TRI64)
+        {
+            const tri64& t = static_cast<const tri64*>(prims_v)[src];
+            q[0] = make_float4(t.v1[0], t.v1[1], t.v1[2], t.e1[0]);
+            q[1] = make_float4(t.e1[1], t.e1[2], t.e2[0], t.e2[1]);
+            uint32_t w[4];
+            std::memcpy(&w[0], &t.e2[2], 4);
+            w[1] = t.prim_id; w[2] = t.geom_id; w[3] = flags;
+            std::memcpy(&q[2], w, 16);
+        }
+        else
+        {
+            const sphere48& s = static_cast<const sphere48*>(prims_v)[src];
+            q[0] = make_float4(s.center[0], s.center[1], s.center[2], s.radius);
+            uint32_t w[4] = { s.prim_id, s.geom_id, flags, 0u };
+            std::memcpy(&q[1], w, 16);
+        }
+    }
+
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    auto* sc = new (std::nothrow) vrh_scene;
+    if (!sc) { set_error("host allocation failed"); return VRH_ERR_OOM; }
+    sc->ctx = ctx;
+    sc->root = root;
+    auto fail = [&](hipError_t e, const char* what) {
+        set_error(std::string(what) + ": " + hipGetErrorString(e));
+        vrh_scene_free(sc);
+        return e == hipErrorOutOfMemory ? VRH_ERR_OOM : VRH_ERR_HIP;
+    };
+    hipError_t e;
+    if ((e = hipMalloc(&sc->pairs, pairs.size() * sizeof(float4))) != hipSuccess) return fail(e, "hipMalloc(pairs)");
+    if ((e = hipMalloc(&sc->prims, lp.size() * sizeof(float4))) != hipSuccess) return fail(e, "hipMalloc(prims)");
+    if ((e = hipMemcpy(sc->pairs, pairs.data(), pairs.size() * sizeof(float4), hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "upload pairs");
+    if ((e = hipMemcpy(sc->prims, lp.data(), lp.size() * sizeof(float4), hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "upload prims");
+    uint64_t bytes = pairs.size() * sizeof(float4) + lp.size() * sizeof(float4);
+    if (face_normals)
+    {
+        if ((e = hipMalloc(&sc->normals, size_t(num_prims) * sizeof(float4))) != hipSuccess) return fail(e, "hipMalloc(normals)");
+        if ((e = hipMemcpy(sc->normals, face_normals, size_t(num_prims) * sizeof(float4), hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "upload normals");
+        bytes += size_t(num_prims) * sizeof(float4);
+    }
+    sc->info.num_nodes = num_nodes;
+    sc->info.num_prims = num_prims;
+    sc->info.num_indices = num_indices;
+    sc->info.prim_kind = prim_kind;
+    sc->info.max_depth = max_depth;
+    sc->info.device_bytes = bytes;
+    *out = sc;
+    return VRH_OK;
+}
+
+VRH_API int vrh_scene_get_info(const vrh_scene* scene, vrh_scene_info* info)
+{
+    VRH_CHECK(scene && info, "vrh_scene_get_info: null");
+    *info = scene->info;
+    return VRH_OK;
+}
+
+VRH_API int vrh_scene_free(vrh_scene* sc)
+{
+    if (!sc) return VRH_OK;
+    if (sc->ctx) (void)hipSetDevice(sc->ctx->device);
+    if (sc->pairs) (void)hipFree(sc->pairs);
+    if (sc->prims) (void)hipFree(sc->prims);
+    if (sc->normals) (void)hipFree(sc->normals);
+    delete sc;
+    return VRH_OK;
+}
+
+// ---- render targets ------------------------------------------------------------------------------
+
+VRH_API int vrh_rt_alloc(vrh_ctx* ctx, uint32_t w, uint32_t h, uint32_t flags, vrh_rt** out)
+{
+    VRH_CHECK(ctx && out && w > 0 && h > 0, "vrh_rt_alloc: bad argument");
+    *out = nullptr;
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    auto* rt = new (std::nothrow) vrh_rt;
+    if (!rt) { set_error("host allocation failed"); return VRH_ERR_OOM; }
+    rt->ctx = ctx; rt->width = w; rt->height = h; rt->owned = true;
+    size_t n = size_t(w) * h;
+    hipError_t e = hipSuccess;
+    if ((flags & VRH_RT_COLOR) && e == hipSuccess) e = hipMalloc(&rt->color, n * sizeof(float4));
+    if ((flags & VRH_RT_PRIM_ID) && e == hipSuccess) e = hipMalloc(&rt->prim_id, n * sizeof(uint32_t));
+    if ((flags & VRH_RT_T) && e == hipSuccess) e = hipMalloc(&rt->t, n * sizeof(float));
+    if ((flags & VRH_RT_OCC) && e == hipSuccess) e = hipMalloc(&rt->occ, n);
+    if (e != hipSuccess)
+    {
+        set_error(std::string("vrh_rt_alloc: ") + hipGetErrorString(e));
+        vrh_rt_free(rt);
+        return VRH_ERR_OOM;
+    }
+    *out = rt;
+    return VRH_OK;
+}
+
+VRH_API int vrh_rt_wrap(vrh_ctx* ctx, uint32_t w, uint32_t h, void* color, uint32_t* prim_id, float* t, uint8_t* occ,
+                        vrh_rt** out)
+{
+    VRH_CHECK(ctx && out && w > 0 && h > 0, "vrh_rt_wrap: bad argument");
+    auto* rt = new (std::nothrow) vrh_rt;
+    if (!rt) { set_error("host allocation failed"); return VRH_ERR_OOM; }
+    rt->ctx = ctx; rt->width = w; rt->height = h; rt->owned = false;
+    rt->color = static_cast<float4*>(color); rt->prim_id = prim_id; rt->t = t; rt->occ = occ;
+    *out = rt;
+    return VRH_OK;
+}
+
+VRH_API int vrh_rt_get_buffers(const vrh_rt* rt, void** color, uint32_t** prim_id, float** t, uint8_t** occ)
+{
+    VRH_CHECK(rt, "vrh_rt_get_buffers: null");
+    if (color) *color = rt->color;
+    if (prim_id) *prim_id = rt->prim_id;
+    if (t) *t = rt->t;
+    if (occ) *occ = rt->occ;
+    return VRH_OK;
+}
+
+VRH_API int vrh_rt_free(vrh_rt* rt)
+{
+    if (!rt) return VRH_OK;
+    if (rt->owned)
+    {
+        if (rt->ctx) (void)hipSetDevice(rt->ctx->device);
+        if (rt->color) (void)hipFree(rt->color);
+        if (rt->prim_id) (void)hipFree(rt->prim_id);
+        if (rt->t) (void)hipFree(rt->t);
+        if (rt->occ) (void)hipFree(rt->occ);
+    }
+    delete rt;
+    return VRH_OK;
+}
+
+namespace {
+__global__ void fill_rt_kernel(float4* color, uint32_t* pid, float* t, uint8_t* occ, size_t n, float4 c)
+{
+    size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (color) color[i] = c;
+    if (pid) pid[i] = 0xFFFFFFFFu;
+    if (t) t[i] = -1.0f;
+    if (occ) occ[i] = 0;
+}
+} // namespace
+
+// gpu_buffer_rt::clear_color_buffer (thrust::fill, gpu_buffer_rt.inl:49-76); side buffers reset to "miss"
+VRH_API int vrh_rt_clear(vrh_ctx* ctx, vrh_rt* rt, const float color[4])
+{
+    VRH_CHECK(ctx && rt, "vrh_rt_clear: null");
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    size_t n = size_t(rt->width) * rt->height;
+    float4 c = color ? make_float4(color[0], color[1], color[2], color[3]) : make_float4(0, 0, 0, 0);
+    hipLaunchKernelGGL(fill_rt_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, ctx->stream,
+                       rt->color, rt->prim_id, rt->t, rt->occ, n, c);
+    VRH_HIP(hipGetLastError());
+    return VRH_OK;
+}
+
+// ---- frame ----------------------------------------------------------------------------------------
+
+VRH_API uint32_t vrh_shard_bands(uint32_t height, uint32_t index, uint32_t count)
+{
+    uint32_t bands = bands_of(height);
+    if (count == 0 || index >= count || index >= bands) return 0;
+    return (bands - index + count - 1) / count;
+}
+
+VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_camera* cam,
+                       const vrh_kernel_desc* k, const vrh_shard* shard, uint32_t frame_num)
+{
+    (void)frame_num;  // the built-in kernels are deterministic; kept for cuda_sched::frame parity
+    VRH_CHECK(ctx && sc && rt && cam && k, "vrh_render: null argument");
+    VRH_CHECK(cam->width > 0 && cam->height > 0, "vrh_render: empty image");
+    VRH_CHECK(k->kind == VRH_KERNEL_PRIMARY || k->kind == VRH_KERNEL_AO, "vrh_render: unknown kernel kind");
+    const bool ao = k->kind == VRH_KERNEL_AO;
+    if (ao)
+    {
+        VRH_CHECK(k->samples >= 1 && k->samples <= 32, "vrh_render: AO samples must be in [1, 32]");
+        VRH_CHECK(sc->info.prim_kind != VRH_PRIM_TRI64 || sc->normals, "vrh_render: AO on triangles needs face normals");
+        VRH_CHECK(sc->normals, "vrh_render: AO needs normals");
+    }
+    vrh_shard whole{ 0, 1, 0, 0 };
+    const vrh_shard& sh = shard ? *shard : whole;
+    VRH_CHECK(sh.count >= 1 && sh.index < sh.count, "vrh_render: bad shard");
+    const uint32_t local_bands = vrh_shard_bands(cam->height, sh.index, sh.count);
+    VRH_CHECK(rt->width == cam->width, "vrh_render: render target width != camera width");
+    if (sh.packed) VRH_CHECK(rt->height >= local_bands * 16u || local_bands == 0, "vrh_render: packed target too small");
+    else VRH_CHECK(rt->height == cam->height, "vrh_render: render target height != camera height");
+
+    uint32_t cap = sc->info.max_depth <= 32 ? 32u : (sc->info.max_depth <= 64 ? 64u : 0u);
+    if (cap == 0) { set_error("vrh_render: BVH depth " + std::to_string(sc->info.max_depth) + " exceeds the 64-entry device stack"); return VRH_ERR_UNSUPPORTED; }
+
+    int rc = select_device(ctx);
+    if (rc) return rc;
+
+    render_params p{};
+    p.pairs = sc->pairs; p.prims = sc->prims; p.normals = sc->normals; p.root = sc->root;
+    std::memcpy(p.eye, cam->eye, 12); std::memcpy(p.cam_u, cam->cam_u, 12);
+    std::memcpy(p.cam_v, cam->cam_v, 12); std::memcpy(p.cam_w, cam->cam_w, 12);
+    p.width = cam->width; p.height = cam->height;
+    p.samples = ao ? k->samples : 0; p.radius = k->radius; p.eps = k->eps;
+    std::memcpy(p.bg, k->bg, 16);
+    p.shard_index = sh.index; p.shard_count = sh.count; p.packed = sh.packed ? 1u : 0u;
+    p.tiles_x = (cam->width + 7u) / 8u;
+    p.num_tiles = local_bands * 2u * p.tiles_x;
+    p.color = rt->color; p.prim_id = rt->prim_id; p.t = rt->t; p.occ = rt->occ;
+    p.counters = ctx->counters;
+
+    const int kind = sc->info.prim_kind == VRH_PRIM_TRI64 ? 0 : 1;
+    const bool count = (k->flags & VRH_KERNEL_COUNT_TESTS) != 0;
+    int per_cu = render_blocks_per_cu(kind, ao, count, int(cap));
+    int block = render_block_threads();
+    int waves_per_block = block / 64;
+    int grid = std::max(1, std::min<int>(ctx->num_cus * per_cu, int((p.num_tiles + waves_per_block - 1) / waves_per_block)));
+
+    const uint32_t slot = ctx->frames % VRH_MAX_TIMED_FRAMES;
+    while (ctx->ev_start.size() <= slot)
+    {
+        hipEvent_t a, b;
+        VRH_HIP(hipEventCreate(&a));
+        VRH_HIP(hipEventCreate(&b));
+        ctx->ev_start.push_back(a);
+        ctx->ev_stop.push_back(b);
+    }
+    VRH_HIP(hipMemsetAsync(ctx->counters, 0, 8 * sizeof(unsigned long long), ctx->stream));
+    VRH_HIP(hipEventRecord(ctx->ev_start[slot], ctx->stream));
+    if (p.num_tiles > 0) VRH_HIP(launch_render(p, kind, ao, count, int(cap), grid, ctx->stream));
+    VRH_HIP(hipEventRecord(ctx->ev_stop[slot], ctx->stream));
+    ctx->last_slot = slot;
+    ctx->frames++;
+
+    ctx->last = vrh_frame_stats{};
+    ctx->last.launches = p.num_tiles > 0 ? 1u : 0u;
+    ctx->last.grid_blocks = uint32_t(grid);
+    ctx->last.block_threads = uint32_t(block);
+    ctx->last.stack_depth = cap;
+    ctx->have_frame = true;
+    return VRH_OK;
+}
+
+VRH_API int vrh_sync(vrh_ctx* ctx)
+{
+    VRH_CHECK(ctx, "vrh_sync: null");
+    VRH_HIP(hipStreamSynchronize(ctx->stream));
+    return VRH_OK;
+}
+
+VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats)
+{
+    VRH_CHECK(ctx && stats, "vrh_last_frame_stats: null");
+    VRH_CHECK(ctx->have_frame, "vrh_last_frame_stats: no frame rendered yet");
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    VRH_HIP(hipEventSynchronize(ctx->ev_stop[ctx->last_slot]));
+    float ms = 0.0f;
+    VRH_HIP(hipEventElapsedTime(&ms, ctx->ev_start[ctx->last_slot], ctx->ev_stop[ctx->last_slot]));
+    unsigned long long c[8];
+    VRH_HIP(hipMemcpy(c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
+    ctx->last.kernel_ms = ms;
+    ctx->last.rays = c[1];
+    ctx->last.hits = c[2];
+    ctx->last.box_tests = c[3];
+    ctx->last.prim_tests = c[4];
+    *stats = ctx->last;
+    return VRH_OK;
+}
+
+VRH_API int vrh_stats_reset(vrh_ctx* ctx)
+{
+    VRH_CHECK(ctx, "vrh_stats_reset: null");
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    VRH_HIP(hipStreamSynchronize(ctx->stream));
+    VRH_HIP(hipMemset(ctx->counters + 8, 0, 8 * sizeof(unsigned long long)));
+    ctx->frames = 0;
+    return VRH_OK;
+}
+
+VRH_API int vrh_get_accum_stats(vrh_ctx* ctx, vrh_accum_stats* out)
+{
+    VRH_CHECK(ctx && out, "vrh_get_accum_stats: null");
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    VRH_HIP(hipStreamSynchronize(ctx->stream));
+    vrh_accum_stats a{};
+    a.frames = ctx->frames;
+    a.timed_frames = std::min<uint32_t>(ctx->frames, VRH_MAX_TIMED_FRAMES);
+    a.kernel_ms_min = 1e300;
+    for (uint32_t i = 0; i < a.timed_frames; ++i)
+    {
+        float ms = 0.0f;
+        VRH_HIP(hipEventElapsedTime(&ms, ctx->ev_start[i], ctx->ev_stop[i]));
+        a.kernel_ms_total += ms;
+        a.kernel_ms_min = std::min<double>(a.kernel_ms_min, ms);
+        a.kernel_ms_max = std::max<double>(a.kernel_ms_max, ms);
+    }
+    if (a.timed_frames == 0) a.kernel_ms_min = 0.0;
+    unsigned long long c[2];
+    VRH_HIP(hipMemcpy(c, ctx->counters + 8, sizeof(c), hipMemcpyDeviceToHost));
+    a.rays = c[0];
+    a.hits = c[1];
+    *out = a;
+    return VRH_OK;
+}
+
+VRH_API int vrh_rt_download(vrh_ctx* ctx, vrh_rt* rt, void* color, uint32_t* prim_id, float* t, uint8_t* occ)
+{
+    VRH_CHECK(ctx && rt, "vrh_rt_download: null");
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    size_t n = size_t(rt->width) * rt->height;
+    VRH_HIP(hipStreamSynchronize(ctx->stream));
+    if (color) { VRH_CHECK(rt->color, "vrh_rt_download: target has no colour buffer"); VRH_HIP(hipMemcpy(color, rt->color, n * 16, hipMemcpyDeviceToHost)); }
+    if (prim_id) { VRH_CHECK(rt->prim_id, "vrh_rt_download: target has no prim_id buffer"); VRH_HIP(hipMemcpy(prim_id, rt->prim_id, n * 4, hipMemcpyDeviceToHost)); }
+    if (t) { VRH_CHECK(rt->t, "vrh_rt_download: target has no t buffer"); VRH_HIP(hipMemcpy(t, rt->t, n * 4, hipMemcpyDeviceToHost)); }
+    if (occ) { VRH_CHECK(rt->occ, "vrh_rt_download: target has no occlusion buffer"); VRH_HIP(hipMemcpy(occ, rt->occ, n, hipMemcpyDeviceToHost)); }
+    return VRH_OK;
+}
+
+VRH_API int vrh_rt_upload(vrh_ctx* ctx, vrh_rt* rt, const void* color, const uint32_t* prim_id, const float* t,
+                          const uint8_t* occ)
+{
+    VRH_CHECK(ctx && rt, "vrh_rt_upload: null");
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    size_t n = size_t(rt->width) * rt->height;
+    VRH_HIP(hipStreamSynchronize(ctx->stream));
+    if (color) { VRH_CHECK(rt->color, "vrh_rt_upload: target has no colour buffer"); VRH_HIP(hipMemcpy(rt->color, color, n * 16, hipMemcpyHostToDevice)); }
+    if (prim_id) { VRH_CHECK(rt->prim_id, "vrh_rt_upload: target has no prim_id buffer"); VRH_HIP(hipMemcpy(rt->prim_id, prim_id, n * 4, hipMemcpyHostToDevice)); }
+    if (t) { VRH_CHECK(rt->t, "vrh_rt_upload: target has no t buffer"); VRH_HIP(hipMemcpy(rt->t, t, n * 4, hipMemcpyHostToDevice)); }
+    if (occ) { VRH_CHECK(rt->occ, "vrh_rt_upload: target has no occlusion buffer"); VRH_HIP(hipMemcpy(rt->occ, occ, n, hipMemcpyHostToDevice)); }
+    return VRH_OK;
+}
+
+VRH_API int vrh_unshard(vrh_ctx* ctx, uint32_t width, uint32_t height, uint32_t count, const void* gcolor,
+                        const uint32_t* gpid, vrh_rt* dst)
+{
+    VRH_CHECK(ctx && dst && count >= 1, "vrh_unshard: bad argument");
+    VRH_CHECK(dst->width == width && dst->height == height, "vrh_unshard: destination size mismatch");
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    uint32_t rows = 16u * vrh_shard_bands(height, 0, count);
+    VRH_HIP(launch_unshard(width, height, count, rows, gcolor, gpid, dst->color, dst->prim_id, ctx->stream));
+    return VRH_OK;
+}
+
+VRH_API int vrh_build_bvh(const void* prims, uint32_t num_prims, uint32_t kind, void* nodes_out,
+                          uint32_t* num_nodes_out, uint32_t* indices_out, uint32_t* max_depth_out)
+{
+    VRH_CHECK(prims && nodes_out && num_nodes_out && indices_out, "vrh_build_bvh: null argument");
+    VRH_CHECK(num_prims >= 1, "vrh_build_bvh: no primitives");
+    VRH_CHECK(kind == VRH_PRIM_TRI64 || kind == VRH_PRIM_SPHERE48, "vrh_build_bvh: unknown prim kind");
+    try
+    {
+        return build_bvh(prims, num_prims, kind, static_cast<node32*>(nodes_out), num_nodes_out, indices_out, max_depth_out);
+    }
+    catch (const std::bad_alloc&) { set_error("vrh_build_bvh: out of host memory"); return VRH_ERR_OOM; }
+}
+
+} // extern "C"
