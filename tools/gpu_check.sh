@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 fatal() { case "$1" in 124|134|137|139) return 0;; esac; return 1; }
 
 echo "== pytest -m gpu"
-timeout -k 10 ${PYTEST_TIMEOUT:-600} python -m pytest tests -m gpu -q -p no:cacheprovider ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 150 ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; tail -25 gpurun_out/pytest_gpu.log; echo "pytest rc=$rc"
 if fatal $rc; then echo "fatal pytest exit; stopping"; exit $rc; fi
 

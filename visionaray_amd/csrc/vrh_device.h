@@ -130,13 +130,18 @@ struct lds_stack
 // far child pushed, leaf primitives tested in index order, AnyHit exits at the first accepted hit
 // (exit_traversal.h:49-56).  Box culling uses the running closest t exactly like the reference;
 // popped nodes are NOT re-culled (the reference does not), which keeps tie resolution identical.
-struct test_counts { uint32_t box, prim; };
+struct test_counts { uint32_t box, prim; bool aborted; };
 
+// step_limit bounds the node visits + primitive tests of one ray (a correct traversal never needs
+// more than nodes + primitives); a corrupt BVH therefore ends the ray with `aborted` set instead
+// of spinning the wave forever.
 template <int KIND, bool ANY, bool COUNT, class Stack>
 __device__ __forceinline__ hit_t trace(const float4* __restrict__ pairs, const float4* __restrict__ prims,
-                                       uint32_t root, const ray_t& r, float max_t, Stack& st, test_counts& cnt)
+                                       uint32_t root, const ray_t& r, float max_t, Stack& st, test_counts& cnt,
+                                       uint32_t step_limit)
 {
     hit_t res = miss_record();
+    uint32_t steps = 0;
     st.sp = 0;
     st.push(root);
     while (!st.empty())
@@ -144,6 +149,7 @@ __device__ __forceinline__ hit_t trace(const float4* __restrict__ pairs, const f
         uint32_t link = st.pop();
         while (!(link & LEAF_BIT))
         {
+            if (++steps > step_limit) { cnt.aborted = true; return res; }
             const float4* p = pairs + 4u * link;
             float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
             float tn0, tn1;
@@ -193,6 +199,7 @@ __device__ __forceinline__ hit_t trace(const float4* __restrict__ pairs, const f
                 }
                 if (flags & END_BIT) break;
                 ++i;
+                if (++steps > step_limit) { cnt.aborted = true; return res; }
             }
         }
     next:;

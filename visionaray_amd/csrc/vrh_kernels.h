@@ -12,6 +12,7 @@ struct render_params
     const float4* prims;      // leaf-ordered primitives (3 float4 tri, 2 float4 sphere)
     const float4* normals;    // per prim_id
     uint32_t root;            // root link (pair 0, or LEAF_BIT|0 for a single-leaf tree)
+    uint32_t step_limit;      // per-ray traversal step bound (nodes + primitives)
 
     float eye[3], cam_u[3], cam_v[3], cam_w[3];
     uint32_t width, height;
@@ -29,7 +30,8 @@ struct render_params
     uint8_t* occ;
 
     // counters (u64): [0] tile dequeue (u32), [1] frame rays, [2] frame hits, [3] frame box tests,
-    // [4] frame primitive tests, [8] total rays, [9] total hits (since vrh_stats_reset)
+    // [4] frame primitive tests, [5] frame error flags (1 = traversal step guard tripped),
+    // [8] total rays, [9] total hits (since vrh_stats_reset)
     unsigned long long* counters;
 };
 

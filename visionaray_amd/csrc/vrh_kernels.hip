@@ -64,7 +64,7 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(render_params P)
     lds_stack<CAP, BLOCK> st;
     st.col = stack_mem + tid;
     st.sp = 0;
-    test_counts cnt = { 0u, 0u };
+    test_counts cnt = { 0u, 0u, false };
 
     for (;;)
     {
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(render_params P)
         if (valid)
         {
             r = primary_ray(P, x, y);
-            h = trace<KIND, false, COUNT>(P.pairs, P.prims, P.root, r, 3.402823466e+38f, st, cnt);
+            h = trace<KIND, false, COUNT>(P.pairs, P.prims, P.root, r, 3.402823466e+38f, st, cnt, P.step_limit);
         }
         float4 color = make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
         uint32_t occ_mask = 0;
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(render_params P)
                     f3 bu = cross(bv, n);
                     f3 d = ao_direction(p, s, bu, bv, n);
                     ray_t ar = make_ray(pos + d * P.eps, d);
-                    hit_t a = trace<KIND, true, COUNT>(P.pairs, P.prims, P.root, ar, P.radius, st, cnt);
+                    hit_t a = trace<KIND, true, COUNT>(P.pairs, P.prims, P.root, ar, P.radius, st, cnt, P.step_limit);
                     occl = a.hit;
                 }
                 // route occlusion bits back to the owning lanes: owner lane collects its bits
@@ -175,6 +175,7 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(render_params P)
             if (P.t) P.t[o] = h.hit ? h.t : -1.0f;
             if (P.occ) P.occ[o] = (uint8_t)occ_mask;
         }
+        if (__ballot(cnt.aborted) != 0ull && lane == 0) atomicOr(P.counters + 5, 1ull);
         if (lane == 0)
         {
             unsigned long long nh = (unsigned long long)__popcll(hitmask);

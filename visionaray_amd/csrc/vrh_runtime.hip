@@ -427,6 +427,7 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
 
     render_params p{};
     p.pairs = sc->pairs; p.prims = sc->prims; p.normals = sc->normals; p.root = sc->root;
+    p.step_limit = sc->info.num_nodes + sc->info.num_indices + 16u;
     std::memcpy(p.eye, cam->eye, 12); std::memcpy(p.cam_u, cam->cam_u, 12);
     std::memcpy(p.cam_v, cam->cam_v, 12); std::memcpy(p.cam_w, cam->cam_w, 12);
     p.width = cam->width; p.height = cam->height;
@@ -494,6 +495,7 @@ VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats)
     ctx->last.box_tests = c[3];
     ctx->last.prim_tests = c[4];
     *stats = ctx->last;
+    if (c[5] & 1ull) { set_error("traversal step guard tripped: corrupt BVH (rays were cut short)"); return VRH_ERR_HIP; }
     return VRH_OK;
 }
 
