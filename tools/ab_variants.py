@@ -1,0 +1,79 @@
+"""A/B launch variants of the traversal kernel in ONE process, interleaved rounds (guide §5.4 rule 24).
+
+    python tools/ab_variants.py [scene] [rounds]
+Each variant is also checked bit-exactly (prim_id / occ / colour hashes) against tests/golden.
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+
+import visionaray_amd as va  # noqa: E402
+from visionaray_amd import scenes  # noqa: E402
+
+scene = sys.argv[1] if len(sys.argv) > 1 else "hf1M"
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+VARIANTS = json.loads(os.environ.get("VRH_AB", "null")) or [
+    {"name": "refill b64", "block_threads": 64, "ao_schedule": 2},
+    {"name": "rounds b64", "block_threads": 64, "ao_schedule": 1},
+    {"name": "refill b256", "block_threads": 256, "ao_schedule": 2},
+    {"name": "rounds b256 cap32", "block_threads": 256, "ao_schedule": 1, "stack_cap": 32},
+    {"name": "refill b64 cap32", "block_threads": 64, "ao_schedule": 2, "stack_cap": 32},
+    {"name": "refill b128", "block_threads": 128, "ao_schedule": 2},
+]
+os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+log = open(os.path.join(ROOT, "gpurun_out", f"ab_{scene}.log"), "a", buffering=1)
+
+
+def say(*a):
+    print(*a, flush=True)
+    print(*a, file=log, flush=True)
+
+
+golden = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
+g = golden.get(scene)
+sys.path.insert(0, ROOT)
+from oracle import oracle as O  # noqa: E402  (hash helper only)
+
+prims = scenes.primitives(scene)
+host = va.build_index_bvh(prims)
+ctx = va.Context(0)
+dev = va.hip_index_bvh(ctx, host, scenes.normals_for(prims))
+cam, W, H = scenes.scene_camera(scene)
+basis = cam.basis(W, H)
+ao = prims.dtype == va.TRIANGLE_DTYPE and os.environ.get("VRH_AB_KERNEL", "ao") == "ao"
+kern = va.ao_kernel(dev) if ao else va.closest_hit_kernel(dev)
+rt = va.hip_buffer_rt(ctx, W, H)
+say(f"scene {scene} {len(prims)} prims depth {host.max_depth} ao={ao}")
+res = {v["name"]: [] for v in VARIANTS}
+for rnd in range(rounds):
+    for v in VARIANTS:
+        ctx.set_option("block_threads", v.get("block_threads", 0))
+        ctx.set_option("stack_cap", v.get("stack_cap", 0))
+        ctx.set_option("ao_schedule", v.get("ao_schedule", 0))
+        ctx.set_option("blocks_per_cu", v.get("blocks_per_cu", 0))
+        ctx.set_option("waves_per_simd", v.get("waves_per_simd", 0))
+        ctx.set_option("exact_minmax", v.get("exact_minmax", 0))
+        ctx.stats_reset()
+        for _ in range(5):
+            va.render(ctx, dev, rt, basis, kern)
+        a = ctx.accum_stats()
+        st = ctx.last_frame_stats()
+        ms = a["kernel_ms_min"]
+        res[v["name"]].append((a["kernel_ms_total"] / a["timed_frames"], ms, a["rays"] / a["frames"]))
+        if rnd == 0 and g is not None:
+            out = rt.download()
+            ok = (O.fnv1a(out["prim_id"]) == g["primid_hash"] and O.fnv1a(out["t"]) == g["t_hash"]
+                  and (not ao or (O.fnv1a(out["occ"]) == g["occ_hash"] and O.fnv1a(out["color"]) == g["color_hash"])))
+            say(f"  {v['name']:24s} grid {st['grid_blocks']} x {st['block_threads']} stack {st['stack_depth']} "
+                f"parity {'OK' if ok else 'MISMATCH'}")
+say(f"{'variant':26s} {'mean ms':>9s} {'min ms':>9s} {'Mrays/s(min)':>13s}")
+for name, vals in res.items():
+    mean = float(np.median([x[0] for x in vals]))
+    mn = float(np.min([x[1] for x in vals]))
+    rays = vals[0][2]
+    say(f"{name:26s} {mean:9.4f} {mn:9.4f} {rays / mn / 1e3:13.1f}")

@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libvrh.so")
+LIB_PATH = os.environ.get("VRH_LIB") or os.path.join(_HERE, "_lib", "libvrh.so")
 
 # enums (vrh.h)
 VRH_OK, VRH_ERR_INVALID, VRH_ERR_HIP, VRH_ERR_OOM, VRH_ERR_UNSUPPORTED, VRH_ERR_NO_DEVICE = range(6)
@@ -30,6 +30,8 @@ class vrh_kernel_desc(C.Structure):
 
 
 VRH_KERNEL_COUNT_TESTS = 1
+VRH_OPT_BLOCK_THREADS, VRH_OPT_STACK_CAP, VRH_OPT_AO_SCHEDULE, VRH_OPT_BLOCKS_PER_CU = 1, 2, 3, 4
+VRH_OPT_WAVES_PER_SIMD, VRH_OPT_EXACT_MINMAX = 5, 6
 VRH_MAX_TIMED_FRAMES = 1024
 
 
@@ -70,6 +72,7 @@ SIGNATURES = {
     "vrh_ctx_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
     "vrh_ctx_create_on_stream": (C.c_int, [C.c_int, _vp, C.POINTER(_vp)]),
     "vrh_ctx_destroy": (C.c_int, [_vp]),
+    "vrh_ctx_set_option": (C.c_int, [_vp, _u32, C.c_int64]),
     "vrh_scene_upload": (C.c_int, [_vp, _vp, _u32, _vp, _u32, _u32, _vp, _u32, _vp, C.POINTER(_vp)]),
     "vrh_scene_get_info": (C.c_int, [_vp, C.POINTER(vrh_scene_info)]),
     "vrh_scene_free": (C.c_int, [_vp]),

@@ -13,6 +13,8 @@ struct render_params
     const float4* normals;    // per prim_id
     uint32_t root;            // root link (pair 0, or LEAF_BIT|0 for a single-leaf tree)
     uint32_t step_limit;      // per-ray traversal step bound (nodes + primitives)
+    uint32_t stack_cap;       // LDS stack entries per lane (>= BVH depth)
+    uint32_t fast_ok;         // node bounds all finite: hardware min/max slab path allowed
 
     float eye[3], cam_u[3], cam_v[3], cam_w[3];
     uint32_t width, height;
@@ -35,9 +37,20 @@ struct render_params
     unsigned long long* counters;
 };
 
-hipError_t launch_render(const render_params& p, int kind, bool ao, bool count, int stack_cap, int grid, hipStream_t s);
-int render_blocks_per_cu(int kind, bool ao, bool count, int stack_cap);
-int render_block_threads();
+struct launch_config
+{
+    int kind;          // 0 triangles, 1 spheres
+    bool ao;
+    bool count;        // VRH_KERNEL_COUNT_TESTS variant
+    int sched;         // AO schedule: 0 rounds, 1 refill
+    int block;         // threads per block (multiple of 64)
+    int stack_cap;     // LDS stack entries per lane
+    int occ;           // unified kernel register budget: min waves per SIMD (1, 6 or 8)
+};
+
+size_t render_lds_bytes(const launch_config& c);
+hipError_t launch_render(const render_params& p, const launch_config& c, int grid, hipStream_t s);
+int render_blocks_per_cu(const launch_config& c);
 hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t count, uint32_t rows_per_shard, const void* gcolor,
                           const uint32_t* gpid, void* color, uint32_t* pid, hipStream_t s);
 

@@ -2,23 +2,30 @@
 //
 // Replaces cuda_sched's render<<<grid,block>>> (cuda_sched.inl:53-153, one thread per pixel on a
 // 2-D grid) with a persistent-thread design:
-//   * the grid is sized to residency (CUs x blocks/CU); every wave pulls 8x8 pixel tiles from a
-//     device-wide atomic counter until the frame's tiles are exhausted (work stealing, the
+//   * the grid is sized to residency (CUs x resident blocks); every wave pulls 8x8 pixel tiles from
+//     a device-wide atomic counter until the frame's tiles are exhausted (work stealing: the
 //     tiled_sched.inl:194 fetch_add moved onto the GPU); a wave's 64 lanes are one 8x8 tile, so
-//     primary rays of a wave are coherent;
-//   * each lane keeps its traversal stack in LDS (column-major, conflict-free);
-//   * AO (ao/main.cpp:183-246) is fused: the hit pixels' 8 any-hit rays are generated on chip and
-//     redistributed over the wave's lanes (ballot + mbcnt compaction through LDS), so no ray buffer
-//     touches HBM and lanes whose pixel missed still trace AO rays.
+//     the primary rays of a wave are coherent;
+//   * each lane keeps its traversal stack in LDS (dynamic shared memory, column-major
+//     [entry][lane] so a wave's pushes/pops are bank-conflict free); the stack capacity is chosen
+//     per scene from the BVH depth (a depth-first traversal never holds more than depth entries);
+//   * AO (ao/main.cpp:183-246) is fused: the tile's hit records are staged in LDS and its
+//     hits x samples any-hit rays are generated on chip -- no ray buffer touches HBM.  Two
+//     schedules: ROUNDS hands rays out 64 at a time (a round waits for its slowest lane); REFILL
+//     gives a lane a new ray the moment its ray terminates (ballot + mbcnt compaction of the idle
+//     lanes), so the wave stays busy until the tile's ray pool is empty.
 #include "vrh_device.h"
 #include "vrh_kernels.h"
 
 namespace vrh {
 namespace dev {
 
-constexpr int BLOCK = 256;          // 4 waves
 constexpr int TILE = 8;             // 8x8 pixels per wave
 constexpr uint32_t BAND = 16;       // shard band height (tiled_sched tile_height)
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr int AO_REC_WORDS = 8;     // per hit slot: isect pos xyz, normal xyz, pixel index, lane
+// per-wave AO area in LDS: 64 hit records + 64 occlusion masks
+constexpr int AO_WAVE_WORDS = 64 * AO_REC_WORDS + 64;
 
 // tile index -> (x, y) of lane, plus the output row (packed shards)
 __device__ __forceinline__ bool tile_pixel(const render_params& P, uint32_t tile, uint32_t lane,
@@ -50,20 +57,46 @@ __device__ __forceinline__ ray_t primary_ray(const render_params& P, uint32_t x,
     return make_ray(mk3(P.eye[0], P.eye[1], P.eye[2]), dir);
 }
 
-template <int KIND, int CAP, bool AO, bool COUNT>
-__global__ __launch_bounds__(BLOCK) void render_kernel(render_params P)
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask)
 {
-    // LDS: traversal stacks [CAP][BLOCK] + per-wave AO work list (pixel slot per ray)
-    __shared__ uint32_t stack_mem[CAP * BLOCK];
-    __shared__ uint32_t ao_pix[AO ? BLOCK : 1];         // lane -> hit record slot, per wave 64
-    __shared__ float ao_hit[AO ? BLOCK * 8 : 1];        // per lane: isect pos xyz, basis n xyz, t, pad
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
 
+// AO ray j of the tile: hit slot j / S, sample j % S (ao/main.cpp:216-238 with the Appendix-A
+// sampler); returns the ray and the slot.
+__device__ __forceinline__ ray_t ao_ray(const render_params& P, const float* recs, uint32_t j, uint32_t S,
+                                        uint32_t& slot, uint32_t& s)
+{
+    slot = j / S;
+    s = j - slot * S;
+    const float* sr = recs + slot * AO_REC_WORDS;
+    f3 pos = mk3(sr[0], sr[1], sr[2]);
+    f3 n = mk3(sr[3], sr[4], sr[5]);
+    uint32_t p = __float_as_uint(sr[6]);
+    // vector3.inl:357-367 make_orthonormal_basis(u, v, w = n)
+    f3 bv = fabsf(n.x) > fabsf(n.y) ? normalize(mk3(-n.z, 0.0f, n.x)) : normalize(mk3(0.0f, n.z, -n.y));
+    f3 bu = cross(bv, n);
+    f3 d = ao_direction(p, s, bu, bv, n);
+    return make_ray(pos + d * P.eps, d);
+}
+
+template <int KIND, bool AO, bool COUNT, int SCHED>
+__global__ void render_kernel(render_params P)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = tid >> 6;
-    lds_stack<CAP, BLOCK> st;
-    st.col = stack_mem + tid;
-    st.sp = 0;
+    const uint32_t block = blockDim.x;
+
+    lds_stack st;
+    st.mem = smem;
+    st.base = tid;
+    st.stride = block;
+    st.top = tid;
+    uint32_t* ao_area = smem + P.stack_cap * block + wave * AO_WAVE_WORDS;
+    float* recs = reinterpret_cast<float*>(ao_area);          // 64 records x AO_REC_WORDS
+    uint32_t* masks = ao_area + 64 * AO_REC_WORDS;             // occlusion mask per hit slot
     test_counts cnt = { 0u, 0u, false };
 
     for (;;)
@@ -85,77 +118,86 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(render_params P)
         }
         float4 color = make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
         uint32_t occ_mask = 0;
-        uint64_t hitmask = __ballot(valid && h.hit);
+        const bool is_hit = valid && h.hit;
+        const uint64_t hitmask = __ballot(is_hit);
         uint32_t nrays = (uint32_t)__popcll(__ballot(valid));
 
         if constexpr (AO)
         {
-            // ---- stage hit records of this wave in LDS -------------------------------------
-            float* rec = ao_hit + (wave * 64u + lane) * 8u;
-            if (valid && h.hit)
+            // ---- stage this wave's hit records (compacted: slot k = k-th hit lane) ----------
+            const uint32_t hits = (uint32_t)__popcll(hitmask);
+            const uint32_t slot = lane_rank(hitmask);
+            if (is_hit)
             {
                 f3 pos = r.ori + r.dir * h.t;                       // ao/main.cpp:202
                 float4 nn = P.normals[h.prim_id];                   // get_normal.h:26-37
+                float* rec = recs + slot * AO_REC_WORDS;
                 rec[0] = pos.x; rec[1] = pos.y; rec[2] = pos.z;
                 rec[3] = nn.x; rec[4] = nn.y; rec[5] = nn.z;
                 rec[6] = __uint_as_float(y * P.width + x);          // global pixel index p
+                masks[slot] = 0u;
             }
-            // compact the hit lanes: slot k of the wave's list = k-th hit lane
-            uint32_t hits = (uint32_t)__popcll(hitmask);
-            uint32_t slot = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(hitmask >> 32),
-                                 __builtin_amdgcn_mbcnt_lo((uint32_t)hitmask, 0u));
-            uint32_t* list = ao_pix + wave * 64u;
-            if (valid && h.hit) list[slot] = lane;
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
-            // ---- AO rays: ray j = (hit slot j / S, sample j % S), spread over all 64 lanes ----
             const uint32_t S = P.samples;
             const uint32_t total = hits * S;
-            uint32_t my_occ_bits = 0;   // bits gathered for the lane's OWN pixel (set below)
-            const float step = 1.0f / (float)S;
-            for (uint32_t base = 0; base < total; base += 64u)
+            if constexpr (SCHED == SCHED_ROUNDS)
             {
-                uint32_t j = base + lane;
-                bool occl = false;
-                uint32_t src_lane = 0, s = 0;
-                if (j < total)
+                for (uint32_t base = 0; base < total; base += 64u)
                 {
-                    uint32_t hs = j / S;
-                    s = j - hs * S;
-                    src_lane = list[hs];
-                    const float* sr = ao_hit + (wave * 64u + src_lane) * 8u;
-                    f3 pos = mk3(sr[0], sr[1], sr[2]);
-                    f3 n = mk3(sr[3], sr[4], sr[5]);
-                    uint32_t p = __float_as_uint(sr[6]);
-                    // vector3.inl:357-367 make_orthonormal_basis(u, v, w = n)
-                    f3 bv = fabsf(n.x) > fabsf(n.y) ? normalize(mk3(-n.z, 0.0f, n.x)) : normalize(mk3(0.0f, n.z, -n.y));
-                    f3 bu = cross(bv, n);
-                    f3 d = ao_direction(p, s, bu, bv, n);
-                    ray_t ar = make_ray(pos + d * P.eps, d);
-                    hit_t a = trace<KIND, true, COUNT>(P.pairs, P.prims, P.root, ar, P.radius, st, cnt, P.step_limit);
-                    occl = a.hit;
-                }
-                // route occlusion bits back to the owning lanes: owner lane collects its bits
-                uint64_t occ_ball = __ballot(occl);
-                // each owner lane checks which of rays [base, base+64) are its own
-                if (valid && h.hit)
-                {
-                    uint32_t my_first = slot * S;                    // my rays: [my_first, my_first+S)
-                    for (uint32_t s2 = 0; s2 < S; ++s2)
+                    uint32_t j = base + lane;
+                    if (j < total)
                     {
-                        uint32_t jj = my_first + s2;
-                        if (jj >= base && jj < base + 64u && ((occ_ball >> (jj - base)) & 1ull))
-                            my_occ_bits |= 1u << s2;
+                        uint32_t hs, s;
+                        ray_t ar = ao_ray(P, recs, j, S, hs, s);
+                        hit_t a = trace<KIND, true, COUNT>(P.pairs, P.prims, P.root, ar, P.radius, st, cnt, P.step_limit);
+                        if (a.hit) atomicOr(&masks[hs], 1u << s);
                     }
                 }
-                (void)src_lane;
             }
-            nrays += total;
-            if (valid && h.hit)
+            else
             {
-                occ_mask = my_occ_bits;
+                // REFILL: a lane whose ray terminated takes the next unassigned ray of the tile
+                uint32_t next = 0;                     // wave-uniform: rays handed out so far
+                uint32_t cur = NONE, cur_slot = 0, cur_s = 0, steps = 0;
+                ray_t ar;
+                for (;;)
+                {
+                    const uint64_t idle = __ballot(cur == NONE);
+                    if (idle)
+                    {
+                        uint32_t cand = next + lane_rank(idle);
+                        next += (uint32_t)__popcll(idle);
+                        if (cur == NONE && cand < total)
+                        {
+                            cur = cand;
+                            ar = ao_ray(P, recs, cand, S, cur_slot, cur_s);
+                            st.reset();
+                            st.push(P.root);
+                            steps = 0;
+                        }
+                    }
+                    if (__ballot(cur != NONE) == 0ull) break;
+                    if (cur != NONE)
+                    {
+                        int done = anyhit_step<KIND, COUNT>(P.pairs, P.prims, ar, P.radius, st, cnt, steps, P.step_limit);
+                        if (done)
+                        {
+                            if (done > 0) atomicOr(&masks[cur_slot], 1u << cur_s);
+                            cur = NONE;
+                        }
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            nrays += total;
+            if (is_hit)
+            {
+                occ_mask = masks[slot];
                 float clr = 1.0f;
+                const float step = 1.0f / (float)S;
                 for (uint32_t s2 = 0; s2 < S; ++s2)
                     if ((occ_mask >> s2) & 1u) clr = clr - step;     // ao/main.cpp:234-238
                 color = make_float4(clr, clr, clr, 1.0f);
@@ -164,15 +206,15 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(render_params P)
         }
         else
         {
-            if (valid && h.hit) color = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+            if (is_hit) color = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
         }
 
         if (valid)
         {
             size_t o = (size_t)orow * P.width + x;
             if (P.color) P.color[o] = color;
-            if (P.prim_id) P.prim_id[o] = h.hit ? h.prim_id : 0xFFFFFFFFu;
-            if (P.t) P.t[o] = h.hit ? h.t : -1.0f;
+            if (P.prim_id) P.prim_id[o] = is_hit ? h.prim_id : 0xFFFFFFFFu;
+            if (P.t) P.t[o] = is_hit ? h.t : -1.0f;
             if (P.occ) P.occ[o] = (uint8_t)occ_mask;
         }
         if (__ballot(cnt.aborted) != 0ull && lane == 0) atomicOr(P.counters + 5, 1ull);
@@ -202,6 +244,242 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(render_params P)
     }
 }
 
+// UNIFIED schedule: one refilling loop per wave.  Primary rays (one per pixel of the wave's tile)
+// and AO rays (published as soon as their primary hit is known) are stepped by the same
+// instruction stream (ray_step); a lane that finishes a ray immediately takes the next one, so
+// neither the primary phase nor the AO phase waits for its slowest lane.  Without AO the wave
+// streams pixels tile after tile and writes each pixel when its ray finishes.
+template <int KIND, bool AO, bool COUNT, int OCC>
+__global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params P)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = tid >> 6;
+    const uint32_t block = blockDim.x;
+    const float FMAX = 3.402823466e+38f;
+
+    lds_stack st;
+    st.mem = smem;
+    st.base = tid;
+    st.stride = block;
+    st.top = tid;
+    uint32_t* ao_area = smem + P.stack_cap * block + wave * AO_WAVE_WORDS;
+    float* recs = reinterpret_cast<float*>(ao_area);
+    uint32_t* masks = ao_area + 64 * AO_REC_WORDS;
+    test_counts cnt = { 0u, 0u, false };
+    uint64_t rays_total = 0, hits_total = 0;
+
+    // lane state: the ray it is stepping
+    constexpr uint32_t IDLE = 0, PRIMARY = 1, AORAY = 2;
+    uint32_t mode = IDLE;
+    ray_t r;
+    float best_t = FMAX, max_t = FMAX;
+    uint32_t best_prim = 0, steps = 0;
+    bool any = false;
+
+    if constexpr (!AO)
+    {
+        // ---- primary visibility: stream pixels, write each when its ray finishes ------------
+        uint32_t tile = 0;
+        if (lane == 0) tile = atomicAdd(reinterpret_cast<uint32_t*>(P.counters), 1u);
+        tile = __shfl(tile, 0);
+        uint32_t handed = 0;                       // pixels of `tile` handed out (wave-uniform)
+        uint32_t out_o = 0;
+        for (;;)
+        {
+            uint64_t idle = __ballot(mode == IDLE);
+            if (idle)
+            {
+                if (handed >= 64u && tile < P.num_tiles)
+                {
+                    if (lane == 0) tile = atomicAdd(reinterpret_cast<uint32_t*>(P.counters), 1u);
+                    tile = __shfl(tile, 0);
+                    handed = 0;
+                }
+                if (tile < P.num_tiles)
+                {
+                    uint32_t cand = handed + lane_rank(idle);
+                    handed = min(64u, handed + (uint32_t)__popcll(idle));
+                    if (mode == IDLE && cand < 64u)
+                    {
+                        uint32_t x, y, orow;
+                        if (tile_pixel(P, tile, cand, x, y, orow))
+                        {
+                            r = primary_ray(P, x, y);
+                            out_o = orow * P.width + x;
+                            best_t = FMAX; best_prim = 0; steps = 0;
+                            st.reset(); st.push(P.root);
+                            mode = PRIMARY;
+                            rays_total += 1;
+                        }
+                    }
+                }
+            }
+            if (__ballot(mode != IDLE) == 0ull)
+            {
+                if (tile >= P.num_tiles) break;
+                continue;
+            }
+            if (mode != IDLE)
+            {
+                int rc = (P.fast_ok && __ballot(!finite_ray(r)) == 0ull)
+                    ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit)
+                    : ray_step<KIND, COUNT, false>(P.pairs, P.prims, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit);
+                if (rc != 0)
+                {
+                    bool hit = best_t != FMAX;
+                    hits_total += hit ? 1 : 0;
+                    if (P.color) P.color[out_o] = hit ? make_float4(1.0f, 1.0f, 1.0f, 1.0f) : make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
+                    if (P.prim_id) P.prim_id[out_o] = hit ? best_prim : 0xFFFFFFFFu;
+                    if (P.t) P.t[out_o] = hit ? best_t : -1.0f;
+                    if (P.occ) P.occ[out_o] = 0;
+                    mode = IDLE;
+                }
+            }
+        }
+    }
+    else
+    {
+        const uint32_t S = P.samples;
+        for (;;)
+        {
+            uint32_t tile = 0;
+            if (lane == 0) tile = atomicAdd(reinterpret_cast<uint32_t*>(P.counters), 1u);
+            tile = __shfl(tile, 0);
+            if (tile >= P.num_tiles) break;
+
+            uint32_t x, y, orow;
+            const bool valid = tile_pixel(P, tile, lane, x, y, orow);
+            // own pixel's results
+            bool my_hit = false, just_done = false;
+            uint32_t my_prim = 0xFFFFFFFFu, my_slot = 0;
+            float my_t = -1.0f;
+            if (valid)
+            {
+                r = primary_ray(P, x, y);
+                best_t = FMAX; best_prim = 0; steps = 0; max_t = FMAX; any = false;
+                st.reset(); st.push(P.root);
+                mode = PRIMARY;
+            }
+            uint32_t pending = (uint32_t)__popcll(__ballot(valid));   // primaries not yet finished
+            rays_total += valid ? 1 : 0;
+            uint32_t published = 0, issued = 0;                        // hit slots, AO rays handed out
+            uint32_t cur_slot = 0, cur_s = 0;
+            for (;;)
+            {
+                // 1. publish primaries that finished last iteration (compacted hit slots)
+                const uint64_t fin = __ballot(just_done);
+                if (fin)
+                {
+                    const uint64_t hfin = __ballot(just_done && my_hit);
+                    if (just_done && my_hit)
+                    {
+                        my_slot = published + lane_rank(hfin);
+                        f3 pos = r.ori + r.dir * my_t;                  // ao/main.cpp:202
+                        float4 nn = P.normals[my_prim];                  // get_normal.h:26-37
+                        float* rec = recs + my_slot * AO_REC_WORDS;
+                        rec[0] = pos.x; rec[1] = pos.y; rec[2] = pos.z;
+                        rec[3] = nn.x; rec[4] = nn.y; rec[5] = nn.z;
+                        rec[6] = __uint_as_float(y * P.width + x);       // global pixel index p
+                        masks[my_slot] = 0u;
+                    }
+                    published += (uint32_t)__popcll(hfin);
+                    pending -= (uint32_t)__popcll(fin);
+                    just_done = false;
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                }
+                // 2. hand the published AO rays to idle lanes
+                const uint32_t avail = published * S;
+                const uint64_t idle = __ballot(mode == IDLE);
+                if (idle && issued < avail)
+                {
+                    uint32_t cand = issued + lane_rank(idle);
+                    issued = min(avail, issued + (uint32_t)__popcll(idle));
+                    if (mode == IDLE && cand < avail)
+                    {
+                        r = ao_ray(P, recs, cand, S, cur_slot, cur_s);
+                        best_t = FMAX; best_prim = 0; steps = 0; max_t = P.radius; any = true;
+                        st.reset(); st.push(P.root);
+                        mode = AORAY;
+                        rays_total += 1;
+                    }
+                }
+                // 3. done when nothing is in flight and nothing is left to hand out
+                if (__ballot(mode != IDLE) == 0ull && pending == 0u && issued >= avail) break;
+                // 4. one traversal step for every busy lane (same code for both ray kinds)
+                if (mode != IDLE)
+                {
+                    int rc = (P.fast_ok && __ballot(!finite_ray(r)) == 0ull)
+                        ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit)
+                        : ray_step<KIND, COUNT, false>(P.pairs, P.prims, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit);
+                    if (rc != 0)
+                    {
+                        if (mode == PRIMARY)
+                        {
+                            my_hit = best_t != FMAX;
+                            my_prim = my_hit ? best_prim : 0xFFFFFFFFu;
+                            my_t = my_hit ? best_t : -1.0f;
+                            just_done = true;
+                        }
+                        else if (rc > 0)
+                        {
+                            atomicOr(&masks[cur_slot], 1u << cur_s);
+                        }
+                        mode = IDLE;
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (valid)
+            {
+                float4 color = make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
+                uint32_t occ_mask = 0;
+                if (my_hit)
+                {
+                    occ_mask = masks[my_slot];
+                    float clr = 1.0f;
+                    const float step = 1.0f / (float)S;
+                    for (uint32_t s2 = 0; s2 < S; ++s2)
+                        if ((occ_mask >> s2) & 1u) clr = clr - step;     // ao/main.cpp:234-238
+                    color = make_float4(clr, clr, clr, 1.0f);
+                    hits_total += 1;
+                }
+                size_t o = (size_t)orow * P.width + x;
+                if (P.color) P.color[o] = color;
+                if (P.prim_id) P.prim_id[o] = my_prim;
+                if (P.t) P.t[o] = my_t;
+                if (P.occ) P.occ[o] = (uint8_t)occ_mask;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+
+    // ---- per-wave totals: one atomic set per wave --------------------------------------------
+    unsigned long long rr = rays_total, hh = hits_total, b = cnt.box, q = cnt.prim;
+    for (int off = 32; off > 0; off >>= 1)
+    {
+        rr += __shfl_down(rr, off);
+        hh += __shfl_down(hh, off);
+        if (COUNT) { b += __shfl_down(b, off); q += __shfl_down(q, off); }
+    }
+    if (__ballot(cnt.aborted) != 0ull && lane == 0) atomicOr(P.counters + 5, 1ull);
+    if (lane == 0)
+    {
+        atomicAdd(P.counters + 1, rr);
+        atomicAdd(P.counters + 2, hh);
+        atomicAdd(P.counters + 8, rr);
+        atomicAdd(P.counters + 9, hh);
+        if (COUNT)
+        {
+            atomicAdd(P.counters + 3, b);
+            atomicAdd(P.counters + 4, q);
+        }
+    }
+}
+
 // un-interleave gathered packed shards [count][bands_max*16][W] into the full image
 __global__ void unshard_kernel(uint32_t W, uint32_t H, uint32_t count, uint32_t rows_per_shard,
                                const float4* __restrict__ gcolor, const uint32_t* __restrict__ gpid,
@@ -223,49 +501,57 @@ __global__ void unshard_kernel(uint32_t W, uint32_t H, uint32_t count, uint32_t 
 
 // ------------------------------------------------------------------------------------------------
 
-// one table entry per compiled variant: kind x AO x COUNT x stack capacity
-struct variant
-{
-    void (*kernel)(render_params);
-};
-
-template <int KIND, int CAP, bool AO, bool COUNT>
-static constexpr variant make_variant() { return { dev::render_kernel<KIND, CAP, AO, COUNT> }; }
-
-template <int KIND, bool AO, bool COUNT>
-static variant pick_cap(int cap)
-{
-    return cap <= 32 ? make_variant<KIND, 32, AO, COUNT>() : make_variant<KIND, 64, AO, COUNT>();
-}
+using kernel_fn = void (*)(render_params);
 
 template <int KIND>
-static variant pick(bool ao, bool count, int cap)
+static kernel_fn pick(bool ao, bool count, int sched, int occ)
 {
-    if (ao) return count ? pick_cap<KIND, true, true>(cap) : pick_cap<KIND, true, false>(cap);
-    return count ? pick_cap<KIND, false, true>(cap) : pick_cap<KIND, false, false>(cap);
+    if (sched == dev::SCHED_UNIFIED)
+    {
+        if (occ == 8)
+        {
+            if (!ao) return count ? dev::render_unified_kernel<KIND, false, true, 8> : dev::render_unified_kernel<KIND, false, false, 8>;
+            return count ? dev::render_unified_kernel<KIND, true, true, 8> : dev::render_unified_kernel<KIND, true, false, 8>;
+        }
+        if (occ == 6)
+        {
+            if (!ao) return count ? dev::render_unified_kernel<KIND, false, true, 6> : dev::render_unified_kernel<KIND, false, false, 6>;
+            return count ? dev::render_unified_kernel<KIND, true, true, 6> : dev::render_unified_kernel<KIND, true, false, 6>;
+        }
+        if (!ao) return count ? dev::render_unified_kernel<KIND, false, true, 1> : dev::render_unified_kernel<KIND, false, false, 1>;
+        return count ? dev::render_unified_kernel<KIND, true, true, 1> : dev::render_unified_kernel<KIND, true, false, 1>;
+    }
+    if (!ao) return count ? dev::render_kernel<KIND, false, true, 0> : dev::render_kernel<KIND, false, false, 0>;
+    if (sched == dev::SCHED_ROUNDS)
+        return count ? dev::render_kernel<KIND, true, true, dev::SCHED_ROUNDS> : dev::render_kernel<KIND, true, false, dev::SCHED_ROUNDS>;
+    return count ? dev::render_kernel<KIND, true, true, dev::SCHED_REFILL> : dev::render_kernel<KIND, true, false, dev::SCHED_REFILL>;
 }
 
-static variant select_variant(int kind, bool ao, bool count, int cap)
+static kernel_fn select_variant(const launch_config& c)
 {
-    return kind == dev::KIND_TRI ? pick<dev::KIND_TRI>(ao, count, cap) : pick<dev::KIND_SPHERE>(ao, count, cap);
+    return c.kind == dev::KIND_TRI ? pick<dev::KIND_TRI>(c.ao, c.count, c.sched, c.occ)
+                                   : pick<dev::KIND_SPHERE>(c.ao, c.count, c.sched, c.occ);
 }
 
-hipError_t launch_render(const render_params& p, int kind, bool ao, bool count, int cap, int grid, hipStream_t s)
+size_t render_lds_bytes(const launch_config& c)
 {
-    variant v = select_variant(kind, ao, count, cap);
-    hipLaunchKernelGGL(v.kernel, dim3(grid), dim3(dev::BLOCK), 0, s, p);
+    size_t words = size_t(c.stack_cap) * c.block + (c.ao ? size_t(c.block / 64) * dev::AO_WAVE_WORDS : 0);
+    return words * 4;
+}
+
+hipError_t launch_render(const render_params& p, const launch_config& c, int grid, hipStream_t s)
+{
+    hipLaunchKernelGGL(select_variant(c), dim3(grid), dim3(c.block), render_lds_bytes(c), s, p);
     return hipGetLastError();
 }
 
-int render_blocks_per_cu(int kind, bool ao, bool count, int cap)
+int render_blocks_per_cu(const launch_config& c)
 {
-    variant v = select_variant(kind, ao, count, cap);
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, v.kernel, dev::BLOCK, 0) != hipSuccess) return 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, select_variant(c), c.block, render_lds_bytes(c)) != hipSuccess)
+        return 1;
     return n > 0 ? n : 1;
 }
-
-int render_block_threads() { return dev::BLOCK; }
 
 hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t count, uint32_t rows_per_shard, const void* gcolor,
                           const uint32_t* gpid, void* color, uint32_t* pid, hipStream_t s)

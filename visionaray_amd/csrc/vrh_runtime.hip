@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <new>
 #include <string>
@@ -53,6 +54,8 @@ struct vrh_ctx
     uint32_t last_slot = 0;
     vrh_frame_stats last{};
     bool have_frame = false;
+    // tuning options (0 = automatic), vrh_ctx_set_option
+    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0;
 };
 
 struct vrh_scene
@@ -62,6 +65,7 @@ struct vrh_scene
     float4* prims = nullptr;
     float4* normals = nullptr;
     uint32_t root = 0;
+    bool finite_bounds = true;   // every node bound finite (enables the hardware min/max slab path)
     vrh_scene_info info{};
 };
 
@@ -148,6 +152,25 @@ VRH_API int vrh_ctx_destroy(vrh_ctx* ctx)
     for (auto e : ctx->ev_stop) (void)hipEventDestroy(e);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
+    return VRH_OK;
+}
+
+VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
+{
+    VRH_CHECK(ctx, "vrh_ctx_set_option: null");
+    VRH_CHECK(value >= 0 && value <= 1024, "vrh_ctx_set_option: value out of range");
+    switch (option)
+    {
+    case VRH_OPT_BLOCK_THREADS:
+        VRH_CHECK(value % 64 == 0, "vrh_ctx_set_option: block threads must be a multiple of 64");
+        ctx->opt_block = int(value); break;
+    case VRH_OPT_STACK_CAP: ctx->opt_stack = int(value); break;
+    case VRH_OPT_AO_SCHEDULE: VRH_CHECK(value <= 3, "vrh_ctx_set_option: schedule is 1, 2 or 3"); ctx->opt_sched = int(value); break;
+    case VRH_OPT_BLOCKS_PER_CU: ctx->opt_bpc = int(value); break;
+    case VRH_OPT_WAVES_PER_SIMD: VRH_CHECK(value == 0 || value == 1 || value == 6 || value == 8, "vrh_ctx_set_option: waves per SIMD is 1, 6 or 8"); ctx->opt_occ = int(value); break;
+    case VRH_OPT_EXACT_MINMAX: ctx->opt_exact_minmax = value ? 1 : 0; break;
+    default: set_error("vrh_ctx_set_option: unknown option"); return VRH_ERR_INVALID;
+    }
     return VRH_OK;
 }
 
@@ -247,12 +270,18 @@ VRH_API int vrh_scene_upload(vrh_ctx* ctx, const void* nodes_v, uint32_t num_nod
         }
     }
 
+    bool finite_bounds = true;
+    for (uint32_t i = 0; i < num_nodes && finite_bounds; ++i)
+        for (int a = 0; a < 3; ++a)
+            finite_bounds = finite_bounds && std::isfinite(nodes[i].bmin[a]) && std::isfinite(nodes[i].bmax[a]);
+
     int rc = select_device(ctx);
     if (rc) return rc;
     auto* sc = new (std::nothrow) vrh_scene;
     if (!sc) { set_error("host allocation failed"); return VRH_ERR_OOM; }
     sc->ctx = ctx;
     sc->root = root;
+    sc->finite_bounds = finite_bounds;
     auto fail = [&](hipError_t e, const char* what) {
         set_error(std::string(what) + ": " + hipGetErrorString(e));
         vrh_scene_free(sc);
@@ -419,8 +448,23 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     if (sh.packed) VRH_CHECK(rt->height >= local_bands * 16u || local_bands == 0, "vrh_render: packed target too small");
     else VRH_CHECK(rt->height == cam->height, "vrh_render: render target height != camera height");
 
-    uint32_t cap = sc->info.max_depth <= 32 ? 32u : (sc->info.max_depth <= 64 ? 64u : 0u);
-    if (cap == 0) { set_error("vrh_render: BVH depth " + std::to_string(sc->info.max_depth) + " exceeds the 64-entry device stack"); return VRH_ERR_UNSUPPORTED; }
+    // a depth-first traversal holds at most `max_depth` stack entries (>= 1 for the root push)
+    const uint32_t need = std::max<uint32_t>(sc->info.max_depth, 1u);
+    uint32_t cap = ctx->opt_stack ? uint32_t(ctx->opt_stack) : ((need + 3u) & ~3u);
+    if (cap < need) { set_error("vrh_render: stack capacity option below the BVH depth"); return VRH_ERR_INVALID; }
+    launch_config lc{};
+    lc.kind = sc->info.prim_kind == VRH_PRIM_TRI64 ? 0 : 1;
+    lc.ao = ao;
+    lc.count = (k->flags & VRH_KERNEL_COUNT_TESTS) != 0;
+    lc.sched = ctx->opt_sched == 0 ? 2 : ctx->opt_sched - 1;   // auto = unified
+    lc.block = ctx->opt_block ? ctx->opt_block : 64;
+    lc.stack_cap = int(cap);
+    lc.occ = ctx->opt_occ ? ctx->opt_occ : 6;
+    if (render_lds_bytes(lc) > 160u * 1024u)
+    {
+        set_error("vrh_render: BVH depth " + std::to_string(sc->info.max_depth) + " needs more LDS stack than a CU has");
+        return VRH_ERR_UNSUPPORTED;
+    }
 
     int rc = select_device(ctx);
     if (rc) return rc;
@@ -428,6 +472,8 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     render_params p{};
     p.pairs = sc->pairs; p.prims = sc->prims; p.normals = sc->normals; p.root = sc->root;
     p.step_limit = sc->info.num_nodes + sc->info.num_indices + 16u;
+    p.stack_cap = cap;
+    p.fast_ok = (sc->finite_bounds && !ctx->opt_exact_minmax) ? 1u : 0u;
     std::memcpy(p.eye, cam->eye, 12); std::memcpy(p.cam_u, cam->cam_u, 12);
     std::memcpy(p.cam_v, cam->cam_v, 12); std::memcpy(p.cam_w, cam->cam_w, 12);
     p.width = cam->width; p.height = cam->height;
@@ -439,11 +485,9 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     p.color = rt->color; p.prim_id = rt->prim_id; p.t = rt->t; p.occ = rt->occ;
     p.counters = ctx->counters;
 
-    const int kind = sc->info.prim_kind == VRH_PRIM_TRI64 ? 0 : 1;
-    const bool count = (k->flags & VRH_KERNEL_COUNT_TESTS) != 0;
-    int per_cu = render_blocks_per_cu(kind, ao, count, int(cap));
-    int block = render_block_threads();
-    int waves_per_block = block / 64;
+    int per_cu = render_blocks_per_cu(lc);
+    if (ctx->opt_bpc) per_cu = std::min(per_cu, ctx->opt_bpc);
+    const int waves_per_block = lc.block / 64;
     int grid = std::max(1, std::min<int>(ctx->num_cus * per_cu, int((p.num_tiles + waves_per_block - 1) / waves_per_block)));
 
     const uint32_t slot = ctx->frames % VRH_MAX_TIMED_FRAMES;
@@ -457,7 +501,7 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     }
     VRH_HIP(hipMemsetAsync(ctx->counters, 0, 8 * sizeof(unsigned long long), ctx->stream));
     VRH_HIP(hipEventRecord(ctx->ev_start[slot], ctx->stream));
-    if (p.num_tiles > 0) VRH_HIP(launch_render(p, kind, ao, count, int(cap), grid, ctx->stream));
+    if (p.num_tiles > 0) VRH_HIP(launch_render(p, lc, grid, ctx->stream));
     VRH_HIP(hipEventRecord(ctx->ev_stop[slot], ctx->stream));
     ctx->last_slot = slot;
     ctx->frames++;
@@ -465,7 +509,7 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     ctx->last = vrh_frame_stats{};
     ctx->last.launches = p.num_tiles > 0 ? 1u : 0u;
     ctx->last.grid_blocks = uint32_t(grid);
-    ctx->last.block_threads = uint32_t(block);
+    ctx->last.block_threads = uint32_t(lc.block);
     ctx->last.stack_depth = cap;
     ctx->have_frame = true;
     return VRH_OK;
