@@ -1,0 +1,310 @@
+// include/visionaray_hip/hip_backend.h -- C++ drop-in of the MI355X traversal backend.
+//
+// Header-only layer over the C-ABI (include/vrh.h, libvrh.so) that presents Visionaray's scheduler
+// / render-target / BVH interface, so application code written for the reference's CUDA path
+//
+//     cuda_index_bvh<P>  device_bvh(host_bvh);                       // bvh.h:443-448
+//     gpu_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> rt;  rt.resize(w, h); // gpu_buffer_rt.h:19-51
+//     cuda_sched<ray> sched;                                          // cuda_sched.h:25-40
+//     sched.frame(kernel, make_sched_params(pixel_sampler::uniform_type{}, cam, rt));
+//
+// ports by renaming the three types to hip_index_bvh / hip_buffer_rt / hip_sched and passing one of
+// the built-in kernels (make_hip_closest_hit_kernel / make_hip_ao_kernel) instead of a lambda --
+// an arbitrary C++ callable cannot cross a C ABI (hard part 6).
+//
+// The templates only assume the reference's concepts, so they work with the reference's own types
+// (camera, sched_params, index_bvh_t, basic_triangle, basic_sphere) and with the minimal standalone
+// types of visionaray_hip/standalone.h:
+//   camera       : eye(), center(), up() (vec3 with .x .y .z), fovy(), aspect()       camera.h:46-95
+//   sched params : .cam (camera by value), .rt (render target by reference)             scheduler.h:52-75
+//   host BVH     : nodes(), indices(), primitives() contiguous containers; 32-B nodes,
+//                  64-B basic_triangle<3,float> or 48-B basic_sphere<float> primitives  bvh.h:317-403
+//
+// Errors: HIP / argument errors surface as visionaray::hip_error (the reference throws
+// visionaray::exception from host code, exception.h).
+#pragma once
+
+#include "../vrh.h"
+
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+namespace visionaray
+{
+
+struct hip_error : std::runtime_error
+{
+    int status;
+    hip_error(const char* what, int s)
+        : std::runtime_error(std::string(what) + " failed (status " + std::to_string(s) + "): " + vrh_last_error())
+        , status(s)
+    {
+    }
+};
+
+namespace hip_detail
+{
+inline void check(int rc, const char* what)
+{
+    if (rc != VRH_OK) throw hip_error(what, rc);
+}
+
+template <typename T, typename = void> struct is_sphere : std::false_type {};
+template <typename T> struct is_sphere<T, decltype((void)std::declval<T>().radius)> : std::true_type {};
+template <typename T, typename = void> struct is_triangle : std::false_type {};
+template <typename T> struct is_triangle<T, decltype((void)std::declval<T>().e2)> : std::true_type {};
+} // hip_detail
+
+//-------------------------------------------------------------------------------------------------
+// hip_context: one GPU (HIP device + stream).  Shared by the objects created on it.
+//
+
+class hip_context
+{
+public:
+    explicit hip_context(int device = 0, void* hip_stream = nullptr)
+    {
+        vrh_ctx* c = nullptr;
+        hip_detail::check(hip_stream ? vrh_ctx_create_on_stream(device, hip_stream, &c) : vrh_ctx_create(device, &c),
+                          "vrh_ctx_create");
+        ctx_.reset(c, [](vrh_ctx* p) { vrh_ctx_destroy(p); });
+    }
+    vrh_ctx* get() const { return ctx_.get(); }
+    void sync() const { hip_detail::check(vrh_sync(get()), "vrh_sync"); }
+    void set_option(uint32_t opt, int64_t value) { hip_detail::check(vrh_ctx_set_option(get(), opt, value), "vrh_ctx_set_option"); }
+    vrh_frame_stats last_frame_stats() const
+    {
+        vrh_frame_stats s{};
+        hip_detail::check(vrh_last_frame_stats(get(), &s), "vrh_last_frame_stats");
+        return s;
+    }
+
+    static std::shared_ptr<hip_context> const& default_context()
+    {
+        static std::shared_ptr<hip_context> d = std::make_shared<hip_context>(0);
+        return d;
+    }
+
+private:
+    std::shared_ptr<vrh_ctx> ctx_;
+};
+
+//-------------------------------------------------------------------------------------------------
+// hip_index_bvh<P>: device-resident copy of a host index BVH (the cuda_index_bvh copy-ctor)
+//
+
+template <typename Primitive>
+class hip_index_bvh
+{
+public:
+    using primitive_type = Primitive;
+    static_assert(hip_detail::is_triangle<Primitive>::value || hip_detail::is_sphere<Primitive>::value,
+                  "hip_index_bvh supports basic_triangle<3,float> and basic_sphere<float>");
+
+    // host_bvh: index_bvh<P> (nodes(), indices(), primitives()); face_normals: 16-B vec3 per
+    // primitive (normals_per_face_binding, get_normal.h:26-37), needed by the AO kernel
+    template <typename HostBVH>
+    explicit hip_index_bvh(HostBVH const& host_bvh, void const* face_normals = nullptr,
+                           std::shared_ptr<hip_context> ctx = hip_context::default_context())
+        : ctx_(std::move(ctx))
+    {
+        static_assert(sizeof(*host_bvh.nodes().data()) == 32, "bvh_node must be 32 bytes");
+        static_assert(sizeof(Primitive) == (hip_detail::is_sphere<Primitive>::value ? 48 : 64),
+                      "primitive layout must match basic_triangle<3,float> / basic_sphere<float>");
+        vrh_scene* s = nullptr;
+        hip_detail::check(vrh_scene_upload(ctx_->get(), host_bvh.nodes().data(), uint32_t(host_bvh.nodes().size()),
+                                           host_bvh.primitives().data(), uint32_t(host_bvh.primitives().size()),
+                                           hip_detail::is_sphere<Primitive>::value ? VRH_PRIM_SPHERE48 : VRH_PRIM_TRI64,
+                                           host_bvh.indices().data(), uint32_t(host_bvh.indices().size()),
+                                           face_normals, &s),
+                          "vrh_scene_upload");
+        scene_.reset(s, [](vrh_scene* p) { vrh_scene_free(p); });
+    }
+
+    vrh_scene* handle() const { return scene_.get(); }
+    hip_context& context() const { return *ctx_; }
+    vrh_scene_info info() const
+    {
+        vrh_scene_info i{};
+        hip_detail::check(vrh_scene_get_info(handle(), &i), "vrh_scene_get_info");
+        return i;
+    }
+
+private:
+    std::shared_ptr<hip_context> ctx_;
+    std::shared_ptr<vrh_scene> scene_;
+};
+
+//-------------------------------------------------------------------------------------------------
+// hip_buffer_rt<CF, DF>: gpu_buffer_rt replacement.  Colour is RGBA32F; the render target also
+// keeps the closest-hit prim_id / t and the AO occlusion mask (the integer outputs used for parity).
+//
+
+template <auto ColorFormat, auto DepthFormat>
+class hip_buffer_rt
+{
+public:
+    struct ref_type          // render_target_ref analogue: raw device pointers + size
+    {
+        float* color;        // RGBA32F
+        uint32_t* prim_id;
+        float* t;
+        uint8_t* occ;
+        size_t width, height;
+    };
+
+    explicit hip_buffer_rt(std::shared_ptr<hip_context> ctx = hip_context::default_context())
+        : ctx_(std::move(ctx))
+    {
+    }
+
+    void resize(size_t w, size_t h)
+    {
+        vrh_rt* r = nullptr;
+        hip_detail::check(vrh_rt_alloc(ctx_->get(), uint32_t(w), uint32_t(h), VRH_RT_ALL, &r), "vrh_rt_alloc");
+        rt_.reset(r, [](vrh_rt* p) { vrh_rt_free(p); });
+        width_ = w;
+        height_ = h;
+    }
+
+    size_t width() const { return width_; }
+    size_t height() const { return height_; }
+
+    template <typename Vec4>
+    void clear_color_buffer(Vec4 const& c)
+    {
+        float f[4] = { float(c.x), float(c.y), float(c.z), float(c.w) };
+        hip_detail::check(vrh_rt_clear(ctx_->get(), rt_.get(), f), "vrh_rt_clear");
+    }
+    void clear_color_buffer()
+    {
+        float f[4] = { 0, 0, 0, 0 };
+        hip_detail::check(vrh_rt_clear(ctx_->get(), rt_.get(), f), "vrh_rt_clear");
+    }
+
+    void begin_frame() {}
+    // end_frame() synchronises, so hip_sched::frame blocks like tiled_sched::frame
+    void end_frame() { ctx_->sync(); }
+
+    ref_type ref()
+    {
+        ref_type r{};
+        void* c = nullptr;
+        hip_detail::check(vrh_rt_get_buffers(rt_.get(), &c, &r.prim_id, &r.t, &r.occ), "vrh_rt_get_buffers");
+        r.color = static_cast<float*>(c);
+        r.width = width_;
+        r.height = height_;
+        return r;
+    }
+
+    // device -> host copies (display_color_buffer analogue; any pointer may be null)
+    void download(float* rgba, uint32_t* prim_id = nullptr, float* t = nullptr, uint8_t* occ = nullptr)
+    {
+        hip_detail::check(vrh_rt_download(ctx_->get(), rt_.get(), rgba, prim_id, t, occ), "vrh_rt_download");
+    }
+
+    vrh_rt* handle() const { return rt_.get(); }
+
+private:
+    std::shared_ptr<hip_context> ctx_;
+    std::shared_ptr<vrh_rt> rt_;
+    size_t width_ = 0, height_ = 0;
+};
+
+//-------------------------------------------------------------------------------------------------
+// Built-in kernels (what a C ABI can carry)
+//
+
+struct hip_builtin_kernel
+{
+    vrh_scene* scene;
+    vrh_kernel_desc desc;
+};
+
+template <typename BVH, typename Vec4>
+hip_builtin_kernel make_hip_closest_hit_kernel(BVH const& bvh, Vec4 const& bg)
+{
+    // closest_hit(ray, bvhs) (traverse_linear.inl:286-329); colour = hit ? 1 : bg
+    hip_builtin_kernel k{ bvh.handle(), {} };
+    k.desc.kind = VRH_KERNEL_PRIMARY;
+    k.desc.bg[0] = bg.x; k.desc.bg[1] = bg.y; k.desc.bg[2] = bg.z; k.desc.bg[3] = bg.w;
+    return k;
+}
+
+template <typename BVH, typename Vec4>
+hip_builtin_kernel make_hip_ao_kernel(BVH const& bvh, Vec4 const& bg, unsigned samples = 8, float radius = 0.1f,
+                                      float eps = 1e-3f)
+{
+    // ao/main.cpp:183-246 with the deterministic Appendix-A sampler
+    hip_builtin_kernel k{ bvh.handle(), {} };
+    k.desc.kind = VRH_KERNEL_AO;
+    k.desc.samples = samples;
+    k.desc.radius = radius;
+    k.desc.eps = eps;
+    k.desc.bg[0] = bg.x; k.desc.bg[1] = bg.y; k.desc.bg[2] = bg.z; k.desc.bg[3] = bg.w;
+    return k;
+}
+
+//-------------------------------------------------------------------------------------------------
+// hip_sched<R>: cuda_sched<R> replacement (persistent-thread HIP kernels, tile work stealing)
+//
+
+template <typename R>
+class hip_sched
+{
+public:
+    explicit hip_sched(std::shared_ptr<hip_context> ctx = hip_context::default_context())
+        : ctx_(std::move(ctx))
+    {
+    }
+
+    // frame(): rt.begin_frame() -> vrh_render -> rt.end_frame() (cuda_sched.inl:306-320; end_frame
+    // syncs).  shard: optional image-tile shard (multi-GPU).
+    template <typename K, typename SP>
+    void frame(K kernel, SP sparams, unsigned frame_num = 0, vrh_shard const* shard = nullptr)
+    {
+        static_assert(std::is_same<K, hip_builtin_kernel>::value,
+                      "hip_sched runs the built-in kernels (make_hip_closest_hit_kernel / make_hip_ao_kernel): "
+                      "an arbitrary callable cannot cross the C ABI");
+        auto const& cam = sparams.cam;
+        auto& rt = sparams.rt;
+        float eye[3] = { cam.eye().x, cam.eye().y, cam.eye().z };
+        float center[3] = { cam.center().x, cam.center().y, cam.center().z };
+        float up[3] = { cam.up().x, cam.up().y, cam.up().z };
+        vrh_camera c{};
+        hip_detail::check(vrh_make_camera(eye, center, up, cam.fovy(), cam.aspect(), uint32_t(rt.width()),
+                                          uint32_t(rt.height()), &c), "vrh_make_camera");
+        rt.begin_frame();
+        hip_detail::check(vrh_render(ctx_->get(), kernel.scene, rt.handle(), &c, &kernel.desc, shard, frame_num),
+                          "vrh_render");
+        rt.end_frame();
+    }
+
+    hip_context& context() const { return *ctx_; }
+
+private:
+    std::shared_ptr<hip_context> ctx_;
+};
+
+// host-side builder with the reference's result (build<index_bvh<P>>, build.inl:165-178):
+// fills nodes / indices of any container pair (resize(), data())
+template <typename Primitive, typename NodeVec, typename IndexVec>
+unsigned hip_build_index_bvh(Primitive const* prims, size_t n, NodeVec& nodes, IndexVec& indices)
+{
+    nodes.resize(2 * n);
+    indices.resize(n);
+    uint32_t nn = 0, depth = 0;
+    hip_detail::check(vrh_build_bvh(prims, uint32_t(n),
+                                    hip_detail::is_sphere<Primitive>::value ? VRH_PRIM_SPHERE48 : VRH_PRIM_TRI64,
+                                    nodes.data(), &nn, indices.data(), &depth),
+                      "vrh_build_bvh");
+    nodes.resize(nn);
+    return depth;
+}
+
+} // visionaray

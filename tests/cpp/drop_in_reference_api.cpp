@@ -1,0 +1,74 @@
+// tests/cpp/drop_in_reference_api.cpp -- drop-in check against the REAL reference API.
+//
+// Compiled (oracle/Makefile `dropin`, build container only) with the reference headers from
+// /root/reference/include and include/visionaray_hip/hip_backend.h: the reference's own camera,
+// basic_triangle<3,float>, build<index_bvh<P>> (build.inl:165-178), make_sched_params
+// (scheduler.h:164-242) and pixel formats drive hip_index_bvh / hip_buffer_rt / hip_sched exactly
+// where cuda_index_bvh / gpu_buffer_rt / cuda_sched stood (viewer.cpp:779-791, cuda_sched.h:25-40).
+// The binary (oracle/_ref/dropin_ref_api) prints the same JSON as examples/ao_hip.
+#include <visionaray/math/math.h>
+#include <visionaray/bvh.h>
+#include <visionaray/camera.h>
+#include <visionaray/pixel_format.h>
+#include <visionaray/scheduler.h>
+
+#include <visionaray_hip/hip_backend.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace visionaray;
+
+static uint64_t fnv1a(const void* p, size_t n)
+{
+    auto b = static_cast<const unsigned char*>(p);
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 0x100000001b3ull; }
+    return h;
+}
+
+int main(int argc, char** argv)
+{
+    unsigned grid = argc > 1 ? unsigned(atoi(argv[1])) : 200;
+    unsigned W = argc > 2 ? unsigned(atoi(argv[2])) : 320;
+    unsigned H = argc > 3 ? unsigned(atoi(argv[3])) : 180;
+    using tri_t = basic_triangle<3, float>;
+    std::vector<tri_t> tris(size_t(2) * grid * grid);
+    if (vrh_gen_heightfield(grid, tris.data()) != VRH_OK) return 2;
+
+    // the reference's own builder and camera
+    auto host_bvh = build<index_bvh<tri_t>>(tris.data(), tris.size());
+    std::vector<vec3> normals(tris.size());
+    for (size_t i = 0; i < tris.size(); ++i) normals[i] = normalize(cross(tris[i].e1, tris[i].e2));
+    camera cam;
+    cam.perspective(45.0f * constants::degrees_to_radians<float>(), W / static_cast<float>(H), 0.001f, 1000.0f);
+    cam.look_at(vec3(0.0f, 0.9f, 1.4f), vec3(0.0f), vec3(0.0f, 1.0f, 0.0f));
+
+    try
+    {
+        hip_index_bvh<tri_t> device_bvh(host_bvh, normals.data());       // was: cuda_index_bvh<tri_t>
+        hip_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> rt;                     // was: gpu_buffer_rt<...>
+        rt.resize(W, H);
+        hip_sched<basic_ray<float>> sched;                                // was: cuda_sched<ray>
+        auto sparams = make_sched_params(pixel_sampler::uniform_type{}, cam, rt);
+        sched.frame(make_hip_ao_kernel(device_bvh, vec4(0.1f, 0.2f, 0.3f, 1.0f)), sparams);
+
+        size_t n = size_t(W) * H;
+        std::vector<float> color(4 * n), t(n);
+        std::vector<uint32_t> pid(n);
+        std::vector<uint8_t> occ(n);
+        rt.download(color.data(), pid.data(), t.data(), occ.data());
+        printf("{\"grid\":%u,\"W\":%u,\"H\":%u,\"rays\":%llu,\"primid_hash\":\"%016llx\",\"t_hash\":\"%016llx\","
+               "\"occ_hash\":\"%016llx\",\"color_hash\":\"%016llx\"}\n", grid, W, H,
+               (unsigned long long)sched.context().last_frame_stats().rays,
+               (unsigned long long)fnv1a(pid.data(), n * 4), (unsigned long long)fnv1a(t.data(), n * 4),
+               (unsigned long long)fnv1a(occ.data(), n), (unsigned long long)fnv1a(color.data(), n * 16));
+    }
+    catch (std::exception const& e)
+    {
+        fprintf(stderr, "dropin: %s\n", e.what());
+        return 1;
+    }
+    return 0;
+}
