@@ -141,8 +141,10 @@ enum vrh_option {
                                     (auto: 3)                                                     */
     VRH_OPT_BLOCKS_PER_CU = 4,   /* resident blocks per CU for the persistent grid (auto: max)     */
     VRH_OPT_WAVES_PER_SIMD = 5,  /* register budget of the unified kernel: 1 (none), 6 or 8 (auto 6) */
-    VRH_OPT_EXACT_MINMAX = 6     /* 1 = always use the ternary min/max slab test (auto: hardware
+    VRH_OPT_EXACT_MINMAX = 6,    /* 1 = always use the ternary min/max slab test (auto: hardware
                                     min/max where provably identical, see vrh_device.h)           */
+    VRH_OPT_XCD_QUEUES = 7       /* tile queues: 1 = one per XCD with stealing, 2 = one global
+                                    queue (auto: 1)                                               */
 };
 VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value);
 

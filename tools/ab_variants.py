@@ -58,6 +58,7 @@ for rnd in range(rounds):
         ctx.set_option("blocks_per_cu", v.get("blocks_per_cu", 0))
         ctx.set_option("waves_per_simd", v.get("waves_per_simd", 0))
         ctx.set_option("exact_minmax", v.get("exact_minmax", 0))
+        ctx.set_option("xcd_queues", v.get("xcd_queues", 0))
         ctx.stats_reset()
         for _ in range(5):
             va.render(ctx, dev, rt, basis, kern)

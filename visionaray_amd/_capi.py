@@ -31,7 +31,7 @@ class vrh_kernel_desc(C.Structure):
 
 VRH_KERNEL_COUNT_TESTS = 1
 VRH_OPT_BLOCK_THREADS, VRH_OPT_STACK_CAP, VRH_OPT_AO_SCHEDULE, VRH_OPT_BLOCKS_PER_CU = 1, 2, 3, 4
-VRH_OPT_WAVES_PER_SIMD, VRH_OPT_EXACT_MINMAX = 5, 6
+VRH_OPT_WAVES_PER_SIMD, VRH_OPT_EXACT_MINMAX, VRH_OPT_XCD_QUEUES = 5, 6, 7
 VRH_MAX_TIMED_FRAMES = 1024
 
 

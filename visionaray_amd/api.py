@@ -157,7 +157,8 @@ class Context:
         """Launch tuning (vrh_ctx_set_option): block threads, stack cap, AO schedule, blocks/CU."""
         names = {"block_threads": capi.VRH_OPT_BLOCK_THREADS, "stack_cap": capi.VRH_OPT_STACK_CAP,
                  "ao_schedule": capi.VRH_OPT_AO_SCHEDULE, "blocks_per_cu": capi.VRH_OPT_BLOCKS_PER_CU,
-                 "waves_per_simd": capi.VRH_OPT_WAVES_PER_SIMD, "exact_minmax": capi.VRH_OPT_EXACT_MINMAX}
+                 "waves_per_simd": capi.VRH_OPT_WAVES_PER_SIMD, "exact_minmax": capi.VRH_OPT_EXACT_MINMAX,
+                 "xcd_queues": capi.VRH_OPT_XCD_QUEUES}
         capi.check("vrh_ctx_set_option", self.handle, names.get(option, option), int(value))
 
     def last_frame_stats(self):

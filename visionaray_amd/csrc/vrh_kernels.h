@@ -31,11 +31,17 @@ struct render_params
     float* t;
     uint8_t* occ;
 
-    // counters (u64): [0] tile dequeue (u32), [1] frame rays, [2] frame hits, [3] frame box tests,
-    // [4] frame primitive tests, [5] frame error flags (1 = traversal step guard tripped),
-    // [8] total rays, [9] total hits (since vrh_stats_reset)
+    // counters (u64): [1] frame rays, [2] frame hits, [3] frame box tests, [4] frame primitive
+    // tests, [5] frame error flags (1 = traversal step guard tripped), [8 + 8q] tile queue head q
+    // (q = 0..7, one 64-B line each) -- [0, COUNTERS_FRAME) reset per frame --
+    // [COUNTERS_TOTAL + 0/1] total rays / hits since vrh_stats_reset
     unsigned long long* counters;
+    uint32_t xcd_queues;      // 1: per-XCD tile queues with stealing; 0: one global queue
 };
+
+constexpr int COUNTERS_FRAME = 80;      // u64 words reset before every frame
+constexpr int COUNTERS_TOTAL = 80;      // u64 words [80], [81]: totals
+constexpr int COUNTERS_WORDS = 128;
 
 struct launch_config
 {

@@ -57,6 +57,46 @@ __device__ __forceinline__ ray_t primary_ray(const render_params& P, uint32_t x,
     return make_ray(mk3(P.eye[0], P.eye[1], P.eye[2]), dir);
 }
 
+// Tile work queues.  The frame's tiles are split into 8 contiguous ranges (horizontal image
+// strips); a wave first drains the range of the XCD it runs on (hardware register XCC_ID), so the
+// BVH nodes of a strip stay in that XCD's L2, then steals from the other ranges in turn.  Which XCD
+// a wave lands on only changes speed: every tile is handed out exactly once by one of the 8
+// atomic heads.  Called by the whole wave; returns the tile or NONE when all ranges are empty.
+struct tile_queue
+{
+    uint32_t q;       // range currently drained (wave-uniform)
+    uint32_t tried;   // ranges found empty so far
+};
+
+__device__ __forceinline__ uint32_t xcc_id()
+{
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & 7u;
+}
+
+__device__ __forceinline__ tile_queue queue_init(const render_params& P)
+{
+    return tile_queue{ P.xcd_queues ? xcc_id() : 0u, 0u };
+}
+
+__device__ __forceinline__ uint32_t next_tile(const render_params& P, tile_queue& tq, uint32_t lane)
+{
+    const uint32_t nq = P.xcd_queues ? 8u : 1u;
+    while (tq.tried < nq)
+    {
+        const uint32_t lo = (uint32_t)(((uint64_t)P.num_tiles * tq.q) / nq);
+        const uint32_t hi = (uint32_t)(((uint64_t)P.num_tiles * (tq.q + 1u)) / nq);
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(reinterpret_cast<uint32_t*>(P.counters + 8u + 8u * tq.q), 1u);
+        t = __shfl(t, 0);
+        if (lo + t < hi) return lo + t;
+        tq.q = (tq.q + 1u) % nq;
+        tq.tried += 1u;
+    }
+    return NONE;
+}
+
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask)
 {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
@@ -98,13 +138,12 @@ __global__ void render_kernel(render_params P)
     float* recs = reinterpret_cast<float*>(ao_area);          // 64 records x AO_REC_WORDS
     uint32_t* masks = ao_area + 64 * AO_REC_WORDS;             // occlusion mask per hit slot
     test_counts cnt = { 0u, 0u, false };
+    tile_queue tq = queue_init(P);
 
     for (;;)
     {
-        uint32_t tile = 0;
-        if (lane == 0) tile = atomicAdd(reinterpret_cast<uint32_t*>(P.counters), 1u);
-        tile = __shfl(tile, 0);
-        if (tile >= P.num_tiles) break;
+        const uint32_t tile = next_tile(P, tq, lane);
+        if (tile == NONE) break;
 
         uint32_t x, y, orow;
         bool valid = tile_pixel(P, tile, lane, x, y, orow);
@@ -223,8 +262,8 @@ __global__ void render_kernel(render_params P)
             unsigned long long nh = (unsigned long long)__popcll(hitmask);
             atomicAdd(P.counters + 1, (unsigned long long)nrays);
             atomicAdd(P.counters + 2, nh);
-            atomicAdd(P.counters + 8, (unsigned long long)nrays);
-            atomicAdd(P.counters + 9, nh);
+            atomicAdd(P.counters + COUNTERS_TOTAL, (unsigned long long)nrays);
+            atomicAdd(P.counters + COUNTERS_TOTAL + 1, nh);
         }
     }
     if (COUNT)
@@ -281,9 +320,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     if constexpr (!AO)
     {
         // ---- primary visibility: stream pixels, write each when its ray finishes ------------
-        uint32_t tile = 0;
-        if (lane == 0) tile = atomicAdd(reinterpret_cast<uint32_t*>(P.counters), 1u);
-        tile = __shfl(tile, 0);
+        tile_queue tq = queue_init(P);
+        uint32_t tile = next_tile(P, tq, lane);
         uint32_t handed = 0;                       // pixels of `tile` handed out (wave-uniform)
         uint32_t out_o = 0;
         for (;;)
@@ -291,13 +329,12 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             uint64_t idle = __ballot(mode == IDLE);
             if (idle)
             {
-                if (handed >= 64u && tile < P.num_tiles)
+                if (handed >= 64u && tile != NONE)
                 {
-                    if (lane == 0) tile = atomicAdd(reinterpret_cast<uint32_t*>(P.counters), 1u);
-                    tile = __shfl(tile, 0);
+                    tile = next_tile(P, tq, lane);
                     handed = 0;
                 }
-                if (tile < P.num_tiles)
+                if (tile != NONE)
                 {
                     uint32_t cand = handed + lane_rank(idle);
                     handed = min(64u, handed + (uint32_t)__popcll(idle));
@@ -318,7 +355,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             }
             if (__ballot(mode != IDLE) == 0ull)
             {
-                if (tile >= P.num_tiles) break;
+                if (tile == NONE) break;
                 continue;
             }
             if (mode != IDLE)
@@ -342,12 +379,11 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     else
     {
         const uint32_t S = P.samples;
+        tile_queue tq = queue_init(P);
         for (;;)
         {
-            uint32_t tile = 0;
-            if (lane == 0) tile = atomicAdd(reinterpret_cast<uint32_t*>(P.counters), 1u);
-            tile = __shfl(tile, 0);
-            if (tile >= P.num_tiles) break;
+            const uint32_t tile = next_tile(P, tq, lane);
+            if (tile == NONE) break;
 
             uint32_t x, y, orow;
             const bool valid = tile_pixel(P, tile, lane, x, y, orow);
@@ -470,8 +506,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     {
         atomicAdd(P.counters + 1, rr);
         atomicAdd(P.counters + 2, hh);
-        atomicAdd(P.counters + 8, rr);
-        atomicAdd(P.counters + 9, hh);
+        atomicAdd(P.counters + COUNTERS_TOTAL, rr);
+        atomicAdd(P.counters + COUNTERS_TOTAL + 1, hh);
         if (COUNT)
         {
             atomicAdd(P.counters + 3, b);

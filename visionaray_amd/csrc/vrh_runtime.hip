@@ -55,7 +55,7 @@ struct vrh_ctx
     vrh_frame_stats last{};
     bool have_frame = false;
     // tuning options (0 = automatic), vrh_ctx_set_option
-    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0;
+    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0;
 };
 
 struct vrh_scene
@@ -130,9 +130,9 @@ VRH_API int vrh_ctx_create_on_stream(int hip_device, void* hip_stream, vrh_ctx**
             if (e != hipSuccess) { set_error(hipGetErrorString(e)); rc = VRH_ERR_HIP; break; }
             ctx->own_stream = true;
         }
-        e = hipMalloc(&ctx->counters, 16 * sizeof(unsigned long long));
+        e = hipMalloc(&ctx->counters, COUNTERS_WORDS * sizeof(unsigned long long));
         if (e != hipSuccess) { set_error(hipGetErrorString(e)); rc = VRH_ERR_OOM; break; }
-        e = hipMemset(ctx->counters, 0, 16 * sizeof(unsigned long long));
+        e = hipMemset(ctx->counters, 0, COUNTERS_WORDS * sizeof(unsigned long long));
         if (e != hipSuccess) { set_error(hipGetErrorString(e)); rc = VRH_ERR_HIP; break; }
     } while (0);
     if (rc != VRH_OK) { vrh_ctx_destroy(ctx); return rc; }
@@ -169,6 +169,7 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
     case VRH_OPT_BLOCKS_PER_CU: ctx->opt_bpc = int(value); break;
     case VRH_OPT_WAVES_PER_SIMD: VRH_CHECK(value == 0 || value == 1 || value == 6 || value == 8, "vrh_ctx_set_option: waves per SIMD is 1, 6 or 8"); ctx->opt_occ = int(value); break;
     case VRH_OPT_EXACT_MINMAX: ctx->opt_exact_minmax = value ? 1 : 0; break;
+    case VRH_OPT_XCD_QUEUES: VRH_CHECK(value <= 2, "vrh_ctx_set_option: xcd queues is 1 (on) or 2 (off)"); ctx->opt_xcd_queues = int(value); break;
     default: set_error("vrh_ctx_set_option: unknown option"); return VRH_ERR_INVALID;
     }
     return VRH_OK;
@@ -484,6 +485,7 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     p.num_tiles = local_bands * 2u * p.tiles_x;
     p.color = rt->color; p.prim_id = rt->prim_id; p.t = rt->t; p.occ = rt->occ;
     p.counters = ctx->counters;
+    p.xcd_queues = ctx->opt_xcd_queues == 2 ? 0u : 1u;
 
     int per_cu = render_blocks_per_cu(lc);
     if (ctx->opt_bpc) per_cu = std::min(per_cu, ctx->opt_bpc);
@@ -499,7 +501,7 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
         ctx->ev_start.push_back(a);
         ctx->ev_stop.push_back(b);
     }
-    VRH_HIP(hipMemsetAsync(ctx->counters, 0, 8 * sizeof(unsigned long long), ctx->stream));
+    VRH_HIP(hipMemsetAsync(ctx->counters, 0, COUNTERS_FRAME * sizeof(unsigned long long), ctx->stream));
     VRH_HIP(hipEventRecord(ctx->ev_start[slot], ctx->stream));
     if (p.num_tiles > 0) VRH_HIP(launch_render(p, lc, grid, ctx->stream));
     VRH_HIP(hipEventRecord(ctx->ev_stop[slot], ctx->stream));
@@ -549,7 +551,7 @@ VRH_API int vrh_stats_reset(vrh_ctx* ctx)
     int rc = select_device(ctx);
     if (rc) return rc;
     VRH_HIP(hipStreamSynchronize(ctx->stream));
-    VRH_HIP(hipMemset(ctx->counters + 8, 0, 8 * sizeof(unsigned long long)));
+    VRH_HIP(hipMemset(ctx->counters + COUNTERS_TOTAL, 0, 16 * sizeof(unsigned long long)));
     ctx->frames = 0;
     return VRH_OK;
 }
@@ -574,7 +576,7 @@ VRH_API int vrh_get_accum_stats(vrh_ctx* ctx, vrh_accum_stats* out)
     }
     if (a.timed_frames == 0) a.kernel_ms_min = 0.0;
     unsigned long long c[2];
-    VRH_HIP(hipMemcpy(c, ctx->counters + 8, sizeof(c), hipMemcpyDeviceToHost));
+    VRH_HIP(hipMemcpy(c, ctx->counters + COUNTERS_TOTAL, sizeof(c), hipMemcpyDeviceToHost));
     a.rays = c[0];
     a.hits = c[1];
     *out = a;
