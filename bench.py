@@ -9,10 +9,11 @@ A "step" is one frame.  Inputs (BVH, primitives, normals) are resident in HBM be
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-N > 1: one process per GPU; the image is sharded by 16-row bands (band b -> rank b % N, SURVEY.md
-§8e), each rank renders its packed shard, and the framebuffer (RGBA32F + u32 prim ids) is gathered
-to rank 0 over RCCL (torch.distributed "nccl") and un-interleaved there (vrh_unshard) -- all inside
-the timed step.  Total work per frame is fixed, so scaling is strong.
+N > 1: one process per GPU; the image is sharded by 8-row bands (band b -> rank b % N, SURVEY.md
+§8e), each rank renders its packed shard, and the framebuffer is gathered to rank 0 over RCCL
+(torch.distributed "nccl"; prim ids + AO masks, 5 B/pixel) and un-interleaved there with the
+RGBA32F colour re-derived exactly (vrh_unshard) -- all inside the timed step.  Total work per frame
+is fixed, so scaling is strong.
 
 Rank 0 prints one JSON line (contract in the task statement) with the roofline of the traversal
 kernel (algorithmic bytes per SURVEY.md §8d from a counting pass, over the hipEvent kernel time of
@@ -45,6 +46,9 @@ def parse():
     ap.add_argument("--kernel", default=None, choices=["ao", "primary"], help="default: ao for triangles")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16, help="host cores for the CPU baseline")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, the measured path) | gloo (host-staged; single-GPU rehearsal only)")
+    ap.add_argument("--no-verify", action="store_true", help="skip the untimed N>1 check against a 1-GPU frame")
     return ap.parse_args()
 
 
@@ -86,9 +90,14 @@ def main():
     import visionaray_amd as va
     from visionaray_amd import _capi, scenes
 
-    torch.cuda.set_device(local)
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device(local % max(ndev, 1))   # ranks > devices only in single-GPU rehearsals
+    local = local % max(ndev, 1)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     kernel = args.kernel or ("ao" if not args.scene.startswith("sph") else "primary")
 
@@ -118,30 +127,47 @@ def main():
     kern_count = va.ao_kernel(dev, count_tests=True) if kernel == "ao" else va.closest_hit_kernel(dev, count_tests=True)
 
     # ---- framebuffers: full image on rank 0, packed shard per rank for N > 1 ------------------
-    rows_max = 16 * va.shard_bands(H, 0, world)
+    # Each rank writes its bands' prim ids and AO masks into ONE buffer [u32 prim ids | u8 masks]
+    # (5 B/pixel); one RCCL gather moves it to rank 0, which un-interleaves it and re-derives the
+    # RGBA32F colour exactly (vrh_unshard) -- the full framebuffer (RGBA32F + prim ids) on rank 0.
+    rows_max = _capi.VRH_BAND_ROWS * va.shard_bands(H, 0, world)
     if world == 1:
         rt = va.hip_buffer_rt(ctx, W, H)
         shard = None
     else:
-        loc_color = torch.empty((rows_max * W, 4), dtype=torch.float32, device="cuda")
-        loc_pid = torch.empty((rows_max * W,), dtype=torch.int32, device="cuda")
-        rt = va.hip_buffer_rt(ctx, W, rows_max, wrap=(loc_color.data_ptr(), loc_pid.data_ptr(), 0, 0))
+        n = rows_max * W
+        loc = torch.empty((5 * n,), dtype=torch.uint8, device="cuda")
+        base = loc.data_ptr()
+        rt = va.hip_buffer_rt(ctx, W, rows_max, wrap=(0, base, 0, base + 4 * n))
         shard = _capi.vrh_shard(rank, world, 1, 0)
         if rank == 0:
-            g_color = torch.empty((world, rows_max * W, 4), dtype=torch.float32, device="cuda")
-            g_pid = torch.empty((world, rows_max * W), dtype=torch.int32, device="cuda")
-            full = va.hip_buffer_rt(ctx, W, H, flags=_capi.VRH_RT_COLOR | _capi.VRH_RT_PRIM_ID)
+            gathered = torch.empty((world, 5 * n), dtype=torch.uint8, device="cuda")
+            gbase = gathered.data_ptr()
+            full = va.hip_buffer_rt(ctx, W, H, flags=_capi.VRH_RT_COLOR | _capi.VRH_RT_PRIM_ID | _capi.VRH_RT_OCC)
+
+    def gather():
+        if args.dist_backend == "nccl":
+            if rank == 0:
+                dist.gather(loc, gather_list=list(gathered.unbind(0)), dst=0)
+            else:
+                dist.gather(loc, dst=0)
+        else:   # gloo rehearsal: stage through host memory
+            torch.cuda.synchronize()
+            host = loc.cpu()
+            if rank == 0:
+                hg = torch.empty((world, host.numel()), dtype=torch.uint8)
+                dist.gather(host, gather_list=list(hg.unbind(0)), dst=0)
+                gathered.copy_(hg)
+            else:
+                dist.gather(host, dst=0)
 
     def step():
         va.render(ctx, dev, rt, basis, kern, shard)
         if world > 1:
+            gather()
             if rank == 0:
-                dist.gather(loc_color, gather_list=list(g_color.unbind(0)), dst=0)
-                dist.gather(loc_pid, gather_list=list(g_pid.unbind(0)), dst=0)
-                va.unshard(ctx, W, H, world, g_color.data_ptr(), g_pid.data_ptr(), full)
-            else:
-                dist.gather(loc_color, dst=0)
-                dist.gather(loc_pid, dst=0)
+                va.unshard(ctx, W, H, world, full, prim_id_ptr=gbase, occ_ptr=gbase + 4 * n,
+                           shard_stride_bytes=5 * n, kernel=kern)
 
     def barrier():
         if world > 1:
@@ -163,6 +189,16 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     acc = ctx.accum_stats()
+
+    # ---- N > 1: the gathered frame must equal a 1-GPU frame (untimed check on rank 0) ------------
+    verified = None
+    if world > 1 and not args.no_verify and rank == 0:
+        ref_rt = va.hip_buffer_rt(ctx, W, H)
+        va.render(ctx, dev, ref_rt, basis, kern, None)
+        a = full.download(t=False)
+        b = ref_rt.download(t=False)
+        verified = bool(all((a[k].view("u1") == b[k].view("u1")).all() for k in ("color", "prim_id", "occ")))
+    barrier()
 
     # ---- aggregate over ranks -------------------------------------------------------------------
     local_vals = torch.tensor([elapsed, float(acc["rays"]), acc["kernel_ms_total"], float(acc["timed_frames"]),
@@ -229,6 +265,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "host_build_s": round(build_s, 3),
+            "gathered_frame_matches_1gpu": verified,
         }
         print(json.dumps(line), flush=True)
 

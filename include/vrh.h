@@ -88,11 +88,13 @@ enum vrh_kernel_flags {
                                      feeds the algorithmic-bytes roofline)    */
 };
 
-/* Image-tile sharding: the image is cut into bands of 16 rows (tiled_sched
- * tile_height, tiled_sched.inl:24-25); shard g of N renders bands b with b % N == g.
+/* Image-tile sharding: the image is cut into bands of VRH_BAND_ROWS = 8 rows (one
+ * row of 8x8 wave tiles; finer than tiled_sched's 16-row tiles so 1080 rows split over 8 GPUs
+ * within 1 %); shard g of N renders bands b with b % N == g.
  * packed = 0: pixels land at their image position in a W x H target.
  * packed = 1: owned bands are stored back to back (band b at local band b / N) in a target of
- *             W x (16 * vrh_shard_bands(H, g, N)) rows -- the layout gathered over RCCL. */
+ *             W x (VRH_BAND_ROWS * vrh_shard_bands(H, g, N)) rows -- the layout gathered over RCCL. */
+#define VRH_BAND_ROWS 8
 typedef struct {
     uint32_t index, count, packed, reserved;
 } vrh_shard;
@@ -192,12 +194,17 @@ VRH_API int vrh_rt_download(vrh_ctx* ctx, vrh_rt* rt, void* color, uint32_t* pri
 VRH_API int vrh_rt_upload(vrh_ctx* ctx, vrh_rt* rt, const void* color, const uint32_t* prim_id, const float* t,
                           const uint8_t* occ);
 
-/* multi-GPU: number of 16-row bands shard g of N owns, and the root-side un-interleave of
- * N gathered packed shards (device pointers laid out [N][bands_max*16][W]) into a full target */
+/* multi-GPU: number of bands shard g of N owns, and the root-side un-interleave of N gathered
+ * packed shards into a full target.  Shard g's array starts at base + g * shard_stride_bytes
+ * (0 = dense [N][rows][W], rows = VRH_BAND_ROWS * vrh_shard_bands(H, 0, N)) and holds rows x W
+ * elements.  gathered_color may be NULL: the colour is then re-derived exactly from the gathered
+ * prim ids and AO masks with `kernel` (background on a miss, 1 - k/samples for k occluded samples,
+ * ao/main.cpp:234-238; samples <= 8), so 5 B/pixel cross xGMI instead of 20. */
 VRH_API uint32_t vrh_shard_bands(uint32_t height, uint32_t index, uint32_t count);
 VRH_API int vrh_unshard(vrh_ctx* ctx, uint32_t width, uint32_t height, uint32_t count,
                         const void* gathered_color, const uint32_t* gathered_prim_id,
-                        vrh_rt* dst);
+                        const uint8_t* gathered_occ, uint64_t shard_stride_bytes,
+                        const vrh_kernel_desc* kernel, vrh_rt* dst);
 
 /* host binned-SAH builder, tree-identical to build<index_bvh<P>> (build.inl:165-178).
  * nodes_out must hold 2*num_prims nodes (32 B each), indices_out num_prims entries. */

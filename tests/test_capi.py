@@ -103,7 +103,7 @@ def test_camera_basis_bits(golden):
 
 def test_shard_band_arithmetic():
     for H in (1, 15, 16, 17, 1080, 512):
-        bands = (H + 15) // 16
+        bands = (H + 7) // 8
         for N in (1, 2, 3, 4, 8):
             got = [va.shard_bands(H, g, N) for g in range(N)]
             assert sum(got) == bands

@@ -36,7 +36,7 @@ def render(ctx, name, W, H, ao=None, samples=8, shard=None, packed=False):
         rt = va.hip_buffer_rt(ctx, W, H)
         va.hip_sched(ctx).frame(kern, va.make_sched_params(va.pixel_sampler.uniform_type, cam, rt))
     else:
-        rows = 16 * va.shard_bands(H, shard[0], shard[1]) if packed else H
+        rows = va._capi.VRH_BAND_ROWS * va.shard_bands(H, shard[0], shard[1]) if packed else H
         rt = va.hip_buffer_rt(ctx, W, max(rows, 1))
         rt.clear_color_buffer((0, 0, 0, 0))
         va.hip_sched(ctx).frame(kern, va.make_sched_params(va.pixel_sampler.uniform_type, cam, rt, image_size=(W, H)),
@@ -88,28 +88,52 @@ def test_primary_kernel_matches_reference_hits(ctx, golden, oracle_mod):
 
 @pytest.mark.parametrize("count", [2, 3, 8])
 def test_packed_shards_gather_to_identical_image(ctx, count):
+    """N packed shards rendered on one GPU, 'gathered' and un-interleaved on the device: both the
+    full-colour gather and the compressed one (prim id + AO mask, colour re-derived) reproduce the
+    single-GPU frame bit for bit."""
     name, W, H = "hf200", 320, 180
     full, _ = render(ctx, name, W, H)
-    rows = 16 * va.shard_bands(H, 0, count)
-    gathered_c = np.zeros((count, rows * W, 4), np.float32)
-    gathered_p = np.full((count, rows * W), 0xFFFFFFFF, np.uint32)
+    rows = _capi.VRH_BAND_ROWS * va.shard_bands(H, 0, count)
+    n = rows * W
+    gathered_c = np.zeros((count, n, 4), np.float32)
+    gathered_p = np.full((count, n), 0xFFFFFFFF, np.uint32)
+    gathered_o = np.zeros((count, n), np.uint8)
     total_rays = 0
     for gi in range(count):
         out, st = render(ctx, name, W, H, shard=(gi, count), packed=True)
-        n = out["prim_id"].shape[0]
-        gathered_c[gi, :n] = out["color"]
-        gathered_p[gi, :n] = out["prim_id"]
+        m = out["prim_id"].shape[0]
+        gathered_c[gi, :m] = out["color"]
+        gathered_p[gi, :m] = out["prim_id"]
+        gathered_o[gi, :m] = out["occ"]
         total_rays += st["rays"]
-    # device un-interleave (vrh_unshard) on uploaded gathered buffers
-    dst = va.hip_buffer_rt(ctx, W, H, flags=_capi.VRH_RT_COLOR | _capi.VRH_RT_PRIM_ID)
-    src = va.hip_buffer_rt(ctx, W, count * rows, flags=_capi.VRH_RT_COLOR | _capi.VRH_RT_PRIM_ID)
-    src.upload(color=gathered_c.reshape(-1, 4), prim_id=gathered_p.reshape(-1))
-    cptr, pptr, _, _ = src.device_buffers()
-    va.unshard(ctx, W, H, count, cptr, pptr, dst)
-    got = dst.download(t=False, occ=False)
-    assert np.array_equal(got["prim_id"], full["prim_id"])
-    assert np.array_equal(got["color"].view(np.uint32), full["color"].view(np.uint32))
     assert total_rays == W * H + 8 * int((full["prim_id"] != 0xFFFFFFFF).sum())
+    flags = _capi.VRH_RT_COLOR | _capi.VRH_RT_PRIM_ID | _capi.VRH_RT_OCC
+    src = va.hip_buffer_rt(ctx, W, count * rows, flags=flags)
+    src.upload(color=gathered_c.reshape(-1, 4), prim_id=gathered_p.reshape(-1), occ=gathered_o.reshape(-1))
+    cptr, pptr, _, optr = src.device_buffers()
+    # (1) full colour gathered
+    dst = va.hip_buffer_rt(ctx, W, H, flags=flags)
+    va.unshard(ctx, W, H, count, dst, color_ptr=cptr, prim_id_ptr=pptr, occ_ptr=optr)
+    got = dst.download(t=False)
+    assert np.array_equal(got["prim_id"], full["prim_id"])
+    assert np.array_equal(got["occ"], full["occ"])
+    assert np.array_equal(got["color"].view(np.uint32), full["color"].view(np.uint32))
+    # (2) compressed: 5 B/pixel in ONE buffer per shard [prim ids | masks], colour re-derived
+    comb = np.zeros((count, 5 * n), np.uint8)
+    comb[:, :4 * n] = gathered_p.view(np.uint8).reshape(count, 4 * n)
+    comb[:, 4 * n:] = gathered_o
+    cbuf = va.hip_buffer_rt(ctx, W, count * rows * 5 // 4 + 1, flags=_capi.VRH_RT_PRIM_ID)
+    padded = np.zeros(cbuf.w * cbuf.h * 4, np.uint8)
+    padded[:comb.size] = comb.reshape(-1)
+    cbuf.upload(prim_id=padded.view(np.uint32))
+    _, base, _, _ = cbuf.device_buffers()
+    dst2 = va.hip_buffer_rt(ctx, W, H, flags=flags)
+    kern = va.ao_kernel(device_scene(ctx, name)[1])
+    va.unshard(ctx, W, H, count, dst2, prim_id_ptr=base, occ_ptr=base + 4 * n, shard_stride_bytes=5 * n, kernel=kern)
+    got2 = dst2.download(t=False)
+    assert np.array_equal(got2["prim_id"], full["prim_id"])
+    assert np.array_equal(got2["occ"], full["occ"])
+    assert np.array_equal(got2["color"].view(np.uint32), full["color"].view(np.uint32))
 
 
 def test_unpacked_shards_compose(ctx):
@@ -119,7 +143,7 @@ def test_unpacked_shards_compose(ctx):
     for gi in range(3):
         out, _ = render(ctx, name, W, H, shard=(gi, 3), packed=False)
         rows = np.arange(H)
-        mine = ((rows // 16) % 3) == gi
+        mine = ((rows // _capi.VRH_BAND_ROWS) % 3) == gi
         m = np.repeat(mine, W)
         acc[m] = out["prim_id"][m]
     assert np.array_equal(acc, full["prim_id"])

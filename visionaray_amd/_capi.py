@@ -30,6 +30,7 @@ class vrh_kernel_desc(C.Structure):
 
 
 VRH_KERNEL_COUNT_TESTS = 1
+VRH_BAND_ROWS = 8
 VRH_OPT_BLOCK_THREADS, VRH_OPT_STACK_CAP, VRH_OPT_AO_SCHEDULE, VRH_OPT_BLOCKS_PER_CU = 1, 2, 3, 4
 VRH_OPT_WAVES_PER_SIMD, VRH_OPT_EXACT_MINMAX, VRH_OPT_XCD_QUEUES = 5, 6, 7
 VRH_MAX_TIMED_FRAMES = 1024
@@ -90,7 +91,7 @@ SIGNATURES = {
     "vrh_rt_download": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "vrh_rt_upload": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "vrh_shard_bands": (C.c_uint32, [_u32, _u32, _u32]),
-    "vrh_unshard": (C.c_int, [_vp, _u32, _u32, _u32, _vp, _vp, _vp]),
+    "vrh_unshard": (C.c_int, [_vp, _u32, _u32, _u32, _vp, _vp, _vp, C.c_uint64, C.POINTER(vrh_kernel_desc), _vp]),
     "vrh_build_bvh": (C.c_int, [_vp, _u32, _u32, _vp, C.POINTER(_u32), _vp, C.POINTER(_u32)]),
     "vrh_gen_heightfield": (C.c_int, [_u32, _vp]),
     "vrh_gen_cornell": (C.c_int, [_vp]),

@@ -387,6 +387,10 @@ def shard_bands(height, index, count):
     return capi.lib().vrh_shard_bands(height, index, count)
 
 
-def unshard(ctx, width, height, count, gathered_color_ptr, gathered_prim_id_ptr, dst_rt):
-    capi.check("vrh_unshard", ctx.handle, width, height, count, C.c_void_p(gathered_color_ptr) if gathered_color_ptr else None,
-               C.c_void_p(gathered_prim_id_ptr) if gathered_prim_id_ptr else None, dst_rt.handle)
+def unshard(ctx, width, height, count, dst_rt, color_ptr=0, prim_id_ptr=0, occ_ptr=0, shard_stride_bytes=0,
+            kernel=None):
+    """vrh_unshard: gathered packed shards -> full render target (device pointers).  Without a
+    gathered colour the colour is re-derived from prim ids + AO masks with `kernel`."""
+    vp = lambda p: C.c_void_p(p) if p else None  # noqa: E731
+    capi.check("vrh_unshard", ctx.handle, width, height, count, vp(color_ptr), vp(prim_id_ptr), vp(occ_ptr),
+               int(shard_stride_bytes), C.byref(kernel.desc) if kernel is not None else None, dst_rt.handle)

@@ -1,6 +1,8 @@
 // visionaray_amd/csrc/vrh_kernels.h -- kernel launch interface (host side of vrh_kernels.hip).
 #pragma once
 
+#include "../../include/vrh.h"
+
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
@@ -57,7 +59,19 @@ struct launch_config
 size_t render_lds_bytes(const launch_config& c);
 hipError_t launch_render(const render_params& p, const launch_config& c, int grid, hipStream_t s);
 int render_blocks_per_cu(const launch_config& c);
-hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t count, uint32_t rows_per_shard, const void* gcolor,
-                          const uint32_t* gpid, void* color, uint32_t* pid, hipStream_t s);
+struct unshard_params
+{
+    uint32_t width, height, count, rows_per_shard;
+    const char* gcolor;          // gathered colour (float4), or null: re-derive from prim id + occ
+    const char* gpid;            // gathered prim ids (u32)
+    const char* gocc;            // gathered AO masks (u8)
+    uint64_t stride_color, stride_pid, stride_occ;   // bytes between consecutive shards
+    float4* color;
+    uint32_t* pid;
+    uint8_t* occ;
+    uint32_t ao, samples;        // colour re-derivation (kernel kind, AO samples)
+    float bg[4];
+};
+hipError_t launch_unshard(const unshard_params& u, hipStream_t s);
 
 } // namespace vrh

@@ -21,24 +21,22 @@ namespace vrh {
 namespace dev {
 
 constexpr int TILE = 8;             // 8x8 pixels per wave
-constexpr uint32_t BAND = 16;       // shard band height (tiled_sched tile_height)
+constexpr uint32_t BAND = VRH_BAND_ROWS;   // shard band height = one row of 8x8 tiles
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr int AO_REC_WORDS = 8;     // per hit slot: isect pos xyz, normal xyz, pixel index, lane
 // per-wave AO area in LDS: 64 hit records + 64 occlusion masks
 constexpr int AO_WAVE_WORDS = 64 * AO_REC_WORDS + 64;
 
-// tile index -> (x, y) of lane, plus the output row (packed shards)
+// tile index -> (x, y) of lane, plus the output row (packed shards).  A band is one row of tiles.
 __device__ __forceinline__ bool tile_pixel(const render_params& P, uint32_t tile, uint32_t lane,
                                            uint32_t& x, uint32_t& y, uint32_t& out_row)
 {
-    uint32_t per_band = 2u * P.tiles_x;           // two 8-row tile rows per 16-row band
-    uint32_t lb = tile / per_band;
-    uint32_t r = tile - lb * per_band;
-    uint32_t sub = r / P.tiles_x;
-    uint32_t tx = r - sub * P.tiles_x;
+    static_assert(BAND == TILE, "a shard band is one row of 8x8 tiles");
+    uint32_t lb = tile / P.tiles_x;               // local band
+    uint32_t tx = tile - lb * P.tiles_x;
     uint32_t band = lb * P.shard_count + P.shard_index;
     x = tx * TILE + (lane & 7u);
-    uint32_t in_band = sub * TILE + (lane >> 3);
+    uint32_t in_band = lane >> 3;
     y = band * BAND + in_band;
     out_row = P.packed ? lb * BAND + in_band : y;
     return x < P.width && y < P.height;
@@ -516,21 +514,37 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     }
 }
 
-// un-interleave gathered packed shards [count][bands_max*16][W] into the full image
-__global__ void unshard_kernel(uint32_t W, uint32_t H, uint32_t count, uint32_t rows_per_shard,
-                               const float4* __restrict__ gcolor, const uint32_t* __restrict__ gpid,
-                               float4* __restrict__ color, uint32_t* __restrict__ pid)
+// un-interleave gathered packed shards [count][rows_per_shard][W] into the full image; without a
+// gathered colour, re-derive it from prim id + AO mask exactly as the traversal kernel writes it
+__global__ void unshard_kernel(unshard_params u)
 {
     uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t y = blockIdx.y;
-    if (x >= W || y >= H) return;
+    if (x >= u.width || y >= u.height) return;
     uint32_t band = y / BAND;
-    uint32_t g = band % count;
-    uint32_t lrow = (band / count) * BAND + (y % BAND);
-    size_t src = ((size_t)g * rows_per_shard + lrow) * W + x;
-    size_t dst = (size_t)y * W + x;
-    if (color && gcolor) color[dst] = gcolor[src];
-    if (pid && gpid) pid[dst] = gpid[src];
+    uint32_t g = band % u.count;
+    uint32_t lrow = (band / u.count) * BAND + (y % BAND);
+    size_t src = (size_t)lrow * u.width + x;
+    size_t dst = (size_t)y * u.width + x;
+    uint32_t pid = u.gpid ? reinterpret_cast<const uint32_t*>(u.gpid + g * u.stride_pid)[src] : 0xFFFFFFFFu;
+    uint32_t occ = u.gocc ? (u.gocc + g * u.stride_occ)[src] : 0u;
+    if (u.pid && u.gpid) u.pid[dst] = pid;
+    if (u.occ && u.gocc) u.occ[dst] = (uint8_t)occ;
+    if (!u.color) return;
+    if (u.gcolor) { u.color[dst] = reinterpret_cast<const float4*>(u.gcolor + g * u.stride_color)[src]; return; }
+    float4 c = make_float4(u.bg[0], u.bg[1], u.bg[2], u.bg[3]);
+    if (pid != 0xFFFFFFFFu)
+    {
+        float clr = 1.0f;
+        if (u.ao)
+        {
+            const float step = 1.0f / (float)u.samples;
+            for (uint32_t s = 0; s < u.samples && s < 8u; ++s)
+                if ((occ >> s) & 1u) clr = clr - step;           // ao/main.cpp:234-238
+        }
+        c = make_float4(clr, clr, clr, 1.0f);
+    }
+    u.color[dst] = c;
 }
 
 } // namespace dev
@@ -589,12 +603,10 @@ int render_blocks_per_cu(const launch_config& c)
     return n > 0 ? n : 1;
 }
 
-hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t count, uint32_t rows_per_shard, const void* gcolor,
-                          const uint32_t* gpid, void* color, uint32_t* pid, hipStream_t s)
+hipError_t launch_unshard(const unshard_params& u, hipStream_t s)
 {
-    dim3 block(256), grid((W + 255) / 256, H);
-    hipLaunchKernelGGL(dev::unshard_kernel, grid, block, 0, s, W, H, count, rows_per_shard,
-                       (const float4*)gcolor, gpid, (float4*)color, pid);
+    dim3 block(256), grid((u.width + 255) / 256, u.height);
+    hipLaunchKernelGGL(dev::unshard_kernel, grid, block, 0, s, u);
     return hipGetLastError();
 }
 

@@ -88,7 +88,7 @@ int select_device(vrh_ctx* ctx)
     return VRH_OK;
 }
 
-uint32_t bands_of(uint32_t height) { return (height + 15u) / 16u; }
+uint32_t bands_of(uint32_t height) { return (height + VRH_BAND_ROWS - 1u) / VRH_BAND_ROWS; }
 
 } // namespace
 
@@ -446,7 +446,7 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     VRH_CHECK(sh.count >= 1 && sh.index < sh.count, "vrh_render: bad shard");
     const uint32_t local_bands = vrh_shard_bands(cam->height, sh.index, sh.count);
     VRH_CHECK(rt->width == cam->width, "vrh_render: render target width != camera width");
-    if (sh.packed) VRH_CHECK(rt->height >= local_bands * 16u || local_bands == 0, "vrh_render: packed target too small");
+    if (sh.packed) VRH_CHECK(rt->height >= local_bands * VRH_BAND_ROWS || local_bands == 0, "vrh_render: packed target too small");
     else VRH_CHECK(rt->height == cam->height, "vrh_render: render target height != camera height");
 
     // a depth-first traversal holds at most `max_depth` stack entries (>= 1 for the root push)
@@ -613,14 +613,34 @@ VRH_API int vrh_rt_upload(vrh_ctx* ctx, vrh_rt* rt, const void* color, const uin
 }
 
 VRH_API int vrh_unshard(vrh_ctx* ctx, uint32_t width, uint32_t height, uint32_t count, const void* gcolor,
-                        const uint32_t* gpid, vrh_rt* dst)
+                        const uint32_t* gpid, const uint8_t* gocc, uint64_t stride, const vrh_kernel_desc* k,
+                        vrh_rt* dst)
 {
     VRH_CHECK(ctx && dst && count >= 1, "vrh_unshard: bad argument");
     VRH_CHECK(dst->width == width && dst->height == height, "vrh_unshard: destination size mismatch");
+    VRH_CHECK(gcolor || !dst->color || (gpid && k), "vrh_unshard: colour needs either gathered colour or prim ids + kernel");
+    VRH_CHECK(gcolor || !dst->color || k->kind != VRH_KERNEL_AO || (gocc && k->samples <= 8),
+              "vrh_unshard: re-deriving AO colour needs the gathered masks and samples <= 8");
     int rc = select_device(ctx);
     if (rc) return rc;
-    uint32_t rows = 16u * vrh_shard_bands(height, 0, count);
-    VRH_HIP(launch_unshard(width, height, count, rows, gcolor, gpid, dst->color, dst->prim_id, ctx->stream));
+    unshard_params u{};
+    u.width = width; u.height = height; u.count = count;
+    u.rows_per_shard = VRH_BAND_ROWS * vrh_shard_bands(height, 0, count);
+    const uint64_t n = uint64_t(u.rows_per_shard) * width;
+    u.gcolor = static_cast<const char*>(gcolor);
+    u.gpid = reinterpret_cast<const char*>(gpid);
+    u.gocc = reinterpret_cast<const char*>(gocc);
+    u.stride_color = stride ? stride : 16 * n;
+    u.stride_pid = stride ? stride : 4 * n;
+    u.stride_occ = stride ? stride : n;
+    u.color = dst->color; u.pid = dst->prim_id; u.occ = dst->occ;
+    if (k)
+    {
+        u.ao = k->kind == VRH_KERNEL_AO ? 1u : 0u;
+        u.samples = k->samples ? k->samples : 1u;
+        std::memcpy(u.bg, k->bg, 16);
+    }
+    VRH_HIP(launch_unshard(u, ctx->stream));
     return VRH_OK;
 }
 
