@@ -109,6 +109,10 @@ typedef struct {
     uint32_t grid_blocks;
     uint32_t block_threads;
     uint32_t stack_depth;     /* per-lane traversal stack entries used by the variant         */
+    /* SIMD utilisation (only with VRH_KERNEL_COUNT_TESTS): wave-level iterations of the refilling
+     * loop, lanes busy summed over them, and wave-level iterations of the node-descent and leaf
+     * loops (lane-level: box_tests / 2 and prim_tests)                                          */
+    uint64_t wave_steps, busy_lane_steps, wave_box_iters, wave_prim_iters;
 } vrh_frame_stats;
 
 typedef struct {
@@ -138,9 +142,8 @@ enum vrh_option {
     VRH_OPT_BLOCK_THREADS = 1,   /* threads per block, multiple of 64 (auto: 64)                  */
     VRH_OPT_STACK_CAP = 2,       /* LDS stack entries per lane, >= BVH depth (auto: depth rounded
                                     up to a multiple of 4)                                        */
-    VRH_OPT_AO_SCHEDULE = 3,     /* 1 = AO rays in rounds of 64, 2 = AO rays refilled per lane after
-                                    the primary phase, 3 = primary + AO rays in one refilling loop
-                                    (auto: 3)                                                     */
+    VRH_OPT_AO_SCHEDULE = 3,     /* 3 = primary + AO rays in one refilling loop (the only schedule;
+                                    0 = auto = 3; the earlier 1/2 schedules were retired)        */
     VRH_OPT_BLOCKS_PER_CU = 4,   /* resident blocks per CU for the persistent grid (auto: max)     */
     VRH_OPT_WAVES_PER_SIMD = 5,  /* register budget of the unified kernel: 1 (none), 6 or 8 (auto 6) */
     VRH_OPT_EXACT_MINMAX = 6,    /* 1 = always use the ternary min/max slab test (auto: hardware

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_contains_gfx950_code_object():
     data = open(_capi.LIB_PATH, "rb").read()
-    assert b"gfx950" in data and b"render_kernel" in data
+    assert b"gfx950" in data and b"render_unified_kernel" in data and b"unshard_kernel" in data
 
 
 @pytest.mark.parametrize("name", ["cornell12", "hf64", "hf200", "sph5000", "hf1M", "sph1M"])

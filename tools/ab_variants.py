@@ -18,12 +18,11 @@ from visionaray_amd import scenes  # noqa: E402
 scene = sys.argv[1] if len(sys.argv) > 1 else "hf1M"
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 VARIANTS = json.loads(os.environ.get("VRH_AB", "null")) or [
-    {"name": "refill b64", "block_threads": 64, "ao_schedule": 2},
-    {"name": "rounds b64", "block_threads": 64, "ao_schedule": 1},
-    {"name": "refill b256", "block_threads": 256, "ao_schedule": 2},
-    {"name": "rounds b256 cap32", "block_threads": 256, "ao_schedule": 1, "stack_cap": 32},
-    {"name": "refill b64 cap32", "block_threads": 64, "ao_schedule": 2, "stack_cap": 32},
-    {"name": "refill b128", "block_threads": 128, "ao_schedule": 2},
+    {"name": "default"},
+    {"name": "exact minmax", "exact_minmax": 1},
+    {"name": "no xcd queues", "xcd_queues": 2},
+    {"name": "occ8", "waves_per_simd": 8},
+    {"name": "b256", "block_threads": 256},
 ]
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 log = open(os.path.join(ROOT, "gpurun_out", f"ab_{scene}.log"), "a", buffering=1)

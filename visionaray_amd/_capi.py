@@ -49,7 +49,9 @@ class vrh_shard(C.Structure):
 class vrh_frame_stats(C.Structure):
     _fields_ = [("kernel_ms", C.c_float), ("rays", C.c_uint64), ("hits", C.c_uint64), ("box_tests", C.c_uint64),
                 ("prim_tests", C.c_uint64), ("launches", C.c_uint32),
-                ("grid_blocks", C.c_uint32), ("block_threads", C.c_uint32), ("stack_depth", C.c_uint32)]
+                ("grid_blocks", C.c_uint32), ("block_threads", C.c_uint32), ("stack_depth", C.c_uint32),
+                ("wave_steps", C.c_uint64), ("busy_lane_steps", C.c_uint64), ("wave_box_iters", C.c_uint64),
+                ("wave_prim_iters", C.c_uint64)]
 
 
 class vrh_scene_info(C.Structure):

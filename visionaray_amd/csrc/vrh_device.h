@@ -4,9 +4,10 @@
 //
 //   pairs  : one 64-B record per inner node n, holding BOTH children's boxes and links, stored at
 //            index (n.first_child - 1) / 2 (the reference allocates children as adjacent pairs at
-//            odd node indices, build.inl:45-50, so this is dense).  4 x float4:
-//              q0 = c0.min.xyz, c0.max.x      q1 = c0.max.yz, c1.min.xy
-//              q2 = c1.min.z,   c1.max.xyz    q3 = link0, link1, 0, 0
+//            odd node indices, build.inl:45-50, so this is dense).  Slab-major and child-interleaved,
+//            so each float4 feeds two packed-fp32 (child 0, child 1) operand pairs:
+//              q0 = c0.min.x c1.min.x c0.min.y c1.min.y    q1 = c0.min.z c1.min.z c0.max.x c1.max.x
+//              q2 = c0.max.y c1.max.y c0.max.z c1.max.z    q3 = link0 link1 0 0
 //            link = pair index of an inner child, or LEAF_BIT | first_prim for a leaf child.
 //            One inner visit = one aligned 64-B read (the reference reads the same 64 B as two
 //            32-B bvh_nodes, intersect.inl:76-79).
@@ -24,6 +25,10 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#ifndef VRH_PACKED_SLABS
+#define VRH_PACKED_SLABS 0   // 1: slab distances with v_pk_add_f32 / v_pk_mul_f32
+#endif
+
 namespace vrh {
 namespace dev {
 
@@ -31,6 +36,7 @@ constexpr uint32_t LEAF_BIT = 0x80000000u;
 constexpr uint32_t END_BIT = 1u;
 constexpr int KIND_TRI = 0;
 constexpr int KIND_SPHERE = 1;
+constexpr float FMAX = 3.402823466e+38f;       // numeric_limits<float>::max(), hit_record ctor
 
 // math/detail/math.h:48-60
 __device__ __forceinline__ float tmin(float x, float y) { return x < y ? x : y; }
@@ -51,23 +57,12 @@ __device__ __forceinline__ f3 normalize(f3 v) { return v * (1.0f / __builtin_sqr
 
 struct ray_t { f3 ori, dir, inv; };
 
-struct hit_t
-{
-    float    t, u, v;
-    uint32_t prim_id, geom_id, list_index;
-    bool     hit;
-};
+typedef float f2 __attribute__((ext_vector_type(2)));   // packed fp32: v_pk_add_f32 / v_pk_mul_f32
 
-__device__ __forceinline__ hit_t miss_record()
-{
-    // hit_record ctor, math/intersect.h:95-103
-    hit_t h;
-    h.t = 3.402823466e+38f; h.u = 0.0f; h.v = 0.0f;
-    h.prim_id = 0; h.geom_id = 0; h.list_index = 0; h.hit = false;
-    return h;
-}
-
-// math/intersect.h:52-70 slab test + update_if.h:60-66,82-88 box is_closer.
+// Both children of a pair: math/intersect.h:52-70 slab test + update_if.h:60-66,82-88 box
+// is_closer.  The slab distances (b - o) * inv of child 0 and child 1 are computed two at a time
+// with packed fp32 adds and multiplies; each half is the same IEEE single operation as the scalar
+// expression, so nothing changes numerically.
 //
 // FAST = false is the reference formulation literally: min/max are the ternaries of
 // math/detail/math.h:48-60 (v_cmp + v_cndmask pairs).  FAST = true uses v_min/v_max/v_min3/v_max3.
@@ -77,24 +72,44 @@ __device__ __forceinline__ hit_t miss_record()
 // infinite (a zero direction component) or an input is not finite, so FAST is used only for rays
 // with finite origin and finite inv over scenes with finite node bounds (checked at upload).
 template <bool FAST>
-__device__ __forceinline__ bool box_closer(float lx, float ly, float lz, float hx, float hy, float hz,
-                                           const ray_t& r, float best_t, float max_t, float& tnear)
+__device__ __forceinline__ void box_pair(float4 q0, float4 q1, float4 q2, const ray_t& r, float best_t,
+                                         float max_t, bool& b0, bool& b1, float& tn0, float& tn1)
 {
-    float t1x = (lx - r.ori.x) * r.inv.x, t1y = (ly - r.ori.y) * r.inv.y, t1z = (lz - r.ori.z) * r.inv.z;
-    float t2x = (hx - r.ori.x) * r.inv.x, t2y = (hy - r.ori.y) * r.inv.y, t2z = (hz - r.ori.z) * r.inv.z;
-    float tn, tf;
+#if VRH_PACKED_SLABS
+    const f2 ox = { r.ori.x, r.ori.x }, oy = { r.ori.y, r.ori.y }, oz = { r.ori.z, r.ori.z };
+    const f2 ix = { r.inv.x, r.inv.x }, iy = { r.inv.y, r.inv.y }, iz = { r.inv.z, r.inv.z };
+    const f2 t1x = (f2{ q0.x, q0.y } - ox) * ix;
+    const f2 t1y = (f2{ q0.z, q0.w } - oy) * iy;
+    const f2 t1z = (f2{ q1.x, q1.y } - oz) * iz;
+    const f2 t2x = (f2{ q1.z, q1.w } - ox) * ix;
+    const f2 t2y = (f2{ q2.x, q2.y } - oy) * iy;
+    const f2 t2z = (f2{ q2.z, q2.w } - oz) * iz;
+#else
+    f2 t1x, t1y, t1z, t2x, t2y, t2z;
+    t1x.x = (q0.x - r.ori.x) * r.inv.x; t1x.y = (q0.y - r.ori.x) * r.inv.x;
+    t1y.x = (q0.z - r.ori.y) * r.inv.y; t1y.y = (q0.w - r.ori.y) * r.inv.y;
+    t1z.x = (q1.x - r.ori.z) * r.inv.z; t1z.y = (q1.y - r.ori.z) * r.inv.z;
+    t2x.x = (q1.z - r.ori.x) * r.inv.x; t2x.y = (q1.w - r.ori.x) * r.inv.x;
+    t2y.x = (q2.x - r.ori.y) * r.inv.y; t2y.y = (q2.y - r.ori.y) * r.inv.y;
+    t2z.x = (q2.z - r.ori.z) * r.inv.z; t2z.y = (q2.w - r.ori.z) * r.inv.z;
+#endif
+    float tf0, tf1;
     if constexpr (FAST)
     {
-        tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1x, t2x), __builtin_fminf(t1y, t2y)), __builtin_fminf(t1z, t2z));
-        tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t1x, t2x), __builtin_fmaxf(t1y, t2y)), __builtin_fmaxf(t1z, t2z));
+        tn0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1x.x, t2x.x), __builtin_fminf(t1y.x, t2y.x)), __builtin_fminf(t1z.x, t2z.x));
+        tf0 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t1x.x, t2x.x), __builtin_fmaxf(t1y.x, t2y.x)), __builtin_fmaxf(t1z.x, t2z.x));
+        tn1 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1x.y, t2x.y), __builtin_fminf(t1y.y, t2y.y)), __builtin_fminf(t1z.y, t2z.y));
+        tf1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t1x.y, t2x.y), __builtin_fmaxf(t1y.y, t2y.y)), __builtin_fmaxf(t1z.y, t2z.y));
     }
     else
     {
-        tn = tmax(tmin(t1x, t2x), tmax(tmin(t1y, t2y), tmin(t1z, t2z)));
-        tf = tmin(tmax(t1x, t2x), tmin(tmax(t1y, t2y), tmax(t1z, t2z)));
+        tn0 = tmax(tmin(t1x.x, t2x.x), tmax(tmin(t1y.x, t2y.x), tmin(t1z.x, t2z.x)));
+        tf0 = tmin(tmax(t1x.x, t2x.x), tmin(tmax(t1y.x, t2y.x), tmax(t1z.x, t2z.x)));
+        tn1 = tmax(tmin(t1x.y, t2x.y), tmax(tmin(t1y.y, t2y.y), tmin(t1z.y, t2z.y)));
+        tf1 = tmin(tmax(t1x.y, t2x.y), tmin(tmax(t1y.y, t2y.y), tmax(t1z.y, t2z.y)));
     }
-    tnear = tn;
-    return (tf >= tn) & (tn < best_t) & (tf >= 0.0f) & (tn < max_t);
+    b0 = (tf0 >= tn0) & (tn0 < best_t) & (tf0 >= 0.0f) & (tn0 < max_t);
+    b1 = (tf1 >= tn1) & (tn1 < best_t) & (tf1 >= 0.0f) & (tn1 < max_t);
 }
 
 __device__ __forceinline__ bool finite_ray(const ray_t& r)
@@ -103,29 +118,11 @@ __device__ __forceinline__ bool finite_ray(const ray_t& r)
         && __builtin_isfinite(r.ori.x) && __builtin_isfinite(r.ori.y) && __builtin_isfinite(r.ori.z);
 }
 
-// math/intersect.h:122-179 ray/triangle, Moller-Trumbore (two-sided, closed edges)
-__device__ __forceinline__ bool isect_tri(const ray_t& r, float4 a, float4 b, float4 c, float& t, float& u, float& v)
-{
-    f3 v1 = mk3(a.x, a.y, a.z), e1 = mk3(a.w, b.x, b.y), e2 = mk3(b.z, b.w, c.x);
-    f3 s1 = cross(r.dir, e2);
-    float div = dot(s1, e1);
-    if (!(div != 0.0f)) return false;
-    float inv_div = 1.0f / div;
-    f3 d = r.ori - v1;
-    float b1 = dot(d, s1) * inv_div;
-    if (!(b1 >= 0.0f && b1 <= 1.0f)) return false;
-    f3 s2 = cross(d, e1);
-    float b2 = dot(r.dir, s2) * inv_div;
-    if (!(b2 >= 0.0f && b1 + b2 <= 1.0f)) return false;
-    t = dot(e2, s2) * inv_div;
-    u = b1; v = b2;
-    return true;
-}
-
-// The same test without early outs (math/intersect.h:122-179): every quantity is computed exactly
-// as the reference computes it; the reference's early returns only skip work whose result it then
-// discards, so the accepted hits and their t are identical.  Avoids divergent branches per lane.
-__device__ __forceinline__ bool isect_tri_nb(const ray_t& r, float4 a, float4 b, float4 c, float& t)
+// math/intersect.h:122-179 ray/triangle (Moller-Trumbore, two-sided, closed edges) without the
+// early outs: every quantity is computed exactly as the reference computes it; the reference's
+// early returns only skip work whose result it then discards, so the accepted hits and their t are
+// identical, and the lanes of a wave do not diverge.
+__device__ __forceinline__ bool isect_tri(const ray_t& r, float4 a, float4 b, float4 c, float& t)
 {
     f3 v1 = mk3(a.x, a.y, a.z), e1 = mk3(a.w, b.x, b.y), e2 = mk3(b.z, b.w, c.x);
     f3 s1 = cross(r.dir, e2);
@@ -156,10 +153,6 @@ __device__ __forceinline__ bool isect_sphere(const ray_t& r, float4 a, float& t)
     return valid;
 }
 
-constexpr int SCHED_ROUNDS = 0;    // AO rays handed out 64 at a time
-constexpr int SCHED_REFILL = 1;    // AO rays refilled per lane; primary rays traced first
-constexpr int SCHED_UNIFIED = 2;   // primary and AO rays share one refilling loop
-
 // Per-lane LDS stack, column-major ([entry][lane]) so a wave's pushes/pops hit 64 distinct banks.
 // The top is kept as a word offset advanced by the block stride (no multiply per push/pop).
 struct lds_stack
@@ -174,153 +167,42 @@ struct lds_stack
     __device__ __forceinline__ bool empty() const { return top == base; }
 };
 
-// detail/bvh/intersect.inl:25-134: depth-first traversal, near child first (ties -> child 1),
-// far child pushed, leaf primitives tested in index order, AnyHit exits at the first accepted hit
-// (exit_traversal.h:49-56).  Box culling uses the running closest t exactly like the reference;
-// popped nodes are NOT re-culled (the reference does not), which keeps tie resolution identical.
-struct test_counts { uint32_t box, prim; bool aborted; };
-
-// step_limit bounds the node visits + primitive tests of one ray (a correct traversal never needs
-// more than nodes + primitives); a corrupt BVH therefore ends the ray with `aborted` set instead
-// of spinning the wave forever.
-template <int KIND, bool ANY, bool COUNT, class Stack>
-__device__ __forceinline__ hit_t trace(const float4* __restrict__ pairs, const float4* __restrict__ prims,
-                                       uint32_t root, const ray_t& r, float max_t, Stack& st, test_counts& cnt,
-                                       uint32_t step_limit)
+// Test counts of the counting variant (VRH_KERNEL_COUNT_TESTS).  box / prim are per lane; the
+// step fields measure SIMD utilisation: `it_box` / `it_prim` are this lane's descent / leaf loop
+// iterations in the current ray_step call, folded by count_wave() into the wave-level totals
+// (w_steps outer iterations, w_box / w_prim = iterations the wave executed, i.e. the lane maximum).
+struct test_counts
 {
-    hit_t res = miss_record();
-    uint32_t steps = 0;
-    st.reset();
-    st.push(root);
-    while (!st.empty())
-    {
-        uint32_t link = st.pop();
-        while (!(link & LEAF_BIT))
-        {
-            if (++steps > step_limit) { cnt.aborted = true; return res; }
-            const float4* p = pairs + 4u * link;
-            float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
-            float tn0, tn1;
-            bool b0 = box_closer<false>(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, r, res.t, max_t, tn0);
-            bool b1 = box_closer<false>(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, r, res.t, max_t, tn1);
-            uint32_t l0 = __float_as_uint(q3.x), l1 = __float_as_uint(q3.y);
-            if (COUNT) cnt.box += 2;
-            if (b0 && b1)
-            {
-                bool near0 = tn0 < tn1;          // intersect.inl:86
-                st.push(near0 ? l1 : l0);
-                link = near0 ? l0 : l1;
-            }
-            else if (b0) link = l0;
-            else if (b1) link = l1;
-            else goto next;
-        }
-        {
-            uint32_t i = link & ~LEAF_BIT;
-            for (;;)
-            {
-                uint32_t flags;
-                float t, u = 0.0f, v = 0.0f;
-                bool h;
-                uint32_t pid, gid;
-                if constexpr (KIND == KIND_TRI)
-                {
-                    const float4* q = prims + 3u * i;
-                    float4 a = q[0], b = q[1], c = q[2];
-                    h = isect_tri(r, a, b, c, t, u, v);
-                    pid = __float_as_uint(c.y); gid = __float_as_uint(c.z); flags = __float_as_uint(c.w);
-                }
-                else
-                {
-                    const float4* q = prims + 2u * i;
-                    float4 a = q[0], b = q[1];
-                    h = isect_sphere(r, a, t);
-                    pid = __float_as_uint(b.x); gid = __float_as_uint(b.y); flags = __float_as_uint(b.z);
-                }
-                if (COUNT) cnt.prim += 1;
-                // update_if.h:48-56 is_closer, update_if.h:27-37 + hit_record.h:54-64 update
-                if (h && t >= 0.0f && t < res.t && t < max_t)
-                {
-                    res.hit = true; res.t = t; res.u = u; res.v = v;
-                    res.prim_id = pid; res.geom_id = gid; res.list_index = i;
-                    if (ANY) return res;
-                }
-                if (flags & END_BIT) break;
-                ++i;
-                if (++steps > step_limit) { cnt.aborted = true; return res; }
-            }
-        }
-    next:;
-    }
-    return res;
+    uint32_t box, prim;
+    bool aborted;
+    uint32_t it_box, it_prim;
+    uint64_t w_steps, w_busy, w_box, w_prim;
+};
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v)
+{
+    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
+    return v;
 }
 
-// One outer iteration of the any-hit loop (intersect.inl:67-130 with AnyHit): pop a node, descend
-// to a leaf, test its primitives.  The stack holds the rest of the ray's state, so a wave can
-// interleave rays (REFILL schedule).  Returns 1 = occluded (first accepted hit, exit_traversal.h:
-// 49-56), -1 = missed (stack empty), 0 = continue.  Before the first hit result.t is max(), so the
-// set of visited nodes -- and the occlusion bit -- does not depend on how iterations interleave.
-template <int KIND, bool COUNT>
-__device__ __forceinline__ int anyhit_step(const float4* __restrict__ pairs, const float4* __restrict__ prims,
-                                           const ray_t& r, float max_t, lds_stack& st, test_counts& cnt,
-                                           uint32_t& steps, uint32_t step_limit)
+// called by every lane of the wave after a step of the busy lanes
+__device__ __forceinline__ void count_wave(test_counts& c, bool busy)
 {
-    const float best_t = 3.402823466e+38f;
-    if (st.empty()) return -1;
-    uint32_t link = st.pop();
-    while (!(link & LEAF_BIT))
-    {
-        if (++steps > step_limit) { cnt.aborted = true; return -1; }
-        const float4* p = pairs + 4u * link;
-        float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
-        float tn0, tn1;
-        bool b0 = box_closer<false>(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, r, best_t, max_t, tn0);
-        bool b1 = box_closer<false>(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, r, best_t, max_t, tn1);
-        uint32_t l0 = __float_as_uint(q3.x), l1 = __float_as_uint(q3.y);
-        if (COUNT) cnt.box += 2;
-        if (b0 && b1)
-        {
-            bool near0 = tn0 < tn1;
-            st.push(near0 ? l1 : l0);
-            link = near0 ? l0 : l1;
-        }
-        else if (b0) link = l0;
-        else if (b1) link = l1;
-        else return st.empty() ? -1 : 0;
-    }
-    uint32_t i = link & ~LEAF_BIT;
-    for (;;)
-    {
-        float t, u, v;
-        bool h;
-        uint32_t flags;
-        if constexpr (KIND == KIND_TRI)
-        {
-            const float4* q = prims + 3u * i;
-            float4 a = q[0], b = q[1], c = q[2];
-            h = isect_tri(r, a, b, c, t, u, v);
-            flags = __float_as_uint(c.w);
-        }
-        else
-        {
-            const float4* q = prims + 2u * i;
-            float4 a = q[0], b = q[1];
-            h = isect_sphere(r, a, t);
-            flags = __float_as_uint(b.z);
-        }
-        if (COUNT) cnt.prim += 1;
-        if (h && t >= 0.0f && t < best_t && t < max_t) return 1;
-        if (flags & END_BIT) break;
-        ++i;
-        if (++steps > step_limit) { cnt.aborted = true; return -1; }
-    }
-    return st.empty() ? -1 : 0;
+    c.w_steps += 1;
+    c.w_busy += (uint64_t)__popcll(__ballot(busy));
+    c.w_box += wave_max(c.it_box);
+    c.w_prim += wave_max(c.it_prim);
+    c.it_box = 0;
+    c.it_prim = 0;
 }
 
-// One outer iteration of the reference loop (intersect.inl:67-130) for EITHER traversal type:
-// closest hit (any = false: boxes culled against the running best_t, all primitives of reached
-// leaves tested, best_t / best_prim updated by is_closer) or any hit (any = true: best_t stays
-// max() until the first accepted hit, which ends the ray).  Lanes of one wave may be in different
+// One outer iteration of the reference loop (detail/bvh/intersect.inl:66-130) for EITHER traversal
+// type: closest hit (any = false: boxes culled against the running best_t, all primitives of
+// reached leaves tested, best_t / best_prim updated by is_closer) or any hit (any = true: best_t
+// stays max() until the first accepted hit, which ends the ray, exit_traversal.h:49-56).  Depth
+// first, near child first (ties -> child 1, intersect.inl:86), far child pushed, leaf primitives in
+// index order; popped nodes are NOT re-culled (the reference does not), which keeps closest-hit
+// tie resolution identical.  Lanes of one wave may be in different
 // modes and still run the same instruction stream.  Returns 1 = any-hit found, -1 = ray finished
 // (stack empty), 0 = continue.
 template <int KIND, bool COUNT, bool FAST>
@@ -337,12 +219,12 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
     while (!(link & LEAF_BIT))
     {
         const float4* p = pairs + 4u * link;
-        float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+        const float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+        bool b0, b1;
         float tn0, tn1;
-        const bool b0 = box_closer<FAST>(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, r, best_t, max_t, tn0);
-        const bool b1 = box_closer<FAST>(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, r, best_t, max_t, tn1);
+        box_pair<FAST>(q0, q1, q2, r, best_t, max_t, b0, b1, tn0, tn1);
         const uint32_t l0 = __float_as_uint(q3.x), l1 = __float_as_uint(q3.y);
-        if (COUNT) cnt.box += 2;
+        if (COUNT) { cnt.box += 2; cnt.it_box += 1; }
         // intersect.inl:84-101 without branches: both hit -> push the far child, descend the near
         // one (near = tn0 < tn1 ? 0 : 1); one hit -> descend it; none -> pop
         const bool both = b0 & b1;
@@ -361,7 +243,7 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
         {
             const float4* q = prims + 3u * i;
             float4 a = q[0], b = q[1], c = q[2];
-            h = isect_tri_nb(r, a, b, c, t);
+            h = isect_tri(r, a, b, c, t);
             pid = __float_as_uint(c.y);
             flags = __float_as_uint(c.w);
         }
@@ -373,7 +255,7 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
             pid = __float_as_uint(b.x);
             flags = __float_as_uint(b.z);
         }
-        if (COUNT) cnt.prim += 1;
+        if (COUNT) { cnt.prim += 1; cnt.it_prim += 1; }
         if (h & (t >= 0.0f) & (t < best_t) & (t < max_t))      // update_if.h:48-56, 73-79
         {
             best_t = t;

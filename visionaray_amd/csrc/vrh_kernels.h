@@ -34,7 +34,9 @@ struct render_params
     uint8_t* occ;
 
     // counters (u64): [1] frame rays, [2] frame hits, [3] frame box tests, [4] frame primitive
-    // tests, [5] frame error flags (1 = traversal step guard tripped), [8 + 8q] tile queue head q
+    // tests, [5] frame error flags (1 = traversal step guard tripped), [6] [7] [9] [10] SIMD
+    // utilisation (wave steps, busy lane-steps, wave descent / leaf iterations; counting variant
+    // only), [8 + 8q] tile queue head q
     // (q = 0..7, one 64-B line each) -- [0, COUNTERS_FRAME) reset per frame --
     // [COUNTERS_TOTAL + 0/1] total rays / hits since vrh_stats_reset
     unsigned long long* counters;
@@ -50,7 +52,6 @@ struct launch_config
     int kind;          // 0 triangles, 1 spheres
     bool ao;
     bool count;        // VRH_KERNEL_COUNT_TESTS variant
-    int sched;         // AO schedule: 0 rounds, 1 refill
     int block;         // threads per block (multiple of 64)
     int stack_cap;     // LDS stack entries per lane
     int occ;           // unified kernel register budget: min waves per SIMD (1, 6 or 8)

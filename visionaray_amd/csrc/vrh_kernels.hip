@@ -10,10 +10,10 @@
 //     [entry][lane] so a wave's pushes/pops are bank-conflict free); the stack capacity is chosen
 //     per scene from the BVH depth (a depth-first traversal never holds more than depth entries);
 //   * AO (ao/main.cpp:183-246) is fused: the tile's hit records are staged in LDS and its
-//     hits x samples any-hit rays are generated on chip -- no ray buffer touches HBM.  Two
-//     schedules: ROUNDS hands rays out 64 at a time (a round waits for its slowest lane); REFILL
-//     gives a lane a new ray the moment its ray terminates (ballot + mbcnt compaction of the idle
-//     lanes), so the wave stays busy until the tile's ray pool is empty.
+//     hits x samples any-hit rays are generated on chip -- no ray buffer touches HBM.  Primary and
+//     AO rays share one refilling loop: a lane whose ray terminates takes the next ray of the tile
+//     at once (ballot + mbcnt compaction of the idle lanes), so the wave stays busy until the
+//     tile's ray pool is empty.
 #include "vrh_device.h"
 #include "vrh_kernels.h"
 
@@ -118,170 +118,7 @@ __device__ __forceinline__ ray_t ao_ray(const render_params& P, const float* rec
     return make_ray(pos + d * P.eps, d);
 }
 
-template <int KIND, bool AO, bool COUNT, int SCHED>
-__global__ void render_kernel(render_params P)
-{
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63u;
-    const uint32_t wave = tid >> 6;
-    const uint32_t block = blockDim.x;
-
-    lds_stack st;
-    st.mem = smem;
-    st.base = tid;
-    st.stride = block;
-    st.top = tid;
-    uint32_t* ao_area = smem + P.stack_cap * block + wave * AO_WAVE_WORDS;
-    float* recs = reinterpret_cast<float*>(ao_area);          // 64 records x AO_REC_WORDS
-    uint32_t* masks = ao_area + 64 * AO_REC_WORDS;             // occlusion mask per hit slot
-    test_counts cnt = { 0u, 0u, false };
-    tile_queue tq = queue_init(P);
-
-    for (;;)
-    {
-        const uint32_t tile = next_tile(P, tq, lane);
-        if (tile == NONE) break;
-
-        uint32_t x, y, orow;
-        bool valid = tile_pixel(P, tile, lane, x, y, orow);
-
-        hit_t h = miss_record();
-        ray_t r;
-        if (valid)
-        {
-            r = primary_ray(P, x, y);
-            h = trace<KIND, false, COUNT>(P.pairs, P.prims, P.root, r, 3.402823466e+38f, st, cnt, P.step_limit);
-        }
-        float4 color = make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
-        uint32_t occ_mask = 0;
-        const bool is_hit = valid && h.hit;
-        const uint64_t hitmask = __ballot(is_hit);
-        uint32_t nrays = (uint32_t)__popcll(__ballot(valid));
-
-        if constexpr (AO)
-        {
-            // ---- stage this wave's hit records (compacted: slot k = k-th hit lane) ----------
-            const uint32_t hits = (uint32_t)__popcll(hitmask);
-            const uint32_t slot = lane_rank(hitmask);
-            if (is_hit)
-            {
-                f3 pos = r.ori + r.dir * h.t;                       // ao/main.cpp:202
-                float4 nn = P.normals[h.prim_id];                   // get_normal.h:26-37
-                float* rec = recs + slot * AO_REC_WORDS;
-                rec[0] = pos.x; rec[1] = pos.y; rec[2] = pos.z;
-                rec[3] = nn.x; rec[4] = nn.y; rec[5] = nn.z;
-                rec[6] = __uint_as_float(y * P.width + x);          // global pixel index p
-                masks[slot] = 0u;
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-
-            const uint32_t S = P.samples;
-            const uint32_t total = hits * S;
-            if constexpr (SCHED == SCHED_ROUNDS)
-            {
-                for (uint32_t base = 0; base < total; base += 64u)
-                {
-                    uint32_t j = base + lane;
-                    if (j < total)
-                    {
-                        uint32_t hs, s;
-                        ray_t ar = ao_ray(P, recs, j, S, hs, s);
-                        hit_t a = trace<KIND, true, COUNT>(P.pairs, P.prims, P.root, ar, P.radius, st, cnt, P.step_limit);
-                        if (a.hit) atomicOr(&masks[hs], 1u << s);
-                    }
-                }
-            }
-            else
-            {
-                // REFILL: a lane whose ray terminated takes the next unassigned ray of the tile
-                uint32_t next = 0;                     // wave-uniform: rays handed out so far
-                uint32_t cur = NONE, cur_slot = 0, cur_s = 0, steps = 0;
-                ray_t ar;
-                for (;;)
-                {
-                    const uint64_t idle = __ballot(cur == NONE);
-                    if (idle)
-                    {
-                        uint32_t cand = next + lane_rank(idle);
-                        next += (uint32_t)__popcll(idle);
-                        if (cur == NONE && cand < total)
-                        {
-                            cur = cand;
-                            ar = ao_ray(P, recs, cand, S, cur_slot, cur_s);
-                            st.reset();
-                            st.push(P.root);
-                            steps = 0;
-                        }
-                    }
-                    if (__ballot(cur != NONE) == 0ull) break;
-                    if (cur != NONE)
-                    {
-                        int done = anyhit_step<KIND, COUNT>(P.pairs, P.prims, ar, P.radius, st, cnt, steps, P.step_limit);
-                        if (done)
-                        {
-                            if (done > 0) atomicOr(&masks[cur_slot], 1u << cur_s);
-                            cur = NONE;
-                        }
-                    }
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            nrays += total;
-            if (is_hit)
-            {
-                occ_mask = masks[slot];
-                float clr = 1.0f;
-                const float step = 1.0f / (float)S;
-                for (uint32_t s2 = 0; s2 < S; ++s2)
-                    if ((occ_mask >> s2) & 1u) clr = clr - step;     // ao/main.cpp:234-238
-                color = make_float4(clr, clr, clr, 1.0f);
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-        else
-        {
-            if (is_hit) color = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
-        }
-
-        if (valid)
-        {
-            size_t o = (size_t)orow * P.width + x;
-            if (P.color) P.color[o] = color;
-            if (P.prim_id) P.prim_id[o] = is_hit ? h.prim_id : 0xFFFFFFFFu;
-            if (P.t) P.t[o] = is_hit ? h.t : -1.0f;
-            if (P.occ) P.occ[o] = (uint8_t)occ_mask;
-        }
-        if (__ballot(cnt.aborted) != 0ull && lane == 0) atomicOr(P.counters + 5, 1ull);
-        if (lane == 0)
-        {
-            unsigned long long nh = (unsigned long long)__popcll(hitmask);
-            atomicAdd(P.counters + 1, (unsigned long long)nrays);
-            atomicAdd(P.counters + 2, nh);
-            atomicAdd(P.counters + COUNTERS_TOTAL, (unsigned long long)nrays);
-            atomicAdd(P.counters + COUNTERS_TOTAL + 1, nh);
-        }
-    }
-    if (COUNT)
-    {
-        // wave-reduce the per-lane test counts, one atomic per wave
-        unsigned long long b = cnt.box, q = cnt.prim;
-        for (int off = 32; off > 0; off >>= 1)
-        {
-            b += __shfl_down(b, off);
-            q += __shfl_down(q, off);
-        }
-        if (lane == 0)
-        {
-            atomicAdd(P.counters + 3, b);
-            atomicAdd(P.counters + 4, q);
-        }
-    }
-}
-
-// UNIFIED schedule: one refilling loop per wave.  Primary rays (one per pixel of the wave's tile)
+// One refilling loop per wave.  Primary rays (one per pixel of the wave's tile)
 // and AO rays (published as soon as their primary hit is known) are stepped by the same
 // instruction stream (ray_step); a lane that finishes a ray immediately takes the next one, so
 // neither the primary phase nor the AO phase waits for its slowest lane.  Without AO the wave
@@ -294,7 +131,6 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     const uint32_t lane = tid & 63u;
     const uint32_t wave = tid >> 6;
     const uint32_t block = blockDim.x;
-    const float FMAX = 3.402823466e+38f;
 
     lds_stack st;
     st.mem = smem;
@@ -304,7 +140,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     uint32_t* ao_area = smem + P.stack_cap * block + wave * AO_WAVE_WORDS;
     float* recs = reinterpret_cast<float*>(ao_area);
     uint32_t* masks = ao_area + 64 * AO_REC_WORDS;
-    test_counts cnt = { 0u, 0u, false };
+    test_counts cnt = {};
     uint64_t rays_total = 0, hits_total = 0;
 
     // lane state: the ray it is stepping
@@ -356,6 +192,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 if (tile == NONE) break;
                 continue;
             }
+            const bool busy = mode != IDLE;
             if (mode != IDLE)
             {
                 int rc = (P.fast_ok && __ballot(!finite_ray(r)) == 0ull)
@@ -372,6 +209,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     mode = IDLE;
                 }
             }
+            if (COUNT) count_wave(cnt, busy);
         }
     }
     else
@@ -443,6 +281,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 // 3. done when nothing is in flight and nothing is left to hand out
                 if (__ballot(mode != IDLE) == 0ull && pending == 0u && issued >= avail) break;
                 // 4. one traversal step for every busy lane (same code for both ray kinds)
+                const bool busy = mode != IDLE;
                 if (mode != IDLE)
                 {
                     int rc = (P.fast_ok && __ballot(!finite_ray(r)) == 0ull)
@@ -464,6 +303,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                         mode = IDLE;
                     }
                 }
+                if (COUNT) count_wave(cnt, busy);
             }
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -510,6 +350,10 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         {
             atomicAdd(P.counters + 3, b);
             atomicAdd(P.counters + 4, q);
+            atomicAdd(P.counters + 6, (unsigned long long)cnt.w_steps);    // wave-uniform values
+            atomicAdd(P.counters + 7, (unsigned long long)cnt.w_busy);
+            atomicAdd(P.counters + 9, (unsigned long long)cnt.w_box);
+            atomicAdd(P.counters + 10, (unsigned long long)cnt.w_prim);
         }
     }
 }
@@ -553,34 +397,25 @@ __global__ void unshard_kernel(unshard_params u)
 
 using kernel_fn = void (*)(render_params);
 
-template <int KIND>
-static kernel_fn pick(bool ao, bool count, int sched, int occ)
+template <int KIND, int OCC>
+static kernel_fn pick_occ(bool ao, bool count)
 {
-    if (sched == dev::SCHED_UNIFIED)
-    {
-        if (occ == 8)
-        {
-            if (!ao) return count ? dev::render_unified_kernel<KIND, false, true, 8> : dev::render_unified_kernel<KIND, false, false, 8>;
-            return count ? dev::render_unified_kernel<KIND, true, true, 8> : dev::render_unified_kernel<KIND, true, false, 8>;
-        }
-        if (occ == 6)
-        {
-            if (!ao) return count ? dev::render_unified_kernel<KIND, false, true, 6> : dev::render_unified_kernel<KIND, false, false, 6>;
-            return count ? dev::render_unified_kernel<KIND, true, true, 6> : dev::render_unified_kernel<KIND, true, false, 6>;
-        }
-        if (!ao) return count ? dev::render_unified_kernel<KIND, false, true, 1> : dev::render_unified_kernel<KIND, false, false, 1>;
-        return count ? dev::render_unified_kernel<KIND, true, true, 1> : dev::render_unified_kernel<KIND, true, false, 1>;
-    }
-    if (!ao) return count ? dev::render_kernel<KIND, false, true, 0> : dev::render_kernel<KIND, false, false, 0>;
-    if (sched == dev::SCHED_ROUNDS)
-        return count ? dev::render_kernel<KIND, true, true, dev::SCHED_ROUNDS> : dev::render_kernel<KIND, true, false, dev::SCHED_ROUNDS>;
-    return count ? dev::render_kernel<KIND, true, true, dev::SCHED_REFILL> : dev::render_kernel<KIND, true, false, dev::SCHED_REFILL>;
+    if (!ao) return count ? dev::render_unified_kernel<KIND, false, true, OCC> : dev::render_unified_kernel<KIND, false, false, OCC>;
+    return count ? dev::render_unified_kernel<KIND, true, true, OCC> : dev::render_unified_kernel<KIND, true, false, OCC>;
+}
+
+template <int KIND>
+static kernel_fn pick(bool ao, bool count, int occ)
+{
+    if (occ == 8) return pick_occ<KIND, 8>(ao, count);
+    if (occ == 6) return pick_occ<KIND, 6>(ao, count);
+    return pick_occ<KIND, 1>(ao, count);
 }
 
 static kernel_fn select_variant(const launch_config& c)
 {
-    return c.kind == dev::KIND_TRI ? pick<dev::KIND_TRI>(c.ao, c.count, c.sched, c.occ)
-                                   : pick<dev::KIND_SPHERE>(c.ao, c.count, c.sched, c.occ);
+    return c.kind == dev::KIND_TRI ? pick<dev::KIND_TRI>(c.ao, c.count, c.occ)
+                                   : pick<dev::KIND_SPHERE>(c.ao, c.count, c.occ);
 }
 
 size_t render_lds_bytes(const launch_config& c)

@@ -55,7 +55,7 @@ struct vrh_ctx
     vrh_frame_stats last{};
     bool have_frame = false;
     // tuning options (0 = automatic), vrh_ctx_set_option
-    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0;
+    int opt_block = 0, opt_stack = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0;
 };
 
 struct vrh_scene
@@ -165,7 +165,7 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
         VRH_CHECK(value % 64 == 0, "vrh_ctx_set_option: block threads must be a multiple of 64");
         ctx->opt_block = int(value); break;
     case VRH_OPT_STACK_CAP: ctx->opt_stack = int(value); break;
-    case VRH_OPT_AO_SCHEDULE: VRH_CHECK(value <= 3, "vrh_ctx_set_option: schedule is 1, 2 or 3"); ctx->opt_sched = int(value); break;
+    case VRH_OPT_AO_SCHEDULE: VRH_CHECK(value == 0 || value == 3, "vrh_ctx_set_option: the only AO schedule is 3 (unified)"); break;
     case VRH_OPT_BLOCKS_PER_CU: ctx->opt_bpc = int(value); break;
     case VRH_OPT_WAVES_PER_SIMD: VRH_CHECK(value == 0 || value == 1 || value == 6 || value == 8, "vrh_ctx_set_option: waves per SIMD is 1, 6 or 8"); ctx->opt_occ = int(value); break;
     case VRH_OPT_EXACT_MINMAX: ctx->opt_exact_minmax = value ? 1 : 0; break;
@@ -215,9 +215,10 @@ VRH_API int vrh_scene_upload(vrh_ctx* ctx, const void* nodes_v, uint32_t num_nod
         uint32_t l0, l1;
         if (!link_of(c0, l0) || !link_of(c1, l1)) { set_error("vrh_scene_upload: malformed node pair " + std::to_string(k)); return VRH_ERR_INVALID; }
         float4* q = &pairs[4 * k];
-        q[0] = make_float4(c0.bmin[0], c0.bmin[1], c0.bmin[2], c0.bmax[0]);
-        q[1] = make_float4(c0.bmax[1], c0.bmax[2], c1.bmin[0], c1.bmin[1]);
-        q[2] = make_float4(c1.bmin[2], c1.bmax[0], c1.bmax[1], c1.bmax[2]);
+        // slab-major, child-interleaved (vrh_device.h): packed (child 0, child 1) operand pairs
+        q[0] = make_float4(c0.bmin[0], c1.bmin[0], c0.bmin[1], c1.bmin[1]);
+        q[1] = make_float4(c0.bmin[2], c1.bmin[2], c0.bmax[0], c1.bmax[0]);
+        q[2] = make_float4(c0.bmax[1], c1.bmax[1], c0.bmax[2], c1.bmax[2]);
         uint32_t w[4] = { l0, l1, 0u, 0u };
         std::memcpy(&q[3], w, 16);
     }
@@ -457,7 +458,6 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     lc.kind = sc->info.prim_kind == VRH_PRIM_TRI64 ? 0 : 1;
     lc.ao = ao;
     lc.count = (k->flags & VRH_KERNEL_COUNT_TESTS) != 0;
-    lc.sched = ctx->opt_sched == 0 ? 2 : ctx->opt_sched - 1;   // auto = unified
     lc.block = ctx->opt_block ? ctx->opt_block : 64;
     lc.stack_cap = int(cap);
     lc.occ = ctx->opt_occ ? ctx->opt_occ : 6;
@@ -533,13 +533,17 @@ VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats)
     VRH_HIP(hipEventSynchronize(ctx->ev_stop[ctx->last_slot]));
     float ms = 0.0f;
     VRH_HIP(hipEventElapsedTime(&ms, ctx->ev_start[ctx->last_slot], ctx->ev_stop[ctx->last_slot]));
-    unsigned long long c[8];
+    unsigned long long c[11];
     VRH_HIP(hipMemcpy(c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     ctx->last.kernel_ms = ms;
     ctx->last.rays = c[1];
     ctx->last.hits = c[2];
     ctx->last.box_tests = c[3];
     ctx->last.prim_tests = c[4];
+    ctx->last.wave_steps = c[6];
+    ctx->last.busy_lane_steps = c[7];
+    ctx->last.wave_box_iters = c[9];
+    ctx->last.wave_prim_iters = c[10];
     *stats = ctx->last;
     if (c[5] & 1ull) { set_error("traversal step guard tripped: corrupt BVH (rays were cut short)"); return VRH_ERR_HIP; }
     return VRH_OK;
