@@ -12,8 +12,10 @@ A "step" is one frame.  Inputs (BVH, primitives, normals) are resident in HBM be
 N > 1: one process per GPU; the image is sharded by 8-row bands (band b -> rank b % N, SURVEY.md
 §8e), each rank renders its packed shard, and the framebuffer is gathered to rank 0 over RCCL
 (torch.distributed "nccl"; prim ids + AO masks, 5 B/pixel) and un-interleaved there with the
-RGBA32F colour re-derived exactly (vrh_unshard) -- all inside the timed step.  Total work per frame
-is fixed, so scaling is strong.
+RGBA32F colour re-derived exactly (vrh_unshard).  Two frames are in flight: frame k renders while
+frame k-1's gather runs on RCCL's stream; the last frame's gather and un-interleave finish inside
+the timed region, so K steps = K complete frames on rank 0.  Total work per frame is fixed, so
+scaling is strong.
 
 Rank 0 prints one JSON line (contract in the task statement) with the roofline of the traversal
 kernel (algorithmic bytes per SURVEY.md §8d from a counting pass, over the hipEvent kernel time of
@@ -135,39 +137,63 @@ def main():
         rt = va.hip_buffer_rt(ctx, W, H)
         shard = None
     else:
+        # two frames in flight: frame k renders into slot k % 2 while frame k - 1's gather (RCCL,
+        # on its own stream) and un-interleave finish; every slot is reused only after the stream
+        # has waited for the gather that read it
         n = rows_max * W
-        loc = torch.empty((5 * n,), dtype=torch.uint8, device="cuda")
-        base = loc.data_ptr()
-        rt = va.hip_buffer_rt(ctx, W, rows_max, wrap=(0, base, 0, base + 4 * n))
+        nslots = 2
+        locs = [torch.empty((5 * n,), dtype=torch.uint8, device="cuda") for _ in range(nslots)]
+        rts = [va.hip_buffer_rt(ctx, W, rows_max, wrap=(0, b.data_ptr(), 0, b.data_ptr() + 4 * n)) for b in locs]
+        rt = rts[0]
         shard = _capi.vrh_shard(rank, world, 1, 0)
         if rank == 0:
-            gathered = torch.empty((world, 5 * n), dtype=torch.uint8, device="cuda")
-            gbase = gathered.data_ptr()
+            gathereds = [torch.empty((world, 5 * n), dtype=torch.uint8, device="cuda") for _ in range(nslots)]
             full = va.hip_buffer_rt(ctx, W, H, flags=_capi.VRH_RT_COLOR | _capi.VRH_RT_PRIM_ID | _capi.VRH_RT_OCC)
 
-    def gather():
+    def gather(slot):
+        loc = locs[slot]
         if args.dist_backend == "nccl":
             if rank == 0:
-                dist.gather(loc, gather_list=list(gathered.unbind(0)), dst=0)
-            else:
-                dist.gather(loc, dst=0)
-        else:   # gloo rehearsal: stage through host memory
-            torch.cuda.synchronize()
-            host = loc.cpu()
-            if rank == 0:
-                hg = torch.empty((world, host.numel()), dtype=torch.uint8)
-                dist.gather(host, gather_list=list(hg.unbind(0)), dst=0)
-                gathered.copy_(hg)
-            else:
-                dist.gather(host, dst=0)
+                return dist.gather(loc, gather_list=list(gathereds[slot].unbind(0)), dst=0, async_op=True)
+            return dist.gather(loc, dst=0, async_op=True)
+        # gloo rehearsal: stage through host memory, synchronously
+        torch.cuda.synchronize()
+        host = loc.cpu()
+        if rank == 0:
+            hg = torch.empty((world, host.numel()), dtype=torch.uint8)
+            dist.gather(host, gather_list=list(hg.unbind(0)), dst=0)
+            gathereds[slot].copy_(hg)
+        else:
+            dist.gather(host, dst=0)
+        return None
+
+    pending = []          # (work, slot) of gathers not yet waited for, oldest first
+
+    def finish_one():
+        work, slot = pending.pop(0)
+        if work is not None:
+            work.wait()   # the compute stream waits for the gather; the host does not block
+        if rank == 0:
+            g = gathereds[slot].data_ptr()
+            va.unshard(ctx, W, H, world, full, prim_id_ptr=g, occ_ptr=g + 4 * n,
+                       shard_stride_bytes=5 * n, kernel=kern)
+
+    frame = [0]
 
     def step():
-        va.render(ctx, dev, rt, basis, kern, shard)
-        if world > 1:
-            gather()
-            if rank == 0:
-                va.unshard(ctx, W, H, world, full, prim_id_ptr=gbase, occ_ptr=gbase + 4 * n,
-                           shard_stride_bytes=5 * n, kernel=kern)
+        if world == 1:
+            va.render(ctx, dev, rt, basis, kern, shard)
+            return
+        slot = frame[0] % nslots
+        frame[0] += 1
+        while len(pending) >= nslots:      # the slot's previous gather must be done before reuse
+            finish_one()
+        va.render(ctx, dev, rts[slot], basis, kern, shard)
+        pending.append((gather(slot), slot))
+
+    def drain():
+        while pending:
+            finish_one()
 
     def barrier():
         if world > 1:
@@ -180,12 +206,14 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    drain()
     barrier()
     ctx.stats_reset()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()               # the last frame's gather and un-interleave are inside the timed region
     barrier()
     elapsed = time.perf_counter() - t0
     acc = ctx.accum_stats()

@@ -118,7 +118,9 @@ typedef struct {
 typedef struct {
     uint32_t num_nodes, num_prims, num_indices, prim_kind;
     uint32_t max_depth;       /* root depth 0; traversal needs <= max_depth stack entries      */
-    uint64_t device_bytes;    /* node pairs + leaf-ordered primitives + normals               */
+    uint64_t device_bytes;    /* node pairs + leaf-ordered primitives + normals + 4-wide records */
+    uint32_t wide_records;    /* 4-wide any-hit records (0: the BVH failed the containment check) */
+    uint32_t wide_depth;      /* levels of the 4-wide tree                                      */
 } vrh_scene_info;
 
 /* camera::look_at + camera::perspective (camera.inl:10-57) followed by the pinhole basis that
@@ -142,14 +144,24 @@ enum vrh_option {
     VRH_OPT_BLOCK_THREADS = 1,   /* threads per block, multiple of 64 (auto: 64)                  */
     VRH_OPT_STACK_CAP = 2,       /* LDS stack entries per lane, >= BVH depth (auto: depth rounded
                                     up to a multiple of 4)                                        */
-    VRH_OPT_AO_SCHEDULE = 3,     /* 3 = primary + AO rays in one refilling loop (the only schedule;
-                                    0 = auto = 3; the earlier 1/2 schedules were retired)        */
+    VRH_OPT_AO_SCHEDULE = 3,     /* refilling loop of a wave: 3 = one descend-to-leaf step per
+                                    iteration, 4 = one traversal item (node pair or primitive)
+                                    per lane and iteration, 5 = items, but only node pairs or
+                                    only primitives per iteration, whichever more lanes wait for
+                                    (auto: 4 for sphere primary visibility, else 3)              */
     VRH_OPT_BLOCKS_PER_CU = 4,   /* resident blocks per CU for the persistent grid (auto: max)     */
     VRH_OPT_WAVES_PER_SIMD = 5,  /* register budget of the unified kernel: 1 (none), 6 or 8 (auto 6) */
     VRH_OPT_EXACT_MINMAX = 6,    /* 1 = always use the ternary min/max slab test (auto: hardware
                                     min/max where provably identical, see vrh_device.h)           */
-    VRH_OPT_XCD_QUEUES = 7       /* tile queues: 1 = one per XCD with stealing, 2 = one global
+    VRH_OPT_XCD_QUEUES = 7,      /* tile queues: 1 = one per XCD with stealing, 2 = one global
                                     queue (auto: 1)                                               */
+    VRH_OPT_REFILL_MIN = 8,      /* item loops: free lanes (1..64) before rays are retired and idle
+                                    lanes refilled (auto: 16)                                    */
+    VRH_OPT_VOTE_LEAF = 9,       /* vote loop: primitive step when 8 x leaf lanes >= this x node
+                                    lanes (1..64, auto: 8 = simple majority)                     */
+    VRH_OPT_WIDE_ANYHIT = 10     /* 4-wide node records for any-hit (AO) rays (step loop): 1 = on
+                                    when the BVH passes the containment check, 2 = off (auto: off,
+                                    measured 6 % slower on hf1M AO than the binary records)      */
 };
 VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value);
 

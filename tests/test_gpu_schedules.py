@@ -1,0 +1,62 @@
+"""GPU: every traversal schedule and record width reaches the same bit-exact result.
+
+The kernel has several ways to organise a wave's work (vrh.h VRH_OPT_AO_SCHEDULE: whole descend-
+to-leaf steps, single items, items by vote; VRH_OPT_WIDE_ANYHIT: 4-wide any-hit records).  Only
+the defaults run in test_gpu_parity.py; here the parity cases are re-run under each non-default
+choice, on the same context, so none of the paths can drift from the reference.
+"""
+import os
+import sys
+
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import test_gpu_parity as base  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = {
+    "step": {"ao_schedule": 3},
+    "item": {"ao_schedule": 4},
+    "item_refill1": {"ao_schedule": 4, "refill_min": 1},
+    "vote": {"ao_schedule": 5},
+    "vote_leafheavy": {"ao_schedule": 5, "vote_leaf": 64},
+    "step_wide": {"ao_schedule": 3, "wide_anyhit": 1},
+    "step_wide_exact": {"ao_schedule": 3, "wide_anyhit": 1, "exact_minmax": 1},
+}
+OPTIONS = ("ao_schedule", "refill_min", "vote_leaf", "wide_anyhit", "exact_minmax")
+
+
+@pytest.fixture(params=sorted(VARIANTS))
+def vctx(request, ctx):
+    for k, v in VARIANTS[request.param].items():
+        ctx.set_option(k, v)
+    yield ctx
+    for k in OPTIONS:
+        ctx.set_option(k, 0)
+
+
+@pytest.mark.parametrize("case", base.FULL_CASES)
+def test_every_pixel(vctx, golden, case):
+    base.test_every_pixel_matches_reference(vctx, golden, case)
+
+
+@pytest.mark.parametrize("case", ["hf1M", "sph1M"])
+def test_full_frame_hashes(vctx, golden, oracle_mod, case):
+    base.test_full_frame_hashes_match_reference(vctx, golden, oracle_mod, case)
+
+
+def test_random_soup(vctx, oracle_mod):
+    base.test_random_soups_vs_oracle(vctx, oracle_mod, 1)
+
+
+def test_edge_cases(vctx, oracle_mod):
+    base.test_edge_cases_single_leaf_zero_dir_components_and_inside_sphere(vctx, oracle_mod)
+
+
+def test_deep_comb(vctx, oracle_mod):
+    base.test_deep_trees_wide_stack_and_rejection(vctx, oracle_mod, 90)
+
+
+def test_packed_shards(vctx):
+    base.test_packed_shards_gather_to_identical_image(vctx, 3)

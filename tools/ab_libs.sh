@@ -16,5 +16,5 @@ for rep in 1 2; do
     VRH_LIB=$lib VRH_AB_KERNEL=primary timeout -k 10 300 python tools/ab_variants.py sph1M 3 || exit $?
   done
 done
-[ -n "$DIAG" ] && timeout -k 10 300 python tools/simd_diag.py
+[ -n "$DIAG" ] && { timeout -k 10 300 python tools/simd_diag.py || exit $?; }
 exit 0

@@ -19,10 +19,10 @@ scene = sys.argv[1] if len(sys.argv) > 1 else "hf1M"
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 VARIANTS = json.loads(os.environ.get("VRH_AB", "null")) or [
     {"name": "default"},
-    {"name": "exact minmax", "exact_minmax": 1},
-    {"name": "no xcd queues", "xcd_queues": 2},
+    {"name": "binary any-hit", "wide_anyhit": 2},
+    {"name": "occ1", "waves_per_simd": 1},
     {"name": "occ8", "waves_per_simd": 8},
-    {"name": "b256", "block_threads": 256},
+    {"name": "item r24", "ao_schedule": 4, "refill_min": 24},
 ]
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 log = open(os.path.join(ROOT, "gpurun_out", f"ab_{scene}.log"), "a", buffering=1)
@@ -47,7 +47,8 @@ basis = cam.basis(W, H)
 ao = prims.dtype == va.TRIANGLE_DTYPE and os.environ.get("VRH_AB_KERNEL", "ao") == "ao"
 kern = va.ao_kernel(dev) if ao else va.closest_hit_kernel(dev)
 rt = va.hip_buffer_rt(ctx, W, H)
-say(f"scene {scene} {len(prims)} prims depth {host.max_depth} ao={ao}")
+say(f"scene {scene} {len(prims)} prims depth {host.max_depth} ao={ao} wide records {dev.info['wide_records']} "
+    f"(depth {dev.info['wide_depth']})")
 res = {v["name"]: [] for v in VARIANTS}
 for rnd in range(rounds):
     for v in VARIANTS:
@@ -58,6 +59,9 @@ for rnd in range(rounds):
         ctx.set_option("waves_per_simd", v.get("waves_per_simd", 0))
         ctx.set_option("exact_minmax", v.get("exact_minmax", 0))
         ctx.set_option("xcd_queues", v.get("xcd_queues", 0))
+        ctx.set_option("refill_min", v.get("refill_min", 0))
+        ctx.set_option("vote_leaf", v.get("vote_leaf", 0))
+        ctx.set_option("wide_anyhit", v.get("wide_anyhit", 0))
         ctx.stats_reset()
         for _ in range(5):
             va.render(ctx, dev, rt, basis, kern)

@@ -23,6 +23,8 @@ def say(*a):
 
 
 ctx = va.Context(0)
+if os.environ.get("VRH_AO_SCHEDULE"):
+    ctx.set_option("ao_schedule", int(os.environ["VRH_AO_SCHEDULE"]))
 for name in sys.argv[1:] or ["hf1M", "sph1M"]:
     prims = scenes.primitives(name)
     host = va.build_index_bvh(prims)

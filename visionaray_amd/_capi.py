@@ -32,7 +32,8 @@ class vrh_kernel_desc(C.Structure):
 VRH_KERNEL_COUNT_TESTS = 1
 VRH_BAND_ROWS = 8
 VRH_OPT_BLOCK_THREADS, VRH_OPT_STACK_CAP, VRH_OPT_AO_SCHEDULE, VRH_OPT_BLOCKS_PER_CU = 1, 2, 3, 4
-VRH_OPT_WAVES_PER_SIMD, VRH_OPT_EXACT_MINMAX, VRH_OPT_XCD_QUEUES = 5, 6, 7
+VRH_OPT_WAVES_PER_SIMD, VRH_OPT_EXACT_MINMAX, VRH_OPT_XCD_QUEUES, VRH_OPT_REFILL_MIN, VRH_OPT_VOTE_LEAF = 5, 6, 7, 8, 9
+VRH_OPT_WIDE_ANYHIT = 10
 VRH_MAX_TIMED_FRAMES = 1024
 
 
@@ -56,7 +57,8 @@ class vrh_frame_stats(C.Structure):
 
 class vrh_scene_info(C.Structure):
     _fields_ = [("num_nodes", C.c_uint32), ("num_prims", C.c_uint32), ("num_indices", C.c_uint32),
-                ("prim_kind", C.c_uint32), ("max_depth", C.c_uint32), ("device_bytes", C.c_uint64)]
+                ("prim_kind", C.c_uint32), ("max_depth", C.c_uint32), ("device_bytes", C.c_uint64),
+                ("wide_records", C.c_uint32), ("wide_depth", C.c_uint32)]
 
 
 class VrhError(RuntimeError):

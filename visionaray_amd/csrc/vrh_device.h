@@ -161,6 +161,7 @@ struct lds_stack
     uint32_t base;        // this lane's column (word offset of entry 0)
     uint32_t top;         // word offset of the next free entry
     uint32_t stride;      // words between entries = threads per block
+    uint32_t end;         // base + capacity * stride
     __device__ __forceinline__ void reset() { top = base; }
     __device__ __forceinline__ void push(uint32_t v) { mem[top] = v; top += stride; }
     __device__ __forceinline__ uint32_t pop() { top -= stride; return mem[top]; }
@@ -196,6 +197,21 @@ __device__ __forceinline__ void count_wave(test_counts& c, bool busy)
     c.it_prim = 0;
 }
 
+constexpr uint32_t QUAD_NONE = 0xFFFFFFFFu;
+
+// One entry of a 4-wide any-hit record (vrh_quad.cpp): the box test of update_if.h:60-66 with
+// best_t = max() (an any-hit ray has no hit yet while it traverses), hardware min/max (the lane's
+// ray is finite, so the slab distances are never NaN).
+__device__ __forceinline__ bool quad_entry(float xl, float yl, float zl, float xh, float yh, float zh,
+                                           const ray_t& r, float max_t, float& tn)
+{
+    const float t1x = (xl - r.ori.x) * r.inv.x, t1y = (yl - r.ori.y) * r.inv.y, t1z = (zl - r.ori.z) * r.inv.z;
+    const float t2x = (xh - r.ori.x) * r.inv.x, t2y = (yh - r.ori.y) * r.inv.y, t2z = (zh - r.ori.z) * r.inv.z;
+    tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1x, t2x), __builtin_fminf(t1y, t2y)), __builtin_fminf(t1z, t2z));
+    const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t1x, t2x), __builtin_fmaxf(t1y, t2y)), __builtin_fmaxf(t1z, t2z));
+    return (tf >= tn) & (tn < FMAX) & (tf >= 0.0f) & (tn < max_t);
+}
+
 // One outer iteration of the reference loop (detail/bvh/intersect.inl:66-130) for EITHER traversal
 // type: closest hit (any = false: boxes culled against the running best_t, all primitives of
 // reached leaves tested, best_t / best_prim updated by is_closer) or any hit (any = true: best_t
@@ -205,8 +221,14 @@ __device__ __forceinline__ void count_wave(test_counts& c, bool busy)
 // tie resolution identical.  Lanes of one wave may be in different
 // modes and still run the same instruction stream.  Returns 1 = any-hit found, -1 = ray finished
 // (stack empty), 0 = continue.
+//
+// `quad` lanes (any-hit rays with a finite ray, scene with 4-wide records) descend the 4-wide
+// records instead: the same set of leaves is reached (vrh_quad.cpp), the order does not matter
+// for an any-hit result, and the nearest hit entry is descended first.  If a record's hits could
+// overflow the stack, the ray restarts on the binary records from `root` (still exact).
 template <int KIND, bool COUNT, bool FAST>
 __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const float4* __restrict__ prims,
+                                        const float4* __restrict__ quads, uint32_t root, bool& quad,
                                         const ray_t& r, float max_t, bool any, lds_stack& st,
                                         float& best_t, uint32_t& best_prim, test_counts& cnt,
                                         uint32_t& steps, uint32_t step_limit)
@@ -216,7 +238,41 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
     if (st.empty()) return -1;
     if (++steps > step_limit) { cnt.aborted = true; return -1; }
     uint32_t link = st.pop();
-    while (!(link & LEAF_BIT))
+    if (quad)
+    {
+        while (!(link & LEAF_BIT))
+        {
+            const float4* p = quads + 8u * link;
+            const float4 xl = p[0], yl = p[1], zl = p[2], xh = p[3], yh = p[4], zh = p[5], lk = p[6];
+            const uint32_t k0 = __float_as_uint(lk.x), k1 = __float_as_uint(lk.y);
+            const uint32_t k2 = __float_as_uint(lk.z), k3 = __float_as_uint(lk.w);
+            float d0, d1, d2, d3;
+            const bool h0 = quad_entry(xl.x, yl.x, zl.x, xh.x, yh.x, zh.x, r, max_t, d0) & (k0 != QUAD_NONE);
+            const bool h1 = quad_entry(xl.y, yl.y, zl.y, xh.y, yh.y, zh.y, r, max_t, d1) & (k1 != QUAD_NONE);
+            const bool h2 = quad_entry(xl.z, yl.z, zl.z, xh.z, yh.z, zh.z, r, max_t, d2) & (k2 != QUAD_NONE);
+            const bool h3 = quad_entry(xl.w, yl.w, zl.w, xh.w, yh.w, zh.w, r, max_t, d3) & (k3 != QUAD_NONE);
+            if (COUNT) cnt.box += 4;
+            if (!(h0 | h1 | h2 | h3)) return st.empty() ? -1 : 0;
+            if (st.top + 3u * st.stride > st.end)
+            {
+                st.reset();
+                st.push(root);
+                quad = false;
+                return 0;
+            }
+            // nearest hit entry first (ties -> lower index), the other hits pushed
+            d0 = h0 ? d0 : INFINITY; d1 = h1 ? d1 : INFINITY; d2 = h2 ? d2 : INFINITY; d3 = h3 ? d3 : INFINITY;
+            const bool a01 = d1 < d0, a23 = d3 < d2;
+            const float m01 = a01 ? d1 : d0, m23 = a23 ? d3 : d2;
+            const uint32_t j = (m23 < m01) ? (a23 ? 3u : 2u) : (a01 ? 1u : 0u);
+            if (h0 & (j != 0u)) st.push(k0);
+            if (h1 & (j != 1u)) st.push(k1);
+            if (h2 & (j != 2u)) st.push(k2);
+            if (h3 & (j != 3u)) st.push(k3);
+            link = j == 0u ? k0 : j == 1u ? k1 : j == 2u ? k2 : k3;
+        }
+    }
+    else while (!(link & LEAF_BIT))
     {
         const float4* p = pairs + 4u * link;
         const float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
@@ -274,6 +330,152 @@ __device__ __forceinline__ ray_t make_ray(f3 ori, f3 dir)
     r.ori = ori; r.dir = dir;
     r.inv = mk3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);   // intersect.inl:63
     return r;
+}
+
+// One traversal ITEM of the reference loop (detail/bvh/intersect.inl:66-130): `item` is either an
+// inner pair (both children box-tested: the near hit child becomes the next item, the far one is
+// pushed, none -> pop) or one primitive of a leaf (LEAF_BIT | leaf-ordered index: tested, then the
+// next primitive of the leaf or, after the leaf's last one, a pop).  The per-lane sequence of box
+// and primitive tests, best_t updates and stack operations is exactly ray_step's (and the
+// reference's); only the unit a wave iterates on is smaller, so a lane that reaches a leaf does
+// not idle while its neighbours keep descending, and the 3 loads a node and a triangle have in
+// common are issued once for the wave.  Returns true when the ray is finished (stack exhausted,
+// any-hit found -> `occluded`, or the step guard).
+template <int KIND, bool COUNT, bool FAST>
+__device__ __forceinline__ bool item_step(const float4* __restrict__ pairs, const float4* __restrict__ prims,
+                                          const ray_t& r, float max_t, bool any, lds_stack& st, uint32_t& item,
+                                          float& best_t, uint32_t& best_prim, bool& occluded, test_counts& cnt,
+                                          uint32_t& steps, uint32_t step_limit)
+{
+    if (++steps > step_limit) { cnt.aborted = true; return true; }
+    const bool leaf = (item & LEAF_BIT) != 0u;
+    const uint32_t idx = item & ~LEAF_BIT;
+    constexpr uint32_t PF4 = KIND == KIND_TRI ? 3u : 2u;
+    const float4* base = leaf ? prims + PF4 * idx : pairs + 4u * idx;
+    const float4 q0 = base[0], q1 = base[1];
+    float4 q2 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), q3 = q2;
+    if constexpr (KIND == KIND_TRI) q2 = base[2];
+    if (!leaf)
+    {
+        if constexpr (KIND != KIND_TRI) q2 = base[2];
+        q3 = base[3];
+    }
+    bool pop;
+    if (!leaf)
+    {
+        bool b0, b1;
+        float tn0, tn1;
+        box_pair<FAST>(q0, q1, q2, r, best_t, max_t, b0, b1, tn0, tn1);
+        const uint32_t l0 = __float_as_uint(q3.x), l1 = __float_as_uint(q3.y);
+        if (COUNT) { cnt.box += 2; cnt.it_box = 1; }
+        const bool both = b0 & b1;
+        const bool go0 = both ? (tn0 < tn1) : b0;          // intersect.inl:84-101
+        if (both) st.push(go0 ? l1 : l0);
+        pop = !(b0 | b1);
+        item = go0 ? l0 : l1;
+    }
+    else
+    {
+        float t;
+        bool h;
+        uint32_t flags, pid;
+        if constexpr (KIND == KIND_TRI)
+        {
+            h = isect_tri(r, q0, q1, q2, t);
+            pid = __float_as_uint(q2.y);
+            flags = __float_as_uint(q2.w);
+        }
+        else
+        {
+            h = isect_sphere(r, q0, t);
+            pid = __float_as_uint(q1.x);
+            flags = __float_as_uint(q1.z);
+        }
+        if (COUNT) { cnt.prim += 1; cnt.it_prim = 1; }
+        if (h & (t >= 0.0f) & (t < best_t) & (t < max_t))      // update_if.h:48-56, 73-79
+        {
+            best_t = t;
+            best_prim = pid;
+            if (any) { occluded = true; return true; }           // exit_traversal.h:49-56
+        }
+        pop = (flags & END_BIT) != 0u;
+        item = item + 1u;
+    }
+    if (pop)
+    {
+        if (st.empty()) return true;
+        item = st.pop();
+    }
+    return false;
+}
+
+// item_step split by kind, for the VOTE schedule (a wave runs only one of the two per iteration).
+// node_step: `item` is an inner pair.  prim_step: `item` is LEAF_BIT | primitive.  Same return
+// convention and the same per-lane sequence of operations as item_step.
+__device__ __forceinline__ bool pop_or_done(lds_stack& st, uint32_t& item)
+{
+    if (st.empty()) return true;
+    item = st.pop();
+    return false;
+}
+
+template <bool COUNT, bool FAST>
+__device__ __forceinline__ bool node_step(const float4* __restrict__ pairs, const ray_t& r, float max_t, lds_stack& st,
+                                          uint32_t& item, float best_t, test_counts& cnt, uint32_t& steps,
+                                          uint32_t step_limit)
+{
+    if (++steps > step_limit) { cnt.aborted = true; return true; }
+    const float4* p = pairs + 4u * item;
+    const float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    bool b0, b1;
+    float tn0, tn1;
+    box_pair<FAST>(q0, q1, q2, r, best_t, max_t, b0, b1, tn0, tn1);
+    const uint32_t l0 = __float_as_uint(q3.x), l1 = __float_as_uint(q3.y);
+    if (COUNT) { cnt.box += 2; cnt.it_box = 1; }
+    const bool both = b0 & b1;
+    const bool go0 = both ? (tn0 < tn1) : b0;              // intersect.inl:84-101
+    if (both) st.push(go0 ? l1 : l0);
+    item = go0 ? l0 : l1;
+    if (!(b0 | b1)) return pop_or_done(st, item);
+    return false;
+}
+
+template <int KIND, bool COUNT>
+__device__ __forceinline__ bool prim_step(const float4* __restrict__ prims, const ray_t& r, float max_t, bool any,
+                                          lds_stack& st, uint32_t& item, float& best_t, uint32_t& best_prim,
+                                          bool& occluded, test_counts& cnt, uint32_t& steps, uint32_t step_limit)
+{
+    if (++steps > step_limit) { cnt.aborted = true; return true; }
+    const uint32_t idx = item & ~LEAF_BIT;
+    float t;
+    bool h;
+    uint32_t flags, pid;
+    if constexpr (KIND == KIND_TRI)
+    {
+        const float4* q = prims + 3u * idx;
+        const float4 a = q[0], b = q[1], c = q[2];
+        h = isect_tri(r, a, b, c, t);
+        pid = __float_as_uint(c.y);
+        flags = __float_as_uint(c.w);
+    }
+    else
+    {
+        const float4* q = prims + 2u * idx;
+        const float4 a = q[0], b = q[1];
+        h = isect_sphere(r, a, t);
+        pid = __float_as_uint(b.x);
+        flags = __float_as_uint(b.z);
+    }
+    if (COUNT) { cnt.prim += 1; cnt.it_prim = 1; }
+    if (h & (t >= 0.0f) & (t < best_t) & (t < max_t))          // update_if.h:48-56, 73-79
+    {
+        best_t = t;
+        best_prim = pid;
+        if (any) { occluded = true; return true; }               // exit_traversal.h:49-56
+    }
+    item = item + 1u;
+    if (flags & END_BIT) return pop_or_done(st, item);
+    return false;
 }
 
 // SURVEY.md Appendix A counter hash

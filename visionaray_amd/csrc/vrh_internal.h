@@ -6,6 +6,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <vector>
 
 namespace vrh {
 
@@ -33,6 +34,13 @@ static_assert(sizeof(tri64) == 64, "triangle layout");
 static_assert(sizeof(sphere48) == 48, "sphere layout");
 
 void set_error(const std::string& msg);
+
+constexpr uint32_t QUAD_NONE = 0xFFFFFFFFu;     // unused entry of a 4-wide record
+
+// 4-wide any-hit records from the binary BVH (vrh_quad.cpp); false = the scene keeps the binary
+// path (containment or box validity does not hold, or the root is a leaf)
+bool build_quads(const node32* nodes, uint32_t num_nodes, std::vector<float>& out, uint32_t& root_link,
+                 uint32_t& quad_depth);
 
 int build_bvh(const void* prims, uint32_t n, uint32_t kind, node32* nodes_out, uint32_t* num_nodes_out,
               uint32_t* indices_out, uint32_t* max_depth_out);

@@ -17,6 +17,8 @@ struct render_params
     uint32_t step_limit;      // per-ray traversal step bound (nodes + primitives)
     uint32_t stack_cap;       // LDS stack entries per lane (>= BVH depth)
     uint32_t fast_ok;         // node bounds all finite: hardware min/max slab path allowed
+    const float4* quads;      // 8 float4 per 4-wide any-hit record (vrh_quad.cpp)
+    uint32_t quad_ok;         // any-hit rays with finite origin / inverse direction use `quads`
 
     float eye[3], cam_u[3], cam_v[3], cam_w[3];
     uint32_t width, height;
@@ -41,6 +43,8 @@ struct render_params
     // [COUNTERS_TOTAL + 0/1] total rays / hits since vrh_stats_reset
     unsigned long long* counters;
     uint32_t xcd_queues;      // 1: per-XCD tile queues with stealing; 0: one global queue
+    uint32_t refill_min;      // item schedule: retire / refill once this many lanes are free
+    uint32_t vote_leaf;       // vote schedule: leaf step when 8 * leaf lanes >= vote_leaf * node lanes
 };
 
 constexpr int COUNTERS_FRAME = 80;      // u64 words reset before every frame
@@ -54,7 +58,8 @@ struct launch_config
     bool count;        // VRH_KERNEL_COUNT_TESTS variant
     int block;         // threads per block (multiple of 64)
     int stack_cap;     // LDS stack entries per lane
-    int occ;           // unified kernel register budget: min waves per SIMD (1, 6 or 8)
+    int occ;           // register budget: min waves per SIMD (1, 6 or 8)
+    int sched;         // 0: step loop (render_unified_kernel), 1: item loop, 2: vote loop (render_item_kernel)
 };
 
 size_t render_lds_bytes(const launch_config& c);

@@ -23,9 +23,15 @@ namespace dev {
 constexpr int TILE = 8;             // 8x8 pixels per wave
 constexpr uint32_t BAND = VRH_BAND_ROWS;   // shard band height = one row of 8x8 tiles
 constexpr uint32_t NONE = 0xFFFFFFFFu;
-constexpr int AO_REC_WORDS = 8;     // per hit slot: isect pos xyz, normal xyz, pixel index, lane
-// per-wave AO area in LDS: 64 hit records + 64 occlusion masks
-constexpr int AO_WAVE_WORDS = 64 * AO_REC_WORDS + 64;
+// Per-wave AO area in LDS.  A wave keeps up to two tiles in flight: the current tile C (primaries
+// and AO rays being handed out) and the draining tile D (all its AO rays handed out, some still
+// being traced).  Hit records (isect position, face normal) are read only when an AO ray is handed
+// out, so one set serves C; occlusion masks and the slot -> pixel map live until a tile finishes,
+// so there are two of each, indexed by the tile's buffer parity.
+constexpr int AO_REC_WORDS = 6;                         // pos xyz, normal xyz
+constexpr int AO_MASKS = 64 * AO_REC_WORDS;             // u32 masks[2][64]
+constexpr int AO_SLOT_PX = AO_MASKS + 2 * 64;           // u8 slot_px[2][64]: pixel (lane) of a hit slot
+constexpr int AO_WAVE_WORDS = AO_SLOT_PX + 2 * 64 / 4;
 
 // tile index -> (x, y) of lane, plus the output row (packed shards).  A band is one row of tiles.
 __device__ __forceinline__ bool tile_pixel(const render_params& P, uint32_t tile, uint32_t lane,
@@ -100,17 +106,14 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask)
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// AO ray j of the tile: hit slot j / S, sample j % S (ao/main.cpp:216-238 with the Appendix-A
-// sampler); returns the ray and the slot.
-__device__ __forceinline__ ray_t ao_ray(const render_params& P, const float* recs, uint32_t j, uint32_t S,
-                                        uint32_t& slot, uint32_t& s)
+// AO ray s of hit slot `slot` whose pixel has global index p (ao/main.cpp:216-238 with the
+// Appendix-A sampler)
+__device__ __forceinline__ ray_t ao_ray(const render_params& P, const float* recs, uint32_t slot, uint32_t s,
+                                        uint32_t p)
 {
-    slot = j / S;
-    s = j - slot * S;
     const float* sr = recs + slot * AO_REC_WORDS;
     f3 pos = mk3(sr[0], sr[1], sr[2]);
     f3 n = mk3(sr[3], sr[4], sr[5]);
-    uint32_t p = __float_as_uint(sr[6]);
     // vector3.inl:357-367 make_orthonormal_basis(u, v, w = n)
     f3 bv = fabsf(n.x) > fabsf(n.y) ? normalize(mk3(-n.z, 0.0f, n.x)) : normalize(mk3(0.0f, n.z, -n.y));
     f3 bu = cross(bv, n);
@@ -137,9 +140,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     st.base = tid;
     st.stride = block;
     st.top = tid;
+    st.end = tid + P.stack_cap * block;
     uint32_t* ao_area = smem + P.stack_cap * block + wave * AO_WAVE_WORDS;
-    float* recs = reinterpret_cast<float*>(ao_area);
-    uint32_t* masks = ao_area + 64 * AO_REC_WORDS;
     test_counts cnt = {};
     uint64_t rays_total = 0, hits_total = 0;
 
@@ -149,7 +151,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     ray_t r;
     float best_t = FMAX, max_t = FMAX;
     uint32_t best_prim = 0, steps = 0;
-    bool any = false;
+    bool any = false, quad = false;
 
     if constexpr (!AO)
     {
@@ -196,8 +198,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             if (mode != IDLE)
             {
                 int rc = (P.fast_ok && __ballot(!finite_ray(r)) == 0ull)
-                    ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit)
-                    : ray_step<KIND, COUNT, false>(P.pairs, P.prims, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit);
+                    ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit)
+                    : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit);
                 if (rc != 0)
                 {
                     bool hit = best_t != FMAX;
@@ -214,120 +216,152 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     }
     else
     {
+        // ---- primary + AO: one refilling loop over a stream of tiles, two tiles in flight ----
         const uint32_t S = P.samples;
+        float* recs = reinterpret_cast<float*>(ao_area);
+        uint32_t* masks = ao_area + AO_MASKS;
+        uint8_t* slot_px = reinterpret_cast<uint8_t*>(ao_area + AO_SLOT_PX);
+        const float4 bg = make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
         tile_queue tq = queue_init(P);
+        // wave-uniform tile state
+        uint32_t tileC = next_tile(P, tq, lane), parC = 0;
+        uint32_t handedC = 0, pendC = 0, pubC = 0, issC = 0;  // primaries handed / in flight, slots, AO rays handed
+        uint32_t tileD = NONE, parD = 0, slotsD = 0;
+        uint32_t inflight0 = 0, inflight1 = 0;                // AO rays in flight per buffer parity
+        // lane state: PRIMARY tag = pixel lane k of tile C; AORAY tag = slot | s << 6 | parity << 11
+        uint32_t tag = 0;
         for (;;)
         {
-            const uint32_t tile = next_tile(P, tq, lane);
-            if (tile == NONE) break;
-
-            uint32_t x, y, orow;
-            const bool valid = tile_pixel(P, tile, lane, x, y, orow);
-            // own pixel's results
-            bool my_hit = false, just_done = false;
-            uint32_t my_prim = 0xFFFFFFFFu, my_slot = 0;
-            float my_t = -1.0f;
-            if (valid)
+            // 1. the draining tile is done when its last AO ray is: write its hit pixels
+            if (tileD != NONE && (parD ? inflight1 : inflight0) == 0u)
             {
-                r = primary_ray(P, x, y);
-                best_t = FMAX; best_prim = 0; steps = 0; max_t = FMAX; any = false;
-                st.reset(); st.push(P.root);
-                mode = PRIMARY;
-            }
-            uint32_t pending = (uint32_t)__popcll(__ballot(valid));   // primaries not yet finished
-            rays_total += valid ? 1 : 0;
-            uint32_t published = 0, issued = 0;                        // hit slots, AO rays handed out
-            uint32_t cur_slot = 0, cur_s = 0;
-            for (;;)
-            {
-                // 1. publish primaries that finished last iteration (compacted hit slots)
-                const uint64_t fin = __ballot(just_done);
-                if (fin)
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (lane < slotsD)
                 {
-                    const uint64_t hfin = __ballot(just_done && my_hit);
-                    if (just_done && my_hit)
-                    {
-                        my_slot = published + lane_rank(hfin);
-                        f3 pos = r.ori + r.dir * my_t;                  // ao/main.cpp:202
-                        float4 nn = P.normals[my_prim];                  // get_normal.h:26-37
-                        float* rec = recs + my_slot * AO_REC_WORDS;
-                        rec[0] = pos.x; rec[1] = pos.y; rec[2] = pos.z;
-                        rec[3] = nn.x; rec[4] = nn.y; rec[5] = nn.z;
-                        rec[6] = __uint_as_float(y * P.width + x);       // global pixel index p
-                        masks[my_slot] = 0u;
-                    }
-                    published += (uint32_t)__popcll(hfin);
-                    pending -= (uint32_t)__popcll(fin);
-                    just_done = false;
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                }
-                // 2. hand the published AO rays to idle lanes
-                const uint32_t avail = published * S;
-                const uint64_t idle = __ballot(mode == IDLE);
-                if (idle && issued < avail)
-                {
-                    uint32_t cand = issued + lane_rank(idle);
-                    issued = min(avail, issued + (uint32_t)__popcll(idle));
-                    if (mode == IDLE && cand < avail)
-                    {
-                        r = ao_ray(P, recs, cand, S, cur_slot, cur_s);
-                        best_t = FMAX; best_prim = 0; steps = 0; max_t = P.radius; any = true;
-                        st.reset(); st.push(P.root);
-                        mode = AORAY;
-                        rays_total += 1;
-                    }
-                }
-                // 3. done when nothing is in flight and nothing is left to hand out
-                if (__ballot(mode != IDLE) == 0ull && pending == 0u && issued >= avail) break;
-                // 4. one traversal step for every busy lane (same code for both ray kinds)
-                const bool busy = mode != IDLE;
-                if (mode != IDLE)
-                {
-                    int rc = (P.fast_ok && __ballot(!finite_ray(r)) == 0ull)
-                        ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit)
-                        : ray_step<KIND, COUNT, false>(P.pairs, P.prims, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit);
-                    if (rc != 0)
-                    {
-                        if (mode == PRIMARY)
-                        {
-                            my_hit = best_t != FMAX;
-                            my_prim = my_hit ? best_prim : 0xFFFFFFFFu;
-                            my_t = my_hit ? best_t : -1.0f;
-                            just_done = true;
-                        }
-                        else if (rc > 0)
-                        {
-                            atomicOr(&masks[cur_slot], 1u << cur_s);
-                        }
-                        mode = IDLE;
-                    }
-                }
-                if (COUNT) count_wave(cnt, busy);
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (valid)
-            {
-                float4 color = make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
-                uint32_t occ_mask = 0;
-                if (my_hit)
-                {
-                    occ_mask = masks[my_slot];
+                    const uint32_t k = slot_px[parD * 64u + lane];
+                    const uint32_t m = masks[parD * 64u + lane];
+                    uint32_t x, y, orow;
+                    tile_pixel(P, tileD, k, x, y, orow);
                     float clr = 1.0f;
                     const float step = 1.0f / (float)S;
                     for (uint32_t s2 = 0; s2 < S; ++s2)
-                        if ((occ_mask >> s2) & 1u) clr = clr - step;     // ao/main.cpp:234-238
-                    color = make_float4(clr, clr, clr, 1.0f);
-                    hits_total += 1;
+                        if ((m >> s2) & 1u) clr = clr - step;                 // ao/main.cpp:234-238
+                    const size_t o = (size_t)orow * P.width + x;
+                    if (P.color) P.color[o] = make_float4(clr, clr, clr, 1.0f);
+                    if (P.occ) P.occ[o] = (uint8_t)m;
                 }
-                size_t o = (size_t)orow * P.width + x;
-                if (P.color) P.color[o] = color;
-                if (P.prim_id) P.prim_id[o] = my_prim;
-                if (P.t) P.t[o] = my_t;
-                if (P.occ) P.occ[o] = (uint8_t)occ_mask;
+                __builtin_amdgcn_wave_barrier();
+                tileD = NONE;
             }
-            __builtin_amdgcn_wave_barrier();
+            // 2. the current tile has handed out all its rays: it drains, the next tile starts
+            if (tileC != NONE && tileD == NONE && handedC >= 64u && pendC == 0u && issC >= pubC * S)
+            {
+                tileD = tileC; parD = parC; slotsD = pubC;
+                tileC = next_tile(P, tq, lane);
+                parC ^= 1u;
+                handedC = 0; pendC = 0; pubC = 0; issC = 0;
+            }
+            // 3. hand out rays to idle lanes: the current tile's AO rays, then its primaries
+            uint64_t idle = __ballot(mode == IDLE);
+            if (idle && issC < pubC * S)
+            {
+                const uint32_t avail = pubC * S;
+                const uint32_t cand = issC + lane_rank(idle);
+                const uint32_t n = min(avail - issC, (uint32_t)__popcll(idle));
+                if (mode == IDLE && cand < avail)
+                {
+                    const uint32_t slot = cand / S, smp = cand - slot * S;
+                    uint32_t x, y, orow;
+                    tile_pixel(P, tileC, slot_px[parC * 64u + slot], x, y, orow);
+                    r = ao_ray(P, recs, slot, smp, y * P.width + x);
+                    best_t = FMAX; best_prim = 0; steps = 0; max_t = P.radius; any = true;
+                    quad = P.quad_ok && finite_ray(r);
+                    st.reset(); st.push(quad ? 0u : P.root);
+                    mode = AORAY;
+                    tag = slot | (smp << 6) | (parC << 11);
+                    rays_total += 1;
+                }
+                issC += n;
+                if (parC) inflight1 += n; else inflight0 += n;
+                idle = __ballot(mode == IDLE);
+            }
+            if (idle && tileC != NONE && handedC < 64u)
+            {
+                const uint32_t k = handedC + lane_rank(idle);
+                handedC = min(64u, handedC + (uint32_t)__popcll(idle));
+                uint32_t x, y, orow;
+                bool started = false;
+                if (mode == IDLE && k < 64u && tile_pixel(P, tileC, k, x, y, orow))
+                {
+                    r = primary_ray(P, x, y);
+                    best_t = FMAX; best_prim = 0; steps = 0; max_t = FMAX; any = false; quad = false;
+                    st.reset(); st.push(P.root);
+                    mode = PRIMARY;
+                    tag = k;
+                    rays_total += 1;
+                    started = true;
+                }
+                pendC += (uint32_t)__popcll(__ballot(started));
+            }
+            const bool busy = mode != IDLE;
+            if (__ballot(busy) == 0ull)
+            {
+                if (tileC == NONE && tileD == NONE) break;
+                continue;
+            }
+            // 4. one traversal step for every busy lane (same code for both ray kinds)
+            int rc = 0;
+            if (busy)
+            {
+                rc = (P.fast_ok && __ballot(!finite_ray(r)) == 0ull)
+                    ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit)
+                    : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit);
+            }
+            if (COUNT) count_wave(cnt, busy);
+            // 5. finished AO rays: record occlusion, retire from their tile's in-flight count
+            const bool ao_done = mode == AORAY && rc != 0;
+            if (ao_done && rc > 0) atomicOr(&masks[(tag >> 11) * 64u + (tag & 63u)], 1u << ((tag >> 6) & 31u));
+            inflight0 -= (uint32_t)__popcll(__ballot(ao_done && (tag >> 11) == 0u));
+            inflight1 -= (uint32_t)__popcll(__ballot(ao_done && (tag >> 11) != 0u));
+            // 6. finished primaries: write prim id / t (and a miss's colour), publish hits as slots
+            const bool pr_done = mode == PRIMARY && rc != 0;
+            const uint64_t fin = __ballot(pr_done);
+            if (fin)
+            {
+                const bool hit = pr_done && best_t != FMAX;
+                const uint64_t hfin = __ballot(hit);
+                if (pr_done)
+                {
+                    uint32_t x, y, orow;
+                    tile_pixel(P, tileC, tag, x, y, orow);
+                    const size_t o = (size_t)orow * P.width + x;
+                    if (P.prim_id) P.prim_id[o] = hit ? best_prim : 0xFFFFFFFFu;
+                    if (P.t) P.t[o] = hit ? best_t : -1.0f;
+                    if (hit)
+                    {
+                        const uint32_t slot = pubC + lane_rank(hfin);
+                        const f3 pos = r.ori + r.dir * best_t;                   // ao/main.cpp:202
+                        const float4 nn = P.normals[best_prim];                  // get_normal.h:26-37
+                        float* rec = recs + slot * AO_REC_WORDS;
+                        rec[0] = pos.x; rec[1] = pos.y; rec[2] = pos.z;
+                        rec[3] = nn.x; rec[4] = nn.y; rec[5] = nn.z;
+                        masks[parC * 64u + slot] = 0u;
+                        slot_px[parC * 64u + slot] = (uint8_t)tag;
+                    }
+                    else
+                    {
+                        if (P.color) P.color[o] = bg;
+                        if (P.occ) P.occ[o] = 0;
+                    }
+                }
+                pubC += (uint32_t)__popcll(hfin);
+                pendC -= (uint32_t)__popcll(fin);
+                hits_total += hit ? 1 : 0;
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            }
+            if (rc != 0) mode = IDLE;
         }
     }
 
@@ -351,6 +385,262 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             atomicAdd(P.counters + 3, b);
             atomicAdd(P.counters + 4, q);
             atomicAdd(P.counters + 6, (unsigned long long)cnt.w_steps);    // wave-uniform values
+            atomicAdd(P.counters + 7, (unsigned long long)cnt.w_busy);
+            atomicAdd(P.counters + 9, (unsigned long long)cnt.w_box);
+            atomicAdd(P.counters + 10, (unsigned long long)cnt.w_prim);
+        }
+    }
+}
+
+// ITEM schedule: the same ray streams as render_unified_kernel (two tiles in flight for AO), but
+// a wave iterates on single traversal items (item_step: one node pair or one primitive per lane)
+// instead of whole descend-to-leaf steps.  The vector-memory unit charges every wave-level load
+// instruction whatever its active lanes, so what counts is how many lanes share each one: a lane
+// that has reached a leaf tests its primitives while its neighbours are still descending.
+// Finished rays are retired and idle lanes refilled only once at least P.refill_min lanes are
+// free (or none is busy), so the ray-generation code runs with many lanes at once.
+template <int KIND, bool AO, bool COUNT, int OCC, bool VOTE>
+__global__ __launch_bounds__(256, OCC) void render_item_kernel(render_params P)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = tid >> 6;
+    const uint32_t block = blockDim.x;
+
+    lds_stack st;
+    st.mem = smem;
+    st.base = tid;
+    st.stride = block;
+    st.top = tid;
+    st.end = tid + P.stack_cap * block;
+    uint32_t* ao_area = smem + P.stack_cap * block + wave * AO_WAVE_WORDS;
+    float* recs = reinterpret_cast<float*>(ao_area);
+    uint32_t* masks = ao_area + AO_MASKS;
+    uint8_t* slot_px = reinterpret_cast<uint8_t*>(ao_area + AO_SLOT_PX);
+    test_counts cnt = {};
+    uint64_t rays_total = 0, hits_total = 0;
+
+    // lane state: mode = ray kind (PRIMARY / AORAY) | DONE once finished and not yet retired
+    constexpr uint32_t IDLE = 0, PRIMARY = 1, AORAY = 2, DONE = 4;
+    uint32_t mode = IDLE;
+    ray_t r;
+    float best_t = FMAX, max_t = FMAX;
+    uint32_t best_prim = 0, steps = 0, item = 0;
+    uint32_t tag = 0;        // PRIMARY: pixel lane k of tile C; AORAY: slot | s << 6 | parity << 11
+    bool any = false, occl = false, finite = true;
+
+    const uint32_t S = AO ? P.samples : 1u;
+    const float4 bg = make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
+    tile_queue tq = queue_init(P);
+    uint32_t tileC = next_tile(P, tq, lane), parC = 0;
+    uint32_t handedC = 0, pendC = 0, pubC = 0, issC = 0;
+    uint32_t tileD = NONE, parD = 0, slotsD = 0;
+    uint32_t inflight0 = 0, inflight1 = 0;
+
+    for (;;)
+    {
+        uint64_t busy = __ballot(mode == PRIMARY || mode == AORAY);
+        if (busy == 0ull || 64u - (uint32_t)__popcll(busy) >= P.refill_min)
+        {
+            // ---- A1. retire finished rays ------------------------------------------------------
+            if constexpr (AO)
+            {
+                const bool ao_done = mode == (AORAY | DONE);
+                if (ao_done && occl) atomicOr(&masks[(tag >> 11) * 64u + (tag & 63u)], 1u << ((tag >> 6) & 31u));
+                inflight0 -= (uint32_t)__popcll(__ballot(ao_done && (tag >> 11) == 0u));
+                inflight1 -= (uint32_t)__popcll(__ballot(ao_done && (tag >> 11) != 0u));
+            }
+            const bool pr_done = mode == (PRIMARY | DONE);
+            const uint64_t fin = __ballot(pr_done);
+            if (fin)
+            {
+                const bool hit = pr_done && best_t != FMAX;
+                const uint64_t hfin = __ballot(hit);
+                if (pr_done)
+                {
+                    // AO: tile C is still the primary's tile (it cannot drain while primaries are
+                    // pending); primary only: tile C may have moved on, the lane kept its pixel
+                    size_t o = tag;
+                    if constexpr (AO)
+                    {
+                        uint32_t x, y, orow;
+                        tile_pixel(P, tileC, tag, x, y, orow);
+                        o = (size_t)orow * P.width + x;
+                    }
+                    if (P.prim_id) P.prim_id[o] = hit ? best_prim : 0xFFFFFFFFu;
+                    if (P.t) P.t[o] = hit ? best_t : -1.0f;
+                    if (AO && hit)
+                    {
+                        const uint32_t slot = pubC + lane_rank(hfin);
+                        const f3 pos = r.ori + r.dir * best_t;                   // ao/main.cpp:202
+                        const float4 nn = P.normals[best_prim];                  // get_normal.h:26-37
+                        float* rec = recs + slot * AO_REC_WORDS;
+                        rec[0] = pos.x; rec[1] = pos.y; rec[2] = pos.z;
+                        rec[3] = nn.x; rec[4] = nn.y; rec[5] = nn.z;
+                        masks[parC * 64u + slot] = 0u;
+                        slot_px[parC * 64u + slot] = (uint8_t)tag;
+                    }
+                    else
+                    {
+                        if (P.color) P.color[o] = hit ? make_float4(1.0f, 1.0f, 1.0f, 1.0f) : bg;
+                        if (P.occ) P.occ[o] = 0;
+                    }
+                }
+                if (AO) pubC += (uint32_t)__popcll(hfin);
+                pendC -= (uint32_t)__popcll(fin);
+                hits_total += hit ? 1 : 0;
+            }
+            if (mode & DONE) mode = IDLE;
+            if constexpr (AO)
+            {
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                // ---- A2. the draining tile is done when its last AO ray is retired -------------
+                if (tileD != NONE && (parD ? inflight1 : inflight0) == 0u)
+                {
+                    if (lane < slotsD)
+                    {
+                        const uint32_t k = slot_px[parD * 64u + lane];
+                        const uint32_t m = masks[parD * 64u + lane];
+                        uint32_t x, y, orow;
+                        tile_pixel(P, tileD, k, x, y, orow);
+                        float clr = 1.0f;
+                        const float step = 1.0f / (float)S;
+                        for (uint32_t s2 = 0; s2 < S; ++s2)
+                            if ((m >> s2) & 1u) clr = clr - step;             // ao/main.cpp:234-238
+                        const size_t o = (size_t)orow * P.width + x;
+                        if (P.color) P.color[o] = make_float4(clr, clr, clr, 1.0f);
+                        if (P.occ) P.occ[o] = (uint8_t)m;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    tileD = NONE;
+                }
+                // ---- A3. the current tile has handed out every ray: it drains, the next starts -
+                if (tileC != NONE && tileD == NONE && handedC >= 64u && pendC == 0u && issC >= pubC * S)
+                {
+                    tileD = tileC; parD = parC; slotsD = pubC;
+                    tileC = next_tile(P, tq, lane);
+                    parC ^= 1u;
+                    handedC = 0; pendC = 0; pubC = 0; issC = 0;
+                }
+            }
+            else
+            {
+                if (tileC != NONE && handedC >= 64u)
+                {
+                    tileC = next_tile(P, tq, lane);
+                    handedC = 0;
+                }
+            }
+            // ---- A4. hand out rays to idle lanes: the current tile's AO rays, then primaries ---
+            uint64_t idle = __ballot(mode == IDLE);
+            if (AO && idle && issC < pubC * S)
+            {
+                const uint32_t avail = pubC * S;
+                const uint32_t cand = issC + lane_rank(idle);
+                const uint32_t n = min(avail - issC, (uint32_t)__popcll(idle));
+                if (mode == IDLE && cand < avail)
+                {
+                    const uint32_t slot = cand / S, smp = cand - slot * S;
+                    uint32_t x, y, orow;
+                    tile_pixel(P, tileC, slot_px[parC * 64u + slot], x, y, orow);
+                    r = ao_ray(P, recs, slot, smp, y * P.width + x);
+                    best_t = FMAX; best_prim = 0; steps = 0; max_t = P.radius; any = true; occl = false;
+                    item = P.root; st.reset();
+                    finite = finite_ray(r);
+                    mode = AORAY;
+                    tag = slot | (smp << 6) | (parC << 11);
+                    rays_total += 1;
+                }
+                issC += n;
+                if (parC) inflight1 += n; else inflight0 += n;
+                idle = __ballot(mode == IDLE);
+            }
+            if (idle && tileC != NONE && handedC < 64u)
+            {
+                const uint32_t k = handedC + lane_rank(idle);
+                handedC = min(64u, handedC + (uint32_t)__popcll(idle));
+                uint32_t x, y, orow;
+                bool started = false;
+                if (mode == IDLE && k < 64u && tile_pixel(P, tileC, k, x, y, orow))
+                {
+                    r = primary_ray(P, x, y);
+                    best_t = FMAX; best_prim = 0; steps = 0; max_t = FMAX; any = false; occl = false;
+                    item = P.root; st.reset();
+                    finite = finite_ray(r);
+                    mode = PRIMARY;
+                    tag = AO ? k : orow * P.width + x;
+                    rays_total += 1;
+                    started = true;
+                }
+                pendC += (uint32_t)__popcll(__ballot(started));
+            }
+            busy = __ballot(mode == PRIMARY || mode == AORAY);
+            if (busy == 0ull)
+            {
+                if (tileC == NONE && tileD == NONE) break;
+                continue;
+            }
+        }
+        // ---- B. one traversal item for every busy lane -------------------------------------------
+        const bool my_busy = mode == PRIMARY || mode == AORAY;
+        if constexpr (VOTE)
+        {
+            // the wave runs the node step or the primitive step, whichever more lanes wait for
+            // (weighted by P.vote_leaf / 8): lanes of the other kind keep their item meanwhile
+            const bool my_leaf = (item & LEAF_BIT) != 0u;
+            const uint32_t nl = (uint32_t)__popcll(__ballot(my_busy && my_leaf));
+            const uint32_t nn = (uint32_t)__popcll(__ballot(my_busy && !my_leaf));
+            const bool leaf_turn = nn == 0u || nl * P.vote_leaf >= nn * 8u;
+            bool done = false;
+            if (leaf_turn)
+            {
+                if (my_busy && my_leaf)
+                    done = prim_step<KIND, COUNT>(P.prims, r, max_t, any, st, item, best_t, best_prim, occl, cnt, steps, P.step_limit);
+            }
+            else
+            {
+                const bool fast = P.fast_ok && __ballot(my_busy && !my_leaf && !finite) == 0ull;
+                if (my_busy && !my_leaf)
+                    done = fast ? node_step<COUNT, true>(P.pairs, r, max_t, st, item, best_t, cnt, steps, P.step_limit)
+                                : node_step<COUNT, false>(P.pairs, r, max_t, st, item, best_t, cnt, steps, P.step_limit);
+            }
+            if (done) mode |= DONE;
+        }
+        else
+        {
+            const bool fast = P.fast_ok && __ballot(my_busy && !finite) == 0ull;
+            if (my_busy)
+            {
+                const bool done = fast
+                    ? item_step<KIND, COUNT, true>(P.pairs, P.prims, r, max_t, any, st, item, best_t, best_prim, occl, cnt, steps, P.step_limit)
+                    : item_step<KIND, COUNT, false>(P.pairs, P.prims, r, max_t, any, st, item, best_t, best_prim, occl, cnt, steps, P.step_limit);
+                if (done) mode |= DONE;
+            }
+        }
+        if (COUNT) count_wave(cnt, my_busy);
+    }
+
+    unsigned long long rr = rays_total, hh = hits_total, b = cnt.box, q = cnt.prim;
+    for (int off = 32; off > 0; off >>= 1)
+    {
+        rr += __shfl_down(rr, off);
+        hh += __shfl_down(hh, off);
+        if (COUNT) { b += __shfl_down(b, off); q += __shfl_down(q, off); }
+    }
+    if (__ballot(cnt.aborted) != 0ull && lane == 0) atomicOr(P.counters + 5, 1ull);
+    if (lane == 0)
+    {
+        atomicAdd(P.counters + 1, rr);
+        atomicAdd(P.counters + 2, hh);
+        atomicAdd(P.counters + COUNTERS_TOTAL, rr);
+        atomicAdd(P.counters + COUNTERS_TOTAL + 1, hh);
+        if (COUNT)
+        {
+            atomicAdd(P.counters + 3, b);
+            atomicAdd(P.counters + 4, q);
+            atomicAdd(P.counters + 6, (unsigned long long)cnt.w_steps);
             atomicAdd(P.counters + 7, (unsigned long long)cnt.w_busy);
             atomicAdd(P.counters + 9, (unsigned long long)cnt.w_box);
             atomicAdd(P.counters + 10, (unsigned long long)cnt.w_prim);
@@ -398,24 +688,34 @@ __global__ void unshard_kernel(unshard_params u)
 using kernel_fn = void (*)(render_params);
 
 template <int KIND, int OCC>
-static kernel_fn pick_occ(bool ao, bool count)
+static kernel_fn pick_occ(bool ao, bool count, int sched)
 {
+    if (sched == 1)
+    {
+        if (!ao) return count ? dev::render_item_kernel<KIND, false, true, OCC, false> : dev::render_item_kernel<KIND, false, false, OCC, false>;
+        return count ? dev::render_item_kernel<KIND, true, true, OCC, false> : dev::render_item_kernel<KIND, true, false, OCC, false>;
+    }
+    if (sched == 2)
+    {
+        if (!ao) return count ? dev::render_item_kernel<KIND, false, true, OCC, true> : dev::render_item_kernel<KIND, false, false, OCC, true>;
+        return count ? dev::render_item_kernel<KIND, true, true, OCC, true> : dev::render_item_kernel<KIND, true, false, OCC, true>;
+    }
     if (!ao) return count ? dev::render_unified_kernel<KIND, false, true, OCC> : dev::render_unified_kernel<KIND, false, false, OCC>;
     return count ? dev::render_unified_kernel<KIND, true, true, OCC> : dev::render_unified_kernel<KIND, true, false, OCC>;
 }
 
 template <int KIND>
-static kernel_fn pick(bool ao, bool count, int occ)
+static kernel_fn pick(bool ao, bool count, int occ, int sched)
 {
-    if (occ == 8) return pick_occ<KIND, 8>(ao, count);
-    if (occ == 6) return pick_occ<KIND, 6>(ao, count);
-    return pick_occ<KIND, 1>(ao, count);
+    if (occ == 8) return pick_occ<KIND, 8>(ao, count, sched);
+    if (occ == 6) return pick_occ<KIND, 6>(ao, count, sched);
+    return pick_occ<KIND, 1>(ao, count, sched);
 }
 
 static kernel_fn select_variant(const launch_config& c)
 {
-    return c.kind == dev::KIND_TRI ? pick<dev::KIND_TRI>(c.ao, c.count, c.occ)
-                                   : pick<dev::KIND_SPHERE>(c.ao, c.count, c.occ);
+    return c.kind == dev::KIND_TRI ? pick<dev::KIND_TRI>(c.ao, c.count, c.occ, c.sched)
+                                   : pick<dev::KIND_SPHERE>(c.ao, c.count, c.occ, c.sched);
 }
 
 size_t render_lds_bytes(const launch_config& c)

@@ -55,7 +55,7 @@ struct vrh_ctx
     vrh_frame_stats last{};
     bool have_frame = false;
     // tuning options (0 = automatic), vrh_ctx_set_option
-    int opt_block = 0, opt_stack = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0;
+    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_vote = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0;
 };
 
 struct vrh_scene
@@ -64,7 +64,9 @@ struct vrh_scene
     float4* pairs = nullptr;
     float4* prims = nullptr;
     float4* normals = nullptr;
+    float4* quads = nullptr;     // 4-wide any-hit records (vrh_quad.cpp), null if the scene has none
     uint32_t root = 0;
+    uint32_t quad_depth = 0;
     bool finite_bounds = true;   // every node bound finite (enables the hardware min/max slab path)
     vrh_scene_info info{};
 };
@@ -165,7 +167,10 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
         VRH_CHECK(value % 64 == 0, "vrh_ctx_set_option: block threads must be a multiple of 64");
         ctx->opt_block = int(value); break;
     case VRH_OPT_STACK_CAP: ctx->opt_stack = int(value); break;
-    case VRH_OPT_AO_SCHEDULE: VRH_CHECK(value == 0 || value == 3, "vrh_ctx_set_option: the only AO schedule is 3 (unified)"); break;
+    case VRH_OPT_AO_SCHEDULE: VRH_CHECK(value == 0 || (value >= 3 && value <= 5), "vrh_ctx_set_option: schedule is 3 (step), 4 (item) or 5 (vote)"); ctx->opt_sched = int(value); break;
+    case VRH_OPT_WIDE_ANYHIT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: wide any-hit is 1 (on) or 2 (off)"); ctx->opt_wide = int(value); break;
+    case VRH_OPT_VOTE_LEAF: VRH_CHECK(value <= 64, "vrh_ctx_set_option: vote weight is 1..64"); ctx->opt_vote = int(value); break;
+    case VRH_OPT_REFILL_MIN: VRH_CHECK(value <= 64, "vrh_ctx_set_option: refill threshold is 1..64"); ctx->opt_refill = int(value); break;
     case VRH_OPT_BLOCKS_PER_CU: ctx->opt_bpc = int(value); break;
     case VRH_OPT_WAVES_PER_SIMD: VRH_CHECK(value == 0 || value == 1 || value == 6 || value == 8, "vrh_ctx_set_option: waves per SIMD is 1, 6 or 8"); ctx->opt_occ = int(value); break;
     case VRH_OPT_EXACT_MINMAX: ctx->opt_exact_minmax = value ? 1 : 0; break;
@@ -277,6 +282,10 @@ VRH_API int vrh_scene_upload(vrh_ctx* ctx, const void* nodes_v, uint32_t num_nod
         for (int a = 0; a < 3; ++a)
             finite_bounds = finite_bounds && std::isfinite(nodes[i].bmin[a]) && std::isfinite(nodes[i].bmax[a]);
 
+    std::vector<float> quads;
+    uint32_t quad_root = 0, quad_depth = 0;
+    const bool have_quads = finite_bounds && build_quads(nodes, num_nodes, quads, quad_root, quad_depth);
+
     int rc = select_device(ctx);
     if (rc) return rc;
     auto* sc = new (std::nothrow) vrh_scene;
@@ -295,6 +304,16 @@ VRH_API int vrh_scene_upload(vrh_ctx* ctx, const void* nodes_v, uint32_t num_nod
     if ((e = hipMemcpy(sc->pairs, pairs.data(), pairs.size() * sizeof(float4), hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "upload pairs");
     if ((e = hipMemcpy(sc->prims, lp.data(), lp.size() * sizeof(float4), hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "upload prims");
     uint64_t bytes = pairs.size() * sizeof(float4) + lp.size() * sizeof(float4);
+    if (have_quads)
+    {
+        const size_t qb = quads.size() * sizeof(float);
+        if ((e = hipMalloc(&sc->quads, qb)) != hipSuccess) return fail(e, "hipMalloc(quads)");
+        if ((e = hipMemcpy(sc->quads, quads.data(), qb, hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "upload quads");
+        sc->quad_depth = quad_depth;
+        sc->info.wide_records = uint32_t(quads.size() / 32);
+        sc->info.wide_depth = quad_depth;
+        bytes += qb;
+    }
     if (face_normals)
     {
         if ((e = hipMalloc(&sc->normals, size_t(num_prims) * sizeof(float4))) != hipSuccess) return fail(e, "hipMalloc(normals)");
@@ -325,6 +344,7 @@ VRH_API int vrh_scene_free(vrh_scene* sc)
     if (sc->pairs) (void)hipFree(sc->pairs);
     if (sc->prims) (void)hipFree(sc->prims);
     if (sc->normals) (void)hipFree(sc->normals);
+    if (sc->quads) (void)hipFree(sc->quads);
     delete sc;
     return VRH_OK;
 }
@@ -461,6 +481,10 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     lc.block = ctx->opt_block ? ctx->opt_block : 64;
     lc.stack_cap = int(cap);
     lc.occ = ctx->opt_occ ? ctx->opt_occ : 6;
+    // auto: the item loop for sphere primary visibility (short leaves of cheap tests, where the
+    // step loop's leaf iterations run at ~20 % lane utilisation), the step loop otherwise
+    if (ctx->opt_sched == 0) lc.sched = (lc.kind == 1 && !ao) ? 1 : 0;
+    else lc.sched = ctx->opt_sched == 4 ? 1 : ctx->opt_sched == 5 ? 2 : 0;
     if (render_lds_bytes(lc) > 160u * 1024u)
     {
         set_error("vrh_render: BVH depth " + std::to_string(sc->info.max_depth) + " needs more LDS stack than a CU has");
@@ -473,8 +497,12 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     render_params p{};
     p.pairs = sc->pairs; p.prims = sc->prims; p.normals = sc->normals; p.root = sc->root;
     p.step_limit = sc->info.num_nodes + sc->info.num_indices + 16u;
+    p.refill_min = ctx->opt_refill ? uint32_t(ctx->opt_refill) : 16u;
+    p.vote_leaf = ctx->opt_vote ? uint32_t(ctx->opt_vote) : 8u;
     p.stack_cap = cap;
     p.fast_ok = (sc->finite_bounds && !ctx->opt_exact_minmax) ? 1u : 0u;
+    p.quads = sc->quads;
+    p.quad_ok = (sc->quads && p.fast_ok && ctx->opt_wide == 1) ? 1u : 0u;   // auto: off (measured slower)
     std::memcpy(p.eye, cam->eye, 12); std::memcpy(p.cam_u, cam->cam_u, 12);
     std::memcpy(p.cam_v, cam->cam_v, 12); std::memcpy(p.cam_w, cam->cam_w, 12);
     p.width = cam->width; p.height = cam->height;
