@@ -155,13 +155,15 @@ enum vrh_option {
                                     min/max where provably identical, see vrh_device.h)           */
     VRH_OPT_XCD_QUEUES = 7,      /* tile queues: 1 = one per XCD with stealing, 2 = one global
                                     queue (auto: 1)                                               */
-    VRH_OPT_REFILL_MIN = 8,      /* item loops: free lanes (1..64) before rays are retired and idle
-                                    lanes refilled (auto: 16)                                    */
+    VRH_OPT_REFILL_MIN = 8,      /* free lanes (1..64) before finished rays are retired and idle
+                                    lanes refilled (auto: 32 step loop, 16 item loops)           */
     VRH_OPT_VOTE_LEAF = 9,       /* vote loop: primitive step when 8 x leaf lanes >= this x node
                                     lanes (1..64, auto: 8 = simple majority)                     */
-    VRH_OPT_WIDE_ANYHIT = 10     /* 4-wide node records for any-hit (AO) rays (step loop): 1 = on
+    VRH_OPT_WIDE_ANYHIT = 10,    /* 4-wide node records for any-hit (AO) rays (step loop): 1 = on
                                     when the BVH passes the containment check, 2 = off (auto: off,
                                     measured 6 % slower on hf1M AO than the binary records)      */
+    VRH_OPT_DESCENT_CAP = 11     /* step loop: inner visits per step before a lane's descent is
+                                    resumed in the next step (1..1024; auto: unlimited)          */
 };
 VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value);
 

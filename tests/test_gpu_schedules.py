@@ -23,8 +23,11 @@ VARIANTS = {
     "vote_leafheavy": {"ao_schedule": 5, "vote_leaf": 64},
     "step_wide": {"ao_schedule": 3, "wide_anyhit": 1},
     "step_wide_exact": {"ao_schedule": 3, "wide_anyhit": 1, "exact_minmax": 1},
+    "step_cap1": {"ao_schedule": 3, "descent_cap": 1},
+    "step_refill24": {"ao_schedule": 3, "refill_min": 24},
+    "step_cap3_wide": {"ao_schedule": 3, "descent_cap": 3, "wide_anyhit": 1},
 }
-OPTIONS = ("ao_schedule", "refill_min", "vote_leaf", "wide_anyhit", "exact_minmax")
+OPTIONS = ("ao_schedule", "refill_min", "vote_leaf", "wide_anyhit", "exact_minmax", "descent_cap")
 
 
 @pytest.fixture(params=sorted(VARIANTS))

@@ -19,10 +19,11 @@ scene = sys.argv[1] if len(sys.argv) > 1 else "hf1M"
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 VARIANTS = json.loads(os.environ.get("VRH_AB", "null")) or [
     {"name": "default"},
-    {"name": "binary any-hit", "wide_anyhit": 2},
-    {"name": "occ1", "waves_per_simd": 1},
-    {"name": "occ8", "waves_per_simd": 8},
-    {"name": "item r24", "ao_schedule": 4, "refill_min": 24},
+    {"name": "refill 2", "refill_min": 2},
+    {"name": "refill 4", "refill_min": 4},
+    {"name": "refill 8", "refill_min": 8},
+    {"name": "refill 16", "refill_min": 16},
+    {"name": "refill 24", "refill_min": 24},
 ]
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 log = open(os.path.join(ROOT, "gpurun_out", f"ab_{scene}.log"), "a", buffering=1)
@@ -62,6 +63,7 @@ for rnd in range(rounds):
         ctx.set_option("refill_min", v.get("refill_min", 0))
         ctx.set_option("vote_leaf", v.get("vote_leaf", 0))
         ctx.set_option("wide_anyhit", v.get("wide_anyhit", 0))
+        ctx.set_option("descent_cap", v.get("descent_cap", 0))
         ctx.stats_reset()
         for _ in range(5):
             va.render(ctx, dev, rt, basis, kern)

@@ -8,15 +8,14 @@ mkdir -p $OUTD
 run() {  # name, counters...
   local name=$1; shift
   echo "== pass $name: $*"
-  timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d $OUTD/$name -o run -- python3 tools/frame_driver.py $SCENE $FRAMES $KIND > $OUTD/$name.log 2>&1
+  timeout -k 10 120 rocprofv3 --pmc "$@" --output-format csv -d $OUTD/$name -o run -- python3 tools/frame_driver.py $SCENE $FRAMES $KIND > $OUTD/$name.log 2>&1
   local rc=$?; tail -2 $OUTD/$name.log; echo "rc=$rc"
   case $rc in 124|134|137|139) exit $rc;; esac
 }
+run vmem SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_VMEM
 run ta TA_BUSY_avr TA_TA_BUSY_sum TA_FLAT_READ_WAVEFRONTS_sum GRBM_GUI_ACTIVE
 run ta2 TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum
-run td TD_TD_BUSY_sum TD_TC_STALL_sum TD_LOAD_WAVEFRONT_sum
 run tcp TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum
 run tcp2 TCP_PENDING_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum
-run vmem SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_VMEM
 run vmem2 SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_BUSY_CU_CYCLES
 exit 0

@@ -159,7 +159,8 @@ class Context:
                  "ao_schedule": capi.VRH_OPT_AO_SCHEDULE, "blocks_per_cu": capi.VRH_OPT_BLOCKS_PER_CU,
                  "waves_per_simd": capi.VRH_OPT_WAVES_PER_SIMD, "exact_minmax": capi.VRH_OPT_EXACT_MINMAX,
                  "xcd_queues": capi.VRH_OPT_XCD_QUEUES, "refill_min": capi.VRH_OPT_REFILL_MIN,
-                 "vote_leaf": capi.VRH_OPT_VOTE_LEAF, "wide_anyhit": capi.VRH_OPT_WIDE_ANYHIT}
+                 "vote_leaf": capi.VRH_OPT_VOTE_LEAF, "wide_anyhit": capi.VRH_OPT_WIDE_ANYHIT,
+                 "descent_cap": capi.VRH_OPT_DESCENT_CAP}
         capi.check("vrh_ctx_set_option", self.handle, names.get(option, option), int(value))
 
     def last_frame_stats(self):

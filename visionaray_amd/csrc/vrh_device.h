@@ -198,6 +198,7 @@ __device__ __forceinline__ void count_wave(test_counts& c, bool busy)
 }
 
 constexpr uint32_t QUAD_NONE = 0xFFFFFFFFu;
+constexpr uint32_t NO_RESUME = 0xFFFFFFFFu;   // ray_step: no descent to resume
 
 // One entry of a 4-wide any-hit record (vrh_quad.cpp): the box test of update_if.h:60-66 with
 // best_t = max() (an any-hit ray has no hit yet while it traverses), hardware min/max (the lane's
@@ -222,6 +223,7 @@ __device__ __forceinline__ bool quad_entry(float xl, float yl, float zl, float x
 // modes and still run the same instruction stream.  Returns 1 = any-hit found, -1 = ray finished
 // (stack empty), 0 = continue.
 //
+// `resume` / `cap`: see the binary descent loop below (cap = ~0u: descend to the leaf in one call).
 // `quad` lanes (any-hit rays with a finite ray, scene with 4-wide records) descend the 4-wide
 // records instead: the same set of leaves is reached (vrh_quad.cpp), the order does not matter
 // for an any-hit result, and the nearest hit entry is descended first.  If a record's hits could
@@ -231,13 +233,22 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
                                         const float4* __restrict__ quads, uint32_t root, bool& quad,
                                         const ray_t& r, float max_t, bool any, lds_stack& st,
                                         float& best_t, uint32_t& best_prim, test_counts& cnt,
-                                        uint32_t& steps, uint32_t step_limit)
+                                        uint32_t& steps, uint32_t step_limit, uint32_t& resume, uint32_t cap)
 {
     // the tree was validated at upload (no cycles, links in range), so the descent terminates;
     // the guard below only bounds the number of outer iterations per ray
-    if (st.empty()) return -1;
-    if (++steps > step_limit) { cnt.aborted = true; return -1; }
-    uint32_t link = st.pop();
+    uint32_t link;
+    if (resume != NO_RESUME)
+    {
+        link = resume;
+        resume = NO_RESUME;
+    }
+    else
+    {
+        if (st.empty()) return -1;
+        if (++steps > step_limit) { cnt.aborted = true; return -1; }
+        link = st.pop();
+    }
     if (quad)
     {
         while (!(link & LEAF_BIT))
@@ -272,8 +283,11 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
             link = j == 0u ? k0 : j == 1u ? k1 : j == 2u ? k2 : k3;
         }
     }
-    else while (!(link & LEAF_BIT))
+    else for (uint32_t it = cap; !(link & LEAF_BIT); --it)
     {
+        // at most `cap` inner visits per call: a lane still descending keeps its node in `resume`
+        // and continues next call, so one long descent does not hold the whole wave
+        if (it == 0u) { resume = link; return 0; }
         const float4* p = pairs + 4u * link;
         const float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
         bool b0, b1;

@@ -45,6 +45,7 @@ struct render_params
     uint32_t xcd_queues;      // 1: per-XCD tile queues with stealing; 0: one global queue
     uint32_t refill_min;      // item schedule: retire / refill once this many lanes are free
     uint32_t vote_leaf;       // vote schedule: leaf step when 8 * leaf lanes >= vote_leaf * node lanes
+    uint32_t descent_cap;     // step loop: inner visits per step before a descent is resumed later
 };
 
 constexpr int COUNTERS_FRAME = 80;      // u64 words reset before every frame

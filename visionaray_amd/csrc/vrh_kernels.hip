@@ -152,6 +152,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     float best_t = FMAX, max_t = FMAX;
     uint32_t best_prim = 0, steps = 0;
     bool any = false, quad = false;
+    uint32_t resume = NO_RESUME;
 
     if constexpr (!AO)
     {
@@ -182,7 +183,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                             r = primary_ray(P, x, y);
                             out_o = orow * P.width + x;
                             best_t = FMAX; best_prim = 0; steps = 0;
-                            st.reset(); st.push(P.root);
+                            st.reset(); st.push(P.root); resume = NO_RESUME;
                             mode = PRIMARY;
                             rays_total += 1;
                         }
@@ -198,8 +199,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             if (mode != IDLE)
             {
                 int rc = (P.fast_ok && __ballot(!finite_ray(r)) == 0ull)
-                    ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit)
-                    : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit);
+                    ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap)
+                    : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap);
                 if (rc != 0)
                 {
                     bool hit = best_t != FMAX;
@@ -262,8 +263,11 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 parC ^= 1u;
                 handedC = 0; pendC = 0; pubC = 0; issC = 0;
             }
-            // 3. hand out rays to idle lanes: the current tile's AO rays, then its primaries
+            // 3. hand out rays to idle lanes: the current tile's AO rays, then its primaries --
+            //    once P.refill_min lanes are idle (or none is busy), so ray generation runs with
+            //    many lanes at once
             uint64_t idle = __ballot(mode == IDLE);
+            if ((uint32_t)__popcll(idle) < P.refill_min && idle != ~0ull) idle = 0ull;
             if (idle && issC < pubC * S)
             {
                 const uint32_t avail = pubC * S;
@@ -277,7 +281,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     r = ao_ray(P, recs, slot, smp, y * P.width + x);
                     best_t = FMAX; best_prim = 0; steps = 0; max_t = P.radius; any = true;
                     quad = P.quad_ok && finite_ray(r);
-                    st.reset(); st.push(quad ? 0u : P.root);
+                    st.reset(); st.push(quad ? 0u : P.root); resume = NO_RESUME;
                     mode = AORAY;
                     tag = slot | (smp << 6) | (parC << 11);
                     rays_total += 1;
@@ -296,7 +300,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 {
                     r = primary_ray(P, x, y);
                     best_t = FMAX; best_prim = 0; steps = 0; max_t = FMAX; any = false; quad = false;
-                    st.reset(); st.push(P.root);
+                    st.reset(); st.push(P.root); resume = NO_RESUME;
                     mode = PRIMARY;
                     tag = k;
                     rays_total += 1;
@@ -315,8 +319,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             if (busy)
             {
                 rc = (P.fast_ok && __ballot(!finite_ray(r)) == 0ull)
-                    ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit)
-                    : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit);
+                    ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap)
+                    : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap);
             }
             if (COUNT) count_wave(cnt, busy);
             // 5. finished AO rays: record occlusion, retire from their tile's in-flight count

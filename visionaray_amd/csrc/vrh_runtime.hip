@@ -55,7 +55,7 @@ struct vrh_ctx
     vrh_frame_stats last{};
     bool have_frame = false;
     // tuning options (0 = automatic), vrh_ctx_set_option
-    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_vote = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0;
+    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_vote = 0, opt_dcap = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0;
 };
 
 struct vrh_scene
@@ -169,6 +169,7 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
     case VRH_OPT_STACK_CAP: ctx->opt_stack = int(value); break;
     case VRH_OPT_AO_SCHEDULE: VRH_CHECK(value == 0 || (value >= 3 && value <= 5), "vrh_ctx_set_option: schedule is 3 (step), 4 (item) or 5 (vote)"); ctx->opt_sched = int(value); break;
     case VRH_OPT_WIDE_ANYHIT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: wide any-hit is 1 (on) or 2 (off)"); ctx->opt_wide = int(value); break;
+    case VRH_OPT_DESCENT_CAP: ctx->opt_dcap = int(value); break;
     case VRH_OPT_VOTE_LEAF: VRH_CHECK(value <= 64, "vrh_ctx_set_option: vote weight is 1..64"); ctx->opt_vote = int(value); break;
     case VRH_OPT_REFILL_MIN: VRH_CHECK(value <= 64, "vrh_ctx_set_option: refill threshold is 1..64"); ctx->opt_refill = int(value); break;
     case VRH_OPT_BLOCKS_PER_CU: ctx->opt_bpc = int(value); break;
@@ -497,8 +498,9 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     render_params p{};
     p.pairs = sc->pairs; p.prims = sc->prims; p.normals = sc->normals; p.root = sc->root;
     p.step_limit = sc->info.num_nodes + sc->info.num_indices + 16u;
-    p.refill_min = ctx->opt_refill ? uint32_t(ctx->opt_refill) : 16u;
+    p.refill_min = ctx->opt_refill ? uint32_t(ctx->opt_refill) : (lc.sched == 0 ? 32u : 16u);   // measured (profiles/r01_ab)
     p.vote_leaf = ctx->opt_vote ? uint32_t(ctx->opt_vote) : 8u;
+    p.descent_cap = ctx->opt_dcap ? uint32_t(ctx->opt_dcap) : 0xFFFFFFFFu;
     p.stack_cap = cap;
     p.fast_ok = (sc->finite_bounds && !ctx->opt_exact_minmax) ? 1u : 0u;
     p.quads = sc->quads;
