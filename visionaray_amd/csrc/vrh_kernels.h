@@ -43,7 +43,8 @@ struct render_params
     // [COUNTERS_TOTAL + 0/1] total rays / hits since vrh_stats_reset
     unsigned long long* counters;
     uint32_t xcd_queues;      // 1: per-XCD tile queues with stealing; 0: one global queue
-    uint32_t refill_min;      // item schedule: retire / refill once this many lanes are free
+    uint32_t refill_min;      // retire / refill once this many lanes are free (AO, item loops)
+    uint32_t refill_min_primary;   // the same for the step loop's primary-only stream
     uint32_t vote_leaf;       // vote schedule: leaf step when 8 * leaf lanes >= vote_leaf * node lanes
     uint32_t descent_cap;     // step loop: inner visits per step before a descent is resumed later
 };

@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     ray_t r;
     float best_t = FMAX, max_t = FMAX;
     uint32_t best_prim = 0, steps = 0;
-    bool any = false, quad = false;
+    bool any = false, quad = false, finite = true;
     uint32_t resume = NO_RESUME;
 
     if constexpr (!AO)
@@ -164,6 +164,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         for (;;)
         {
             uint64_t idle = __ballot(mode == IDLE);
+            if ((uint32_t)__popcll(idle) < P.refill_min_primary && idle != ~0ull) idle = 0ull;
             if (idle)
             {
                 if (handed >= 64u && tile != NONE)
@@ -181,6 +182,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                         if (tile_pixel(P, tile, cand, x, y, orow))
                         {
                             r = primary_ray(P, x, y);
+                            finite = finite_ray(r);
                             out_o = orow * P.width + x;
                             best_t = FMAX; best_prim = 0; steps = 0;
                             st.reset(); st.push(P.root); resume = NO_RESUME;
@@ -198,7 +200,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             const bool busy = mode != IDLE;
             if (mode != IDLE)
             {
-                int rc = (P.fast_ok && __ballot(!finite_ray(r)) == 0ull)
+                int rc = (P.fast_ok && __ballot(!finite) == 0ull)
                     ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap)
                     : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap);
                 if (rc != 0)
@@ -280,7 +282,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     tile_pixel(P, tileC, slot_px[parC * 64u + slot], x, y, orow);
                     r = ao_ray(P, recs, slot, smp, y * P.width + x);
                     best_t = FMAX; best_prim = 0; steps = 0; max_t = P.radius; any = true;
-                    quad = P.quad_ok && finite_ray(r);
+                    finite = finite_ray(r);
+                    quad = P.quad_ok && finite;
                     st.reset(); st.push(quad ? 0u : P.root); resume = NO_RESUME;
                     mode = AORAY;
                     tag = slot | (smp << 6) | (parC << 11);
@@ -299,6 +302,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 if (mode == IDLE && k < 64u && tile_pixel(P, tileC, k, x, y, orow))
                 {
                     r = primary_ray(P, x, y);
+                    finite = finite_ray(r);
                     best_t = FMAX; best_prim = 0; steps = 0; max_t = FMAX; any = false; quad = false;
                     st.reset(); st.push(P.root); resume = NO_RESUME;
                     mode = PRIMARY;
@@ -318,7 +322,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             int rc = 0;
             if (busy)
             {
-                rc = (P.fast_ok && __ballot(!finite_ray(r)) == 0ull)
+                rc = (P.fast_ok && __ballot(!finite) == 0ull)
                     ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap)
                     : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap);
             }

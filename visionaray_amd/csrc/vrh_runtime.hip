@@ -499,6 +499,7 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     p.pairs = sc->pairs; p.prims = sc->prims; p.normals = sc->normals; p.root = sc->root;
     p.step_limit = sc->info.num_nodes + sc->info.num_indices + 16u;
     p.refill_min = ctx->opt_refill ? uint32_t(ctx->opt_refill) : (lc.sched == 0 ? 32u : 16u);   // measured (profiles/r01_ab)
+    p.refill_min_primary = ctx->opt_refill ? uint32_t(ctx->opt_refill) : 1u;
     p.vote_leaf = ctx->opt_vote ? uint32_t(ctx->opt_vote) : 8u;
     p.descent_cap = ctx->opt_dcap ? uint32_t(ctx->opt_dcap) : 0xFFFFFFFFu;
     p.stack_cap = cap;
