@@ -15,6 +15,10 @@
  *   vrh_rt_download    <- gpu_buffer_rt::display_color_buffer D2H   gpu_buffer_rt.inl:90-119
  *   vrh_sync           <- (none: cuda_sched is async) ; called by hip_buffer_rt::end_frame()
  *   vrh_build_bvh      <- build<index_bvh<P>>(prims, n)              detail/bvh/build.inl:165-178 (+ sah.h)
+ *   vrh_shading_create <- make_kernel_params(binding, prims, normals, materials, lights, ...)
+ *                                                                     kernels.h:357-389 (device copies of
+ *                         the material / light arrays, as viewer.cpp:501-523 uploads them)
+ *   VRH_KERNEL_SIMPLE  <- simple::kernel<Params>                     detail/simple.inl:19-83
  *
  * Status codes: every function returns 0 on success and never throws or longjmps across the ABI;
  * vrh_last_error() gives a thread-local message for the last failure on the calling thread.
@@ -34,6 +38,7 @@ extern "C" {
 typedef struct vrh_ctx   vrh_ctx;    /* one per GPU: device + hipStream_t + events + work counters */
 typedef struct vrh_scene vrh_scene;  /* device-resident index BVH (+ face normals)               */
 typedef struct vrh_rt    vrh_rt;     /* device render target (colour + side buffers)             */
+typedef struct vrh_shading vrh_shading; /* device materials + lights of the shading kernels       */
 
 enum vrh_status {
     VRH_OK = 0,
@@ -54,8 +59,23 @@ enum vrh_prim_kind {
 /* built-in kernels (a C ABI cannot carry an arbitrary C++ lambda; SURVEY.md §7 hard part 6) */
 enum vrh_kernel_kind {
     VRH_KERNEL_PRIMARY = 0,   /* closest_hit primary visibility: colour = hit ? 1 : bg     */
-    VRH_KERNEL_AO = 1         /* ao/main.cpp:183-246 with the Appendix-A counter sampler  */
+    VRH_KERNEL_AO = 1,        /* ao/main.cpp:183-246 with the Appendix-A counter sampler  */
+    VRH_KERNEL_SIMPLE = 2     /* simple::kernel (detail/simple.inl:19-83): closest hit, then
+                                 ambient + one plastic::shade per point light, two-sided  */
 };
+
+enum vrh_normal_binding {
+    VRH_NORMALS_PER_FACE = 0,    /* normals_per_face_binding: face normals[prim_id] (upload)  */
+    VRH_NORMALS_PER_VERTEX = 1   /* normals_per_vertex_binding: 3 per prim_id, interpolated
+                                    with the hit's barycentrics (vrh_scene_set_vertex_normals) */
+};
+
+/* plastic<float> (material.h:267-323, detail/material/plastic.inl): ambient ca * ka, lambertian
+ * diffuse cd * kd, blinn specular cs * ks with exponent exp.  Indexed by the hit's geom_id. */
+typedef struct { float ca[3]; float ka; float cd[3]; float kd; float cs[3]; float ks; float exp; } vrh_plastic;
+/* point_light<float> (point_light.h:18-66, detail/point_light.inl): intensity cl * kl with
+ * attenuation 1 / (constant + linear * d + quadratic * d * d) */
+typedef struct { float position[3]; float cl[3]; float kl; float constant_att, linear_att, quadratic_att; } vrh_point_light;
 
 enum vrh_rt_flags {
     VRH_RT_COLOR = 1u,        /* RGBA32F colour (pixel_access.h:582-604 store)             */
@@ -81,6 +101,10 @@ typedef struct {
     float    eps;             /* AO origin offset along the sample direction (1e-3)        */
     float    bg[4];           /* miss colour                                               */
     uint32_t flags;           /* vrh_kernel_flags                                          */
+    /* VRH_KERNEL_SIMPLE only (make_kernel_params arguments, kernels.h:357-389) */
+    uint32_t normal_binding;  /* vrh_normal_binding                                        */
+    float    ambient[4];      /* ambient_color (RGBA; rgb scaled by a, spectrum.inl:375)   */
+    const vrh_shading* shading;   /* materials + lights (vrh_shading_create)              */
 } vrh_kernel_desc;
 
 enum vrh_kernel_flags {
@@ -121,6 +145,9 @@ typedef struct {
     uint64_t device_bytes;    /* node pairs + leaf-ordered primitives + normals + 4-wide records */
     uint32_t wide_records;    /* 4-wide any-hit records (0: the BVH failed the containment check) */
     uint32_t wide_depth;      /* levels of the 4-wide tree                                      */
+    uint32_t max_prim_id;     /* largest prim_id / geom_id of the primitives                    */
+    uint32_t max_geom_id;
+    uint32_t vertex_normals;  /* per-vertex normals set (vrh_scene_set_vertex_normals)          */
 } vrh_scene_info;
 
 /* camera::look_at + camera::perspective (camera.inl:10-57) followed by the pinhole basis that
@@ -176,6 +203,15 @@ VRH_API int vrh_scene_upload(vrh_ctx* ctx, const void* nodes, uint32_t num_nodes
                              const void* face_normals, vrh_scene** out);
 VRH_API int vrh_scene_get_info(const vrh_scene* scene, vrh_scene_info* info);
 VRH_API int vrh_scene_free(vrh_scene* scene);
+/* per-vertex normals (vec3, 16-B stride): normals[3 * prim_id + k] for vertex k (v1, v1+e1, v1+e2),
+ * the normals_per_vertex_binding array of get_shading_normal.h:64-84 */
+VRH_API int vrh_scene_set_vertex_normals(vrh_scene* scene, const void* normals, uint32_t num_normals);
+
+/* materials (plastic, indexed by geom_id) and point lights of VRH_KERNEL_SIMPLE, copied to the
+ * device; referenced by vrh_kernel_desc.shading */
+VRH_API int vrh_shading_create(vrh_ctx* ctx, const vrh_plastic* materials, uint32_t num_materials,
+                               const vrh_point_light* lights, uint32_t num_lights, vrh_shading** out);
+VRH_API int vrh_shading_free(vrh_shading* shading);
 
 /* render targets.  vrh_rt_alloc owns its buffers (flags = vrh_rt_flags); vrh_rt_wrap borrows
  * caller device pointers (any may be NULL), e.g. torch tensors used for the RCCL gather. */

@@ -27,7 +27,13 @@ NODE_DTYPE = np.dtype([("bmin", "<f4", 3), ("first", "<u4"), ("bmax", "<f4", 3),
 assert TRI_DTYPE.itemsize == 64 and SPHERE_DTYPE.itemsize == 48 and NODE_DTYPE.itemsize == 32
 
 VO_TRI, VO_SPHERE = 0, 1
-VO_MODE_PRIMARY, VO_MODE_AO = 0, 1
+VO_MODE_PRIMARY, VO_MODE_AO, VO_MODE_SIMPLE = 0, 1, 2
+VO_NORMALS_PER_FACE, VO_NORMALS_PER_VERTEX = 0, 1
+# plastic<float> / point_light<float> parameter records (vrh_oracle.h vo_plastic / vo_point_light)
+PLASTIC_DTYPE = np.dtype([("ca", "<f4", 3), ("ka", "<f4"), ("cd", "<f4", 3), ("kd", "<f4"), ("cs", "<f4", 3),
+                          ("ks", "<f4"), ("exp", "<f4")])
+POINT_LIGHT_DTYPE = np.dtype([("position", "<f4", 3), ("cl", "<f4", 3), ("kl", "<f4"), ("constant_att", "<f4"),
+                              ("linear_att", "<f4"), ("quadratic_att", "<f4")])
 
 
 class _Bvh(C.Structure):
@@ -41,7 +47,7 @@ class _Counters(C.Structure):
 
 class _Scene(C.Structure):
     _fields_ = [("nodes", C.c_void_p), ("indices", C.c_void_p), ("prims", C.c_void_p),
-                ("kind", C.c_int), ("normals", C.c_void_p)]
+                ("kind", C.c_int), ("normals", C.c_void_p), ("vertex_normals", C.c_void_p)]
 
 
 class _Camera(C.Structure):
@@ -51,7 +57,9 @@ class _Camera(C.Structure):
 
 class _Kernel(C.Structure):
     _fields_ = [("mode", C.c_int), ("samples", C.c_int), ("radius", C.c_float), ("eps", C.c_float),
-                ("bg", C.c_float * 4)]
+                ("bg", C.c_float * 4), ("materials", C.c_void_p), ("num_materials", C.c_int),
+                ("lights", C.c_void_p), ("num_lights", C.c_int), ("ambient", C.c_float * 4),
+                ("normal_binding", C.c_int)]
 
 
 _lib = None
@@ -83,6 +91,7 @@ def lib():
                                        vp, vp, vp, vp, C.c_int]
         L.vo_render_pixels.restype = C.c_uint64
         L.vo_fnv1a.argtypes = [vp, sz, C.c_uint64]; L.vo_fnv1a.restype = C.c_uint64
+        L.vo_vertex_normals.argtypes = [vp, sz, vp]; L.vo_vertex_normals.restype = None
         _lib = L
     return _lib
 
@@ -173,6 +182,7 @@ class Scene:
     indices: np.ndarray
     normals: np.ndarray | None
     max_depth: int
+    vertex_normals: np.ndarray | None = None
 
 
 def make_scene(name):
@@ -182,12 +192,18 @@ def make_scene(name):
     return Scene(name, kind, prims, nodes, idx, normals, depth)
 
 
-def _structs(scene, cam, mode, samples=8, radius=0.1, eps=1e-3, bg=(0.1, 0.2, 0.3, 1.0)):
+def _structs(scene, cam, mode, samples=8, radius=0.1, eps=1e-3, bg=(0.1, 0.2, 0.3, 1.0), materials=None,
+             lights=None, ambient=(0.0, 0.0, 0.0, 0.0), binding=VO_NORMALS_PER_FACE):
     s = _Scene(_p(scene.nodes).value, _p(scene.indices).value, _p(scene.prims).value, scene.kind,
-               _p(scene.normals).value if scene.normals is not None else None)
+               _p(scene.normals).value if scene.normals is not None else None,
+               _p(scene.vertex_normals).value if scene.vertex_normals is not None else None)
     eye, u, v, w, W, H = cam
     c = _Camera((C.c_float * 3)(*eye), (C.c_float * 3)(*u), (C.c_float * 3)(*v), (C.c_float * 3)(*w), W, H)
-    k = _Kernel(mode, samples, radius, eps, (C.c_float * 4)(*bg))
+    k = _Kernel(mode, samples, radius, eps, (C.c_float * 4)(*bg),
+                _p(materials).value if materials is not None else None, 0 if materials is None else len(materials),
+                _p(lights).value if lights is not None else None, 0 if lights is None else len(lights),
+                (C.c_float * 4)(*ambient), binding)
+    _structs.keep = (materials, lights)
     return s, c, k
 
 
@@ -225,6 +241,51 @@ def render_pixels(scene, cam, pixels, mode=VO_MODE_AO, threads=0, **kw):
     out["rays"] = int(lib().vo_render_pixels(C.byref(s), C.byref(c), C.byref(k), _p(pixels), n, _p(out["color"]),
                                              _p(out["prim_id"]), _p(out["t"]), _p(out["occ"]), threads))
     return out
+
+
+# ---- simple::kernel shading spec (mirrors shade_spec() in oracle/ref_harness.cpp) -----------------
+
+def shade_spec():
+    """Three plastic materials (by geom_id), two point lights, ambient, background."""
+    m = np.zeros(3, PLASTIC_DTYPE)
+    m[0] = ((0.2, 0.2, 0.2), 1.0, (0.8, 0.3, 0.2), 1.0, (1.0, 1.0, 1.0), 0.4, 32.0)
+    m[1] = ((0.1, 0.1, 0.1), 0.5, (0.2, 0.7, 0.3), 0.9, (0.9, 0.9, 0.9), 0.2, 8.0)
+    m[2] = ((0.05, 0.05, 0.1), 1.0, (0.3, 0.3, 0.9), 0.7, (1.0, 0.8, 0.6), 0.6, 64.5)
+    lt = np.zeros(2, POINT_LIGHT_DTYPE)
+    lt[0] = ((0.5, 2.0, 1.5), (1.0, 1.0, 1.0), 1.0, 1.0, 0.0, 0.0)
+    lt[1] = ((-1.5, 1.0, 0.5), (1.0, 0.8, 0.6), 0.7, 1.0, 0.1, 0.05)
+    return m, lt, (0.4, 0.4, 0.4, 0.5), (0.1, 0.2, 0.3, 1.0)
+
+
+def vertex_normals(face_nrm):
+    """Deterministic per-vertex normals (3 per triangle, float4 rows) for the shading tests."""
+    face_nrm = np.ascontiguousarray(face_nrm, np.float32)
+    out = np.zeros((len(face_nrm) * 3, 4), np.float32)
+    lib().vo_vertex_normals(_p(face_nrm), len(face_nrm), _p(out))
+    return out
+
+
+def make_shade_scene(name):
+    """Triangle scene of the shading tests: geom_id = prim index % 3, face + vertex normals."""
+    kind, prims = gen_prims(name)
+    assert kind == VO_TRI
+    prims["geom_id"] = np.arange(len(prims), dtype=np.uint32) % 3
+    nodes, idx, depth = build_bvh(prims, kind)
+    fn = face_normals(prims)
+    return Scene(name, kind, prims, nodes, idx, fn, depth, vertex_normals(fn))
+
+
+def render_simple(scene, cam, binding, rows=None, threads=0):
+    m, lt, amb, bg = shade_spec()
+    return render(scene, cam, mode=VO_MODE_SIMPLE, rows=rows, threads=threads, materials=m, lights=lt,
+                  ambient=amb, bg=bg, binding=binding)
+
+
+def ref_shade(name, outdir, binding, W=None, H=None):
+    args = [REF_BIN, "shade", name, outdir, "vertex" if binding == VO_NORMALS_PER_VERTEX else "face"]
+    args += [str(W), str(H)] if W else []
+    r = subprocess.run(args, check=True, capture_output=True, text=True)
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def fnv1a(arr):

@@ -8,6 +8,12 @@
 //                                    139-151) of primary closest_hit (traverse_linear.inl:286-329) and
 //                                    the parity version of the ao/main.cpp:183-246 kernel (SURVEY.md
 //                                    Appendix A), written as raw little-endian arrays + hashes.
+//   shade  <scene> <outdir> <face|vertex> [W H]
+//                                  : simple::kernel (detail/simple.inl:19-83) through the reference's
+//                                    make_kernel_params (kernels.h:357-389), plastic<float> materials
+//                                    by geom_id (= prim index % 3) and two point lights (the spec in
+//                                    shade_spec() below, mirrored by tests/shading_spec.py), colour
+//                                    frame written as color.bin + hash.
 //   bench  <scene> <threads> <frames> [W H] [samples]
 //                                  : the reference SSE4 CPU path, tiled_sched<basic_ray<simd::float4>>
 //                                    (tiled_sched.inl:365-391) running the ao/main.cpp:183-246 kernel
@@ -21,6 +27,9 @@
 #include <visionaray/bvh.h>
 #include <visionaray/camera.h>
 #include <visionaray/get_normal.h>
+#include <visionaray/kernels.h>
+#include <visionaray/material.h>
+#include <visionaray/point_light.h>
 #include <visionaray/result_record.h>
 #include <visionaray/sampling.h>
 #include <visionaray/random_sampler.h>
@@ -324,6 +333,103 @@ static int run_golden(scene_desc const& d, aligned_vector<P>& prims, std::vector
 }
 
 //-------------------------------------------------------------------------------------------------
+// shade: simple::kernel with plastic materials and point lights
+//
+
+struct shade_spec
+{
+    aligned_vector<plastic<float>> materials;
+    aligned_vector<point_light<float>> lights;
+    vec4 ambient, bg;
+};
+
+static shade_spec make_shade_spec()
+{
+    shade_spec sp;
+    struct { float ca[3], ka, cd[3], kd, cs[3], ks, exp; } m[3] = {
+        { { 0.2f, 0.2f, 0.2f }, 1.0f, { 0.8f, 0.3f, 0.2f }, 1.0f, { 1.0f, 1.0f, 1.0f }, 0.4f, 32.0f },
+        { { 0.1f, 0.1f, 0.1f }, 0.5f, { 0.2f, 0.7f, 0.3f }, 0.9f, { 0.9f, 0.9f, 0.9f }, 0.2f, 8.0f },
+        { { 0.05f, 0.05f, 0.1f }, 1.0f, { 0.3f, 0.3f, 0.9f }, 0.7f, { 1.0f, 0.8f, 0.6f }, 0.6f, 64.5f } };
+    for (auto const& d : m)
+    {
+        plastic<float> p;
+        p.set_ca(from_rgb(vec3(d.ca[0], d.ca[1], d.ca[2])));
+        p.set_ka(d.ka);
+        p.set_cd(from_rgb(vec3(d.cd[0], d.cd[1], d.cd[2])));
+        p.set_kd(d.kd);
+        p.set_cs(from_rgb(vec3(d.cs[0], d.cs[1], d.cs[2])));
+        p.set_ks(d.ks);
+        p.set_specular_exp(d.exp);
+        sp.materials.push_back(p);
+    }
+    point_light<float> l0;
+    l0.set_position(vec3(0.5f, 2.0f, 1.5f));
+    l0.set_cl(vec3(1.0f, 1.0f, 1.0f));
+    l0.set_kl(1.0f);
+    sp.lights.push_back(l0);
+    point_light<float> l1;
+    l1.set_position(vec3(-1.5f, 1.0f, 0.5f));
+    l1.set_cl(vec3(1.0f, 0.8f, 0.6f));
+    l1.set_kl(0.7f);
+    l1.set_constant_attenuation(1.0f);
+    l1.set_linear_attenuation(0.1f);
+    l1.set_quadratic_attenuation(0.05f);
+    sp.lights.push_back(l1);
+    sp.ambient = vec4(0.4f, 0.4f, 0.4f, 0.5f);
+    sp.bg = vec4(0.1f, 0.2f, 0.3f, 1.0f);
+    return sp;
+}
+
+static int run_shade(scene_desc const& d, aligned_vector<tri_t>& prims, std::vector<vec3> const& face_normals,
+                     std::string const& outdir, bool per_vertex, int W, int H)
+{
+    for (size_t i = 0; i < prims.size(); ++i) prims[i].geom_id = unsigned(i % 3);
+    auto bvh = build<index_bvh<tri_t>>(prims.data(), prims.size());
+    using bvh_ref = typename index_bvh<tri_t>::bvh_ref;
+    std::vector<bvh_ref> bvhs{ bvh.ref() };
+    // per-vertex normals: prim k, vertex j: normalize(n_k + 0.4 * (U(b) - 0.5, ...)), b = (3k + j) * 3
+    std::vector<vec3> vnormals(prims.size() * 3);
+    for (size_t k = 0; k < prims.size(); ++k)
+        for (uint32_t j = 0; j < 3; ++j)
+        {
+            uint32_t b = (uint32_t(k) * 3u + j) * 3u;
+            vec3 p((U(b) - 0.5f) * 0.4f, (U(b + 1) - 0.5f) * 0.4f, (U(b + 2) - 0.5f) * 0.4f);
+            vnormals[k * 3 + j] = normalize(face_normals[k] + p);
+        }
+    shade_spec sp = make_shade_spec();
+    camera cam = make_camera(d, W, H);
+    simple_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> rt;
+    rt.resize(W, H);
+    auto sparams = make_sched_params(pixel_sampler::uniform_type{}, cam, rt);
+    simple_sched<ray> sched;
+    if (per_vertex)
+    {
+        auto kp = make_kernel_params(normals_per_vertex_binding{}, bvhs.data(), bvhs.data() + bvhs.size(),
+                                     vnormals.data(), sp.materials.data(), sp.lights.data(),
+                                     sp.lights.data() + sp.lights.size(), 5u, 1e-3f, sp.bg, sp.ambient);
+        simple::kernel<decltype(kp)> kern;
+        kern.params = kp;
+        sched.frame(kern, sparams);
+    }
+    else
+    {
+        auto kp = make_kernel_params(normals_per_face_binding{}, bvhs.data(), bvhs.data() + bvhs.size(),
+                                     face_normals.data(), sp.materials.data(), sp.lights.data(),
+                                     sp.lights.data() + sp.lights.size(), 5u, 1e-3f, sp.bg, sp.ambient);
+        simple::kernel<decltype(kp)> kern;
+        kern.params = kp;
+        sched.frame(kern, sparams);
+    }
+    size_t npx = size_t(W) * H;
+    write_file(outdir + "/color.bin", rt.color(), npx * 16);
+    fnv hc;
+    hc.bytes(rt.color(), npx * 16);
+    printf("{\"scene\":\"%s\",\"W\":%d,\"H\":%d,\"binding\":\"%s\",\"color_hash\":\"%016llx\"}\n",
+           d.name.c_str(), W, H, per_vertex ? "vertex" : "face", (unsigned long long)hc.h);
+    return 0;
+}
+
+//-------------------------------------------------------------------------------------------------
 // bench: reference SSE4 tiled_sched<ray4> path, ao/main.cpp kernel
 //
 
@@ -452,6 +558,19 @@ int main(int argc, char** argv)
         {
             return run_golden(d, prims, normals, outdir, W, H, !d.spheres);
         });
+    }
+    if (mode == "shade")
+    {
+        if (argc < 5 || d.spheres) return 2;
+        std::string outdir = argv[3];
+        bool per_vertex = std::string(argv[4]) == "vertex";
+        int W = argc > 6 ? atoi(argv[5]) : d.W;
+        int H = argc > 6 ? atoi(argv[6]) : d.H;
+        aligned_vector<tri_t> t;
+        if (d.grid == 0) make_cornell(t); else make_heightfield(d.grid, t);
+        std::vector<vec3> normals(t.size());
+        for (size_t i = 0; i < t.size(); ++i) normals[i] = normalize(cross(t[i].e1, t[i].e2));
+        return run_shade(d, t, normals, outdir, per_vertex, W, H);
     }
     if (mode == "bench")
     {

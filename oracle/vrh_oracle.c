@@ -506,6 +506,7 @@ static inline void primary_ray(const vo_camera* cam, unsigned x, unsigned y, v3*
 }
 
 typedef struct { float color[4]; uint32_t prim_id; float t; uint8_t occ; uint32_t list_index; uint32_t rays; } px_out;
+static void shade_simple(const vo_scene* s, const vo_kernel* k, v3 ori, v3 dir, const vo_hit* hr, float out[4]);
 
 /* ao/main.cpp:183-246 with the deterministic sampler of SURVEY.md Appendix A */
 static px_out shade_pixel(const vo_scene* s, const vo_camera* cam, const vo_kernel* k, unsigned x, unsigned y,
@@ -520,6 +521,10 @@ static px_out shade_pixel(const vo_scene* s, const vo_camera* cam, const vo_kern
     vo_hit hr = vo_intersect(fo, fd, s->nodes, s->indices, s->prims, s->kind, 0, FLT_MAX, cnt);
     if (!hr.hit) return o;
     o.prim_id = hr.prim_id; o.t = hr.t; o.list_index = hr.list_index;
+    if (k->mode == VO_MODE_SIMPLE) {
+        shade_simple(s, k, ori, dir, &hr, o.color);
+        return o;
+    }
     if (k->mode != VO_MODE_AO) {
         o.color[0] = o.color[1] = o.color[2] = o.color[3] = 1.0f;
         return o;
@@ -551,6 +556,73 @@ static px_out shade_pixel(const vo_scene* s, const vo_camera* cam, const vo_kern
     o.color[0] = o.color[1] = o.color[2] = clr;
     o.color[3] = 1.0f;
     return o;
+}
+
+/* detail/simple.inl:26-79 (simple::kernel) with plastic materials and point lights: ambient term,
+ * two-sided shading normal (faceforward), one plastic::shade per light.  Colour of a hit pixel. */
+static void shade_simple(const vo_scene* s, const vo_kernel* k, v3 ori, v3 dir, const vo_hit* hr, float out[4])
+{
+    v3 pos = add(ori, muls(dir, hr->t));                               /* simple.inl:37 */
+    v3 gn, sn;
+    if (k->normal_binding == VO_NORMALS_PER_FACE) {
+        gn = sn = ld(&s->normals[hr->prim_id]);                         /* get_normal.h:26-37 */
+    } else {
+        /* get_surface.h:336-376 -> get_normal(hr, primitive(list_index)) (get_normal.h:110-116)
+         * and get_shading_normal.h:64-84 with lerp(a,b,c,u,v) (math.h:466-475) */
+        const vo_tri* tri = (const vo_tri*)s->prims + s->indices[hr->list_index];
+        gn = normalize(cross(ld(&tri->e1), ld(&tri->e2)));
+        v3 n0 = ld(&s->vertex_normals[hr->prim_id * 3u]);
+        v3 n1 = ld(&s->vertex_normals[hr->prim_id * 3u + 1u]);
+        v3 n2 = ld(&s->vertex_normals[hr->prim_id * 3u + 2u]);
+        v3 s2 = muls(n2, hr->v), s3 = muls(n1, hr->u), s1 = muls(n0, 1.0f - (hr->u + hr->v));
+        sn = normalize(add(add(s1, s2), s3));
+    }
+    const vo_plastic* m = &k->materials[hr->geom_id];
+    const float PI = 3.14159265358979323846264338328e+00f, INV_PI = 3.18309886183790691216444201928e-01f;
+    /* plastic.inl:13-16 ambient() = ca * ka; * from_rgba(ambient) (spectrum.inl:375-378) */
+    v3 amb_c = mk(k->ambient[0] * k->ambient[3], k->ambient[1] * k->ambient[3], k->ambient[2] * k->ambient[3]);
+    v3 shaded = mul(muls(mk(m->ca[0], m->ca[1], m->ca[2]), m->ka), amb_c);
+    v3 view = mk(-dir.x, -dir.y, -dir.z);
+    v3 n = dot(gn, view) < 0.0f ? mk(-sn.x, -sn.y, -sn.z) : sn;          /* vector.inl:674-681 */
+    for (int li = 0; li < k->num_lights; ++li) {
+        const vo_point_light* L = &k->lights[li];
+        v3 lpos = mk(L->position[0], L->position[1], L->position[2]);
+        v3 wi = normalize(sub(lpos, pos));                              /* simple.inl:59 */
+        v3 wo = view;
+        float ndotl = fmax_ref(0.0f, dot(n, wi));                       /* plastic.inl:29 */
+        /* brdf.h:36-41 lambertian::f = cd * kd * inv_pi */
+        v3 diff = muls(muls(mk(m->cd[0], m->cd[1], m->cd[2]), m->kd), INV_PI);
+        /* brdf.h:111-122 blinn::f */
+        v3 h = normalize(add(wo, wi));
+        float hdotn = fmax_ref(0.0f, dot(h, n));
+        v3 spec = muls(mk(m->cs[0], m->cs[1], m->cs[2]), m->ks);
+        float sat = fmax_ref(0.0f, fmin_ref(dot(wi, h), 1.0f));          /* math.h:454-457 */
+        float p5 = powf(1.0f - sat, 5.0f);
+        v3 schlick = add(spec, muls(mk(1.0f - spec.x, 1.0f - spec.y, 1.0f - spec.z), p5));
+        float nfactor = (m->exp + 2.0f) / (8.0f * PI);
+        v3 bl = muls(muls(schlick, nfactor), powf(hdotn, m->exp));
+        /* point_light.inl:12-28 intensity: (cl * kl) * float(1.0 / (c + l*d + q*d*d)) */
+        float dist = sqrtf(dot(sub(lpos, pos), sub(lpos, pos)));
+        float den = L->constant_att + L->linear_att * dist + L->quadratic_att * dist * dist;
+        float att = (float)(1.0 / (double)den);
+        v3 I = muls(muls(mk(L->cl[0], L->cl[1], L->cl[2]), L->kl), att);
+        /* plastic.inl:21-37: pi * (cd + blinn) * I * ndotl */
+        v3 clr = muls(mul(smul(PI, add(diff, bl)), I), ndotl);
+        shaded = add(shaded, clr);                                      /* simple.inl:63 */
+    }
+    out[0] = shaded.x; out[1] = shaded.y; out[2] = shaded.z; out[3] = 1.0f;   /* to_rgba */
+}
+
+void vo_vertex_normals(const vo_vec3* face_normals, size_t n, vo_vec3* out)
+{
+    for (size_t k = 0; k < n; ++k) {
+        v3 fn = ld(&face_normals[k]);
+        for (uint32_t j = 0; j < 3; ++j) {
+            uint32_t b = ((uint32_t)k * 3u + j) * 3u;
+            v3 p = mk((vo_uniform(b) - 0.5f) * 0.4f, (vo_uniform(b + 1u) - 0.5f) * 0.4f, (vo_uniform(b + 2u) - 0.5f) * 0.4f);
+            st(&out[k * 3 + j], normalize(add(fn, p)));
+        }
+    }
 }
 
 uint64_t vo_render_rows(const vo_scene* s, const vo_camera* cam, const vo_kernel* k, int y0, int y1,

@@ -30,7 +30,14 @@ typedef struct { uint32_t geom_id, prim_id, pad0, pad1; vo_vec3 center; float ra
 typedef struct { float bmin[3]; uint32_t first; float bmax[3]; uint32_t num_prims; } vo_node;
 
 enum { VO_TRI = 0, VO_SPHERE = 1 };
-enum { VO_MODE_PRIMARY = 0, VO_MODE_AO = 1 };
+enum { VO_MODE_PRIMARY = 0, VO_MODE_AO = 1, VO_MODE_SIMPLE = 2 };
+enum { VO_NORMALS_PER_FACE = 0, VO_NORMALS_PER_VERTEX = 1 };
+
+/* plastic<float> (material.h:267-323, detail/material/plastic.inl): ambient ca*ka, lambertian
+ * diffuse cd*kd, blinn specular cs*ks with exponent exp */
+typedef struct { float ca[3]; float ka; float cd[3]; float kd; float cs[3]; float ks; float exp; } vo_plastic;
+/* point_light<float> (point_light.h, detail/point_light.inl) */
+typedef struct { float position[3]; float cl[3]; float kl; float constant_att, linear_att, quadratic_att; } vo_point_light;
 
 /* ---- synthetic scenes, SURVEY.md Appendix A ---- */
 uint32_t vo_wang(uint32_t a);
@@ -67,19 +74,29 @@ vo_hit vo_intersect(const float ori[3], const float dir[3], const vo_node* nodes
 /* ---- a frame, simple_sched order (row-major), over rows [y0, y1) ---- */
 typedef struct {
     const vo_node* nodes; const uint32_t* indices; const void* prims; int kind;
-    const vo_vec3* normals;               /* per prim_id, for AO */
+    const vo_vec3* normals;               /* per prim_id (AO; simple kernel, per-face binding) */
+    const vo_vec3* vertex_normals;        /* 3 per prim_id (simple kernel, per-vertex binding) */
 } vo_scene;
 typedef struct {
     float eye[3], cam_u[3], cam_v[3], cam_w[3];
     int   width, height;
 } vo_camera;
 typedef struct {
-    int   mode;                           /* VO_MODE_PRIMARY | VO_MODE_AO */
+    int   mode;                           /* VO_MODE_PRIMARY | VO_MODE_AO | VO_MODE_SIMPLE */
     int   samples;                        /* AO samples (8) */
     float radius;                         /* AO radius (0.1) */
     float eps;                            /* AO origin offset (1e-3) */
     float bg[4];                          /* miss colour */
+    /* simple::kernel (detail/simple.inl:19-83) */
+    const vo_plastic* materials; int num_materials;       /* indexed by geom_id */
+    const vo_point_light* lights; int num_lights;
+    float ambient[4];
+    int   normal_binding;                 /* VO_NORMALS_PER_FACE | VO_NORMALS_PER_VERTEX */
 } vo_kernel;
+
+/* deterministic per-vertex normals for tests: prim k, vertex j: normalize(n_k + 0.4 * (U(b) - 0.5,
+ * U(b+1) - 0.5, U(b+2) - 0.5)) with b = (3k + j) * 3 and n_k the face normal */
+void vo_vertex_normals(const vo_vec3* face_normals, size_t n, vo_vec3* out);
 
 /* Any output pointer may be NULL.  Arrays are full-image sized (W*H), indexed y*W+x.
  * threads <= 0: all cores (OpenMP).  Returns rays traced (primary + AO) over the rows. */

@@ -2,7 +2,8 @@
 
 Run in the build container (needs /root/reference to build the harness):
 
-    make -C oracle ref && python tests/golden/make_golden.py
+    make -C oracle ref && python tests/golden/make_golden.py            (everything)
+    python tests/golden/make_golden.py --shade                          (only the shading cases)
 
 For every case the reference harness renders a full simple_sched<basic_ray<float>> frame
 (primary closest_hit + the Appendix-A AO kernel for triangle scenes) and this script stores:
@@ -39,6 +40,16 @@ CASES = [
 ]
 
 
+# simple::kernel shading cases (reference harness "shade" mode): (case, scene, W, H, binding, full dump?)
+SHADE_CASES = [
+    ("shade_cornell12_face", "cornell12", 128, 128, "face", True),
+    ("shade_cornell12_vertex", "cornell12", 128, 128, "vertex", True),
+    ("shade_hf64_face", "hf64", 160, 90, "face", True),
+    ("shade_hf64_vertex", "hf64", 160, 90, "vertex", True),
+    ("shade_hf1M_vertex", "hf1M", 1920, 1080, "vertex", False),
+]
+
+
 def fnv1a(a):
     """FNV-1a 64 over the little-endian bytes (computed by the oracle's C helper for speed)."""
     sys.path.insert(0, ROOT)
@@ -46,12 +57,32 @@ def fnv1a(a):
     return O.fnv1a(np.ascontiguousarray(a).view(np.uint8).reshape(-1))
 
 
+def shade_cases(out, rng):
+    for case, scene, W, H, binding, full in SHADE_CASES:
+        with tempfile.TemporaryDirectory() as d:
+            r = subprocess.run([REF, "shade", scene, d, binding, str(W), str(H)], check=True, capture_output=True,
+                               text=True)
+            info = json.loads(r.stdout.strip().splitlines()[-1])
+            color = np.fromfile(os.path.join(d, "color.bin"), np.float32).reshape(-1, 4)
+            rec = {"scene": scene, "W": W, "H": H, "binding": binding, "color_hash": fnv1a(color)}
+            assert rec["color_hash"] == info["color_hash"]
+            if full:
+                np.savez_compressed(os.path.join(HERE, case + ".npz"), color=color)
+            else:
+                pix = np.sort(rng.choice(W * H, 4096, replace=False)).astype(np.uint32)
+                np.savez_compressed(os.path.join(HERE, case + ".npz"), pixels=pix, color=color[pix])
+            out[case] = rec
+            print(case, rec["color_hash"], flush=True)
+
+
 def main():
     if not os.path.exists(REF):
         sys.exit("build the reference harness first: make -C oracle ref")
-    out = {}
+    only_shade = "--shade" in sys.argv
+    path = os.path.join(HERE, "golden.json")
+    out = json.load(open(path)) if only_shade else {}
     rng = np.random.default_rng(12345)
-    for case, scene, W, H, full in CASES:
+    for case, scene, W, H, full in ([] if only_shade else CASES):
         with tempfile.TemporaryDirectory() as d:
             r = subprocess.run([REF, "golden", scene, d, str(W), str(H)], check=True, capture_output=True, text=True)
             info = json.loads(r.stdout.strip().splitlines()[-1])
@@ -79,7 +110,8 @@ def main():
                                     occ=occ[pix], color=color[pix])
             out[case] = rec
             print(case, rec["hits"], rec["ao_occluded"], rec["primid_hash"], flush=True)
-    with open(os.path.join(HERE, "golden.json"), "w") as f:
+    shade_cases(out, np.random.default_rng(54321))
+    with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 
 

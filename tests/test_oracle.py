@@ -110,3 +110,18 @@ def test_oracle_matches_live_reference(oracle_mod, scene, W, H):
         if mode == O.VO_MODE_AO:
             assert np.array_equal(out["occ"], np.fromfile(os.path.join(d, "occ.bin"), np.uint8))
         assert int((out["prim_id"] != 0xFFFFFFFF).sum()) == info["hits"]
+
+
+@pytest.mark.parametrize("case", ["shade_cornell12_face", "shade_cornell12_vertex", "shade_hf64_face",
+                                  "shade_hf64_vertex"])
+def test_oracle_simple_kernel_matches_reference(golden, oracle_mod, case):
+    """simple::kernel restatement (plastic + point lights, both normal bindings) bit-identical to
+    the reference's own frames (tests/golden/shade_*.npz)."""
+    O = oracle_mod
+    g = golden[case]
+    sc = O.make_shade_scene(g["scene"])
+    out = O.render_simple(sc, O.scene_camera(g["scene"], g["W"], g["H"]),
+                          O.VO_NORMALS_PER_VERTEX if g["binding"] == "vertex" else O.VO_NORMALS_PER_FACE)
+    ref = np.load(os.path.join(os.path.dirname(__file__), "golden", case + ".npz"))["color"]
+    assert np.array_equal(out["color"].view(np.uint32), ref.view(np.uint32))
+    assert O.fnv1a(out["color"]) == g["color_hash"]

@@ -15,7 +15,8 @@ LIB_PATH = os.environ.get("VRH_LIB") or os.path.join(_HERE, "_lib", "libvrh.so")
 # enums (vrh.h)
 VRH_OK, VRH_ERR_INVALID, VRH_ERR_HIP, VRH_ERR_OOM, VRH_ERR_UNSUPPORTED, VRH_ERR_NO_DEVICE = range(6)
 VRH_PRIM_TRI64, VRH_PRIM_SPHERE48 = 0, 1
-VRH_KERNEL_PRIMARY, VRH_KERNEL_AO = 0, 1
+VRH_KERNEL_PRIMARY, VRH_KERNEL_AO, VRH_KERNEL_SIMPLE = 0, 1, 2
+VRH_NORMALS_PER_FACE, VRH_NORMALS_PER_VERTEX = 0, 1
 VRH_RT_COLOR, VRH_RT_PRIM_ID, VRH_RT_T, VRH_RT_OCC, VRH_RT_ALL = 1, 2, 4, 8, 15
 
 
@@ -26,7 +27,18 @@ class vrh_camera(C.Structure):
 
 class vrh_kernel_desc(C.Structure):
     _fields_ = [("kind", C.c_uint32), ("samples", C.c_uint32), ("radius", C.c_float), ("eps", C.c_float),
-                ("bg", C.c_float * 4), ("flags", C.c_uint32)]
+                ("bg", C.c_float * 4), ("flags", C.c_uint32), ("normal_binding", C.c_uint32),
+                ("ambient", C.c_float * 4), ("shading", C.c_void_p)]
+
+
+class vrh_plastic(C.Structure):
+    _fields_ = [("ca", C.c_float * 3), ("ka", C.c_float), ("cd", C.c_float * 3), ("kd", C.c_float),
+                ("cs", C.c_float * 3), ("ks", C.c_float), ("exp", C.c_float)]
+
+
+class vrh_point_light(C.Structure):
+    _fields_ = [("position", C.c_float * 3), ("cl", C.c_float * 3), ("kl", C.c_float), ("constant_att", C.c_float),
+                ("linear_att", C.c_float), ("quadratic_att", C.c_float)]
 
 
 VRH_KERNEL_COUNT_TESTS = 1
@@ -58,7 +70,8 @@ class vrh_frame_stats(C.Structure):
 class vrh_scene_info(C.Structure):
     _fields_ = [("num_nodes", C.c_uint32), ("num_prims", C.c_uint32), ("num_indices", C.c_uint32),
                 ("prim_kind", C.c_uint32), ("max_depth", C.c_uint32), ("device_bytes", C.c_uint64),
-                ("wide_records", C.c_uint32), ("wide_depth", C.c_uint32)]
+                ("wide_records", C.c_uint32), ("wide_depth", C.c_uint32), ("max_prim_id", C.c_uint32),
+                ("max_geom_id", C.c_uint32), ("vertex_normals", C.c_uint32)]
 
 
 class VrhError(RuntimeError):
@@ -81,6 +94,9 @@ SIGNATURES = {
     "vrh_scene_upload": (C.c_int, [_vp, _vp, _u32, _vp, _u32, _u32, _vp, _u32, _vp, C.POINTER(_vp)]),
     "vrh_scene_get_info": (C.c_int, [_vp, C.POINTER(vrh_scene_info)]),
     "vrh_scene_free": (C.c_int, [_vp]),
+    "vrh_scene_set_vertex_normals": (C.c_int, [_vp, _vp, _u32]),
+    "vrh_shading_create": (C.c_int, [_vp, _vp, _u32, _vp, _u32, C.POINTER(_vp)]),
+    "vrh_shading_free": (C.c_int, [_vp]),
     "vrh_rt_alloc": (C.c_int, [_vp, _u32, _u32, _u32, C.POINTER(_vp)]),
     "vrh_rt_wrap": (C.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _vp, C.POINTER(_vp)]),
     "vrh_rt_get_buffers": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp)]),

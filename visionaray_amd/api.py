@@ -207,9 +207,23 @@ class hip_index_bvh:
                    len(host_bvh.prims), host_bvh.prim_kind, _p(host_bvh.indices), len(host_bvh.indices),
                    _p(nrm), C.byref(h))
         self.handle = h
+        self._refresh_info()
+
+    def _refresh_info(self):
         info = capi.vrh_scene_info()
-        capi.check("vrh_scene_get_info", h, C.byref(info))
+        capi.check("vrh_scene_get_info", self.handle, C.byref(info))
         self.info = {k: getattr(info, k) for k, _ in info._fields_}
+
+    def set_vertex_normals(self, normals):
+        """normals_per_vertex_binding array: (3 * num prim ids, 3 or 4) float32, row 3*prim_id + k."""
+        n = np.asarray(normals, np.float32)
+        if n.ndim != 2 or n.shape[1] not in (3, 4):
+            raise ValueError("vertex normals must be (3 * prims, 3|4) float32")
+        if n.shape[1] == 3:
+            n = np.concatenate([n, np.zeros((len(n), 1), np.float32)], 1)
+        n = np.ascontiguousarray(n)
+        capi.check("vrh_scene_set_vertex_normals", self.handle, _p(n), len(n))
+        self._refresh_info()
 
     def close(self):
         if self.handle:
@@ -353,6 +367,68 @@ def ao_kernel(bvh, samples=8, radius=0.1, eps=1e-3, bg=(0.1, 0.2, 0.3, 1.0), cou
     return _builtin_kernel(bvh, capi.VRH_KERNEL_AO, samples, radius, eps, bg, count_tests)
 
 
+# ---- shading ----------------------------------------------------------------
+
+PLASTIC_DTYPE = np.dtype([("ca", "<f4", 3), ("ka", "<f4"), ("cd", "<f4", 3), ("kd", "<f4"), ("cs", "<f4", 3),
+                          ("ks", "<f4"), ("exp", "<f4")])
+POINT_LIGHT_DTYPE = np.dtype([("position", "<f4", 3), ("cl", "<f4", 3), ("kl", "<f4"), ("constant_att", "<f4"),
+                              ("linear_att", "<f4"), ("quadratic_att", "<f4")])
+normals_per_face_binding = capi.VRH_NORMALS_PER_FACE
+normals_per_vertex_binding = capi.VRH_NORMALS_PER_VERTEX
+
+
+def plastic(ca=(0.0, 0.0, 0.0), ka=1.0, cd=(0.8, 0.8, 0.8), kd=1.0, cs=(0.0, 0.0, 0.0), ks=0.0, exp=1.0):
+    """One plastic<float> material record (material.h:267-323 setters: set_ca/ka/cd/kd/cs/ks/specular_exp)."""
+    m = np.zeros((), PLASTIC_DTYPE)
+    m["ca"], m["ka"], m["cd"], m["kd"], m["cs"], m["ks"], m["exp"] = ca, ka, cd, kd, cs, ks, exp
+    return m
+
+
+def point_light(position, cl=(1.0, 1.0, 1.0), kl=1.0, constant_att=1.0, linear_att=0.0, quadratic_att=0.0):
+    """One point_light<float> record (point_light.h:18-66; attenuation defaults 1, 0, 0)."""
+    l_ = np.zeros((), POINT_LIGHT_DTYPE)
+    l_["position"], l_["cl"], l_["kl"] = position, cl, kl
+    l_["constant_att"], l_["linear_att"], l_["quadratic_att"] = constant_att, linear_att, quadratic_att
+    return l_
+
+
+class shading:
+    """Device materials (plastic, indexed by geom_id) + point lights: the materials / lights
+    arguments of make_kernel_params (kernels.h:357-389), copied to the GPU once."""
+
+    def __init__(self, ctx, materials, lights):
+        self.ctx = ctx
+        self.materials = np.ascontiguousarray(np.atleast_1d(materials), PLASTIC_DTYPE)
+        self.lights = np.ascontiguousarray(np.atleast_1d(lights), POINT_LIGHT_DTYPE)
+        h = C.c_void_p()
+        capi.check("vrh_shading_create", ctx.handle, _p(self.materials), len(self.materials),
+                   _p(self.lights) if len(self.lights) else None, len(self.lights), C.byref(h))
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            capi.lib().vrh_shading_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def simple_kernel(bvh, shade, binding=normals_per_face_binding, bg=(0.0, 0.0, 0.0, 0.0),
+                  ambient=(0.0, 0.0, 0.0, 0.0), count_tests=False):
+    """simple::kernel (detail/simple.inl:19-83) over make_kernel_params(binding, prims, normals,
+    materials, lights, bounces, eps, bg, ambient): closest hit, ambient + plastic::shade per light."""
+    k = _builtin_kernel(bvh, capi.VRH_KERNEL_SIMPLE, 0, 0.0, 0.0, bg, count_tests)
+    k.desc.normal_binding = binding
+    k.desc.ambient = (C.c_float * 4)(*ambient)
+    k.desc.shading = shade.handle
+    k.shade = shade          # keep the device arrays alive
+    return k
+
+
 class hip_sched:
     """hip_sched<R>: drop-in for cuda_sched<R> (cuda_sched.h:25-40).
 
@@ -365,7 +441,7 @@ class hip_sched:
 
     def frame(self, kernel, sparams, frame_num=0, shard=None, sync=True):
         if not isinstance(kernel, _builtin_kernel):
-            raise TypeError("hip_sched runs built-in kernels only (closest_hit_kernel / ao_kernel): an arbitrary "
+            raise TypeError("hip_sched runs built-in kernels only (closest_hit_kernel / ao_kernel / simple_kernel): an arbitrary "
                             "callable cannot cross the C ABI")
         rt = sparams.rt
         cam = sparams.cam.basis(*sparams.image_size)

@@ -122,7 +122,7 @@ __device__ __forceinline__ bool finite_ray(const ray_t& r)
 // early outs: every quantity is computed exactly as the reference computes it; the reference's
 // early returns only skip work whose result it then discards, so the accepted hits and their t are
 // identical, and the lanes of a wave do not diverge.
-__device__ __forceinline__ bool isect_tri(const ray_t& r, float4 a, float4 b, float4 c, float& t)
+__device__ __forceinline__ bool isect_tri(const ray_t& r, float4 a, float4 b, float4 c, float& t, float& u, float& v)
 {
     f3 v1 = mk3(a.x, a.y, a.z), e1 = mk3(a.w, b.x, b.y), e2 = mk3(b.z, b.w, c.x);
     f3 s1 = cross(r.dir, e2);
@@ -133,8 +133,20 @@ __device__ __forceinline__ bool isect_tri(const ray_t& r, float4 a, float4 b, fl
     f3 s2 = cross(d, e1);
     float b2 = dot(r.dir, s2) * inv_div;
     t = dot(e2, s2) * inv_div;
+    u = b1;
+    v = b2;
     return (div != 0.0f) & (b1 >= 0.0f) & (b1 <= 1.0f) & (b2 >= 0.0f) & (b1 + b2 <= 1.0f);
 }
+
+__device__ __forceinline__ bool isect_tri(const ray_t& r, float4 a, float4 b, float4 c, float& t)
+{
+    float u, v;
+    return isect_tri(r, a, b, c, t, u, v);
+}
+
+// extra closest-hit state the shading kernels need: barycentrics (hit_record u, v) and the
+// leaf-order index of the hit primitive (hit_record_bvh::primitive_list_index)
+struct hit_extra { float u, v; uint32_t li; };
 
 // math/intersect.h:186-221 ray/sphere
 __device__ __forceinline__ bool isect_sphere(const ray_t& r, float4 a, float& t)
@@ -228,12 +240,13 @@ __device__ __forceinline__ bool quad_entry(float xl, float yl, float zl, float x
 // records instead: the same set of leaves is reached (vrh_quad.cpp), the order does not matter
 // for an any-hit result, and the nearest hit entry is descended first.  If a record's hits could
 // overflow the stack, the ray restarts on the binary records from `root` (still exact).
-template <int KIND, bool COUNT, bool FAST>
+template <int KIND, bool COUNT, bool FAST, bool UV = false>
 __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const float4* __restrict__ prims,
                                         const float4* __restrict__ quads, uint32_t root, bool& quad,
                                         const ray_t& r, float max_t, bool any, lds_stack& st,
                                         float& best_t, uint32_t& best_prim, test_counts& cnt,
-                                        uint32_t& steps, uint32_t step_limit, uint32_t& resume, uint32_t cap)
+                                        uint32_t& steps, uint32_t step_limit, uint32_t& resume, uint32_t cap,
+                                        hit_extra* hx = nullptr)
 {
     // the tree was validated at upload (no cycles, links in range), so the descent terminates;
     // the guard below only bounds the number of outer iterations per ray
@@ -306,14 +319,14 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
     uint32_t i = link & ~LEAF_BIT;
     for (;;)
     {
-        float t;
+        float t, hu = 0.0f, hv = 0.0f;
         bool h;
         uint32_t flags, pid;
         if constexpr (KIND == KIND_TRI)
         {
             const float4* q = prims + 3u * i;
             float4 a = q[0], b = q[1], c = q[2];
-            h = isect_tri(r, a, b, c, t);
+            h = isect_tri(r, a, b, c, t, hu, hv);
             pid = __float_as_uint(c.y);
             flags = __float_as_uint(c.w);
         }
@@ -330,6 +343,7 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
         {
             best_t = t;
             best_prim = pid;
+            if constexpr (UV) { hx->u = hu; hx->v = hv; hx->li = i; }   // hit_record.h:54-64
             if (any) return 1;                                   // exit_traversal.h:49-56
         }
         if (flags & END_BIT) break;

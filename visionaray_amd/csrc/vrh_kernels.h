@@ -2,6 +2,7 @@
 #pragma once
 
 #include "../../include/vrh.h"
+#include "vrh_shade.h"
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -47,6 +48,7 @@ struct render_params
     uint32_t refill_min_primary;   // the same for the step loop's primary-only stream
     uint32_t vote_leaf;       // vote schedule: leaf step when 8 * leaf lanes >= vote_leaf * node lanes
     uint32_t descent_cap;     // step loop: inner visits per step before a descent is resumed later
+    dev::shade_params shade;  // VRH_KERNEL_SIMPLE: materials, lights, normal binding, ambient
 };
 
 constexpr int COUNTERS_FRAME = 80;      // u64 words reset before every frame
@@ -62,6 +64,7 @@ struct launch_config
     int stack_cap;     // LDS stack entries per lane
     int occ;           // register budget: min waves per SIMD (1, 6 or 8)
     int sched;         // 0: step loop (render_unified_kernel), 1: item loop, 2: vote loop (render_item_kernel)
+    bool shade;        // VRH_KERNEL_SIMPLE epilogue (step loop, triangles)
 };
 
 size_t render_lds_bytes(const launch_config& c);

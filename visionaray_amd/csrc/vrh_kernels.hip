@@ -126,7 +126,7 @@ __device__ __forceinline__ ray_t ao_ray(const render_params& P, const float* rec
 // instruction stream (ray_step); a lane that finishes a ray immediately takes the next one, so
 // neither the primary phase nor the AO phase waits for its slowest lane.  Without AO the wave
 // streams pixels tile after tile and writes each pixel when its ray finishes.
-template <int KIND, bool AO, bool COUNT, int OCC>
+template <int KIND, bool AO, bool COUNT, int OCC, bool SHADE = false>
 __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params P)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -161,6 +161,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         uint32_t tile = next_tile(P, tq, lane);
         uint32_t handed = 0;                       // pixels of `tile` handed out (wave-uniform)
         uint32_t out_o = 0;
+        hit_extra hx = { 0.0f, 0.0f, 0u };
         for (;;)
         {
             uint64_t idle = __ballot(mode == IDLE);
@@ -201,13 +202,16 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             if (mode != IDLE)
             {
                 int rc = (P.fast_ok && __ballot(!finite) == 0ull)
-                    ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap)
-                    : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap);
+                    ? ray_step<KIND, COUNT, true, SHADE>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, &hx)
+                    : ray_step<KIND, COUNT, false, SHADE>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, &hx);
                 if (rc != 0)
                 {
                     bool hit = best_t != FMAX;
                     hits_total += hit ? 1 : 0;
-                    if (P.color) P.color[out_o] = hit ? make_float4(1.0f, 1.0f, 1.0f, 1.0f) : make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
+                    float4 c = hit ? make_float4(1.0f, 1.0f, 1.0f, 1.0f) : make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
+                    if constexpr (SHADE)
+                        if (hit) c = shade_simple(P.shade, P.prims, P.normals, r, best_t, best_prim, hx);
+                    if (P.color) P.color[out_o] = c;
                     if (P.prim_id) P.prim_id[out_o] = hit ? best_prim : 0xFFFFFFFFu;
                     if (P.t) P.t[out_o] = hit ? best_t : -1.0f;
                     if (P.occ) P.occ[out_o] = 0;
@@ -712,6 +716,14 @@ static kernel_fn pick_occ(bool ao, bool count, int sched)
     return count ? dev::render_unified_kernel<KIND, true, true, OCC> : dev::render_unified_kernel<KIND, true, false, OCC>;
 }
 
+// simple::kernel epilogue: triangles, step loop
+template <int OCC>
+static kernel_fn pick_shade(bool count)
+{
+    return count ? dev::render_unified_kernel<dev::KIND_TRI, false, true, OCC, true>
+                 : dev::render_unified_kernel<dev::KIND_TRI, false, false, OCC, true>;
+}
+
 template <int KIND>
 static kernel_fn pick(bool ao, bool count, int occ, int sched)
 {
@@ -722,6 +734,7 @@ static kernel_fn pick(bool ao, bool count, int occ, int sched)
 
 static kernel_fn select_variant(const launch_config& c)
 {
+    if (c.shade) return c.occ == 8 ? pick_shade<8>(c.count) : c.occ == 6 ? pick_shade<6>(c.count) : pick_shade<1>(c.count);
     return c.kind == dev::KIND_TRI ? pick<dev::KIND_TRI>(c.ao, c.count, c.occ, c.sched)
                                    : pick<dev::KIND_SPHERE>(c.ao, c.count, c.occ, c.sched);
 }

@@ -65,10 +65,19 @@ struct vrh_scene
     float4* prims = nullptr;
     float4* normals = nullptr;
     float4* quads = nullptr;     // 4-wide any-hit records (vrh_quad.cpp), null if the scene has none
+    float4* vnormals = nullptr;  // per-vertex normals (3 per prim_id), VRH_NORMALS_PER_VERTEX
     uint32_t root = 0;
     uint32_t quad_depth = 0;
     bool finite_bounds = true;   // every node bound finite (enables the hardware min/max slab path)
     vrh_scene_info info{};
+};
+
+struct vrh_shading
+{
+    vrh_ctx* ctx = nullptr;
+    dev::plastic_t* materials = nullptr;
+    dev::point_light_t* lights = nullptr;
+    uint32_t num_materials = 0, num_lights = 0;
 };
 
 struct vrh_rt
@@ -283,6 +292,15 @@ VRH_API int vrh_scene_upload(vrh_ctx* ctx, const void* nodes_v, uint32_t num_nod
         for (int a = 0; a < 3; ++a)
             finite_bounds = finite_bounds && std::isfinite(nodes[i].bmin[a]) && std::isfinite(nodes[i].bmax[a]);
 
+    uint32_t max_prim_id = 0, max_geom_id = 0;
+    for (uint32_t i = 0; i < num_prims; ++i)
+    {
+        uint32_t ids[2];
+        std::memcpy(ids, static_cast<const uint8_t*>(prims_v) + size_t(i) * (prim_kind == VRH_PRIM_TRI64 ? 64u : 48u), 8);
+        max_geom_id = std::max(max_geom_id, ids[0]);
+        max_prim_id = std::max(max_prim_id, ids[1]);
+    }
+
     std::vector<float> quads;
     uint32_t quad_root = 0, quad_depth = 0;
     const bool have_quads = finite_bounds && build_quads(nodes, num_nodes, quads, quad_root, quad_depth);
@@ -326,6 +344,8 @@ VRH_API int vrh_scene_upload(vrh_ctx* ctx, const void* nodes_v, uint32_t num_nod
     sc->info.num_indices = num_indices;
     sc->info.prim_kind = prim_kind;
     sc->info.max_depth = max_depth;
+    sc->info.max_prim_id = max_prim_id;
+    sc->info.max_geom_id = max_geom_id;
     sc->info.device_bytes = bytes;
     *out = sc;
     return VRH_OK;
@@ -346,7 +366,67 @@ VRH_API int vrh_scene_free(vrh_scene* sc)
     if (sc->prims) (void)hipFree(sc->prims);
     if (sc->normals) (void)hipFree(sc->normals);
     if (sc->quads) (void)hipFree(sc->quads);
+    if (sc->vnormals) (void)hipFree(sc->vnormals);
     delete sc;
+    return VRH_OK;
+}
+
+VRH_API int vrh_scene_set_vertex_normals(vrh_scene* sc, const void* normals, uint32_t num_normals)
+{
+    VRH_CHECK(sc && normals, "vrh_scene_set_vertex_normals: null argument");
+    VRH_CHECK(sc->info.prim_kind == VRH_PRIM_TRI64, "vrh_scene_set_vertex_normals: triangles only");
+    VRH_CHECK(uint64_t(num_normals) >= 3ull * (uint64_t(sc->info.max_prim_id) + 1ull),
+              "vrh_scene_set_vertex_normals: need 3 normals per prim_id (3 * (max prim_id + 1))");
+    int rc = select_device(sc->ctx);
+    if (rc) return rc;
+    if (sc->vnormals) { (void)hipFree(sc->vnormals); sc->vnormals = nullptr; sc->info.vertex_normals = 0; }
+    const size_t bytes = size_t(num_normals) * sizeof(float4);
+    VRH_HIP(hipMalloc(&sc->vnormals, bytes));
+    VRH_HIP(hipMemcpy(sc->vnormals, normals, bytes, hipMemcpyHostToDevice));
+    sc->info.vertex_normals = 1;
+    sc->info.device_bytes += bytes;
+    return VRH_OK;
+}
+
+VRH_API int vrh_shading_create(vrh_ctx* ctx, const vrh_plastic* materials, uint32_t num_materials,
+                               const vrh_point_light* lights, uint32_t num_lights, vrh_shading** out)
+{
+    static_assert(sizeof(vrh_plastic) == sizeof(dev::plastic_t), "plastic layout");
+    static_assert(sizeof(vrh_point_light) == sizeof(dev::point_light_t), "light layout");
+    VRH_CHECK(ctx && out && materials && num_materials > 0, "vrh_shading_create: need at least one material");
+    VRH_CHECK(num_lights == 0 || lights, "vrh_shading_create: null lights");
+    *out = nullptr;
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    auto* sh = new (std::nothrow) vrh_shading;
+    if (!sh) { set_error("host allocation failed"); return VRH_ERR_OOM; }
+    sh->ctx = ctx;
+    sh->num_materials = num_materials;
+    sh->num_lights = num_lights;
+    hipError_t e = hipMalloc(&sh->materials, sizeof(vrh_plastic) * num_materials);
+    if (e == hipSuccess) e = hipMemcpy(sh->materials, materials, sizeof(vrh_plastic) * num_materials, hipMemcpyHostToDevice);
+    if (e == hipSuccess && num_lights)
+    {
+        e = hipMalloc(&sh->lights, sizeof(vrh_point_light) * num_lights);
+        if (e == hipSuccess) e = hipMemcpy(sh->lights, lights, sizeof(vrh_point_light) * num_lights, hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess)
+    {
+        set_error(std::string("vrh_shading_create: ") + hipGetErrorString(e));
+        vrh_shading_free(sh);
+        return e == hipErrorOutOfMemory ? VRH_ERR_OOM : VRH_ERR_HIP;
+    }
+    *out = sh;
+    return VRH_OK;
+}
+
+VRH_API int vrh_shading_free(vrh_shading* sh)
+{
+    if (!sh) return VRH_OK;
+    if (sh->ctx) (void)hipSetDevice(sh->ctx->device);
+    if (sh->materials) (void)hipFree(sh->materials);
+    if (sh->lights) (void)hipFree(sh->lights);
+    delete sh;
     return VRH_OK;
 }
 
@@ -455,8 +535,18 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     (void)frame_num;  // the built-in kernels are deterministic; kept for cuda_sched::frame parity
     VRH_CHECK(ctx && sc && rt && cam && k, "vrh_render: null argument");
     VRH_CHECK(cam->width > 0 && cam->height > 0, "vrh_render: empty image");
-    VRH_CHECK(k->kind == VRH_KERNEL_PRIMARY || k->kind == VRH_KERNEL_AO, "vrh_render: unknown kernel kind");
+    VRH_CHECK(k->kind <= VRH_KERNEL_SIMPLE, "vrh_render: unknown kernel kind");
     const bool ao = k->kind == VRH_KERNEL_AO;
+    const bool shade = k->kind == VRH_KERNEL_SIMPLE;
+    if (shade)
+    {
+        VRH_CHECK(k->shading, "vrh_render: VRH_KERNEL_SIMPLE needs a vrh_shading (materials, lights)");
+        if (sc->info.prim_kind != VRH_PRIM_TRI64) { set_error("vrh_render: VRH_KERNEL_SIMPLE supports triangles"); return VRH_ERR_UNSUPPORTED; }
+        VRH_CHECK(k->shading->num_materials > sc->info.max_geom_id, "vrh_render: a geom_id has no material");
+        VRH_CHECK(k->normal_binding <= VRH_NORMALS_PER_VERTEX, "vrh_render: unknown normal binding");
+        if (k->normal_binding == VRH_NORMALS_PER_FACE) VRH_CHECK(sc->normals, "vrh_render: per-face shading needs face normals");
+        else VRH_CHECK(sc->vnormals, "vrh_render: per-vertex shading needs vrh_scene_set_vertex_normals");
+    }
     if (ao)
     {
         VRH_CHECK(k->samples >= 1 && k->samples <= 32, "vrh_render: AO samples must be in [1, 32]");
@@ -482,10 +572,12 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     lc.block = ctx->opt_block ? ctx->opt_block : 64;
     lc.stack_cap = int(cap);
     lc.occ = ctx->opt_occ ? ctx->opt_occ : 6;
+    lc.shade = shade;
     // auto: the item loop for sphere primary visibility (short leaves of cheap tests, where the
     // step loop's leaf iterations run at ~20 % lane utilisation), the step loop otherwise
     if (ctx->opt_sched == 0) lc.sched = (lc.kind == 1 && !ao) ? 1 : 0;
     else lc.sched = ctx->opt_sched == 4 ? 1 : ctx->opt_sched == 5 ? 2 : 0;
+    if (shade) lc.sched = 0;   // the shading epilogue lives in the step loop
     if (render_lds_bytes(lc) > 160u * 1024u)
     {
         set_error("vrh_render: BVH depth " + std::to_string(sc->info.max_depth) + " needs more LDS stack than a CU has");
@@ -513,10 +605,19 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     std::memcpy(p.bg, k->bg, 16);
     p.shard_index = sh.index; p.shard_count = sh.count; p.packed = sh.packed ? 1u : 0u;
     p.tiles_x = (cam->width + 7u) / 8u;
-    p.num_tiles = local_bands * 2u * p.tiles_x;
+    p.num_tiles = local_bands * p.tiles_x;           // a band is one row of 8x8 tiles
     p.color = rt->color; p.prim_id = rt->prim_id; p.t = rt->t; p.occ = rt->occ;
     p.counters = ctx->counters;
     p.xcd_queues = ctx->opt_xcd_queues == 2 ? 0u : 1u;
+    if (shade)
+    {
+        p.shade.materials = k->shading->materials;
+        p.shade.lights = k->shading->lights;
+        p.shade.num_lights = k->shading->num_lights;
+        p.shade.per_vertex = k->normal_binding == VRH_NORMALS_PER_VERTEX ? 1u : 0u;
+        p.shade.vnormals = sc->vnormals;
+        std::memcpy(p.shade.ambient, k->ambient, 16);
+    }
 
     int per_cu = render_blocks_per_cu(lc);
     if (ctx->opt_bpc) per_cu = std::min(per_cu, ctx->opt_bpc);
@@ -654,6 +755,8 @@ VRH_API int vrh_unshard(vrh_ctx* ctx, uint32_t width, uint32_t height, uint32_t 
     VRH_CHECK(ctx && dst && count >= 1, "vrh_unshard: bad argument");
     VRH_CHECK(dst->width == width && dst->height == height, "vrh_unshard: destination size mismatch");
     VRH_CHECK(gcolor || !dst->color || (gpid && k), "vrh_unshard: colour needs either gathered colour or prim ids + kernel");
+    VRH_CHECK(gcolor || !dst->color || k->kind != VRH_KERNEL_SIMPLE,
+              "vrh_unshard: shaded colour cannot be re-derived; gather the colour buffer");
     VRH_CHECK(gcolor || !dst->color || k->kind != VRH_KERNEL_AO || (gocc && k->samples <= 8),
               "vrh_unshard: re-deriving AO colour needs the gathered masks and samples <= 8");
     int rc = select_device(ctx);
