@@ -37,6 +37,11 @@
 namespace visionaray
 {
 
+// normal binding tags of make_kernel_params (tags.h:46-47), declared here so the shading kernel
+// factory can take them; the reference's (or standalone.h's) definitions complete them
+struct normals_per_face_binding;
+struct normals_per_vertex_binding;
+
 struct hip_error : std::runtime_error
 {
     int status;
@@ -124,6 +129,18 @@ public:
                                            face_normals, &s),
                           "vrh_scene_upload");
         scene_.reset(s, [](vrh_scene* p) { vrh_scene_free(p); });
+    }
+
+    // normals_per_vertex_binding array (get_shading_normal.h:64-84): 3 per primitive, entry
+    // 3 * prim_id + k for vertex k; any container of vec3-likes (x, y, z)
+    template <typename Normals>
+    void set_vertex_normals(Normals const& normals)
+    {
+        std::vector<float> rows;
+        rows.reserve(4 * normals.size());
+        for (auto const& n : normals) { rows.push_back(n.x); rows.push_back(n.y); rows.push_back(n.z); rows.push_back(0.0f); }
+        hip_detail::check(vrh_scene_set_vertex_normals(handle(), rows.data(), uint32_t(normals.size())),
+                          "vrh_scene_set_vertex_normals");
     }
 
     vrh_scene* handle() const { return scene_.get(); }
@@ -251,6 +268,105 @@ hip_builtin_kernel make_hip_ao_kernel(BVH const& bvh, Vec4 const& bg, unsigned s
 }
 
 //-------------------------------------------------------------------------------------------------
+// Shading: materials + lights of make_kernel_params (kernels.h:357-389)
+// on the device, and the simple::kernel (detail/simple.inl:19-83) built-in.
+//
+
+namespace hip_detail
+{
+template <typename S, typename = void> struct has_samples : std::false_type {};
+template <typename S> struct has_samples<S, decltype((void)std::declval<S>().samples())> : std::true_type {};
+
+// rgb of a spectrum<float> (RGB spectrum: samples() is a vec3, spectrum.h:25-36) or of a vec3
+template <typename S>
+void rgb(S const& s, float out[3])
+{
+    if constexpr (has_samples<S>::value) { auto v = s.samples(); out[0] = v.x; out[1] = v.y; out[2] = v.z; }
+    else { out[0] = s.x; out[1] = s.y; out[2] = s.z; }
+}
+
+// plastic<float> through its getters (material.h:297-316)
+template <typename M>
+vrh_plastic to_plastic(M const& m)
+{
+    vrh_plastic p{};
+    rgb(m.get_ca(), p.ca); p.ka = m.get_ka();
+    rgb(m.get_cd(), p.cd); p.kd = m.get_kd();
+    rgb(m.get_cs(), p.cs); p.ks = m.get_ks();
+    p.exp = m.get_specular_exp();
+    return p;
+}
+inline vrh_plastic to_plastic(vrh_plastic const& m) { return m; }
+
+// point_light<float> (point_light.h:18-66) has no cl / kl getters; with the default constant
+// attenuation 1, intensity(position()) is exactly cl * kl (point_light.inl:12-28).  Other
+// attenuations: pass vrh_point_light records instead.
+template <typename L>
+vrh_point_light to_point_light(L const& l)
+{
+    if (l.constant_attenuation() != 1.0f)
+        throw hip_error("point_light with constant attenuation != 1: pass vrh_point_light records", VRH_ERR_INVALID);
+    vrh_point_light r{};
+    auto pos = l.position();
+    r.position[0] = pos.x; r.position[1] = pos.y; r.position[2] = pos.z;
+    auto i = l.intensity(pos);
+    r.cl[0] = i.x; r.cl[1] = i.y; r.cl[2] = i.z;
+    r.kl = 1.0f;
+    r.constant_att = 1.0f;
+    r.linear_att = l.linear_attenuation();
+    r.quadratic_att = l.quadratic_attenuation();
+    return r;
+}
+inline vrh_point_light to_point_light(vrh_point_light const& l) { return l; }
+
+inline uint32_t binding_of(normals_per_face_binding const&) { return VRH_NORMALS_PER_FACE; }
+inline uint32_t binding_of(normals_per_vertex_binding const&) { return VRH_NORMALS_PER_VERTEX; }
+} // hip_detail
+
+// device materials (plastic, indexed by geom_id) and point lights
+class hip_shading
+{
+public:
+    template <typename Materials, typename Lights>
+    hip_shading(Materials const& materials, Lights const& lights,
+                std::shared_ptr<hip_context> ctx = hip_context::default_context())
+        : ctx_(std::move(ctx))
+    {
+        std::vector<vrh_plastic> m;
+        for (auto const& x : materials) m.push_back(hip_detail::to_plastic(x));
+        std::vector<vrh_point_light> l;
+        for (auto const& x : lights) l.push_back(hip_detail::to_point_light(x));
+        vrh_shading* s = nullptr;
+        hip_detail::check(vrh_shading_create(ctx_->get(), m.data(), uint32_t(m.size()), l.data(), uint32_t(l.size()), &s),
+                          "vrh_shading_create");
+        shading_.reset(s, [](vrh_shading* p) { vrh_shading_free(p); });
+    }
+
+    vrh_shading* handle() const { return shading_.get(); }
+
+private:
+    std::shared_ptr<hip_context> ctx_;
+    std::shared_ptr<vrh_shading> shading_;
+};
+
+// simple::kernel over make_kernel_params(binding, prims, normals, materials, lights, bounces, eps,
+// bg, ambient): the normals live in the hip_index_bvh (face normals at upload, per-vertex normals
+// via set_vertex_normals), materials / lights in the hip_shading
+template <typename NormalBinding, typename BVH, typename Vec4>
+hip_builtin_kernel make_hip_simple_kernel(NormalBinding const& binding, BVH const& bvh, hip_shading const& shading,
+                                          Vec4 const& bg, Vec4 const& ambient)
+{
+    hip_builtin_kernel k{ bvh.handle(), {} };
+    k.desc.kind = VRH_KERNEL_SIMPLE;
+    k.desc.bg[0] = bg.x; k.desc.bg[1] = bg.y; k.desc.bg[2] = bg.z; k.desc.bg[3] = bg.w;
+    k.desc.ambient[0] = ambient.x; k.desc.ambient[1] = ambient.y; k.desc.ambient[2] = ambient.z;
+    k.desc.ambient[3] = ambient.w;
+    k.desc.normal_binding = hip_detail::binding_of(binding);
+    k.desc.shading = shading.handle();
+    return k;
+}
+
+//-------------------------------------------------------------------------------------------------
 // hip_sched<R>: cuda_sched<R> replacement (persistent-thread HIP kernels, tile work stealing)
 //
 
@@ -269,7 +385,8 @@ public:
     void frame(K kernel, SP sparams, unsigned frame_num = 0, vrh_shard const* shard = nullptr)
     {
         static_assert(std::is_same<K, hip_builtin_kernel>::value,
-                      "hip_sched runs the built-in kernels (make_hip_closest_hit_kernel / make_hip_ao_kernel): "
+                      "hip_sched runs the built-in kernels (make_hip_closest_hit_kernel / make_hip_ao_kernel / "
+                      "make_hip_simple_kernel): "
                       "an arbitrary callable cannot cross the C ABI");
         auto const& cam = sparams.cam;
         auto& rt = sparams.rt;

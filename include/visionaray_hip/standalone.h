@@ -33,6 +33,11 @@ struct alignas(16) vec4
 };
 
 struct basic_ray_float {};                 // tag standing in for basic_ray<float> (hip_sched<R>)
+
+// normal binding tags (tags.h:44-47)
+struct normal_binding {};
+struct normals_per_face_binding : normal_binding {};
+struct normals_per_vertex_binding : normal_binding {};
 using ray = basic_ray_float;
 
 // basic_triangle<3,float>: geom_id@0 prim_id@4 v1@16 e1@32 e2@48 (64 B)

@@ -57,3 +57,28 @@ def test_reference_api_program_on_hip_backend(golden):
     out = _run(DROPIN, 200, g["W"], g["H"])
     for k in ("primid_hash", "t_hash", "occ_hash", "color_hash"):
         assert out[k] == g[k], k
+
+
+DROPIN_SHADE = os.path.join(ROOT, "oracle", "_ref", "dropin_simple_kernel")
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/include"), reason="reference headers absent")
+def test_cpp_shading_drop_in_compiles_against_reference_headers():
+    src = os.path.join(ROOT, "tests", "cpp", "drop_in_simple_kernel.cpp")
+    subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-w", "-I/root/reference/include",
+                    "-I", os.path.join(ROOT, "include"), src], check=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(DROPIN_SHADE), reason="drop-in binary is built in the build container only")
+@pytest.mark.parametrize("binding", ["face", "vertex"])
+def test_reference_shading_objects_on_hip_backend(golden, tmp_path, binding):
+    """The reference's plastic<float> / point_light<float> objects through hip_shading +
+    make_hip_simple_kernel reproduce the reference's simple::kernel frame (radiance within 1e-5)."""
+    import numpy as np
+    g = golden["shade_hf64_" + binding]
+    out_bin = tmp_path / "color.bin"
+    _run(DROPIN_SHADE, 64, g["W"], g["H"], binding, out_bin)
+    got = np.fromfile(out_bin, np.float32).reshape(-1, 4)
+    ref = np.load(os.path.join(ROOT, "tests", "golden", "shade_hf64_%s.npz" % binding))["color"]
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=0.0)
