@@ -225,6 +225,16 @@ public:
         hip_detail::check(vrh_rt_download(ctx_->get(), rt_.get(), rgba, prim_id, t, occ), "vrh_rt_download");
     }
 
+    // hit lists of multi_hit<N> kernels: entry [pixel * N + k], misses 0xFFFFFFFF / -1
+    void enable_multi_hit(unsigned max_hits)
+    {
+        hip_detail::check(vrh_rt_alloc_multi_hit(ctx_->get(), rt_.get(), max_hits), "vrh_rt_alloc_multi_hit");
+    }
+    void download_multi_hit(uint32_t* prim_ids, float* t)
+    {
+        hip_detail::check(vrh_rt_download_multi_hit(ctx_->get(), rt_.get(), prim_ids, t), "vrh_rt_download_multi_hit");
+    }
+
     vrh_rt* handle() const { return rt_.get(); }
 
 private:
@@ -366,6 +376,21 @@ hip_builtin_kernel make_hip_simple_kernel(NormalBinding const& binding, BVH cons
     return k;
 }
 
+// multi_hit<N> (traverse_linear.inl:333-380) with the compositing kernel of the reference's
+// multi_hit example (examples/multi_hit/main.cpp:166-235); the N-entry hit lists land in the render
+// target (hip_buffer_rt::enable_multi_hit(N), download_multi_hit)
+template <unsigned N, typename NormalBinding, typename BVH, typename Vec4>
+hip_builtin_kernel make_hip_multi_hit_kernel(NormalBinding const& binding, BVH const& bvh, hip_shading const& shading,
+                                             Vec4 const& bg)
+{
+    static_assert(N >= 1 && N <= VRH_MAX_HITS, "multi_hit<N>: 1 <= N <= 16");
+    hip_builtin_kernel k = make_hip_simple_kernel(binding, bvh, shading, bg, bg);
+    k.desc.kind = VRH_KERNEL_MULTI_HIT;
+    k.desc.ambient[0] = k.desc.ambient[1] = k.desc.ambient[2] = k.desc.ambient[3] = 0.0f;
+    k.desc.max_hits = N;
+    return k;
+}
+
 //-------------------------------------------------------------------------------------------------
 // hip_sched<R>: cuda_sched<R> replacement (persistent-thread HIP kernels, tile work stealing)
 //
@@ -386,7 +411,7 @@ public:
     {
         static_assert(std::is_same<K, hip_builtin_kernel>::value,
                       "hip_sched runs the built-in kernels (make_hip_closest_hit_kernel / make_hip_ao_kernel / "
-                      "make_hip_simple_kernel): "
+                      "make_hip_simple_kernel / make_hip_multi_hit_kernel): "
                       "an arbitrary callable cannot cross the C ABI");
         auto const& cam = sparams.cam;
         auto& rt = sparams.rt;

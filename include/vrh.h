@@ -60,9 +60,13 @@ enum vrh_prim_kind {
 enum vrh_kernel_kind {
     VRH_KERNEL_PRIMARY = 0,   /* closest_hit primary visibility: colour = hit ? 1 : bg     */
     VRH_KERNEL_AO = 1,        /* ao/main.cpp:183-246 with the Appendix-A counter sampler  */
-    VRH_KERNEL_SIMPLE = 2     /* simple::kernel (detail/simple.inl:19-83): closest hit, then
+    VRH_KERNEL_SIMPLE = 2,    /* simple::kernel (detail/simple.inl:19-83): closest hit, then
                                  ambient + one plastic::shade per point light, two-sided  */
+    VRH_KERNEL_MULTI_HIT = 3  /* multi_hit<N> (traverse_linear.inl:333-380, detail/multi_hit.h):
+                                 the N closest hits per pixel (render-target hit lists) and the
+                                 front-to-back compositing kernel of examples/multi_hit/main.cpp */
 };
+#define VRH_MAX_HITS 16
 
 enum vrh_normal_binding {
     VRH_NORMALS_PER_FACE = 0,    /* normals_per_face_binding: face normals[prim_id] (upload)  */
@@ -101,10 +105,12 @@ typedef struct {
     float    eps;             /* AO origin offset along the sample direction (1e-3)        */
     float    bg[4];           /* miss colour                                               */
     uint32_t flags;           /* vrh_kernel_flags                                          */
-    /* VRH_KERNEL_SIMPLE only (make_kernel_params arguments, kernels.h:357-389) */
+    /* VRH_KERNEL_SIMPLE / MULTI_HIT (make_kernel_params arguments, kernels.h:357-389) */
     uint32_t normal_binding;  /* vrh_normal_binding                                        */
     float    ambient[4];      /* ambient_color (RGBA; rgb scaled by a, spectrum.inl:375)   */
     const vrh_shading* shading;   /* materials + lights (vrh_shading_create)              */
+    uint32_t max_hits;        /* VRH_KERNEL_MULTI_HIT: N (1..VRH_MAX_HITS)                  */
+    uint32_t reserved;
 } vrh_kernel_desc;
 
 enum vrh_kernel_flags {
@@ -221,6 +227,10 @@ VRH_API int vrh_rt_wrap(vrh_ctx* ctx, uint32_t width, uint32_t height, void* col
 VRH_API int vrh_rt_get_buffers(const vrh_rt* rt, void** color, uint32_t** prim_id, float** t, uint8_t** occ);
 VRH_API int vrh_rt_clear(vrh_ctx* ctx, vrh_rt* rt, const float color[4]);
 VRH_API int vrh_rt_free(vrh_rt* rt);
+/* multi_hit<N> hit lists of a render target: W*H*N prim ids and t, entry [pixel * N + k] is the
+ * k-th closest hit (misses: 0xFFFFFFFF / -1) */
+VRH_API int vrh_rt_alloc_multi_hit(vrh_ctx* ctx, vrh_rt* rt, uint32_t max_hits);
+VRH_API int vrh_rt_download_multi_hit(vrh_ctx* ctx, vrh_rt* rt, uint32_t* prim_ids, float* t);   /* syncs */
 
 /* one frame (asynchronous on the context stream); shard may be NULL (= whole image) */
 VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* scene, vrh_rt* rt, const vrh_camera* cam,

@@ -27,7 +27,7 @@ NODE_DTYPE = np.dtype([("bmin", "<f4", 3), ("first", "<u4"), ("bmax", "<f4", 3),
 assert TRI_DTYPE.itemsize == 64 and SPHERE_DTYPE.itemsize == 48 and NODE_DTYPE.itemsize == 32
 
 VO_TRI, VO_SPHERE = 0, 1
-VO_MODE_PRIMARY, VO_MODE_AO, VO_MODE_SIMPLE = 0, 1, 2
+VO_MODE_PRIMARY, VO_MODE_AO, VO_MODE_SIMPLE, VO_MODE_MULTI_HIT = 0, 1, 2, 3
 VO_NORMALS_PER_FACE, VO_NORMALS_PER_VERTEX = 0, 1
 # plastic<float> / point_light<float> parameter records (vrh_oracle.h vo_plastic / vo_point_light)
 PLASTIC_DTYPE = np.dtype([("ca", "<f4", 3), ("ka", "<f4"), ("cd", "<f4", 3), ("kd", "<f4"), ("cs", "<f4", 3),
@@ -59,7 +59,7 @@ class _Kernel(C.Structure):
     _fields_ = [("mode", C.c_int), ("samples", C.c_int), ("radius", C.c_float), ("eps", C.c_float),
                 ("bg", C.c_float * 4), ("materials", C.c_void_p), ("num_materials", C.c_int),
                 ("lights", C.c_void_p), ("num_lights", C.c_int), ("ambient", C.c_float * 4),
-                ("normal_binding", C.c_int)]
+                ("normal_binding", C.c_int), ("max_hits", C.c_int)]
 
 
 _lib = None
@@ -92,6 +92,8 @@ def lib():
         L.vo_render_pixels.restype = C.c_uint64
         L.vo_fnv1a.argtypes = [vp, sz, C.c_uint64]; L.vo_fnv1a.restype = C.c_uint64
         L.vo_vertex_normals.argtypes = [vp, sz, vp]; L.vo_vertex_normals.restype = None
+        L.vo_render_multi.argtypes = [C.POINTER(_Scene), C.POINTER(_Camera), C.POINTER(_Kernel), vp, vp, vp, C.c_int]
+        L.vo_render_multi.restype = C.c_uint64
         _lib = L
     return _lib
 
@@ -114,6 +116,8 @@ SCENES = {
 def scene_spec(name):
     if name in SCENES:
         return SCENES[name]
+    if name.startswith("hfstack"):
+        return (VO_TRI, int(name[7:].split("x")[0]), (0.0, 0.9, 1.4), 1920, 1080)
     if name.startswith("hf"):
         return (VO_TRI, int(name[2:]), (0.0, 0.9, 1.4), 1920, 1080)
     if name.startswith("sph"):
@@ -124,6 +128,16 @@ def scene_spec(name):
 def gen_prims(name):
     kind, param, _, _, _ = scene_spec(name)
     L = lib()
+    if name.startswith("hfstack"):
+        # K copies of hf<G>, layer k shifted down by 0.03 * k (ref_harness.cpp make_hfstack)
+        layers = int(name.split("x")[1])
+        _, one = gen_prims("hf%d" % param)
+        out = np.concatenate([one] * layers)
+        for k in range(layers):
+            blk = out[k * len(one):(k + 1) * len(one)]
+            blk["v1"][:, 1] = blk["v1"][:, 1] - np.float32(0.03) * np.float32(k)
+            blk["prim_id"] = np.arange(k * len(one), (k + 1) * len(one), dtype=np.uint32)
+        return kind, out
     if kind == VO_TRI:
         if param == 0:
             a = np.zeros(12, TRI_DTYPE)
@@ -193,7 +207,7 @@ def make_scene(name):
 
 
 def _structs(scene, cam, mode, samples=8, radius=0.1, eps=1e-3, bg=(0.1, 0.2, 0.3, 1.0), materials=None,
-             lights=None, ambient=(0.0, 0.0, 0.0, 0.0), binding=VO_NORMALS_PER_FACE):
+             lights=None, ambient=(0.0, 0.0, 0.0, 0.0), binding=VO_NORMALS_PER_FACE, max_hits=0):
     s = _Scene(_p(scene.nodes).value, _p(scene.indices).value, _p(scene.prims).value, scene.kind,
                _p(scene.normals).value if scene.normals is not None else None,
                _p(scene.vertex_normals).value if scene.vertex_normals is not None else None)
@@ -202,7 +216,7 @@ def _structs(scene, cam, mode, samples=8, radius=0.1, eps=1e-3, bg=(0.1, 0.2, 0.
     k = _Kernel(mode, samples, radius, eps, (C.c_float * 4)(*bg),
                 _p(materials).value if materials is not None else None, 0 if materials is None else len(materials),
                 _p(lights).value if lights is not None else None, 0 if lights is None else len(lights),
-                (C.c_float * 4)(*ambient), binding)
+                (C.c_float * 4)(*ambient), binding, max_hits)
     _structs.keep = (materials, lights)
     return s, c, k
 
@@ -279,6 +293,27 @@ def render_simple(scene, cam, binding, rows=None, threads=0):
     m, lt, amb, bg = shade_spec()
     return render(scene, cam, mode=VO_MODE_SIMPLE, rows=rows, threads=threads, materials=m, lights=lt,
                   ambient=amb, bg=bg, binding=binding)
+
+
+def render_multi(scene, cam, binding, max_hits=16, threads=0):
+    """multi_hit<max_hits> frame: hit lists (W*H, max_hits) + the multi_hit example's colour."""
+    m, lt, amb, bg = shade_spec()
+    _, _, _, _, W, H = cam
+    out = {"color": np.zeros((H * W, 4), np.float32),
+           "mh_prim_id": np.full((H * W, max_hits), 0xFFFFFFFF, np.uint32),
+           "mh_t": np.full((H * W, max_hits), -1.0, np.float32)}
+    s, c, k = _structs(scene, cam, VO_MODE_MULTI_HIT, materials=m, lights=lt, ambient=amb, bg=bg, binding=binding,
+                       max_hits=max_hits)
+    lib().vo_render_multi(C.byref(s), C.byref(c), C.byref(k), _p(out["color"]), _p(out["mh_prim_id"]),
+                          _p(out["mh_t"]), threads)
+    return out
+
+
+def ref_multi(name, outdir, binding, W=None, H=None):
+    args = [REF_BIN, "multi", name, outdir, "vertex" if binding == VO_NORMALS_PER_VERTEX else "face"]
+    args += [str(W), str(H)] if W else []
+    r = subprocess.run(args, check=True, capture_output=True, text=True)
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def ref_shade(name, outdir, binding, W=None, H=None):

@@ -14,6 +14,11 @@
 //                                    by geom_id (= prim index % 3) and two point lights (the spec in
 //                                    shade_spec() below, mirrored by tests/shading_spec.py), colour
 //                                    frame written as color.bin + hash.
+//   multi  <scene> <outdir> <face|vertex> [W H]
+//                                  : multi_hit<16> (traverse_linear.inl:333-380) per pixel over the
+//                                    shade-mode scene, hit lists (prim_id / t) + the compositing
+//                                    kernel of examples/multi_hit/main.cpp:166-235 (restated on the
+//                                    reference's get_surface / plastic::shade).
 //   bench  <scene> <threads> <frames> [W H] [samples]
 //                                  : the reference SSE4 CPU path, tiled_sched<basic_ray<simd::float4>>
 //                                    (tiled_sched.inl:365-391) running the ao/main.cpp:183-246 kernel
@@ -100,6 +105,23 @@ static void make_heightfield(int grid, aligned_vector<tri_t>& tris)
     }
 }
 
+// hfstack<G>x<K>: K copies of hf<G>, layer k shifted down by 0.03 * k (prim_id = k * n + i): rays
+// from above cross many layers (multi-hit tests)
+static void make_hfstack(int grid, int layers, aligned_vector<tri_t>& tris)
+{
+    aligned_vector<tri_t> one;
+    make_heightfield(grid, one);
+    tris.resize(one.size() * layers);
+    for (int k = 0; k < layers; ++k)
+        for (size_t i = 0; i < one.size(); ++i)
+        {
+            tri_t t = one[i];
+            t.v1.y = t.v1.y - 0.03f * float(k);
+            t.prim_id = unsigned(size_t(k) * one.size() + i);
+            tris[size_t(k) * one.size() + i] = t;
+        }
+}
+
 static void make_cornell(aligned_vector<tri_t>& tris)
 {
     const float q[6][4][3] = {
@@ -169,6 +191,7 @@ struct scene_desc
     bool spheres = false;
     int  grid = 0;        // heightfield grid, 0 = cornell
     int  nspheres = 0;
+    int  layers = 0;      // hfstack
     vec3 eye;
     int  W = 1920, H = 1080;
 };
@@ -181,6 +204,12 @@ static scene_desc lookup(std::string const& name)
     else if (name == "hf1M")  { d.grid = 708;  d.eye = vec3(0.0f, 0.9f, 1.4f); }
     else if (name == "hf10M") { d.grid = 2236; d.eye = vec3(0.0f, 0.9f, 1.4f); }
     else if (name == "sph1M") { d.spheres = true; d.nspheres = 1000000; d.eye = vec3(0.0f, 0.0f, 3.5f); }
+    else if (name.compare(0, 7, "hfstack") == 0)
+    {
+        d.grid = atoi(name.c_str() + 7);
+        d.layers = atoi(strchr(name.c_str(), 'x') + 1);
+        d.eye = vec3(0.0f, 0.9f, 1.4f);
+    }
     else if (name.compare(0, 2, "hf") == 0) { d.grid = atoi(name.c_str() + 2); d.eye = vec3(0.0f, 0.9f, 1.4f); }
     else if (name.compare(0, 3, "sph") == 0) { d.spheres = true; d.nspheres = atoi(name.c_str() + 3); d.eye = vec3(0.0f, 0.0f, 3.5f); }
     else { fprintf(stderr, "unknown scene %s\n", name.c_str()); exit(2); }
@@ -430,6 +459,104 @@ static int run_shade(scene_desc const& d, aligned_vector<tri_t>& prims, std::vec
 }
 
 //-------------------------------------------------------------------------------------------------
+// multi: multi_hit<16> hit lists + the multi_hit example's compositing
+//
+
+template <typename Params>
+static void run_multi_frame(Params const& params, camera const& cam, int W, int H, std::string const& outdir)
+{
+    constexpr int N = 16;
+    simple_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> rt;
+    rt.resize(W, H);
+    auto sparams = make_sched_params(pixel_sampler::uniform_type{}, cam, rt);
+    simple_sched<ray> sched;
+    size_t npx = size_t(W) * H;
+    std::vector<uint32_t> mh_pid(npx * N, 0xFFFFFFFFu);
+    std::vector<float> mh_t(npx * N, -1.0f);
+    sched.frame([&](ray r, unsigned x, unsigned y) -> result_record<float>
+    {
+        using S = float;
+        using C = vector<4, S>;
+        using V = vector<3, S>;
+        result_record<S> result;
+        result.color = C(0.0);
+        auto hit_rec = multi_hit<N>(r, params.prims.begin, params.prims.end);
+        size_t p = size_t(y) * W + x;
+        for (int i = 0; i < N; ++i)
+        {
+            if (!hit_rec[i].hit) break;
+            mh_pid[p * N + i] = hit_rec[i].prim_id;
+            mh_t[p * N + i] = hit_rec[i].t;
+        }
+        result.hit = hit_rec[0].hit;
+        result.isect_pos = r.ori + r.dir * hit_rec[0].t;
+        for (size_t i = 0; i < hit_rec.size(); ++i)
+        {
+            if (!hit_rec[i].hit) break;
+            hit_rec[i].isect_pos = r.ori + r.dir * hit_rec[i].t;
+            auto surf = get_surface(hit_rec[i], params);
+            auto view_dir = -r.dir;
+            auto n = surf.shading_normal;
+            n = faceforward(n, view_dir, surf.geometric_normal);
+            auto it = params.lights.begin;
+            auto sr = make_shade_record<Params, S>();
+            sr.active = hit_rec[i].hit;
+            sr.isect_pos = hit_rec[i].isect_pos;
+            sr.normal = n;
+            sr.view_dir = view_dir;
+            sr.light_dir = normalize(V(it->position()) - hit_rec[i].isect_pos);
+            sr.light = *it;
+            auto shaded_clr = surf.shade(sr);
+            auto color = to_rgba(shaded_clr);
+            color.w = S(0.3);
+            color.xyz() *= color.w;
+            result.color += select(hit_rec[i].hit, color * (1.0f - result.color.w), C(0.0));
+        }
+        return result;
+    }, sparams);
+    write_file(outdir + "/color.bin", rt.color(), npx * 16);
+    write_file(outdir + "/mh_prim_id.bin", mh_pid.data(), mh_pid.size() * 4);
+    write_file(outdir + "/mh_t.bin", mh_t.data(), mh_t.size() * 4);
+    fnv hc, hp, ht;
+    hc.bytes(rt.color(), npx * 16);
+    hp.bytes(mh_pid.data(), mh_pid.size() * 4);
+    ht.bytes(mh_t.data(), mh_t.size() * 4);
+    size_t hits = 0;
+    for (auto v : mh_pid) hits += v != 0xFFFFFFFFu;
+    printf("{\"W\":%d,\"H\":%d,\"max_hits\":%d,\"hits\":%zu,\"color_hash\":\"%016llx\","
+           "\"mh_primid_hash\":\"%016llx\",\"mh_t_hash\":\"%016llx\"}\n", W, H, N, hits,
+           (unsigned long long)hc.h, (unsigned long long)hp.h, (unsigned long long)ht.h);
+}
+
+static int run_multi(scene_desc const& d, aligned_vector<tri_t>& prims, std::vector<vec3> const& face_normals,
+                     std::string const& outdir, bool per_vertex, int W, int H)
+{
+    for (size_t i = 0; i < prims.size(); ++i) prims[i].geom_id = unsigned(i % 3);
+    auto bvh = build<index_bvh<tri_t>>(prims.data(), prims.size());
+    using bvh_ref = typename index_bvh<tri_t>::bvh_ref;
+    std::vector<bvh_ref> bvhs{ bvh.ref() };
+    std::vector<vec3> vnormals(prims.size() * 3);
+    for (size_t k = 0; k < prims.size(); ++k)
+        for (uint32_t j = 0; j < 3; ++j)
+        {
+            uint32_t b = (uint32_t(k) * 3u + j) * 3u;
+            vec3 p((U(b) - 0.5f) * 0.4f, (U(b + 1) - 0.5f) * 0.4f, (U(b + 2) - 0.5f) * 0.4f);
+            vnormals[k * 3 + j] = normalize(face_normals[k] + p);
+        }
+    shade_spec sp = make_shade_spec();
+    camera cam = make_camera(d, W, H);
+    if (per_vertex)
+        run_multi_frame(make_kernel_params(normals_per_vertex_binding{}, bvhs.data(), bvhs.data() + bvhs.size(),
+                                           vnormals.data(), sp.materials.data(), sp.lights.data(),
+                                           sp.lights.data() + sp.lights.size()), cam, W, H, outdir);
+    else
+        run_multi_frame(make_kernel_params(normals_per_face_binding{}, bvhs.data(), bvhs.data() + bvhs.size(),
+                                           face_normals.data(), sp.materials.data(), sp.lights.data(),
+                                           sp.lights.data() + sp.lights.size()), cam, W, H, outdir);
+    return 0;
+}
+
+//-------------------------------------------------------------------------------------------------
 // bench: reference SSE4 tiled_sched<ray4> path, ao/main.cpp kernel
 //
 
@@ -532,7 +659,7 @@ static int with_scene(scene_desc const& d, F&& f)
         return f(s, normals);
     }
     aligned_vector<tri_t> t;
-    if (d.grid == 0) make_cornell(t); else make_heightfield(d.grid, t);
+    if (d.grid == 0) make_cornell(t); else if (d.layers) make_hfstack(d.grid, d.layers, t); else make_heightfield(d.grid, t);
     std::vector<vec3> normals(t.size());
     for (size_t i = 0; i < t.size(); ++i) normals[i] = normalize(cross(t[i].e1, t[i].e2));
     return f(t, normals);
@@ -567,10 +694,23 @@ int main(int argc, char** argv)
         int W = argc > 6 ? atoi(argv[5]) : d.W;
         int H = argc > 6 ? atoi(argv[6]) : d.H;
         aligned_vector<tri_t> t;
-        if (d.grid == 0) make_cornell(t); else make_heightfield(d.grid, t);
+        if (d.grid == 0) make_cornell(t); else if (d.layers) make_hfstack(d.grid, d.layers, t); else make_heightfield(d.grid, t);
         std::vector<vec3> normals(t.size());
         for (size_t i = 0; i < t.size(); ++i) normals[i] = normalize(cross(t[i].e1, t[i].e2));
         return run_shade(d, t, normals, outdir, per_vertex, W, H);
+    }
+    if (mode == "multi")
+    {
+        if (argc < 5 || d.spheres) return 2;
+        std::string outdir = argv[3];
+        bool per_vertex = std::string(argv[4]) == "vertex";
+        int W = argc > 6 ? atoi(argv[5]) : d.W;
+        int H = argc > 6 ? atoi(argv[6]) : d.H;
+        aligned_vector<tri_t> t;
+        if (d.grid == 0) make_cornell(t); else if (d.layers) make_hfstack(d.grid, d.layers, t); else make_heightfield(d.grid, t);
+        std::vector<vec3> normals(t.size());
+        for (size_t i = 0; i < t.size(); ++i) normals[i] = normalize(cross(t[i].e1, t[i].e2));
+        return run_multi(d, t, normals, outdir, per_vertex, W, H);
     }
     if (mode == "bench")
     {

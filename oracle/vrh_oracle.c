@@ -489,6 +489,79 @@ out:
     return res;
 }
 
+int vo_intersect_multi(const float ori_[3], const float dir_[3], const vo_node* nodes, const uint32_t* indices,
+                       const void* prims, int kind, int n, vo_hit* res, vo_counters* cnt)
+{
+    v3 ori = mk(ori_[0], ori_[1], ori_[2]);
+    v3 dir = mk(dir_[0], dir_[1], dir_[2]);
+    for (int k = 0; k < n; ++k) {            /* hit_record ctor: hit false, t = max() */
+        res[k].hit = 0; res[k].prim_id = 0; res[k].geom_id = 0; res[k].list_index = 0;
+        res[k].t = FLT_MAX; res[k].u = 0.0f; res[k].v = 0.0f;
+    }
+    uint64_t nbox = 0, nprim = 0;
+    uint32_t stack[4096];
+    int sp = 0;
+    stack[sp++] = 0;
+    v3 inv_dir = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+    while (sp > 0) {
+        const vo_node* node = &nodes[stack[--sp]];
+        int terminated = 0;
+        while (node->num_prims == 0) {
+            const vo_node* ch = &nodes[node->first];
+            float tn[2], tf[2]; int hb[2];
+            for (int c = 0; c < 2; ++c) {
+                v3 t1 = mul(sub(mk(ch[c].bmin[0], ch[c].bmin[1], ch[c].bmin[2]), ori), inv_dir);
+                v3 t2 = mul(sub(mk(ch[c].bmax[0], ch[c].bmax[1], ch[c].bmax[2]), ori), inv_dir);
+                tn[c] = fmax_ref(fmin_ref(t1.x, t2.x), fmax_ref(fmin_ref(t1.y, t2.y), fmin_ref(t1.z, t2.z)));
+                tf[c] = fmin_ref(fmax_ref(t1.x, t2.x), fmin_ref(fmax_ref(t1.y, t2.y), fmax_ref(t1.z, t2.z)));
+                int h = tf[c] >= tn[c];
+                /* multi_hit.h:221-244: is_closer against any kept record (max_t = max()) */
+                int closer = 0;
+                for (int k = 0; k < n && !closer; ++k)
+                    closer = h && tn[c] < res[k].t && tf[c] >= 0.0f && tn[c] < FLT_MAX;
+                hb[c] = closer;
+            }
+            nbox += 2;
+            if (hb[0] && hb[1]) {
+                unsigned near_addr = (tn[0] < tn[1]) ? 0u : 1u;
+                if (sp == 4096) goto out;
+                stack[sp++] = node->first + (near_addr ^ 1u);
+                node = &nodes[node->first + near_addr];
+            } else if (hb[0]) {
+                node = &nodes[node->first];
+            } else if (hb[1]) {
+                node = &nodes[node->first + 1];
+            } else {
+                terminated = 1;
+                break;
+            }
+        }
+        if (terminated) continue;
+        for (uint32_t i = node->first; i != node->first + node->num_prims; ++i) {
+            prim_hit hr = kind == VO_TRI ? isect_tri(ori, dir, (const vo_tri*)prims + indices[i])
+                                         : isect_sphere(ori, dir, (const vo_sphere*)prims + indices[i]);
+            ++nprim;
+            int closer = 0;
+            for (int k = 0; k < n && !closer; ++k)
+                closer = hr.hit && hr.t >= 0.0f && hr.t < res[k].t && hr.t < FLT_MAX;
+            if (!closer) continue;
+            /* update_if -> insert_sorted(hr, result, is_closer_t) (multi_hit.h:180-189, algorithm.h:46-75) */
+            int pos = n;
+            for (int k = 0; k < n; ++k)
+                if (hr.hit && hr.t >= 0.0f && hr.t < res[k].t) { pos = k; break; }
+            if (pos == n) continue;
+            for (int k = n - 1; k > pos; --k) res[k] = res[k - 1];
+            res[pos].hit = 1; res[pos].t = hr.t; res[pos].prim_id = hr.prim_id; res[pos].geom_id = hr.geom_id;
+            res[pos].u = hr.u; res[pos].v = hr.v; res[pos].list_index = i;
+        }
+    }
+out:
+    if (cnt) { cnt->box_tests += nbox; cnt->prim_tests += nprim; }
+    int hits = 0;
+    for (int k = 0; k < n; ++k) hits += res[k].hit;
+    return hits;
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* Pixel pipeline + kernels                                                                    */
 
@@ -611,6 +684,56 @@ static void shade_simple(const vo_scene* s, const vo_kernel* k, v3 ori, v3 dir, 
         shaded = add(shaded, clr);                                      /* simple.inl:63 */
     }
     out[0] = shaded.x; out[1] = shaded.y; out[2] = shaded.z; out[3] = 1.0f;   /* to_rgba */
+}
+
+/* examples/multi_hit/main.cpp:166-235: for every kept hit (in t order) the surface of
+ * get_surface(hit_rec[i], params), plastic::shade with the FIRST light (no ambient), alpha 0.3,
+ * front-to-back compositing; colour starts at 0 */
+static void shade_multi(const vo_scene* s, const vo_kernel* k, v3 ori, v3 dir, const vo_hit* hits, int n, float out[4])
+{
+    float acc[4] = { 0.0f, 0.0f, 0.0f, 0.0f };
+    for (int i = 0; i < n; ++i) {
+        if (!hits[i].hit) break;
+        float c[4];
+        vo_kernel one = *k;
+        one.num_lights = k->num_lights > 0 ? 1 : 0;
+        one.ambient[0] = one.ambient[1] = one.ambient[2] = one.ambient[3] = 0.0f;
+        shade_simple(s, &one, ori, dir, &hits[i], c);     /* ambient 0: ca*ka*0 = 0, then + shade */
+        c[3] = 0.3f;
+        c[0] = c[0] * c[3]; c[1] = c[1] * c[3]; c[2] = c[2] * c[3];
+        float f = 1.0f - acc[3];
+        for (int q = 0; q < 4; ++q) acc[q] = acc[q] + c[q] * f;
+    }
+    memcpy(out, acc, sizeof(acc));
+}
+
+uint64_t vo_render_multi(const vo_scene* s, const vo_camera* cam, const vo_kernel* k, float* color,
+                         uint32_t* mh_prim_id, float* mh_t, int threads)
+{
+    int W = cam->width, H = cam->height, n = k->max_hits;
+    if (n < 1 || n > VO_MAX_HITS) return 0;
+#ifdef _OPENMP
+    if (threads <= 0) threads = omp_get_max_threads();
+#else
+    threads = 1;
+#endif
+    #pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
+    for (int y = 0; y < H; ++y) {
+        for (int x = 0; x < W; ++x) {
+            v3 ori, dir;
+            primary_ray(cam, (unsigned)x, (unsigned)y, &ori, &dir);
+            float fo[3] = { ori.x, ori.y, ori.z }, fd[3] = { dir.x, dir.y, dir.z };
+            vo_hit hits[VO_MAX_HITS];
+            vo_intersect_multi(fo, fd, s->nodes, s->indices, s->prims, s->kind, n, hits, NULL);
+            size_t p = (size_t)y * W + x;
+            for (int i = 0; i < n; ++i) {
+                if (mh_prim_id) mh_prim_id[p * n + i] = hits[i].hit ? hits[i].prim_id : 0xFFFFFFFFu;
+                if (mh_t) mh_t[p * n + i] = hits[i].hit ? hits[i].t : -1.0f;
+            }
+            if (color) shade_multi(s, k, ori, dir, hits, n, color + 4 * p);
+        }
+    }
+    return (uint64_t)W * H;
 }
 
 void vo_vertex_normals(const vo_vec3* face_normals, size_t n, vo_vec3* out)

@@ -30,7 +30,8 @@ typedef struct { uint32_t geom_id, prim_id, pad0, pad1; vo_vec3 center; float ra
 typedef struct { float bmin[3]; uint32_t first; float bmax[3]; uint32_t num_prims; } vo_node;
 
 enum { VO_TRI = 0, VO_SPHERE = 1 };
-enum { VO_MODE_PRIMARY = 0, VO_MODE_AO = 1, VO_MODE_SIMPLE = 2 };
+enum { VO_MODE_PRIMARY = 0, VO_MODE_AO = 1, VO_MODE_SIMPLE = 2, VO_MODE_MULTI_HIT = 3 };
+enum { VO_MAX_HITS = 16 };
 enum { VO_NORMALS_PER_FACE = 0, VO_NORMALS_PER_VERTEX = 1 };
 
 /* plastic<float> (material.h:267-323, detail/material/plastic.inl): ambient ca*ka, lambertian
@@ -71,6 +72,12 @@ typedef struct { uint64_t box_tests, prim_tests; } vo_counters;
 vo_hit vo_intersect(const float ori[3], const float dir[3], const vo_node* nodes, const uint32_t* indices,
                     const void* prims, int kind, int any_hit, float max_t, vo_counters* cnt);
 
+/* multi_hit<N> (traverse_linear.inl:333-380 -> intersect<MultiHit, N>, detail/multi_hit.h): the N
+ * closest hits sorted by t (insert_sorted, algorithm.h:46-75: ties after the existing ones);
+ * boxes and primitives are tested against the N-th kept t.  out[N]; returns the hit count. */
+int vo_intersect_multi(const float ori[3], const float dir[3], const vo_node* nodes, const uint32_t* indices,
+                       const void* prims, int kind, int n, vo_hit* out, vo_counters* cnt);
+
 /* ---- a frame, simple_sched order (row-major), over rows [y0, y1) ---- */
 typedef struct {
     const vo_node* nodes; const uint32_t* indices; const void* prims; int kind;
@@ -92,6 +99,7 @@ typedef struct {
     const vo_point_light* lights; int num_lights;
     float ambient[4];
     int   normal_binding;                 /* VO_NORMALS_PER_FACE | VO_NORMALS_PER_VERTEX */
+    int   max_hits;                       /* VO_MODE_MULTI_HIT: N (<= VO_MAX_HITS) */
 } vo_kernel;
 
 /* deterministic per-vertex normals for tests: prim k, vertex j: normalize(n_k + 0.4 * (U(b) - 0.5,
@@ -103,6 +111,12 @@ void vo_vertex_normals(const vo_vec3* face_normals, size_t n, vo_vec3* out);
 uint64_t vo_render_rows(const vo_scene* s, const vo_camera* cam, const vo_kernel* k, int y0, int y1,
                         float* color, uint32_t* prim_id, float* t, uint8_t* occ, uint32_t* list_index,
                         int threads, vo_counters* cnt);
+
+/* VO_MODE_MULTI_HIT frame: per pixel the hit list (mh_prim_id / mh_t: W*H*max_hits, misses
+ * 0xFFFFFFFF / -1) and the colour of examples/multi_hit/main.cpp:166-235 (front-to-back
+ * compositing of plastic::shade with the first light, alpha 0.3). */
+uint64_t vo_render_multi(const vo_scene* s, const vo_camera* cam, const vo_kernel* k, float* color,
+                         uint32_t* mh_prim_id, float* mh_t, int threads);
 
 /* Same, for an explicit list of pixel indices (p = y*W + x); outputs are indexed by list position. */
 uint64_t vo_render_pixels(const vo_scene* s, const vo_camera* cam, const vo_kernel* k,

@@ -3,7 +3,8 @@
 Run in the build container (needs /root/reference to build the harness):
 
     make -C oracle ref && python tests/golden/make_golden.py            (everything)
-    python tests/golden/make_golden.py --shade                          (only the shading cases)
+    python tests/golden/make_golden.py --shade                          (shading + multi-hit cases)
+    python tests/golden/make_golden.py --multi                          (only the multi-hit cases)
 
 For every case the reference harness renders a full simple_sched<basic_ray<float>> frame
 (primary closest_hit + the Appendix-A AO kernel for triangle scenes) and this script stores:
@@ -50,6 +51,14 @@ SHADE_CASES = [
 ]
 
 
+# multi_hit<16> cases (harness "multi" mode): hit lists + the multi_hit example's colour
+MULTI_CASES = [
+    ("multi_cornell12_face", "cornell12", 128, 128, "face"),
+    ("multi_hfstack32x24_face", "hfstack32x24", 160, 90, "face"),
+    ("multi_hfstack32x24_vertex", "hfstack32x24", 160, 90, "vertex"),
+]
+
+
 def fnv1a(a):
     """FNV-1a 64 over the little-endian bytes (computed by the oracle's C helper for speed)."""
     sys.path.insert(0, ROOT)
@@ -75,10 +84,27 @@ def shade_cases(out, rng):
             print(case, rec["color_hash"], flush=True)
 
 
+def multi_cases(out):
+    for case, scene, W, H, binding in MULTI_CASES:
+        with tempfile.TemporaryDirectory() as d:
+            r = subprocess.run([REF, "multi", scene, d, binding, str(W), str(H)], check=True, capture_output=True,
+                               text=True)
+            info = json.loads(r.stdout.strip().splitlines()[-1])
+            color = np.fromfile(os.path.join(d, "color.bin"), np.float32).reshape(-1, 4)
+            pid = np.fromfile(os.path.join(d, "mh_prim_id.bin"), np.uint32).reshape(W * H, -1)
+            t = np.fromfile(os.path.join(d, "mh_t.bin"), np.float32).reshape(W * H, -1)
+            rec = {"scene": scene, "W": W, "H": H, "binding": binding, "max_hits": info["max_hits"],
+                   "hits": info["hits"], "color_hash": fnv1a(color), "mh_primid_hash": fnv1a(pid),
+                   "mh_t_hash": fnv1a(t)}
+            np.savez_compressed(os.path.join(HERE, case + ".npz"), color=color, mh_prim_id=pid, mh_t=t)
+            out[case] = rec
+            print(case, rec["hits"], rec["color_hash"], flush=True)
+
+
 def main():
     if not os.path.exists(REF):
         sys.exit("build the reference harness first: make -C oracle ref")
-    only_shade = "--shade" in sys.argv
+    only_shade = "--shade" in sys.argv or "--multi" in sys.argv
     path = os.path.join(HERE, "golden.json")
     out = json.load(open(path)) if only_shade else {}
     rng = np.random.default_rng(12345)
@@ -110,7 +136,9 @@ def main():
                                     occ=occ[pix], color=color[pix])
             out[case] = rec
             print(case, rec["hits"], rec["ao_occluded"], rec["primid_hash"], flush=True)
-    shade_cases(out, np.random.default_rng(54321))
+    if "--multi" not in sys.argv:
+        shade_cases(out, np.random.default_rng(54321))
+    multi_cases(out)
     with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 

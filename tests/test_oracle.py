@@ -125,3 +125,19 @@ def test_oracle_simple_kernel_matches_reference(golden, oracle_mod, case):
     ref = np.load(os.path.join(os.path.dirname(__file__), "golden", case + ".npz"))["color"]
     assert np.array_equal(out["color"].view(np.uint32), ref.view(np.uint32))
     assert O.fnv1a(out["color"]) == g["color_hash"]
+
+
+@pytest.mark.parametrize("case", ["multi_cornell12_face", "multi_hfstack32x24_face", "multi_hfstack32x24_vertex"])
+def test_oracle_multi_hit_matches_reference(golden, oracle_mod, case):
+    """multi_hit<16> restatement (insert_sorted lists + the example's compositing) bit-identical to
+    the reference's frames (tests/golden/multi_*.npz)."""
+    O = oracle_mod
+    g = golden[case]
+    sc = O.make_shade_scene(g["scene"])
+    out = O.render_multi(sc, O.scene_camera(g["scene"], g["W"], g["H"]),
+                         O.VO_NORMALS_PER_VERTEX if g["binding"] == "vertex" else O.VO_NORMALS_PER_FACE)
+    ref = np.load(os.path.join(os.path.dirname(__file__), "golden", case + ".npz"))
+    assert np.array_equal(out["mh_prim_id"], ref["mh_prim_id"])
+    assert np.array_equal(out["mh_t"].view(np.uint32), ref["mh_t"].view(np.uint32))
+    assert np.array_equal(out["color"].view(np.uint32), ref["color"].view(np.uint32))
+    assert O.fnv1a(out["color"]) == g["color_hash"]

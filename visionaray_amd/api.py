@@ -282,6 +282,18 @@ class hip_buffer_rt:
         capi.check("vrh_rt_get_buffers", self.handle, *[C.byref(b) for b in bufs])
         return tuple(b.value for b in bufs)
 
+    def alloc_multi_hit(self, max_hits):
+        """Hit-list side buffers of multi_hit<max_hits> (W * H * max_hits prim ids and t)."""
+        capi.check("vrh_rt_alloc_multi_hit", self.ctx.handle, self.handle, max_hits)
+        self.max_hits = max_hits
+
+    def download_multi_hit(self):
+        n = self.w * self.h * self.max_hits
+        pid = np.empty(n, np.uint32)
+        t = np.empty(n, np.float32)
+        capi.check("vrh_rt_download_multi_hit", self.ctx.handle, self.handle, _p(pid), _p(t))
+        return {"mh_prim_id": pid.reshape(-1, self.max_hits), "mh_t": t.reshape(-1, self.max_hits)}
+
     def download(self, color=True, prim_id=True, t=True, occ=True):
         n = self.w * self.h
         has = self.device_buffers()
@@ -426,6 +438,17 @@ def simple_kernel(bvh, shade, binding=normals_per_face_binding, bg=(0.0, 0.0, 0.
     k.desc.ambient = (C.c_float * 4)(*ambient)
     k.desc.shading = shade.handle
     k.shade = shade          # keep the device arrays alive
+    return k
+
+
+def multi_hit_kernel(bvh, shade, max_hits=16, binding=normals_per_vertex_binding, bg=(0.0, 0.0, 0.0, 0.0),
+                     count_tests=False):
+    """multi_hit<max_hits> (traverse_linear.inl:333-380): the max_hits closest hits per pixel into
+    the render target's hit lists (hip_buffer_rt.alloc_multi_hit) and the colour of the multi_hit
+    example kernel (examples/multi_hit/main.cpp:166-235: first light, alpha 0.3, front to back)."""
+    k = simple_kernel(bvh, shade, binding=binding, bg=bg, count_tests=count_tests)
+    k.desc.kind = capi.VRH_KERNEL_MULTI_HIT
+    k.desc.max_hits = max_hits
     return k
 
 

@@ -24,6 +24,7 @@
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <type_traits>
 
 #ifndef VRH_PACKED_SLABS
 #define VRH_PACKED_SLABS 0   // 1: slab distances with v_pk_add_f32 / v_pk_mul_f32
@@ -240,13 +241,13 @@ __device__ __forceinline__ bool quad_entry(float xl, float yl, float zl, float x
 // records instead: the same set of leaves is reached (vrh_quad.cpp), the order does not matter
 // for an any-hit result, and the nearest hit entry is descended first.  If a record's hits could
 // overflow the stack, the ray restarts on the binary records from `root` (still exact).
-template <int KIND, bool COUNT, bool FAST, bool UV = false>
+template <int KIND, bool COUNT, bool FAST, bool UV = false, class MultiList = void>
 __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const float4* __restrict__ prims,
                                         const float4* __restrict__ quads, uint32_t root, bool& quad,
                                         const ray_t& r, float max_t, bool any, lds_stack& st,
                                         float& best_t, uint32_t& best_prim, test_counts& cnt,
                                         uint32_t& steps, uint32_t step_limit, uint32_t& resume, uint32_t cap,
-                                        hit_extra* hx = nullptr)
+                                        hit_extra* hx = nullptr, const MultiList* mh = nullptr)
 {
     // the tree was validated at upload (no cycles, links in range), so the descent terminates;
     // the guard below only bounds the number of outer iterations per ray
@@ -341,10 +342,19 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
         if (COUNT) { cnt.prim += 1; cnt.it_prim += 1; }
         if (h & (t >= 0.0f) & (t < best_t) & (t < max_t))      // update_if.h:48-56, 73-79
         {
-            best_t = t;
-            best_prim = pid;
-            if constexpr (UV) { hx->u = hu; hx->v = hv; hx->li = i; }   // hit_record.h:54-64
-            if (any) return 1;                                   // exit_traversal.h:49-56
+            if constexpr (!std::is_void<MultiList>::value)
+            {
+                // multi_hit<N>: is_closer against the kept hits (multi_hit.h:221-244) = t below the
+                // N-th kept t (best_t), then insert_sorted; best_t becomes the new N-th t
+                best_t = mh->insert(t, pid, i, hu, hv);
+            }
+            else
+            {
+                best_t = t;
+                best_prim = pid;
+                if constexpr (UV) { hx->u = hu; hx->v = hv; hx->li = i; }   // hit_record.h:54-64
+                if (any) return 1;                               // exit_traversal.h:49-56
+            }
         }
         if (flags & END_BIT) break;
         ++i;

@@ -48,7 +48,10 @@ struct render_params
     uint32_t refill_min_primary;   // the same for the step loop's primary-only stream
     uint32_t vote_leaf;       // vote schedule: leaf step when 8 * leaf lanes >= vote_leaf * node lanes
     uint32_t descent_cap;     // step loop: inner visits per step before a descent is resumed later
-    dev::shade_params shade;  // VRH_KERNEL_SIMPLE: materials, lights, normal binding, ambient
+    dev::shade_params shade;  // VRH_KERNEL_SIMPLE / MULTI_HIT: materials, lights, normal binding, ambient
+    uint32_t max_hits;        // VRH_KERNEL_MULTI_HIT: N
+    uint32_t* mh_prim_id;     // [pixel][N] hit lists (render target side buffers)
+    float* mh_t;
 };
 
 constexpr int COUNTERS_FRAME = 80;      // u64 words reset before every frame
@@ -64,7 +67,8 @@ struct launch_config
     int stack_cap;     // LDS stack entries per lane
     int occ;           // register budget: min waves per SIMD (1, 6 or 8)
     int sched;         // 0: step loop (render_unified_kernel), 1: item loop, 2: vote loop (render_item_kernel)
-    bool shade;        // VRH_KERNEL_SIMPLE epilogue (step loop, triangles)
+    int epi;           // primary epilogue: 0 plain, 1 VRH_KERNEL_SIMPLE, 2 VRH_KERNEL_MULTI_HIT (triangles)
+    int max_hits;      // MULTI_HIT: N (LDS hit lists)
 };
 
 size_t render_lds_bytes(const launch_config& c);

@@ -126,7 +126,9 @@ __device__ __forceinline__ ray_t ao_ray(const render_params& P, const float* rec
 // instruction stream (ray_step); a lane that finishes a ray immediately takes the next one, so
 // neither the primary phase nor the AO phase waits for its slowest lane.  Without AO the wave
 // streams pixels tile after tile and writes each pixel when its ray finishes.
-template <int KIND, bool AO, bool COUNT, int OCC, bool SHADE = false>
+// EPI: primary-ray epilogue -- 0 colour = hit ? 1 : bg, 1 simple::kernel shading, 2 multi_hit<N>
+// hit lists + the multi_hit example's compositing
+template <int KIND, bool AO, bool COUNT, int OCC, int EPI = 0>
 __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params P)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -162,6 +164,11 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         uint32_t handed = 0;                       // pixels of `tile` handed out (wave-uniform)
         uint32_t out_o = 0;
         hit_extra hx = { 0.0f, 0.0f, 0u };
+        mh_list mh;
+        mh.mem = smem;
+        mh.base = P.stack_cap * block + tid;
+        mh.stride = block;
+        mh.n = EPI == 2 ? P.max_hits : 1u;
         for (;;)
         {
             uint64_t idle = __ballot(mode == IDLE);
@@ -186,6 +193,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                             finite = finite_ray(r);
                             out_o = orow * P.width + x;
                             best_t = FMAX; best_prim = 0; steps = 0;
+                            if constexpr (EPI == 2) mh.reset();
                             st.reset(); st.push(P.root); resume = NO_RESUME;
                             mode = PRIMARY;
                             rays_total += 1;
@@ -201,16 +209,31 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             const bool busy = mode != IDLE;
             if (mode != IDLE)
             {
+                using ML = typename std::conditional<EPI == 2, mh_list, void>::type;
                 int rc = (P.fast_ok && __ballot(!finite) == 0ull)
-                    ? ray_step<KIND, COUNT, true, SHADE>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, &hx)
-                    : ray_step<KIND, COUNT, false, SHADE>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, &hx);
+                    ? ray_step<KIND, COUNT, true, EPI == 1, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, &hx, &mh)
+                    : ray_step<KIND, COUNT, false, EPI == 1, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, &hx, &mh);
                 if (rc != 0)
                 {
+                    if constexpr (EPI == 2)
+                    {
+                        // multi_hit: the list's first entry is the frame's prim id / t
+                        for (uint32_t k = 0; k < mh.n; ++k)
+                        {
+                            const float tk = mh.t(k);
+                            if (P.mh_prim_id) P.mh_prim_id[size_t(out_o) * mh.n + k] = tk < FMAX ? mh.at(1, k) : 0xFFFFFFFFu;
+                            if (P.mh_t) P.mh_t[size_t(out_o) * mh.n + k] = tk < FMAX ? tk : -1.0f;
+                        }
+                        best_t = mh.t(0);
+                        best_prim = mh.at(1, 0);
+                    }
                     bool hit = best_t != FMAX;
                     hits_total += hit ? 1 : 0;
                     float4 c = hit ? make_float4(1.0f, 1.0f, 1.0f, 1.0f) : make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
-                    if constexpr (SHADE)
+                    if constexpr (EPI == 1)
                         if (hit) c = shade_simple(P.shade, P.prims, P.normals, r, best_t, best_prim, hx);
+                    if constexpr (EPI == 2)
+                        c = shade_multi(P.shade, P.prims, P.normals, r, mh);
                     if (P.color) P.color[out_o] = c;
                     if (P.prim_id) P.prim_id[out_o] = hit ? best_prim : 0xFFFFFFFFu;
                     if (P.t) P.t[out_o] = hit ? best_t : -1.0f;
@@ -716,12 +739,15 @@ static kernel_fn pick_occ(bool ao, bool count, int sched)
     return count ? dev::render_unified_kernel<KIND, true, true, OCC> : dev::render_unified_kernel<KIND, true, false, OCC>;
 }
 
-// simple::kernel epilogue: triangles, step loop
+// simple::kernel / multi_hit epilogues: triangles, step loop
 template <int OCC>
-static kernel_fn pick_shade(bool count)
+static kernel_fn pick_shade(bool count, int epi)
 {
-    return count ? dev::render_unified_kernel<dev::KIND_TRI, false, true, OCC, true>
-                 : dev::render_unified_kernel<dev::KIND_TRI, false, false, OCC, true>;
+    if (epi == 2)
+        return count ? dev::render_unified_kernel<dev::KIND_TRI, false, true, OCC, 2>
+                     : dev::render_unified_kernel<dev::KIND_TRI, false, false, OCC, 2>;
+    return count ? dev::render_unified_kernel<dev::KIND_TRI, false, true, OCC, 1>
+                 : dev::render_unified_kernel<dev::KIND_TRI, false, false, OCC, 1>;
 }
 
 template <int KIND>
@@ -734,14 +760,15 @@ static kernel_fn pick(bool ao, bool count, int occ, int sched)
 
 static kernel_fn select_variant(const launch_config& c)
 {
-    if (c.shade) return c.occ == 8 ? pick_shade<8>(c.count) : c.occ == 6 ? pick_shade<6>(c.count) : pick_shade<1>(c.count);
+    if (c.epi) return c.occ == 8 ? pick_shade<8>(c.count, c.epi) : c.occ == 6 ? pick_shade<6>(c.count, c.epi) : pick_shade<1>(c.count, c.epi);
     return c.kind == dev::KIND_TRI ? pick<dev::KIND_TRI>(c.ao, c.count, c.occ, c.sched)
                                    : pick<dev::KIND_SPHERE>(c.ao, c.count, c.occ, c.sched);
 }
 
 size_t render_lds_bytes(const launch_config& c)
 {
-    size_t words = size_t(c.stack_cap) * c.block + (c.ao ? size_t(c.block / 64) * dev::AO_WAVE_WORDS : 0);
+    size_t words = size_t(c.stack_cap) * c.block + (c.ao ? size_t(c.block / 64) * dev::AO_WAVE_WORDS : 0)
+                 + (c.epi == 2 ? size_t(5) * c.max_hits * c.block : 0);
     return words * 4;
 }
 

@@ -89,6 +89,9 @@ struct vrh_rt
     float* t = nullptr;
     uint8_t* occ = nullptr;
     bool owned = false;
+    uint32_t* mh_prim_id = nullptr;   // multi_hit<N> lists [pixel][N] (always owned)
+    float* mh_t = nullptr;
+    uint32_t mh_n = 0;
 };
 
 namespace {
@@ -490,6 +493,12 @@ VRH_API int vrh_rt_free(vrh_rt* rt)
         if (rt->t) (void)hipFree(rt->t);
         if (rt->occ) (void)hipFree(rt->occ);
     }
+    if (rt->mh_prim_id || rt->mh_t)
+    {
+        if (rt->ctx) (void)hipSetDevice(rt->ctx->device);
+        if (rt->mh_prim_id) (void)hipFree(rt->mh_prim_id);
+        if (rt->mh_t) (void)hipFree(rt->mh_t);
+    }
     delete rt;
     return VRH_OK;
 }
@@ -535,13 +544,19 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     (void)frame_num;  // the built-in kernels are deterministic; kept for cuda_sched::frame parity
     VRH_CHECK(ctx && sc && rt && cam && k, "vrh_render: null argument");
     VRH_CHECK(cam->width > 0 && cam->height > 0, "vrh_render: empty image");
-    VRH_CHECK(k->kind <= VRH_KERNEL_SIMPLE, "vrh_render: unknown kernel kind");
+    VRH_CHECK(k->kind <= VRH_KERNEL_MULTI_HIT, "vrh_render: unknown kernel kind");
     const bool ao = k->kind == VRH_KERNEL_AO;
-    const bool shade = k->kind == VRH_KERNEL_SIMPLE;
+    const bool multi = k->kind == VRH_KERNEL_MULTI_HIT;
+    const bool shade = k->kind == VRH_KERNEL_SIMPLE || multi;
+    if (multi)
+    {
+        VRH_CHECK(k->max_hits >= 1 && k->max_hits <= VRH_MAX_HITS, "vrh_render: max_hits must be in [1, 16]");
+        VRH_CHECK(rt->mh_n == k->max_hits, "vrh_render: render target needs vrh_rt_alloc_multi_hit(max_hits)");
+    }
     if (shade)
     {
-        VRH_CHECK(k->shading, "vrh_render: VRH_KERNEL_SIMPLE needs a vrh_shading (materials, lights)");
-        if (sc->info.prim_kind != VRH_PRIM_TRI64) { set_error("vrh_render: VRH_KERNEL_SIMPLE supports triangles"); return VRH_ERR_UNSUPPORTED; }
+        VRH_CHECK(k->shading, "vrh_render: the shading kernels need a vrh_shading (materials, lights)");
+        if (sc->info.prim_kind != VRH_PRIM_TRI64) { set_error("vrh_render: the shading kernels support triangles"); return VRH_ERR_UNSUPPORTED; }
         VRH_CHECK(k->shading->num_materials > sc->info.max_geom_id, "vrh_render: a geom_id has no material");
         VRH_CHECK(k->normal_binding <= VRH_NORMALS_PER_VERTEX, "vrh_render: unknown normal binding");
         if (k->normal_binding == VRH_NORMALS_PER_FACE) VRH_CHECK(sc->normals, "vrh_render: per-face shading needs face normals");
@@ -572,7 +587,8 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     lc.block = ctx->opt_block ? ctx->opt_block : 64;
     lc.stack_cap = int(cap);
     lc.occ = ctx->opt_occ ? ctx->opt_occ : 6;
-    lc.shade = shade;
+    lc.epi = multi ? 2 : shade ? 1 : 0;
+    lc.max_hits = multi ? int(k->max_hits) : 0;
     // auto: the item loop for sphere primary visibility (short leaves of cheap tests, where the
     // step loop's leaf iterations run at ~20 % lane utilisation), the step loop otherwise
     if (ctx->opt_sched == 0) lc.sched = (lc.kind == 1 && !ao) ? 1 : 0;
@@ -617,6 +633,12 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
         p.shade.per_vertex = k->normal_binding == VRH_NORMALS_PER_VERTEX ? 1u : 0u;
         p.shade.vnormals = sc->vnormals;
         std::memcpy(p.shade.ambient, k->ambient, 16);
+    }
+    if (multi)
+    {
+        p.max_hits = k->max_hits;
+        p.mh_prim_id = rt->mh_prim_id;
+        p.mh_t = rt->mh_t;
     }
 
     int per_cu = render_blocks_per_cu(lc);
@@ -733,6 +755,35 @@ VRH_API int vrh_rt_download(vrh_ctx* ctx, vrh_rt* rt, void* color, uint32_t* pri
     return VRH_OK;
 }
 
+VRH_API int vrh_rt_alloc_multi_hit(vrh_ctx* ctx, vrh_rt* rt, uint32_t max_hits)
+{
+    VRH_CHECK(ctx && rt, "vrh_rt_alloc_multi_hit: null");
+    VRH_CHECK(max_hits >= 1 && max_hits <= VRH_MAX_HITS, "vrh_rt_alloc_multi_hit: max_hits must be in [1, 16]");
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    if (rt->mh_prim_id) { (void)hipFree(rt->mh_prim_id); rt->mh_prim_id = nullptr; }
+    if (rt->mh_t) { (void)hipFree(rt->mh_t); rt->mh_t = nullptr; }
+    rt->mh_n = 0;
+    const size_t n = size_t(rt->width) * rt->height * max_hits;
+    VRH_HIP(hipMalloc(&rt->mh_prim_id, n * 4));
+    VRH_HIP(hipMalloc(&rt->mh_t, n * 4));
+    rt->mh_n = max_hits;
+    return VRH_OK;
+}
+
+VRH_API int vrh_rt_download_multi_hit(vrh_ctx* ctx, vrh_rt* rt, uint32_t* prim_ids, float* t)
+{
+    VRH_CHECK(ctx && rt, "vrh_rt_download_multi_hit: null");
+    VRH_CHECK(rt->mh_n, "vrh_rt_download_multi_hit: no multi-hit buffers (vrh_rt_alloc_multi_hit)");
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    const size_t n = size_t(rt->width) * rt->height * rt->mh_n;
+    VRH_HIP(hipStreamSynchronize(ctx->stream));
+    if (prim_ids) VRH_HIP(hipMemcpy(prim_ids, rt->mh_prim_id, n * 4, hipMemcpyDeviceToHost));
+    if (t) VRH_HIP(hipMemcpy(t, rt->mh_t, n * 4, hipMemcpyDeviceToHost));
+    return VRH_OK;
+}
+
 VRH_API int vrh_rt_upload(vrh_ctx* ctx, vrh_rt* rt, const void* color, const uint32_t* prim_id, const float* t,
                           const uint8_t* occ)
 {
@@ -755,7 +806,7 @@ VRH_API int vrh_unshard(vrh_ctx* ctx, uint32_t width, uint32_t height, uint32_t 
     VRH_CHECK(ctx && dst && count >= 1, "vrh_unshard: bad argument");
     VRH_CHECK(dst->width == width && dst->height == height, "vrh_unshard: destination size mismatch");
     VRH_CHECK(gcolor || !dst->color || (gpid && k), "vrh_unshard: colour needs either gathered colour or prim ids + kernel");
-    VRH_CHECK(gcolor || !dst->color || k->kind != VRH_KERNEL_SIMPLE,
+    VRH_CHECK(gcolor || !dst->color || k->kind < VRH_KERNEL_SIMPLE,
               "vrh_unshard: shaded colour cannot be re-derived; gather the colour buffer");
     VRH_CHECK(gcolor || !dst->color || k->kind != VRH_KERNEL_AO || (gocc && k->samples <= 8),
               "vrh_unshard: re-deriving AO colour needs the gathered masks and samples <= 8");
