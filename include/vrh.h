@@ -15,6 +15,8 @@
  *   vrh_rt_download    <- gpu_buffer_rt::display_color_buffer D2H   gpu_buffer_rt.inl:90-119
  *   vrh_sync           <- (none: cuda_sched is async) ; called by hip_buffer_rt::end_frame()
  *   vrh_build_bvh      <- build<index_bvh<P>>(prims, n)              detail/bvh/build.inl:165-178 (+ sah.h)
+ *   vrh_scene_build    <- build<index_bvh<P>> + cuda_index_bvh copy, on the GPU (linear BVH)
+ *   vrh_bvh_sah_cost   <- sah_cost(bvh)                              detail/bvh/statistics.h:30-73
  *   vrh_shading_create <- make_kernel_params(binding, prims, normals, materials, lights, ...)
  *                                                                     kernels.h:357-389 (device copies of
  *                         the material / light arrays, as viewer.cpp:501-523 uploads them)
@@ -154,6 +156,8 @@ typedef struct {
     uint32_t max_prim_id;     /* largest prim_id / geom_id of the primitives                    */
     uint32_t max_geom_id;
     uint32_t vertex_normals;  /* per-vertex normals set (vrh_scene_set_vertex_normals)          */
+    uint32_t gpu_built;       /* built by vrh_scene_build                                        */
+    float    build_ms;        /* vrh_scene_build: device time of the build kernels               */
 } vrh_scene_info;
 
 /* camera::look_at + camera::perspective (camera.inl:10-57) followed by the pinhole basis that
@@ -268,6 +272,26 @@ VRH_API int vrh_unshard(vrh_ctx* ctx, uint32_t width, uint32_t height, uint32_t 
                         const void* gathered_color, const uint32_t* gathered_prim_id,
                         const uint8_t* gathered_occ, uint64_t shard_stride_bytes,
                         const vrh_kernel_desc* kernel, vrh_rt* dst);
+
+/* GPU BVH construction: a linear BVH (Morton order, Karras 2012 hierarchy,
+ * leaves of up to max_leaf primitives) built on the device straight into a scene -- no host build,
+ * no host re-layout.  The tree differs from build<index_bvh<P>> (binned SAH), so closest-hit ties
+ * on shared edges can resolve to another primitive; vrh_bvh_sah_cost measures its quality. */
+enum vrh_build_method { VRH_BUILD_LBVH = 0 };
+typedef struct {
+    uint32_t method;          /* vrh_build_method                                               */
+    uint32_t max_leaf;        /* primitives per leaf (1..64; the reference's SAH builder uses 4)  */
+} vrh_build_desc;
+VRH_API int vrh_scene_build(vrh_ctx* ctx, const void* prims, uint32_t num_prims, uint32_t prim_kind,
+                            const void* face_normals, const vrh_build_desc* desc, vrh_scene** out);
+/* the scene's tree in the reference layout (bvh_node, index array): nodes_out holds *num_nodes
+ * entries on input (NULL: only query the count), indices_out num_prims entries.  Works for
+ * uploaded and GPU-built scenes alike. */
+VRH_API int vrh_scene_download_bvh(vrh_ctx* ctx, const vrh_scene* scene, void* nodes_out, uint32_t* num_nodes,
+                                   uint32_t* indices_out);
+/* sah_cost (detail/bvh/statistics.h:30-73): ci * sum A(inner) / A(root) + cl * sum A(leaf) / A(root)
+ * + cp * sum A(leaf) * N(leaf) / A(root), in the reference's float arithmetic */
+VRH_API int vrh_bvh_sah_cost(const void* nodes, uint32_t num_nodes, float ci, float cl, float cp, float* cost);
 
 /* host binned-SAH builder, tree-identical to build<index_bvh<P>> (build.inl:165-178).
  * nodes_out must hold 2*num_prims nodes (32 B each), indices_out num_prims entries. */

@@ -32,6 +32,7 @@
 #include <visionaray/bvh.h>
 #include <visionaray/camera.h>
 #include <visionaray/get_normal.h>
+#include <visionaray/detail/bvh/statistics.h>
 #include <visionaray/kernels.h>
 #include <visionaray/material.h>
 #include <visionaray/point_light.h>
@@ -698,6 +699,20 @@ int main(int argc, char** argv)
         std::vector<vec3> normals(t.size());
         for (size_t i = 0; i < t.size(); ++i) normals[i] = normalize(cross(t[i].e1, t[i].e2));
         return run_shade(d, t, normals, outdir, per_vertex, W, H);
+    }
+    if (mode == "sah")
+    {
+        // sah_cost (detail/bvh/statistics.h:30-73) of the reference's own tree
+        return with_scene(d, [&](auto& prims, std::vector<vec3> const&)
+        {
+            using P = typename std::decay<decltype(prims[0])>::type;
+            auto bvh = build<index_bvh<P>>(prims.data(), prims.size());
+            uint32_t bits;
+            float c = sah_cost(bvh);
+            std::memcpy(&bits, &c, 4);
+            printf("{\"scene\":\"%s\",\"sah_cost\":%.9g,\"sah_cost_bits\":\"%08x\"}\n", d.name.c_str(), c, bits);
+            return 0;
+        });
     }
     if (mode == "multi")
     {

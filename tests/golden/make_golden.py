@@ -5,6 +5,7 @@ Run in the build container (needs /root/reference to build the harness):
     make -C oracle ref && python tests/golden/make_golden.py            (everything)
     python tests/golden/make_golden.py --shade                          (shading + multi-hit cases)
     python tests/golden/make_golden.py --multi                          (only the multi-hit cases)
+    python tests/golden/make_golden.py --sah                            (only the sah_cost values)
 
 For every case the reference harness renders a full simple_sched<basic_ray<float>> frame
 (primary closest_hit + the Appendix-A AO kernel for triangle scenes) and this script stores:
@@ -59,6 +60,10 @@ MULTI_CASES = [
 ]
 
 
+# sah_cost (detail/bvh/statistics.h) of the reference's own trees
+SAH_SCENES = ["cornell12", "hf64", "hf200", "sph5000", "hf1M", "sph1M"]
+
+
 def fnv1a(a):
     """FNV-1a 64 over the little-endian bytes (computed by the oracle's C helper for speed)."""
     sys.path.insert(0, ROOT)
@@ -101,10 +106,20 @@ def multi_cases(out):
             print(case, rec["hits"], rec["color_hash"], flush=True)
 
 
+def sah_cases(out):
+    rec = {}
+    for scene in SAH_SCENES:
+        r = subprocess.run([REF, "sah", scene], check=True, capture_output=True, text=True)
+        info = json.loads(r.stdout.strip().splitlines()[-1])
+        rec[scene] = info["sah_cost_bits"]
+        print("sah", scene, info["sah_cost"], flush=True)
+    out["sah_cost_bits"] = rec
+
+
 def main():
     if not os.path.exists(REF):
         sys.exit("build the reference harness first: make -C oracle ref")
-    only_shade = "--shade" in sys.argv or "--multi" in sys.argv
+    only_shade = "--shade" in sys.argv or "--multi" in sys.argv or "--sah" in sys.argv
     path = os.path.join(HERE, "golden.json")
     out = json.load(open(path)) if only_shade else {}
     rng = np.random.default_rng(12345)
@@ -136,9 +151,13 @@ def main():
                                     occ=occ[pix], color=color[pix])
             out[case] = rec
             print(case, rec["hits"], rec["ao_occluded"], rec["primid_hash"], flush=True)
-    if "--multi" not in sys.argv:
-        shade_cases(out, np.random.default_rng(54321))
-    multi_cases(out)
+    if "--sah" in sys.argv:
+        sah_cases(out)
+    else:
+        if "--multi" not in sys.argv:
+            shade_cases(out, np.random.default_rng(54321))
+        multi_cases(out)
+        sah_cases(out)
     with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 

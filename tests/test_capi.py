@@ -128,3 +128,11 @@ def test_error_paths_without_device():
 def test_unsupported_primitive_dtype():
     with pytest.raises(TypeError):
         va.build_index_bvh(np.zeros(4, np.float32))
+
+
+@pytest.mark.parametrize("name", ["cornell12", "hf64", "hf200", "sph5000", "hf1M", "sph1M"])
+def test_sah_cost_matches_reference(golden, name):
+    """vrh_bvh_sah_cost (statistics.h:30-73) of the product-built tree == the reference's own value, bit for bit."""
+    b = va.build_index_bvh(scenes.primitives(name))
+    c = np.float32(va.sah_cost(b.nodes)).view(np.uint32)
+    assert "%08x" % int(c) == golden["sah_cost_bits"][name]

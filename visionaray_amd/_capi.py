@@ -73,7 +73,15 @@ class vrh_scene_info(C.Structure):
     _fields_ = [("num_nodes", C.c_uint32), ("num_prims", C.c_uint32), ("num_indices", C.c_uint32),
                 ("prim_kind", C.c_uint32), ("max_depth", C.c_uint32), ("device_bytes", C.c_uint64),
                 ("wide_records", C.c_uint32), ("wide_depth", C.c_uint32), ("max_prim_id", C.c_uint32),
-                ("max_geom_id", C.c_uint32), ("vertex_normals", C.c_uint32)]
+                ("max_geom_id", C.c_uint32), ("vertex_normals", C.c_uint32), ("gpu_built", C.c_uint32),
+                ("build_ms", C.c_float)]
+
+
+class vrh_build_desc(C.Structure):
+    _fields_ = [("method", C.c_uint32), ("max_leaf", C.c_uint32)]
+
+
+VRH_BUILD_LBVH = 0
 
 
 class VrhError(RuntimeError):
@@ -100,6 +108,9 @@ SIGNATURES = {
     "vrh_shading_create": (C.c_int, [_vp, _vp, _u32, _vp, _u32, C.POINTER(_vp)]),
     "vrh_shading_free": (C.c_int, [_vp]),
     "vrh_rt_alloc_multi_hit": (C.c_int, [_vp, _vp, _u32]),
+    "vrh_scene_build": (C.c_int, [_vp, _vp, _u32, _u32, _vp, _vp, C.POINTER(_vp)]),
+    "vrh_scene_download_bvh": (C.c_int, [_vp, _vp, _vp, C.POINTER(_u32), _vp]),
+    "vrh_bvh_sah_cost": (C.c_int, [_vp, _u32, C.c_float, C.c_float, C.c_float, C.POINTER(C.c_float)]),
     "vrh_rt_download_multi_hit": (C.c_int, [_vp, _vp, _vp, _vp]),
     "vrh_rt_alloc": (C.c_int, [_vp, _u32, _u32, _u32, C.POINTER(_vp)]),
     "vrh_rt_wrap": (C.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _vp, C.POINTER(_vp)]),

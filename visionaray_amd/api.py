@@ -225,6 +225,31 @@ class hip_index_bvh:
         capi.check("vrh_scene_set_vertex_normals", self.handle, _p(n), len(n))
         self._refresh_info()
 
+    @classmethod
+    def gpu_build(cls, ctx, prims, normals=None, max_leaf=4):
+        """vrh_scene_build: a linear BVH built on the GPU straight into a device scene (no host
+        build or re-layout); the tree differs from build<index_bvh<P>> (see vrh.h)."""
+        self = cls.__new__(cls)
+        self.ctx = ctx
+        prims = np.ascontiguousarray(prims)
+        kind = capi.VRH_PRIM_TRI64 if prims.dtype == TRIANGLE_DTYPE else capi.VRH_PRIM_SPHERE48
+        nrm = None if normals is None else np.ascontiguousarray(normals, np.float32)
+        h = C.c_void_p()
+        desc = capi.vrh_build_desc(capi.VRH_BUILD_LBVH, max_leaf)
+        capi.check("vrh_scene_build", ctx.handle, _p(prims), len(prims), kind, _p(nrm), C.byref(desc), C.byref(h))
+        self.handle = h
+        self._refresh_info()
+        return self
+
+    def download_bvh(self):
+        """(nodes, indices) of a GPU-built scene in the reference layout (BVH_NODE_DTYPE, uint32)."""
+        n = C.c_uint32(0)
+        capi.check("vrh_scene_download_bvh", self.ctx.handle, self.handle, None, C.byref(n), None)
+        nodes = np.zeros(n.value, BVH_NODE_DTYPE)
+        idx = np.zeros(self.info["num_indices"], np.uint32)
+        capi.check("vrh_scene_download_bvh", self.ctx.handle, self.handle, _p(nodes), C.byref(n), _p(idx))
+        return nodes, idx
+
     def close(self):
         if self.handle:
             capi.lib().vrh_scene_free(self.handle)
@@ -427,6 +452,14 @@ class shading:
             self.close()
         except Exception:
             pass
+
+
+def sah_cost(nodes, ci=1.2, cl=0.0, cp=1.0):
+    """sah_cost(bvh) (detail/bvh/statistics.h:30-73) of a reference-layout node array."""
+    nodes = np.ascontiguousarray(nodes, BVH_NODE_DTYPE)
+    out = C.c_float()
+    capi.check("vrh_bvh_sah_cost", _p(nodes), len(nodes), ci, cl, cp, C.byref(out))
+    return float(out.value)
 
 
 def simple_kernel(bvh, shade, binding=normals_per_face_binding, bg=(0.0, 0.0, 0.0, 0.0),

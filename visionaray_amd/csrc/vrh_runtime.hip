@@ -7,6 +7,7 @@
 
 #include "vrh_internal.h"
 #include "vrh_kernels.h"
+#include "vrh_lbvh.h"
 
 #include <hip/hip_runtime.h>
 
@@ -66,6 +67,8 @@ struct vrh_scene
     float4* normals = nullptr;
     float4* quads = nullptr;     // 4-wide any-hit records (vrh_quad.cpp), null if the scene has none
     float4* vnormals = nullptr;  // per-vertex normals (3 per prim_id), VRH_NORMALS_PER_VERTEX
+    node32* dnodes = nullptr;    // GPU-built scenes: the tree in the reference layout (download)
+    uint32_t* dindices = nullptr;
     uint32_t root = 0;
     uint32_t quad_depth = 0;
     bool finite_bounds = true;   // every node bound finite (enables the hardware min/max slab path)
@@ -370,7 +373,101 @@ VRH_API int vrh_scene_free(vrh_scene* sc)
     if (sc->normals) (void)hipFree(sc->normals);
     if (sc->quads) (void)hipFree(sc->quads);
     if (sc->vnormals) (void)hipFree(sc->vnormals);
+    if (sc->dnodes) (void)hipFree(sc->dnodes);
+    if (sc->dindices) (void)hipFree(sc->dindices);
     delete sc;
+    return VRH_OK;
+}
+
+VRH_API int vrh_scene_build(vrh_ctx* ctx, const void* prims, uint32_t num_prims, uint32_t prim_kind,
+                            const void* face_normals, const vrh_build_desc* desc, vrh_scene** out)
+{
+    VRH_CHECK(ctx && prims && out && num_prims >= 1, "vrh_scene_build: bad argument");
+    VRH_CHECK(prim_kind == VRH_PRIM_TRI64 || prim_kind == VRH_PRIM_SPHERE48, "vrh_scene_build: unknown prim_kind");
+    VRH_CHECK(!desc || desc->method == VRH_BUILD_LBVH, "vrh_scene_build: unknown build method");
+    *out = nullptr;
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    lbvh_out b;
+    std::string err;
+    rc = build_lbvh(prims, num_prims, prim_kind, desc && desc->max_leaf ? desc->max_leaf : 4u, ctx->stream, b, err);
+    if (rc) { set_error(err); return rc; }
+    auto* sc = new (std::nothrow) vrh_scene;
+    if (!sc)
+    {
+        for (void* p : { (void*)b.nodes, (void*)b.indices, (void*)b.pairs, (void*)b.prims }) (void)hipFree(p);
+        set_error("host allocation failed");
+        return VRH_ERR_OOM;
+    }
+    sc->ctx = ctx;
+    sc->pairs = b.pairs; sc->prims = b.prims; sc->dnodes = b.nodes; sc->dindices = b.indices;
+    sc->root = b.root;
+    sc->finite_bounds = b.finite;
+    uint64_t bytes = uint64_t(std::max(b.num_pairs, 1u)) * 64 + uint64_t(num_prims) * (prim_kind == VRH_PRIM_TRI64 ? 48 : 32);
+    if (face_normals)
+    {
+        hipError_t e = hipMalloc(&sc->normals, size_t(num_prims) * sizeof(float4));
+        if (e == hipSuccess) e = hipMemcpy(sc->normals, face_normals, size_t(num_prims) * sizeof(float4), hipMemcpyHostToDevice);
+        if (e != hipSuccess)
+        {
+            set_error(std::string("vrh_scene_build: normals: ") + hipGetErrorString(e));
+            vrh_scene_free(sc);
+            return VRH_ERR_HIP;
+        }
+        bytes += uint64_t(num_prims) * sizeof(float4);
+    }
+    sc->info.num_nodes = b.num_nodes;
+    sc->info.num_prims = num_prims;
+    sc->info.num_indices = num_prims;
+    sc->info.prim_kind = prim_kind;
+    sc->info.max_depth = b.max_depth;
+    sc->info.device_bytes = bytes;
+    sc->info.max_prim_id = b.max_prim_id;
+    sc->info.max_geom_id = b.max_geom_id;
+    sc->info.gpu_built = 1;
+    sc->info.build_ms = b.build_ms;
+    *out = sc;
+    return VRH_OK;
+}
+
+VRH_API int vrh_scene_download_bvh(vrh_ctx* ctx, const vrh_scene* sc, void* nodes_out, uint32_t* num_nodes,
+                                   uint32_t* indices_out)
+{
+    VRH_CHECK(ctx && sc && num_nodes, "vrh_scene_download_bvh: null argument");
+    if (!sc->dnodes) { set_error("vrh_scene_download_bvh: only GPU-built scenes keep their tree on the device"); return VRH_ERR_UNSUPPORTED; }
+    if (!nodes_out) { *num_nodes = sc->info.num_nodes; return VRH_OK; }
+    VRH_CHECK(*num_nodes >= sc->info.num_nodes, "vrh_scene_download_bvh: nodes_out too small");
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    VRH_HIP(hipStreamSynchronize(ctx->stream));
+    VRH_HIP(hipMemcpy(nodes_out, sc->dnodes, size_t(sc->info.num_nodes) * sizeof(node32), hipMemcpyDeviceToHost));
+    if (indices_out) VRH_HIP(hipMemcpy(indices_out, sc->dindices, size_t(sc->info.num_indices) * 4, hipMemcpyDeviceToHost));
+    *num_nodes = sc->info.num_nodes;
+    return VRH_OK;
+}
+
+VRH_API int vrh_bvh_sah_cost(const void* nodes_v, uint32_t num_nodes, float ci, float cl, float cp, float* cost)
+{
+    VRH_CHECK(nodes_v && num_nodes >= 1 && cost, "vrh_bvh_sah_cost: bad argument");
+    auto nodes = static_cast<const node32*>(nodes_v);
+    // aabb.inl:177-196 surface_area = 2 * (s.x * s.y + s.y * s.z + s.z * s.x), s = max - min
+    auto area = [](const node32& n) {
+        const float sx = n.bmax[0] - n.bmin[0], sy = n.bmax[1] - n.bmin[1], sz = n.bmax[2] - n.bmin[2];
+        return 2.0f * (sx * sy + sy * sz + sz * sx);
+    };
+    const float A_r = area(nodes[0]);
+    float A_l = 0.0f, A_i = 0.0f, A_l_x_N_n = 0.0f;
+    for (uint32_t i = 0; i < num_nodes; ++i)
+    {
+        if (nodes[i].num_prims != 0)
+        {
+            A_l += area(nodes[i]);
+            A_l_x_N_n += area(nodes[i]) * static_cast<float>(nodes[i].num_prims);
+        }
+        else
+            A_i += area(nodes[i]);
+    }
+    *cost = ci * (A_i / A_r) + cl * (A_l / A_r) + cp * (A_l_x_N_n / A_r);
     return VRH_OK;
 }
 
