@@ -32,6 +32,19 @@ struct alignas(16) vec4
     vec4(float a, float b, float c, float d) : x(a), y(b), z(c), w(d) {}
 };
 
+struct vec2
+{
+    float x = 0, y = 0;
+    vec2() = default;
+    vec2(float a, float b) : x(a), y(b) {}
+};
+struct aabb
+{
+    vec3 min, max;
+    aabb() = default;
+    aabb(vec3 const& lo, vec3 const& hi) : min(lo), max(hi) {}
+};
+
 struct basic_ray_float {};                 // tag standing in for basic_ray<float> (hip_sched<R>)
 
 // normal binding tags (tags.h:44-47)
@@ -91,6 +104,22 @@ Tree build(P const* prims, size_t n)
     t.max_depth = hip_build_index_bvh(prims, n, t.nodes(), t.indices());
     return t;
 }
+
+// model (src/common/model.h:20-49) as visionaray_hip/obj_loader.h fills it; materials are the
+// C-ABI plastic records (same fields as plastic<float>), textures are not part of it
+struct model
+{
+    using triangle_type = basic_triangle;
+    using normal_type = vec3;
+    using tex_coord_type = vec2;
+    using material_type = vrh_plastic;
+    std::vector<triangle_type> primitives;
+    std::vector<normal_type> shading_normals;
+    std::vector<normal_type> geometric_normals;
+    std::vector<tex_coord_type> tex_coords;
+    std::vector<material_type> materials;
+    aabb bbox;
+};
 
 namespace constants
 {

@@ -21,6 +21,7 @@
  *                                                                     kernels.h:357-389 (device copies of
  *                         the material / light arrays, as viewer.cpp:501-523 uploads them)
  *   VRH_KERNEL_SIMPLE  <- simple::kernel<Params>                     detail/simple.inl:19-83
+ *   vrh_obj_load       <- load_obj(filename, model&)                 src/common/obj_loader.cpp:299-527
  *
  * Status codes: every function returns 0 on success and never throws or longjmps across the ABI;
  * vrh_last_error() gives a thread-local message for the last failure on the calling thread.
@@ -298,6 +299,37 @@ VRH_API int vrh_bvh_sah_cost(const void* nodes, uint32_t num_nodes, float ci, fl
 VRH_API int vrh_build_bvh(const void* prims, uint32_t num_prims, uint32_t prim_kind,
                           void* nodes_out, uint32_t* num_nodes_out, uint32_t* indices_out,
                           uint32_t* max_depth_out);
+
+/* Wavefront OBJ input <- load_obj(filename, model&)   obj_loader.cpp:299-527
+ * (grammar obj_grammar.cpp:40-77, model model.h:20-49).  The model matches the reference's field by
+ * field: triangles in TRI64 layout with prim_id = kept-triangle order and geom_id = last `usemtl`
+ * material, degenerate triangles dropped, 3 shading normals / tex coords per triangle whose corners
+ * all carry them, geometric normals normalize(cross(e1, e2)), plastic materials from the MTL files
+ * (padded with the reference's default material), bbox over v1, v1+e1, v1+e2.  Textures are not
+ * loaded (vrh_obj_material_texture gives the map_Kd path).  Errors: unreadable file or a face index
+ * outside the data read so far -> VRH_ERR_INVALID (the reference throws / is undefined there). */
+typedef struct vrh_obj vrh_obj;
+typedef struct {
+    uint32_t num_triangles;          /* model::primitives                                        */
+    uint32_t num_shading_normals;    /* model::shading_normals (== 3 * num_triangles: per vertex) */
+    uint32_t num_tex_coords;         /* model::tex_coords, incl. the reference's dummy padding   */
+    uint32_t num_materials;          /* model::materials                                         */
+    uint32_t num_degenerate;         /* zero-area triangles rejected (store_triangle :72-80)     */
+    uint32_t num_unknown_materials;  /* `usemtl` names not found in any mtllib                   */
+    uint32_t num_missing_files;      /* `mtllib` files that do not exist                         */
+    uint32_t reserved;
+    float bbox_min[3], bbox_max[3];  /* model::bbox (invalid = FLT_MAX / -FLT_MAX when empty)     */
+} vrh_obj_info;
+VRH_API int vrh_obj_load(const char* filename, vrh_obj** out);
+VRH_API int vrh_obj_get_info(const vrh_obj* obj, vrh_obj_info* info);
+/* copies out the arrays (NULL pointers skipped): triangles num_triangles TRI64, geometric_normals
+ * 4 floats per triangle, shading_normals 4 floats per entry, tex_coords 2 floats per entry,
+ * materials num_materials entries */
+VRH_API int vrh_obj_get_data(const vrh_obj* obj, void* triangles, float* geometric_normals,
+                             float* shading_normals, float* tex_coords, vrh_plastic* materials);
+VRH_API const char* vrh_obj_material_name(const vrh_obj* obj, uint32_t index);     /* "" for padding */
+VRH_API const char* vrh_obj_material_texture(const vrh_obj* obj, uint32_t index);  /* map_Kd or ""   */
+VRH_API int vrh_obj_free(vrh_obj* obj);
 
 /* synthetic scenes of SURVEY.md Appendix A (bench / test inputs) */
 VRH_API int vrh_gen_heightfield(uint32_t grid, void* tris_out);        /* 2*grid*grid TRI64   */

@@ -84,6 +84,13 @@ class vrh_build_desc(C.Structure):
 VRH_BUILD_LBVH = 0
 
 
+class vrh_obj_info(C.Structure):
+    _fields_ = [("num_triangles", C.c_uint32), ("num_shading_normals", C.c_uint32),
+                ("num_tex_coords", C.c_uint32), ("num_materials", C.c_uint32), ("num_degenerate", C.c_uint32),
+                ("num_unknown_materials", C.c_uint32), ("num_missing_files", C.c_uint32),
+                ("reserved", C.c_uint32), ("bbox_min", C.c_float * 3), ("bbox_max", C.c_float * 3)]
+
+
 class VrhError(RuntimeError):
     def __init__(self, fn, code, msg):
         super().__init__(f"{fn} failed (status {code}): {msg}")
@@ -132,6 +139,12 @@ SIGNATURES = {
     "vrh_gen_cornell": (C.c_int, [_vp]),
     "vrh_gen_spheres": (C.c_int, [_u32, _vp]),
     "vrh_face_normals": (C.c_int, [_vp, _u32, _vp]),
+    "vrh_obj_load": (C.c_int, [C.c_char_p, C.POINTER(_vp)]),
+    "vrh_obj_get_info": (C.c_int, [_vp, C.POINTER(vrh_obj_info)]),
+    "vrh_obj_get_data": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "vrh_obj_material_name": (C.c_char_p, [_vp, _u32]),
+    "vrh_obj_material_texture": (C.c_char_p, [_vp, _u32]),
+    "vrh_obj_free": (C.c_int, [_vp]),
 }
 
 _lib = None

@@ -454,6 +454,48 @@ class shading:
             pass
 
 
+class model:
+    """Scene read from a Wavefront OBJ file: the reference's `model` (src/common/model.h:20-49).
+
+    primitives         TRIANGLE_DTYPE, prim_id = kept-triangle order, geom_id = `usemtl` material
+    shading_normals    (M, 4) float32, three per triangle whose corners all carry `vn`
+    geometric_normals  (N, 4) float32, normalize(cross(e1, e2)) -- the per-face normals
+    tex_coords         (K, 2) float32, incl. the reference's dummy padding
+    materials          PLASTIC_DTYPE (ca = Ka, cd = Kd, cs = Ks, ka = kd = ks = 1, exp = Ns)
+    material_names / textures   `usemtl` name and map_Kd path per material ("" for padding)
+    bbox               (2, 3) float32 [min, max]
+    """
+
+    def has_vertex_normals(self):
+        return len(self.shading_normals) == 3 * len(self.primitives) and len(self.primitives) > 0
+
+
+def load_obj(filename):
+    """load_obj(filename, model&) (src/common/obj_loader.cpp:299-527) through libvrh's parser."""
+    h = C.c_void_p()
+    capi.check("vrh_obj_load", str(filename).encode(), C.byref(h))
+    try:
+        info = capi.vrh_obj_info()
+        capi.check("vrh_obj_get_info", h, C.byref(info))
+        m = model()
+        m.primitives = np.zeros(info.num_triangles, TRIANGLE_DTYPE)
+        m.geometric_normals = np.zeros((info.num_triangles, 4), np.float32)
+        m.shading_normals = np.zeros((info.num_shading_normals, 4), np.float32)
+        m.tex_coords = np.zeros((info.num_tex_coords, 2), np.float32)
+        m.materials = np.zeros(info.num_materials, PLASTIC_DTYPE)
+        capi.check("vrh_obj_get_data", h, _p(m.primitives), _p(m.geometric_normals), _p(m.shading_normals),
+                   _p(m.tex_coords), _p(m.materials))
+        m.material_names = [capi.lib().vrh_obj_material_name(h, i).decode() for i in range(info.num_materials)]
+        m.textures = [capi.lib().vrh_obj_material_texture(h, i).decode() for i in range(info.num_materials)]
+        m.bbox = np.array([list(info.bbox_min), list(info.bbox_max)], np.float32)
+        m.num_degenerate = info.num_degenerate
+        m.num_unknown_materials = info.num_unknown_materials
+        m.num_missing_files = info.num_missing_files
+        return m
+    finally:
+        capi.lib().vrh_obj_free(h)
+
+
 def sah_cost(nodes, ci=1.2, cl=0.0, cp=1.0):
     """sah_cost(bvh) (detail/bvh/statistics.h:30-73) of a reference-layout node array."""
     nodes = np.ascontiguousarray(nodes, BVH_NODE_DTYPE)
