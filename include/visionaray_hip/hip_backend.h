@@ -131,6 +131,28 @@ public:
         scene_.reset(s, [](vrh_scene* p) { vrh_scene_free(p); });
     }
 
+    // build<index_bvh<P>> + the copy to the device in one step, on the GPU (vrh_scene_build: linear
+    // BVH, leaves of <= max_leaf primitives).  prims: contiguous container of P; face_normals: any
+    // container of vec3-likes, one per primitive (may be empty for spheres / primary-only use).
+    template <typename Prims, typename Normals>
+    static hip_index_bvh gpu_build(Prims const& prims, Normals const& face_normals, uint32_t max_leaf = 4,
+                                   std::shared_ptr<hip_context> ctx = hip_context::default_context())
+    {
+        static_assert(sizeof(*prims.data()) == sizeof(Primitive), "primitive container of the BVH's type");
+        std::vector<float> rows;
+        rows.reserve(4 * face_normals.size());
+        for (auto const& n : face_normals) { rows.push_back(n.x); rows.push_back(n.y); rows.push_back(n.z); rows.push_back(0.0f); }
+        if (!rows.empty() && face_normals.size() != prims.size())
+            throw hip_error("gpu_build: one face normal per primitive", VRH_ERR_INVALID);
+        vrh_build_desc desc{ VRH_BUILD_LBVH, max_leaf };
+        vrh_scene* s = nullptr;
+        hip_detail::check(vrh_scene_build(ctx->get(), prims.data(), uint32_t(prims.size()),
+                                          hip_detail::is_sphere<Primitive>::value ? VRH_PRIM_SPHERE48 : VRH_PRIM_TRI64,
+                                          rows.empty() ? nullptr : rows.data(), &desc, &s),
+                          "vrh_scene_build");
+        return hip_index_bvh(s, std::move(ctx));
+    }
+
     // normals_per_vertex_binding array (get_shading_normal.h:64-84): 3 per primitive, entry
     // 3 * prim_id + k for vertex k; any container of vec3-likes (x, y, z)
     template <typename Normals>
@@ -153,6 +175,11 @@ public:
     }
 
 private:
+    hip_index_bvh(vrh_scene* s, std::shared_ptr<hip_context> ctx) : ctx_(std::move(ctx))
+    {
+        scene_.reset(s, [](vrh_scene* p) { vrh_scene_free(p); });
+    }
+
     std::shared_ptr<hip_context> ctx_;
     std::shared_ptr<vrh_scene> scene_;
 };

@@ -1,6 +1,10 @@
 // tests/cpp/drop_in_obj_model.cpp -- visionaray_hip/obj_loader.h filling a model, printed as JSON
 // (float bit patterns) for tests/test_obj.py.  Built against the reference's own model class
 // (src/common/model.h, plastic<float> materials) with -DREFERENCE_MODEL, else standalone.h's.
+// With a second argument (standalone build, GPU): the viewer's path on the loaded model --
+// hip_index_bvh::gpu_build, per-vertex normals, hip_shading from the model's materials, one
+// simple::kernel frame (256 x 160) -- written as RGBA32F + prim_id to that file
+// (tests/test_gpu_obj.py compares it with the Python path).
 #ifdef REFERENCE_MODEL
 #include <common/model.h>
 #include <visionaray/material.h>
@@ -52,6 +56,42 @@ int main(int argc, char** argv)
         std::printf("{\"error\": %d}\n", e.status);
         return 0;
     }
+#ifndef REFERENCE_MODEL
+    if (argc > 2)
+    {
+        const unsigned W = 256, H = 160;
+        try
+        {
+            auto device_bvh = hip_index_bvh<basic_triangle>::gpu_build(mod.primitives, mod.geometric_normals);
+            device_bvh.set_vertex_normals(mod.shading_normals);
+            std::vector<vrh_point_light> lights(1);
+            lights[0] = vrh_point_light{ { 0.5f, 2.0f, 1.5f }, { 1.0f, 1.0f, 1.0f }, 1.0f, 1.0f, 0.0f, 0.0f };
+            hip_shading shading(mod.materials, lights);
+            hip_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> rt;
+            rt.resize(W, H);
+            camera cam;
+            cam.perspective(45.0f * constants::degrees_to_radians<float>(), W / static_cast<float>(H), 0.001f, 1000.0f);
+            cam.look_at(vec3(0.3f, 1.1f, 1.6f), vec3(0.0f, 0.0f, 0.0f), vec3(0.0f, 1.0f, 0.0f));
+            hip_sched<ray> sched;
+            sched.frame(make_hip_simple_kernel(normals_per_vertex_binding{}, device_bvh, shading,
+                                               vec4(0.1f, 0.2f, 0.3f, 1.0f), vec4(0.4f, 0.4f, 0.4f, 0.5f)),
+                        make_sched_params(pixel_sampler::uniform_type{}, cam, rt));
+            std::vector<float> color(size_t(4) * W * H);
+            std::vector<uint32_t> prim(size_t(W) * H);
+            rt.download(color.data(), prim.data());
+            FILE* f = std::fopen(argv[2], "wb");
+            if (!f || std::fwrite(color.data(), 4, color.size(), f) != color.size() ||
+                std::fwrite(prim.data(), 4, prim.size(), f) != prim.size())
+                return 3;
+            std::fclose(f);
+        }
+        catch (std::exception const& e)
+        {
+            std::fprintf(stderr, "drop_in_obj_model: %s\n", e.what());
+            return 1;
+        }
+    }
+#endif
     std::printf("{\"ids\": [");
     for (size_t i = 0; i < mod.primitives.size(); ++i)
         std::printf("%s%u, %u", i ? ", " : "", mod.primitives[i].geom_id, mod.primitives[i].prim_id);

@@ -78,3 +78,37 @@ def test_obj_scene_simple_kernel(ctx, oracle_mod, terrain, binding):
     # every material of the file shows up
     geom = m.primitives["geom_id"][out["prim_id"][hit]]
     assert set(np.unique(geom).tolist()) == {0, 1, 2}
+
+
+def test_cpp_viewer_path_on_obj(ctx, oracle_mod, terrain, tmp_path):
+    """tests/cpp/drop_in_obj_model.cpp (standalone model, compiled here): load_obj -> gpu_build ->
+    simple::kernel with the file's materials; same frame as the Python path on the same GPU tree."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "visionaray_amd", "_lib")
+    exe = tmp_path / "objview"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-I", os.path.join(root, "include"),
+                    os.path.join(root, "tests", "cpp", "drop_in_obj_model.cpp"), "-o", str(exe), "-L", lib, "-lvrh",
+                    "-Wl,-rpath," + lib], check=True)
+    out_file = tmp_path / "frame.bin"
+    subprocess.run([str(exe), terrain, str(out_file)], check=True, capture_output=True, timeout=300)
+    W, H = 256, 160
+    raw = np.fromfile(out_file, np.uint32)
+    color = raw[:4 * W * H].view(np.float32).reshape(-1, 4)
+    prim = raw[4 * W * H:]
+
+    m = va.load_obj(terrain)
+    dev = va.hip_index_bvh.gpu_build(ctx, m.primitives, m.geometric_normals)
+    dev.set_vertex_normals(m.shading_normals)
+    lt = va.point_light((0.5, 2.0, 1.5))
+    sh = va.shading(ctx, m.materials, lt)
+    cam, _ = _cameras(oracle_mod, W, H)
+    rt = va.hip_buffer_rt(ctx, W, H)
+    va.hip_sched(ctx).frame(va.simple_kernel(dev, sh, binding=va.normals_per_vertex_binding, bg=(0.1, 0.2, 0.3, 1.0),
+                                             ambient=(0.4, 0.4, 0.4, 0.5)),
+                            va.make_sched_params(va.pixel_sampler.uniform_type, cam, rt))
+    out = rt.download()
+    assert (prim != 0xFFFFFFFF).mean() > 0.5
+    assert np.array_equal(prim, out["prim_id"])
+    assert np.array_equal(color.view(np.uint32), out["color"].view(np.uint32))
