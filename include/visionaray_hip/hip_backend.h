@@ -406,6 +406,20 @@ hip_builtin_kernel make_hip_simple_kernel(NormalBinding const& binding, BVH cons
 // multi_hit<N> (traverse_linear.inl:333-380) with the compositing kernel of the reference's
 // multi_hit example (examples/multi_hit/main.cpp:166-235); the N-entry hit lists land in the render
 // target (hip_buffer_rt::enable_multi_hit(N), download_multi_hit)
+// whitted::kernel (detail/whitted.inl:186-277) over make_kernel_params(binding, prims, normals,
+// materials, lights, num_bounces, epsilon, bg, ambient): simple::kernel's shading plus a shadow ray
+// per light and the plastic reflection (kr 0.1)
+template <typename NormalBinding, typename BVH, typename Vec4>
+hip_builtin_kernel make_hip_whitted_kernel(NormalBinding const& binding, BVH const& bvh, hip_shading const& shading,
+                                           unsigned num_bounces, float epsilon, Vec4 const& bg, Vec4 const& ambient)
+{
+    hip_builtin_kernel k = make_hip_simple_kernel(binding, bvh, shading, bg, ambient);
+    k.desc.kind = VRH_KERNEL_WHITTED;
+    k.desc.num_bounces = num_bounces;
+    k.desc.eps = epsilon;
+    return k;
+}
+
 template <unsigned N, typename NormalBinding, typename BVH, typename Vec4>
 hip_builtin_kernel make_hip_multi_hit_kernel(NormalBinding const& binding, BVH const& bvh, hip_shading const& shading,
                                              Vec4 const& bg)

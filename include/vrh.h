@@ -21,6 +21,7 @@
  *                                                                     kernels.h:357-389 (device copies of
  *                         the material / light arrays, as viewer.cpp:501-523 uploads them)
  *   VRH_KERNEL_SIMPLE  <- simple::kernel<Params>                     detail/simple.inl:19-83
+ *   VRH_KERNEL_WHITTED <- whitted::kernel<Params>                    detail/whitted.inl:186-277
  *   vrh_obj_load       <- load_obj(filename, model&)                 src/common/obj_loader.cpp:299-527
  *
  * Status codes: every function returns 0 on success and never throws or longjmps across the ABI;
@@ -65,9 +66,13 @@ enum vrh_kernel_kind {
     VRH_KERNEL_AO = 1,        /* ao/main.cpp:183-246 with the Appendix-A counter sampler  */
     VRH_KERNEL_SIMPLE = 2,    /* simple::kernel (detail/simple.inl:19-83): closest hit, then
                                  ambient + one plastic::shade per point light, two-sided  */
-    VRH_KERNEL_MULTI_HIT = 3  /* multi_hit<N> (traverse_linear.inl:333-380, detail/multi_hit.h):
+    VRH_KERNEL_MULTI_HIT = 3, /* multi_hit<N> (traverse_linear.inl:333-380, detail/multi_hit.h):
                                  the N closest hits per pixel (render-target hit lists) and the
                                  front-to-back compositing kernel of examples/multi_hit/main.cpp */
+    VRH_KERNEL_WHITTED = 4    /* whitted::kernel (detail/whitted.inl:186-277): simple::kernel's
+                                 shading with an any-hit shadow ray per light and plastic
+                                 reflections (kr 0.1) for num_bounces iterations; eps is the
+                                 scene epsilon (shadow / reflection ray origin offset)       */
 };
 #define VRH_MAX_HITS 16
 
@@ -105,7 +110,8 @@ typedef struct {
     uint32_t kind;            /* vrh_kernel_kind                                          */
     uint32_t samples;         /* AO samples per hit pixel (ao/main.cpp default 8, <= 32)   */
     float    radius;          /* AO any_hit max_t (default 0.1)                            */
-    float    eps;             /* AO origin offset along the sample direction (1e-3)        */
+    float    eps;             /* AO origin offset along the sample direction (1e-3); the
+                                 whitted kernel's scene epsilon                              */
     float    bg[4];           /* miss colour                                               */
     uint32_t flags;           /* vrh_kernel_flags                                          */
     /* VRH_KERNEL_SIMPLE / MULTI_HIT (make_kernel_params arguments, kernels.h:357-389) */
@@ -113,7 +119,7 @@ typedef struct {
     float    ambient[4];      /* ambient_color (RGBA; rgb scaled by a, spectrum.inl:375)   */
     const vrh_shading* shading;   /* materials + lights (vrh_shading_create)              */
     uint32_t max_hits;        /* VRH_KERNEL_MULTI_HIT: N (1..VRH_MAX_HITS)                  */
-    uint32_t reserved;
+    uint32_t num_bounces;     /* VRH_KERNEL_WHITTED: num_bounces (viewer default 4)          */
 } vrh_kernel_desc;
 
 enum vrh_kernel_flags {

@@ -27,7 +27,7 @@ NODE_DTYPE = np.dtype([("bmin", "<f4", 3), ("first", "<u4"), ("bmax", "<f4", 3),
 assert TRI_DTYPE.itemsize == 64 and SPHERE_DTYPE.itemsize == 48 and NODE_DTYPE.itemsize == 32
 
 VO_TRI, VO_SPHERE = 0, 1
-VO_MODE_PRIMARY, VO_MODE_AO, VO_MODE_SIMPLE, VO_MODE_MULTI_HIT = 0, 1, 2, 3
+VO_MODE_PRIMARY, VO_MODE_AO, VO_MODE_SIMPLE, VO_MODE_MULTI_HIT, VO_MODE_WHITTED = 0, 1, 2, 3, 4
 VO_NORMALS_PER_FACE, VO_NORMALS_PER_VERTEX = 0, 1
 # plastic<float> / point_light<float> parameter records (vrh_oracle.h vo_plastic / vo_point_light)
 PLASTIC_DTYPE = np.dtype([("ca", "<f4", 3), ("ka", "<f4"), ("cd", "<f4", 3), ("kd", "<f4"), ("cs", "<f4", 3),
@@ -59,7 +59,7 @@ class _Kernel(C.Structure):
     _fields_ = [("mode", C.c_int), ("samples", C.c_int), ("radius", C.c_float), ("eps", C.c_float),
                 ("bg", C.c_float * 4), ("materials", C.c_void_p), ("num_materials", C.c_int),
                 ("lights", C.c_void_p), ("num_lights", C.c_int), ("ambient", C.c_float * 4),
-                ("normal_binding", C.c_int), ("max_hits", C.c_int)]
+                ("normal_binding", C.c_int), ("max_hits", C.c_int), ("num_bounces", C.c_int)]
 
 
 _lib = None
@@ -207,7 +207,7 @@ def make_scene(name):
 
 
 def _structs(scene, cam, mode, samples=8, radius=0.1, eps=1e-3, bg=(0.1, 0.2, 0.3, 1.0), materials=None,
-             lights=None, ambient=(0.0, 0.0, 0.0, 0.0), binding=VO_NORMALS_PER_FACE, max_hits=0):
+             lights=None, ambient=(0.0, 0.0, 0.0, 0.0), binding=VO_NORMALS_PER_FACE, max_hits=0, num_bounces=0):
     s = _Scene(_p(scene.nodes).value, _p(scene.indices).value, _p(scene.prims).value, scene.kind,
                _p(scene.normals).value if scene.normals is not None else None,
                _p(scene.vertex_normals).value if scene.vertex_normals is not None else None)
@@ -216,7 +216,7 @@ def _structs(scene, cam, mode, samples=8, radius=0.1, eps=1e-3, bg=(0.1, 0.2, 0.
     k = _Kernel(mode, samples, radius, eps, (C.c_float * 4)(*bg),
                 _p(materials).value if materials is not None else None, 0 if materials is None else len(materials),
                 _p(lights).value if lights is not None else None, 0 if lights is None else len(lights),
-                (C.c_float * 4)(*ambient), binding, max_hits)
+                (C.c_float * 4)(*ambient), binding, max_hits, num_bounces)
     _structs.keep = (materials, lights)
     return s, c, k
 
@@ -293,6 +293,21 @@ def render_simple(scene, cam, binding, rows=None, threads=0):
     m, lt, amb, bg = shade_spec()
     return render(scene, cam, mode=VO_MODE_SIMPLE, rows=rows, threads=threads, materials=m, lights=lt,
                   ambient=amb, bg=bg, binding=binding)
+
+
+def whitted_spec():
+    """shade_spec() plus a third light inside the scenes (so shadows fall inside the Cornell box)."""
+    m, lt, amb, bg = shade_spec()
+    l3 = np.zeros(3, POINT_LIGHT_DTYPE)
+    l3[:2] = lt
+    l3[2] = ((0.2, 0.6, 0.3), (0.9, 0.9, 1.0), 0.8, 1.0, 0.2, 0.1)
+    return m, l3, amb, bg
+
+
+def render_whitted(scene, cam, binding, num_bounces=4, eps=1e-3, rows=None, threads=0):
+    m, lt, amb, bg = whitted_spec()
+    return render(scene, cam, mode=VO_MODE_WHITTED, rows=rows, threads=threads, materials=m, lights=lt,
+                  ambient=amb, bg=bg, binding=binding, num_bounces=num_bounces, eps=eps)
 
 
 def render_multi(scene, cam, binding, max_hits=16, threads=0):

@@ -14,6 +14,9 @@
 //                                    by geom_id (= prim index % 3) and two point lights (the spec in
 //                                    shade_spec() below, mirrored by tests/shading_spec.py), colour
 //                                    frame written as color.bin + hash.
+//   whitted <scene> <outdir> <face|vertex> [W H] [bounces eps]
+//                                  : whitted::kernel (detail/whitted.inl:186-277) through the same
+//                                    make_kernel_params, shade_spec + a third light (whitted_spec).
 //   multi  <scene> <outdir> <face|vertex> [W H]
 //                                  : multi_hit<16> (traverse_linear.inl:333-380) per pixel over the
 //                                    shade-mode scene, hit lists (prim_id / t) + the compositing
@@ -410,8 +413,39 @@ static shade_spec make_shade_spec()
     return sp;
 }
 
+// whitted_spec (tests' oracle.whitted_spec): shade_spec plus a light inside the scenes
+static shade_spec make_whitted_spec()
+{
+    shade_spec sp = make_shade_spec();
+    point_light<float> l2;
+    l2.set_position(vec3(0.2f, 0.6f, 0.3f));
+    l2.set_cl(vec3(0.9f, 0.9f, 1.0f));
+    l2.set_kl(0.8f);
+    l2.set_constant_attenuation(1.0f);
+    l2.set_linear_attenuation(0.2f);
+    l2.set_quadratic_attenuation(0.1f);
+    sp.lights.push_back(l2);
+    return sp;
+}
+
+template <template <typename> class Kernel, typename Binding, typename Normals>
+static void shade_frame(std::vector<typename index_bvh<tri_t>::bvh_ref> const& bvhs, Normals const* normals,
+                        shade_spec const& sp, unsigned bounces, float eps, camera const& cam,
+                        simple_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED>& rt)
+{
+    auto sparams = make_sched_params(pixel_sampler::uniform_type{}, cam, rt);
+    simple_sched<ray> sched;
+    auto kp = make_kernel_params(Binding{}, bvhs.data(), bvhs.data() + bvhs.size(), normals, sp.materials.data(),
+                                 sp.lights.data(), sp.lights.data() + sp.lights.size(), bounces, eps, sp.bg,
+                                 sp.ambient);
+    Kernel<decltype(kp)> kern;
+    kern.params = kp;
+    sched.frame(kern, sparams);
+}
+
 static int run_shade(scene_desc const& d, aligned_vector<tri_t>& prims, std::vector<vec3> const& face_normals,
-                     std::string const& outdir, bool per_vertex, int W, int H)
+                     std::string const& outdir, bool per_vertex, int W, int H, bool whitted = false,
+                     unsigned bounces = 4, float eps = 1e-3f)
 {
     for (size_t i = 0; i < prims.size(); ++i) prims[i].geom_id = unsigned(i % 3);
     auto bvh = build<index_bvh<tri_t>>(prims.data(), prims.size());
@@ -426,36 +460,26 @@ static int run_shade(scene_desc const& d, aligned_vector<tri_t>& prims, std::vec
             vec3 p((U(b) - 0.5f) * 0.4f, (U(b + 1) - 0.5f) * 0.4f, (U(b + 2) - 0.5f) * 0.4f);
             vnormals[k * 3 + j] = normalize(face_normals[k] + p);
         }
-    shade_spec sp = make_shade_spec();
+    shade_spec sp = whitted ? make_whitted_spec() : make_shade_spec();
     camera cam = make_camera(d, W, H);
     simple_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> rt;
     rt.resize(W, H);
-    auto sparams = make_sched_params(pixel_sampler::uniform_type{}, cam, rt);
-    simple_sched<ray> sched;
-    if (per_vertex)
-    {
-        auto kp = make_kernel_params(normals_per_vertex_binding{}, bvhs.data(), bvhs.data() + bvhs.size(),
-                                     vnormals.data(), sp.materials.data(), sp.lights.data(),
-                                     sp.lights.data() + sp.lights.size(), 5u, 1e-3f, sp.bg, sp.ambient);
-        simple::kernel<decltype(kp)> kern;
-        kern.params = kp;
-        sched.frame(kern, sparams);
-    }
+    if (whitted && per_vertex)
+        shade_frame<whitted::kernel, normals_per_vertex_binding>(bvhs, vnormals.data(), sp, bounces, eps, cam, rt);
+    else if (whitted)
+        shade_frame<whitted::kernel, normals_per_face_binding>(bvhs, face_normals.data(), sp, bounces, eps, cam, rt);
+    else if (per_vertex)
+        shade_frame<simple::kernel, normals_per_vertex_binding>(bvhs, vnormals.data(), sp, 5u, 1e-3f, cam, rt);
     else
-    {
-        auto kp = make_kernel_params(normals_per_face_binding{}, bvhs.data(), bvhs.data() + bvhs.size(),
-                                     face_normals.data(), sp.materials.data(), sp.lights.data(),
-                                     sp.lights.data() + sp.lights.size(), 5u, 1e-3f, sp.bg, sp.ambient);
-        simple::kernel<decltype(kp)> kern;
-        kern.params = kp;
-        sched.frame(kern, sparams);
-    }
+        shade_frame<simple::kernel, normals_per_face_binding>(bvhs, face_normals.data(), sp, 5u, 1e-3f, cam, rt);
     size_t npx = size_t(W) * H;
     write_file(outdir + "/color.bin", rt.color(), npx * 16);
     fnv hc;
     hc.bytes(rt.color(), npx * 16);
-    printf("{\"scene\":\"%s\",\"W\":%d,\"H\":%d,\"binding\":\"%s\",\"color_hash\":\"%016llx\"}\n",
-           d.name.c_str(), W, H, per_vertex ? "vertex" : "face", (unsigned long long)hc.h);
+    printf("{\"scene\":\"%s\",\"W\":%d,\"H\":%d,\"binding\":\"%s\",\"kernel\":\"%s\",\"bounces\":%u,"
+           "\"eps\":%.9g,\"color_hash\":\"%016llx\"}\n",
+           d.name.c_str(), W, H, per_vertex ? "vertex" : "face", whitted ? "whitted" : "simple", bounces, eps,
+           (unsigned long long)hc.h);
     return 0;
 }
 
@@ -687,18 +711,21 @@ int main(int argc, char** argv)
             return run_golden(d, prims, normals, outdir, W, H, !d.spheres);
         });
     }
-    if (mode == "shade")
+    if (mode == "shade" || mode == "whitted")
     {
+        // shade|whitted <scene> <outdir> <face|vertex> [W H] [bounces eps]
         if (argc < 5 || d.spheres) return 2;
         std::string outdir = argv[3];
         bool per_vertex = std::string(argv[4]) == "vertex";
         int W = argc > 6 ? atoi(argv[5]) : d.W;
         int H = argc > 6 ? atoi(argv[6]) : d.H;
+        unsigned bounces = argc > 8 ? unsigned(atoi(argv[7])) : 4u;
+        float eps = argc > 8 ? float(atof(argv[8])) : 1e-3f;
         aligned_vector<tri_t> t;
         if (d.grid == 0) make_cornell(t); else if (d.layers) make_hfstack(d.grid, d.layers, t); else make_heightfield(d.grid, t);
         std::vector<vec3> normals(t.size());
         for (size_t i = 0; i < t.size(); ++i) normals[i] = normalize(cross(t[i].e1, t[i].e2));
-        return run_shade(d, t, normals, outdir, per_vertex, W, H);
+        return run_shade(d, t, normals, outdir, per_vertex, W, H, mode == "whitted", bounces, eps);
     }
     if (mode == "sah")
     {

@@ -580,6 +580,8 @@ static inline void primary_ray(const vo_camera* cam, unsigned x, unsigned y, v3*
 
 typedef struct { float color[4]; uint32_t prim_id; float t; uint8_t occ; uint32_t list_index; uint32_t rays; } px_out;
 static void shade_simple(const vo_scene* s, const vo_kernel* k, v3 ori, v3 dir, const vo_hit* hr, float out[4]);
+static void shade_whitted(const vo_scene* s, const vo_kernel* k, v3 ori, v3 dir, vo_hit hr, float out[4],
+                          uint32_t* rays, vo_counters* cnt);
 
 /* ao/main.cpp:183-246 with the deterministic sampler of SURVEY.md Appendix A */
 static px_out shade_pixel(const vo_scene* s, const vo_camera* cam, const vo_kernel* k, unsigned x, unsigned y,
@@ -596,6 +598,10 @@ static px_out shade_pixel(const vo_scene* s, const vo_camera* cam, const vo_kern
     o.prim_id = hr.prim_id; o.t = hr.t; o.list_index = hr.list_index;
     if (k->mode == VO_MODE_SIMPLE) {
         shade_simple(s, k, ori, dir, &hr, o.color);
+        return o;
+    }
+    if (k->mode == VO_MODE_WHITTED) {
+        shade_whitted(s, k, ori, dir, hr, o.color, &o.rays, cnt);
         return o;
     }
     if (k->mode != VO_MODE_AO) {
@@ -631,59 +637,120 @@ static px_out shade_pixel(const vo_scene* s, const vo_camera* cam, const vo_kern
     return o;
 }
 
+/* get_surface (get_surface.h:336-376, 576-592) of a triangle hit: geometric + shading normal by
+ * the normal binding, material by geom_id */
+static const vo_plastic* surface(const vo_scene* s, const vo_kernel* k, const vo_hit* hr, v3* gn, v3* sn)
+{
+    if (k->normal_binding == VO_NORMALS_PER_FACE) {
+        *gn = *sn = ld(&s->normals[hr->prim_id]);                       /* get_normal.h:26-37 */
+    } else {
+        /* get_surface.h:336-376 -> get_normal(hr, primitive(list_index)) (get_normal.h:110-116)
+         * and get_shading_normal.h:64-84 with lerp(a,b,c,u,v) (math.h:466-475) */
+        const vo_tri* tri = (const vo_tri*)s->prims + s->indices[hr->list_index];
+        *gn = normalize(cross(ld(&tri->e1), ld(&tri->e2)));
+        v3 n0 = ld(&s->vertex_normals[hr->prim_id * 3u]);
+        v3 n1 = ld(&s->vertex_normals[hr->prim_id * 3u + 1u]);
+        v3 n2 = ld(&s->vertex_normals[hr->prim_id * 3u + 2u]);
+        v3 s2 = muls(n2, hr->v), s3 = muls(n1, hr->u), s1 = muls(n0, 1.0f - (hr->u + hr->v));
+        *sn = normalize(add(add(s1, s2), s3));
+    }
+    return &k->materials[hr->geom_id];
+}
+
+/* plastic.inl:13-16 ambient() = ca * ka, times from_rgba(ambient_color) (spectrum.inl:375-378) */
+static v3 ambient_term(const vo_kernel* k, const vo_plastic* m)
+{
+    v3 amb_c = mk(k->ambient[0] * k->ambient[3], k->ambient[1] * k->ambient[3], k->ambient[2] * k->ambient[3]);
+    return mul(muls(mk(m->ca[0], m->ca[1], m->ca[2]), m->ka), amb_c);
+}
+
+/* plastic::shade (plastic.inl:21-37) for one point light at surface point pos: pi * (lambertian +
+ * blinn) * intensity * ndotl */
+static v3 plastic_light(const vo_plastic* m, v3 n, v3 view, v3 pos, const vo_point_light* L)
+{
+    const float PI = 3.14159265358979323846264338328e+00f, INV_PI = 3.18309886183790691216444201928e-01f;
+    v3 lpos = mk(L->position[0], L->position[1], L->position[2]);
+    v3 wi = normalize(sub(lpos, pos));                                  /* simple.inl:59 */
+    v3 wo = view;
+    float ndotl = fmax_ref(0.0f, dot(n, wi));                           /* plastic.inl:29 */
+    /* brdf.h:36-41 lambertian::f = cd * kd * inv_pi */
+    v3 diff = muls(muls(mk(m->cd[0], m->cd[1], m->cd[2]), m->kd), INV_PI);
+    /* brdf.h:111-122 blinn::f */
+    v3 h = normalize(add(wo, wi));
+    float hdotn = fmax_ref(0.0f, dot(h, n));
+    v3 spec = muls(mk(m->cs[0], m->cs[1], m->cs[2]), m->ks);
+    float sat = fmax_ref(0.0f, fmin_ref(dot(wi, h), 1.0f));              /* math.h:454-457 */
+    float p5 = powf(1.0f - sat, 5.0f);
+    v3 schlick = add(spec, muls(mk(1.0f - spec.x, 1.0f - spec.y, 1.0f - spec.z), p5));
+    float nfactor = (m->exp + 2.0f) / (8.0f * PI);
+    v3 bl = muls(muls(schlick, nfactor), powf(hdotn, m->exp));
+    /* point_light.inl:12-28 intensity: (cl * kl) * float(1.0 / (c + l*d + q*d*d)) */
+    float dist = sqrtf(dot(sub(lpos, pos), sub(lpos, pos)));
+    float den = L->constant_att + L->linear_att * dist + L->quadratic_att * dist * dist;
+    float att = (float)(1.0 / (double)den);
+    v3 I = muls(muls(mk(L->cl[0], L->cl[1], L->cl[2]), L->kl), att);
+    return muls(mul(smul(PI, add(diff, bl)), I), ndotl);
+}
+
 /* detail/simple.inl:26-79 (simple::kernel) with plastic materials and point lights: ambient term,
  * two-sided shading normal (faceforward), one plastic::shade per light.  Colour of a hit pixel. */
 static void shade_simple(const vo_scene* s, const vo_kernel* k, v3 ori, v3 dir, const vo_hit* hr, float out[4])
 {
     v3 pos = add(ori, muls(dir, hr->t));                               /* simple.inl:37 */
     v3 gn, sn;
-    if (k->normal_binding == VO_NORMALS_PER_FACE) {
-        gn = sn = ld(&s->normals[hr->prim_id]);                         /* get_normal.h:26-37 */
-    } else {
-        /* get_surface.h:336-376 -> get_normal(hr, primitive(list_index)) (get_normal.h:110-116)
-         * and get_shading_normal.h:64-84 with lerp(a,b,c,u,v) (math.h:466-475) */
-        const vo_tri* tri = (const vo_tri*)s->prims + s->indices[hr->list_index];
-        gn = normalize(cross(ld(&tri->e1), ld(&tri->e2)));
-        v3 n0 = ld(&s->vertex_normals[hr->prim_id * 3u]);
-        v3 n1 = ld(&s->vertex_normals[hr->prim_id * 3u + 1u]);
-        v3 n2 = ld(&s->vertex_normals[hr->prim_id * 3u + 2u]);
-        v3 s2 = muls(n2, hr->v), s3 = muls(n1, hr->u), s1 = muls(n0, 1.0f - (hr->u + hr->v));
-        sn = normalize(add(add(s1, s2), s3));
-    }
-    const vo_plastic* m = &k->materials[hr->geom_id];
-    const float PI = 3.14159265358979323846264338328e+00f, INV_PI = 3.18309886183790691216444201928e-01f;
-    /* plastic.inl:13-16 ambient() = ca * ka; * from_rgba(ambient) (spectrum.inl:375-378) */
-    v3 amb_c = mk(k->ambient[0] * k->ambient[3], k->ambient[1] * k->ambient[3], k->ambient[2] * k->ambient[3]);
-    v3 shaded = mul(muls(mk(m->ca[0], m->ca[1], m->ca[2]), m->ka), amb_c);
+    const vo_plastic* m = surface(s, k, hr, &gn, &sn);
+    v3 shaded = ambient_term(k, m);
     v3 view = mk(-dir.x, -dir.y, -dir.z);
     v3 n = dot(gn, view) < 0.0f ? mk(-sn.x, -sn.y, -sn.z) : sn;          /* vector.inl:674-681 */
-    for (int li = 0; li < k->num_lights; ++li) {
-        const vo_point_light* L = &k->lights[li];
-        v3 lpos = mk(L->position[0], L->position[1], L->position[2]);
-        v3 wi = normalize(sub(lpos, pos));                              /* simple.inl:59 */
-        v3 wo = view;
-        float ndotl = fmax_ref(0.0f, dot(n, wi));                       /* plastic.inl:29 */
-        /* brdf.h:36-41 lambertian::f = cd * kd * inv_pi */
-        v3 diff = muls(muls(mk(m->cd[0], m->cd[1], m->cd[2]), m->kd), INV_PI);
-        /* brdf.h:111-122 blinn::f */
-        v3 h = normalize(add(wo, wi));
-        float hdotn = fmax_ref(0.0f, dot(h, n));
-        v3 spec = muls(mk(m->cs[0], m->cs[1], m->cs[2]), m->ks);
-        float sat = fmax_ref(0.0f, fmin_ref(dot(wi, h), 1.0f));          /* math.h:454-457 */
-        float p5 = powf(1.0f - sat, 5.0f);
-        v3 schlick = add(spec, muls(mk(1.0f - spec.x, 1.0f - spec.y, 1.0f - spec.z), p5));
-        float nfactor = (m->exp + 2.0f) / (8.0f * PI);
-        v3 bl = muls(muls(schlick, nfactor), powf(hdotn, m->exp));
-        /* point_light.inl:12-28 intensity: (cl * kl) * float(1.0 / (c + l*d + q*d*d)) */
-        float dist = sqrtf(dot(sub(lpos, pos), sub(lpos, pos)));
-        float den = L->constant_att + L->linear_att * dist + L->quadratic_att * dist * dist;
-        float att = (float)(1.0 / (double)den);
-        v3 I = muls(muls(mk(L->cl[0], L->cl[1], L->cl[2]), L->kl), att);
-        /* plastic.inl:21-37: pi * (cd + blinn) * I * ndotl */
-        v3 clr = muls(mul(smul(PI, add(diff, bl)), I), ndotl);
-        shaded = add(shaded, clr);                                      /* simple.inl:63 */
-    }
+    for (int li = 0; li < k->num_lights; ++li)
+        shaded = add(shaded, plastic_light(m, n, view, pos, &k->lights[li]));   /* simple.inl:63 */
     out[0] = shaded.x; out[1] = shaded.y; out[2] = shaded.z; out[3] = 1.0f;   /* to_rgba */
+}
+
+/* detail/whitted.inl:186-277 (whitted::kernel) for a pixel whose primary ray hit (hr): loop while
+ * the last closest hit hit, throughput > epsilon and depth++ < num_bounces: ambient, an any-hit
+ * shadow ray per light (origin pos + l * eps, max_t = |pos - light|), colour += shaded *
+ * throughput, then the plastic bounce (specular_bounce fall-through, whitted.inl:64-77):
+ * reflect(view, shading normal) = 2 dot(n, view) n - view with kr = 0.1.  The reflection ray is
+ * traced only when the next loop test can pass (its hit is unused otherwise). */
+static void shade_whitted(const vo_scene* s, const vo_kernel* k, v3 ori, v3 dir, vo_hit hr, float out[4],
+                          uint32_t* rays, vo_counters* cnt)
+{
+    v3 color = mk(0.0f, 0.0f, 0.0f);
+    float thr = 1.0f;
+    int depth = 0;
+    while (hr.hit && thr > k->eps && depth++ < k->num_bounces) {
+        v3 pos = add(ori, muls(dir, hr.t));                            /* whitted.inl:223 */
+        v3 gn, sn;
+        const vo_plastic* m = surface(s, k, &hr, &gn, &sn);
+        v3 shaded = ambient_term(k, m);
+        v3 view = mk(-dir.x, -dir.y, -dir.z);
+        v3 n = dot(gn, view) < 0.0f ? mk(-sn.x, -sn.y, -sn.z) : sn;      /* faceforward */
+        for (int li = 0; li < k->num_lights; ++li) {
+            const vo_point_light* L = &k->lights[li];
+            v3 lpos = mk(L->position[0], L->position[1], L->position[2]);
+            v3 ldir = normalize(sub(lpos, pos));
+            v3 so = add(pos, muls(ldir, k->eps));
+            float max_t = sqrtf(dot(sub(pos, lpos), sub(pos, lpos)));   /* length(isect_pos - pos) */
+            float fo[3] = { so.x, so.y, so.z }, fd[3] = { ldir.x, ldir.y, ldir.z };
+            vo_hit sh = vo_intersect(fo, fd, s->nodes, s->indices, s->prims, s->kind, 1, max_t, cnt);
+            ++*rays;
+            /* shaded_clr += select(active, clr, 0) */
+            shaded = add(shaded, sh.hit ? mk(0.0f, 0.0f, 0.0f) : plastic_light(m, n, view, pos, L));
+        }
+        color = add(color, muls(shaded, thr));
+        float d2 = 2.0f * dot(sn, view);                               /* vector.inl:683-689 */
+        v3 rd = sub(mk(d2 * sn.x, d2 * sn.y, d2 * sn.z), view);
+        float thr2 = thr * 0.1f;
+        if (!(thr2 > k->eps && depth < k->num_bounces)) break;
+        ori = add(pos, muls(rd, k->eps));
+        dir = rd;
+        float fo[3] = { ori.x, ori.y, ori.z }, fd[3] = { dir.x, dir.y, dir.z };
+        hr = vo_intersect(fo, fd, s->nodes, s->indices, s->prims, s->kind, 0, FLT_MAX, cnt);
+        ++*rays;
+        thr = thr2;
+    }
+    out[0] = color.x; out[1] = color.y; out[2] = color.z; out[3] = 1.0f;     /* to_rgba */
 }
 
 /* examples/multi_hit/main.cpp:166-235: for every kept hit (in t order) the surface of

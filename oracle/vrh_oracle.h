@@ -30,7 +30,7 @@ typedef struct { uint32_t geom_id, prim_id, pad0, pad1; vo_vec3 center; float ra
 typedef struct { float bmin[3]; uint32_t first; float bmax[3]; uint32_t num_prims; } vo_node;
 
 enum { VO_TRI = 0, VO_SPHERE = 1 };
-enum { VO_MODE_PRIMARY = 0, VO_MODE_AO = 1, VO_MODE_SIMPLE = 2, VO_MODE_MULTI_HIT = 3 };
+enum { VO_MODE_PRIMARY = 0, VO_MODE_AO = 1, VO_MODE_SIMPLE = 2, VO_MODE_MULTI_HIT = 3, VO_MODE_WHITTED = 4 };
 enum { VO_MAX_HITS = 16 };
 enum { VO_NORMALS_PER_FACE = 0, VO_NORMALS_PER_VERTEX = 1 };
 
@@ -100,6 +100,7 @@ typedef struct {
     float ambient[4];
     int   normal_binding;                 /* VO_NORMALS_PER_FACE | VO_NORMALS_PER_VERTEX */
     int   max_hits;                       /* VO_MODE_MULTI_HIT: N (<= VO_MAX_HITS) */
+    int   num_bounces;                    /* VO_MODE_WHITTED (eps = scene epsilon) */
 } vo_kernel;
 
 /* deterministic per-vertex normals for tests: prim k, vertex j: normalize(n_k + 0.4 * (U(b) - 0.5,

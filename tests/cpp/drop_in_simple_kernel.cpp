@@ -32,7 +32,10 @@ static float U(uint32_t k) { return float(wang(k) >> 8) * (1.0f / 16777216.0f); 
 
 int main(int argc, char** argv)
 {
-    if (argc < 6) { fprintf(stderr, "usage: %s grid W H face|vertex out.bin\n", argv[0]); return 2; }
+    if (argc < 6) { fprintf(stderr, "usage: %s grid W H face|vertex out.bin [whitted bounces eps]\n", argv[0]); return 2; }
+    const bool whitted = argc > 8 && std::string(argv[6]) == "whitted";
+    const unsigned bounces = whitted ? unsigned(atoi(argv[7])) : 0u;
+    const float eps = whitted ? float(atof(argv[8])) : 0.0f;
     unsigned grid = unsigned(atoi(argv[1])), W = unsigned(atoi(argv[2])), H = unsigned(atoi(argv[3]));
     bool per_vertex = std::string(argv[4]) == "vertex";
     using tri_t = basic_triangle<3, float>;
@@ -67,6 +70,14 @@ int main(int argc, char** argv)
     lights[1].set_position(vec3(-1.5f, 1.0f, 0.5f)); lights[1].set_cl(vec3(1.0f, 0.8f, 0.6f)); lights[1].set_kl(0.7f);
     lights[1].set_constant_attenuation(1.0f); lights[1].set_linear_attenuation(0.1f);
     lights[1].set_quadratic_attenuation(0.05f);
+    if (whitted)
+    {
+        // whitted_spec: a third light inside the scene
+        point_light<float> l2;
+        l2.set_position(vec3(0.2f, 0.6f, 0.3f)); l2.set_cl(vec3(0.9f, 0.9f, 1.0f)); l2.set_kl(0.8f);
+        l2.set_constant_attenuation(1.0f); l2.set_linear_attenuation(0.2f); l2.set_quadratic_attenuation(0.1f);
+        lights.push_back(l2);
+    }
 
     camera cam;
     cam.perspective(45.0f * constants::degrees_to_radians<float>(), W / static_cast<float>(H), 0.001f, 1000.0f);
@@ -81,7 +92,13 @@ int main(int argc, char** argv)
         hip_sched<basic_ray<float>> sched;
         auto sparams = make_sched_params(pixel_sampler::uniform_type{}, cam, rt);
         vec4 bg(0.1f, 0.2f, 0.3f, 1.0f), ambient(0.4f, 0.4f, 0.4f, 0.5f);
-        if (per_vertex)
+        if (whitted && per_vertex)           // was: whitted::kernel<decltype(kparams)>{kparams}
+            sched.frame(make_hip_whitted_kernel(normals_per_vertex_binding{}, device_bvh, shading, bounces, eps, bg,
+                                                ambient), sparams);
+        else if (whitted)
+            sched.frame(make_hip_whitted_kernel(normals_per_face_binding{}, device_bvh, shading, bounces, eps, bg,
+                                                ambient), sparams);
+        else if (per_vertex)
             sched.frame(make_hip_simple_kernel(normals_per_vertex_binding{}, device_bvh, shading, bg, ambient), sparams);
         else
             sched.frame(make_hip_simple_kernel(normals_per_face_binding{}, device_bvh, shading, bg, ambient), sparams);

@@ -6,6 +6,7 @@ Run in the build container (needs /root/reference to build the harness):
     python tests/golden/make_golden.py --shade                          (shading + multi-hit cases)
     python tests/golden/make_golden.py --multi                          (only the multi-hit cases)
     python tests/golden/make_golden.py --sah                            (only the sah_cost values)
+    python tests/golden/make_golden.py --whitted                        (only the whitted cases)
 
 For every case the reference harness renders a full simple_sched<basic_ray<float>> frame
 (primary closest_hit + the Appendix-A AO kernel for triangle scenes) and this script stores:
@@ -60,6 +61,17 @@ MULTI_CASES = [
 ]
 
 
+# whitted::kernel cases (harness "whitted" mode, whitted_spec): name, scene, W, H, binding,
+# num_bounces, epsilon, full frame?
+WHITTED_CASES = [
+    ("whitted_cornell12_face", "cornell12", 128, 128, "face", 4, "0.001", True),
+    ("whitted_cornell12_vertex", "cornell12", 128, 128, "vertex", 6, "0.0005", True),
+    ("whitted_hfstack32x24_face", "hfstack32x24", 160, 90, "face", 10, "0.0001", True),
+    ("whitted_hf64_vertex", "hf64", 160, 90, "vertex", 2, "0.01", True),
+    ("whitted_hf1M_face", "hf1M", 1920, 1080, "face", 4, "0.001", False),
+]
+
+
 # sah_cost (detail/bvh/statistics.h) of the reference's own trees
 SAH_SCENES = ["cornell12", "hf64", "hf200", "sph5000", "hf1M", "sph1M"]
 
@@ -106,6 +118,25 @@ def multi_cases(out):
             print(case, rec["hits"], rec["color_hash"], flush=True)
 
 
+def whitted_cases(out, rng):
+    for case, scene, W, H, binding, bounces, eps, full in WHITTED_CASES:
+        with tempfile.TemporaryDirectory() as d:
+            r = subprocess.run([REF, "whitted", scene, d, binding, str(W), str(H), str(bounces), eps], check=True,
+                               capture_output=True, text=True)
+            info = json.loads(r.stdout.strip().splitlines()[-1])
+            color = np.fromfile(os.path.join(d, "color.bin"), np.float32).reshape(-1, 4)
+            rec = {"scene": scene, "W": W, "H": H, "binding": binding, "bounces": bounces, "eps": float(eps),
+                   "color_hash": fnv1a(color)}
+            assert rec["color_hash"] == info["color_hash"]
+            if full:
+                np.savez_compressed(os.path.join(HERE, case + ".npz"), color=color)
+            else:
+                pix = np.sort(rng.choice(W * H, 4096, replace=False)).astype(np.uint32)
+                np.savez_compressed(os.path.join(HERE, case + ".npz"), pixels=pix, color=color[pix])
+            out[case] = rec
+            print(case, rec["color_hash"], flush=True)
+
+
 def sah_cases(out):
     rec = {}
     for scene in SAH_SCENES:
@@ -119,7 +150,7 @@ def sah_cases(out):
 def main():
     if not os.path.exists(REF):
         sys.exit("build the reference harness first: make -C oracle ref")
-    only_shade = "--shade" in sys.argv or "--multi" in sys.argv or "--sah" in sys.argv
+    only_shade = any(f in sys.argv for f in ("--shade", "--multi", "--sah", "--whitted"))
     path = os.path.join(HERE, "golden.json")
     out = json.load(open(path)) if only_shade else {}
     rng = np.random.default_rng(12345)
@@ -151,13 +182,16 @@ def main():
                                     occ=occ[pix], color=color[pix])
             out[case] = rec
             print(case, rec["hits"], rec["ao_occluded"], rec["primid_hash"], flush=True)
-    if "--sah" in sys.argv:
+    if "--whitted" in sys.argv:
+        whitted_cases(out, np.random.default_rng(777))
+    elif "--sah" in sys.argv:
         sah_cases(out)
     else:
         if "--multi" not in sys.argv:
             shade_cases(out, np.random.default_rng(54321))
         multi_cases(out)
         sah_cases(out)
+        whitted_cases(out, np.random.default_rng(777))
     with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 

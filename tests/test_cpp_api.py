@@ -82,3 +82,17 @@ def test_reference_shading_objects_on_hip_backend(golden, tmp_path, binding):
     got = np.fromfile(out_bin, np.float32).reshape(-1, 4)
     ref = np.load(os.path.join(ROOT, "tests", "golden", "shade_hf64_%s.npz" % binding))["color"]
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=0.0)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(DROPIN_SHADE), reason="drop-in binary is built in the build container only")
+def test_reference_whitted_objects_on_hip_backend(golden, tmp_path):
+    """make_hip_whitted_kernel with the reference's own material / light objects reproduces the
+    reference's whitted::kernel frame (radiance within 1e-5)."""
+    import numpy as np
+    g = golden["whitted_hf64_vertex"]
+    out_bin = tmp_path / "color.bin"
+    _run(DROPIN_SHADE, 64, g["W"], g["H"], "vertex", out_bin, "whitted", g["bounces"], g["eps"])
+    got = np.fromfile(out_bin, np.float32).reshape(-1, 4)
+    ref = np.load(os.path.join(ROOT, "tests", "golden", "whitted_hf64_vertex.npz"))["color"]
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=0.0)

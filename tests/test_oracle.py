@@ -127,6 +127,37 @@ def test_oracle_simple_kernel_matches_reference(golden, oracle_mod, case):
     assert O.fnv1a(out["color"]) == g["color_hash"]
 
 
+WHITTED_FULL = ["whitted_cornell12_face", "whitted_cornell12_vertex", "whitted_hfstack32x24_face",
+                "whitted_hf64_vertex"]
+
+
+@pytest.mark.parametrize("case", WHITTED_FULL)
+def test_oracle_whitted_matches_reference(golden, oracle_mod, case):
+    """whitted::kernel restatement (shadow rays per light, plastic reflections, throughput /
+    num_bounces loop) bit-identical to the reference's frames (tests/golden/whitted_*.npz)."""
+    O = oracle_mod
+    g = golden[case]
+    sc = O.make_shade_scene(g["scene"])
+    out = O.render_whitted(sc, O.scene_camera(g["scene"], g["W"], g["H"]),
+                           O.VO_NORMALS_PER_VERTEX if g["binding"] == "vertex" else O.VO_NORMALS_PER_FACE,
+                           num_bounces=g["bounces"], eps=g["eps"])
+    ref = np.load(os.path.join(os.path.dirname(__file__), "golden", case + ".npz"))["color"]
+    assert np.array_equal(out["color"].view(np.uint32), ref.view(np.uint32))
+    assert O.fnv1a(out["color"]) == g["color_hash"]
+
+
+def test_oracle_whitted_hf1M_sample(golden, oracle_mod):
+    O = oracle_mod
+    g = golden["whitted_hf1M_face"]
+    ref = np.load(os.path.join(os.path.dirname(__file__), "golden", "whitted_hf1M_face.npz"))
+    sc = O.make_shade_scene("hf1M")
+    m, lt, amb, bg = O.whitted_spec()
+    out = O.render_pixels(sc, O.scene_camera("hf1M", g["W"], g["H"]), ref["pixels"], mode=O.VO_MODE_WHITTED,
+                          materials=m, lights=lt, ambient=amb, bg=bg, binding=O.VO_NORMALS_PER_FACE,
+                          num_bounces=g["bounces"], eps=g["eps"])
+    assert np.array_equal(out["color"].view(np.uint32), ref["color"].view(np.uint32))
+
+
 @pytest.mark.parametrize("case", ["multi_cornell12_face", "multi_hfstack32x24_face", "multi_hfstack32x24_vertex"])
 def test_oracle_multi_hit_matches_reference(golden, oracle_mod, case):
     """multi_hit<16> restatement (insert_sorted lists + the example's compositing) bit-identical to

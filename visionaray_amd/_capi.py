@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("VRH_LIB") or os.path.join(_HERE, "_lib", "libvrh.so")
 # enums (vrh.h)
 VRH_OK, VRH_ERR_INVALID, VRH_ERR_HIP, VRH_ERR_OOM, VRH_ERR_UNSUPPORTED, VRH_ERR_NO_DEVICE = range(6)
 VRH_PRIM_TRI64, VRH_PRIM_SPHERE48 = 0, 1
-VRH_KERNEL_PRIMARY, VRH_KERNEL_AO, VRH_KERNEL_SIMPLE, VRH_KERNEL_MULTI_HIT = 0, 1, 2, 3
+VRH_KERNEL_PRIMARY, VRH_KERNEL_AO, VRH_KERNEL_SIMPLE, VRH_KERNEL_MULTI_HIT, VRH_KERNEL_WHITTED = 0, 1, 2, 3, 4
 VRH_MAX_HITS = 16
 VRH_NORMALS_PER_FACE, VRH_NORMALS_PER_VERTEX = 0, 1
 VRH_RT_COLOR, VRH_RT_PRIM_ID, VRH_RT_T, VRH_RT_OCC, VRH_RT_ALL = 1, 2, 4, 8, 15
@@ -30,7 +30,7 @@ class vrh_kernel_desc(C.Structure):
     _fields_ = [("kind", C.c_uint32), ("samples", C.c_uint32), ("radius", C.c_float), ("eps", C.c_float),
                 ("bg", C.c_float * 4), ("flags", C.c_uint32), ("normal_binding", C.c_uint32),
                 ("ambient", C.c_float * 4), ("shading", C.c_void_p), ("max_hits", C.c_uint32),
-                ("reserved", C.c_uint32)]
+                ("num_bounces", C.c_uint32)]
 
 
 class vrh_plastic(C.Structure):

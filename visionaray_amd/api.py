@@ -527,6 +527,18 @@ def multi_hit_kernel(bvh, shade, max_hits=16, binding=normals_per_vertex_binding
     return k
 
 
+def whitted_kernel(bvh, shade, binding=normals_per_face_binding, bg=(0.0, 0.0, 0.0, 0.0),
+                   ambient=(0.0, 0.0, 0.0, 0.0), num_bounces=4, epsilon=1e-3, count_tests=False):
+    """whitted::kernel (detail/whitted.inl:186-277) over make_kernel_params(binding, prims, normals,
+    materials, lights, num_bounces, epsilon, bg, ambient): simple::kernel's shading with an any-hit
+    shadow ray per light and the plastic reflection (kr 0.1) for num_bounces loop iterations."""
+    k = simple_kernel(bvh, shade, binding=binding, bg=bg, ambient=ambient, count_tests=count_tests)
+    k.desc.kind = capi.VRH_KERNEL_WHITTED
+    k.desc.num_bounces = num_bounces
+    k.desc.eps = epsilon
+    return k
+
+
 class hip_sched:
     """hip_sched<R>: drop-in for cuda_sched<R> (cuda_sched.h:25-40).
 
@@ -539,7 +551,7 @@ class hip_sched:
 
     def frame(self, kernel, sparams, frame_num=0, shard=None, sync=True):
         if not isinstance(kernel, _builtin_kernel):
-            raise TypeError("hip_sched runs built-in kernels only (closest_hit_kernel / ao_kernel / simple_kernel): an arbitrary "
+            raise TypeError("hip_sched runs built-in kernels only (closest_hit / ao / simple / multi_hit / whitted): an arbitrary "
                             "callable cannot cross the C ABI")
         rt = sparams.rt
         cam = sparams.cam.basis(*sparams.image_size)

@@ -50,6 +50,7 @@ struct render_params
     uint32_t descent_cap;     // step loop: inner visits per step before a descent is resumed later
     dev::shade_params shade;  // VRH_KERNEL_SIMPLE / MULTI_HIT: materials, lights, normal binding, ambient
     uint32_t max_hits;        // VRH_KERNEL_MULTI_HIT: N
+    uint32_t num_bounces;     // VRH_KERNEL_WHITTED: loop iterations (eps = scene epsilon)
     uint32_t* mh_prim_id;     // [pixel][N] hit lists (render target side buffers)
     float* mh_t;
 };
@@ -67,7 +68,7 @@ struct launch_config
     int stack_cap;     // LDS stack entries per lane
     int occ;           // register budget: min waves per SIMD (1, 6 or 8)
     int sched;         // 0: step loop (render_unified_kernel), 1: item loop, 2: vote loop (render_item_kernel)
-    int epi;           // primary epilogue: 0 plain, 1 VRH_KERNEL_SIMPLE, 2 VRH_KERNEL_MULTI_HIT (triangles)
+    int epi;           // primary epilogue: 0 plain, 1 VRH_KERNEL_SIMPLE, 2 VRH_KERNEL_MULTI_HIT, 3 VRH_KERNEL_WHITTED (triangles)
     int max_hits;      // MULTI_HIT: N (LDS hit lists)
 };
 

@@ -127,7 +127,8 @@ __device__ __forceinline__ ray_t ao_ray(const render_params& P, const float* rec
 // neither the primary phase nor the AO phase waits for its slowest lane.  Without AO the wave
 // streams pixels tile after tile and writes each pixel when its ray finishes.
 // EPI: primary-ray epilogue -- 0 colour = hit ? 1 : bg, 1 simple::kernel shading, 2 multi_hit<N>
-// hit lists + the multi_hit example's compositing
+// hit lists + the multi_hit example's compositing, 3 whitted::kernel (the lane traces its pixel's
+// shadow and reflection rays one after the other before it takes the next pixel)
 template <int KIND, bool AO, bool COUNT, int OCC, int EPI = 0>
 __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params P)
 {
@@ -169,6 +170,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         mh.base = P.stack_cap * block + tid;
         mh.stride = block;
         mh.n = EPI == 2 ? P.max_hits : 1u;
+        whitted_lane w;
+        w.shadow = 0; w.depth = 0;
         for (;;)
         {
             uint64_t idle = __ballot(mode == IDLE);
@@ -194,6 +197,11 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                             out_o = orow * P.width + x;
                             best_t = FMAX; best_prim = 0; steps = 0;
                             if constexpr (EPI == 2) mh.reset();
+                            if constexpr (EPI == 3)
+                            {
+                                w.color = mk3(0.0f, 0.0f, 0.0f); w.thr = 1.0f; w.depth = 0; w.shadow = 0;
+                                max_t = FMAX; any = false; quad = false;
+                            }
                             st.reset(); st.push(P.root); resume = NO_RESUME;
                             mode = PRIMARY;
                             rays_total += 1;
@@ -210,10 +218,87 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             if (mode != IDLE)
             {
                 using ML = typename std::conditional<EPI == 2, mh_list, void>::type;
+                constexpr bool UV = EPI == 1 || EPI == 3;
+                const float mt = EPI == 3 ? max_t : FMAX;
+                const bool an = EPI == 3 ? any : false;
                 int rc = (P.fast_ok && __ballot(!finite) == 0ull)
-                    ? ray_step<KIND, COUNT, true, EPI == 1, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, &hx, &mh)
-                    : ray_step<KIND, COUNT, false, EPI == 1, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, FMAX, false, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, &hx, &mh);
-                if (rc != 0)
+                    ? ray_step<KIND, COUNT, true, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, &hx, &mh)
+                    : ray_step<KIND, COUNT, false, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, &hx, &mh);
+                if constexpr (EPI == 3)
+                {
+                    if (rc != 0)
+                    {
+                        // whitted.inl:211-275: 0 = next ray set up, 1 = pixel done (colour in w)
+                        int done = 0;
+                        if (!w.shadow)
+                        {
+                            const bool hit = best_t != FMAX;
+                            if (w.depth == 0u)
+                            {
+                                hits_total += hit ? 1 : 0;
+                                if (P.prim_id) P.prim_id[out_o] = hit ? best_prim : 0xFFFFFFFFu;
+                                if (P.t) P.t[out_o] = hit ? best_t : -1.0f;
+                                if (P.occ) P.occ[out_o] = 0;
+                                if (!hit)
+                                {
+                                    if (P.color) P.color[out_o] = make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
+                                    mode = IDLE;
+                                }
+                            }
+                            if (mode != IDLE)
+                            {
+                                // loop test: hit && throughput > epsilon && depth++ < num_bounces
+                                if (hit && w.thr > P.eps && w.depth < P.num_bounces)
+                                {
+                                    w.depth += 1u;
+                                    whitted_surface(P.shade, P.prims, P.normals, w, r, best_t, best_prim, hx);
+                                }
+                                else
+                                    done = 1;
+                            }
+                        }
+                        else
+                            whitted_light_done(P.shade, w, rc > 0);
+                        if (mode != IDLE && !done)
+                        {
+                            if (w.li < P.shade.num_lights)
+                            {
+                                r = whitted_shadow_ray(P.shade, w, P.eps, max_t);
+                                any = true; w.shadow = 1;
+                                finite = finite_ray(r);
+                                quad = P.quad_ok && finite;
+                            }
+                            else
+                            {
+                                // color += shaded * throughput; the reflection ray is traced only
+                                // if the next loop test can pass (its result is unused otherwise)
+                                w.color = w.color + w.shaded * w.thr;
+                                const float thr2 = w.thr * 0.1f;
+                                if (thr2 > P.eps && w.depth < P.num_bounces)
+                                {
+                                    r = make_ray(w.pos + w.rdir * P.eps, w.rdir);
+                                    w.thr = thr2; w.shadow = 0;
+                                    max_t = FMAX; any = false; quad = false;
+                                    finite = finite_ray(r);
+                                }
+                                else
+                                    done = 1;
+                            }
+                            if (!done)
+                            {
+                                best_t = FMAX; best_prim = 0; steps = 0;
+                                st.reset(); st.push(quad ? 0u : P.root); resume = NO_RESUME;
+                                rays_total += 1;
+                            }
+                        }
+                        if (done)
+                        {
+                            if (P.color) P.color[out_o] = make_float4(w.color.x, w.color.y, w.color.z, 1.0f);
+                            mode = IDLE;
+                        }
+                    }
+                }
+                else if (rc != 0)
                 {
                     if constexpr (EPI == 2)
                     {
@@ -743,6 +828,9 @@ static kernel_fn pick_occ(bool ao, bool count, int sched)
 template <int OCC>
 static kernel_fn pick_shade(bool count, int epi)
 {
+    if (epi == 3)
+        return count ? dev::render_unified_kernel<dev::KIND_TRI, false, true, OCC, 3>
+                     : dev::render_unified_kernel<dev::KIND_TRI, false, false, OCC, 3>;
     if (epi == 2)
         return count ? dev::render_unified_kernel<dev::KIND_TRI, false, true, OCC, 2>
                      : dev::render_unified_kernel<dev::KIND_TRI, false, false, OCC, 2>;

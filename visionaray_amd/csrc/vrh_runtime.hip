@@ -641,10 +641,11 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     (void)frame_num;  // the built-in kernels are deterministic; kept for cuda_sched::frame parity
     VRH_CHECK(ctx && sc && rt && cam && k, "vrh_render: null argument");
     VRH_CHECK(cam->width > 0 && cam->height > 0, "vrh_render: empty image");
-    VRH_CHECK(k->kind <= VRH_KERNEL_MULTI_HIT, "vrh_render: unknown kernel kind");
+    VRH_CHECK(k->kind <= VRH_KERNEL_WHITTED, "vrh_render: unknown kernel kind");
     const bool ao = k->kind == VRH_KERNEL_AO;
     const bool multi = k->kind == VRH_KERNEL_MULTI_HIT;
-    const bool shade = k->kind == VRH_KERNEL_SIMPLE || multi;
+    const bool whitted = k->kind == VRH_KERNEL_WHITTED;
+    const bool shade = k->kind == VRH_KERNEL_SIMPLE || multi || whitted;
     if (multi)
     {
         VRH_CHECK(k->max_hits >= 1 && k->max_hits <= VRH_MAX_HITS, "vrh_render: max_hits must be in [1, 16]");
@@ -683,8 +684,8 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     lc.count = (k->flags & VRH_KERNEL_COUNT_TESTS) != 0;
     lc.block = ctx->opt_block ? ctx->opt_block : 64;
     lc.stack_cap = int(cap);
-    lc.occ = ctx->opt_occ ? ctx->opt_occ : 6;
-    lc.epi = multi ? 2 : shade ? 1 : 0;
+    lc.epi = whitted ? 3 : multi ? 2 : shade ? 1 : 0;
+    lc.occ = ctx->opt_occ ? ctx->opt_occ : (lc.epi == 3 ? 1 : 6);   // whitted: no VGPR cap (its lane state spills at 6)
     lc.max_hits = multi ? int(k->max_hits) : 0;
     // auto: the item loop for sphere primary visibility (short leaves of cheap tests, where the
     // step loop's leaf iterations run at ~20 % lane utilisation), the step loop otherwise
@@ -731,6 +732,7 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
         p.shade.vnormals = sc->vnormals;
         std::memcpy(p.shade.ambient, k->ambient, 16);
     }
+    p.num_bounces = whitted ? k->num_bounces : 0u;
     if (multi)
     {
         p.max_hits = k->max_hits;

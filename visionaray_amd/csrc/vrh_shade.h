@@ -30,7 +30,7 @@ struct shade_params
 
 __device__ __forceinline__ f3 neg(f3 a) { return mk3(-a.x, -a.y, -a.z); }
 
-struct surface_t { f3 gn, sn; plastic_t m; };
+struct surface_t { f3 gn, sn; plastic_t m; uint32_t mi; };
 
 // get_surface (get_surface.h:336-376, 576-592) for a triangle hit: normals by binding, material by
 // the primitive's geom_id
@@ -41,7 +41,8 @@ __device__ inline surface_t get_surface(const shade_params& S, const float4* __r
     surface_t sf;
     const float4* q = prims + 3u * li;
     const float4 qb = q[1], qc = q[2];
-    sf.m = S.materials[__float_as_uint(qc.z)];
+    sf.mi = __float_as_uint(qc.z);
+    sf.m = S.materials[sf.mi];
     if (!S.per_vertex)
     {
         const float4 nn = normals[prim_id];                            // get_normal.h:26-37
@@ -105,6 +106,63 @@ __device__ inline float4 shade_simple(const shade_params& S, const float4* __res
     for (uint32_t li = 0; li < S.num_lights; ++li)
         shaded = shaded + plastic_shade(sf.m, n, view, pos, S.lights[li]);   // simple.inl:63
     return make_float4(shaded.x, shaded.y, shaded.z, 1.0f);           // to_rgba
+}
+
+// whitted::kernel (detail/whitted.inl:186-277) as a per-lane state machine: a closest-hit ray
+// (primary or reflection) that hits sets up the surface, then one any-hit shadow ray per light
+// (max_t = distance to the light), then the reflection ray of the plastic fall-through bounce
+// (reflect(view, shading normal), kr = 0.1, whitted.inl:64-77).  The lane keeps what the loop body
+// carries between those rays.
+struct whitted_lane
+{
+    f3 color;        // accumulated radiance (`color`)
+    f3 shaded;       // this bounce: ambient + unshadowed lights (`shaded_clr`)
+    f3 pos, n, view; // isect_pos, two-sided shading normal, view_dir
+    f3 rdir;         // reflected direction of this bounce
+    float thr;       // throughput
+    uint32_t depth;  // loop iterations entered
+    uint32_t li;     // light of the shadow ray in flight
+    uint32_t mi;     // material (geom_id)
+    uint32_t shadow; // 1 while a shadow ray is traced
+};
+
+// loop body up to the light loop (whitted.inl:225-233), for a hit at t of ray r
+__device__ inline void whitted_surface(const shade_params& S, const float4* __restrict__ prims,
+                                       const float4* __restrict__ normals, whitted_lane& w, const ray_t& r, float t,
+                                       uint32_t prim_id, const hit_extra& hx)
+{
+    w.pos = r.ori + r.dir * t;
+    const surface_t sf = get_surface(S, prims, normals, prim_id, hx.li, hx.u, hx.v);
+    w.mi = sf.mi;
+    const f3 amb = mk3(S.ambient[0] * S.ambient[3], S.ambient[1] * S.ambient[3], S.ambient[2] * S.ambient[3]);
+    w.shaded = (mk3(sf.m.ca[0], sf.m.ca[1], sf.m.ca[2]) * sf.m.ka) * amb;
+    w.view = neg(r.dir);
+    w.n = dot(sf.gn, w.view) < 0.0f ? neg(sf.sn) : sf.sn;           // faceforward
+    // specular_bounce(plastic) = reflect(view_dir, shading_normal): 2 * dot(n, i) * n - i
+    // (vector.inl:683-689), with the un-flipped shading normal (whitted.inl:262)
+    const float d2 = 2.0f * dot(sf.sn, w.view);
+    w.rdir = mk3(d2 * sf.sn.x, d2 * sf.sn.y, d2 * sf.sn.z) - w.view;
+    w.li = 0;
+}
+
+// shadow ray of light w.li (whitted.inl:237-252): origin pushed along the light direction, any hit
+// closer than the light
+__device__ inline ray_t whitted_shadow_ray(const shade_params& S, const whitted_lane& w, float eps, float& max_t)
+{
+    const point_light_t& L = S.lights[w.li];
+    const f3 lpos = mk3(L.position[0], L.position[1], L.position[2]);
+    const f3 ldir = normalize(lpos - w.pos);
+    const f3 dv = w.pos - lpos;
+    max_t = __builtin_sqrtf(dot(dv, dv));                              // length(isect_pos - position)
+    return make_ray(w.pos + ldir * eps, ldir);
+}
+
+// a shadow ray ended: add the light's plastic::shade unless occluded (select(active, clr, 0))
+__device__ inline void whitted_light_done(const shade_params& S, whitted_lane& w, bool occluded)
+{
+    const f3 c = occluded ? mk3(0.0f, 0.0f, 0.0f) : plastic_shade(S.materials[w.mi], w.n, w.view, w.pos, S.lights[w.li]);
+    w.shaded = w.shaded + c;
+    w.li += 1u;
 }
 
 // per-lane sorted hit list of multi_hit<N> in LDS, column-major [field][entry][lane]
