@@ -64,7 +64,7 @@ def test_whitted_kernel_full_frame_hf1M(ctx, golden, oracle_mod):
     np.testing.assert_allclose(out["color"][ref["pixels"]], ref["color"], rtol=RTOL, atol=0.0)
     assert O.fnv1a(out["prim_id"]) == golden["hf1M"]["primid_hash"]
     st = ctx.last_frame_stats()
-    assert st.rays > 1920 * 1080                           # shadow + reflection rays were traced
+    assert st["rays"] > 1920 * 1080                           # shadow + reflection rays were traced
 
 
 def test_whitted_zero_bounces_is_black(ctx, oracle_mod):

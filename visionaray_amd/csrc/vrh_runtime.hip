@@ -685,7 +685,9 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     lc.block = ctx->opt_block ? ctx->opt_block : 64;
     lc.stack_cap = int(cap);
     lc.epi = whitted ? 3 : multi ? 2 : shade ? 1 : 0;
-    lc.occ = ctx->opt_occ ? ctx->opt_occ : (lc.epi == 3 ? 1 : 6);   // whitted: no VGPR cap (its lane state spills at 6)
+    // shading epilogues: no VGPR cap (their lane state spills at 6 waves/SIMD; measured faster at 4,
+    // profiles/r01_shade/shade_bench.jsonl)
+    lc.occ = ctx->opt_occ ? ctx->opt_occ : (lc.epi ? 1 : 6);
     lc.max_hits = multi ? int(k->max_hits) : 0;
     // auto: the item loop for sphere primary visibility (short leaves of cheap tests, where the
     // step loop's leaf iterations run at ~20 % lane utilisation), the step loop otherwise
