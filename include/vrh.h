@@ -191,7 +191,10 @@ enum vrh_option {
     VRH_OPT_AO_SCHEDULE = 3,     /* refilling loop of a wave: 3 = one descend-to-leaf step per
                                     iteration, 4 = one traversal item (node pair or primitive)
                                     per lane and iteration, 5 = items, but only node pairs or
-                                    only primitives per iteration, whichever more lanes wait for
+                                    only primitives per iteration, whichever more lanes wait for,
+                                    6 = two-pass AO: primaries publish hit records, then every
+                                    wave takes AO rays ray by ray from the frame's hit lists
+                                    (AO only; others as 3)
                                     (auto: 4 for sphere primary visibility, else 3)              */
     VRH_OPT_BLOCKS_PER_CU = 4,   /* resident blocks per CU for the persistent grid (auto: max)     */
     VRH_OPT_WAVES_PER_SIMD = 5,  /* register budget of the unified kernel: 1 (none), 6 or 8 (auto 6) */
@@ -246,6 +249,16 @@ VRH_API int vrh_rt_download_multi_hit(vrh_ctx* ctx, vrh_rt* rt, uint32_t* prim_i
 /* one frame (asynchronous on the context stream); shard may be NULL (= whole image) */
 VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* scene, vrh_rt* rt, const vrh_camera* cam,
                        const vrh_kernel_desc* kernel, const vrh_shard* shard, uint32_t frame_num);
+/* frames in flight: num_frames (1..VRH_MAX_BATCH) frames of one scene and kernel in ONE persistent
+ * launch.  Frame f renders cams[f] (all of one size) into rows [f * R, (f + 1) * R) of rt, where
+ * R = the image height (rt is W x num_frames*H) or, for a packed shard, R = rt height / num_frames.
+ * The frames' tiles share the work queues, interleaved tile by tile, so a wave goes on to the next
+ * frame's tiles instead of idling while the last tiles of a frame finish; every frame's output is
+ * identical to its own vrh_render. */
+#define VRH_MAX_BATCH 8
+VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* scene, vrh_rt* rt, const vrh_camera* cams,
+                             uint32_t num_frames, const vrh_kernel_desc* kernel, const vrh_shard* shard,
+                             uint32_t frame_num);
 VRH_API int vrh_sync(vrh_ctx* ctx);
 VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats);   /* syncs */
 

@@ -1,0 +1,119 @@
+"""GPU: frames in flight (vrh_render_batch) -- every frame of a batched launch is bit-identical to
+the same frame rendered alone by vrh_render, for each kernel, traversal schedule and packed shard.
+
+A batch interleaves the frames' tiles in the work queues (vrh.h), so a wave moves from one frame's
+tile to another's; these tests pin that the per-frame cameras and output rows never mix.  Frames
+use distinct cameras (the eye moved along a small orbit), so a swapped camera or row is visible.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import visionaray_amd as va
+from visionaray_amd import _capi, scenes
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import test_gpu_parity as base  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def frame_cameras(name, W, H, n):
+    """n bases of the scene camera with the eye rotated about +y by 3 degrees per frame."""
+    cam, _, _ = scenes.scene_camera(name, W, H)
+    ex, ey, ez = cam.eye
+    out = []
+    for f in range(n):
+        a = np.radians(3.0 * f)
+        c = va.camera()
+        c.perspective(cam.fovy, cam.aspect, cam.z_near, cam.z_far)
+        c.look_at((float(ex * np.cos(a) + ez * np.sin(a)), ey, float(-ex * np.sin(a) + ez * np.cos(a))),
+                  cam.center, cam.up)
+        out.append(c.basis(W, H))
+    return out
+
+
+def kernel_for(dev, kind):
+    return va.ao_kernel(dev) if kind == "ao" else va.closest_hit_kernel(dev)
+
+
+def single(ctx, dev, W, rows, basis, kern, shard=None):
+    rt = va.hip_buffer_rt(ctx, W, rows)
+    rt.clear_color_buffer((0, 0, 0, 0))
+    va.render(ctx, dev, rt, basis, kern, shard)
+    out = rt.download()
+    rt.close()
+    return out
+
+
+def check_batch(ctx, name, W, H, kind, n, shard=None):
+    _, dev = base.device_scene(ctx, name)
+    kern = kernel_for(dev, kind)
+    bases = frame_cameras(name, W, H, n)
+    rows = _capi.VRH_BAND_ROWS * va.shard_bands(H, shard.index, shard.count) if shard is not None and shard.packed else H
+    rt = va.hip_buffer_rt(ctx, W, n * rows)
+    rt.clear_color_buffer((0, 0, 0, 0))
+    va.render_batch(ctx, dev, rt, bases, kern, shard)
+    got = rt.download()
+    stats = ctx.last_frame_stats()
+    rt.close()
+    rays = 0
+    for f in range(n):
+        ref = single(ctx, dev, W, rows, bases[f], kern, shard)
+        rays += ctx.last_frame_stats()["rays"]
+        sl = slice(f * rows * W, (f + 1) * rows * W)
+        for k in ("prim_id", "occ"):
+            assert np.array_equal(got[k][sl], ref[k]), f"frame {f}: {k} differs"
+        for k in ("t", "color"):
+            assert np.array_equal(got[k][sl].view(np.uint32), ref[k].view(np.uint32)), f"frame {f}: {k} bits differ"
+    assert stats["rays"] == rays
+    # the frames really differ (distinct cameras)
+    if n > 1:
+        assert not np.array_equal(got["prim_id"][:rows * W], got["prim_id"][rows * W:2 * rows * W])
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+@pytest.mark.parametrize("kind", ["ao", "primary"])
+def test_batch_frames_equal_single_frames(ctx, kind, n):
+    check_batch(ctx, "hf200", 320, 180, kind, n)
+
+
+@pytest.mark.parametrize("n", [2, 5])
+def test_batch_spheres(ctx, n):
+    check_batch(ctx, "sph5000", 256, 144, "primary", n)
+
+
+@pytest.mark.parametrize("sched", [4, 5, 6])
+def test_batch_under_other_schedules(ctx, sched):
+    ctx.set_option("ao_schedule", sched)
+    try:
+        check_batch(ctx, "hf200", 320, 180, "ao", 3)
+        check_batch(ctx, "sph5000", 256, 144, "primary", 2)
+    finally:
+        ctx.set_option("ao_schedule", 0)
+
+
+@pytest.mark.parametrize("count,index", [(3, 0), (3, 2), (8, 5)])
+def test_batch_packed_shards(ctx, count, index):
+    check_batch(ctx, "hf200", 320, 180, "ao", 4, shard=_capi.vrh_shard(index, count, 1, 0))
+
+
+def test_batch_arguments_are_checked(ctx):
+    _, dev = base.device_scene(ctx, "hf64")
+    kern = va.ao_kernel(dev)
+    bases = frame_cameras("hf64", 160, 90, 2)
+    rt = va.hip_buffer_rt(ctx, 160, 90)          # one frame's rows for a 2-frame batch
+    with pytest.raises(va.VrhError):
+        va.render_batch(ctx, dev, rt, bases, kern)
+    rt.close()
+    rt = va.hip_buffer_rt(ctx, 160, 90 * (_capi.VRH_MAX_BATCH + 1))
+    with pytest.raises(va.VrhError):
+        va.render_batch(ctx, dev, rt, bases[:1] * (_capi.VRH_MAX_BATCH + 1), kern)
+    rt.close()
+    odd = frame_cameras("hf64", 160, 80, 1)[0]
+    rt = va.hip_buffer_rt(ctx, 160, 180)
+    with pytest.raises(va.VrhError):
+        va.render_batch(ctx, dev, rt, [bases[0], odd], kern)
+    rt.close()

@@ -1,7 +1,7 @@
 """GPU: every traversal schedule and record width reaches the same bit-exact result.
 
 The kernel has several ways to organise a wave's work (vrh.h VRH_OPT_AO_SCHEDULE: whole descend-
-to-leaf steps, single items, items by vote; VRH_OPT_WIDE_ANYHIT: 4-wide any-hit records).  Only
+to-leaf steps, single items, items by vote, two-pass AO; VRH_OPT_WIDE_ANYHIT: 4-wide any-hit records).  Only
 the defaults run in test_gpu_parity.py; here the parity cases are re-run under each non-default
 choice, on the same context, so none of the paths can drift from the reference.
 """
@@ -26,8 +26,11 @@ VARIANTS = {
     "step_cap1": {"ao_schedule": 3, "descent_cap": 1},
     "step_refill24": {"ao_schedule": 3, "refill_min": 24},
     "step_cap3_wide": {"ao_schedule": 3, "descent_cap": 3, "wide_anyhit": 1},
+    "two_pass": {"ao_schedule": 6},
+    "two_pass_wide_refill1": {"ao_schedule": 6, "wide_anyhit": 1, "refill_min": 1},
+    "two_pass_global_queue": {"ao_schedule": 6, "xcd_queues": 2},
 }
-OPTIONS = ("ao_schedule", "refill_min", "vote_leaf", "wide_anyhit", "exact_minmax", "descent_cap")
+OPTIONS = ("ao_schedule", "refill_min", "vote_leaf", "wide_anyhit", "exact_minmax", "descent_cap", "xcd_queues")
 
 
 @pytest.fixture(params=sorted(VARIANTS))

@@ -16,7 +16,8 @@ kind = sys.argv[3] if len(sys.argv) > 3 else ("ao" if scene.startswith("hf") els
 prims = scenes.primitives(scene)
 host = va.build_index_bvh(prims)
 ctx = va.Context(0)
-for opt in ("waves_per_simd", "block_threads", "exact_minmax", "xcd_queues"):
+for opt in ("waves_per_simd", "block_threads", "exact_minmax", "xcd_queues", "ao_schedule", "wide_anyhit",
+            "refill_min", "descent_cap"):
     v = os.environ.get("VRH_" + opt.upper())
     if v is not None:
         ctx.set_option(opt, int(v))

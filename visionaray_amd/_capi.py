@@ -45,6 +45,7 @@ class vrh_point_light(C.Structure):
 
 VRH_KERNEL_COUNT_TESTS = 1
 VRH_BAND_ROWS = 8
+VRH_MAX_BATCH = 8
 VRH_OPT_BLOCK_THREADS, VRH_OPT_STACK_CAP, VRH_OPT_AO_SCHEDULE, VRH_OPT_BLOCKS_PER_CU = 1, 2, 3, 4
 VRH_OPT_WAVES_PER_SIMD, VRH_OPT_EXACT_MINMAX, VRH_OPT_XCD_QUEUES, VRH_OPT_REFILL_MIN, VRH_OPT_VOTE_LEAF = 5, 6, 7, 8, 9
 VRH_OPT_WIDE_ANYHIT, VRH_OPT_DESCENT_CAP = 10, 11
@@ -126,6 +127,8 @@ SIGNATURES = {
     "vrh_rt_free": (C.c_int, [_vp]),
     "vrh_render": (C.c_int, [_vp, _vp, _vp, C.POINTER(vrh_camera), C.POINTER(vrh_kernel_desc),
                              C.POINTER(vrh_shard), _u32]),
+    "vrh_render_batch": (C.c_int, [_vp, _vp, _vp, C.POINTER(vrh_camera), _u32, C.POINTER(vrh_kernel_desc),
+                                   C.POINTER(vrh_shard), _u32]),
     "vrh_sync": (C.c_int, [_vp]),
     "vrh_last_frame_stats": (C.c_int, [_vp, C.POINTER(vrh_frame_stats)]),
     "vrh_stats_reset": (C.c_int, [_vp]),

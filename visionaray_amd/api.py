@@ -571,6 +571,15 @@ def render(ctx, bvh, rt, cam_basis, kernel, shard=None):
                C.byref(shard) if shard is not None else None, 0)
 
 
+def render_batch(ctx, bvh, rt, cam_bases, kernel, shard=None):
+    """vrh_render_batch: len(cam_bases) frames in one persistent launch (frames in flight); frame f
+    lands in rows [f * R, (f + 1) * R) of rt (R = image height, or rt height / frames when packed)."""
+    n = len(cam_bases)
+    cams = (capi.vrh_camera * n)(*cam_bases)
+    capi.check("vrh_render_batch", ctx.handle, bvh.handle, rt.handle, cams, n, C.byref(kernel.desc),
+               C.byref(shard) if shard is not None else None, 0)
+
+
 def shard_bands(height, index, count):
     return capi.lib().vrh_shard_bands(height, index, count)
 

@@ -9,6 +9,8 @@
 
 namespace vrh {
 
+struct frame_camera { float eye[3], cam_u[3], cam_v[3], cam_w[3]; };
+
 struct render_params
 {
     const float4* pairs;      // 4 float4 per inner node pair record
@@ -21,7 +23,9 @@ struct render_params
     const float4* quads;      // 8 float4 per 4-wide any-hit record (vrh_quad.cpp)
     uint32_t quad_ok;         // any-hit rays with finite origin / inverse direction use `quads`
 
-    float eye[3], cam_u[3], cam_v[3], cam_w[3];
+    frame_camera cam[VRH_MAX_BATCH];   // pinhole basis of every frame of the launch
+    uint32_t num_frames;      // frames rendered by this launch (vrh_render_batch)
+    uint32_t frame_rows;      // output rows per frame: frame f owns rows [f * frame_rows, (f + 1) * frame_rows)
     uint32_t width, height;
 
     uint32_t samples;
@@ -29,7 +33,7 @@ struct render_params
     float bg[4];
 
     uint32_t shard_index, shard_count, packed;
-    uint32_t tiles_x, num_tiles;
+    uint32_t tiles_x, num_tiles;   // num_tiles = work units of the launch: frames x tiles per frame
 
     float4* color;
     uint32_t* prim_id;
@@ -40,7 +44,8 @@ struct render_params
     // tests, [5] frame error flags (1 = traversal step guard tripped), [6] [7] [9] [10] SIMD
     // utilisation (wave steps, busy lane-steps, wave descent / leaf iterations; counting variant
     // only), [8 + 8q] tile queue head q
-    // (q = 0..7, one 64-B line each) -- [0, COUNTERS_FRAME) reset per frame --
+    // (q = 0..7, one 64-B line each), [80 + 8q] hit records in list q and [144 + 8q] AO rays of
+    // list q handed out (two-pass AO) -- [0, COUNTERS_FRAME) reset per frame --
     // [COUNTERS_TOTAL + 0/1] total rays / hits since vrh_stats_reset
     unsigned long long* counters;
     uint32_t xcd_queues;      // 1: per-XCD tile queues with stealing; 0: one global queue
@@ -53,11 +58,19 @@ struct render_params
     uint32_t num_bounces;     // VRH_KERNEL_WHITTED: loop iterations (eps = scene epsilon)
     uint32_t* mh_prim_id;     // [pixel][N] hit lists (render target side buffers)
     float* mh_t;
+    // two-pass AO (launch_config::sched 3): pass 1 publishes every primary hit as a 32-B record
+    // (isect pos, pixel index | face normal, output offset) into the hit list of its tile's queue
+    // (list q holds up to 64 records per tile of queue range q); pass 2 traces the lists' AO rays,
+    // one byte per ray into `aobits` ([record][sample]); the resolve pass folds them into colour
+    float4* hitrec;
+    uint8_t* aobits;
 };
 
-constexpr int COUNTERS_FRAME = 80;      // u64 words reset before every frame
-constexpr int COUNTERS_TOTAL = 80;      // u64 words [80], [81]: totals
-constexpr int COUNTERS_WORDS = 128;
+constexpr int COUNTERS_FRAME = 208;     // u64 words reset before every frame
+constexpr int COUNTERS_HITS = 80;       // [80 + 8q]: hit records of list q (two-pass AO)
+constexpr int COUNTERS_AOHEAD = 144;    // [144 + 8q]: AO rays of list q handed out
+constexpr int COUNTERS_TOTAL = 208;     // u64 words [208], [209]: totals
+constexpr int COUNTERS_WORDS = 256;
 
 struct launch_config
 {
@@ -67,14 +80,21 @@ struct launch_config
     int block;         // threads per block (multiple of 64)
     int stack_cap;     // LDS stack entries per lane
     int occ;           // register budget: min waves per SIMD (1, 6 or 8)
-    int sched;         // 0: step loop (render_unified_kernel), 1: item loop, 2: vote loop (render_item_kernel)
-    int epi;           // primary epilogue: 0 plain, 1 VRH_KERNEL_SIMPLE, 2 VRH_KERNEL_MULTI_HIT, 3 VRH_KERNEL_WHITTED (triangles)
+    int sched;         // 0: step loop (render_unified_kernel), 1: item loop, 2: vote loop (render_item_kernel),
+                       // 3: two-pass AO (primary pass publishing hit records, AO pass, resolve)
+    int epi;           // primary epilogue: 0 plain, 1 VRH_KERNEL_SIMPLE, 2 VRH_KERNEL_MULTI_HIT, 3 VRH_KERNEL_WHITTED (triangles),
+                       // 4 hit records for the two-pass AO
     int max_hits;      // MULTI_HIT: N (LDS hit lists)
 };
 
 size_t render_lds_bytes(const launch_config& c);
 hipError_t launch_render(const render_params& p, const launch_config& c, int grid, hipStream_t s);
 int render_blocks_per_cu(const launch_config& c);
+// two-pass AO: pass 2 (AO rays of the hit lists) and the resolve pass (AO bytes -> colour, mask)
+size_t ao_pass_lds_bytes(const launch_config& c);
+hipError_t launch_ao_pass(const render_params& p, const launch_config& c, int grid, hipStream_t s);
+int ao_pass_blocks_per_cu(const launch_config& c);
+hipError_t launch_ao_resolve(const render_params& p, hipStream_t s);
 struct unshard_params
 {
     uint32_t width, height, count, rows_per_shard;

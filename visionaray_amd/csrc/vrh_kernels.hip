@@ -33,32 +33,50 @@ constexpr int AO_MASKS = 64 * AO_REC_WORDS;             // u32 masks[2][64]
 constexpr int AO_SLOT_PX = AO_MASKS + 2 * 64;           // u8 slot_px[2][64]: pixel (lane) of a hit slot
 constexpr int AO_WAVE_WORDS = AO_SLOT_PX + 2 * 64 / 4;
 
-// tile index -> (x, y) of lane, plus the output row (packed shards).  A band is one row of tiles.
-__device__ __forceinline__ bool tile_pixel(const render_params& P, uint32_t tile, uint32_t lane,
-                                           uint32_t& x, uint32_t& y, uint32_t& out_row)
+// work unit -> frame f (unit % frames: the frames of a launch interleave tile by tile, so every
+// queue range below is the same image strip of each frame), tile (unit / frames) -> (x, y) of lane,
+// plus the output row (frame f's rows start at f * frame_rows; packed shards).  A band is one row
+// of tiles.
+__device__ __forceinline__ bool tile_pixel(const render_params& P, uint32_t unit, uint32_t lane,
+                                           uint32_t& x, uint32_t& y, uint32_t& out_row, uint32_t& f)
 {
     static_assert(BAND == TILE, "a shard band is one row of 8x8 tiles");
+    uint32_t tile = unit;
+    f = 0;
+    if (P.num_frames > 1)
+    {
+        tile = unit / P.num_frames;
+        f = unit - tile * P.num_frames;
+    }
     uint32_t lb = tile / P.tiles_x;               // local band
     uint32_t tx = tile - lb * P.tiles_x;
     uint32_t band = lb * P.shard_count + P.shard_index;
     x = tx * TILE + (lane & 7u);
     uint32_t in_band = lane >> 3;
     y = band * BAND + in_band;
-    out_row = P.packed ? lb * BAND + in_band : y;
+    out_row = f * P.frame_rows + (P.packed ? lb * BAND + in_band : y);
     return x < P.width && y < P.height;
 }
 
-// sched_common.h:130-150 make_primary_ray_impl (pinhole, uniform pixel sampler)
-__device__ __forceinline__ ray_t primary_ray(const render_params& P, uint32_t x, uint32_t y)
+__device__ __forceinline__ bool tile_pixel(const render_params& P, uint32_t unit, uint32_t lane,
+                                           uint32_t& x, uint32_t& y, uint32_t& out_row)
 {
+    uint32_t f;
+    return tile_pixel(P, unit, lane, x, y, out_row, f);
+}
+
+// sched_common.h:130-150 make_primary_ray_impl (pinhole, uniform pixel sampler), frame f's camera
+__device__ __forceinline__ ray_t primary_ray(const render_params& P, uint32_t f, uint32_t x, uint32_t y)
+{
+    const frame_camera& c = P.cam[f];
     float fx = (float)x, fy = (float)y;
     float u = 2.0f * (fx + 0.5f) / (float)P.width - 1.0f;
     float v = 2.0f * (fy + 0.5f) / (float)P.height - 1.0f;
-    f3 cu = mk3(P.cam_u[0], P.cam_u[1], P.cam_u[2]);
-    f3 cv = mk3(P.cam_v[0], P.cam_v[1], P.cam_v[2]);
-    f3 cw = mk3(P.cam_w[0], P.cam_w[1], P.cam_w[2]);
+    f3 cu = mk3(c.cam_u[0], c.cam_u[1], c.cam_u[2]);
+    f3 cv = mk3(c.cam_v[0], c.cam_v[1], c.cam_v[2]);
+    f3 cw = mk3(c.cam_w[0], c.cam_w[1], c.cam_w[2]);
     f3 dir = normalize((cu * u + cv * v) + cw);
-    return make_ray(mk3(P.eye[0], P.eye[1], P.eye[2]), dir);
+    return make_ray(mk3(c.eye[0], c.eye[1], c.eye[2]), dir);
 }
 
 // Tile work queues.  The frame's tiles are split into 8 contiguous ranges (horizontal image
@@ -162,8 +180,10 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         // ---- primary visibility: stream pixels, write each when its ray finishes ------------
         tile_queue tq = queue_init(P);
         uint32_t tile = next_tile(P, tq, lane);
+        uint32_t tile_q = tq.q;                    // the queue range `tile` came from (its hit list)
         uint32_t handed = 0;                       // pixels of `tile` handed out (wave-uniform)
         uint32_t out_o = 0;
+        uint32_t lane_q = 0, lane_px = 0;          // EPI 4: hit list and image pixel of the lane's ray
         hit_extra hx = { 0.0f, 0.0f, 0u };
         mh_list mh;
         mh.mem = smem;
@@ -181,6 +201,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 if (handed >= 64u && tile != NONE)
                 {
                     tile = next_tile(P, tq, lane);
+                    tile_q = tq.q;
                     handed = 0;
                 }
                 if (tile != NONE)
@@ -189,12 +210,13 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     handed = min(64u, handed + (uint32_t)__popcll(idle));
                     if (mode == IDLE && cand < 64u)
                     {
-                        uint32_t x, y, orow;
-                        if (tile_pixel(P, tile, cand, x, y, orow))
+                        uint32_t x, y, orow, fr;
+                        if (tile_pixel(P, tile, cand, x, y, orow, fr))
                         {
-                            r = primary_ray(P, x, y);
+                            r = primary_ray(P, fr, x, y);
                             finite = finite_ray(r);
                             out_o = orow * P.width + x;
+                            if constexpr (EPI == 4) { lane_q = tile_q; lane_px = y * P.width + x; }
                             best_t = FMAX; best_prim = 0; steps = 0;
                             if constexpr (EPI == 2) mh.reset();
                             if constexpr (EPI == 3)
@@ -215,6 +237,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 continue;
             }
             const bool busy = mode != IDLE;
+            bool publish = false;                  // EPI 4: this lane's primary hit becomes a record
             if (mode != IDLE)
             {
                 using ML = typename std::conditional<EPI == 2, mh_list, void>::type;
@@ -319,11 +342,41 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                         if (hit) c = shade_simple(P.shade, P.prims, P.normals, r, best_t, best_prim, hx);
                     if constexpr (EPI == 2)
                         c = shade_multi(P.shade, P.prims, P.normals, r, mh);
-                    if (P.color) P.color[out_o] = c;
+                    // EPI 4: a hit pixel's colour and AO mask are written by the resolve pass
+                    if (P.color && (EPI != 4 || !hit)) P.color[out_o] = c;
                     if (P.prim_id) P.prim_id[out_o] = hit ? best_prim : 0xFFFFFFFFu;
                     if (P.t) P.t[out_o] = hit ? best_t : -1.0f;
-                    if (P.occ) P.occ[out_o] = 0;
+                    if (P.occ && (EPI != 4 || !hit)) P.occ[out_o] = 0;
+                    if constexpr (EPI == 4) publish = hit;   // the ray state stays valid until the refill
                     mode = IDLE;
+                }
+            }
+            if constexpr (EPI == 4)
+            {
+                // append the finished hits to their tiles' lists (one atomic per list and step):
+                // record = (isect pos, image pixel) (face normal, output offset), ao/main.cpp:202,
+                // get_normal.h:26-37
+                uint64_t pend = __ballot(publish);
+                while (pend)
+                {
+                    const uint32_t first = (uint32_t)__builtin_ctzll(pend);
+                    const uint32_t q0 = __shfl(lane_q, first);
+                    const bool mine = publish && lane_q == q0;
+                    const uint64_t m = __ballot(mine);
+                    uint32_t j0 = 0;
+                    if (lane == first)
+                        j0 = atomicAdd(reinterpret_cast<uint32_t*>(P.counters + COUNTERS_HITS + 8u * q0), (uint32_t)__popcll(m));
+                    j0 = __shfl(j0, first);
+                    if (mine)
+                    {
+                        const uint32_t rec = 64u * (uint32_t)(((uint64_t)P.num_tiles * q0) / (P.xcd_queues ? 8u : 1u))
+                                           + j0 + lane_rank(m);
+                        const f3 pos = r.ori + r.dir * best_t;
+                        const float4 nn = P.normals[best_prim];
+                        P.hitrec[2u * rec] = make_float4(pos.x, pos.y, pos.z, __uint_as_float(lane_px));
+                        P.hitrec[2u * rec + 1u] = make_float4(nn.x, nn.y, nn.z, __uint_as_float(out_o));
+                    }
+                    pend &= ~m;
                 }
             }
             if (COUNT) count_wave(cnt, busy);
@@ -409,11 +462,11 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             {
                 const uint32_t k = handedC + lane_rank(idle);
                 handedC = min(64u, handedC + (uint32_t)__popcll(idle));
-                uint32_t x, y, orow;
+                uint32_t x, y, orow, fr;
                 bool started = false;
-                if (mode == IDLE && k < 64u && tile_pixel(P, tileC, k, x, y, orow))
+                if (mode == IDLE && k < 64u && tile_pixel(P, tileC, k, x, y, orow, fr))
                 {
-                    r = primary_ray(P, x, y);
+                    r = primary_ray(P, fr, x, y);
                     finite = finite_ray(r);
                     best_t = FMAX; best_prim = 0; steps = 0; max_t = FMAX; any = false; quad = false;
                     st.reset(); st.push(P.root); resume = NO_RESUME;
@@ -510,6 +563,142 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             atomicAdd(P.counters + 10, (unsigned long long)cnt.w_prim);
         }
     }
+}
+
+// Two-pass AO, pass 2: the AO rays of the hit lists pass 1 published (render_unified_kernel,
+// EPI 4).  Ray g of list q = sample g % S of record g / S; lanes take rays straight from the list
+// heads (one atomic per refill for all idle lanes of the wave), so the frame's AO work is shared
+// out ray by ray instead of tile by tile: a shard of a few thousand tiles still keeps every wave
+// of the chip busy to the end.  A wave drains the list of its own XCD first (the strip whose BVH
+// nodes pass 1 left in that XCD's L2), then the others.  Same rays, same arithmetic and the same
+// any-hit traversal as the fused kernel (ao/main.cpp:216-238), so the occlusion bits are equal.
+template <int KIND, bool COUNT, int OCC>
+__global__ __launch_bounds__(256, OCC) void ao_pass_kernel(render_params P)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t block = blockDim.x;
+
+    lds_stack st;
+    st.mem = smem;
+    st.base = tid;
+    st.stride = block;
+    st.top = tid;
+    st.end = tid + P.stack_cap * block;
+    test_counts cnt = {};
+    uint64_t rays_total = 0;
+
+    const uint32_t S = P.samples;
+    const uint32_t nq = P.xcd_queues ? 8u : 1u;
+    uint32_t q = P.xcd_queues ? xcc_id() : 0u, tried = 0;
+    // hit records of list q: low word of the u64 counter COUNTERS_HITS + 8q (pass 1 is complete)
+    auto hits = [&](uint32_t qq) { return *reinterpret_cast<const uint32_t*>(P.counters + COUNTERS_HITS + 8u * qq); };
+    uint32_t total = hits(q) * S;                 // AO rays of list q
+
+    bool busy = false, quad = false, finite = true;
+    ray_t r;
+    float best_t = FMAX;
+    uint32_t best_prim = 0, steps = 0, resume = NO_RESUME, tag = 0;
+    for (;;)
+    {
+        uint64_t idle = __ballot(!busy);
+        if ((uint32_t)__popcll(idle) < P.refill_min && idle != ~0ull) idle = 0ull;
+        while (idle && tried < nq)
+        {
+            const uint32_t n = (uint32_t)__popcll(idle);
+            uint32_t a = 0;
+            if (lane == 0) a = atomicAdd(reinterpret_cast<uint32_t*>(P.counters + COUNTERS_AOHEAD + 8u * q), n);
+            a = __shfl(a, 0);
+            const uint32_t take = a < total ? min(n, total - a) : 0u;
+            const uint32_t cand = lane_rank(idle);
+            if (!busy && cand < take)
+            {
+                const uint32_t g = a + cand;
+                const uint32_t j = g / S, s = g - j * S;
+                const uint32_t rec = 64u * (uint32_t)(((uint64_t)P.num_tiles * q) / nq) + j;
+                const float4 r0 = P.hitrec[2u * rec], r1 = P.hitrec[2u * rec + 1u];
+                const f3 pos = mk3(r0.x, r0.y, r0.z), nrm = mk3(r1.x, r1.y, r1.z);
+                // vector3.inl:357-367 make_orthonormal_basis(u, v, w = n)
+                const f3 bv = fabsf(nrm.x) > fabsf(nrm.y) ? normalize(mk3(-nrm.z, 0.0f, nrm.x)) : normalize(mk3(0.0f, nrm.z, -nrm.y));
+                const f3 bu = cross(bv, nrm);
+                const f3 d = ao_direction(__float_as_uint(r0.w), s, bu, bv, nrm);
+                r = make_ray(pos + d * P.eps, d);
+                best_t = FMAX; best_prim = 0; steps = 0;
+                finite = finite_ray(r);
+                quad = P.quad_ok && finite;
+                st.reset(); st.push(quad ? 0u : P.root); resume = NO_RESUME;
+                tag = rec * S + s;
+                busy = true;
+                rays_total += 1;
+            }
+            if (take == n) break;
+            idle = __ballot(!busy);
+            q = (q + 1u) % nq;                    // list q is exhausted: move on to the next
+            tried += 1u;
+            if (tried < nq) total = hits(q) * S;
+        }
+        if (__ballot(busy) == 0ull) break;        // every list exhausted, no ray in flight
+        int rc = 0;
+        if (busy)
+        {
+            rc = (P.fast_ok && __ballot(!finite) == 0ull)
+                ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap)
+                : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap);
+        }
+        if (COUNT) count_wave(cnt, busy);
+        if (busy && rc != 0)
+        {
+            P.aobits[tag] = rc > 0 ? 1u : 0u;
+            busy = false;
+        }
+    }
+
+    unsigned long long rr = rays_total, b = cnt.box, pq = cnt.prim;
+    for (int off = 32; off > 0; off >>= 1)
+    {
+        rr += __shfl_down(rr, off);
+        if (COUNT) { b += __shfl_down(b, off); pq += __shfl_down(pq, off); }
+    }
+    if (__ballot(cnt.aborted) != 0ull && lane == 0) atomicOr(P.counters + 5, 1ull);
+    if (lane == 0)
+    {
+        atomicAdd(P.counters + 1, rr);
+        atomicAdd(P.counters + COUNTERS_TOTAL, rr);
+        if (COUNT)
+        {
+            atomicAdd(P.counters + 3, b);
+            atomicAdd(P.counters + 4, pq);
+            atomicAdd(P.counters + 6, (unsigned long long)cnt.w_steps);
+            atomicAdd(P.counters + 7, (unsigned long long)cnt.w_busy);
+            atomicAdd(P.counters + 9, (unsigned long long)cnt.w_box);
+            atomicAdd(P.counters + 10, (unsigned long long)cnt.w_prim);
+        }
+    }
+}
+
+// Two-pass AO, resolve: record slot -> colour 1 - k/S over the occluded samples in sample order
+// (ao/main.cpp:234-238) and the sample mask, at the record's output offset
+__global__ void ao_resolve_kernel(render_params P)
+{
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= 64u * P.num_tiles) return;
+    const uint32_t nq = P.xcd_queues ? 8u : 1u;
+    // list q owns record slots [64 lo(q), 64 lo(q + 1)), lo(q) = num_tiles * q / nq
+    const uint32_t tile = slot / 64u;
+    const uint32_t q = (uint32_t)((((uint64_t)tile + 1u) * nq - 1u) / P.num_tiles);
+    const uint32_t j = slot - 64u * (uint32_t)(((uint64_t)P.num_tiles * q) / nq);
+    if (j >= *reinterpret_cast<const uint32_t*>(P.counters + COUNTERS_HITS + 8u * q)) return;
+    const uint32_t o = __float_as_uint(P.hitrec[2u * slot + 1u].w);
+    const uint32_t S = P.samples;
+    const uint8_t* bits = P.aobits + (size_t)slot * S;
+    float clr = 1.0f;
+    const float step = 1.0f / (float)S;
+    uint32_t m = 0;
+    for (uint32_t s = 0; s < S; ++s)
+        if (bits[s]) { clr = clr - step; m |= 1u << s; }
+    if (P.color) P.color[o] = make_float4(clr, clr, clr, 1.0f);
+    if (P.occ) P.occ[o] = (uint8_t)m;
 }
 
 // ITEM schedule: the same ray streams as render_unified_kernel (two tiles in flight for AO), but
@@ -681,11 +870,11 @@ __global__ __launch_bounds__(256, OCC) void render_item_kernel(render_params P)
             {
                 const uint32_t k = handedC + lane_rank(idle);
                 handedC = min(64u, handedC + (uint32_t)__popcll(idle));
-                uint32_t x, y, orow;
+                uint32_t x, y, orow, fr;
                 bool started = false;
-                if (mode == IDLE && k < 64u && tile_pixel(P, tileC, k, x, y, orow))
+                if (mode == IDLE && k < 64u && tile_pixel(P, tileC, k, x, y, orow, fr))
                 {
-                    r = primary_ray(P, x, y);
+                    r = primary_ray(P, fr, x, y);
                     best_t = FMAX; best_prim = 0; steps = 0; max_t = FMAX; any = false; occl = false;
                     item = P.root; st.reset();
                     finite = finite_ray(r);
@@ -846,8 +1035,27 @@ static kernel_fn pick(bool ao, bool count, int occ, int sched)
     return pick_occ<KIND, 1>(ao, count, sched);
 }
 
+// two-pass AO, pass 1: primary visibility publishing hit records
+template <int KIND>
+static kernel_fn pick_publish(bool count, int occ)
+{
+    if (occ == 8) return count ? dev::render_unified_kernel<KIND, false, true, 8, 4> : dev::render_unified_kernel<KIND, false, false, 8, 4>;
+    if (occ == 6) return count ? dev::render_unified_kernel<KIND, false, true, 6, 4> : dev::render_unified_kernel<KIND, false, false, 6, 4>;
+    return count ? dev::render_unified_kernel<KIND, false, true, 1, 4> : dev::render_unified_kernel<KIND, false, false, 1, 4>;
+}
+
+template <int KIND>
+static kernel_fn pick_ao_pass(bool count, int occ)
+{
+    if (occ == 8) return count ? dev::ao_pass_kernel<KIND, true, 8> : dev::ao_pass_kernel<KIND, false, 8>;
+    if (occ == 6) return count ? dev::ao_pass_kernel<KIND, true, 6> : dev::ao_pass_kernel<KIND, false, 6>;
+    return count ? dev::ao_pass_kernel<KIND, true, 1> : dev::ao_pass_kernel<KIND, false, 1>;
+}
+
 static kernel_fn select_variant(const launch_config& c)
 {
+    if (c.epi == 4) return c.kind == dev::KIND_TRI ? pick_publish<dev::KIND_TRI>(c.count, c.occ)
+                                                   : pick_publish<dev::KIND_SPHERE>(c.count, c.occ);
     if (c.epi) return c.occ == 8 ? pick_shade<8>(c.count, c.epi) : c.occ == 6 ? pick_shade<6>(c.count, c.epi) : pick_shade<1>(c.count, c.epi);
     return c.kind == dev::KIND_TRI ? pick<dev::KIND_TRI>(c.ao, c.count, c.occ, c.sched)
                                    : pick<dev::KIND_SPHERE>(c.ao, c.count, c.occ, c.sched);
@@ -872,6 +1080,34 @@ int render_blocks_per_cu(const launch_config& c)
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, select_variant(c), c.block, render_lds_bytes(c)) != hipSuccess)
         return 1;
     return n > 0 ? n : 1;
+}
+
+size_t ao_pass_lds_bytes(const launch_config& c) { return size_t(c.stack_cap) * c.block * 4; }
+
+static kernel_fn ao_pass_variant(const launch_config& c)
+{
+    return c.kind == dev::KIND_TRI ? pick_ao_pass<dev::KIND_TRI>(c.count, c.occ) : pick_ao_pass<dev::KIND_SPHERE>(c.count, c.occ);
+}
+
+hipError_t launch_ao_pass(const render_params& p, const launch_config& c, int grid, hipStream_t s)
+{
+    hipLaunchKernelGGL(ao_pass_variant(c), dim3(grid), dim3(c.block), ao_pass_lds_bytes(c), s, p);
+    return hipGetLastError();
+}
+
+int ao_pass_blocks_per_cu(const launch_config& c)
+{
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ao_pass_variant(c), c.block, ao_pass_lds_bytes(c)) != hipSuccess)
+        return 1;
+    return n > 0 ? n : 1;
+}
+
+hipError_t launch_ao_resolve(const render_params& p, hipStream_t s)
+{
+    const uint32_t n = 64u * p.num_tiles;
+    hipLaunchKernelGGL(dev::ao_resolve_kernel, dim3((n + 255u) / 256u), dim3(256), 0, s, p);
+    return hipGetLastError();
 }
 
 hipError_t launch_unshard(const unshard_params& u, hipStream_t s)

@@ -57,6 +57,10 @@ struct vrh_ctx
     bool have_frame = false;
     // tuning options (0 = automatic), vrh_ctx_set_option
     int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_vote = 0, opt_dcap = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0;
+    // two-pass AO scratch (grown on demand): 32-B hit records and one byte per AO ray, per pixel slot
+    float4* hitrec = nullptr;
+    uint8_t* aobits = nullptr;
+    size_t hitrec_slots = 0, aobits_bytes = 0;
 };
 
 struct vrh_scene
@@ -165,6 +169,8 @@ VRH_API int vrh_ctx_destroy(vrh_ctx* ctx)
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->counters) (void)hipFree(ctx->counters);
+    if (ctx->hitrec) (void)hipFree(ctx->hitrec);
+    if (ctx->aobits) (void)hipFree(ctx->aobits);
     for (auto e : ctx->ev_start) (void)hipEventDestroy(e);
     for (auto e : ctx->ev_stop) (void)hipEventDestroy(e);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -182,7 +188,7 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
         VRH_CHECK(value % 64 == 0, "vrh_ctx_set_option: block threads must be a multiple of 64");
         ctx->opt_block = int(value); break;
     case VRH_OPT_STACK_CAP: ctx->opt_stack = int(value); break;
-    case VRH_OPT_AO_SCHEDULE: VRH_CHECK(value == 0 || (value >= 3 && value <= 5), "vrh_ctx_set_option: schedule is 3 (step), 4 (item) or 5 (vote)"); ctx->opt_sched = int(value); break;
+    case VRH_OPT_AO_SCHEDULE: VRH_CHECK(value == 0 || (value >= 3 && value <= 6), "vrh_ctx_set_option: schedule is 3 (step), 4 (item), 5 (vote) or 6 (two-pass AO)"); ctx->opt_sched = int(value); break;
     case VRH_OPT_WIDE_ANYHIT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: wide any-hit is 1 (on) or 2 (off)"); ctx->opt_wide = int(value); break;
     case VRH_OPT_DESCENT_CAP: ctx->opt_dcap = int(value); break;
     case VRH_OPT_VOTE_LEAF: VRH_CHECK(value <= 64, "vrh_ctx_set_option: vote weight is 1..64"); ctx->opt_vote = int(value); break;
@@ -638,8 +644,19 @@ VRH_API uint32_t vrh_shard_bands(uint32_t height, uint32_t index, uint32_t count
 VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_camera* cam,
                        const vrh_kernel_desc* k, const vrh_shard* shard, uint32_t frame_num)
 {
+    return vrh_render_batch(ctx, sc, rt, cam, 1, k, shard, frame_num);
+}
+
+VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_camera* cams,
+                             uint32_t num_frames, const vrh_kernel_desc* k, const vrh_shard* shard,
+                             uint32_t frame_num)
+{
     (void)frame_num;  // the built-in kernels are deterministic; kept for cuda_sched::frame parity
-    VRH_CHECK(ctx && sc && rt && cam && k, "vrh_render: null argument");
+    VRH_CHECK(ctx && sc && rt && cams && k, "vrh_render: null argument");
+    VRH_CHECK(num_frames >= 1 && num_frames <= VRH_MAX_BATCH, "vrh_render_batch: 1..VRH_MAX_BATCH frames");
+    const vrh_camera* cam = cams;
+    for (uint32_t f = 1; f < num_frames; ++f)
+        VRH_CHECK(cams[f].width == cam->width && cams[f].height == cam->height, "vrh_render_batch: frames differ in size");
     VRH_CHECK(cam->width > 0 && cam->height > 0, "vrh_render: empty image");
     VRH_CHECK(k->kind <= VRH_KERNEL_WHITTED, "vrh_render: unknown kernel kind");
     const bool ao = k->kind == VRH_KERNEL_AO;
@@ -671,8 +688,15 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     VRH_CHECK(sh.count >= 1 && sh.index < sh.count, "vrh_render: bad shard");
     const uint32_t local_bands = vrh_shard_bands(cam->height, sh.index, sh.count);
     VRH_CHECK(rt->width == cam->width, "vrh_render: render target width != camera width");
-    if (sh.packed) VRH_CHECK(rt->height >= local_bands * VRH_BAND_ROWS || local_bands == 0, "vrh_render: packed target too small");
-    else VRH_CHECK(rt->height == cam->height, "vrh_render: render target height != camera height");
+    // frame f of the batch owns rows [f * frame_rows, (f + 1) * frame_rows) of the target
+    uint32_t frame_rows = cam->height;
+    if (sh.packed)
+    {
+        frame_rows = rt->height / num_frames;
+        VRH_CHECK(frame_rows >= local_bands * VRH_BAND_ROWS || local_bands == 0, "vrh_render: packed target too small");
+    }
+    else VRH_CHECK(rt->height == cam->height * num_frames, "vrh_render: render target height != camera height x frames");
+    VRH_CHECK(uint64_t(rt->height) * rt->width < (1ull << 32), "vrh_render: render target too large");
 
     // a depth-first traversal holds at most `max_depth` stack entries (>= 1 for the root push)
     const uint32_t need = std::max<uint32_t>(sc->info.max_depth, 1u);
@@ -692,8 +716,11 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     // auto: the item loop for sphere primary visibility (short leaves of cheap tests, where the
     // step loop's leaf iterations run at ~20 % lane utilisation), the step loop otherwise
     if (ctx->opt_sched == 0) lc.sched = (lc.kind == 1 && !ao) ? 1 : 0;
-    else lc.sched = ctx->opt_sched == 4 ? 1 : ctx->opt_sched == 5 ? 2 : 0;
+    else lc.sched = ctx->opt_sched == 4 ? 1 : ctx->opt_sched == 5 ? 2 : (ctx->opt_sched == 6 && ao) ? 3 : 0;
     if (shade) lc.sched = 0;   // the shading epilogue lives in the step loop
+    // two-pass AO: pass 1 is the step loop's primary stream with the hit-record epilogue
+    launch_config lc1 = lc;
+    if (lc.sched == 3) { lc1.ao = false; lc1.epi = 4; lc1.sched = 0; }
     if (render_lds_bytes(lc) > 160u * 1024u)
     {
         set_error("vrh_render: BVH depth " + std::to_string(sc->info.max_depth) + " needs more LDS stack than a CU has");
@@ -714,14 +741,19 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     p.fast_ok = (sc->finite_bounds && !ctx->opt_exact_minmax) ? 1u : 0u;
     p.quads = sc->quads;
     p.quad_ok = (sc->quads && p.fast_ok && ctx->opt_wide == 1) ? 1u : 0u;   // auto: off (measured slower)
-    std::memcpy(p.eye, cam->eye, 12); std::memcpy(p.cam_u, cam->cam_u, 12);
-    std::memcpy(p.cam_v, cam->cam_v, 12); std::memcpy(p.cam_w, cam->cam_w, 12);
+    for (uint32_t f = 0; f < num_frames; ++f)
+    {
+        std::memcpy(p.cam[f].eye, cams[f].eye, 12); std::memcpy(p.cam[f].cam_u, cams[f].cam_u, 12);
+        std::memcpy(p.cam[f].cam_v, cams[f].cam_v, 12); std::memcpy(p.cam[f].cam_w, cams[f].cam_w, 12);
+    }
+    p.num_frames = num_frames;
+    p.frame_rows = frame_rows;
     p.width = cam->width; p.height = cam->height;
     p.samples = ao ? k->samples : 0; p.radius = k->radius; p.eps = k->eps;
     std::memcpy(p.bg, k->bg, 16);
     p.shard_index = sh.index; p.shard_count = sh.count; p.packed = sh.packed ? 1u : 0u;
     p.tiles_x = (cam->width + 7u) / 8u;
-    p.num_tiles = local_bands * p.tiles_x;           // a band is one row of 8x8 tiles
+    p.num_tiles = num_frames * local_bands * p.tiles_x;   // a band is one row of 8x8 tiles
     p.color = rt->color; p.prim_id = rt->prim_id; p.t = rt->t; p.occ = rt->occ;
     p.counters = ctx->counters;
     p.xcd_queues = ctx->opt_xcd_queues == 2 ? 0u : 1u;
@@ -742,10 +774,32 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
         p.mh_t = rt->mh_t;
     }
 
-    int per_cu = render_blocks_per_cu(lc);
+    const bool two_pass = lc.sched == 3;
+    int per_cu = render_blocks_per_cu(two_pass ? lc1 : lc);
     if (ctx->opt_bpc) per_cu = std::min(per_cu, ctx->opt_bpc);
     const int waves_per_block = lc.block / 64;
     int grid = std::max(1, std::min<int>(ctx->num_cus * per_cu, int((p.num_tiles + waves_per_block - 1) / waves_per_block)));
+    int grid2 = 0;
+    if (two_pass)
+    {
+        // scratch: a 32-B record and `samples` AO bytes per pixel slot of the frame's tiles
+        const size_t slots = size_t(64) * p.num_tiles;
+        if (ctx->hitrec_slots < slots || ctx->aobits_bytes < slots * p.samples)
+        {
+            VRH_HIP(hipStreamSynchronize(ctx->stream));   // earlier frames may still read them
+            if (ctx->hitrec) { (void)hipFree(ctx->hitrec); ctx->hitrec = nullptr; ctx->hitrec_slots = 0; }
+            if (ctx->aobits) { (void)hipFree(ctx->aobits); ctx->aobits = nullptr; ctx->aobits_bytes = 0; }
+            VRH_HIP(hipMalloc(&ctx->hitrec, slots * 32));
+            ctx->hitrec_slots = slots;
+            VRH_HIP(hipMalloc(&ctx->aobits, slots * 32));   // room for the largest sample count
+            ctx->aobits_bytes = slots * 32;
+        }
+        p.hitrec = ctx->hitrec;
+        p.aobits = ctx->aobits;
+        int per_cu2 = ao_pass_blocks_per_cu(lc);
+        if (ctx->opt_bpc) per_cu2 = std::min(per_cu2, ctx->opt_bpc);
+        grid2 = std::max(1, ctx->num_cus * per_cu2);
+    }
 
     const uint32_t slot = ctx->frames % VRH_MAX_TIMED_FRAMES;
     while (ctx->ev_start.size() <= slot)
@@ -758,13 +812,23 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     }
     VRH_HIP(hipMemsetAsync(ctx->counters, 0, COUNTERS_FRAME * sizeof(unsigned long long), ctx->stream));
     VRH_HIP(hipEventRecord(ctx->ev_start[slot], ctx->stream));
-    if (p.num_tiles > 0) VRH_HIP(launch_render(p, lc, grid, ctx->stream));
+    if (p.num_tiles > 0)
+    {
+        if (two_pass)
+        {
+            VRH_HIP(launch_render(p, lc1, grid, ctx->stream));
+            VRH_HIP(launch_ao_pass(p, lc, grid2, ctx->stream));
+            VRH_HIP(launch_ao_resolve(p, ctx->stream));
+        }
+        else
+            VRH_HIP(launch_render(p, lc, grid, ctx->stream));
+    }
     VRH_HIP(hipEventRecord(ctx->ev_stop[slot], ctx->stream));
     ctx->last_slot = slot;
     ctx->frames++;
 
     ctx->last = vrh_frame_stats{};
-    ctx->last.launches = p.num_tiles > 0 ? 1u : 0u;
+    ctx->last.launches = p.num_tiles > 0 ? (two_pass ? 3u : 1u) : 0u;
     ctx->last.grid_blocks = uint32_t(grid);
     ctx->last.block_threads = uint32_t(lc.block);
     ctx->last.stack_depth = cap;
