@@ -9,13 +9,18 @@ A "step" is one frame.  Inputs (BVH, primitives, normals) are resident in HBM be
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
+Frames in flight (default F = 8): every persistent launch renders F frames (vrh_render_batch),
+their tiles interleaved in the work queues, so no wave idles while the last tiles of a frame finish
+-- the kernel-level tail is paid once per F frames.  Every frame is fully traced and written; the
+last timed frames are checked against a separately rendered frame (frames_match_1gpu_frame).
+
 N > 1: one process per GPU; the image is sharded by 8-row bands (band b -> rank b % N, SURVEY.md
-§8e), each rank renders its packed shard, and the framebuffer is gathered to rank 0 over RCCL
-(torch.distributed "nccl"; prim ids + AO masks, 5 B/pixel) and un-interleaved there with the
-RGBA32F colour re-derived exactly (vrh_unshard).  Two frames are in flight: frame k renders while
-frame k-1's gather runs on RCCL's stream; the last frame's gather and un-interleave finish inside
-the timed region, so K steps = K complete frames on rank 0.  Total work per frame is fixed, so
-scaling is strong.
+§8e), each rank renders its packed shard of every frame, and the framebuffers are gathered to rank
+0 over RCCL (torch.distributed "nccl"; prim ids + AO masks, 5 B/pixel, one gather per launch) and
+un-interleaved there with the RGBA32F colour re-derived exactly (vrh_unshard).  Two launches are in
+flight: launch k renders while launch k-1's gather runs on RCCL's stream; the last launch's gather
+and un-interleave finish inside the timed region, so K steps = K complete frames on rank 0.  Total
+work (K frames) is fixed as N grows, so scaling is strong.
 
 Rank 0 prints one JSON line (contract in the task statement) with the roofline of the traversal
 kernel (algorithmic bytes per SURVEY.md §8d from a counting pass, over the hipEvent kernel time of
@@ -42,15 +47,17 @@ OUT_BYTES_PRIMARY = 24          # RGBA32F + u32 prim_id + f32 t per primary ray 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=16, help="untimed frames (default: two launches, so every buffer is touched)")
     ap.add_argument("--scene", default="hf1M", help="hf1M (C3, default) | hf10M (C4) | sph1M (C5)")
     ap.add_argument("--kernel", default=None, choices=["ao", "primary"], help="default: ao for triangles")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16, help="host cores for the CPU baseline")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, the measured path) | gloo (host-staged; single-GPU rehearsal only)")
-    ap.add_argument("--no-verify", action="store_true", help="skip the untimed N>1 check against a 1-GPU frame")
+    ap.add_argument("--no-verify", action="store_true", help="skip the untimed check of the last frames against a 1-GPU frame")
+    ap.add_argument("--frames-in-flight", type=int, default=8,
+                    help="frames per persistent launch (vrh_render_batch, 1..8); every frame is still fully traced")
     return ap.parse_args()
 
 
@@ -60,7 +67,13 @@ def cpu_baseline(scene, kernel, threads):
     from oracle import oracle as O
     samples = 8 if kernel == "ao" else 0
     if os.path.exists(O.REF_BENCH_BIN):
-        r = O.ref_bench(scene, threads, 3, 1920, 1080, samples, timeout=900)
+        print(f"cpu baseline: reference tiled_sched, {threads} threads ...", file=sys.stderr, flush=True)
+        try:
+            r = O.ref_bench(scene, threads, 3, 1920, 1080, samples, timeout=150)
+        except subprocess.TimeoutExpired:
+            # tiled_sched's lost-wakeup race can stall a frame: one more try (CPU only)
+            print("cpu baseline: timed out, retrying once", file=sys.stderr, flush=True)
+            r = O.ref_bench(scene, threads, 3, 1920, 1080, samples, timeout=150)
         return {"value": round(r["mrays_per_s"], 3), "unit": "Mrays/s", "cores": threads, "kind": "reference",
                 "sample": f"{scene} 1920x1080, {samples} AO spp, tiled_sched<basic_ray<simd::float4>> -O3 -msse4.1, "
                           f"median of 3 frames after 1 warm-up ({r['rays_per_frame']} rays/frame)"}
@@ -128,33 +141,50 @@ def main():
     kern = va.ao_kernel(dev) if kernel == "ao" else va.closest_hit_kernel(dev)
     kern_count = va.ao_kernel(dev, count_tests=True) if kernel == "ao" else va.closest_hit_kernel(dev, count_tests=True)
 
-    # ---- framebuffers: full image on rank 0, packed shard per rank for N > 1 ------------------
-    # Each rank writes its bands' prim ids and AO masks into ONE buffer [u32 prim ids | u8 masks]
-    # (5 B/pixel); one RCCL gather moves it to rank 0, which un-interleaves it and re-derives the
-    # RGBA32F colour exactly (vrh_unshard) -- the full framebuffer (RGBA32F + prim ids) on rank 0.
-    rows_max = _capi.VRH_BAND_ROWS * va.shard_bands(H, 0, world)
-    if world == 1:
-        rt = va.hip_buffer_rt(ctx, W, H)
-        shard = None
-    else:
-        # two frames in flight: frame k renders into slot k % 2 while frame k - 1's gather (RCCL,
-        # on its own stream) and un-interleave finish; every slot is reused only after the stream
-        # has waited for the gather that read it
-        n = rows_max * W
-        nslots = 2
-        locs = [torch.empty((5 * n,), dtype=torch.uint8, device="cuda") for _ in range(nslots)]
-        rts = [va.hip_buffer_rt(ctx, W, rows_max, wrap=(0, b.data_ptr(), 0, b.data_ptr() + 4 * n)) for b in locs]
-        rt = rts[0]
-        shard = _capi.vrh_shard(rank, world, 1, 0)
-        if rank == 0:
-            gathereds = [torch.empty((world, 5 * n), dtype=torch.uint8, device="cuda") for _ in range(nslots)]
-            full = va.hip_buffer_rt(ctx, W, H, flags=_capi.VRH_RT_COLOR | _capi.VRH_RT_PRIM_ID | _capi.VRH_RT_OCC)
+    # ---- frames in flight: every launch renders up to F frames (vrh_render_batch) -------------
+    F = max(1, min(args.frames_in_flight, _capi.VRH_MAX_BATCH))
 
-    def gather(slot):
-        loc = locs[slot]
+    def batches(k):
+        return [F] * (k // F) + ([k % F] if k % F else [])
+
+    # ---- framebuffers: full image on rank 0, packed shard per rank for N > 1 ------------------
+    # Each rank writes its bands' prim ids and AO masks into ONE buffer per batch
+    # [u32 prim ids of b frames | u8 masks of b frames] (5 B/pixel); one RCCL gather per batch moves
+    # it to rank 0, which un-interleaves every frame and re-derives the RGBA32F colour exactly
+    # (vrh_unshard) -- the full framebuffer (RGBA32F + prim ids) of every frame on rank 0.
+    rows_max = _capi.VRH_BAND_ROWS * va.shard_bands(H, 0, world)
+    n1 = rows_max * W                         # pixels of one frame's packed shard
+    shard = _capi.vrh_shard(rank, world, 1, 0) if world > 1 else None
+    nslots = 2                                # batch k renders while batch k - 1's gather runs
+    bufs = {}                                 # batch size -> buffers
+
+    def buffers(b):
+        if b in bufs:
+            return bufs[b]
+        if world == 1:
+            bufs[b] = {"rt": va.hip_buffer_rt(ctx, W, H * b)}
+            return bufs[b]
+        nb = n1 * b
+        locs = [torch.empty((5 * nb,), dtype=torch.uint8, device="cuda") for _ in range(nslots)]
+        d = {"locs": locs,
+             "rts": [va.hip_buffer_rt(ctx, W, rows_max * b, wrap=(0, x.data_ptr(), 0, x.data_ptr() + 4 * nb))
+                     for x in locs]}
+        if rank == 0:
+            d["gathered"] = [torch.empty((world, 5 * nb), dtype=torch.uint8, device="cuda") for _ in range(nslots)]
+        bufs[b] = d
+        return d
+
+    fulls = []
+    if world > 1 and rank == 0:
+        fulls = [va.hip_buffer_rt(ctx, W, H, flags=_capi.VRH_RT_COLOR | _capi.VRH_RT_PRIM_ID | _capi.VRH_RT_OCC)
+                 for _ in range(F)]
+
+    def gather(b, slot):
+        d = bufs[b]
+        loc = d["locs"][slot]
         if args.dist_backend == "nccl":
             if rank == 0:
-                return dist.gather(loc, gather_list=list(gathereds[slot].unbind(0)), dst=0, async_op=True)
+                return dist.gather(loc, gather_list=list(d["gathered"][slot].unbind(0)), dst=0, async_op=True)
             return dist.gather(loc, dst=0, async_op=True)
         # gloo rehearsal: stage through host memory, synchronously
         torch.cuda.synchronize()
@@ -162,34 +192,38 @@ def main():
         if rank == 0:
             hg = torch.empty((world, host.numel()), dtype=torch.uint8)
             dist.gather(host, gather_list=list(hg.unbind(0)), dst=0)
-            gathereds[slot].copy_(hg)
+            d["gathered"][slot].copy_(hg)
         else:
             dist.gather(host, dst=0)
         return None
 
-    pending = []          # (work, slot) of gathers not yet waited for, oldest first
+    pending = []          # (work, batch size, slot) of gathers not yet waited for, oldest first
 
     def finish_one():
-        work, slot = pending.pop(0)
+        work, b, slot = pending.pop(0)
         if work is not None:
             work.wait()   # the compute stream waits for the gather; the host does not block
         if rank == 0:
-            g = gathereds[slot].data_ptr()
-            va.unshard(ctx, W, H, world, full, prim_id_ptr=g, occ_ptr=g + 4 * n,
-                       shard_stride_bytes=5 * n, kernel=kern)
+            g = bufs[b]["gathered"][slot].data_ptr()
+            nb = n1 * b
+            for f in range(b):
+                va.unshard(ctx, W, H, world, fulls[f], prim_id_ptr=g + 4 * f * n1, occ_ptr=g + 4 * nb + f * n1,
+                           shard_stride_bytes=5 * nb, kernel=kern)
 
-    frame = [0]
+    launch = [0]
 
-    def step():
+    def run_batch(b):
+        d = buffers(b)
         if world == 1:
-            va.render(ctx, dev, rt, basis, kern, shard)
+            va.render_batch(ctx, dev, d["rt"], [basis] * b, kern, None)
             return
-        slot = frame[0] % nslots
-        frame[0] += 1
-        while len(pending) >= nslots:      # the slot's previous gather must be done before reuse
+        slot = launch[0] % nslots
+        launch[0] += 1
+        # the slot's previous gather must be done before it is overwritten
+        while any(pb == b and ps == slot for _, pb, ps in pending) or len(pending) >= nslots:
             finish_one()
-        va.render(ctx, dev, rts[slot], basis, kern, shard)
-        pending.append((gather(slot), slot))
+        va.render_batch(ctx, dev, d["rts"][slot], [basis] * b, kern, shard)
+        pending.append((gather(b, slot), b, slot))
 
     def drain():
         while pending:
@@ -200,32 +234,52 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    # ---- counting pass (untimed): box / primitive tests per ray for the algorithmic bytes ------
-    va.render(ctx, dev, rt, basis, kern_count, shard)
+    # ---- counting pass (untimed, one frame): box / primitive tests per ray ----------------------
+    one_rows = rows_max if world > 1 else H
+    rt_one = va.hip_buffer_rt(ctx, W, one_rows)
+    va.render(ctx, dev, rt_one, basis, kern_count, shard)
     cstats = ctx.last_frame_stats()
 
-    for _ in range(args.warmup):
-        step()
+    # ---- reference frame for the check below (rank 0, untimed): one vrh_render of the whole image
+    # on another traversal schedule (the item loop; the step loop for sphere scenes, whose default
+    # is the item loop) -- an independent code path, and a different kernel in the rocprof summary,
+    # so every launch of the measured kernel is an F-frame launch
+    ref = None
+    if not args.no_verify and rank == 0:
+        ctx.set_option("ao_schedule", 3 if args.scene.startswith("sph") else 4)
+        ref_rt = va.hip_buffer_rt(ctx, W, H)
+        va.render(ctx, dev, ref_rt, basis, kern, None)
+        ref = ref_rt.download(t=False)
+        ref_rt.close()
+        ctx.set_option("ao_schedule", 0)
+
+    for b in batches(args.warmup):
+        run_batch(b)
+    for b in set(batches(args.steps)):    # allocate the timed batches' buffers outside the timing
+        buffers(b)
     drain()
     barrier()
     ctx.stats_reset()
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    drain()               # the last frame's gather and un-interleave are inside the timed region
+    for b in batches(args.steps):
+        run_batch(b)
+    drain()               # the last batch's gather and un-interleave are inside the timed region
     barrier()
     elapsed = time.perf_counter() - t0
     acc = ctx.accum_stats()
+    last_b = batches(args.steps)[-1]
 
-    # ---- N > 1: the gathered frame must equal a 1-GPU frame (untimed check on rank 0) ------------
+    # ---- the timed frames are right: N > 1 gathered frames (rank 0) equal a 1-GPU frame ---------
     verified = None
-    if world > 1 and not args.no_verify and rank == 0:
-        ref_rt = va.hip_buffer_rt(ctx, W, H)
-        va.render(ctx, dev, ref_rt, basis, kern, None)
-        a = full.download(t=False)
-        b = ref_rt.download(t=False)
-        verified = bool(all((a[k].view("u1") == b[k].view("u1")).all() for k in ("color", "prim_id", "occ")))
+    if ref is not None:
+        b = ref
+        if world > 1:
+            outs = [fulls[f].download(t=False) for f in range(last_b)]
+        else:
+            a = bufs[last_b]["rt"].download(t=False)
+            outs = [{k: v[f * W * H:(f + 1) * W * H] for k, v in a.items()} for f in range(last_b)]
+        verified = bool(all((o[k].view("u1") == b[k].view("u1")).all() for o in outs for k in ("color", "prim_id", "occ")))
     barrier()
 
     # ---- aggregate over ranks -------------------------------------------------------------------
@@ -251,7 +305,8 @@ def main():
         primary_rays = W * H
         bytes_frame = NODE_BYTES * n_box + (s_prim + INDEX_BYTES) * n_prim + OUT_BYTES_PRIMARY * primary_rays
         bytes_per_ray = bytes_frame / n_rays
-        # dominant kernel = the traversal kernel; per-launch algorithmic bytes over its mean hipEvent time
+        # dominant kernel = the traversal kernel; per-launch (F frames) algorithmic bytes over its mean
+        # hipEvent time
         k_ms_mean = float(local_vals[2]) / max(float(local_vals[3]), 1.0)    # rank 0's launches
         local_bytes = bytes_per_ray * float(acc["rays"]) / max(float(acc["timed_frames"]), 1.0)
         achieved = local_bytes / (k_ms_mean * 1e-3) / 1e9
@@ -261,7 +316,8 @@ def main():
             try:
                 with open(pmc) as f:
                     pm = json.load(f)
-                if pm.get("scene") == args.scene and pm.get("kernel") == kernel and pm.get("gpus") == 1 and world == 1:
+                if (pm.get("scene") == args.scene and pm.get("kernel") == kernel and pm.get("gpus") == 1 and world == 1
+                        and pm.get("frames_per_launch", 1) == F):
                     traffic = pm.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
@@ -287,13 +343,15 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "render_kernel (traversal)", "kernel_ms_mean": round(k_ms_mean, 4),
+                "kernel": "render_unified_kernel (traversal)", "kernel_ms_mean": round(k_ms_mean, 4),
+                "frames_per_launch": F, "kernel_ms_per_frame": round(float(local_vals[2]) / args.steps, 4),
                 "bytes_per_ray": round(bytes_per_ray, 1), "box_tests_per_ray": round(n_box / n_rays, 3),
                 "prim_tests_per_ray": round(n_prim / n_rays, 3),
             },
             "cpu_baseline": cpu,
             "host_build_s": round(build_s, 3),
-            "gathered_frame_matches_1gpu": verified,
+            "frames_in_flight": F,
+            "frames_match_1gpu_frame": verified,
         }
         print(json.dumps(line), flush=True)
 

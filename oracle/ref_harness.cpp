@@ -654,6 +654,10 @@ static int run_bench(scene_desc const& d, aligned_vector<P>& prims, std::vector<
     uint64_t rays_per_frame = 0;
     for (int f = 0; f < frames; ++f)
     {
+        // the same lost wakeup between frames: a worker still leaving the last frame's tile loop
+        // misses the next notify_all, and if all of them do, frame() waits forever -- give them
+        // time to reach threads_start.wait() (outside the timed region)
+        std::this_thread::sleep_for(std::chrono::milliseconds(100));
         rays = 0;
         auto t0 = std::chrono::steady_clock::now();
         sched.frame(kernel, sparams);

@@ -5,7 +5,7 @@ gfx950 correction of MI355X_MICROARCH.md §HBM: FETCH_SIZE counts 128-B read req
 (TCC_EA0_RDREQ x 64), so the read side is doubled; WRITE_SIZE is taken as is.  FETCH_SIZE counts
 L2 misses towards the fabric, Infinity-Cache hits included, so it is an upper bound on DRAM bytes.
 
-    python tools/pmc_summary.py gpurun_out/pmc profiles/pmc_traffic.json scene kernel
+    python tools/pmc_summary.py gpurun_out/pmc profiles/pmc_traffic.json scene kernel [frames per launch]
 """
 import csv
 import json
@@ -30,10 +30,11 @@ def main():
     d, out = sys.argv[1], sys.argv[2]
     scene = sys.argv[3] if len(sys.argv) > 3 else "hf1M"
     kernel = sys.argv[4] if len(sys.argv) > 4 else "ao"
+    fpl = int(sys.argv[5]) if len(sys.argv) > 5 else 1
     c = {}
     for name in ("fetch", "write", "sq1", "sq2", "tcc", "lds"):
         c.update(load(d, name))
-    res = {"scene": scene, "kernel": kernel, "gpus": 1, "counters_per_dispatch": c}
+    res = {"scene": scene, "kernel": kernel, "gpus": 1, "frames_per_launch": fpl, "counters_per_dispatch": c}
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         read = c["FETCH_SIZE"] * 1024 * 2
         write = c["WRITE_SIZE"] * 1024

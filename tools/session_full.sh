@@ -1,17 +1,18 @@
 #!/bin/bash
 # Full measurement session: GPU tests, smoke, bench (default = C3) + other configs, rocprof
-# kernel trace of the bench command, PMC passes.  Each GPU step has its own time limit.
+# kernel trace of the bench command, PMC passes (PMC=0 skips them).  Each GPU step has its own
+# time limit; a fatal status (timeout, abort, segfault) ends the session.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 fatal() { case "$1" in 124|134|137|139) return 0;; esac; return 1; }
-step() { local name=$1 limit=$2; shift 2; echo "== $name"; timeout -k 10 $limit "$@" > gpurun_out/$name.log 2>&1; local rc=$?; tail -${TAILN:-3} gpurun_out/$name.log; echo "$name rc=$rc"; if fatal $rc; then exit $rc; fi; }
-TAILN=4 step pytest_gpu 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 200
+step() { local name=$1 limit=$2; shift 2; echo "== $name"; timeout -k 10 $limit "$@" > gpurun_out/$name.log 2>&1; local rc=$?; grep -v amdgpu.ids gpurun_out/$name.log | tail -${TAILN:-2} | cut -c1-1200; echo "$name rc=$rc"; if fatal $rc; then exit $rc; fi; }
+TAILN=4 step pytest_gpu 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py
-step bench_c2 300 python bench.py --kernel primary --no-cpu-baseline --steps 20
-step bench_c4 300 python bench.py --scene hf10M --no-cpu-baseline --steps 10
-step bench_c5 300 python bench.py --scene sph1M --no-cpu-baseline --steps 20
-step rocprof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline
-if [ -n "$PMC" ]; then step pmc 900 bash tools/profile_pmc.sh; fi
+step bench_c2 300 python bench.py --kernel primary --no-cpu-baseline
+step bench_c4 300 python bench.py --scene hf10M --no-cpu-baseline
+step bench_c5 300 python bench.py --scene sph1M --no-cpu-baseline
+TAILN=1 step rocprof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline
+if [ "${PMC:-1}" != 0 ]; then TAILN=20 step pmc 900 bash tools/profile_pmc.sh; fi
 exit 0

@@ -33,7 +33,7 @@ struct render_params
     float bg[4];
 
     uint32_t shard_index, shard_count, packed;
-    uint32_t tiles_x, num_tiles;   // num_tiles = work units of the launch: frames x tiles per frame
+    uint32_t tiles_x, num_tiles;   // tiles of ONE frame (the launch has num_frames x num_tiles units)
 
     float4* color;
     uint32_t* prim_id;

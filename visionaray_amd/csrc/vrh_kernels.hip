@@ -33,21 +33,16 @@ constexpr int AO_MASKS = 64 * AO_REC_WORDS;             // u32 masks[2][64]
 constexpr int AO_SLOT_PX = AO_MASKS + 2 * 64;           // u8 slot_px[2][64]: pixel (lane) of a hit slot
 constexpr int AO_WAVE_WORDS = AO_SLOT_PX + 2 * 64 / 4;
 
-// work unit -> frame f (unit % frames: the frames of a launch interleave tile by tile, so every
-// queue range below is the same image strip of each frame), tile (unit / frames) -> (x, y) of lane,
-// plus the output row (frame f's rows start at f * frame_rows; packed shards).  A band is one row
-// of tiles.
-__device__ __forceinline__ bool tile_pixel(const render_params& P, uint32_t unit, uint32_t lane,
+// tile id (next_tile: frame f << TILE_FRAME_SHIFT | tile of that frame) -> (x, y) of lane, plus the
+// output row (frame f's rows start at f * frame_rows; packed shards).  A band is one row of tiles.
+constexpr uint32_t TILE_FRAME_SHIFT = 29;
+constexpr uint32_t TILE_MASK = (1u << TILE_FRAME_SHIFT) - 1u;
+__device__ __forceinline__ bool tile_pixel(const render_params& P, uint32_t id, uint32_t lane,
                                            uint32_t& x, uint32_t& y, uint32_t& out_row, uint32_t& f)
 {
     static_assert(BAND == TILE, "a shard band is one row of 8x8 tiles");
-    uint32_t tile = unit;
-    f = 0;
-    if (P.num_frames > 1)
-    {
-        tile = unit / P.num_frames;
-        f = unit - tile * P.num_frames;
-    }
+    f = id >> TILE_FRAME_SHIFT;
+    const uint32_t tile = id & TILE_MASK;
     uint32_t lb = tile / P.tiles_x;               // local band
     uint32_t tx = tile - lb * P.tiles_x;
     uint32_t band = lb * P.shard_count + P.shard_index;
@@ -79,11 +74,14 @@ __device__ __forceinline__ ray_t primary_ray(const render_params& P, uint32_t f,
     return make_ray(mk3(c.eye[0], c.eye[1], c.eye[2]), dir);
 }
 
-// Tile work queues.  The frame's tiles are split into 8 contiguous ranges (horizontal image
-// strips); a wave first drains the range of the XCD it runs on (hardware register XCC_ID), so the
-// BVH nodes of a strip stay in that XCD's L2, then steals from the other ranges in turn.  Which XCD
-// a wave lands on only changes speed: every tile is handed out exactly once by one of the 8
-// atomic heads.  Called by the whole wave; returns the tile or NONE when all ranges are empty.
+// Tile work queues.  A frame's tiles are split into 8 contiguous ranges (horizontal image strips);
+// queue q hands out strip q of frame 0, then strip q of frame 1, ... (frames of one launch,
+// vrh_render_batch).  A wave first drains the queue of the XCD it runs on (hardware register
+// XCC_ID), so the BVH nodes of a strip stay in that XCD's L2, then steals from the other queues in
+// turn -- a wave never idles while another frame of the launch still has tiles.  Which XCD a wave
+// lands on only changes speed: every (frame, tile) is handed out exactly once by one of the 8
+// atomic heads.  Called by the whole wave; returns the tile id (frame << TILE_FRAME_SHIFT | tile)
+// or NONE when all queues are empty.
 struct tile_queue
 {
     uint32_t q;       // range currently drained (wave-uniform)
@@ -102,21 +100,37 @@ __device__ __forceinline__ tile_queue queue_init(const render_params& P)
     return tile_queue{ P.xcd_queues ? xcc_id() : 0u, 0u };
 }
 
+// first tile of strip q of a frame (num_tiles * q / nq)
+__device__ __forceinline__ uint32_t strip_lo(const render_params& P, uint32_t q, uint32_t nq)
+{
+    return (uint32_t)(((uint64_t)P.num_tiles * q) / nq);
+}
+
 __device__ __forceinline__ uint32_t next_tile(const render_params& P, tile_queue& tq, uint32_t lane)
 {
     const uint32_t nq = P.xcd_queues ? 8u : 1u;
     while (tq.tried < nq)
     {
-        const uint32_t lo = (uint32_t)(((uint64_t)P.num_tiles * tq.q) / nq);
-        const uint32_t hi = (uint32_t)(((uint64_t)P.num_tiles * (tq.q + 1u)) / nq);
+        const uint32_t lo = strip_lo(P, tq.q, nq);
+        const uint32_t len = strip_lo(P, tq.q + 1u, nq) - lo;
         uint32_t t = 0;
         if (lane == 0) t = atomicAdd(reinterpret_cast<uint32_t*>(P.counters + 8u + 8u * tq.q), 1u);
         t = __shfl(t, 0);
-        if (lo + t < hi) return lo + t;
+        if (t < len * P.num_frames)
+        {
+            const uint32_t f = t / len;
+            return (f << TILE_FRAME_SHIFT) | (lo + t - f * len);
+        }
         tq.q = (tq.q + 1u) % nq;
         tq.tried += 1u;
     }
     return NONE;
+}
+
+// two-pass AO: hit list q holds up to 64 records per (frame, tile) of queue q; its first slot
+__device__ __forceinline__ uint32_t list_base(const render_params& P, uint32_t q, uint32_t nq)
+{
+    return 64u * P.num_frames * strip_lo(P, q, nq);
 }
 
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask)
@@ -369,8 +383,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     j0 = __shfl(j0, first);
                     if (mine)
                     {
-                        const uint32_t rec = 64u * (uint32_t)(((uint64_t)P.num_tiles * q0) / (P.xcd_queues ? 8u : 1u))
-                                           + j0 + lane_rank(m);
+                        const uint32_t rec = list_base(P, q0, P.xcd_queues ? 8u : 1u) + j0 + lane_rank(m);
                         const f3 pos = r.ori + r.dir * best_t;
                         const float4 nn = P.normals[best_prim];
                         P.hitrec[2u * rec] = make_float4(pos.x, pos.y, pos.z, __uint_as_float(lane_px));
@@ -616,7 +629,7 @@ __global__ __launch_bounds__(256, OCC) void ao_pass_kernel(render_params P)
             {
                 const uint32_t g = a + cand;
                 const uint32_t j = g / S, s = g - j * S;
-                const uint32_t rec = 64u * (uint32_t)(((uint64_t)P.num_tiles * q) / nq) + j;
+                const uint32_t rec = list_base(P, q, nq) + j;
                 const float4 r0 = P.hitrec[2u * rec], r1 = P.hitrec[2u * rec + 1u];
                 const f3 pos = mk3(r0.x, r0.y, r0.z), nrm = mk3(r1.x, r1.y, r1.z);
                 // vector3.inl:357-367 make_orthonormal_basis(u, v, w = n)
@@ -682,12 +695,13 @@ __global__ __launch_bounds__(256, OCC) void ao_pass_kernel(render_params P)
 __global__ void ao_resolve_kernel(render_params P)
 {
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
-    if (slot >= 64u * P.num_tiles) return;
+    if (slot >= 64u * P.num_frames * P.num_tiles) return;
     const uint32_t nq = P.xcd_queues ? 8u : 1u;
-    // list q owns record slots [64 lo(q), 64 lo(q + 1)), lo(q) = num_tiles * q / nq
-    const uint32_t tile = slot / 64u;
+    // list q owns record slots [64 F lo(q), 64 F lo(q + 1)), lo(q) = strip_lo(q), F = frames, so
+    // slot / (64 F) is a tile of strip q
+    const uint32_t tile = slot / (64u * P.num_frames);
     const uint32_t q = (uint32_t)((((uint64_t)tile + 1u) * nq - 1u) / P.num_tiles);
-    const uint32_t j = slot - 64u * (uint32_t)(((uint64_t)P.num_tiles * q) / nq);
+    const uint32_t j = slot - list_base(P, q, nq);
     if (j >= *reinterpret_cast<const uint32_t*>(P.counters + COUNTERS_HITS + 8u * q)) return;
     const uint32_t o = __float_as_uint(P.hitrec[2u * slot + 1u].w);
     const uint32_t S = P.samples;
@@ -1105,7 +1119,7 @@ int ao_pass_blocks_per_cu(const launch_config& c)
 
 hipError_t launch_ao_resolve(const render_params& p, hipStream_t s)
 {
-    const uint32_t n = 64u * p.num_tiles;
+    const uint32_t n = 64u * p.num_frames * p.num_tiles;
     hipLaunchKernelGGL(dev::ao_resolve_kernel, dim3((n + 255u) / 256u), dim3(256), 0, s, p);
     return hipGetLastError();
 }

@@ -753,7 +753,8 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     std::memcpy(p.bg, k->bg, 16);
     p.shard_index = sh.index; p.shard_count = sh.count; p.packed = sh.packed ? 1u : 0u;
     p.tiles_x = (cam->width + 7u) / 8u;
-    p.num_tiles = num_frames * local_bands * p.tiles_x;   // a band is one row of 8x8 tiles
+    p.num_tiles = local_bands * p.tiles_x;        // a band is one row of 8x8 tiles
+    VRH_CHECK(uint64_t(p.num_tiles) * 64u * num_frames < (1ull << 32), "vrh_render: image too large");
     p.color = rt->color; p.prim_id = rt->prim_id; p.t = rt->t; p.occ = rt->occ;
     p.counters = ctx->counters;
     p.xcd_queues = ctx->opt_xcd_queues == 2 ? 0u : 1u;
@@ -778,12 +779,13 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     int per_cu = render_blocks_per_cu(two_pass ? lc1 : lc);
     if (ctx->opt_bpc) per_cu = std::min(per_cu, ctx->opt_bpc);
     const int waves_per_block = lc.block / 64;
-    int grid = std::max(1, std::min<int>(ctx->num_cus * per_cu, int((p.num_tiles + waves_per_block - 1) / waves_per_block)));
+    const uint64_t units = uint64_t(num_frames) * p.num_tiles;
+    int grid = std::max(1, int(std::min<uint64_t>(uint64_t(ctx->num_cus) * per_cu, (units + waves_per_block - 1) / waves_per_block)));
     int grid2 = 0;
     if (two_pass)
     {
         // scratch: a 32-B record and `samples` AO bytes per pixel slot of the frame's tiles
-        const size_t slots = size_t(64) * p.num_tiles;
+        const size_t slots = size_t(64) * units;
         if (ctx->hitrec_slots < slots || ctx->aobits_bytes < slots * p.samples)
         {
             VRH_HIP(hipStreamSynchronize(ctx->stream));   // earlier frames may still read them
