@@ -468,6 +468,34 @@ public:
         rt.end_frame();
     }
 
+    // frames in flight (vrh_render_batch): ONE persistent launch renders cams.size() frames of
+    // one scene and kernel (up to VRH_MAX_BATCH), camera f into rows [f * H, (f + 1) * H) of rt,
+    // whose height is cams.size() * H.  Every frame equals its own frame() call; the launch's tail
+    // is paid once instead of once per frame.  Synchronous like frame().
+    template <typename K, typename Camera, typename RT>
+    void frames(K kernel, std::vector<Camera> const& cams, RT& rt, unsigned frame_num = 0)
+    {
+        static_assert(std::is_same<K, hip_builtin_kernel>::value,
+                      "hip_sched runs the built-in kernels: an arbitrary callable cannot cross the C ABI");
+        if (cams.empty() || rt.height() % cams.size() != 0)
+            throw std::runtime_error("hip_sched::frames: render target height must be frames x image height");
+        const uint32_t W = uint32_t(rt.width()), H = uint32_t(rt.height() / cams.size());
+        std::vector<vrh_camera> c(cams.size());
+        for (size_t f = 0; f < cams.size(); ++f)
+        {
+            auto const& cam = cams[f];
+            float eye[3] = { cam.eye().x, cam.eye().y, cam.eye().z };
+            float center[3] = { cam.center().x, cam.center().y, cam.center().z };
+            float up[3] = { cam.up().x, cam.up().y, cam.up().z };
+            hip_detail::check(vrh_make_camera(eye, center, up, cam.fovy(), cam.aspect(), W, H, &c[f]), "vrh_make_camera");
+        }
+        rt.begin_frame();
+        hip_detail::check(vrh_render_batch(ctx_->get(), kernel.scene, rt.handle(), c.data(), uint32_t(c.size()),
+                                           &kernel.desc, nullptr, frame_num),
+                          "vrh_render_batch");
+        rt.end_frame();
+    }
+
     hip_context& context() const { return *ctx_; }
 
 private:

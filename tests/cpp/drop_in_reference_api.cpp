@@ -16,6 +16,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 using namespace visionaray;
@@ -59,11 +60,46 @@ int main(int argc, char** argv)
         std::vector<uint32_t> pid(n);
         std::vector<uint8_t> occ(n);
         rt.download(color.data(), pid.data(), t.data(), occ.data());
+        unsigned long long rays = sched.context().last_frame_stats().rays;
+
+        // frames in flight: three frames (the reference camera, then the eye raised twice) in one
+        // launch; each must equal its own frame() call
+        std::vector<camera> cams(3, cam);
+        cams[1].look_at(vec3(0.0f, 1.0f, 1.4f), vec3(0.0f), vec3(0.0f, 1.0f, 0.0f));
+        cams[2].look_at(vec3(0.0f, 1.1f, 1.4f), vec3(0.0f), vec3(0.0f, 1.0f, 0.0f));
+        hip_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> rt3;
+        rt3.resize(W, 3 * H);
+        auto kern = make_hip_ao_kernel(device_bvh, vec4(0.1f, 0.2f, 0.3f, 1.0f));
+        sched.frames(kern, cams, rt3);
+        std::vector<float> color3(12 * n), t3(3 * n);
+        std::vector<uint32_t> pid3(3 * n);
+        std::vector<uint8_t> occ3(3 * n);
+        rt3.download(color3.data(), pid3.data(), t3.data(), occ3.data());
+        bool batch_ok = true;
+        for (size_t f = 0; f < 3; ++f)
+        {
+            hip_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> one;
+            one.resize(W, H);
+            auto sp = make_sched_params(pixel_sampler::uniform_type{}, cams[f], one);
+            sched.frame(kern, sp);
+            one.download(color.data(), pid.data(), t.data(), occ.data());
+            batch_ok = batch_ok && std::memcmp(color.data(), color3.data() + 4 * f * n, 16 * n) == 0
+                && std::memcmp(pid.data(), pid3.data() + f * n, 4 * n) == 0
+                && std::memcmp(t.data(), t3.data() + f * n, 4 * n) == 0
+                && std::memcmp(occ.data(), occ3.data() + f * n, n) == 0;
+        }
+        batch_ok = batch_ok && std::memcmp(pid3.data(), pid3.data() + n, 4 * n) != 0;   // distinct cameras
+        // the first frame of the batch is the reference camera's frame
+        std::memcpy(color.data(), color3.data(), 16 * n);
+        std::memcpy(pid.data(), pid3.data(), 4 * n);
+        std::memcpy(t.data(), t3.data(), 4 * n);
+        std::memcpy(occ.data(), occ3.data(), n);
+
         printf("{\"grid\":%u,\"W\":%u,\"H\":%u,\"rays\":%llu,\"primid_hash\":\"%016llx\",\"t_hash\":\"%016llx\","
-               "\"occ_hash\":\"%016llx\",\"color_hash\":\"%016llx\"}\n", grid, W, H,
-               (unsigned long long)sched.context().last_frame_stats().rays,
+               "\"occ_hash\":\"%016llx\",\"color_hash\":\"%016llx\",\"batch_ok\":%s}\n", grid, W, H, rays,
                (unsigned long long)fnv1a(pid.data(), n * 4), (unsigned long long)fnv1a(t.data(), n * 4),
-               (unsigned long long)fnv1a(occ.data(), n), (unsigned long long)fnv1a(color.data(), n * 16));
+               (unsigned long long)fnv1a(occ.data(), n), (unsigned long long)fnv1a(color.data(), n * 16),
+               batch_ok ? "true" : "false");
     }
     catch (std::exception const& e)
     {

@@ -57,6 +57,7 @@ def test_reference_api_program_on_hip_backend(golden):
     out = _run(DROPIN, 200, g["W"], g["H"])
     for k in ("primid_hash", "t_hash", "occ_hash", "color_hash"):
         assert out[k] == g[k], k
+    assert out["batch_ok"], "hip_sched::frames: a frame of the batch differs from its own frame()"
 
 
 DROPIN_SHADE = os.path.join(ROOT, "oracle", "_ref", "dropin_simple_kernel")
