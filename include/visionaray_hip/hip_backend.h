@@ -386,6 +386,42 @@ private:
     std::shared_ptr<vrh_shading> shading_;
 };
 
+// Mask intersector (vrh_hit_mask_create): what the intersector example's mask_intersector
+// (examples/intersector/main.cpp:251-330, a basic_intersector clearing hr.hit from a mask over the
+// hit's texture coordinate) does, with the mask given as data.  tex_coords: 3 per prim_id (the
+// model's tex_coords, any type with .x / .y); mask: w x h bytes, row-major.
+class hip_hit_mask
+{
+public:
+    template <typename TexCoords>
+    hip_hit_mask(TexCoords const& tex_coords, uint8_t const* mask, unsigned w, unsigned h,
+                 std::shared_ptr<hip_context> ctx = hip_context::default_context())
+        : ctx_(std::move(ctx))
+    {
+        std::vector<float> tc;
+        tc.reserve(2 * tex_coords.size());
+        for (auto const& c : tex_coords) { tc.push_back(c.x); tc.push_back(c.y); }
+        vrh_hit_mask* m = nullptr;
+        hip_detail::check(vrh_hit_mask_create(ctx_->get(), tc.data(), uint32_t(tex_coords.size()), mask, w, h, &m),
+                          "vrh_hit_mask_create");
+        mask_.reset(m, [](vrh_hit_mask* p) { vrh_hit_mask_free(p); });
+    }
+
+    vrh_hit_mask* handle() const { return mask_.get(); }
+
+private:
+    std::shared_ptr<hip_context> ctx_;
+    std::shared_ptr<vrh_hit_mask> mask_;
+};
+
+// closest_hit(ray, begin, end, intersector) / any_hit(..., intersector) for every ray of a built-in
+// kernel (traverse_linear.inl:232-329): the kernel with the mask intersector attached
+inline hip_builtin_kernel with_intersector(hip_builtin_kernel k, hip_hit_mask const& mask)
+{
+    k.desc.hit_mask = mask.handle();
+    return k;
+}
+
 // simple::kernel over make_kernel_params(binding, prims, normals, materials, lights, bounces, eps,
 // bg, ambient): the normals live in the hip_index_bvh (face normals at upload, per-vertex normals
 // via set_vertex_normals), materials / lights in the hip_shading

@@ -106,6 +106,8 @@ typedef struct {
     uint32_t width, height;   /* full image size (primary ray u,v and the AO pixel index use it) */
 } vrh_camera;
 
+typedef struct vrh_hit_mask vrh_hit_mask;   /* see vrh_hit_mask_create                      */
+
 typedef struct {
     uint32_t kind;            /* vrh_kernel_kind                                          */
     uint32_t samples;         /* AO samples per hit pixel (ao/main.cpp default 8, <= 32)   */
@@ -120,6 +122,7 @@ typedef struct {
     const vrh_shading* shading;   /* materials + lights (vrh_shading_create)              */
     uint32_t max_hits;        /* VRH_KERNEL_MULTI_HIT: N (1..VRH_MAX_HITS)                  */
     uint32_t num_bounces;     /* VRH_KERNEL_WHITTED: num_bounces (viewer default 4)          */
+    const vrh_hit_mask* hit_mask; /* mask intersector for triangles (NULL: none)              */
 } vrh_kernel_desc;
 
 enum vrh_kernel_flags {
@@ -349,6 +352,23 @@ VRH_API int vrh_obj_get_data(const vrh_obj* obj, void* triangles, float* geometr
 VRH_API const char* vrh_obj_material_name(const vrh_obj* obj, uint32_t index);     /* "" for padding */
 VRH_API const char* vrh_obj_material_texture(const vrh_obj* obj, uint32_t index);  /* map_Kd or ""   */
 VRH_API int vrh_obj_free(vrh_obj* obj);
+
+/* Mask intersector <- a basic_intersector (intersector.h:24-119) whose
+ * operator()(ray, basic_triangle) wraps intersect() and clears hr.hit where a mask over the hit's
+ * texture coordinate says so -- the intersector example's mask_intersector
+ * (examples/intersector/main.cpp:251-330), with the example's procedural heart test given as data.
+ * Per-triangle texture coordinates (3 x vec2 per prim_id, the model's tex_coords layout,
+ * get_tex_coord.h:25-38) and a W x H byte mask: a triangle hit at barycentrics (u, v) is kept iff
+ *   tc = lerp(tc[3p], tc[3p+1], tc[3p+2], u, v)              (math.h:468-475, operation order kept)
+ *   i  = x < W ? u32(x) : W - 1,  x = (tc.x > 0 ? tc.x : 0) * float(W)   (j likewise with H)
+ *   mask[j * W + i] != 0.
+ * Applied to every triangle hit of every ray of the kernel (closest hit, AO / shadow any hit,
+ * multi_hit, the shading kernels), in the leaf test itself -- no extra pass, no indirect call.
+ * Spheres are not masked.  Kernels with a mask run the step-loop schedule. */
+VRH_API int vrh_hit_mask_create(vrh_ctx* ctx, const float* tex_coords, uint32_t num_tex_coords,
+                                const uint8_t* mask, uint32_t mask_width, uint32_t mask_height,
+                                vrh_hit_mask** out);
+VRH_API int vrh_hit_mask_free(vrh_hit_mask* mask);
 
 /* synthetic scenes of SURVEY.md Appendix A (bench / test inputs) */
 VRH_API int vrh_gen_heightfield(uint32_t grid, void* tris_out);        /* 2*grid*grid TRI64   */

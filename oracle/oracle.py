@@ -45,9 +45,14 @@ class _Counters(C.Structure):
     _fields_ = [("box_tests", C.c_uint64), ("prim_tests", C.c_uint64)]
 
 
+class _HitMask(C.Structure):
+    _fields_ = [("tc", C.c_void_p), ("mask", C.c_void_p), ("w", C.c_int), ("h", C.c_int)]
+
+
 class _Scene(C.Structure):
     _fields_ = [("nodes", C.c_void_p), ("indices", C.c_void_p), ("prims", C.c_void_p),
-                ("kind", C.c_int), ("normals", C.c_void_p), ("vertex_normals", C.c_void_p)]
+                ("kind", C.c_int), ("normals", C.c_void_p), ("vertex_normals", C.c_void_p),
+                ("hit_mask", C.c_void_p)]
 
 
 class _Camera(C.Structure):
@@ -207,17 +212,25 @@ def make_scene(name):
 
 
 def _structs(scene, cam, mode, samples=8, radius=0.1, eps=1e-3, bg=(0.1, 0.2, 0.3, 1.0), materials=None,
-             lights=None, ambient=(0.0, 0.0, 0.0, 0.0), binding=VO_NORMALS_PER_FACE, max_hits=0, num_bounces=0):
+             lights=None, ambient=(0.0, 0.0, 0.0, 0.0), binding=VO_NORMALS_PER_FACE, max_hits=0, num_bounces=0,
+             hit_mask=None):
+    hm = None
+    if hit_mask is not None:
+        tc, mask = hit_mask
+        tc = np.ascontiguousarray(tc, np.float32)
+        mask = np.ascontiguousarray(mask, np.uint8)
+        hm = _HitMask(_p(tc).value, _p(mask).value, mask.shape[1], mask.shape[0])
     s = _Scene(_p(scene.nodes).value, _p(scene.indices).value, _p(scene.prims).value, scene.kind,
                _p(scene.normals).value if scene.normals is not None else None,
-               _p(scene.vertex_normals).value if scene.vertex_normals is not None else None)
+               _p(scene.vertex_normals).value if scene.vertex_normals is not None else None,
+               C.cast(C.pointer(hm), C.c_void_p).value if hm is not None else None)
     eye, u, v, w, W, H = cam
     c = _Camera((C.c_float * 3)(*eye), (C.c_float * 3)(*u), (C.c_float * 3)(*v), (C.c_float * 3)(*w), W, H)
     k = _Kernel(mode, samples, radius, eps, (C.c_float * 4)(*bg),
                 _p(materials).value if materials is not None else None, 0 if materials is None else len(materials),
                 _p(lights).value if lights is not None else None, 0 if lights is None else len(lights),
                 (C.c_float * 4)(*ambient), binding, max_hits, num_bounces)
-    _structs.keep = (materials, lights)
+    _structs.keep = (materials, lights, hm, hit_mask and (tc, mask))
     return s, c, k
 
 
@@ -289,10 +302,10 @@ def make_shade_scene(name):
     return Scene(name, kind, prims, nodes, idx, fn, depth, vertex_normals(fn))
 
 
-def render_simple(scene, cam, binding, rows=None, threads=0):
+def render_simple(scene, cam, binding, rows=None, threads=0, hit_mask=None):
     m, lt, amb, bg = shade_spec()
     return render(scene, cam, mode=VO_MODE_SIMPLE, rows=rows, threads=threads, materials=m, lights=lt,
-                  ambient=amb, bg=bg, binding=binding)
+                  ambient=amb, bg=bg, binding=binding, hit_mask=hit_mask)
 
 
 def whitted_spec():
@@ -304,13 +317,13 @@ def whitted_spec():
     return m, l3, amb, bg
 
 
-def render_whitted(scene, cam, binding, num_bounces=4, eps=1e-3, rows=None, threads=0):
+def render_whitted(scene, cam, binding, num_bounces=4, eps=1e-3, rows=None, threads=0, hit_mask=None):
     m, lt, amb, bg = whitted_spec()
     return render(scene, cam, mode=VO_MODE_WHITTED, rows=rows, threads=threads, materials=m, lights=lt,
-                  ambient=amb, bg=bg, binding=binding, num_bounces=num_bounces, eps=eps)
+                  ambient=amb, bg=bg, binding=binding, num_bounces=num_bounces, eps=eps, hit_mask=hit_mask)
 
 
-def render_multi(scene, cam, binding, max_hits=16, threads=0):
+def render_multi(scene, cam, binding, max_hits=16, threads=0, hit_mask=None):
     """multi_hit<max_hits> frame: hit lists (W*H, max_hits) + the multi_hit example's colour."""
     m, lt, amb, bg = shade_spec()
     _, _, _, _, W, H = cam
@@ -318,7 +331,7 @@ def render_multi(scene, cam, binding, max_hits=16, threads=0):
            "mh_prim_id": np.full((H * W, max_hits), 0xFFFFFFFF, np.uint32),
            "mh_t": np.full((H * W, max_hits), -1.0, np.float32)}
     s, c, k = _structs(scene, cam, VO_MODE_MULTI_HIT, materials=m, lights=lt, ambient=amb, bg=bg, binding=binding,
-                       max_hits=max_hits)
+                       max_hits=max_hits, hit_mask=hit_mask)
     lib().vo_render_multi(C.byref(s), C.byref(c), C.byref(k), _p(out["color"]), _p(out["mh_prim_id"]),
                           _p(out["mh_t"]), threads)
     return out

@@ -233,9 +233,42 @@ static camera make_camera(scene_desc const& d, int W, int H)
 // golden: scalar simple_sched frame, primary closest hit + parity AO
 //
 
-template <typename P>
+//-------------------------------------------------------------------------------------------------
+// mask: the intersector example's mask_intersector (examples/intersector/main.cpp:251-330) -- a
+// basic_intersector (intersector.h:24-119) whose triangle operator() clears hr.hit where a mask over
+// the hit's texture coordinate (get_tex_coord.h:25-38 -> lerp, math.h:468-475) says so -- with the
+// example's procedural heart replaced by a byte mask (the test's data), looked up at the nearest
+// texel exactly as vrh.h vrh_hit_mask_create states
+//
+
+struct mask_intersector : basic_intersector<mask_intersector>
+{
+    using basic_intersector<mask_intersector>::operator();
+
+    template <typename R, typename S>
+    auto operator()(R const& ray, basic_triangle<3, S> const& tri) -> decltype( intersect(ray, tri) )
+    {
+        auto hr = intersect(ray, tri);
+        if (!hr.hit) return hr;
+        vec2 tc = get_tex_coord(tex_coords, hr, tri);
+        hr.hit &= mask[texel(tc.y, h) * unsigned(w) + texel(tc.x, w)] != 0;
+        return hr;
+    }
+
+    static unsigned texel(float c, int n)
+    {
+        float x = (c > 0.0f ? c : 0.0f) * float(n);
+        return x < float(n) ? unsigned(x) : unsigned(n - 1);
+    }
+
+    vec2 const* tex_coords = nullptr;
+    uint8_t const* mask = nullptr;
+    int w = 0, h = 0;
+};
+
+template <typename P, typename Isect = default_intersector>
 static int run_golden(scene_desc const& d, aligned_vector<P>& prims, std::vector<vec3> const& normals,
-                      std::string const& outdir, int W, int H, bool do_ao)
+                      std::string const& outdir, int W, int H, bool do_ao, Isect isect = Isect{})
 {
     auto t0 = std::chrono::steady_clock::now();
     auto bvh = build<index_bvh<P>>(prims.data(), prims.size());
@@ -295,7 +328,7 @@ static int run_golden(scene_desc const& d, aligned_vector<P>& prims, std::vector
     {
         result_record<float> result;
         result.color = bg;
-        auto hr = closest_hit(r, prims_begin, prims_end);
+        auto hr = closest_hit(r, prims_begin, prims_end, isect);
         result.hit = hr.hit;
         size_t p = size_t(y) * W + x;
         if (!hr.hit) return result;
@@ -325,7 +358,7 @@ static int run_golden(scene_desc const& d, aligned_vector<P>& prims, std::vector
             ray ao;
             ao.ori = hr.isect_pos + dir * 1E-3f;
             ao.dir = dir;
-            auto ar = any_hit(ao, prims_begin, prims_end, 0.1f);
+            auto ar = any_hit(ao, prims_begin, prims_end, 0.1f, isect);
             ++ao_rays;
             if (ar.hit) { clr = clr - 1.0f / 8; mask |= uint8_t(1u << smp); ++ao_occ; }
         }
@@ -730,6 +763,39 @@ int main(int argc, char** argv)
         std::vector<vec3> normals(t.size());
         for (size_t i = 0; i < t.size(); ++i) normals[i] = normalize(cross(t[i].e1, t[i].e2));
         return run_shade(d, t, normals, outdir, per_vertex, W, H, mode == "whitted", bounces, eps);
+    }
+    if (mode == "mask")
+    {
+        // mask <scene> <outdir> <mask.bin> <mask_w> <mask_h> [W H]: golden frame (primary + AO) with
+        // the mask intersector; tex coords = planar (x, z) projection of every corner, written to
+        // outdir/tex_coords.bin
+        if (argc < 7 || d.spheres) return 2;
+        std::string outdir = argv[3];
+        int mw = atoi(argv[5]), mh = atoi(argv[6]);
+        int W = argc > 8 ? atoi(argv[7]) : d.W;
+        int H = argc > 8 ? atoi(argv[8]) : d.H;
+        std::vector<uint8_t> mask(size_t(mw) * mh);
+        FILE* f = fopen(argv[4], "rb");
+        if (!f || fread(mask.data(), 1, mask.size(), f) != mask.size()) { if (f) fclose(f); return 3; }
+        fclose(f);
+        aligned_vector<tri_t> t;
+        if (d.grid == 0) make_cornell(t); else if (d.layers) make_hfstack(d.grid, d.layers, t); else make_heightfield(d.grid, t);
+        std::vector<vec3> normals(t.size());
+        for (size_t i = 0; i < t.size(); ++i) normals[i] = normalize(cross(t[i].e1, t[i].e2));
+        // per prim_id: corners v1, v1 + e1, v1 + e2 -> (x * 0.5 + 0.5, z * 0.5 + 0.5)
+        std::vector<vec2> tc(3 * t.size());
+        for (auto const& tri : t)
+        {
+            vec3 c[3] = { tri.v1, tri.v1 + tri.e1, tri.v1 + tri.e2 };
+            for (int k = 0; k < 3; ++k) tc[3 * tri.prim_id + k] = vec2(c[k].x * 0.5f + 0.5f, c[k].z * 0.5f + 0.5f);
+        }
+        write_file(outdir + "/tex_coords.bin", tc.data(), tc.size() * sizeof(vec2));
+        mask_intersector isect;
+        isect.tex_coords = tc.data();
+        isect.mask = mask.data();
+        isect.w = mw;
+        isect.h = mh;
+        return run_golden(d, t, normals, outdir, W, H, true, isect);
     }
     if (mode == "sah")
     {

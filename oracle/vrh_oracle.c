@@ -423,8 +423,32 @@ static inline prim_hit isect_sphere(v3 ori, v3 dir, const vo_sphere* s)
     return r;
 }
 
+/* the example's mask test on a triangle hit (vrh_oracle.h vo_hit_mask); hr.hit &= mask */
+static inline unsigned mask_texel(float c, int n)
+{
+    float x = (c > 0.0f ? c : 0.0f) * (float)n;
+    return x < (float)n ? (unsigned)x : (unsigned)(n - 1);
+}
+
+static inline int mask_keep(const vo_hit_mask* m, uint32_t prim_id, float u, float v)
+{
+    const float* a = m->tc + 6u * prim_id;       /* 3 x (x, y) per prim_id */
+    /* lerp(a, b, c, u, v), math.h:468-475: s2 = c * v; s3 = b * u; s1 = a * (1 - (u + v)); s1 + s2 + s3 */
+    float w = 1.0f - (u + v);
+    float x = (a[0] * w + a[4] * v) + a[2] * u;
+    float y = (a[1] * w + a[5] * v) + a[3] * u;
+    return m->mask[mask_texel(y, m->h) * (unsigned)m->w + mask_texel(x, m->w)] != 0;
+}
+
 vo_hit vo_intersect(const float ori_[3], const float dir_[3], const vo_node* nodes, const uint32_t* indices,
                     const void* prims, int kind, int any_hit, float max_t, vo_counters* cnt)
+{
+    return vo_intersect_masked(ori_, dir_, nodes, indices, prims, kind, any_hit, max_t, NULL, cnt);
+}
+
+vo_hit vo_intersect_masked(const float ori_[3], const float dir_[3], const vo_node* nodes, const uint32_t* indices,
+                           const void* prims, int kind, int any_hit, float max_t, const vo_hit_mask* mask,
+                           vo_counters* cnt)
 {
     v3 ori = mk(ori_[0], ori_[1], ori_[2]);
     v3 dir = mk(dir_[0], dir_[1], dir_[2]);
@@ -476,6 +500,7 @@ vo_hit vo_intersect(const float ori_[3], const float dir_[3], const vo_node* nod
             prim_hit hr = kind == VO_TRI ? isect_tri(ori, dir, (const vo_tri*)prims + indices[i])
                                          : isect_sphere(ori, dir, (const vo_sphere*)prims + indices[i]);
             ++nprim;
+            if (mask && kind == VO_TRI && hr.hit) hr.hit = mask_keep(mask, hr.prim_id, hr.u, hr.v);
             /* update_if.h:48-56,73-79 is_closer + update_if.h:27-37 + hit_record.h:54-64 */
             int closer = hr.hit && hr.t >= 0.0f && hr.t < res.t && hr.t < max_t;
             if (!closer) continue;
@@ -491,6 +516,13 @@ out:
 
 int vo_intersect_multi(const float ori_[3], const float dir_[3], const vo_node* nodes, const uint32_t* indices,
                        const void* prims, int kind, int n, vo_hit* res, vo_counters* cnt)
+{
+    return vo_intersect_multi_masked(ori_, dir_, nodes, indices, prims, kind, n, res, NULL, cnt);
+}
+
+int vo_intersect_multi_masked(const float ori_[3], const float dir_[3], const vo_node* nodes, const uint32_t* indices,
+                              const void* prims, int kind, int n, vo_hit* res, const vo_hit_mask* mask,
+                              vo_counters* cnt)
 {
     v3 ori = mk(ori_[0], ori_[1], ori_[2]);
     v3 dir = mk(dir_[0], dir_[1], dir_[2]);
@@ -541,6 +573,7 @@ int vo_intersect_multi(const float ori_[3], const float dir_[3], const vo_node* 
             prim_hit hr = kind == VO_TRI ? isect_tri(ori, dir, (const vo_tri*)prims + indices[i])
                                          : isect_sphere(ori, dir, (const vo_sphere*)prims + indices[i]);
             ++nprim;
+            if (mask && kind == VO_TRI && hr.hit) hr.hit = mask_keep(mask, hr.prim_id, hr.u, hr.v);
             int closer = 0;
             for (int k = 0; k < n && !closer; ++k)
                 closer = hr.hit && hr.t >= 0.0f && hr.t < res[k].t && hr.t < FLT_MAX;
@@ -593,7 +626,7 @@ static px_out shade_pixel(const vo_scene* s, const vo_camera* cam, const vo_kern
     v3 ori, dir;
     primary_ray(cam, x, y, &ori, &dir);
     float fo[3] = { ori.x, ori.y, ori.z }, fd[3] = { dir.x, dir.y, dir.z };
-    vo_hit hr = vo_intersect(fo, fd, s->nodes, s->indices, s->prims, s->kind, 0, FLT_MAX, cnt);
+    vo_hit hr = vo_intersect_masked(fo, fd, s->nodes, s->indices, s->prims, s->kind, 0, FLT_MAX, s->hit_mask, cnt);
     if (!hr.hit) return o;
     o.prim_id = hr.prim_id; o.t = hr.t; o.list_index = hr.list_index;
     if (k->mode == VO_MODE_SIMPLE) {
@@ -628,7 +661,7 @@ static px_out shade_pixel(const vo_scene* s, const vo_camera* cam, const vo_kern
         v3 d = normalize(add(add(smul(sx, bu), smul(sy, bv)), smul(sz, n)));
         v3 ao = add(isect_pos, muls(d, k->eps));
         float ao_o[3] = { ao.x, ao.y, ao.z }, ao_d[3] = { d.x, d.y, d.z };
-        vo_hit ar = vo_intersect(ao_o, ao_d, s->nodes, s->indices, s->prims, s->kind, 1, k->radius, cnt);
+        vo_hit ar = vo_intersect_masked(ao_o, ao_d, s->nodes, s->indices, s->prims, s->kind, 1, k->radius, s->hit_mask, cnt);
         o.rays++;
         if (ar.hit) { clr = clr - step; o.occ |= (uint8_t)(1u << smp); }
     }
@@ -733,7 +766,7 @@ static void shade_whitted(const vo_scene* s, const vo_kernel* k, v3 ori, v3 dir,
             v3 so = add(pos, muls(ldir, k->eps));
             float max_t = sqrtf(dot(sub(pos, lpos), sub(pos, lpos)));   /* length(isect_pos - pos) */
             float fo[3] = { so.x, so.y, so.z }, fd[3] = { ldir.x, ldir.y, ldir.z };
-            vo_hit sh = vo_intersect(fo, fd, s->nodes, s->indices, s->prims, s->kind, 1, max_t, cnt);
+            vo_hit sh = vo_intersect_masked(fo, fd, s->nodes, s->indices, s->prims, s->kind, 1, max_t, s->hit_mask, cnt);
             ++*rays;
             /* shaded_clr += select(active, clr, 0) */
             shaded = add(shaded, sh.hit ? mk(0.0f, 0.0f, 0.0f) : plastic_light(m, n, view, pos, L));
@@ -746,7 +779,7 @@ static void shade_whitted(const vo_scene* s, const vo_kernel* k, v3 ori, v3 dir,
         ori = add(pos, muls(rd, k->eps));
         dir = rd;
         float fo[3] = { ori.x, ori.y, ori.z }, fd[3] = { dir.x, dir.y, dir.z };
-        hr = vo_intersect(fo, fd, s->nodes, s->indices, s->prims, s->kind, 0, FLT_MAX, cnt);
+        hr = vo_intersect_masked(fo, fd, s->nodes, s->indices, s->prims, s->kind, 0, FLT_MAX, s->hit_mask, cnt);
         ++*rays;
         thr = thr2;
     }
@@ -791,7 +824,7 @@ uint64_t vo_render_multi(const vo_scene* s, const vo_camera* cam, const vo_kerne
             primary_ray(cam, (unsigned)x, (unsigned)y, &ori, &dir);
             float fo[3] = { ori.x, ori.y, ori.z }, fd[3] = { dir.x, dir.y, dir.z };
             vo_hit hits[VO_MAX_HITS];
-            vo_intersect_multi(fo, fd, s->nodes, s->indices, s->prims, s->kind, n, hits, NULL);
+            vo_intersect_multi_masked(fo, fd, s->nodes, s->indices, s->prims, s->kind, n, hits, s->hit_mask, NULL);
             size_t p = (size_t)y * W + x;
             for (int i = 0; i < n; ++i) {
                 if (mh_prim_id) mh_prim_id[p * n + i] = hits[i].hit ? hits[i].prim_id : 0xFFFFFFFFu;

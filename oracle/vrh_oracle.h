@@ -72,17 +72,30 @@ typedef struct { uint64_t box_tests, prim_tests; } vo_counters;
 vo_hit vo_intersect(const float ori[3], const float dir[3], const vo_node* nodes, const uint32_t* indices,
                     const void* prims, int kind, int any_hit, float max_t, vo_counters* cnt);
 
+/* the intersector example's mask_intersector (examples/intersector/main.cpp:251-330) as data, the
+ * product's vrh_hit_mask: a triangle hit keeps hr.hit iff mask[j * w + i] != 0 at the texel of
+ * tc = lerp(tc[3p], tc[3p+1], tc[3p+2], u, v) (math.h:468-475), i = x < w ? (u32)x : w - 1 with
+ * x = (tc.x > 0 ? tc.x : 0) * (float)w, j likewise */
+typedef struct { const float* tc; const uint8_t* mask; int w, h; } vo_hit_mask;
+vo_hit vo_intersect_masked(const float ori[3], const float dir[3], const vo_node* nodes, const uint32_t* indices,
+                           const void* prims, int kind, int any_hit, float max_t, const vo_hit_mask* mask,
+                           vo_counters* cnt);
+
 /* multi_hit<N> (traverse_linear.inl:333-380 -> intersect<MultiHit, N>, detail/multi_hit.h): the N
  * closest hits sorted by t (insert_sorted, algorithm.h:46-75: ties after the existing ones);
  * boxes and primitives are tested against the N-th kept t.  out[N]; returns the hit count. */
 int vo_intersect_multi(const float ori[3], const float dir[3], const vo_node* nodes, const uint32_t* indices,
                        const void* prims, int kind, int n, vo_hit* out, vo_counters* cnt);
+int vo_intersect_multi_masked(const float ori[3], const float dir[3], const vo_node* nodes, const uint32_t* indices,
+                              const void* prims, int kind, int n, vo_hit* out, const vo_hit_mask* mask,
+                              vo_counters* cnt);
 
 /* ---- a frame, simple_sched order (row-major), over rows [y0, y1) ---- */
 typedef struct {
     const vo_node* nodes; const uint32_t* indices; const void* prims; int kind;
     const vo_vec3* normals;               /* per prim_id (AO; simple kernel, per-face binding) */
     const vo_vec3* vertex_normals;        /* 3 per prim_id (simple kernel, per-vertex binding) */
+    const vo_hit_mask* hit_mask;          /* mask intersector for every ray (NULL: none) */
 } vo_scene;
 typedef struct {
     float eye[3], cam_u[3], cam_v[3], cam_w[3];

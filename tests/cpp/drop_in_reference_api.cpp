@@ -95,7 +95,39 @@ int main(int argc, char** argv)
         std::memcpy(t.data(), t3.data(), 4 * n);
         std::memcpy(occ.data(), occ3.data(), n);
 
-        printf("{\"grid\":%u,\"W\":%u,\"H\":%u,\"rays\":%llu,\"primid_hash\":\"%016llx\",\"t_hash\":\"%016llx\","
+        // mask intersector (optional argv[4] = mask file, argv[5] = its size n): the AO frame with
+        // with_intersector(kernel, hip_hit_mask) over planar (x, z) tex coords of every corner
+        unsigned long long mask_hashes[4] = { 0, 0, 0, 0 };
+        if (argc > 5)
+        {
+            unsigned mn = unsigned(atoi(argv[5]));
+            std::vector<uint8_t> mask(size_t(mn) * mn);
+            FILE* f = fopen(argv[4], "rb");
+            if (!f || fread(mask.data(), 1, mask.size(), f) != mask.size()) { if (f) fclose(f); return 3; }
+            fclose(f);
+            std::vector<vec2> tc(3 * tris.size());
+            for (auto const& tri : tris)
+            {
+                vec3 c[3] = { tri.v1, tri.v1 + tri.e1, tri.v1 + tri.e2 };
+                for (int k = 0; k < 3; ++k) tc[3 * tri.prim_id + k] = vec2(c[k].x * 0.5f + 0.5f, c[k].z * 0.5f + 0.5f);
+            }
+            hip_hit_mask hm(tc, mask.data(), mn, mn);
+            hip_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> mrt;
+            mrt.resize(W, H);
+            auto msp = make_sched_params(pixel_sampler::uniform_type{}, cam, mrt);
+            sched.frame(with_intersector(kern, hm), msp);
+            std::vector<float> mc(4 * n), mt(n);
+            std::vector<uint32_t> mp(n);
+            std::vector<uint8_t> mo(n);
+            mrt.download(mc.data(), mp.data(), mt.data(), mo.data());
+            mask_hashes[0] = fnv1a(mp.data(), n * 4);
+            mask_hashes[1] = fnv1a(mt.data(), n * 4);
+            mask_hashes[2] = fnv1a(mo.data(), n);
+            mask_hashes[3] = fnv1a(mc.data(), n * 16);
+        }
+        printf("{\"mask_primid_hash\":\"%016llx\",\"mask_t_hash\":\"%016llx\",\"mask_occ_hash\":\"%016llx\","
+               "\"mask_color_hash\":\"%016llx\",", mask_hashes[0], mask_hashes[1], mask_hashes[2], mask_hashes[3]);
+        printf("\"grid\":%u,\"W\":%u,\"H\":%u,\"rays\":%llu,\"primid_hash\":\"%016llx\",\"t_hash\":\"%016llx\","
                "\"occ_hash\":\"%016llx\",\"color_hash\":\"%016llx\",\"batch_ok\":%s}\n", grid, W, H, rays,
                (unsigned long long)fnv1a(pid.data(), n * 4), (unsigned long long)fnv1a(t.data(), n * 4),
                (unsigned long long)fnv1a(occ.data(), n), (unsigned long long)fnv1a(color.data(), n * 16),

@@ -7,6 +7,7 @@ Run in the build container (needs /root/reference to build the harness):
     python tests/golden/make_golden.py --multi                          (only the multi-hit cases)
     python tests/golden/make_golden.py --sah                            (only the sah_cost values)
     python tests/golden/make_golden.py --whitted                        (only the whitted cases)
+    python tests/golden/make_golden.py --mask                           (only the mask-intersector cases)
 
 For every case the reference harness renders a full simple_sched<basic_ray<float>> frame
 (primary closest_hit + the Appendix-A AO kernel for triangle scenes) and this script stores:
@@ -69,6 +70,14 @@ WHITTED_CASES = [
     ("whitted_hfstack32x24_face", "hfstack32x24", 160, 90, "face", 10, "0.0001", True),
     ("whitted_hf64_vertex", "hf64", 160, 90, "vertex", 2, "0.01", True),
     ("whitted_hf1M_face", "hf1M", 1920, 1080, "face", 4, "0.001", False),
+]
+
+
+# mask intersector cases (harness "mask" mode): the intersector example's mask_intersector with a
+# heart-shaped byte mask over planar (x, z) texture coordinates: name, scene, W, H, mask size
+MASK_CASES = [
+    ("mask_hf200_320x180", "hf200", 320, 180, 128),
+    ("mask_hf64_160x90", "hf64", 160, 90, 37),
 ]
 
 
@@ -137,6 +146,30 @@ def whitted_cases(out, rng):
             print(case, rec["color_hash"], flush=True)
 
 
+def mask_cases(out):
+    sys.path.insert(0, ROOT)
+    from visionaray_amd import scenes  # noqa: E402  (the heart mask generator)
+    for case, scene, W, H, n in MASK_CASES:
+        mask = scenes.heart_mask(n)
+        with tempfile.TemporaryDirectory() as d:
+            mpath = os.path.join(d, "mask.bin")
+            mask.tofile(mpath)
+            r = subprocess.run([REF, "mask", scene, d, mpath, str(n), str(n), str(W), str(H)], check=True,
+                               capture_output=True, text=True)
+            info = json.loads(r.stdout.strip().splitlines()[-1])
+            pid = np.fromfile(os.path.join(d, "prim_id.bin"), np.uint32)
+            t = np.fromfile(os.path.join(d, "t.bin"), np.float32)
+            occ = np.fromfile(os.path.join(d, "occ.bin"), np.uint8)
+            color = np.fromfile(os.path.join(d, "color.bin"), np.float32).reshape(-1, 4)
+            tc = np.fromfile(os.path.join(d, "tex_coords.bin"), np.float32).reshape(-1, 2)
+            rec = {"scene": scene, "W": W, "H": H, "mask_size": n, "hits": info["hits"], "ao_rays": info["ao_rays"],
+                   "ao_occluded": info["ao_occluded"], "primid_hash": fnv1a(pid), "t_hash": fnv1a(t),
+                   "occ_hash": fnv1a(occ), "color_hash": fnv1a(color), "tex_coords_hash": fnv1a(tc)}
+            np.savez_compressed(os.path.join(HERE, case + ".npz"), prim_id=pid, t=t, occ=occ, color=color, mask=mask)
+            out[case] = rec
+            print(case, rec["hits"], rec["ao_occluded"], flush=True)
+
+
 def sah_cases(out):
     rec = {}
     for scene in SAH_SCENES:
@@ -150,7 +183,7 @@ def sah_cases(out):
 def main():
     if not os.path.exists(REF):
         sys.exit("build the reference harness first: make -C oracle ref")
-    only_shade = any(f in sys.argv for f in ("--shade", "--multi", "--sah", "--whitted"))
+    only_shade = any(f in sys.argv for f in ("--shade", "--multi", "--sah", "--whitted", "--mask"))
     path = os.path.join(HERE, "golden.json")
     out = json.load(open(path)) if only_shade else {}
     rng = np.random.default_rng(12345)
@@ -182,7 +215,9 @@ def main():
                                     occ=occ[pix], color=color[pix])
             out[case] = rec
             print(case, rec["hits"], rec["ao_occluded"], rec["primid_hash"], flush=True)
-    if "--whitted" in sys.argv:
+    if "--mask" in sys.argv:
+        mask_cases(out)
+    elif "--whitted" in sys.argv:
         whitted_cases(out, np.random.default_rng(777))
     elif "--sah" in sys.argv:
         sah_cases(out)
@@ -192,6 +227,7 @@ def main():
         multi_cases(out)
         sah_cases(out)
         whitted_cases(out, np.random.default_rng(777))
+        mask_cases(out)
     with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 

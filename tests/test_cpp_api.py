@@ -60,6 +60,21 @@ def test_reference_api_program_on_hip_backend(golden):
     assert out["batch_ok"], "hip_sched::frames: a frame of the batch differs from its own frame()"
 
 
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(DROPIN), reason="drop-in binary is built in the build container only")
+def test_reference_api_program_with_mask_intersector(golden, tmp_path):
+    """hip_hit_mask + with_intersector on the reference's own triangles and camera reproduce the
+    reference's mask-intersector frame (harness `mask` mode) bit for bit."""
+    import numpy as np
+    g = golden["mask_hf200_320x180"]
+    mask = np.load(os.path.join(ROOT, "tests", "golden", "mask_hf200_320x180.npz"))["mask"]
+    mpath = tmp_path / "mask.bin"
+    mask.tofile(mpath)
+    out = _run(DROPIN, 200, g["W"], g["H"], mpath, mask.shape[0])
+    for k in ("primid_hash", "t_hash", "occ_hash", "color_hash"):
+        assert out["mask_" + k] == g[k], k
+
+
 DROPIN_SHADE = os.path.join(ROOT, "oracle", "_ref", "dropin_simple_kernel")
 
 

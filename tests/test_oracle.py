@@ -172,3 +172,50 @@ def test_oracle_multi_hit_matches_reference(golden, oracle_mod, case):
     assert np.array_equal(out["mh_t"].view(np.uint32), ref["mh_t"].view(np.uint32))
     assert np.array_equal(out["color"].view(np.uint32), ref["color"].view(np.uint32))
     assert O.fnv1a(out["color"]) == g["color_hash"]
+
+
+# ---- mask intersector: the intersector example's mask_intersector -------
+
+MASK_CASES = ["mask_hf200_320x180", "mask_hf64_160x90"]
+
+
+def mask_inputs(g, ref):
+    from visionaray_amd import scenes
+    tc = scenes.planar_tex_coords(scenes.primitives(g["scene"]))
+    return tc, ref["mask"]
+
+
+@pytest.mark.parametrize("case", MASK_CASES)
+def test_oracle_mask_intersector_matches_reference(oracle_mod, golden, case):
+    """Primary closest_hit and AO any_hit through the reference's basic_intersector with the mask
+    test (harness `mask` mode) against the oracle's vo_hit_mask, every pixel, bit for bit."""
+    O = oracle_mod
+    g = golden[case]
+    ref = np.load(os.path.join(HERE, "golden", case + ".npz"))
+    tc, mask = mask_inputs(g, ref)
+    assert O.fnv1a(tc) == g["tex_coords_hash"], "planar tex coords differ from the harness's"
+    sc = O.make_scene(g["scene"])
+    cam = O.scene_camera(g["scene"], g["W"], g["H"])
+    out = O.render(sc, cam, mode=O.VO_MODE_AO, hit_mask=(tc, mask))
+    assert np.array_equal(out["prim_id"], ref["prim_id"])
+    assert np.array_equal(out["t"].view(np.uint32), ref["t"].view(np.uint32))
+    assert np.array_equal(out["occ"], ref["occ"])
+    assert np.array_equal(out["color"].view(np.uint32), ref["color"].view(np.uint32))
+    assert out["rays"] == g["W"] * g["H"] + g["ao_rays"]
+    # the mask really cuts: fewer hits than the unmasked frame of the same scene
+    plain = O.render(sc, cam, mode=O.VO_MODE_PRIMARY)
+    assert g["hits"] < int((plain["prim_id"] != 0xFFFFFFFF).sum())
+
+
+def test_oracle_mask_all_ones_is_identity(oracle_mod):
+    """An all-keep mask leaves every result unchanged (hr.hit &= true)."""
+    O = oracle_mod
+    from visionaray_amd import scenes
+    sc = O.make_scene("hf64")
+    cam = O.scene_camera("hf64", 80, 45)
+    tc = scenes.planar_tex_coords(scenes.primitives("hf64"))
+    a = O.render(sc, cam, mode=O.VO_MODE_AO)
+    b = O.render(sc, cam, mode=O.VO_MODE_AO, hit_mask=(tc, np.ones((3, 5), np.uint8)))
+    for k in ("prim_id", "occ"):
+        assert np.array_equal(a[k], b[k])
+    assert np.array_equal(a["color"].view(np.uint32), b["color"].view(np.uint32))

@@ -2,6 +2,7 @@
 
     python tools/ab_variants.py [scene] [rounds]
 Each variant is also checked bit-exactly (prim_id / occ / colour hashes) against tests/golden.
+VRH_AB_BATCH = frames per launch (default 8, as bench.py); times are per frame.
 """
 import json
 import os
@@ -47,7 +48,8 @@ cam, W, H = scenes.scene_camera(scene)
 basis = cam.basis(W, H)
 ao = prims.dtype == va.TRIANGLE_DTYPE and os.environ.get("VRH_AB_KERNEL", "ao") == "ao"
 kern = va.ao_kernel(dev) if ao else va.closest_hit_kernel(dev)
-rt = va.hip_buffer_rt(ctx, W, H)
+F = int(os.environ.get("VRH_AB_BATCH", "8"))
+rt = va.hip_buffer_rt(ctx, W, H * F)
 say(f"scene {scene} {len(prims)} prims depth {host.max_depth} ao={ao} wide records {dev.info['wide_records']} "
     f"(depth {dev.info['wide_depth']})")
 res = {v["name"]: [] for v in VARIANTS}
@@ -65,14 +67,14 @@ for rnd in range(rounds):
         ctx.set_option("wide_anyhit", v.get("wide_anyhit", 0))
         ctx.set_option("descent_cap", v.get("descent_cap", 0))
         ctx.stats_reset()
-        for _ in range(5):
-            va.render(ctx, dev, rt, basis, kern)
+        for _ in range(3):
+            va.render_batch(ctx, dev, rt, [basis] * F, kern)
         a = ctx.accum_stats()
         st = ctx.last_frame_stats()
-        ms = a["kernel_ms_min"]
-        res[v["name"]].append((a["kernel_ms_total"] / a["timed_frames"], ms, a["rays"] / a["frames"]))
+        ms = a["kernel_ms_min"] / F
+        res[v["name"]].append((a["kernel_ms_total"] / a["timed_frames"] / F, ms, a["rays"] / a["frames"] / F))
         if rnd == 0 and g is not None:
-            out = rt.download()
+            out = {k: x[:W * H] for k, x in rt.download().items()}
             ok = (O.fnv1a(out["prim_id"]) == g["primid_hash"] and O.fnv1a(out["t"]) == g["t_hash"]
                   and (not ao or (O.fnv1a(out["occ"]) == g["occ_hash"] and O.fnv1a(out["color"]) == g["color_hash"])))
             say(f"  {v['name']:24s} grid {st['grid_blocks']} x {st['block_threads']} stack {st['stack_depth']} "

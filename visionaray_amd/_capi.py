@@ -30,7 +30,7 @@ class vrh_kernel_desc(C.Structure):
     _fields_ = [("kind", C.c_uint32), ("samples", C.c_uint32), ("radius", C.c_float), ("eps", C.c_float),
                 ("bg", C.c_float * 4), ("flags", C.c_uint32), ("normal_binding", C.c_uint32),
                 ("ambient", C.c_float * 4), ("shading", C.c_void_p), ("max_hits", C.c_uint32),
-                ("num_bounces", C.c_uint32)]
+                ("num_bounces", C.c_uint32), ("hit_mask", C.c_void_p)]
 
 
 class vrh_plastic(C.Structure):
@@ -115,6 +115,8 @@ SIGNATURES = {
     "vrh_scene_set_vertex_normals": (C.c_int, [_vp, _vp, _u32]),
     "vrh_shading_create": (C.c_int, [_vp, _vp, _u32, _vp, _u32, C.POINTER(_vp)]),
     "vrh_shading_free": (C.c_int, [_vp]),
+    "vrh_hit_mask_create": (C.c_int, [_vp, _vp, _u32, _vp, _u32, _u32, C.POINTER(_vp)]),
+    "vrh_hit_mask_free": (C.c_int, [_vp]),
     "vrh_rt_alloc_multi_hit": (C.c_int, [_vp, _vp, _u32]),
     "vrh_scene_build": (C.c_int, [_vp, _vp, _u32, _u32, _vp, _vp, C.POINTER(_vp)]),
     "vrh_scene_download_bvh": (C.c_int, [_vp, _vp, _vp, C.POINTER(_u32), _vp]),

@@ -404,6 +404,45 @@ def ao_kernel(bvh, samples=8, radius=0.1, eps=1e-3, bg=(0.1, 0.2, 0.3, 1.0), cou
     return _builtin_kernel(bvh, capi.VRH_KERNEL_AO, samples, radius, eps, bg, count_tests)
 
 
+# ---- mask intersector ------------------------------------------------------
+
+class hit_mask:
+    """The intersector example's mask_intersector (examples/intersector/main.cpp:251-330: a
+    basic_intersector whose operator()(ray, tri) clears hr.hit where a mask over the hit's texture
+    coordinate says so) as data: tex_coords (3 x (u, v) per prim_id, float32) and a (H, W) uint8
+    mask; vrh.h vrh_hit_mask_create states the lookup.  Attach with with_hit_mask(kernel, mask)."""
+
+    def __init__(self, ctx, tex_coords, mask):
+        self.ctx = ctx
+        self.tex_coords = np.ascontiguousarray(tex_coords, np.float32).reshape(-1, 2)
+        self.mask = np.ascontiguousarray(mask, np.uint8)
+        if self.mask.ndim != 2:
+            raise ValueError("hit_mask: mask must be (H, W)")
+        h = C.c_void_p()
+        capi.check("vrh_hit_mask_create", ctx.handle, _p(self.tex_coords), len(self.tex_coords), _p(self.mask),
+                   self.mask.shape[1], self.mask.shape[0], C.byref(h))
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            capi.lib().vrh_hit_mask_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def with_hit_mask(kernel, mask):
+    """closest_hit / any_hit with the mask intersector for every ray of `kernel` (the reference's
+    closest_hit(ray, begin, end, intersector) / any_hit(..., intersector), traverse_linear.inl:232-329)."""
+    kernel.desc.hit_mask = mask.handle if mask is not None else None
+    kernel.hit_mask = mask
+    return kernel
+
+
 # ---- shading (SURVEY.md §8f rank 1) ----------------------------------------------------------------
 
 PLASTIC_DTYPE = np.dtype([("ca", "<f4", 3), ("ka", "<f4"), ("cd", "<f4", 3), ("kd", "<f4"), ("cs", "<f4", 3),

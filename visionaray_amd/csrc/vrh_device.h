@@ -145,6 +145,31 @@ __device__ __forceinline__ bool isect_tri(const ray_t& r, float4 a, float4 b, fl
     return isect_tri(r, a, b, c, t, u, v);
 }
 
+// Mask intersector (vrh_hit_mask_create): the intersector example's mask_intersector
+// (examples/intersector/main.cpp:251-330) as data.  tc = lerp(tc0, tc1, tc2, u, v) in the order of
+// math.h:468-475 (s2 = c v, s3 = b u, s1 = a (1 - (u + v)), (s1 + s2) + s3), then a nearest texel.
+struct hit_mask_params
+{
+    const float2* tc;         // 3 per prim_id
+    const uint8_t* mask;      // w x h, row-major; null = no mask
+    uint32_t w, h;
+};
+
+__device__ __forceinline__ uint32_t mask_texel(float c, uint32_t n)
+{
+    const float x = (c > 0.0f ? c : 0.0f) * (float)n;      // NaN -> 0
+    return x < (float)n ? (uint32_t)x : n - 1u;
+}
+
+__device__ __forceinline__ bool mask_keep(const hit_mask_params& m, uint32_t prim_id, float u, float v)
+{
+    const float2 a = m.tc[3u * prim_id], b = m.tc[3u * prim_id + 1u], c = m.tc[3u * prim_id + 2u];
+    const float w = 1.0f - (u + v);
+    const float x = (a.x * w + c.x * v) + b.x * u;
+    const float y = (a.y * w + c.y * v) + b.y * u;
+    return m.mask[mask_texel(y, m.h) * m.w + mask_texel(x, m.w)] != 0;
+}
+
 // extra closest-hit state the shading kernels need: barycentrics (hit_record u, v) and the
 // leaf-order index of the hit primitive (hit_record_bvh::primitive_list_index)
 struct hit_extra { float u, v; uint32_t li; };
@@ -247,7 +272,8 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
                                         const ray_t& r, float max_t, bool any, lds_stack& st,
                                         float& best_t, uint32_t& best_prim, test_counts& cnt,
                                         uint32_t& steps, uint32_t step_limit, uint32_t& resume, uint32_t cap,
-                                        hit_extra* hx = nullptr, const MultiList* mh = nullptr)
+                                        hit_extra* hx = nullptr, const MultiList* mh = nullptr,
+                                        const hit_mask_params* hm = nullptr)
 {
     // the tree was validated at upload (no cycles, links in range), so the descent terminates;
     // the guard below only bounds the number of outer iterations per ray
@@ -340,7 +366,12 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
             flags = __float_as_uint(b.z);
         }
         if (COUNT) { cnt.prim += 1; cnt.it_prim += 1; }
-        if (h & (t >= 0.0f) & (t < best_t) & (t < max_t))      // update_if.h:48-56, 73-79
+        bool closer = h & (t >= 0.0f) & (t < best_t) & (t < max_t);     // update_if.h:48-56, 73-79
+        // mask intersector: hr.hit &= mask (a pure test, so applying it only where the hit would be
+        // taken equals masking every primitive test)
+        if constexpr (KIND == KIND_TRI)
+            if (closer && hm != nullptr && hm->mask != nullptr) closer = mask_keep(*hm, pid, hu, hv);
+        if (closer)
         {
             if constexpr (!std::is_void<MultiList>::value)
             {

@@ -64,6 +64,7 @@ struct render_params
     // one byte per ray into `aobits` ([record][sample]); the resolve pass folds them into colour
     float4* hitrec;
     uint8_t* aobits;
+    dev::hit_mask_params hmask;   // mask intersector (vrh_hit_mask), hmask.mask == null: none
 };
 
 constexpr int COUNTERS_FRAME = 208;     // u64 words reset before every frame

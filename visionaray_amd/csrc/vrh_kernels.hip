@@ -179,6 +179,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     uint32_t* ao_area = smem + P.stack_cap * block + wave * AO_WAVE_WORDS;
     test_counts cnt = {};
     uint64_t rays_total = 0, hits_total = 0;
+    const hit_mask_params hml = P.hmask;          // a local copy: &P would spill the kernel arguments
+    const hit_mask_params* hm = &hml;             // ray_step tests hm->mask
 
     // lane state: the ray it is stepping
     constexpr uint32_t IDLE = 0, PRIMARY = 1, AORAY = 2;
@@ -259,8 +261,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 const float mt = EPI == 3 ? max_t : FMAX;
                 const bool an = EPI == 3 ? any : false;
                 int rc = (P.fast_ok && __ballot(!finite) == 0ull)
-                    ? ray_step<KIND, COUNT, true, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, &hx, &mh)
-                    : ray_step<KIND, COUNT, false, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, &hx, &mh);
+                    ? ray_step<KIND, COUNT, true, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, &hx, &mh, hm)
+                    : ray_step<KIND, COUNT, false, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, &hx, &mh, hm);
                 if constexpr (EPI == 3)
                 {
                     if (rc != 0)
@@ -501,8 +503,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             if (busy)
             {
                 rc = (P.fast_ok && __ballot(!finite) == 0ull)
-                    ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap)
-                    : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap);
+                    ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, nullptr, static_cast<const void*>(nullptr), hm)
+                    : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, nullptr, static_cast<const void*>(nullptr), hm);
             }
             if (COUNT) count_wave(cnt, busy);
             // 5. finished AO rays: record occlusion, retire from their tile's in-flight count
@@ -601,6 +603,8 @@ __global__ __launch_bounds__(256, OCC) void ao_pass_kernel(render_params P)
     st.end = tid + P.stack_cap * block;
     test_counts cnt = {};
     uint64_t rays_total = 0;
+    const hit_mask_params hml = P.hmask;          // a local copy: &P would spill the kernel arguments
+    const hit_mask_params* hm = &hml;             // ray_step tests hm->mask
 
     const uint32_t S = P.samples;
     const uint32_t nq = P.xcd_queues ? 8u : 1u;
@@ -656,8 +660,8 @@ __global__ __launch_bounds__(256, OCC) void ao_pass_kernel(render_params P)
         if (busy)
         {
             rc = (P.fast_ok && __ballot(!finite) == 0ull)
-                ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap)
-                : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap);
+                ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, nullptr, static_cast<const void*>(nullptr), hm)
+                : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, nullptr, static_cast<const void*>(nullptr), hm);
         }
         if (COUNT) count_wave(cnt, busy);
         if (busy && rc != 0)

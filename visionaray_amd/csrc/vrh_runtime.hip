@@ -87,6 +87,14 @@ struct vrh_shading
     uint32_t num_materials = 0, num_lights = 0;
 };
 
+struct vrh_hit_mask
+{
+    vrh_ctx* ctx = nullptr;
+    float2* tc = nullptr;         // 3 per prim_id
+    uint8_t* mask = nullptr;
+    uint32_t num_tc = 0, w = 0, h = 0;
+};
+
 struct vrh_rt
 {
     vrh_ctx* ctx = nullptr;
@@ -526,6 +534,47 @@ VRH_API int vrh_shading_create(vrh_ctx* ctx, const vrh_plastic* materials, uint3
     return VRH_OK;
 }
 
+VRH_API int vrh_hit_mask_create(vrh_ctx* ctx, const float* tex_coords, uint32_t num_tex_coords,
+                                const uint8_t* mask, uint32_t mask_width, uint32_t mask_height, vrh_hit_mask** out)
+{
+    VRH_CHECK(ctx && out && tex_coords && mask, "vrh_hit_mask_create: null argument");
+    VRH_CHECK(num_tex_coords >= 3 && num_tex_coords % 3 == 0, "vrh_hit_mask_create: 3 tex coords per triangle");
+    VRH_CHECK(mask_width > 0 && mask_height > 0 && uint64_t(mask_width) * mask_height < (1ull << 32),
+              "vrh_hit_mask_create: bad mask size");
+    *out = nullptr;
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    auto* m = new (std::nothrow) vrh_hit_mask;
+    if (!m) { set_error("host allocation failed"); return VRH_ERR_OOM; }
+    m->ctx = ctx;
+    m->num_tc = num_tex_coords;
+    m->w = mask_width;
+    m->h = mask_height;
+    const size_t mb = size_t(mask_width) * mask_height;
+    hipError_t e = hipMalloc(&m->tc, sizeof(float2) * num_tex_coords);
+    if (e == hipSuccess) e = hipMemcpy(m->tc, tex_coords, sizeof(float2) * num_tex_coords, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&m->mask, mb);
+    if (e == hipSuccess) e = hipMemcpy(m->mask, mask, mb, hipMemcpyHostToDevice);
+    if (e != hipSuccess)
+    {
+        set_error(std::string("vrh_hit_mask_create: ") + hipGetErrorString(e));
+        vrh_hit_mask_free(m);
+        return e == hipErrorOutOfMemory ? VRH_ERR_OOM : VRH_ERR_HIP;
+    }
+    *out = m;
+    return VRH_OK;
+}
+
+VRH_API int vrh_hit_mask_free(vrh_hit_mask* m)
+{
+    if (!m) return VRH_OK;
+    if (m->ctx) (void)hipSetDevice(m->ctx->device);
+    if (m->tc) (void)hipFree(m->tc);
+    if (m->mask) (void)hipFree(m->mask);
+    delete m;
+    return VRH_OK;
+}
+
 VRH_API int vrh_shading_free(vrh_shading* sh)
 {
     if (!sh) return VRH_OK;
@@ -683,6 +732,13 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
         VRH_CHECK(sc->info.prim_kind != VRH_PRIM_TRI64 || sc->normals, "vrh_render: AO on triangles needs face normals");
         VRH_CHECK(sc->normals, "vrh_render: AO needs normals");
     }
+    const vrh_hit_mask* hmask = k->hit_mask;
+    if (hmask)
+    {
+        VRH_CHECK(hmask->ctx == ctx, "vrh_render: hit mask of another context");
+        VRH_CHECK(sc->info.prim_kind != VRH_PRIM_TRI64 || uint64_t(hmask->num_tc) >= 3ull * (uint64_t(sc->info.max_prim_id) + 1),
+                  "vrh_render: hit mask has fewer than 3 tex coords per prim_id");
+    }
     vrh_shard whole{ 0, 1, 0, 0 };
     const vrh_shard& sh = shard ? *shard : whole;
     VRH_CHECK(sh.count >= 1 && sh.index < sh.count, "vrh_render: bad shard");
@@ -718,6 +774,7 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     if (ctx->opt_sched == 0) lc.sched = (lc.kind == 1 && !ao) ? 1 : 0;
     else lc.sched = ctx->opt_sched == 4 ? 1 : ctx->opt_sched == 5 ? 2 : (ctx->opt_sched == 6 && ao) ? 3 : 0;
     if (shade) lc.sched = 0;   // the shading epilogue lives in the step loop
+    if (hmask) lc.sched = 0;   // the mask test lives in the step loop's leaf test
     // two-pass AO: pass 1 is the step loop's primary stream with the hit-record epilogue
     launch_config lc1 = lc;
     if (lc.sched == 3) { lc1.ao = false; lc1.epi = 4; lc1.sched = 0; }
@@ -768,6 +825,8 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
         std::memcpy(p.shade.ambient, k->ambient, 16);
     }
     p.num_bounces = whitted ? k->num_bounces : 0u;
+    if (hmask && sc->info.prim_kind == VRH_PRIM_TRI64)
+        p.hmask = dev::hit_mask_params{ hmask->tc, hmask->mask, hmask->w, hmask->h };
     if (multi)
     {
         p.max_hits = k->max_hits;
