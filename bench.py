@@ -255,8 +255,11 @@ def main():
 
     for b in batches(args.warmup):
         run_batch(b)
-    for b in set(batches(args.steps)):    # allocate the timed batches' buffers outside the timing
-        buffers(b)
+    # every buffer the timed batches use (each batch size, each in-flight slot) is written once
+    # before timing, whatever --warmup is
+    for b in sorted(set(batches(args.steps))):
+        for _ in range(nslots if world > 1 else 1):
+            run_batch(b)
     drain()
     barrier()
     ctx.stats_reset()

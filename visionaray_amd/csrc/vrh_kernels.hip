@@ -28,7 +28,8 @@ constexpr uint32_t NONE = 0xFFFFFFFFu;
 // being traced).  Hit records (isect position, face normal) are read only when an AO ray is handed
 // out, so one set serves C; occlusion masks and the slot -> pixel map live until a tile finishes,
 // so there are two of each, indexed by the tile's buffer parity.
-constexpr int AO_REC_WORDS = 6;                         // pos xyz, normal xyz
+constexpr int AO_REC_WORDS = 4;                         // pos xyz, prim id (its normal is re-read per AO ray:
+                                                        // 512 B less LDS per wave = 24 instead of 22 waves/CU)
 constexpr int AO_MASKS = 64 * AO_REC_WORDS;             // u32 masks[2][64]
 constexpr int AO_SLOT_PX = AO_MASKS + 2 * 64;           // u8 slot_px[2][64]: pixel (lane) of a hit slot
 constexpr int AO_WAVE_WORDS = AO_SLOT_PX + 2 * 64 / 4;
@@ -145,7 +146,8 @@ __device__ __forceinline__ ray_t ao_ray(const render_params& P, const float* rec
 {
     const float* sr = recs + slot * AO_REC_WORDS;
     f3 pos = mk3(sr[0], sr[1], sr[2]);
-    f3 n = mk3(sr[3], sr[4], sr[5]);
+    const float4 nn = P.normals[__float_as_uint(sr[3])];              // get_normal.h:26-37
+    f3 n = mk3(nn.x, nn.y, nn.z);
     // vector3.inl:357-367 make_orthonormal_basis(u, v, w = n)
     f3 bv = fabsf(n.x) > fabsf(n.y) ? normalize(mk3(-n.z, 0.0f, n.x)) : normalize(mk3(0.0f, n.z, -n.y));
     f3 bu = cross(bv, n);
@@ -530,10 +532,9 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     {
                         const uint32_t slot = pubC + lane_rank(hfin);
                         const f3 pos = r.ori + r.dir * best_t;                   // ao/main.cpp:202
-                        const float4 nn = P.normals[best_prim];                  // get_normal.h:26-37
                         float* rec = recs + slot * AO_REC_WORDS;
                         rec[0] = pos.x; rec[1] = pos.y; rec[2] = pos.z;
-                        rec[3] = nn.x; rec[4] = nn.y; rec[5] = nn.z;
+                        rec[3] = __uint_as_float(best_prim);
                         masks[parC * 64u + slot] = 0u;
                         slot_px[parC * 64u + slot] = (uint8_t)tag;
                     }
@@ -801,10 +802,9 @@ __global__ __launch_bounds__(256, OCC) void render_item_kernel(render_params P)
                     {
                         const uint32_t slot = pubC + lane_rank(hfin);
                         const f3 pos = r.ori + r.dir * best_t;                   // ao/main.cpp:202
-                        const float4 nn = P.normals[best_prim];                  // get_normal.h:26-37
                         float* rec = recs + slot * AO_REC_WORDS;
                         rec[0] = pos.x; rec[1] = pos.y; rec[2] = pos.z;
-                        rec[3] = nn.x; rec[4] = nn.y; rec[5] = nn.z;
+                        rec[3] = __uint_as_float(best_prim);
                         masks[parC * 64u + slot] = 0u;
                         slot_px[parC * 64u + slot] = (uint8_t)tag;
                     }
