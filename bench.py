@@ -324,6 +324,21 @@ def main():
                     traffic = pm.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        # what actually limits the kernel (PMC, tools/profile_mem.sh): busy fractions of the
+        # vector-memory address (TA) and data (TD) units, when measured for this configuration
+        limiter = None
+        pmm = os.path.join(ROOT, "profiles", "pmc_mem.json")
+        if os.path.exists(pmm) and world == 1:
+            try:
+                with open(pmm) as f:
+                    pm = json.load(f)
+                if pm.get("scene") == args.scene and pm.get("kernel") == kernel and pm.get("frames_per_launch") == F:
+                    limiter = {"unit": "vector-memory pipeline (L1 / TA address / TD data)",
+                               "td_busy": round(pm["td_busy_frac"], 3), "ta_busy": round(pm["ta_busy_frac"], 3),
+                               "l1_hit": round(1.0 - pm["l1_to_l2_reads_per_access"], 3),
+                               "source": "profiles/pmc_mem.json (rocprofv3 --pmc, same workload)"}
+            except Exception:
+                limiter = None
         line = {
             "metric": "Mrays/s (primary + 8-sample AO)" if kernel == "ao" else "Mrays/s (primary)",
             "value": round(mrays, 3),
@@ -350,6 +365,7 @@ def main():
                 "frames_per_launch": F, "kernel_ms_per_frame": round(float(local_vals[2]) / args.steps, 4),
                 "bytes_per_ray": round(bytes_per_ray, 1), "box_tests_per_ray": round(n_box / n_rays, 3),
                 "prim_tests_per_ray": round(n_prim / n_rays, 3),
+                "measured_limiter": limiter,
             },
             "cpu_baseline": cpu,
             "host_build_s": round(build_s, 3),

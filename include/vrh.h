@@ -155,6 +155,7 @@ typedef struct {
      * loop, lanes busy summed over them, and wave-level iterations of the node-descent and leaf
      * loops (lane-level: box_tests / 2 and prim_tests)                                          */
     uint64_t wave_steps, busy_lane_steps, wave_box_iters, wave_prim_iters;
+    uint64_t wave_box_uniform_iters;  /* of wave_box_iters: those whose active lanes all fetch ONE node */
 } vrh_frame_stats;
 
 typedef struct {
@@ -212,8 +213,13 @@ enum vrh_option {
     VRH_OPT_WIDE_ANYHIT = 10,    /* 4-wide node records for any-hit (AO) rays (step loop): 1 = on
                                     when the BVH passes the containment check, 2 = off (auto: off,
                                     measured 6 % slower on hf1M AO than the binary records)      */
-    VRH_OPT_DESCENT_CAP = 11     /* step loop: inner visits per step before a lane's descent is
+    VRH_OPT_DESCENT_CAP = 11,    /* step loop: inner visits per step before a lane's descent is
                                     resumed in the next step (1..1024; auto: unlimited)          */
+    VRH_OPT_POP_ON_MISS = 12,    /* step loop: a descent that misses both children pops its stack
+                                    and keeps descending in the same step: 1 = on, 2 = off (auto: off) */
+    VRH_OPT_COOP_FETCH = 13      /* step loop: each quad of lanes fetches its four pair records
+                                    together (one coalesced 64-B request per record) and transposes
+                                    them with DPP: 1 = on, 2 = off (auto: off)                    */
 };
 VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value);
 

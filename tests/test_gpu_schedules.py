@@ -29,8 +29,14 @@ VARIANTS = {
     "two_pass": {"ao_schedule": 6},
     "two_pass_wide_refill1": {"ao_schedule": 6, "wide_anyhit": 1, "refill_min": 1},
     "two_pass_global_queue": {"ao_schedule": 6, "xcd_queues": 2},
+    "step_pop_on_miss": {"ao_schedule": 3, "pop_on_miss": 1},
+    "step_pop_cap2_wide": {"ao_schedule": 3, "pop_on_miss": 1, "descent_cap": 2, "wide_anyhit": 1},
+    "coop": {"ao_schedule": 3, "coop_fetch": 1},
+    "coop_exact_pop_cap3": {"ao_schedule": 3, "coop_fetch": 1, "exact_minmax": 1, "pop_on_miss": 1, "descent_cap": 3},
+    "coop_two_pass": {"ao_schedule": 6, "coop_fetch": 1},
 }
-OPTIONS = ("ao_schedule", "refill_min", "vote_leaf", "wide_anyhit", "exact_minmax", "descent_cap", "xcd_queues")
+OPTIONS = ("ao_schedule", "refill_min", "vote_leaf", "wide_anyhit", "exact_minmax", "descent_cap", "xcd_queues",
+           "pop_on_miss", "coop_fetch")
 
 
 @pytest.fixture(params=sorted(VARIANTS))

@@ -66,6 +66,8 @@ for rnd in range(rounds):
         ctx.set_option("vote_leaf", v.get("vote_leaf", 0))
         ctx.set_option("wide_anyhit", v.get("wide_anyhit", 0))
         ctx.set_option("descent_cap", v.get("descent_cap", 0))
+        ctx.set_option("pop_on_miss", v.get("pop_on_miss", 0))
+        ctx.set_option("coop_fetch", v.get("coop_fetch", 0))
         ctx.stats_reset()
         for _ in range(3):
             va.render_batch(ctx, dev, rt, [basis] * F, kern)

@@ -1,0 +1,50 @@
+"""Summarise tools/profile_mem.sh passes (vector-memory path) into profiles/<name>.json: busy
+fractions of the TA (address) and TD (data) units, L1 accesses per wave-level load, L1 -> L2 miss
+rate and L2 read latency, per launch of the traversal kernel.
+
+    python tools/pmc_mem_summary.py gpurun_out/pmc_mem profiles/pmc_mem.json [scene kernel frames-per-launch]
+"""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def main():
+    d, out = sys.argv[1], sys.argv[2]
+    scene = sys.argv[3] if len(sys.argv) > 3 else "hf1M"
+    kernel = sys.argv[4] if len(sys.argv) > 4 else "ao"
+    fpl = int(sys.argv[5]) if len(sys.argv) > 5 else 8
+    agg = defaultdict(list)
+    for name in sorted(os.listdir(d)):
+        p = os.path.join(d, name, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        for r in csv.DictReader(open(p)):
+            k = r["Kernel_Name"]
+            if "render_unified_kernel" not in k or "true, true" in k:    # the traversal kernel, not the counting pass
+                continue
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    c = {k: sum(v) / len(v) for k, v in agg.items()}
+    cus = 256
+    cycles = c["GRBM_GUI_ACTIVE"] / 8            # GRBM_GUI_ACTIVE is summed over the 8 XCDs
+    res = {
+        "scene": scene, "kernel": kernel, "gpus": 1, "frames_per_launch": fpl,
+        "counters_per_dispatch": c,
+        "kernel_cycles": cycles,
+        "ta_busy_frac": c["TA_TA_BUSY_sum"] / (cus * cycles),
+        "td_busy_frac": c["TD_TD_BUSY_sum"] / (cus * cycles),
+        "l1_accesses_per_vmem_instr": c["TCP_TOTAL_CACHE_ACCESSES_sum"] / c["SQ_INSTS_VMEM_RD"],
+        "l1_to_l2_reads_per_access": c["TCP_TCC_READ_REQ_sum"] / c["TCP_TOTAL_CACHE_ACCESSES_sum"],
+        "l2_read_latency_cycles": c["TCP_TCC_READ_REQ_LATENCY_sum"] / c["TCP_TCC_READ_REQ_sum"],
+        "note": "TA/TD busy = fraction of kernel cycles the vector-memory address / data units of the 256 CUs "
+                "are busy; the traversal kernel's limiter when TD is near 1",
+    }
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1, sort_keys=True)
+    print(json.dumps({k: v for k, v in res.items() if k != "counters_per_dispatch"}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -3,12 +3,12 @@
 # SQ VMEM levels) over tools/frame_driver.py; one counter group per pass, no tracing domains.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-SCENE=${SCENE:-hf1M}; FRAMES=${FRAMES:-10}; KIND=${KIND:-ao}; OUTD=${OUTD:-gpurun_out/pmc_mem}
+SCENE=${SCENE:-hf1M}; FRAMES=${FRAMES:-4}; KIND=${KIND:-ao}; BATCH=${BATCH:-8}; OUTD=${OUTD:-gpurun_out/pmc_mem}
 mkdir -p $OUTD
 run() {  # name, counters...
   local name=$1; shift
   echo "== pass $name: $*"
-  timeout -k 10 120 rocprofv3 --pmc "$@" --output-format csv -d $OUTD/$name -o run -- python3 tools/frame_driver.py $SCENE $FRAMES $KIND > $OUTD/$name.log 2>&1
+  timeout -k 10 120 rocprofv3 --pmc "$@" --output-format csv -d $OUTD/$name -o run -- python3 tools/frame_driver.py $SCENE $FRAMES $KIND $BATCH > $OUTD/$name.log 2>&1
   local rc=$?; tail -2 $OUTD/$name.log; echo "rc=$rc"
   case $rc in 124|134|137|139) exit $rc;; esac
 }

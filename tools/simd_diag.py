@@ -43,4 +43,5 @@ for name in sys.argv[1:] or ["hf1M", "sph1M"]:
             f"| wave steps {ws} busy-lane util {s['busy_lane_steps'] / (64 * ws):.3f} "
             f"descent util {s['box_tests'] / 2 / max(64 * s['wave_box_iters'], 1):.3f} "
             f"leaf util {s['prim_tests'] / max(64 * s['wave_prim_iters'], 1):.3f} "
-            f"| per wave step: descent iters {s['wave_box_iters'] / ws:.2f} leaf iters {s['wave_prim_iters'] / ws:.2f}")
+            f"| per wave step: descent iters {s['wave_box_iters'] / ws:.2f} leaf iters {s['wave_prim_iters'] / ws:.2f} "
+            f"| one-node (uniform) descent iters {s['wave_box_uniform_iters'] / max(s['wave_box_iters'], 1):.3f}")

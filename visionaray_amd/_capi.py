@@ -48,7 +48,7 @@ VRH_BAND_ROWS = 8
 VRH_MAX_BATCH = 8
 VRH_OPT_BLOCK_THREADS, VRH_OPT_STACK_CAP, VRH_OPT_AO_SCHEDULE, VRH_OPT_BLOCKS_PER_CU = 1, 2, 3, 4
 VRH_OPT_WAVES_PER_SIMD, VRH_OPT_EXACT_MINMAX, VRH_OPT_XCD_QUEUES, VRH_OPT_REFILL_MIN, VRH_OPT_VOTE_LEAF = 5, 6, 7, 8, 9
-VRH_OPT_WIDE_ANYHIT, VRH_OPT_DESCENT_CAP = 10, 11
+VRH_OPT_WIDE_ANYHIT, VRH_OPT_DESCENT_CAP, VRH_OPT_POP_ON_MISS, VRH_OPT_COOP_FETCH = 10, 11, 12, 13
 VRH_MAX_TIMED_FRAMES = 1024
 
 
@@ -67,7 +67,7 @@ class vrh_frame_stats(C.Structure):
                 ("prim_tests", C.c_uint64), ("launches", C.c_uint32),
                 ("grid_blocks", C.c_uint32), ("block_threads", C.c_uint32), ("stack_depth", C.c_uint32),
                 ("wave_steps", C.c_uint64), ("busy_lane_steps", C.c_uint64), ("wave_box_iters", C.c_uint64),
-                ("wave_prim_iters", C.c_uint64)]
+                ("wave_prim_iters", C.c_uint64), ("wave_box_uniform_iters", C.c_uint64)]
 
 
 class vrh_scene_info(C.Structure):

@@ -256,15 +256,21 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             }
             const bool busy = mode != IDLE;
             bool publish = false;                  // EPI 4: this lane's primary hit becomes a record
+            using ML = typename std::conditional<EPI == 2, mh_list, void>::type;
+            constexpr bool UV = EPI == 1 || EPI == 3;
+            const float mt = EPI == 3 ? max_t : FMAX;
+            const bool an = EPI == 3 ? any : false;
+            // cooperative pair fetch: every lane takes part (quad exchanges), idle lanes included
+            int rc_coop = 0;
+            if (P.coop)
+                rc_coop = (P.fast_ok && __ballot(busy && !finite) == 0ull)
+                    ? ray_step_coop<KIND, COUNT, true, UV, ML>(busy, P.pairs, P.prims, P.root, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, &hx, &mh, hm)
+                    : ray_step_coop<KIND, COUNT, false, UV, ML>(busy, P.pairs, P.prims, P.root, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, &hx, &mh, hm);
             if (mode != IDLE)
             {
-                using ML = typename std::conditional<EPI == 2, mh_list, void>::type;
-                constexpr bool UV = EPI == 1 || EPI == 3;
-                const float mt = EPI == 3 ? max_t : FMAX;
-                const bool an = EPI == 3 ? any : false;
-                int rc = (P.fast_ok && __ballot(!finite) == 0ull)
-                    ? ray_step<KIND, COUNT, true, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, &hx, &mh, hm)
-                    : ray_step<KIND, COUNT, false, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, &hx, &mh, hm);
+                int rc = P.coop ? rc_coop : (P.fast_ok && __ballot(!finite) == 0ull)
+                    ? ray_step<KIND, COUNT, true, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, &hx, &mh, hm)
+                    : ray_step<KIND, COUNT, false, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, &hx, &mh, hm);
                 if constexpr (EPI == 3)
                 {
                     if (rc != 0)
@@ -502,11 +508,18 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             }
             // 4. one traversal step for every busy lane (same code for both ray kinds)
             int rc = 0;
-            if (busy)
+            if (P.coop)
+            {
+                // cooperative pair fetch: every lane takes part (quad exchanges), idle lanes included
+                rc = (P.fast_ok && __ballot(busy && !finite) == 0ull)
+                    ? ray_step_coop<KIND, COUNT, true>(busy, P.pairs, P.prims, P.root, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, nullptr, static_cast<const void*>(nullptr), hm)
+                    : ray_step_coop<KIND, COUNT, false>(busy, P.pairs, P.prims, P.root, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, nullptr, static_cast<const void*>(nullptr), hm);
+            }
+            else if (busy)
             {
                 rc = (P.fast_ok && __ballot(!finite) == 0ull)
-                    ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, nullptr, static_cast<const void*>(nullptr), hm)
-                    : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, nullptr, static_cast<const void*>(nullptr), hm);
+                    ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, nullptr, static_cast<const void*>(nullptr), hm)
+                    : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, nullptr, static_cast<const void*>(nullptr), hm);
             }
             if (COUNT) count_wave(cnt, busy);
             // 5. finished AO rays: record occlusion, retire from their tile's in-flight count
@@ -555,12 +568,12 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     }
 
     // ---- per-wave totals: one atomic set per wave --------------------------------------------
-    unsigned long long rr = rays_total, hh = hits_total, b = cnt.box, q = cnt.prim;
+    unsigned long long rr = rays_total, hh = hits_total, b = cnt.box, q = cnt.prim, uni_sum = cnt.w_uni;
     for (int off = 32; off > 0; off >>= 1)
     {
         rr += __shfl_down(rr, off);
         hh += __shfl_down(hh, off);
-        if (COUNT) { b += __shfl_down(b, off); q += __shfl_down(q, off); }
+        if (COUNT) { b += __shfl_down(b, off); q += __shfl_down(q, off); uni_sum += __shfl_down(uni_sum, off); }
     }
     if (__ballot(cnt.aborted) != 0ull && lane == 0) atomicOr(P.counters + 5, 1ull);
     if (lane == 0)
@@ -577,6 +590,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             atomicAdd(P.counters + 7, (unsigned long long)cnt.w_busy);
             atomicAdd(P.counters + 9, (unsigned long long)cnt.w_box);
             atomicAdd(P.counters + 10, (unsigned long long)cnt.w_prim);
+            atomicAdd(P.counters + 11, (unsigned long long)uni_sum);
         }
     }
 }
@@ -658,11 +672,17 @@ __global__ __launch_bounds__(256, OCC) void ao_pass_kernel(render_params P)
         }
         if (__ballot(busy) == 0ull) break;        // every list exhausted, no ray in flight
         int rc = 0;
-        if (busy)
+        if (P.coop)
+        {
+            rc = (P.fast_ok && __ballot(busy && !finite) == 0ull)
+                ? ray_step_coop<KIND, COUNT, true>(busy, P.pairs, P.prims, P.root, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, nullptr, static_cast<const void*>(nullptr), hm)
+                : ray_step_coop<KIND, COUNT, false>(busy, P.pairs, P.prims, P.root, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, nullptr, static_cast<const void*>(nullptr), hm);
+        }
+        else if (busy)
         {
             rc = (P.fast_ok && __ballot(!finite) == 0ull)
-                ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, nullptr, static_cast<const void*>(nullptr), hm)
-                : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, nullptr, static_cast<const void*>(nullptr), hm);
+                ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, nullptr, static_cast<const void*>(nullptr), hm)
+                : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, nullptr, static_cast<const void*>(nullptr), hm);
         }
         if (COUNT) count_wave(cnt, busy);
         if (busy && rc != 0)
@@ -672,11 +692,11 @@ __global__ __launch_bounds__(256, OCC) void ao_pass_kernel(render_params P)
         }
     }
 
-    unsigned long long rr = rays_total, b = cnt.box, pq = cnt.prim;
+    unsigned long long rr = rays_total, b = cnt.box, pq = cnt.prim, uni_sum = cnt.w_uni;
     for (int off = 32; off > 0; off >>= 1)
     {
         rr += __shfl_down(rr, off);
-        if (COUNT) { b += __shfl_down(b, off); pq += __shfl_down(pq, off); }
+        if (COUNT) { b += __shfl_down(b, off); pq += __shfl_down(pq, off); uni_sum += __shfl_down(uni_sum, off); }
     }
     if (__ballot(cnt.aborted) != 0ull && lane == 0) atomicOr(P.counters + 5, 1ull);
     if (lane == 0)
@@ -691,6 +711,7 @@ __global__ __launch_bounds__(256, OCC) void ao_pass_kernel(render_params P)
             atomicAdd(P.counters + 7, (unsigned long long)cnt.w_busy);
             atomicAdd(P.counters + 9, (unsigned long long)cnt.w_box);
             atomicAdd(P.counters + 10, (unsigned long long)cnt.w_prim);
+            atomicAdd(P.counters + 11, (unsigned long long)uni_sum);
         }
     }
 }
@@ -949,12 +970,12 @@ __global__ __launch_bounds__(256, OCC) void render_item_kernel(render_params P)
         if (COUNT) count_wave(cnt, my_busy);
     }
 
-    unsigned long long rr = rays_total, hh = hits_total, b = cnt.box, q = cnt.prim;
+    unsigned long long rr = rays_total, hh = hits_total, b = cnt.box, q = cnt.prim, uni_sum = cnt.w_uni;
     for (int off = 32; off > 0; off >>= 1)
     {
         rr += __shfl_down(rr, off);
         hh += __shfl_down(hh, off);
-        if (COUNT) { b += __shfl_down(b, off); q += __shfl_down(q, off); }
+        if (COUNT) { b += __shfl_down(b, off); q += __shfl_down(q, off); uni_sum += __shfl_down(uni_sum, off); }
     }
     if (__ballot(cnt.aborted) != 0ull && lane == 0) atomicOr(P.counters + 5, 1ull);
     if (lane == 0)
@@ -971,6 +992,7 @@ __global__ __launch_bounds__(256, OCC) void render_item_kernel(render_params P)
             atomicAdd(P.counters + 7, (unsigned long long)cnt.w_busy);
             atomicAdd(P.counters + 9, (unsigned long long)cnt.w_box);
             atomicAdd(P.counters + 10, (unsigned long long)cnt.w_prim);
+            atomicAdd(P.counters + 11, (unsigned long long)uni_sum);
         }
     }
 }

@@ -56,7 +56,7 @@ struct vrh_ctx
     vrh_frame_stats last{};
     bool have_frame = false;
     // tuning options (0 = automatic), vrh_ctx_set_option
-    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_vote = 0, opt_dcap = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0;
+    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_vote = 0, opt_dcap = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0, opt_pop = 0, opt_coop = 0;
     // two-pass AO scratch (grown on demand): 32-B hit records and one byte per AO ray, per pixel slot
     float4* hitrec = nullptr;
     uint8_t* aobits = nullptr;
@@ -199,6 +199,8 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
     case VRH_OPT_AO_SCHEDULE: VRH_CHECK(value == 0 || (value >= 3 && value <= 6), "vrh_ctx_set_option: schedule is 3 (step), 4 (item), 5 (vote) or 6 (two-pass AO)"); ctx->opt_sched = int(value); break;
     case VRH_OPT_WIDE_ANYHIT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: wide any-hit is 1 (on) or 2 (off)"); ctx->opt_wide = int(value); break;
     case VRH_OPT_DESCENT_CAP: ctx->opt_dcap = int(value); break;
+    case VRH_OPT_COOP_FETCH: VRH_CHECK(value <= 2, "vrh_ctx_set_option: cooperative fetch is 1 (on) or 2 (off)"); ctx->opt_coop = int(value); break;
+    case VRH_OPT_POP_ON_MISS: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pop on miss is 1 (on) or 2 (off)"); ctx->opt_pop = int(value); break;
     case VRH_OPT_VOTE_LEAF: VRH_CHECK(value <= 64, "vrh_ctx_set_option: vote weight is 1..64"); ctx->opt_vote = int(value); break;
     case VRH_OPT_REFILL_MIN: VRH_CHECK(value <= 64, "vrh_ctx_set_option: refill threshold is 1..64"); ctx->opt_refill = int(value); break;
     case VRH_OPT_BLOCKS_PER_CU: ctx->opt_bpc = int(value); break;
@@ -794,6 +796,10 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     p.refill_min_primary = ctx->opt_refill ? uint32_t(ctx->opt_refill) : 1u;
     p.vote_leaf = ctx->opt_vote ? uint32_t(ctx->opt_vote) : 8u;
     p.descent_cap = ctx->opt_dcap ? uint32_t(ctx->opt_dcap) : 0xFFFFFFFFu;
+    p.pop_on_miss = ctx->opt_pop == 1 ? 1u : 0u;
+    // cooperative pair fetch (step loop, binary records; the 4-wide any-hit records keep the
+    // per-lane fetch)
+    p.coop = (ctx->opt_coop == 1 && !p.quad_ok) ? 1u : 0u;
     p.stack_cap = cap;
     p.fast_ok = (sc->finite_bounds && !ctx->opt_exact_minmax) ? 1u : 0u;
     p.quads = sc->quads;
@@ -913,7 +919,7 @@ VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats)
     VRH_HIP(hipEventSynchronize(ctx->ev_stop[ctx->last_slot]));
     float ms = 0.0f;
     VRH_HIP(hipEventElapsedTime(&ms, ctx->ev_start[ctx->last_slot], ctx->ev_stop[ctx->last_slot]));
-    unsigned long long c[11];
+    unsigned long long c[12];
     VRH_HIP(hipMemcpy(c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     ctx->last.kernel_ms = ms;
     ctx->last.rays = c[1];
@@ -924,6 +930,7 @@ VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats)
     ctx->last.busy_lane_steps = c[7];
     ctx->last.wave_box_iters = c[9];
     ctx->last.wave_prim_iters = c[10];
+    ctx->last.wave_box_uniform_iters = c[11];
     *stats = ctx->last;
     if (c[5] & 1ull) { set_error("traversal step guard tripped: corrupt BVH (rays were cut short)"); return VRH_ERR_HIP; }
     return VRH_OK;
