@@ -14,5 +14,5 @@ step bench_c2 300 python bench.py --kernel primary --no-cpu-baseline
 step bench_c4 300 python bench.py --scene hf10M --no-cpu-baseline
 step bench_c5 300 python bench.py --scene sph1M --no-cpu-baseline
 TAILN=1 step rocprof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline
-if [ "${PMC:-1}" != 0 ]; then TAILN=20 step pmc 900 bash tools/profile_pmc.sh; fi
+if [ "${PMC:-1}" != 0 ]; then TAILN=20 step pmc 900 bash tools/profile_pmc.sh; TAILN=20 step pmc_mem 900 bash tools/profile_mem.sh; fi
 exit 0
