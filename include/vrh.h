@@ -201,7 +201,7 @@ enum vrh_option {
                                     (AO only; others as 3)
                                     (auto: 4 for sphere primary visibility, else 3)              */
     VRH_OPT_BLOCKS_PER_CU = 4,   /* resident blocks per CU for the persistent grid (auto: max)     */
-    VRH_OPT_WAVES_PER_SIMD = 5,  /* register budget of the unified kernel: 1 (none), 6 or 8 (auto 6) */
+    VRH_OPT_WAVES_PER_SIMD = 5,  /* register budget of the unified kernel: 1 (none), 5, 6 or 8 (auto: 5 AO, 6 primary) */
     VRH_OPT_EXACT_MINMAX = 6,    /* 1 = always use the ternary min/max slab test (auto: hardware
                                     min/max where provably identical, see vrh_device.h)           */
     VRH_OPT_XCD_QUEUES = 7,      /* tile queues: 1 = one per XCD with stealing, 2 = one global
@@ -217,9 +217,11 @@ enum vrh_option {
                                     resumed in the next step (1..1024; auto: unlimited)          */
     VRH_OPT_POP_ON_MISS = 12,    /* step loop: a descent that misses both children pops its stack
                                     and keeps descending in the same step: 1 = on, 2 = off (auto: off) */
-    VRH_OPT_COOP_FETCH = 13      /* step loop: each quad of lanes fetches its four pair records
+    VRH_OPT_COOP_FETCH = 13,     /* step loop: each quad of lanes fetches its four pair records
                                     together (one coalesced 64-B request per record) and transposes
                                     them with DPP: 1 = on, 2 = off (auto: off)                    */
+    VRH_OPT_SCALAR_FETCH = 14    /* step loop: a pair record every active lane of a wave wants is
+                                    fetched once through the scalar cache: 1 = on, 2 = off (auto: on) */
 };
 VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value);
 

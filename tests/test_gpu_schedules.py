@@ -34,9 +34,14 @@ VARIANTS = {
     "coop": {"ao_schedule": 3, "coop_fetch": 1},
     "coop_exact_pop_cap3": {"ao_schedule": 3, "coop_fetch": 1, "exact_minmax": 1, "pop_on_miss": 1, "descent_cap": 3},
     "coop_two_pass": {"ao_schedule": 6, "coop_fetch": 1},
+    "scalar_off": {"ao_schedule": 3, "scalar_fetch": 2},
+    "scalar_off_pop_cap2": {"ao_schedule": 3, "scalar_fetch": 2, "pop_on_miss": 1, "descent_cap": 2},
+    "two_pass_occ5": {"ao_schedule": 6, "waves_per_simd": 5},
+    "occ5": {"ao_schedule": 3, "waves_per_simd": 5},
+    "occ6": {"ao_schedule": 3, "waves_per_simd": 6},
 }
 OPTIONS = ("ao_schedule", "refill_min", "vote_leaf", "wide_anyhit", "exact_minmax", "descent_cap", "xcd_queues",
-           "pop_on_miss", "coop_fetch")
+           "pop_on_miss", "coop_fetch", "scalar_fetch", "waves_per_simd")
 
 
 @pytest.fixture(params=sorted(VARIANTS))

@@ -68,6 +68,7 @@ for rnd in range(rounds):
         ctx.set_option("descent_cap", v.get("descent_cap", 0))
         ctx.set_option("pop_on_miss", v.get("pop_on_miss", 0))
         ctx.set_option("coop_fetch", v.get("coop_fetch", 0))
+        ctx.set_option("scalar_fetch", v.get("scalar_fetch", 0))
         ctx.stats_reset()
         for _ in range(3):
             va.render_batch(ctx, dev, rt, [basis] * F, kern)

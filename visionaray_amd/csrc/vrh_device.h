@@ -336,9 +336,12 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
                                         const ray_t& r, float max_t, bool any, lds_stack& st,
                                         float& best_t, uint32_t& best_prim, test_counts& cnt,
                                         uint32_t& steps, uint32_t step_limit, uint32_t& resume, uint32_t cap,
-                                        bool pop_on_miss, hit_extra* hx = nullptr, const MultiList* mh = nullptr,
+                                        uint32_t flags, hit_extra* hx = nullptr, const MultiList* mh = nullptr,
                                         const hit_mask_params* hm = nullptr)
 {
+    // flags (render_params::step_flags): bit 0 pop on miss, bit 1 scalar fetch of wave-uniform pairs
+    const bool pop_on_miss = (flags & 1u) != 0u;
+    const bool scalar_uniform = SCALAR_UNIFORM && (flags & 2u) != 0u;
     // the tree was validated at upload (no cycles, links in range), so the descent terminates;
     // the guard below only bounds the number of outer iterations per ray
     uint32_t link;
@@ -404,13 +407,16 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
         // in about a third of the wave-level descent iterations every active lane fetches the SAME
         // pair (upper tree levels): those fetch it once through the scalar cache instead (s_load on
         // a wave-uniform address, constant address space), the rest per lane (56 of the record's
-        // 64 B: two boxes, two links).  Same bytes either way.
+        // 64 B: two boxes, two links).  Same bytes either way.  (Extending this to waves whose lanes
+        // want 2 or 3 distinct pairs -- one scalar load each, selected per lane -- measured 2-10 %
+        // slower: profiles/r01_ab_peel/.)
         float4 q0, q1, q2;
         float2 q3;
+        typedef const __attribute__((address_space(4))) float cfloat;
         const uint32_t lf = (uint32_t)__builtin_amdgcn_readfirstlane((int)link);
-        if (SCALAR_UNIFORM && __ballot(link != lf) == 0ull)
+        const uint64_t rest1 = __ballot(link != lf);
+        if (scalar_uniform && rest1 == 0ull)
         {
-            typedef const __attribute__((address_space(4))) float cfloat;
             cfloat* cp = (cfloat*)(const float*)(pairs) + 16u * lf;
             q0 = make_float4(cp[0], cp[1], cp[2], cp[3]);
             q1 = make_float4(cp[4], cp[5], cp[6], cp[7]);
@@ -487,10 +493,12 @@ __device__ __forceinline__ int ray_step_coop(bool active, const float4* __restri
                                              uint32_t root, const ray_t& r, float max_t, bool any, lds_stack& st,
                                              float& best_t, uint32_t& best_prim, test_counts& cnt,
                                              uint32_t& steps, uint32_t step_limit, uint32_t& resume, uint32_t cap,
-                                             bool pop_on_miss, hit_extra* hx = nullptr, const MultiList* mh = nullptr,
+                                             uint32_t flags, hit_extra* hx = nullptr, const MultiList* mh = nullptr,
                                              const hit_mask_params* hm = nullptr)
 {
     (void)root;
+    const bool pop_on_miss = (flags & 1u) != 0u;
+    const bool scalar_uniform = SCALAR_UNIFORM && (flags & 2u) != 0u;
     int rc = 0;
     bool desc = false;
     uint32_t link = 0u;
@@ -517,7 +525,7 @@ __device__ __forceinline__ int ray_step_coop(bool active, const float4* __restri
         const uint32_t lf = (uint32_t)__builtin_amdgcn_readlane((int)fl, (int)__builtin_ctzll(dm));
         float4 q0, q1, q2;
         float2 q3;
-        if (SCALAR_UNIFORM && __ballot(desc && fl != lf) == 0ull)
+        if (scalar_uniform && __ballot(desc && fl != lf) == 0ull)
         {
             typedef const __attribute__((address_space(4))) float cfloat;
             cfloat* cp = (cfloat*)(const float*)(pairs) + 16u * lf;

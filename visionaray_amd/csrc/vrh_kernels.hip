@@ -264,13 +264,13 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             int rc_coop = 0;
             if (P.coop)
                 rc_coop = (P.fast_ok && __ballot(busy && !finite) == 0ull)
-                    ? ray_step_coop<KIND, COUNT, true, UV, ML>(busy, P.pairs, P.prims, P.root, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, &hx, &mh, hm)
-                    : ray_step_coop<KIND, COUNT, false, UV, ML>(busy, P.pairs, P.prims, P.root, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, &hx, &mh, hm);
+                    ? ray_step_coop<KIND, COUNT, true, UV, ML>(busy, P.pairs, P.prims, P.root, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, &hx, &mh, hm)
+                    : ray_step_coop<KIND, COUNT, false, UV, ML>(busy, P.pairs, P.prims, P.root, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, &hx, &mh, hm);
             if (mode != IDLE)
             {
                 int rc = P.coop ? rc_coop : (P.fast_ok && __ballot(!finite) == 0ull)
-                    ? ray_step<KIND, COUNT, true, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, &hx, &mh, hm)
-                    : ray_step<KIND, COUNT, false, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, &hx, &mh, hm);
+                    ? ray_step<KIND, COUNT, true, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, &hx, &mh, hm)
+                    : ray_step<KIND, COUNT, false, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, &hx, &mh, hm);
                 if constexpr (EPI == 3)
                 {
                     if (rc != 0)
@@ -512,14 +512,14 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             {
                 // cooperative pair fetch: every lane takes part (quad exchanges), idle lanes included
                 rc = (P.fast_ok && __ballot(busy && !finite) == 0ull)
-                    ? ray_step_coop<KIND, COUNT, true>(busy, P.pairs, P.prims, P.root, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, nullptr, static_cast<const void*>(nullptr), hm)
-                    : ray_step_coop<KIND, COUNT, false>(busy, P.pairs, P.prims, P.root, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, nullptr, static_cast<const void*>(nullptr), hm);
+                    ? ray_step_coop<KIND, COUNT, true>(busy, P.pairs, P.prims, P.root, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm)
+                    : ray_step_coop<KIND, COUNT, false>(busy, P.pairs, P.prims, P.root, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm);
             }
             else if (busy)
             {
                 rc = (P.fast_ok && __ballot(!finite) == 0ull)
-                    ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, nullptr, static_cast<const void*>(nullptr), hm)
-                    : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, nullptr, static_cast<const void*>(nullptr), hm);
+                    ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm)
+                    : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm);
             }
             if (COUNT) count_wave(cnt, busy);
             // 5. finished AO rays: record occlusion, retire from their tile's in-flight count
@@ -675,14 +675,14 @@ __global__ __launch_bounds__(256, OCC) void ao_pass_kernel(render_params P)
         if (P.coop)
         {
             rc = (P.fast_ok && __ballot(busy && !finite) == 0ull)
-                ? ray_step_coop<KIND, COUNT, true>(busy, P.pairs, P.prims, P.root, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, nullptr, static_cast<const void*>(nullptr), hm)
-                : ray_step_coop<KIND, COUNT, false>(busy, P.pairs, P.prims, P.root, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, nullptr, static_cast<const void*>(nullptr), hm);
+                ? ray_step_coop<KIND, COUNT, true>(busy, P.pairs, P.prims, P.root, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm)
+                : ray_step_coop<KIND, COUNT, false>(busy, P.pairs, P.prims, P.root, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm);
         }
         else if (busy)
         {
             rc = (P.fast_ok && __ballot(!finite) == 0ull)
-                ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, nullptr, static_cast<const void*>(nullptr), hm)
-                : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.pop_on_miss != 0u, nullptr, static_cast<const void*>(nullptr), hm);
+                ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm)
+                : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm);
         }
         if (COUNT) count_wave(cnt, busy);
         if (busy && rc != 0)
@@ -1072,6 +1072,7 @@ static kernel_fn pick(bool ao, bool count, int occ, int sched)
 {
     if (occ == 8) return pick_occ<KIND, 8>(ao, count, sched);
     if (occ == 6) return pick_occ<KIND, 6>(ao, count, sched);
+    if (occ == 5) return pick_occ<KIND, 5>(ao, count, sched);
     return pick_occ<KIND, 1>(ao, count, sched);
 }
 

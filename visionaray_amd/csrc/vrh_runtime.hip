@@ -56,7 +56,7 @@ struct vrh_ctx
     vrh_frame_stats last{};
     bool have_frame = false;
     // tuning options (0 = automatic), vrh_ctx_set_option
-    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_vote = 0, opt_dcap = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0, opt_pop = 0, opt_coop = 0;
+    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_vote = 0, opt_dcap = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0, opt_pop = 0, opt_coop = 0, opt_scalar = 0;
     // two-pass AO scratch (grown on demand): 32-B hit records and one byte per AO ray, per pixel slot
     float4* hitrec = nullptr;
     uint8_t* aobits = nullptr;
@@ -201,10 +201,11 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
     case VRH_OPT_DESCENT_CAP: ctx->opt_dcap = int(value); break;
     case VRH_OPT_COOP_FETCH: VRH_CHECK(value <= 2, "vrh_ctx_set_option: cooperative fetch is 1 (on) or 2 (off)"); ctx->opt_coop = int(value); break;
     case VRH_OPT_POP_ON_MISS: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pop on miss is 1 (on) or 2 (off)"); ctx->opt_pop = int(value); break;
+    case VRH_OPT_SCALAR_FETCH: VRH_CHECK(value <= 2, "vrh_ctx_set_option: scalar fetch is 1 (on) or 2 (off)"); ctx->opt_scalar = int(value); break;
     case VRH_OPT_VOTE_LEAF: VRH_CHECK(value <= 64, "vrh_ctx_set_option: vote weight is 1..64"); ctx->opt_vote = int(value); break;
     case VRH_OPT_REFILL_MIN: VRH_CHECK(value <= 64, "vrh_ctx_set_option: refill threshold is 1..64"); ctx->opt_refill = int(value); break;
     case VRH_OPT_BLOCKS_PER_CU: ctx->opt_bpc = int(value); break;
-    case VRH_OPT_WAVES_PER_SIMD: VRH_CHECK(value == 0 || value == 1 || value == 6 || value == 8, "vrh_ctx_set_option: waves per SIMD is 1, 6 or 8"); ctx->opt_occ = int(value); break;
+    case VRH_OPT_WAVES_PER_SIMD: VRH_CHECK(value == 0 || value == 1 || value == 5 || value == 6 || value == 8, "vrh_ctx_set_option: waves per SIMD is 1, 5, 6 or 8"); ctx->opt_occ = int(value); break;
     case VRH_OPT_EXACT_MINMAX: ctx->opt_exact_minmax = value ? 1 : 0; break;
     case VRH_OPT_XCD_QUEUES: VRH_CHECK(value <= 2, "vrh_ctx_set_option: xcd queues is 1 (on) or 2 (off)"); ctx->opt_xcd_queues = int(value); break;
     default: set_error("vrh_ctx_set_option: unknown option"); return VRH_ERR_INVALID;
@@ -768,8 +769,9 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     lc.stack_cap = int(cap);
     lc.epi = whitted ? 3 : multi ? 2 : shade ? 1 : 0;
     // shading epilogues: no VGPR cap (their lane state spills at 6 waves/SIMD; measured faster at 4,
-    // profiles/r01_shade/shade_bench.jsonl)
-    lc.occ = ctx->opt_occ ? ctx->opt_occ : (lc.epi ? 1 : 6);
+    // profiles/r01_shade/shade_bench.jsonl); AO on the step loop: 5 waves/SIMD (96 VGPRs, no spills:
+    // 4-6 % faster than 6 with 18 spilled VGPRs); primary visibility: 6 (profiles/r01_ab_waves/)
+    lc.occ = ctx->opt_occ ? ctx->opt_occ : lc.epi ? 1 : (lc.ao && lc.sched == 0) ? 5 : 6;
     lc.max_hits = multi ? int(k->max_hits) : 0;
     // auto: the item loop for sphere primary visibility (short leaves of cheap tests, where the
     // step loop's leaf iterations run at ~20 % lane utilisation), the step loop otherwise
@@ -796,7 +798,7 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     p.refill_min_primary = ctx->opt_refill ? uint32_t(ctx->opt_refill) : 1u;
     p.vote_leaf = ctx->opt_vote ? uint32_t(ctx->opt_vote) : 8u;
     p.descent_cap = ctx->opt_dcap ? uint32_t(ctx->opt_dcap) : 0xFFFFFFFFu;
-    p.pop_on_miss = ctx->opt_pop == 1 ? 1u : 0u;
+    p.step_flags = (ctx->opt_pop == 1 ? 1u : 0u) | (ctx->opt_scalar == 2 ? 0u : 2u);
     // cooperative pair fetch (step loop, binary records; the 4-wide any-hit records keep the
     // per-lane fetch)
     p.coop = (ctx->opt_coop == 1 && !p.quad_ok) ? 1u : 0u;
