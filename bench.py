@@ -336,6 +336,8 @@ def main():
                     limiter = {"unit": "vector-memory pipeline (L1 / TA address / TD data)",
                                "td_busy": round(pm["td_busy_frac"], 3), "ta_busy": round(pm["ta_busy_frac"], 3),
                                "l1_hit": round(1.0 - pm["l1_to_l2_reads_per_access"], 3),
+                               "td_stalled_on_l1": (round(pm["td_stalled_on_l1_frac"], 3)
+                                                    if pm.get("td_stalled_on_l1_frac") is not None else None),
                                "source": "profiles/pmc_mem.json (rocprofv3 --pmc, same workload)"}
             except Exception:
                 limiter = None

@@ -38,8 +38,12 @@ def main():
         "l1_accesses_per_vmem_instr": c["TCP_TOTAL_CACHE_ACCESSES_sum"] / c["SQ_INSTS_VMEM_RD"],
         "l1_to_l2_reads_per_access": c["TCP_TCC_READ_REQ_sum"] / c["TCP_TOTAL_CACHE_ACCESSES_sum"],
         "l2_read_latency_cycles": c["TCP_TCC_READ_REQ_LATENCY_sum"] / c["TCP_TCC_READ_REQ_sum"],
+        "td_stalled_on_l1_frac": (c["TD_TC_STALL_sum"] / c["TD_TD_BUSY_sum"]) if "TD_TC_STALL_sum" in c else None,
+        "l1_pending_stall_frac": (c["TCP_PENDING_STALL_CYCLES_sum"] / (cus * cycles))
+                                 if "TCP_PENDING_STALL_CYCLES_sum" in c else None,
         "note": "TA/TD busy = fraction of kernel cycles the vector-memory address / data units of the 256 CUs "
-                "are busy; the traversal kernel's limiter when TD is near 1",
+                "are busy; td_stalled_on_l1 = share of the TD busy cycles spent waiting for the L1 (TCP); "
+                "l1_pending_stall = fraction of cycles the L1 stalls on outstanding misses",
     }
     with open(out, "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
