@@ -1,6 +1,8 @@
 // Microbenchmark: per-lane 64-B record fetch (4 x dwordx4 per lane, 64 records per wave-load) vs a
 // cooperative fetch (lane row r loads quarter r of the records of its 4-lane column group, then a
-// 4x4 transpose with v_permlane32_swap / v_permlane16_swap): dependent chains of random records.
+// 4x4 transpose with v_permlane32_swap / v_permlane16_swap), a quad-cooperative fetch transposed with
+// DPP, and the same quad fetch transposed through LDS (register-staged: ds_write + ds_read; or
+// global_load_lds_dwordx4 straight into LDS + ds_read): dependent chains of random records.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -52,6 +54,9 @@ __device__ __forceinline__ void qtr4f(float4& a0, float4& a1, float4& a2, float4
 __global__ __launch_bounds__(64) void chase(const float4* __restrict__ tab, uint32_t mask, int coop, int iters,
                                             uint32_t* out)
 {
+    // LDS staging of the quad fetch: load j lands in region j (lane-linear, 16 B per lane);
+    // lane 4k + j then reads its record as 64 contiguous bytes of region j at slot 4k
+    __shared__ float4 stage[4][64];
     const uint32_t lane = threadIdx.x & 63u, row = lane >> 4;
     uint32_t link = (blockIdx.x * 64u + lane) * 2654435761u & mask;
     float acc = 0.0f;
@@ -70,6 +75,31 @@ __global__ __launch_bounds__(64) void chase(const float4* __restrict__ tab, uint
             const uint32_t m = lane & 3u;
             q0 = tab[4u * l0 + m]; q1 = tab[4u * l1 + m]; q2 = tab[4u * l2 + m]; q3 = tab[4u * l3 + m];
             qtr4f(q0, q1, q2, q3, lane);               // q_k = quarter k of my own record
+        }
+        else if (coop == 3 || coop == 4)
+        {
+            uint32_t l0 = link, l1 = link, l2 = link, l3 = link;
+            qtr4(l0, l1, l2, l3, lane);                // l_j = link of quad lane j
+            const uint32_t m = lane & 3u;
+            if (coop == 3)
+            {
+                const float4 a0 = tab[4u * l0 + m], a1 = tab[4u * l1 + m], a2 = tab[4u * l2 + m], a3 = tab[4u * l3 + m];
+                stage[0][lane] = a0; stage[1][lane] = a1; stage[2][lane] = a2; stage[3][lane] = a3;
+            }
+            else
+            {
+                typedef __attribute__((address_space(1))) void gvoid;
+                typedef __attribute__((address_space(3))) void lvoid;
+                __builtin_amdgcn_global_load_lds((gvoid*)(tab + 4u * l0 + m), (lvoid*)&stage[0][0], 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((gvoid*)(tab + 4u * l1 + m), (lvoid*)&stage[1][0], 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((gvoid*)(tab + 4u * l2 + m), (lvoid*)&stage[2][0], 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((gvoid*)(tab + 4u * l3 + m), (lvoid*)&stage[3][0], 16, 0, 0);
+                __builtin_amdgcn_s_waitcnt(0x0070);    // vmcnt(0) (lgkmcnt/expcnt left at max)
+            }
+            __builtin_amdgcn_wave_barrier();
+            const float4* mine = &stage[m][lane & ~3u];
+            q0 = mine[0]; q1 = mine[1]; q2 = mine[2]; q3 = mine[3];
+            __builtin_amdgcn_wave_barrier();
         }
         else
         {
@@ -98,14 +128,16 @@ int main(int argc, char** argv)
     (void)hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice);
     hipEvent_t a, b; (void)hipEventCreate(&a); (void)hipEventCreate(&b);
     std::vector<uint32_t> r0(blocks * 64), r1(blocks * 64);
-    for (int coop = 0; coop < 3; ++coop)
+    const char* names[] = { "per-lane 4 x dwordx4", "row-cooperative + permlane transpose", "quad-cooperative + DPP transpose",
+                            "quad-cooperative + LDS transpose (reg-staged)", "quad-cooperative + global_load_lds + LDS read" };
+    for (int coop = 0; coop < 5; ++coop)
     {
         hipLaunchKernelGGL(chase, dim3(blocks), dim3(64), 0, 0, d, nrec - 1, coop, iters, coop ? o2 : o);
         (void)hipEventRecord(a);
         hipLaunchKernelGGL(chase, dim3(blocks), dim3(64), 0, 0, d, nrec - 1, coop, iters, coop ? o2 : o);
         (void)hipEventRecord(b); (void)hipEventSynchronize(b);
         float ms = 0; (void)hipEventElapsedTime(&ms, a, b);
-        printf("table %u KB %s: %.3f ms, %.1f record fetches/ns\n", nrec / 16, coop == 2 ? "quad-cooperative + DPP transpose" : coop ? "row-cooperative + permlane transpose" : "per-lane 4 x dwordx4",
+        printf("table %u KB %s: %.3f ms, %.1f record fetches/ns\n", nrec / 16, names[coop],
                ms, double(blocks) * 64 * iters / (ms * 1e6));
         if (coop) { (void)hipMemcpy(r1.data(), o2, r1.size() * 4, hipMemcpyDeviceToHost); (void)hipMemcpy(r0.data(), o, r0.size() * 4, hipMemcpyDeviceToHost); printf("  same results as per-lane: %s\n", r0 == r1 ? "yes" : "NO"); }
     }
