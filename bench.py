@@ -47,8 +47,8 @@ OUT_BYTES_PRIMARY = 24          # RGBA32F + u32 prim_id + f32 t per primary ray 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=32)
-    ap.add_argument("--warmup", type=int, default=16, help="untimed frames (default: two launches, so every buffer is touched)")
+    ap.add_argument("--steps", type=int, default=64, help="timed frames (default: two 32-frame launches)")
+    ap.add_argument("--warmup", type=int, default=32, help="untimed frames (default: one launch)")
     ap.add_argument("--scene", default="hf1M", help="hf1M (C3, default) | hf10M (C4) | sph1M (C5)")
     ap.add_argument("--kernel", default=None, choices=["ao", "primary"], help="default: ao for triangles")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -56,8 +56,8 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, the measured path) | gloo (host-staged; single-GPU rehearsal only)")
     ap.add_argument("--no-verify", action="store_true", help="skip the untimed check of the last frames against a 1-GPU frame")
-    ap.add_argument("--frames-in-flight", type=int, default=8,
-                    help="frames per persistent launch (vrh_render_batch, 1..8); every frame is still fully traced")
+    ap.add_argument("--frames-in-flight", type=int, default=32,
+                    help="frames per persistent launch (vrh_render_batch, 1..32); every frame is still fully traced")
     return ap.parse_args()
 
 

@@ -266,7 +266,7 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* scene, vrh_rt* rt, const v
  * The frames' tiles share the work queues, interleaved tile by tile, so a wave goes on to the next
  * frame's tiles instead of idling while the last tiles of a frame finish; every frame's output is
  * identical to its own vrh_render. */
-#define VRH_MAX_BATCH 8
+#define VRH_MAX_BATCH 32
 VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* scene, vrh_rt* rt, const vrh_camera* cams,
                              uint32_t num_frames, const vrh_kernel_desc* kernel, const vrh_shard* shard,
                              uint32_t frame_num);

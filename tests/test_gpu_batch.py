@@ -74,7 +74,7 @@ def check_batch(ctx, name, W, H, kind, n, shard=None):
         assert not np.array_equal(got["prim_id"][:rows * W], got["prim_id"][rows * W:2 * rows * W])
 
 
-@pytest.mark.parametrize("n", [1, 2, 3, 8])
+@pytest.mark.parametrize("n", [1, 2, 3, 8, 17, 32])
 @pytest.mark.parametrize("kind", ["ao", "primary"])
 def test_batch_frames_equal_single_frames(ctx, kind, n):
     check_batch(ctx, "hf200", 320, 180, kind, n)
@@ -95,9 +95,9 @@ def test_batch_under_other_schedules(ctx, sched):
         ctx.set_option("ao_schedule", 0)
 
 
-@pytest.mark.parametrize("count,index", [(3, 0), (3, 2), (8, 5)])
-def test_batch_packed_shards(ctx, count, index):
-    check_batch(ctx, "hf200", 320, 180, "ao", 4, shard=_capi.vrh_shard(index, count, 1, 0))
+@pytest.mark.parametrize("count,index,n", [(3, 0, 4), (3, 2, 4), (8, 5, 4), (8, 7, 32)])
+def test_batch_packed_shards(ctx, count, index, n):
+    check_batch(ctx, "hf200", 320, 180, "ao", n, shard=_capi.vrh_shard(index, count, 1, 0))
 
 
 def test_batch_arguments_are_checked(ctx):

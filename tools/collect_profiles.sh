@@ -13,8 +13,8 @@ for p in fetch write sq1 sq2 tcc lds; do cp gpurun_out/pmc/$p/run_counter_collec
 for p in vmem ta td ta2 tcp tcp2 vmem2; do
   [ -f gpurun_out/pmc_mem/$p/run_counter_collection.csv ] && cp gpurun_out/pmc_mem/$p/run_counter_collection.csv "$D/pmc_mem/$p.csv"
 done
-python3 tools/pmc_summary.py gpurun_out/pmc profiles/pmc_traffic.json hf1M ao 8 > /dev/null
-python3 tools/pmc_mem_summary.py gpurun_out/pmc_mem profiles/pmc_mem.json hf1M ao 8 > /dev/null
+python3 tools/pmc_summary.py gpurun_out/pmc profiles/pmc_traffic.json hf1M ao 32 > /dev/null
+python3 tools/pmc_mem_summary.py gpurun_out/pmc_mem profiles/pmc_mem.json hf1M ao 32 > /dev/null
 python3 - "$D" <<'EOF'
 import csv, sys
 d = sys.argv[1]

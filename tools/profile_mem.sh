@@ -3,7 +3,7 @@
 # SQ VMEM levels) over tools/frame_driver.py; one counter group per pass, no tracing domains.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-SCENE=${SCENE:-hf1M}; FRAMES=${FRAMES:-4}; KIND=${KIND:-ao}; BATCH=${BATCH:-8}; OUTD=${OUTD:-gpurun_out/pmc_mem}
+SCENE=${SCENE:-hf1M}; FRAMES=${FRAMES:-4}; KIND=${KIND:-ao}; BATCH=${BATCH:-32}; OUTD=${OUTD:-gpurun_out/pmc_mem}
 mkdir -p $OUTD
 run() {  # name, counters...
   local name=$1; shift

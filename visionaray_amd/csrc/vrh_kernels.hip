@@ -36,7 +36,7 @@ constexpr int AO_WAVE_WORDS = AO_SLOT_PX + 2 * 64 / 4;
 
 // tile id (next_tile: frame f << TILE_FRAME_SHIFT | tile of that frame) -> (x, y) of lane, plus the
 // output row (frame f's rows start at f * frame_rows; packed shards).  A band is one row of tiles.
-constexpr uint32_t TILE_FRAME_SHIFT = 29;
+constexpr uint32_t TILE_FRAME_SHIFT = 26;   // frames < 64, tiles of one frame < 2^26
 constexpr uint32_t TILE_MASK = (1u << TILE_FRAME_SHIFT) - 1u;
 __device__ __forceinline__ bool tile_pixel(const render_params& P, uint32_t id, uint32_t lane,
                                            uint32_t& x, uint32_t& y, uint32_t& out_row, uint32_t& f)

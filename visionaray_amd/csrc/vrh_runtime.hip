@@ -819,7 +819,7 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     p.shard_index = sh.index; p.shard_count = sh.count; p.packed = sh.packed ? 1u : 0u;
     p.tiles_x = (cam->width + 7u) / 8u;
     p.num_tiles = local_bands * p.tiles_x;        // a band is one row of 8x8 tiles
-    VRH_CHECK(uint64_t(p.num_tiles) * 64u * num_frames < (1ull << 32), "vrh_render: image too large");
+    VRH_CHECK(uint64_t(p.num_tiles) * 64u * num_frames < (1ull << 32) && p.num_tiles < (1u << 26), "vrh_render: image too large");
     p.color = rt->color; p.prim_id = rt->prim_id; p.t = rt->t; p.occ = rt->occ;
     p.counters = ctx->counters;
     p.xcd_queues = ctx->opt_xcd_queues == 2 ? 0u : 1u;
