@@ -21,7 +21,7 @@ d = sys.argv[1]
 rows = sorted(csv.DictReader(open('gpurun_out/prof/run_kernel_trace.csv')), key=lambda r: int(r['Start_Timestamp']))
 with open(d + '/bench_launches.txt', 'w') as f:
     f.write("# every traversal launch of `python bench.py --no-cpu-baseline` under rocprofv3 --kernel-trace, in order\n")
-    f.write("# (count pass, reference frame on the item loop, warm-up launches, a buffer-priming launch, the timed 8-frame launches)\n")
+    f.write("# (count pass, reference frame on the item loop, warm-up launches, a buffer-priming launch, the timed F-frame launches)\n")
     for r in rows:
         if 'render' in r['Kernel_Name']:
             f.write("%9.3f ms  %s\n" % ((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6, r['Kernel_Name']))
