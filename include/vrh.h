@@ -207,16 +207,19 @@ enum vrh_option {
     VRH_OPT_XCD_QUEUES = 7,      /* tile queues: 1 = one per XCD with stealing, 2 = one global
                                     queue (auto: 1)                                               */
     VRH_OPT_REFILL_MIN = 8,      /* free lanes (1..64) before finished rays are retired and idle
-                                    lanes refilled (auto: 32 step loop, 16 item loops)           */
+                                    lanes refilled (auto: 32 step loop and primary item loop, 16
+                                    AO item loops)                                                */
     VRH_OPT_VOTE_LEAF = 9,       /* vote loop: primitive step when 8 x leaf lanes >= this x node
                                     lanes (1..64, auto: 8 = simple majority)                     */
     VRH_OPT_WIDE_ANYHIT = 10,    /* 4-wide node records for any-hit (AO) rays (step loop): 1 = on
                                     when the BVH passes the containment check, 2 = off (auto: off,
                                     measured 6 % slower on hf1M AO than the binary records)      */
     VRH_OPT_DESCENT_CAP = 11,    /* step loop: inner visits per step before a lane's descent is
-                                    resumed in the next step (1..1024; auto: unlimited)          */
+                                    resumed in the next step (1..1024; auto: 8 for primary
+                                    visibility, unlimited for AO)                                 */
     VRH_OPT_POP_ON_MISS = 12,    /* step loop: a descent that misses both children pops its stack
-                                    and keeps descending in the same step: 1 = on, 2 = off (auto: off) */
+                                    and keeps descending in the same step: 1 = on, 2 = off (auto: on
+                                    for primary visibility, off for AO)                           */
     VRH_OPT_COOP_FETCH = 13,     /* step loop: each quad of lanes fetches its four pair records
                                     together (one coalesced 64-B request per record) and transposes
                                     them with DPP: 1 = on, 2 = off (auto: off)                    */

@@ -39,6 +39,9 @@ VARIANTS = {
     "two_pass_occ5": {"ao_schedule": 6, "waves_per_simd": 5},
     "occ5": {"ao_schedule": 3, "waves_per_simd": 5},
     "occ6": {"ao_schedule": 3, "waves_per_simd": 6},
+    # the primary-visibility defaults switched off (pop on miss, descent cap 8, item refill 32)
+    "no_pop_uncapped": {"pop_on_miss": 2, "descent_cap": 1024, "refill_min": 16},
+    "pop_cap10": {"pop_on_miss": 1, "descent_cap": 10},
 }
 OPTIONS = ("ao_schedule", "refill_min", "vote_leaf", "wide_anyhit", "exact_minmax", "descent_cap", "xcd_queues",
            "pop_on_miss", "coop_fetch", "scalar_fetch", "waves_per_simd")

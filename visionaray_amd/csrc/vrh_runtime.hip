@@ -794,11 +794,16 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     render_params p{};
     p.pairs = sc->pairs; p.prims = sc->prims; p.normals = sc->normals; p.root = sc->root;
     p.step_limit = sc->info.num_nodes + sc->info.num_indices + 16u;
-    p.refill_min = ctx->opt_refill ? uint32_t(ctx->opt_refill) : (lc.sched == 0 ? 32u : 16u);   // measured (profiles/r01_ab)
+    // measured: profiles/r01_ab (AO), profiles/r01_ab_primary (primary visibility: the item loop
+    // refills at 32 free lanes; the step loop pops on a miss and caps a descent at 8 visits per
+    // step, +6 % on hf1M and +36 % on hf10M; both hurt AO)
+    const bool primary_step = lc.sched == 0 && !lc.ao && lc.epi == 0;
+    p.refill_min = ctx->opt_refill ? uint32_t(ctx->opt_refill) : (lc.sched == 0 || (lc.sched == 1 && !lc.ao)) ? 32u : 16u;
     p.refill_min_primary = ctx->opt_refill ? uint32_t(ctx->opt_refill) : 1u;
     p.vote_leaf = ctx->opt_vote ? uint32_t(ctx->opt_vote) : 8u;
-    p.descent_cap = ctx->opt_dcap ? uint32_t(ctx->opt_dcap) : 0xFFFFFFFFu;
-    p.step_flags = (ctx->opt_pop == 1 ? 1u : 0u) | (ctx->opt_scalar == 2 ? 0u : 2u);
+    p.descent_cap = ctx->opt_dcap ? uint32_t(ctx->opt_dcap) : primary_step ? 8u : 0xFFFFFFFFu;
+    const bool pop = ctx->opt_pop == 1 || (ctx->opt_pop == 0 && primary_step);
+    p.step_flags = (pop ? 1u : 0u) | (ctx->opt_scalar == 2 ? 0u : 2u);
     // cooperative pair fetch (step loop, binary records; the 4-wide any-hit records keep the
     // per-lane fetch)
     p.coop = (ctx->opt_coop == 1 && !p.quad_ok) ? 1u : 0u;
