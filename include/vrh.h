@@ -219,7 +219,7 @@ enum vrh_option {
                                     visibility, unlimited for AO)                                 */
     VRH_OPT_POP_ON_MISS = 12,    /* step loop: a descent that misses both children pops its stack
                                     and keeps descending in the same step: 1 = on, 2 = off (auto: on
-                                    for primary visibility, off for AO)                           */
+                                    for primary visibility and shading kernels, off for AO)       */
     VRH_OPT_COOP_FETCH = 13,     /* step loop: each quad of lanes fetches its four pair records
                                     together (one coalesced 64-B request per record) and transposes
                                     them with DPP: 1 = on, 2 = off (auto: off)                    */

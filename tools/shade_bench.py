@@ -18,6 +18,8 @@ def main():
     ap.add_argument("--scene", default="hf1M")
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--occ", default="0,1,6,8")
+    ap.add_argument("--variants", default=None,
+                    help='JSON list of option dicts, e.g. [{"pop_on_miss": 1, "descent_cap": 8}] (replaces --occ)')
     a = ap.parse_args()
     import numpy as np
     import torch  # noqa: F401
@@ -51,9 +53,12 @@ def main():
     }
     sched = va.hip_sched(ctx)
     sp = va.make_sched_params(va.pixel_sampler.uniform_type, cam, rt)
+    variants = json.loads(a.variants) if a.variants else [{"waves_per_simd": int(x)} for x in a.occ.split(",")]
     for name, k in kernels.items():
-        for occ in [int(x) for x in a.occ.split(",")]:
-            ctx.set_option("waves_per_simd", occ)
+        for v in variants:
+            for opt, val in v.items():
+                ctx.set_option(opt, val)
+            occ = v.get("waves_per_simd", 0)
             try:
                 for _ in range(2):
                     sched.frame(k, sp)
@@ -66,13 +71,14 @@ def main():
                 dt = time.perf_counter() - t0
                 st = ctx.accum_stats()
                 rays = int(st["rays"])
-                print(json.dumps({"kernel": name, "occ": occ, "scene": a.scene, "W": W, "H": H,
+                print(json.dumps({"kernel": name, "occ": occ, "options": v, "scene": a.scene, "W": W, "H": H,
                                   "ms_per_frame": round(dt / a.frames * 1e3, 3),
                                   "rays_per_frame": rays // a.frames,
                                   "Mrays_per_s": round(rays / dt / 1e6, 1)}), flush=True)
             except Exception as e:  # report and go on with the next variant
-                print(json.dumps({"kernel": name, "occ": occ, "error": str(e)}), flush=True)
-    ctx.set_option("waves_per_simd", 0)
+                print(json.dumps({"kernel": name, "occ": occ, "options": v, "error": str(e)}), flush=True)
+            for opt in v:
+                ctx.set_option(opt, 0)
 
 
 if __name__ == "__main__":

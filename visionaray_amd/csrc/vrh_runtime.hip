@@ -802,7 +802,8 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     p.refill_min_primary = ctx->opt_refill ? uint32_t(ctx->opt_refill) : 1u;
     p.vote_leaf = ctx->opt_vote ? uint32_t(ctx->opt_vote) : 8u;
     p.descent_cap = ctx->opt_dcap ? uint32_t(ctx->opt_dcap) : primary_step ? 8u : 0xFFFFFFFFu;
-    const bool pop = ctx->opt_pop == 1 || (ctx->opt_pop == 0 && primary_step);
+    // shading epilogues (simple / multi_hit / whitted) pop on a miss too: +4-7 % (profiles/r01_shade/)
+    const bool pop = ctx->opt_pop == 1 || (ctx->opt_pop == 0 && (primary_step || lc.epi != 0));
     p.step_flags = (pop ? 1u : 0u) | (ctx->opt_scalar == 2 ? 0u : 2u);
     // cooperative pair fetch (step loop, binary records; the 4-wide any-hit records keep the
     // per-lane fetch)
