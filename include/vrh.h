@@ -222,7 +222,8 @@ enum vrh_option {
                                     for primary visibility and shading kernels, off for AO)       */
     VRH_OPT_COOP_FETCH = 13,     /* step loop: each quad of lanes fetches its four pair records
                                     together (one coalesced 64-B request per record) and transposes
-                                    them with DPP: 1 = on, 2 = off (auto: off)                    */
+                                    them with DPP: 1 = on, 2 = off (auto: off; 1 needs a build
+                                    with -DVRH_COOP=1, else VRH_ERR_UNSUPPORTED)                  */
     VRH_OPT_SCALAR_FETCH = 14    /* step loop: a pair record every active lane of a wave wants is
                                     fetched once through the scalar cache: 1 = on, 2 = off (auto: on) */
 };

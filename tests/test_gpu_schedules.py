@@ -12,6 +12,7 @@ import pytest
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import test_gpu_parity as base  # noqa: E402
+import visionaray_amd as va  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -49,6 +50,8 @@ OPTIONS = ("ao_schedule", "refill_min", "vote_leaf", "wide_anyhit", "exact_minma
 
 @pytest.fixture(params=sorted(VARIANTS))
 def vctx(request, ctx):
+    if VARIANTS[request.param].get("coop_fetch") == 1 and not va.coop_fetch_available(ctx):
+        pytest.skip("cooperative fetch not compiled in (VRH_COOP=0, the default build)")
     for k, v in VARIANTS[request.param].items():
         ctx.set_option(k, v)
     yield ctx

@@ -1,4 +1,5 @@
 #!/bin/bash
+# Needs a build with the cooperative fetch compiled in: make -C visionaray_amd variant NAME=coop DEFS=-DVRH_COOP=1, then run with VRH_LIB=visionaray_amd/_lib/libvrh_coop.so (the default build has it off).
 # A/B of the cooperative pair fetch (VRH_OPT_COOP_FETCH) against the per-lane fetch, same process,
 # interleaved rounds: hf1M AO, hf1M primary, hf10M AO.  The full GPU test suite first.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1

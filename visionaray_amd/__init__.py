@@ -9,14 +9,14 @@ from .api import (BVH_NODE_DTYPE, DEGREES_TO_RADIANS, PLASTIC_DTYPE, POINT_LIGHT
                   TRIANGLE_DTYPE, Context, ao_kernel, build_index_bvh, camera, closest_hit_kernel, device_count,
                   face_normals, hip_buffer_rt, hit_mask, with_hit_mask, hip_index_bvh, hip_sched, index_bvh, make_sched_params,
                   load_obj, make_spheres, make_triangles, model, multi_hit_kernel, normals_per_face_binding, normals_per_vertex_binding, pixel_sampler,
-                  plastic, point_light, render, render_batch, sah_cost, shading, shard_bands, simple_kernel, unshard, whitted_kernel)
+                  coop_fetch_available, plastic, point_light, render, render_batch, sah_cost, shading, shard_bands, simple_kernel, unshard, whitted_kernel)
 from ._capi import VrhError
 
 __all__ = [
     "BVH_NODE_DTYPE", "DEGREES_TO_RADIANS", "SPHERE_DTYPE", "TRIANGLE_DTYPE", "Context", "VrhError", "ao_kernel",
     "build_index_bvh", "camera", "closest_hit_kernel", "device_count", "face_normals", "hip_buffer_rt",
     "hip_index_bvh", "hip_sched", "index_bvh", "make_sched_params", "make_spheres", "make_triangles",
-    "pixel_sampler", "render", "render_batch", "shard_bands", "unshard", "_capi", "PLASTIC_DTYPE", "POINT_LIGHT_DTYPE",
+    "pixel_sampler", "coop_fetch_available", "render", "render_batch", "shard_bands", "unshard", "_capi", "PLASTIC_DTYPE", "POINT_LIGHT_DTYPE",
     "normals_per_face_binding", "normals_per_vertex_binding", "plastic", "point_light", "shading", "simple_kernel",
     "multi_hit_kernel", "sah_cost", "hit_mask", "with_hit_mask", "load_obj", "model", "whitted_kernel",
 ]

@@ -29,6 +29,11 @@
 #ifndef VRH_SCALAR_UNIFORM
 #define VRH_SCALAR_UNIFORM 1   // wave-uniform pair fetches through the scalar cache (ray_step)
 #endif
+#ifndef VRH_COOP
+// 1: the cooperative pair fetch (VRH_OPT_COOP_FETCH) is compiled into the kernels.  Off by default:
+// measured slower, and its mere presence costs 0.5-2.5 % (profiles/r01_ab_nocoop.log)
+#define VRH_COOP 0
+#endif
 #ifndef VRH_PACKED_SLABS
 #define VRH_PACKED_SLABS 0   // 1: slab distances with v_pk_add_f32 / v_pk_mul_f32
 #endif
@@ -37,6 +42,7 @@ namespace vrh {
 namespace dev {
 
 constexpr bool SCALAR_UNIFORM = VRH_SCALAR_UNIFORM != 0;
+constexpr bool COOP_FETCH = VRH_COOP != 0;
 constexpr uint32_t LEAF_BIT = 0x80000000u;
 constexpr uint32_t END_BIT = 1u;
 constexpr int KIND_TRI = 0;

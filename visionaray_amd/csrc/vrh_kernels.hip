@@ -262,13 +262,13 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             const bool an = EPI == 3 ? any : false;
             // cooperative pair fetch: every lane takes part (quad exchanges), idle lanes included
             int rc_coop = 0;
-            if (P.coop)
+            if (COOP_FETCH && P.coop)
                 rc_coop = (P.fast_ok && __ballot(busy && !finite) == 0ull)
                     ? ray_step_coop<KIND, COUNT, true, UV, ML>(busy, P.pairs, P.prims, P.root, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, &hx, &mh, hm)
                     : ray_step_coop<KIND, COUNT, false, UV, ML>(busy, P.pairs, P.prims, P.root, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, &hx, &mh, hm);
             if (mode != IDLE)
             {
-                int rc = P.coop ? rc_coop : (P.fast_ok && __ballot(!finite) == 0ull)
+                int rc = (COOP_FETCH && P.coop) ? rc_coop : (P.fast_ok && __ballot(!finite) == 0ull)
                     ? ray_step<KIND, COUNT, true, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, &hx, &mh, hm)
                     : ray_step<KIND, COUNT, false, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, &hx, &mh, hm);
                 if constexpr (EPI == 3)
@@ -508,7 +508,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             }
             // 4. one traversal step for every busy lane (same code for both ray kinds)
             int rc = 0;
-            if (P.coop)
+            if (COOP_FETCH && P.coop)
             {
                 // cooperative pair fetch: every lane takes part (quad exchanges), idle lanes included
                 rc = (P.fast_ok && __ballot(busy && !finite) == 0ull)
@@ -672,7 +672,7 @@ __global__ __launch_bounds__(256, OCC) void ao_pass_kernel(render_params P)
         }
         if (__ballot(busy) == 0ull) break;        // every list exhausted, no ray in flight
         int rc = 0;
-        if (P.coop)
+        if (COOP_FETCH && P.coop)
         {
             rc = (P.fast_ok && __ballot(busy && !finite) == 0ull)
                 ? ray_step_coop<KIND, COUNT, true>(busy, P.pairs, P.prims, P.root, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm)

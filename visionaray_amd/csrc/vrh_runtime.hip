@@ -199,7 +199,14 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
     case VRH_OPT_AO_SCHEDULE: VRH_CHECK(value == 0 || (value >= 3 && value <= 6), "vrh_ctx_set_option: schedule is 3 (step), 4 (item), 5 (vote) or 6 (two-pass AO)"); ctx->opt_sched = int(value); break;
     case VRH_OPT_WIDE_ANYHIT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: wide any-hit is 1 (on) or 2 (off)"); ctx->opt_wide = int(value); break;
     case VRH_OPT_DESCENT_CAP: ctx->opt_dcap = int(value); break;
-    case VRH_OPT_COOP_FETCH: VRH_CHECK(value <= 2, "vrh_ctx_set_option: cooperative fetch is 1 (on) or 2 (off)"); ctx->opt_coop = int(value); break;
+    case VRH_OPT_COOP_FETCH:
+        VRH_CHECK(value <= 2, "vrh_ctx_set_option: cooperative fetch is 1 (on) or 2 (off)");
+        if (value == 1 && !dev::COOP_FETCH)
+        {
+            set_error("vrh_ctx_set_option: cooperative fetch not compiled in (build with -DVRH_COOP=1)");
+            return VRH_ERR_UNSUPPORTED;
+        }
+        ctx->opt_coop = int(value); break;
     case VRH_OPT_POP_ON_MISS: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pop on miss is 1 (on) or 2 (off)"); ctx->opt_pop = int(value); break;
     case VRH_OPT_SCALAR_FETCH: VRH_CHECK(value <= 2, "vrh_ctx_set_option: scalar fetch is 1 (on) or 2 (off)"); ctx->opt_scalar = int(value); break;
     case VRH_OPT_VOTE_LEAF: VRH_CHECK(value <= 64, "vrh_ctx_set_option: vote weight is 1..64"); ctx->opt_vote = int(value); break;
