@@ -224,8 +224,12 @@ enum vrh_option {
                                     together (one coalesced 64-B request per record) and transposes
                                     them with DPP: 1 = on, 2 = off (auto: off; 1 needs a build
                                     with -DVRH_COOP=1, else VRH_ERR_UNSUPPORTED)                  */
-    VRH_OPT_SCALAR_FETCH = 14    /* step loop: a pair record every active lane of a wave wants is
+    VRH_OPT_SCALAR_FETCH = 14,   /* step loop: a pair record every active lane of a wave wants is
                                     fetched once through the scalar cache: 1 = on, 2 = off (auto: on) */
+    VRH_OPT_PAIR_LAYOUT = 15,    /* scene upload (read by vrh_scene_upload): 1 = node pairs in
+                                    depth-first preorder, a pair's child-0 pair next to it in one
+                                    128-B line; 2 = the builder's order (auto: 2; 1 measured
+                                    neutral)                                                      */
 };
 VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value);
 

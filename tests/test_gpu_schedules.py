@@ -43,9 +43,11 @@ VARIANTS = {
     # the primary-visibility defaults switched off (pop on miss, descent cap 8, item refill 32)
     "no_pop_uncapped": {"pop_on_miss": 2, "descent_cap": 1024, "refill_min": 16},
     "pop_cap10": {"pop_on_miss": 1, "descent_cap": 10},
+    # scenes uploaded with the line-paired record layout (the option is read at upload)
+    "pair_layout": {"pair_layout": 1},
 }
 OPTIONS = ("ao_schedule", "refill_min", "vote_leaf", "wide_anyhit", "exact_minmax", "descent_cap", "xcd_queues",
-           "pop_on_miss", "coop_fetch", "scalar_fetch", "waves_per_simd")
+           "pop_on_miss", "coop_fetch", "scalar_fetch", "waves_per_simd", "pair_layout")
 
 
 @pytest.fixture(params=sorted(VARIANTS))

@@ -161,7 +161,8 @@ class Context:
                  "xcd_queues": capi.VRH_OPT_XCD_QUEUES, "refill_min": capi.VRH_OPT_REFILL_MIN,
                  "vote_leaf": capi.VRH_OPT_VOTE_LEAF, "wide_anyhit": capi.VRH_OPT_WIDE_ANYHIT,
                  "descent_cap": capi.VRH_OPT_DESCENT_CAP, "pop_on_miss": capi.VRH_OPT_POP_ON_MISS,
-                 "coop_fetch": capi.VRH_OPT_COOP_FETCH, "scalar_fetch": capi.VRH_OPT_SCALAR_FETCH}
+                 "coop_fetch": capi.VRH_OPT_COOP_FETCH, "scalar_fetch": capi.VRH_OPT_SCALAR_FETCH,
+                 "pair_layout": capi.VRH_OPT_PAIR_LAYOUT}
         capi.check("vrh_ctx_set_option", self.handle, names.get(option, option), int(value))
 
     def last_frame_stats(self):

@@ -56,7 +56,7 @@ struct vrh_ctx
     vrh_frame_stats last{};
     bool have_frame = false;
     // tuning options (0 = automatic), vrh_ctx_set_option
-    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_vote = 0, opt_dcap = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0, opt_pop = 0, opt_coop = 0, opt_scalar = 0;
+    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_vote = 0, opt_dcap = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0, opt_pop = 0, opt_coop = 0, opt_scalar = 0, opt_layout = 0;
     // two-pass AO scratch (grown on demand): 32-B hit records and one byte per AO ray, per pixel slot
     float4* hitrec = nullptr;
     uint8_t* aobits = nullptr;
@@ -208,6 +208,7 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
         }
         ctx->opt_coop = int(value); break;
     case VRH_OPT_POP_ON_MISS: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pop on miss is 1 (on) or 2 (off)"); ctx->opt_pop = int(value); break;
+    case VRH_OPT_PAIR_LAYOUT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pair layout is 1 (line pairing) or 2 (builder order)"); ctx->opt_layout = int(value); break;
     case VRH_OPT_SCALAR_FETCH: VRH_CHECK(value <= 2, "vrh_ctx_set_option: scalar fetch is 1 (on) or 2 (off)"); ctx->opt_scalar = int(value); break;
     case VRH_OPT_VOTE_LEAF: VRH_CHECK(value <= 64, "vrh_ctx_set_option: vote weight is 1..64"); ctx->opt_vote = int(value); break;
     case VRH_OPT_REFILL_MIN: VRH_CHECK(value <= 64, "vrh_ctx_set_option: refill threshold is 1..64"); ctx->opt_refill = int(value); break;
@@ -287,6 +288,42 @@ VRH_API int vrh_scene_upload(vrh_ctx* ctx, const void* nodes_v, uint32_t num_nod
                     st.push_back({ w[c], e.second + 1 });
                 }
         }
+    }
+
+    // -- cache-line pairing (VRH_OPT_PAIR_LAYOUT = 1; auto off: measured neutral, within 1.3 %,
+    // profiles/r01_ab_layout.log): re-lay the pair records in a depth-first
+    // preorder that puts each pair's child-0 pair right after it, so a parent and a child share a
+    // 128-B line on half of the descent steps (31 % in the builder's order).  Links are renumbered;
+    // the tree, the traversal order and every result are unchanged.
+    if (ctx->opt_layout == 1 && npairs > 1 && !(root & 0x80000000u))
+    {
+        std::vector<uint32_t> perm(npairs, 0xFFFFFFFFu);
+        uint32_t next = 0;
+        std::vector<uint32_t> st{ root };
+        while (!st.empty())
+        {
+            const uint32_t k = st.back(); st.pop_back();
+            perm[k] = next++;
+            uint32_t w[4];
+            std::memcpy(w, &pairs[4 * k + 3], 16);
+            if (!(w[1] & 0x80000000u)) st.push_back(w[1]);
+            if (!(w[0] & 0x80000000u)) st.push_back(w[0]);
+        }
+        for (uint32_t k = 0; k < npairs; ++k)
+            if (perm[k] == 0xFFFFFFFFu) perm[k] = next++;      // unreachable records keep a slot
+        std::vector<float4> np(pairs.size());
+        for (uint32_t k = 0; k < npairs; ++k)
+        {
+            float4* d = &np[4 * size_t(perm[k])];
+            std::memcpy(d, &pairs[4 * size_t(k)], 64);
+            uint32_t w[4];
+            std::memcpy(w, &d[3], 16);
+            for (int c = 0; c < 2; ++c)
+                if (!(w[c] & 0x80000000u)) w[c] = perm[w[c]];
+            std::memcpy(&d[3], w, 16);
+        }
+        pairs.swap(np);
+        root = perm[root];
     }
 
     // -- leaf-ordered primitives with END flags
