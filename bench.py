@@ -9,29 +9,41 @@ A "step" is one frame.  Inputs (BVH, primitives, normals) are resident in HBM be
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Frames in flight (default F = 8): every persistent launch renders F frames (vrh_render_batch),
-their tiles interleaved in the work queues, so no wave idles while the last tiles of a frame finish
--- the kernel-level tail is paid once per F frames.  Every frame is fully traced and written; the
-last timed frames are checked against a separately rendered frame (frames_match_1gpu_frame).
+Frames: every frame has its own frame number (vrh_render's frame_num -> its own AO sample set,
+as the reference reseeds per frame, cuda_sched.inl:38-45, 79): the W warm-up frames are numbers
+1..W, the K timed frames W+1..W+K; frame 0 and frame 3 are rendered once, untimed, and checked
+against the reference's fixtures (tests/golden).
 
-N > 1: one process per GPU; the image is sharded by 8-row bands (band b -> rank b % N, SURVEY.md
-§8e), each rank renders its packed shard of every frame, and the framebuffers are gathered to rank
-0 over RCCL (torch.distributed "nccl"; prim ids + AO masks, 5 B/pixel, one gather per launch) and
-un-interleaved there with the RGBA32F colour re-derived exactly (vrh_unshard).  Two launches are in
-flight: launch k renders while launch k-1's gather runs on RCCL's stream; the last launch's gather
-and un-interleave finish inside the timed region, so K steps = K complete frames on rank 0.  Total
-work (K frames) is fixed as N grows, so scaling is strong.
+Frames in flight: the K timed frames run as K / F persistent launches of F frames each
+(vrh_render_batch; F = the largest divisor of K not above --frames-in-flight), so the kernel's
+tail is paid once per launch.  `value` is K frames' rays over the wall time of the timed region.
+The hip_sched::frame path -- one synchronous launch per frame, as the reference's scheduler
+issues frames -- is measured separately over --single-frames frames (median): single_frame_*.
 
-Rank 0 prints one JSON line (contract in the task statement) with the roofline of the traversal
-kernel (algorithmic bytes per SURVEY.md §8d from a counting pass, over the hipEvent kernel time of
-the timed frames) and the CPU baseline (the reference's own SSE4 tiled_sched path, oracle/_ref,
-timed on this host on a bounded sample).
+N > 1: one process per GPU, one libvrh render group over RCCL (vrh_group_join, the id broadcast
+by torch.distributed): each rank renders its image-tile shard (8-row bands, band b -> rank b % N,
+SURVEY.md §8e) of every frame and libvrh gathers the packed shards to rank 0 with ncclSend /
+ncclRecv on its own stream and un-interleaves them there (vrh_render_sharded).  K frames are
+fixed as N grows: scaling "strong".
+
+Rank 0 prints one JSON line (the contract of the task statement) with:
+  * roofline: the unit that binds the traversal kernel is the vector-memory path (L1 / TA / TD;
+    PMC: profiles/r02_pmc/), so `achieved` is the kernel's L1 line traffic -- distinct 128-B lines
+    per wave-level load / store (the coalescer model of the counting variant, vrh_frame_stats
+    l1_lines, cross-checked against rocprofv3 TCP_TOTAL_CACHE_ACCESSES) x 128 B per launch over
+    the hipEvent launch time -- and `peak` the same quantity measured on the access-shape
+    microbenchmark (tools/micro/l1_roof.hip -> profiles/l1_roof.json).  The SURVEY §8d
+    algorithmic HBM bytes are kept as roofline.hbm_algorithmic (informational);
+  * cpu_baseline: the reference's own SSE4 tiled_sched path (oracle/_ref, built from
+    /root/reference by oracle/Makefile) on a bounded sample, with the host's core count and model.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
+import statistics
 import subprocess
 import sys
 import time
@@ -42,23 +54,42 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
 TRI_BYTES, SPHERE_BYTES, INDEX_BYTES, NODE_BYTES = 64, 48, 4, 32
 OUT_BYTES_PRIMARY = 24          # RGBA32F + u32 prim_id + f32 t per primary ray
+L1_LINE_BYTES = 128
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=64, help="timed frames (default: two 32-frame launches)")
-    ap.add_argument("--warmup", type=int, default=32, help="untimed frames (default: one launch)")
+    ap.add_argument("--steps", type=int, default=64, help="timed frames")
+    ap.add_argument("--warmup", type=int, default=32, help="untimed frames before the timed region")
     ap.add_argument("--scene", default="hf1M", help="hf1M (C3, default) | hf10M (C4) | sph1M (C5)")
     ap.add_argument("--kernel", default=None, choices=["ao", "primary"], help="default: ao for triangles")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16, help="host cores for the CPU baseline")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="nccl (= RCCL, the measured path) | gloo (host-staged; single-GPU rehearsal only)")
-    ap.add_argument("--no-verify", action="store_true", help="skip the untimed check of the last frames against a 1-GPU frame")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline")
+    ap.add_argument("--no-verify", action="store_true", help="skip the untimed checks against the fixtures")
     ap.add_argument("--frames-in-flight", type=int, default=32,
-                    help="frames per persistent launch (vrh_render_batch, 1..32); every frame is still fully traced")
+                    help="max frames per persistent launch (vrh_render_batch, 1..32)")
+    ap.add_argument("--single-frames", type=int, default=10, help="frames of the hip_sched::frame leg (median)")
+    ap.add_argument("--shards", type=int, default=0,
+                    help="image-tile shards of the render group (0 = one per rank); > ranks: a rank renders several")
     return ap.parse_args()
+
+
+def host_info():
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    return {"cpu_model": model, "host_cpus": os.cpu_count(), "cpus_available": avail}
 
 
 def cpu_baseline(scene, kernel, threads):
@@ -66,6 +97,7 @@ def cpu_baseline(scene, kernel, threads):
     the same scene and camera at full resolution, 1 warm-up + 3 timed frames (~2-10 s)."""
     from oracle import oracle as O
     samples = 8 if kernel == "ao" else 0
+    info = host_info()
     if os.path.exists(O.REF_BENCH_BIN):
         print(f"cpu baseline: reference tiled_sched, {threads} threads ...", file=sys.stderr, flush=True)
         try:
@@ -76,7 +108,8 @@ def cpu_baseline(scene, kernel, threads):
             r = O.ref_bench(scene, threads, 3, 1920, 1080, samples, timeout=150)
         return {"value": round(r["mrays_per_s"], 3), "unit": "Mrays/s", "cores": threads, "kind": "reference",
                 "sample": f"{scene} 1920x1080, {samples} AO spp, tiled_sched<basic_ray<simd::float4>> -O3 -msse4.1, "
-                          f"median of 3 frames after 1 warm-up ({r['rays_per_frame']} rays/frame)"}
+                          f"{threads} worker threads, median of 3 frames after 1 warm-up ({r['rays_per_frame']} rays/frame)",
+                **info}
     # fallback: the plain-C restatement (scalar, OpenMP rows) on 1/8 of the image rows
     sc = O.make_scene(scene)
     cam = O.scene_camera(scene)
@@ -87,7 +120,22 @@ def cpu_baseline(scene, kernel, threads):
     out = O.render(sc, cam, mode=mode, rows=rows, threads=threads)
     dt = time.perf_counter() - t0
     return {"value": round(out["rays"] / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{scene} rows {rows[0]}-{rows[1]} of 1920x1080 ({out['rays']} rays), scalar C restatement"}
+            "sample": f"{scene} rows {rows[0]}-{rows[1]} of 1920x1080 ({out['rays']} rays), scalar C restatement",
+            **info}
+
+
+def frames_per_launch(steps, cap):
+    """The largest divisor of `steps` that is <= cap (every timed launch has the same size)."""
+    cap = max(1, min(cap, 32))
+    return max(d for d in range(1, cap + 1) if steps % d == 0)
+
+
+def load_json(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
 
 
 def main():
@@ -98,7 +146,8 @@ def main():
     if world != args.gpus:
         print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}; using WORLD_SIZE", file=sys.stderr)
 
-    # torch first: its HIP runtime is then the one libvrh.so binds to (one runtime per process)
+    # torch first: its HIP runtime (and RCCL) is then the one libvrh.so binds to (one per process)
+    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -106,13 +155,10 @@ def main():
     from visionaray_amd import _capi, scenes
 
     ndev = torch.cuda.device_count()
-    torch.cuda.set_device(local % max(ndev, 1))   # ranks > devices only in single-GPU rehearsals
     local = local % max(ndev, 1)
+    torch.cuda.set_device(local)
     if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     kernel = args.kernel or ("ao" if not args.scene.startswith("sph") else "primary")
 
@@ -123,172 +169,149 @@ def main():
             cpu = cpu_baseline(args.scene, kernel, args.cpu_threads)
         except Exception as e:  # reported, never fatal for the GPU measurement
             cpu = {"value": None, "unit": "Mrays/s", "cores": args.cpu_threads, "kind": "reference",
-                   "sample": f"failed: {e}"}
+                   "sample": f"failed: {e}", **host_info()}
 
     # ---- scene: host build, upload (excluded from timing) --------------------------------------
     t0 = time.perf_counter()
     prims = scenes.primitives(args.scene)
     host = va.build_index_bvh(prims)
     build_s = time.perf_counter() - t0
-    # one explicit stream shared by libvrh launches and torch/RCCL, so render -> gather -> unshard
-    # are ordered on the device without host syncs
-    stream = torch.cuda.Stream()
-    torch.cuda.set_stream(stream)
-    ctx = va.Context(local, stream=stream.cuda_stream)
+    ctx = va.Context(local)
     dev = va.hip_index_bvh(ctx, host, scenes.normals_for(prims))
     cam, W, H = scenes.scene_camera(args.scene)
     basis = cam.basis(W, H)
-    kern = va.ao_kernel(dev) if kernel == "ao" else va.closest_hit_kernel(dev)
-    kern_count = va.ao_kernel(dev, count_tests=True) if kernel == "ao" else va.closest_hit_kernel(dev, count_tests=True)
+    mk = va.ao_kernel if kernel == "ao" else va.closest_hit_kernel
+    kern, kern_count = mk(dev), mk(dev, count_tests=True)
+    rays_key = "rays"
 
-    # ---- frames in flight: every launch renders up to F frames (vrh_render_batch) -------------
-    F = max(1, min(args.frames_in_flight, _capi.VRH_MAX_BATCH))
+    F = frames_per_launch(args.steps, args.frames_in_flight)
+    launches = args.steps // F
 
-    def batches(k):
-        return [F] * (k // F) + ([k % F] if k % F else [])
-
-    # ---- framebuffers: full image on rank 0, packed shard per rank for N > 1 ------------------
-    # Each rank writes its bands' prim ids and AO masks into ONE buffer per batch
-    # [u32 prim ids of b frames | u8 masks of b frames] (5 B/pixel); one RCCL gather per batch moves
-    # it to rank 0, which un-interleaves every frame and re-derives the RGBA32F colour exactly
-    # (vrh_unshard) -- the full framebuffer (RGBA32F + prim ids) of every frame on rank 0.
-    rows_max = _capi.VRH_BAND_ROWS * va.shard_bands(H, 0, world)
-    n1 = rows_max * W                         # pixels of one frame's packed shard
-    shard = _capi.vrh_shard(rank, world, 1, 0) if world > 1 else None
-    nslots = 2                                # batch k renders while batch k - 1's gather runs
-    bufs = {}                                 # batch size -> buffers
-
-    def buffers(b):
-        if b in bufs:
-            return bufs[b]
-        if world == 1:
-            bufs[b] = {"rt": va.hip_buffer_rt(ctx, W, H * b)}
-            return bufs[b]
-        nb = n1 * b
-        locs = [torch.empty((5 * nb,), dtype=torch.uint8, device="cuda") for _ in range(nslots)]
-        d = {"locs": locs,
-             "rts": [va.hip_buffer_rt(ctx, W, rows_max * b, wrap=(0, x.data_ptr(), 0, x.data_ptr() + 4 * nb))
-                     for x in locs]}
+    # ---- render paths -----------------------------------------------------------------------
+    group = None
+    if world > 1:
+        # the group id travels over torch.distributed once; the data path is libvrh + RCCL
+        uid = torch.zeros(va.GROUP_ID_BYTES, dtype=torch.uint8, device="cuda")
         if rank == 0:
-            d["gathered"] = [torch.empty((world, 5 * nb), dtype=torch.uint8, device="cuda") for _ in range(nslots)]
-        bufs[b] = d
-        return d
+            uid.copy_(torch.frombuffer(bytearray(va.render_group.unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, 0)
+        group = va.render_group(ctx, world, rank, bytes(uid.cpu().numpy().tobytes()))
+    full_rts = {}
 
-    fulls = []
-    if world > 1 and rank == 0:
-        fulls = [va.hip_buffer_rt(ctx, W, H, flags=_capi.VRH_RT_COLOR | _capi.VRH_RT_PRIM_ID | _capi.VRH_RT_OCC)
-                 for _ in range(F)]
+    def target(b):
+        """Full-image target of b frames (rank 0; every rank for N = 1)."""
+        if b not in full_rts:
+            flags = _capi.VRH_RT_ALL if world == 1 else _capi.VRH_RT_COLOR | _capi.VRH_RT_PRIM_ID | _capi.VRH_RT_OCC
+            full_rts[b] = va.hip_buffer_rt(ctx, W, H * b, flags=flags) if (world == 1 or rank == 0) else None
+        return full_rts[b]
 
-    def gather(b, slot):
-        d = bufs[b]
-        loc = d["locs"][slot]
-        if args.dist_backend == "nccl":
-            if rank == 0:
-                return dist.gather(loc, gather_list=list(d["gathered"][slot].unbind(0)), dst=0, async_op=True)
-            return dist.gather(loc, dst=0, async_op=True)
-        # gloo rehearsal: stage through host memory, synchronously
-        torch.cuda.synchronize()
-        host = loc.cpu()
-        if rank == 0:
-            hg = torch.empty((world, host.numel()), dtype=torch.uint8)
-            dist.gather(host, gather_list=list(hg.unbind(0)), dst=0)
-            d["gathered"][slot].copy_(hg)
-        else:
-            dist.gather(host, dst=0)
-        return None
-
-    pending = []          # (work, batch size, slot) of gathers not yet waited for, oldest first
-
-    def finish_one():
-        work, b, slot = pending.pop(0)
-        if work is not None:
-            work.wait()   # the compute stream waits for the gather; the host does not block
-        if rank == 0:
-            g = bufs[b]["gathered"][slot].data_ptr()
-            nb = n1 * b
-            for f in range(b):
-                va.unshard(ctx, W, H, world, fulls[f], prim_id_ptr=g + 4 * f * n1, occ_ptr=g + 4 * nb + f * n1,
-                           shard_stride_bytes=5 * nb, kernel=kern)
-
-    launch = [0]
+    next_frame = [1]
 
     def run_batch(b):
-        d = buffers(b)
+        fn = next_frame[0]
+        next_frame[0] += b
         if world == 1:
-            va.render_batch(ctx, dev, d["rt"], [basis] * b, kern, None)
-            return
-        slot = launch[0] % nslots
-        launch[0] += 1
-        # the slot's previous gather must be done before it is overwritten
-        while any(pb == b and ps == slot for _, pb, ps in pending) or len(pending) >= nslots:
-            finish_one()
-        va.render_batch(ctx, dev, d["rts"][slot], [basis] * b, kern, shard)
-        pending.append((gather(b, slot), b, slot))
+            va.render_batch(ctx, dev, target(b), [basis] * b, kern, None, frame_num=fn)
+        else:
+            group.render(dev, kern, target(b), [basis] * b, frame_num=fn, shards=args.shards)
+        return fn
 
-    def drain():
-        while pending:
-            finish_one()
+    def sync():
+        if group is not None:
+            group.sync()
+        ctx.sync()
 
     def barrier():
+        sync()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
-    # ---- counting pass (untimed, one frame): box / primitive tests per ray ----------------------
-    one_rows = rows_max if world > 1 else H
-    rt_one = va.hip_buffer_rt(ctx, W, one_rows)
-    va.render(ctx, dev, rt_one, basis, kern_count, shard)
+    # ---- counting pass (untimed, one frame on rank 0's whole image): tests and L1 lines per ray --
+    rt_one = va.hip_buffer_rt(ctx, W, H)
+    va.render(ctx, dev, rt_one, basis, kern_count, None, frame_num=0)
     cstats = ctx.last_frame_stats()
 
-    # ---- reference frame for the check below (rank 0, untimed): one vrh_render of the whole image
-    # on another traversal schedule (the item loop; the step loop for sphere scenes, whose default
-    # is the item loop) -- an independent code path, and a different kernel in the rocprof summary,
-    # so every launch of the measured kernel is an F-frame launch
-    ref = None
+    # ---- fixtures: frame 0 and frame 3 against the reference's outputs (untimed) ---------------
+    verify = {}
     if not args.no_verify and rank == 0:
-        ctx.set_option("ao_schedule", 3 if args.scene.startswith("sph") else 4)
-        ref_rt = va.hip_buffer_rt(ctx, W, H)
-        va.render(ctx, dev, ref_rt, basis, kern, None)
-        ref = ref_rt.download(t=False)
-        ref_rt.close()
-        ctx.set_option("ao_schedule", 0)
+        golden = load_json(os.path.join(ROOT, "tests", "golden", "golden.json")) or {}
+        for case, fnum in ((args.scene, 0), (f"frame3_{args.scene}", 3)):
+            g = golden.get(case)
+            path = os.path.join(ROOT, "tests", "golden", case + ".npz")
+            if not g or not os.path.exists(path) or (kernel == "ao") != (g.get("ao_rays", 0) > 0):
+                continue
+            va.render(ctx, dev, rt_one, basis, kern, None, frame_num=fnum)
+            out = rt_one.download()
+            ref = np.load(path)
+            pix = ref["pixels"]
+            ok = all(np.array_equal(out[k][pix].view(np.uint8), ref[k].view(np.uint8))
+                     for k in ("prim_id", "t", "occ", "color") if k in ref)
+            verify[f"frame{fnum}_matches_reference_sample"] = bool(ok)
+    rt_one.close()
 
-    for b in batches(args.warmup):
-        run_batch(b)
-    # every buffer the timed batches use (each batch size, each in-flight slot) is written once
-    # before timing, whatever --warmup is
-    for b in sorted(set(batches(args.steps))):
-        for _ in range(nslots if world > 1 else 1):
-            run_batch(b)
-    drain()
+    # ---- warm-up, then every timed batch size is run once so first-touch costs stay out ----------
+    for _ in range(args.warmup // F):
+        run_batch(F)
+    for _ in range(args.warmup % F):
+        run_batch(1)
+    run_batch(F)
     barrier()
     ctx.stats_reset()
     barrier()
+    first_timed = next_frame[0]
     t0 = time.perf_counter()
-    for b in batches(args.steps):
-        run_batch(b)
-    drain()               # the last batch's gather and un-interleave are inside the timed region
+    for _ in range(launches):
+        run_batch(F)
     barrier()
     elapsed = time.perf_counter() - t0
     acc = ctx.accum_stats()
-    last_b = batches(args.steps)[-1]
 
-    # ---- the timed frames are right: N > 1 gathered frames (rank 0) equal a 1-GPU frame ---------
-    verified = None
-    if ref is not None:
-        b = ref
-        if world > 1:
-            outs = [fulls[f].download(t=False) for f in range(last_b)]
-        else:
-            a = bufs[last_b]["rt"].download(t=False)
-            outs = [{k: v[f * W * H:(f + 1) * W * H] for k, v in a.items()} for f in range(last_b)]
-        verified = bool(all((o[k].view("u1") == b[k].view("u1")).all() for o in outs for k in ("color", "prim_id", "occ")))
+    # ---- the timed frames are distinct and correct: the last launch's first and last frame equal
+    # their own single-frame render (rank 0, untimed)
+    if not args.no_verify and rank == 0:
+        last = target(F).download(t=False)
+        n = W * H
+        one = va.hip_buffer_rt(ctx, W, H)
+        ok = True
+        last_fn = first_timed + (launches - 1) * F
+        for f in sorted({0, F - 1}):
+            va.render(ctx, dev, one, basis, kern, None, frame_num=last_fn + f)
+            single = one.download(t=False)
+            ok &= all(np.array_equal(last[k][f * n:(f + 1) * n].view(np.uint8), single[k].view(np.uint8))
+                      for k in ("color", "prim_id", "occ") if k in last)
+        verify["timed_frames_match_single_frame_renders"] = bool(ok)
+        if kernel == "ao" and F > 1:
+            verify["timed_frames_distinct"] = not np.array_equal(last["occ"][:n], last["occ"][(F - 1) * n:F * n])
+        one.close()
     barrier()
 
+    # ---- hip_sched::frame leg: one synchronous launch per frame (rank 0, N = 1) ---------------------
+    single = None
+    if world == 1 and args.single_frames > 0:
+        rt_s = va.hip_buffer_rt(ctx, W, H)
+        sched = va.hip_sched(ctx)
+        sp = va.make_sched_params(va.pixel_sampler.uniform_type, cam, rt_s)
+        k_ms, wall_ms, rays = [], [], []
+        sched.frame(kern, sp, frame_num=next_frame[0])     # warm-up of this launch shape
+        for i in range(args.single_frames):
+            t1 = time.perf_counter()
+            sched.frame(kern, sp, frame_num=next_frame[0] + 1 + i)
+            wall_ms.append((time.perf_counter() - t1) * 1e3)
+            st = ctx.last_frame_stats()
+            k_ms.append(st["kernel_ms"])
+            rays.append(st["rays"])
+        rpf = statistics.median(rays)
+        single = {"frames": args.single_frames, "kernel_ms_median": round(statistics.median(k_ms), 4),
+                  "wall_ms_median": round(statistics.median(wall_ms), 4),
+                  "mrays_kernel": round(rpf / statistics.median(k_ms) / 1e3, 3),
+                  "mrays_wall": round(rpf / statistics.median(wall_ms) / 1e3, 3),
+                  "path": "hip_sched::frame -> vrh_render + vrh_sync (one launch per frame)"}
+        rt_s.close()
+
     # ---- aggregate over ranks -------------------------------------------------------------------
-    local_vals = torch.tensor([elapsed, float(acc["rays"]), acc["kernel_ms_total"], float(acc["timed_frames"]),
-                               float(cstats["box_tests"]), float(cstats["prim_tests"]), float(cstats["rays"]),
-                               float(cstats["hits"])], dtype=torch.float64, device="cuda")
+    local_vals = torch.tensor([elapsed, float(acc[rays_key]), acc["kernel_ms_total"], float(acc["timed_frames"])],
+                              dtype=torch.float64, device="cuda")
     if world > 1:
         mx = local_vals.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -301,46 +324,24 @@ def main():
     mrays = total_rays / t_max / 1e6
 
     if rank == 0:
-        # algorithmic bytes: 32 B per box test (a 64-B child pair per inner visit),
-        # (S_prim + 4 index) B per primitive test, 24 B of output per primary ray
         s_prim = TRI_BYTES if args.scene.startswith("hf") or args.scene == "cornell12" else SPHERE_BYTES
-        n_box, n_prim, n_rays = float(sm[4]), float(sm[5]), float(sm[6])
-        primary_rays = W * H
-        bytes_frame = NODE_BYTES * n_box + (s_prim + INDEX_BYTES) * n_prim + OUT_BYTES_PRIMARY * primary_rays
+        n_box, n_prim, n_rays = float(cstats["box_tests"]), float(cstats["prim_tests"]), float(cstats["rays"])
+        bytes_frame = NODE_BYTES * n_box + (s_prim + INDEX_BYTES) * n_prim + OUT_BYTES_PRIMARY * W * H
         bytes_per_ray = bytes_frame / n_rays
-        # dominant kernel = the traversal kernel; per-launch (F frames) algorithmic bytes over its mean
-        # hipEvent time
-        k_ms_mean = float(local_vals[2]) / max(float(local_vals[3]), 1.0)    # rank 0's launches
-        local_bytes = bytes_per_ray * float(acc["rays"]) / max(float(acc["timed_frames"]), 1.0)
-        achieved = local_bytes / (k_ms_mean * 1e-3) / 1e9
+        # the dominant kernel: rank 0's traversal launches of the timed region (F frames each)
+        k_ms_mean = float(local_vals[2]) / max(float(local_vals[3]), 1.0)
+        rays_launch = float(acc[rays_key]) / max(float(acc["timed_frames"]), 1.0)
+        frame_share = rays_launch / n_rays                      # frames per launch on this rank (N > 1: a shard)
+        roof = load_json(os.path.join(ROOT, "profiles", "l1_roof.json"))
+        lines_launch = float(cstats["l1_lines"]) * frame_share
+        achieved = lines_launch * L1_LINE_BYTES / (k_ms_mean * 1e-3) / 1e9
+        peak = roof.get("peak_gbs") if roof else None
+        hbm_alg = bytes_per_ray * rays_launch / (k_ms_mean * 1e-3) / 1e9
+        pmc = load_json(os.path.join(ROOT, "profiles", "pmc_traffic.json")) or {}
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            try:
-                with open(pmc) as f:
-                    pm = json.load(f)
-                if (pm.get("scene") == args.scene and pm.get("kernel") == kernel and pm.get("gpus") == 1 and world == 1
-                        and pm.get("frames_per_launch", 1) == F):
-                    traffic = pm.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        # what actually limits the kernel (PMC, tools/profile_mem.sh): busy fractions of the
-        # vector-memory address (TA) and data (TD) units, when measured for this configuration
-        limiter = None
-        pmm = os.path.join(ROOT, "profiles", "pmc_mem.json")
-        if os.path.exists(pmm) and world == 1:
-            try:
-                with open(pmm) as f:
-                    pm = json.load(f)
-                if pm.get("scene") == args.scene and pm.get("kernel") == kernel and pm.get("frames_per_launch") == F:
-                    limiter = {"unit": "vector-memory pipeline (L1 / TA address / TD data)",
-                               "td_busy": round(pm["td_busy_frac"], 3), "ta_busy": round(pm["ta_busy_frac"], 3),
-                               "l1_hit": round(1.0 - pm["l1_to_l2_reads_per_access"], 3),
-                               "td_stalled_on_l1": (round(pm["td_stalled_on_l1_frac"], 3)
-                                                    if pm.get("td_stalled_on_l1_frac") is not None else None),
-                               "source": "profiles/pmc_mem.json (rocprofv3 --pmc, same workload)"}
-            except Exception:
-                limiter = None
+        if (pmc.get("scene") == args.scene and pmc.get("kernel") == kernel and world == 1
+                and pmc.get("frames_per_launch") == F):
+            traffic = pmc.get("hbm_bytes_per_launch")
         line = {
             "metric": "Mrays/s (primary + 8-sample AO)" if kernel == "ao" else "Mrays/s (primary)",
             "value": round(mrays, 3),
@@ -353,31 +354,49 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (SURVEY.md Appendix A procedural scene, deterministic)",
+            "data": "synthetic (SURVEY.md Appendix A procedural scene, deterministic; frame numbers 1.. give distinct AO samples)",
             "config": {
                 "workload": f"{args.scene} {W}x{H} 1 spp primary" + (" + 8 AO any-hit rays/hit (r=0.1)" if kernel == "ao" else ""),
                 "scene": args.scene, "primitives": int(len(prims)), "bvh_nodes": int(len(host.nodes)),
                 "width": W, "height": H, "ao_samples": 8 if kernel == "ao" else 0,
-                "rays_per_frame": int(n_rays), "parallelism": f"image-tile shard x{world}" + (" + RCCL gather" if world > 1 else ""),
+                "rays_per_frame": int(n_rays),
+                "parallelism": f"image-tile shard x{world}" + (" + RCCL gather (libvrh render group)" if world > 1 else ""),
+                "frames_per_launch": F, "launches": launches,
+                "frame_numbers": [first_timed, first_timed + args.steps - 1],
             },
             "roofline": {
-                "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "render_unified_kernel (traversal)", "kernel_ms_mean": round(k_ms_mean, 4),
-                "frames_per_launch": F, "kernel_ms_per_frame": round(float(local_vals[2]) / args.steps, 4),
-                "bytes_per_ray": round(bytes_per_ray, 1), "box_tests_per_ray": round(n_box / n_rays, 3),
-                "prim_tests_per_ray": round(n_prim / n_rays, 3),
-                "measured_limiter": limiter,
+                "bound": "l1", "unit": "GB/s",
+                "achieved": round(achieved, 1), "peak": peak,
+                "frac": round(achieved / peak, 4) if peak else None,
+                "traffic": traffic,
+                "what": "vector-L1 line traffic (distinct 128-B lines per wave-level load/store x 128 B) of the "
+                        "traversal launch over its hipEvent time; peak = the same on tools/micro/l1_roof.hip's "
+                        "per-lane dependent 64-B gathers (profiles/l1_roof.json)",
+                "kernel": "render_unified_kernel (traversal, frames in flight)" if F > 1 else "render_unified_kernel",
+                "kernel_ms_mean": round(k_ms_mean, 4), "frames_per_launch": F,
+                "kernel_ms_per_frame": round(k_ms_mean / F, 4),
+                "l1_lines_per_launch": round(lines_launch),
+                "l1_lines_per_ray": round(float(cstats["l1_lines"]) / n_rays, 3),
+                "l1_lines_per_vmem_instr": round(float(cstats["l1_lines"]) / max(float(cstats["vmem_instrs"]), 1.0), 3),
+                "roof_source": roof.get("source") if roof else None,
+                "hbm_algorithmic": {
+                    "bytes_per_ray": round(bytes_per_ray, 1), "box_tests_per_ray": round(n_box / n_rays, 3),
+                    "prim_tests_per_ray": round(n_prim / n_rays, 3), "achieved_gbs": round(hbm_alg, 1),
+                    "frac_of_8tbs": round(hbm_alg / HBM_PEAK_GBS, 4),
+                    "note": "SURVEY.md §8d algorithmic bytes; the scene lives in L2 / Infinity Cache, so this is not "
+                            "HBM traffic (that is `traffic`)"},
             },
+            "single_frame": single,
+            "single_frame_mrays": single["mrays_kernel"] if single else None,
             "cpu_baseline": cpu,
             "host_build_s": round(build_s, 3),
-            "frames_in_flight": F,
-            "frames_match_1gpu_frame": verified,
+            "verify": verify,
         }
         print(json.dumps(line), flush=True)
 
     if world > 1:
-        dist.barrier()
+        barrier()
+        group.close()
         dist.destroy_process_group()
 
 

@@ -3,7 +3,10 @@
 // host, upload (hip_index_bvh), render one AO frame with hip_sched, print FNV-1a hashes of the
 // integer outputs as JSON (compared against tests/golden by tests/test_cpp_api.py).
 //
-//     ao_hip [grid] [width] [height] [frames]
+//     ao_hip [grid] [width] [height] [frames] [frame_num]
+//
+// Every frame is rendered with frame number frame_num (default 0: the parity frame of SURVEY.md
+// Appendix A); ao/main.cpp passes ++frame_num instead, which gives every frame its own AO samples.
 #include <visionaray_hip/standalone.h>
 
 #include <chrono>
@@ -28,6 +31,7 @@ int main(int argc, char** argv)
     unsigned W = argc > 2 ? unsigned(atoi(argv[2])) : 1920;
     unsigned H = argc > 3 ? unsigned(atoi(argv[3])) : 1080;
     int frames = argc > 4 ? atoi(argv[4]) : 1;
+    unsigned frame_num = argc > 5 ? unsigned(atoi(argv[5])) : 0u;
     try
     {
         // scene + host BVH: build<index_bvh<P>> (build.inl:165-178)
@@ -56,7 +60,7 @@ int main(int argc, char** argv)
         for (int f = 0; f < frames; ++f)
         {
             auto t0 = std::chrono::steady_clock::now();
-            sched.frame(kernel, sparams, unsigned(f));
+            sched.frame(kernel, sparams, frame_num);
             auto t1 = std::chrono::steady_clock::now();
             best_ms = std::min(best_ms, std::chrono::duration<double, std::milli>(t1 - t0).count());
             rays = sched.context().last_frame_stats().rays;

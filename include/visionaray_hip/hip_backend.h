@@ -63,6 +63,28 @@ template <typename T, typename = void> struct is_sphere : std::false_type {};
 template <typename T> struct is_sphere<T, decltype((void)std::declval<T>().radius)> : std::true_type {};
 template <typename T, typename = void> struct is_triangle : std::false_type {};
 template <typename T> struct is_triangle<T, decltype((void)std::declval<T>().e2)> : std::true_type {};
+
+// sched_params::scissor_box (scheduler.h:25-31; make_sched_params sets recti(0, 0, w, h), :175),
+// read as cuda_sched reads it (cuda_sched.inl:71): x <= px < w, y <= py < h
+template <typename SP, typename = void> struct has_scissor : std::false_type {};
+template <typename SP> struct has_scissor<SP, decltype((void)std::declval<SP>().scissor_box)> : std::true_type {};
+
+template <typename SP>
+void set_scissor(SP const& sp, vrh_camera& c)
+{
+    if constexpr (has_scissor<SP>::value)
+    {
+        auto const& sb = sp.scissor_box;
+        c.scissor[0] = uint32_t(sb.x > 0 ? sb.x : 0);
+        c.scissor[1] = uint32_t(sb.y > 0 ? sb.y : 0);
+        c.scissor[2] = uint32_t(sb.w > 0 ? sb.w : 0);
+        c.scissor[3] = uint32_t(sb.h > 0 ? sb.h : 0);
+        // recti(0, 0, 0, 0) is an empty box for the reference, but all-zero means "whole image" in
+        // the C ABI: pass the same empty pixel set as (1, 1, 1, 1)
+        if (c.scissor[0] == 0 && c.scissor[1] == 0 && c.scissor[2] == 0 && c.scissor[3] == 0)
+            c.scissor[0] = c.scissor[1] = c.scissor[2] = c.scissor[3] = 1u;
+    }
+}
 } // hip_detail
 
 //-------------------------------------------------------------------------------------------------
@@ -97,6 +119,67 @@ public:
 
 private:
     std::shared_ptr<vrh_ctx> ctx_;
+};
+
+//-------------------------------------------------------------------------------------------------
+// hip_render_group: several GPUs rendering one frame together (vrh.h vrh_group_*): image-tile
+// shards on every device, gathered to device 0 over RCCL.  One process driving every GPU:
+// hip_render_group(devices) (ncclCommInitAll); one process per GPU: hip_render_group(ctx, nranks,
+// rank, id) with the id from hip_render_group::unique_id() on rank 0.
+//
+
+class hip_render_group
+{
+public:
+    // every visible device (devices empty) or the given ones; member i renders on devices[i]
+    explicit hip_render_group(std::vector<int> devices = {})
+    {
+        if (devices.empty())
+        {
+            int n = 0;
+            hip_detail::check(vrh_device_count(&n), "vrh_device_count");
+            for (int d = 0; d < n; ++d) devices.push_back(d);
+        }
+        std::vector<vrh_ctx*> raw;
+        for (int d : devices)
+        {
+            ctxs_.push_back(std::make_shared<hip_context>(d));
+            raw.push_back(ctxs_.back()->get());
+        }
+        std::vector<vrh_group*> g(raw.size(), nullptr);
+        hip_detail::check(vrh_group_create_local(uint32_t(raw.size()), raw.data(), g.data()), "vrh_group_create_local");
+        for (auto* p : g) groups_.emplace_back(p, [](vrh_group* q) { vrh_group_free(q); });
+    }
+
+    // one rank of a group spread over processes
+    hip_render_group(std::shared_ptr<hip_context> ctx, uint32_t nranks, uint32_t rank, vrh_group_id const& id)
+    {
+        vrh_group* g = nullptr;
+        hip_detail::check(vrh_group_join(ctx->get(), nranks, rank, &id, &g), "vrh_group_join");
+        ctxs_.push_back(std::move(ctx));
+        groups_.emplace_back(g, [](vrh_group* q) { vrh_group_free(q); });
+    }
+
+    static vrh_group_id unique_id()
+    {
+        vrh_group_id id{};
+        hip_detail::check(vrh_group_get_id(&id), "vrh_group_get_id");
+        return id;
+    }
+
+    size_t size() const { return groups_.size(); }              // members driven by this process
+    std::shared_ptr<hip_context> const& context(size_t i) const { return ctxs_[i]; }
+    vrh_group* handle(size_t i) const { return groups_[i].get(); }
+    bool has_root() const
+    {
+        for (auto const& g : groups_) { uint32_t r = 1; vrh_group_info(g.get(), nullptr, &r); if (r == 0) return true; }
+        return false;
+    }
+    void sync() const { for (auto const& g : groups_) hip_detail::check(vrh_group_sync(g.get()), "vrh_group_sync"); }
+
+private:
+    std::vector<std::shared_ptr<hip_context>> ctxs_;
+    std::vector<std::shared_ptr<vrh_group>> groups_;
 };
 
 //-------------------------------------------------------------------------------------------------
@@ -180,6 +263,39 @@ private:
         scene_.reset(s, [](vrh_scene* p) { vrh_scene_free(p); });
     }
 
+    std::shared_ptr<hip_context> ctx_;
+    std::shared_ptr<vrh_scene> scene_;
+};
+
+//-------------------------------------------------------------------------------------------------
+// hip_index_bvh_list<P>: a list of device BVHs rendered as one scene -- the [begin, end) range of
+// bvh_refs that closest_hit / any_hit take (traverse_linear.inl:76-141; ao/main.cpp:171-178 builds
+// such a vector).  Every BVH is traversed on its own per ray and merged by is_closer / update_if
+// (vrh.h vrh_scene_list_create).  face_normals: one 16-B vec3 per prim_id over the whole list.
+//
+
+template <typename Primitive>
+class hip_index_bvh_list
+{
+public:
+    using primitive_type = Primitive;
+
+    hip_index_bvh_list(std::vector<hip_index_bvh<Primitive>> const& bvhs, void const* face_normals = nullptr,
+                       uint32_t num_normals = 0, std::shared_ptr<hip_context> ctx = hip_context::default_context())
+        : ctx_(std::move(ctx))
+    {
+        std::vector<vrh_scene const*> h;
+        for (auto const& b : bvhs) h.push_back(b.handle());
+        vrh_scene* s = nullptr;
+        hip_detail::check(vrh_scene_list_create(ctx_->get(), h.data(), uint32_t(h.size()), face_normals, num_normals, &s),
+                          "vrh_scene_list_create");
+        scene_.reset(s, [](vrh_scene* p) { vrh_scene_free(p); });
+    }
+
+    vrh_scene* handle() const { return scene_.get(); }
+    hip_context& context() const { return *ctx_; }
+
+private:
     std::shared_ptr<hip_context> ctx_;
     std::shared_ptr<vrh_scene> scene_;
 };
@@ -481,6 +597,48 @@ public:
     {
     }
 
+    // multi-GPU: frames sharded over a render group; `shards` image-tile shards
+    // (0 = one per GPU).  frame() then takes one built-in kernel per member of the group (each
+    // made from that member's BVH replica) and a render target on member 0's device.
+    explicit hip_sched(hip_render_group& group, unsigned shards = 0)
+        : ctx_(group.context(0))
+        , group_(&group)
+        , shards_(shards)
+    {
+    }
+
+    template <typename SP>
+    void frame(std::vector<hip_builtin_kernel> const& kernels, SP sparams, unsigned frame_num = 0)
+    {
+        if (!group_ || kernels.size() != group_->size())
+            throw std::runtime_error("hip_sched::frame: one kernel per member of the render group");
+        auto const& cam = sparams.cam;
+        auto& rt = sparams.rt;
+        float eye[3] = { cam.eye().x, cam.eye().y, cam.eye().z };
+        float center[3] = { cam.center().x, cam.center().y, cam.center().z };
+        float up[3] = { cam.up().x, cam.up().y, cam.up().z };
+        vrh_camera c{};
+        hip_detail::check(vrh_make_camera(eye, center, up, cam.fovy(), cam.aspect(), uint32_t(rt.width()),
+                                          uint32_t(rt.height()), &c), "vrh_make_camera");
+        hip_detail::set_scissor(sparams, c);
+        std::vector<vrh_group*> g;
+        std::vector<vrh_scene const*> sc;
+        std::vector<vrh_kernel_desc> kd;
+        for (size_t i = 0; i < kernels.size(); ++i)
+        {
+            g.push_back(group_->handle(i));
+            sc.push_back(kernels[i].scene);
+            kd.push_back(kernels[i].desc);
+        }
+        rt.begin_frame();
+        hip_detail::check(vrh_render_sharded(uint32_t(g.size()), g.data(), sc.data(), kd.data(),
+                                             group_->has_root() ? rt.handle() : nullptr, VRH_RT_ALL, &c, 1, frame_num,
+                                             shards_),
+                          "vrh_render_sharded");
+        group_->sync();
+        rt.end_frame();
+    }
+
     // frame(): rt.begin_frame() -> vrh_render -> rt.end_frame() (cuda_sched.inl:306-320; end_frame
     // syncs).  shard: optional image-tile shard (multi-GPU).
     template <typename K, typename SP>
@@ -498,6 +656,7 @@ public:
         vrh_camera c{};
         hip_detail::check(vrh_make_camera(eye, center, up, cam.fovy(), cam.aspect(), uint32_t(rt.width()),
                                           uint32_t(rt.height()), &c), "vrh_make_camera");
+        hip_detail::set_scissor(sparams, c);
         rt.begin_frame();
         hip_detail::check(vrh_render(ctx_->get(), kernel.scene, rt.handle(), &c, &kernel.desc, shard, frame_num),
                           "vrh_render");
@@ -506,8 +665,9 @@ public:
 
     // frames in flight (vrh_render_batch): ONE persistent launch renders cams.size() frames of
     // one scene and kernel (up to VRH_MAX_BATCH), camera f into rows [f * H, (f + 1) * H) of rt,
-    // whose height is cams.size() * H.  Every frame equals its own frame() call; the launch's tail
-    // is paid once instead of once per frame.  Synchronous like frame().
+    // whose height is cams.size() * H, with frame number frame_num + f.  Every frame equals its
+    // own frame() call; the launch's tail is paid once instead of once per frame.  Synchronous
+    // like frame().
     template <typename K, typename Camera, typename RT>
     void frames(K kernel, std::vector<Camera> const& cams, RT& rt, unsigned frame_num = 0)
     {
@@ -536,6 +696,8 @@ public:
 
 private:
     std::shared_ptr<hip_context> ctx_;
+    hip_render_group* group_ = nullptr;
+    unsigned shards_ = 0;
 };
 
 // host-side builder with the reference's result (build<index_bvh<P>>, build.inl:165-178):

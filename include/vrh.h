@@ -97,20 +97,26 @@ enum vrh_rt_flags {
     VRH_RT_ALL = 15u
 };
 
-/* Host-computed pinhole basis exactly as simple_sched.inl:61-89 derives it (bit-exact floats). */
+/* Host-computed pinhole basis exactly as simple_sched.inl:61-89 derives it (bit-exact floats),
+ * plus the frame's scissor box (sched_params::scissor_box, scheduler.h:25-31; default
+ * recti(0, 0, w, h), scheduler.h:175).  As cuda_sched uses it (cuda_sched.inl:71) the box is
+ * {x, y, w, h} with w / h the EXCLUSIVE right / bottom edges: pixels x <= px < w, y <= py < h are
+ * rendered, every other pixel of the target is left untouched.  All four zero = the whole image. */
 typedef struct {
     float    eye[3];
     float    cam_u[3];
     float    cam_v[3];
     float    cam_w[3];
     uint32_t width, height;   /* full image size (primary ray u,v and the AO pixel index use it) */
+    uint32_t scissor[4];      /* x, y, w, h (exclusive edges); all zero: whole image             */
 } vrh_camera;
 
 typedef struct vrh_hit_mask vrh_hit_mask;   /* see vrh_hit_mask_create                      */
 
 typedef struct {
     uint32_t kind;            /* vrh_kernel_kind                                          */
-    uint32_t samples;         /* AO samples per hit pixel (ao/main.cpp default 8, <= 32)   */
+    uint32_t samples;         /* AO samples per hit pixel (ao/main.cpp default 8, <= 32; a
+                                 VRH_RT_OCC target records at most 8)                        */
     float    radius;          /* AO any_hit max_t (default 0.1)                            */
     float    eps;             /* AO origin offset along the sample direction (1e-3); the
                                  whitted kernel's scene epsilon                              */
@@ -151,11 +157,17 @@ typedef struct {
     uint32_t grid_blocks;
     uint32_t block_threads;
     uint32_t stack_depth;     /* per-lane traversal stack entries used by the variant         */
+    uint32_t frames;          /* frames of the last launch (vrh_render_batch)                  */
     /* SIMD utilisation (only with VRH_KERNEL_COUNT_TESTS): wave-level iterations of the refilling
      * loop, lanes busy summed over them, and wave-level iterations of the node-descent and leaf
      * loops (lane-level: box_tests / 2 and prim_tests)                                          */
     uint64_t wave_steps, busy_lane_steps, wave_box_iters, wave_prim_iters;
     uint64_t wave_box_uniform_iters;  /* of wave_box_iters: those whose active lanes all fetch ONE node */
+    /* vector-L1 coalescer model (only with VRH_KERNEL_COUNT_TESTS): over every wave-level
+     * vector-memory instruction of the traversal (node pair, primitive and normal loads, output
+     * stores), the distinct 128-B lines and 64-B segments its active lanes touch, and the number
+     * of such instructions -- the per-launch work of the L1 / TA / TD path that bounds the kernel */
+    uint64_t l1_lines, l1_segments, vmem_instrs;
 } vrh_frame_stats;
 
 typedef struct {
@@ -169,6 +181,7 @@ typedef struct {
     uint32_t vertex_normals;  /* per-vertex normals set (vrh_scene_set_vertex_normals)          */
     uint32_t gpu_built;       /* built by vrh_scene_build                                        */
     float    build_ms;        /* vrh_scene_build: device time of the build kernels               */
+    uint32_t num_bvhs;        /* BVHs in the scene (> 1: a list, vrh_scene_list_create)          */
 } vrh_scene_info;
 
 /* camera::look_at + camera::perspective (camera.inl:10-57) followed by the pinhole basis that
@@ -194,12 +207,10 @@ enum vrh_option {
                                     up to a multiple of 4)                                        */
     VRH_OPT_AO_SCHEDULE = 3,     /* refilling loop of a wave: 3 = one descend-to-leaf step per
                                     iteration, 4 = one traversal item (node pair or primitive)
-                                    per lane and iteration, 5 = items, but only node pairs or
-                                    only primitives per iteration, whichever more lanes wait for,
-                                    6 = two-pass AO: primaries publish hit records, then every
-                                    wave takes AO rays ray by ray from the frame's hit lists
-                                    (AO only; others as 3)
-                                    (auto: 4 for sphere primary visibility, else 3)              */
+                                    per lane and iteration (primary visibility; AO always runs 3)
+                                    (auto: 4 for sphere primary visibility, else 3).  Round 1's
+                                    vote loop, item-loop AO and two-pass AO were removed: never
+                                    faster (profiles/r01_ab*)                                     */
     VRH_OPT_BLOCKS_PER_CU = 4,   /* resident blocks per CU for the persistent grid (auto: max)     */
     VRH_OPT_WAVES_PER_SIMD = 5,  /* register budget of the unified kernel: 1 (none), 5, 6 or 8 (auto: 5 AO, 6 primary) */
     VRH_OPT_EXACT_MINMAX = 6,    /* 1 = always use the ternary min/max slab test (auto: hardware
@@ -207,10 +218,7 @@ enum vrh_option {
     VRH_OPT_XCD_QUEUES = 7,      /* tile queues: 1 = one per XCD with stealing, 2 = one global
                                     queue (auto: 1)                                               */
     VRH_OPT_REFILL_MIN = 8,      /* free lanes (1..64) before finished rays are retired and idle
-                                    lanes refilled (auto: 32 step loop and primary item loop, 16
-                                    AO item loops)                                                */
-    VRH_OPT_VOTE_LEAF = 9,       /* vote loop: primitive step when 8 x leaf lanes >= this x node
-                                    lanes (1..64, auto: 8 = simple majority)                     */
+                                    lanes refilled (auto: 32)                                     */
     VRH_OPT_WIDE_ANYHIT = 10,    /* 4-wide node records for any-hit (AO) rays (step loop): 1 = on
                                     when the BVH passes the containment check, 2 = off (auto: off,
                                     measured 6 % slower on hf1M AO than the binary records)      */
@@ -241,6 +249,19 @@ VRH_API int vrh_scene_upload(vrh_ctx* ctx, const void* nodes, uint32_t num_nodes
                              const uint32_t* indices, uint32_t num_indices,
                              const void* face_normals, vrh_scene** out);
 VRH_API int vrh_scene_get_info(const vrh_scene* scene, vrh_scene_info* info);
+
+/* A list of BVHs rendered as one scene <- closest_hit / any_hit over [begin, end) of bvh_refs
+ * (traverse_linear.inl:76-141, 232-329; the kernels of ao/main.cpp:183 and the viewer pass such a
+ * list).  Per ray every BVH is traversed on its own, in list order, with a fresh result and the same
+ * max_t, and merged into the running result by update_if(result, hr, is_closer(hr, result, max_t))
+ * (strictly closer wins, hit_record.h:54-64); any-hit rays stop at the first BVH with a hit.  The
+ * members (single BVHs of one primitive type, same context) are copied into the list, which owns its
+ * device memory; the members may be freed afterwards.  face_normals (vec3, 16-B stride, indexed by
+ * prim_id, num_normals > every member's largest prim_id) feed AO: the get_normal(normals, hit)
+ * array of the kernel.  Primary and AO kernels. */
+#define VRH_MAX_SCENE_LIST 8
+VRH_API int vrh_scene_list_create(vrh_ctx* ctx, const vrh_scene* const* scenes, uint32_t count,
+                                  const void* face_normals, uint32_t num_normals, vrh_scene** out);
 VRH_API int vrh_scene_free(vrh_scene* scene);
 /* per-vertex normals (vec3, 16-B stride): normals[3 * prim_id + k] for vertex k (v1, v1+e1, v1+e2),
  * the normals_per_vertex_binding array of get_shading_normal.h:64-84 */
@@ -265,11 +286,17 @@ VRH_API int vrh_rt_free(vrh_rt* rt);
 VRH_API int vrh_rt_alloc_multi_hit(vrh_ctx* ctx, vrh_rt* rt, uint32_t max_hits);
 VRH_API int vrh_rt_download_multi_hit(vrh_ctx* ctx, vrh_rt* rt, uint32_t* prim_ids, float* t);   /* syncs */
 
-/* one frame (asynchronous on the context stream); shard may be NULL (= whole image) */
+/* one frame (asynchronous on the context stream); shard may be NULL (= whole image).
+ * frame_num is cuda_sched::frame's frame number (cuda_sched.inl:306-320): the reference reseeds
+ * its sampler every frame (cuda_sched.inl:38-45, 79; ao/main.cpp:245 passes ++frame_num).  Here it
+ * offsets the deterministic Appendix-A AO sampler: the counter of frame n is
+ * ((p*8 + s)*16 + k)*2 + n * 0x9E3779B1 (u32 wrap), so frame 0 is the parity frame and every frame
+ * number gives its own AO sample set.  The other built-in kernels draw no random numbers. */
 VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* scene, vrh_rt* rt, const vrh_camera* cam,
                        const vrh_kernel_desc* kernel, const vrh_shard* shard, uint32_t frame_num);
 /* frames in flight: num_frames (1..VRH_MAX_BATCH) frames of one scene and kernel in ONE persistent
- * launch.  Frame f renders cams[f] (all of one size) into rows [f * R, (f + 1) * R) of rt, where
+ * launch, with frame numbers frame_num, frame_num + 1, ...
+ * Frame f renders cams[f] (all of one size) into rows [f * R, (f + 1) * R) of rt, where
  * R = the image height (rt is W x num_frames*H) or, for a packed shard, R = rt height / num_frames.
  * The frames' tiles share the work queues, interleaved tile by tile, so a wave goes on to the next
  * frame's tiles instead of idling while the last tiles of a frame finish; every frame's output is
@@ -311,6 +338,42 @@ VRH_API int vrh_unshard(vrh_ctx* ctx, uint32_t width, uint32_t height, uint32_t 
                         const void* gathered_color, const uint32_t* gathered_prim_id,
                         const uint8_t* gathered_occ, uint64_t shard_stride_bytes,
                         const vrh_kernel_desc* kernel, vrh_rt* dst);
+
+/* ---- multi-GPU render groups --------------------------------------------------
+ * The image is cut into 8-row bands dealt round-robin to S shards (band b -> shard b % S); shard s
+ * is rendered by rank s % N of an N-rank group, packed (vrh_shard.packed), and every shard is
+ * gathered to rank 0 over RCCL (ncclSend / ncclRecv, one pair per shard, xGMI point-to-point) and
+ * laid back into image order there (vrh_unshard's kernel).  The reference has no multi-GPU path;
+ * this lifts tiled_sched's tile distribution (tiled_sched.inl:24-25, 175-224) across devices.
+ * A group is one RCCL communicator; a vrh_group is one rank's membership (one context = one GPU):
+ *   - one process per GPU: rank 0 calls vrh_group_get_id, hands the id to every rank (any channel,
+ *     e.g. torch.distributed / MPI), every rank calls vrh_group_join (collective);
+ *   - one process driving every GPU: vrh_group_create_local(ndev, ctxs, out[ndev]).
+ * Results are bit-identical to the one-GPU image (the shards partition the pixels; every pixel's
+ * arithmetic is unchanged). */
+typedef struct vrh_group vrh_group;
+typedef struct { char internal[128]; } vrh_group_id;   /* = ncclUniqueId */
+VRH_API int vrh_group_get_id(vrh_group_id* id);
+VRH_API int vrh_group_join(vrh_ctx* ctx, uint32_t nranks, uint32_t rank, const vrh_group_id* id, vrh_group** out);
+VRH_API int vrh_group_create_local(uint32_t ndev, vrh_ctx* const* ctxs, vrh_group** out);
+VRH_API int vrh_group_info(const vrh_group* group, uint32_t* nranks, uint32_t* rank);
+VRH_API int vrh_group_sync(vrh_group* group);   /* waits for the renders AND the exchange */
+VRH_API int vrh_group_free(vrh_group* group);
+/* Render num_frames frames (frame numbers frame_num, frame_num + 1, ...) sharded over a group and
+ * gather them to rank 0.  groups / scenes / kernels: the n members this caller drives (n = 1 for
+ * one process per GPU; every device for vrh_group_create_local), scene i and the kernel's shading /
+ * mask objects on group i's context.  Every rank passes the same kernel, fields, cameras, frames
+ * and shard count.  dst: rank 0's W x (H * num_frames) target (NULL on the other ranks); fields
+ * (vrh_rt_flags) = the buffers assembled there (the same on every rank).  The built-in primary / AO
+ * kernels' colour is re-derived on the root from prim id + AO mask (AO samples <= 8), so 4-5 B
+ * per pixel cross xGMI; shading kernels gather their RGBA32F colour.  shards: S (0 = one per rank;
+ * S > N: rank r renders shards r, r + N, ... -- so a one-rank group still runs the whole path).
+ * Asynchronous: renders on each context's stream, the exchange and un-interleave on the group's
+ * own stream (two staging slots: the next call's renders overlap this call's exchange);
+ * vrh_group_sync waits for both. */
+VRH_API int vrh_render_sharded(uint32_t n, vrh_group* const* groups, const vrh_scene* const* scenes,
+                               const vrh_kernel_desc* kernels, vrh_rt* dst, uint32_t fields,
+                               const vrh_camera* cams, uint32_t num_frames, uint32_t frame_num, uint32_t shards);
 
 /* GPU BVH construction: a linear BVH (Morton order, Karras 2012 hierarchy,
  * leaves of up to max_leaf primitives) built on the device straight into a scene -- no host build,

@@ -50,21 +50,26 @@ class _HitMask(C.Structure):
 
 
 class _Scene(C.Structure):
-    _fields_ = [("nodes", C.c_void_p), ("indices", C.c_void_p), ("prims", C.c_void_p),
-                ("kind", C.c_int), ("normals", C.c_void_p), ("vertex_normals", C.c_void_p),
-                ("hit_mask", C.c_void_p)]
+    pass
+
+
+_Scene._fields_ = [("nodes", C.c_void_p), ("indices", C.c_void_p), ("prims", C.c_void_p),
+                   ("kind", C.c_int), ("normals", C.c_void_p), ("vertex_normals", C.c_void_p),
+                   ("hit_mask", C.c_void_p), ("next", C.POINTER(_Scene))]
 
 
 class _Camera(C.Structure):
     _fields_ = [("eye", C.c_float * 3), ("cam_u", C.c_float * 3), ("cam_v", C.c_float * 3),
-                ("cam_w", C.c_float * 3), ("width", C.c_int), ("height", C.c_int)]
+                ("cam_w", C.c_float * 3), ("width", C.c_int), ("height", C.c_int),
+                ("scissor", C.c_uint * 4)]
 
 
 class _Kernel(C.Structure):
     _fields_ = [("mode", C.c_int), ("samples", C.c_int), ("radius", C.c_float), ("eps", C.c_float),
                 ("bg", C.c_float * 4), ("materials", C.c_void_p), ("num_materials", C.c_int),
                 ("lights", C.c_void_p), ("num_lights", C.c_int), ("ambient", C.c_float * 4),
-                ("normal_binding", C.c_int), ("max_hits", C.c_int), ("num_bounces", C.c_int)]
+                ("normal_binding", C.c_int), ("max_hits", C.c_int), ("num_bounces", C.c_int),
+                ("frame_num", C.c_uint32)]
 
 
 _lib = None
@@ -213,24 +218,32 @@ def make_scene(name):
 
 def _structs(scene, cam, mode, samples=8, radius=0.1, eps=1e-3, bg=(0.1, 0.2, 0.3, 1.0), materials=None,
              lights=None, ambient=(0.0, 0.0, 0.0, 0.0), binding=VO_NORMALS_PER_FACE, max_hits=0, num_bounces=0,
-             hit_mask=None):
+             hit_mask=None, frame_num=0, scissor=None):
+    """scene: a Scene, or a list of Scenes = a BVH-ref list (normals of the first entry, indexed
+    by prim_id over the whole list); scissor: (x0, y0, x1, y1) as cuda_sched reads it."""
     hm = None
     if hit_mask is not None:
         tc, mask = hit_mask
         tc = np.ascontiguousarray(tc, np.float32)
         mask = np.ascontiguousarray(mask, np.uint8)
         hm = _HitMask(_p(tc).value, _p(mask).value, mask.shape[1], mask.shape[0])
-    s = _Scene(_p(scene.nodes).value, _p(scene.indices).value, _p(scene.prims).value, scene.kind,
-               _p(scene.normals).value if scene.normals is not None else None,
-               _p(scene.vertex_normals).value if scene.vertex_normals is not None else None,
-               C.cast(C.pointer(hm), C.c_void_p).value if hm is not None else None)
+    members = list(scene) if isinstance(scene, (list, tuple)) else [scene]
+    chain = []
+    for m in reversed(members):
+        nxt = C.pointer(chain[-1]) if chain else None
+        chain.append(_Scene(_p(m.nodes).value, _p(m.indices).value, _p(m.prims).value, m.kind,
+                            _p(m.normals).value if m.normals is not None else None,
+                            _p(m.vertex_normals).value if m.vertex_normals is not None else None,
+                            C.cast(C.pointer(hm), C.c_void_p).value if hm is not None else None, nxt))
+    s = chain[-1]
     eye, u, v, w, W, H = cam
-    c = _Camera((C.c_float * 3)(*eye), (C.c_float * 3)(*u), (C.c_float * 3)(*v), (C.c_float * 3)(*w), W, H)
+    c = _Camera((C.c_float * 3)(*eye), (C.c_float * 3)(*u), (C.c_float * 3)(*v), (C.c_float * 3)(*w), W, H,
+                (C.c_uint * 4)(*(scissor or (0, 0, 0, 0))))
     k = _Kernel(mode, samples, radius, eps, (C.c_float * 4)(*bg),
                 _p(materials).value if materials is not None else None, 0 if materials is None else len(materials),
                 _p(lights).value if lights is not None else None, 0 if lights is None else len(lights),
-                (C.c_float * 4)(*ambient), binding, max_hits, num_bounces)
-    _structs.keep = (materials, lights, hm, hit_mask and (tc, mask))
+                (C.c_float * 4)(*ambient), binding, max_hits, num_bounces, frame_num)
+    _structs.keep = (materials, lights, hm, hit_mask and (tc, mask), chain, members)
     return s, c, k
 
 

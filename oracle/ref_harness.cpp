@@ -266,9 +266,25 @@ struct mask_intersector : basic_intersector<mask_intersector>
     int w = 0, h = 0;
 };
 
+// the parity AO sampler of SURVEY.md Appendix A, frame n offset by n * 0x9E3779B1 (the build's
+// stand-in for the reference's per-frame reseeding, cuda_sched.inl:38-45, 79; frame 0 = Appendix A):
+// Malley sample s of pixel p
+static vec2 ao_sample(uint32_t p, int smp, uint32_t frame_num)
+{
+    for (uint32_t k = 0; k < 16; ++k)
+    {
+        uint32_t ctr = ((p * 8u + uint32_t(smp)) * 16u + k) * 2u + frame_num * 0x9E3779B1u;
+        float xa = 2.0f * U(ctr) - 1.0f;
+        float ya = 2.0f * U(ctr + 1) - 1.0f;
+        if (xa * xa + ya * ya < 1.0f) return vec2(xa, ya);
+    }
+    return vec2(0.0f, 0.0f);
+}
+
 template <typename P, typename Isect = default_intersector>
 static int run_golden(scene_desc const& d, aligned_vector<P>& prims, std::vector<vec3> const& normals,
-                      std::string const& outdir, int W, int H, bool do_ao, Isect isect = Isect{})
+                      std::string const& outdir, int W, int H, bool do_ao, Isect isect = Isect{},
+                      uint32_t frame_num = 0)
 {
     auto t0 = std::chrono::steady_clock::now();
     auto bvh = build<index_bvh<P>>(prims.data(), prims.size());
@@ -345,14 +361,8 @@ static int run_golden(scene_desc const& d, aligned_vector<P>& prims, std::vector
         uint8_t mask = 0;
         for (int smp = 0; smp < 8; ++smp)
         {
-            float sx = 0.0f, sy = 0.0f;
-            for (uint32_t k = 0; k < 16; ++k)
-            {
-                uint32_t ctr = ((uint32_t(p) * 8u + uint32_t(smp)) * 16u + k) * 2u;
-                float xa = 2.0f * U(ctr) - 1.0f;
-                float ya = 2.0f * U(ctr + 1) - 1.0f;
-                if (xa * xa + ya * ya < 1.0f) { sx = xa; sy = ya; break; }
-            }
+            vec2 sxy = ao_sample(uint32_t(p), smp, frame_num);
+            float sx = sxy.x, sy = sxy.y;
             float sz = sqrt(std::max(0.0f, 1.0f - sx * sx - sy * sy));
             auto dir = normalize(sx * uu + sy * vv + sz * w);
             ray ao;
@@ -727,6 +737,109 @@ static int with_scene(scene_desc const& d, F&& f)
     return f(t, normals);
 }
 
+//-------------------------------------------------------------------------------------------------
+// list: closest_hit / any_hit over a LIST of two BVH refs (traverse_linear.inl:76-141) -- the
+// scene's triangles split by prim_id parity, each half its own build<index_bvh<P>> -- rendered by
+// tiled_sched<ray> (tiled_sched.inl:365-391) with a scissor box (the clip of tiled_sched.inl:
+// 244-260): pixels x0 <= x < x1, y0 <= y < y1 (tiled_sched reads recti(x, y, width, height), so
+// the box is recti(x0, y0, x1 - x0, y1 - y0); cuda_sched reads the same pixel set from
+// recti(x0, y0, x1, y1), cuda_sched.inl:71).  Kernel: the golden primary + parity AO of frame
+// `frame_num`.  Pixels outside the box keep the cleared target (colour 0, prim_id ~0, t -1, occ 0).
+//
+
+static int run_list(scene_desc const& d, aligned_vector<tri_t> const& all, std::string const& outdir, int W, int H,
+                    int const sb[4], uint32_t frame_num)
+{
+    aligned_vector<tri_t> part[2];
+    for (auto const& tri : all) part[tri.prim_id % 2u].push_back(tri);
+    std::vector<vec3> normals(all.size());
+    for (auto const& tri : all) normals[tri.prim_id] = normalize(cross(tri.e1, tri.e2));
+    auto b0 = build<index_bvh<tri_t>>(part[0].data(), part[0].size());
+    auto b1 = build<index_bvh<tri_t>>(part[1].data(), part[1].size());
+    for (int k = 0; k < 2; ++k)
+    {
+        auto const& b = k == 0 ? b0 : b1;
+        std::string pre = outdir + "/bvh" + std::to_string(k) + "_";
+        write_file(pre + "nodes.bin", b.nodes().data(), b.nodes().size() * sizeof(bvh_node));
+        write_file(pre + "indices.bin", b.indices().data(), b.indices().size() * 4);
+        write_file(pre + "prims.bin", part[k].data(), part[k].size() * sizeof(tri_t));
+    }
+    using bvh_ref = index_bvh<tri_t>::bvh_ref;
+    std::vector<bvh_ref> bvhs{ b0.ref(), b1.ref() };
+    auto prims_begin = bvhs.data();
+    auto prims_end = bvhs.data() + bvhs.size();
+
+    camera cam = make_camera(d, W, H);
+    size_t npx = size_t(W) * H;
+    std::vector<uint32_t> prim_id(npx, 0xFFFFFFFFu), leaf_pos(npx, 0xFFFFFFFFu);
+    std::vector<float> tval(npx, -1.0f);
+    std::vector<uint8_t> occ(npx, 0);
+    simple_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> rt;
+    rt.resize(W, H);
+    rt.clear_color_buffer(vec4(0.0f));
+    auto sparams = make_sched_params(pixel_sampler::uniform_type{}, cam, rt);
+    sparams.scissor_box = recti(sb[0], sb[1], sb[2] - sb[0], sb[3] - sb[1]);
+    const vec4 bg(0.1f, 0.2f, 0.3f, 1.0f);
+    std::atomic<uint64_t> ao_rays{0}, ao_occ{0};
+    tiled_sched<ray> sched(2);
+    // tiled_sched can lose the wakeup of a worker that is not waiting yet (tiled_sched.inl:181,386)
+    std::this_thread::sleep_for(std::chrono::milliseconds(200));
+    sched.frame([&](ray r, unsigned x, unsigned y) -> result_record<float>
+    {
+        result_record<float> result;
+        result.color = bg;
+        auto hr = closest_hit(r, prims_begin, prims_end);
+        result.hit = hr.hit;
+        size_t p = size_t(y) * W + x;
+        if (!hr.hit) return result;
+        prim_id[p] = hr.prim_id;
+        tval[p] = hr.t;
+        leaf_pos[p] = hr.primitive_list_index;
+        hr.isect_pos = r.ori + r.dir * hr.t;
+        vec4 clr(1.0f);
+        vec3 n = normals[hr.prim_id];
+        vec3 uu, vv, w = n;
+        make_orthonormal_basis(uu, vv, w);
+        uint8_t mask = 0;
+        for (int smp = 0; smp < 8; ++smp)
+        {
+            vec2 sxy = ao_sample(uint32_t(p), smp, frame_num);
+            float sz = sqrt(std::max(0.0f, 1.0f - sxy.x * sxy.x - sxy.y * sxy.y));
+            auto dir = normalize(sxy.x * uu + sxy.y * vv + sz * w);
+            ray ao;
+            ao.ori = hr.isect_pos + dir * 1E-3f;
+            ao.dir = dir;
+            auto ar = any_hit(ao, prims_begin, prims_end, 0.1f);
+            ++ao_rays;
+            if (ar.hit) { clr = clr - 1.0f / 8; mask |= uint8_t(1u << smp); ++ao_occ; }
+        }
+        occ[p] = mask;
+        result.color = vec4(clr.xyz(), 1.0f);
+        return result;
+    }, sparams, frame_num);
+
+    write_file(outdir + "/prim_id.bin", prim_id.data(), npx * 4);
+    write_file(outdir + "/t.bin", tval.data(), npx * 4);
+    write_file(outdir + "/leaf_pos.bin", leaf_pos.data(), npx * 4);
+    write_file(outdir + "/occ.bin", occ.data(), npx);
+    write_file(outdir + "/color.bin", rt.color(), npx * 16);
+    fnv hp, ht, ho, hc;
+    uint64_t hits = 0;
+    for (size_t p = 0; p < npx; ++p)
+    {
+        hp.u32(prim_id[p]); ht.u32(fbits(tval[p])); ho.bytes(&occ[p], 1);
+        hits += prim_id[p] != 0xFFFFFFFFu;
+    }
+    hc.bytes(rt.color(), npx * 16);
+    printf("{\"scene\":\"%s\",\"W\":%d,\"H\":%d,\"scissor\":[%d,%d,%d,%d],\"frame\":%u,\"bvh_nodes\":[%zu,%zu],"
+           "\"hits\":%llu,\"ao_rays\":%llu,\"ao_occluded\":%llu,\"primid_hash\":\"%016llx\",\"t_hash\":\"%016llx\","
+           "\"occmask_hash\":\"%016llx\",\"color_hash\":\"%016llx\"}\n",
+           d.name.c_str(), W, H, sb[0], sb[1], sb[2], sb[3], frame_num, b0.nodes().size(), b1.nodes().size(),
+           (unsigned long long)hits, (unsigned long long)ao_rays.load(), (unsigned long long)ao_occ.load(),
+           (unsigned long long)hp.h, (unsigned long long)ht.h, (unsigned long long)ho.h, (unsigned long long)hc.h);
+    return 0;
+}
+
 int main(int argc, char** argv)
 {
     if (argc < 3)
@@ -743,9 +856,10 @@ int main(int argc, char** argv)
         std::string outdir = argv[3];
         int W = argc > 5 ? atoi(argv[4]) : d.W;
         int H = argc > 5 ? atoi(argv[5]) : d.H;
+        uint32_t frame_num = argc > 6 ? uint32_t(strtoul(argv[6], nullptr, 10)) : 0u;
         return with_scene(d, [&](auto& prims, std::vector<vec3> const& normals)
         {
-            return run_golden(d, prims, normals, outdir, W, H, !d.spheres);
+            return run_golden(d, prims, normals, outdir, W, H, !d.spheres, default_intersector{}, frame_num);
         });
     }
     if (mode == "shade" || mode == "whitted")
@@ -796,6 +910,18 @@ int main(int argc, char** argv)
         isect.w = mw;
         isect.h = mh;
         return run_golden(d, t, normals, outdir, W, H, true, isect);
+    }
+    if (mode == "list")
+    {
+        // list <scene> <outdir> <W> <H> <x0> <y0> <x1> <y1> <frame>: BVH-ref lists + scissor box
+        if (argc < 11 || d.spheres) return 2;
+        std::string outdir = argv[3];
+        int W = atoi(argv[4]), H = atoi(argv[5]);
+        int sb[4] = { atoi(argv[6]), atoi(argv[7]), atoi(argv[8]), atoi(argv[9]) };
+        uint32_t frame_num = uint32_t(strtoul(argv[10], nullptr, 10));
+        aligned_vector<tri_t> t;
+        if (d.grid == 0) make_cornell(t); else if (d.layers) make_hfstack(d.grid, d.layers, t); else make_heightfield(d.grid, t);
+        return run_list(d, t, outdir, W, H, sb, frame_num);
     }
     if (mode == "sah")
     {

@@ -612,6 +612,24 @@ static inline void primary_ray(const vo_camera* cam, unsigned x, unsigned y, v3*
 }
 
 typedef struct { float color[4]; uint32_t prim_id; float t; uint8_t occ; uint32_t list_index; uint32_t rays; } px_out;
+
+/* closest_hit / any_hit over a list of BVH refs (traverse_linear.inl:76-141): each BVH traversed
+ * with a fresh result and the same max_t; hr merged by update_if(result, hr, is_closer(hr, result,
+ * max_t)) (update_if.h:27-79, hit_record.h:54-64: strictly closer); exit_traversal<AnyHit> after
+ * every merge (exit_traversal.h:49-56) */
+static vo_hit trace(const vo_scene* s, const float o[3], const float d[3], int any, float max_t, vo_counters* cnt)
+{
+    if (!s->next) return vo_intersect_masked(o, d, s->nodes, s->indices, s->prims, s->kind, any, max_t, s->hit_mask, cnt);
+    vo_hit res;
+    memset(&res, 0, sizeof(res));
+    res.t = FLT_MAX;                      /* hit_record ctor: t = numeric_limits<float>::max() */
+    for (const vo_scene* b = s; b; b = b->next) {
+        vo_hit hr = vo_intersect_masked(o, d, b->nodes, b->indices, b->prims, b->kind, any, max_t, s->hit_mask, cnt);
+        if (hr.hit && hr.t >= 0.0f && hr.t < res.t && hr.t < max_t) res = hr;
+        if (any && res.hit) break;
+    }
+    return res;
+}
 static void shade_simple(const vo_scene* s, const vo_kernel* k, v3 ori, v3 dir, const vo_hit* hr, float out[4]);
 static void shade_whitted(const vo_scene* s, const vo_kernel* k, v3 ori, v3 dir, vo_hit hr, float out[4],
                           uint32_t* rays, vo_counters* cnt);
@@ -626,7 +644,7 @@ static px_out shade_pixel(const vo_scene* s, const vo_camera* cam, const vo_kern
     v3 ori, dir;
     primary_ray(cam, x, y, &ori, &dir);
     float fo[3] = { ori.x, ori.y, ori.z }, fd[3] = { dir.x, dir.y, dir.z };
-    vo_hit hr = vo_intersect_masked(fo, fd, s->nodes, s->indices, s->prims, s->kind, 0, FLT_MAX, s->hit_mask, cnt);
+    vo_hit hr = trace(s, fo, fd, 0, FLT_MAX, cnt);
     if (!hr.hit) return o;
     o.prim_id = hr.prim_id; o.t = hr.t; o.list_index = hr.list_index;
     if (k->mode == VO_MODE_SIMPLE) {
@@ -652,7 +670,7 @@ static px_out shade_pixel(const vo_scene* s, const vo_camera* cam, const vo_kern
     for (int smp = 0; smp < k->samples; ++smp) {
         float sx = 0.0f, sy = 0.0f;
         for (uint32_t kk = 0; kk < 16; ++kk) {
-            uint32_t ctr = ((p * 8u + (uint32_t)smp) * 16u + kk) * 2u;
+            uint32_t ctr = ((p * 8u + (uint32_t)smp) * 16u + kk) * 2u + k->frame_num * 0x9E3779B1u;
             float xa = 2.0f * vo_uniform(ctr) - 1.0f;
             float ya = 2.0f * vo_uniform(ctr + 1) - 1.0f;
             if (xa * xa + ya * ya < 1.0f) { sx = xa; sy = ya; break; }
@@ -661,7 +679,7 @@ static px_out shade_pixel(const vo_scene* s, const vo_camera* cam, const vo_kern
         v3 d = normalize(add(add(smul(sx, bu), smul(sy, bv)), smul(sz, n)));
         v3 ao = add(isect_pos, muls(d, k->eps));
         float ao_o[3] = { ao.x, ao.y, ao.z }, ao_d[3] = { d.x, d.y, d.z };
-        vo_hit ar = vo_intersect_masked(ao_o, ao_d, s->nodes, s->indices, s->prims, s->kind, 1, k->radius, s->hit_mask, cnt);
+        vo_hit ar = trace(s, ao_o, ao_d, 1, k->radius, cnt);
         o.rays++;
         if (ar.hit) { clr = clr - step; o.occ |= (uint8_t)(1u << smp); }
     }
@@ -854,6 +872,11 @@ uint64_t vo_render_rows(const vo_scene* s, const vo_camera* cam, const vo_kernel
 {
     uint64_t rays = 0, nbox = 0, nprim = 0;
     int W = cam->width;
+    const unsigned* sb = cam->scissor;
+    const int whole = sb[0] == 0 && sb[1] == 0 && sb[2] == 0 && sb[3] == 0;
+    const int cx0 = whole ? 0 : (int)sb[0], cy0 = whole ? 0 : (int)sb[1];
+    const int cx1 = whole ? W : (int)(sb[2] < (unsigned)W ? sb[2] : (unsigned)W);
+    const int cy1 = whole ? cam->height : (int)(sb[3] < (unsigned)cam->height ? sb[3] : (unsigned)cam->height);
 #ifdef _OPENMP
     if (threads <= 0) threads = omp_get_max_threads();
 #else
@@ -862,7 +885,8 @@ uint64_t vo_render_rows(const vo_scene* s, const vo_camera* cam, const vo_kernel
     #pragma omp parallel for schedule(dynamic, 1) num_threads(threads) reduction(+:rays,nbox,nprim)
     for (int y = y0; y < y1; ++y) {
         vo_counters c = { 0, 0 };
-        for (int x = 0; x < W; ++x) {
+        if (y < cy0 || y >= cy1) continue;              /* outside the scissor box: not written */
+        for (int x = cx0; x < cx1; ++x) {
             px_out o = shade_pixel(s, cam, k, (unsigned)x, (unsigned)y, &c);
             size_t p = (size_t)y * W + x;
             if (color) memcpy(color + 4 * p, o.color, 16);

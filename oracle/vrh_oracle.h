@@ -91,15 +91,24 @@ int vo_intersect_multi_masked(const float ori[3], const float dir[3], const vo_n
                               vo_counters* cnt);
 
 /* ---- a frame, simple_sched order (row-major), over rows [y0, y1) ---- */
-typedef struct {
+typedef struct vo_scene vo_scene;
+struct vo_scene {
     const vo_node* nodes; const uint32_t* indices; const void* prims; int kind;
     const vo_vec3* normals;               /* per prim_id (AO; simple kernel, per-face binding) */
     const vo_vec3* vertex_normals;        /* 3 per prim_id (simple kernel, per-vertex binding) */
     const vo_hit_mask* hit_mask;          /* mask intersector for every ray (NULL: none) */
-} vo_scene;
+    /* BVH-ref list (traverse_linear.inl:76-141): the next BVH of the list (NULL: last).  Primary /
+     * AO rays traverse every BVH on its own and merge with update_if(result, hr, is_closer(hr,
+     * result, max_t)); any hit stops at the first BVH with a hit.  normals / vertex_normals /
+     * hit_mask are the first entry's. */
+    const vo_scene* next;
+};
 typedef struct {
     float eye[3], cam_u[3], cam_v[3], cam_w[3];
     int   width, height;
+    /* scissor box as cuda_sched reads it (cuda_sched.inl:71): pixels x0 <= x < x1, y0 <= y < y1 are
+     * rendered, the others not written; all zero = whole image */
+    unsigned scissor[4];
 } vo_camera;
 typedef struct {
     int   mode;                           /* VO_MODE_PRIMARY | VO_MODE_AO | VO_MODE_SIMPLE */
@@ -114,6 +123,9 @@ typedef struct {
     int   normal_binding;                 /* VO_NORMALS_PER_FACE | VO_NORMALS_PER_VERTEX */
     int   max_hits;                       /* VO_MODE_MULTI_HIT: N (<= VO_MAX_HITS) */
     int   num_bounces;                    /* VO_MODE_WHITTED (eps = scene epsilon) */
+    /* frame number (cuda_sched::frame's frame_num): the AO sampler counter of frame n is
+     * ((p*8 + s)*16 + k)*2 + n * 0x9E3779B1 (u32 wrap); frame 0 = SURVEY.md Appendix A */
+    uint32_t frame_num;
 } vo_kernel;
 
 /* deterministic per-vertex normals for tests: prim k, vertex j: normalize(n_k + 0.4 * (U(b) - 0.5,

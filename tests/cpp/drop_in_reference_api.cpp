@@ -81,7 +81,7 @@ int main(int argc, char** argv)
             hip_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> one;
             one.resize(W, H);
             auto sp = make_sched_params(pixel_sampler::uniform_type{}, cams[f], one);
-            sched.frame(kern, sp);
+            sched.frame(kern, sp, unsigned(f));       // frame f of the batch has frame number f
             one.download(color.data(), pid.data(), t.data(), occ.data());
             batch_ok = batch_ok && std::memcmp(color.data(), color3.data() + 4 * f * n, 16 * n) == 0
                 && std::memcmp(pid.data(), pid3.data() + f * n, 4 * n) == 0

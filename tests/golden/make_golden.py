@@ -8,6 +8,8 @@ Run in the build container (needs /root/reference to build the harness):
     python tests/golden/make_golden.py --sah                            (only the sah_cost values)
     python tests/golden/make_golden.py --whitted                        (only the whitted cases)
     python tests/golden/make_golden.py --mask                           (only the mask-intersector cases)
+    python tests/golden/make_golden.py --frames                         (only the frame-number cases)
+    python tests/golden/make_golden.py --list                           (only the BVH-list + scissor cases)
 
 For every case the reference harness renders a full simple_sched<basic_ray<float>> frame
 (primary closest_hit + the Appendix-A AO kernel for triangle scenes) and this script stores:
@@ -78,6 +80,25 @@ WHITTED_CASES = [
 MASK_CASES = [
     ("mask_hf200_320x180", "hf200", 320, 180, 128),
     ("mask_hf64_160x90", "hf64", 160, 90, 37),
+]
+
+
+# frame-number cases (harness "golden" mode with a frame number: the AO sampler of frame n, vrh.h
+# vrh_render): name, scene, W, H, frame number, full frame?
+FRAME_CASES = [
+    ("frame7_hf64_160x90", "hf64", 160, 90, 7, True),
+    ("frame1_hf200_320x180", "hf200", 320, 180, 1, True),
+    ("frame3_hf1M", "hf1M", 1920, 1080, 3, False),
+]
+
+
+# BVH-ref list + scissor cases (harness "list" mode: the scene's triangles split by prim_id parity
+# into two BVHs, closest_hit / any_hit over the list, tiled_sched with a scissor box): name, scene,
+# W, H, scissor (x0, y0, x1, y1: pixels x0 <= x < x1, y0 <= y < y1), frame number
+LIST_CASES = [
+    ("list_hf64_160x90", "hf64", 160, 90, (17, 9, 141, 77), 3),
+    ("list_hf200_320x180", "hf200", 320, 180, (40, 30, 300, 150), 0),
+    ("list_cornell12_128", "cornell12", 128, 128, (5, 0, 128, 100), 11),
 ]
 
 
@@ -170,6 +191,53 @@ def mask_cases(out):
             print(case, rec["hits"], rec["ao_occluded"], flush=True)
 
 
+def frame_cases(out, rng):
+    for case, scene, W, H, frame, full in FRAME_CASES:
+        with tempfile.TemporaryDirectory() as d:
+            r = subprocess.run([REF, "golden", scene, d, str(W), str(H), str(frame)], check=True, capture_output=True,
+                               text=True)
+            info = json.loads(r.stdout.strip().splitlines()[-1])
+            pid = np.fromfile(os.path.join(d, "prim_id.bin"), np.uint32)
+            t = np.fromfile(os.path.join(d, "t.bin"), np.float32)
+            occ = np.fromfile(os.path.join(d, "occ.bin"), np.uint8)
+            color = np.fromfile(os.path.join(d, "color.bin"), np.float32).reshape(-1, 4)
+            rec = {"scene": scene, "W": W, "H": H, "frame": frame, "hits": info["hits"], "ao_rays": info["ao_rays"],
+                   "ao_occluded": info["ao_occluded"], "primid_hash": fnv1a(pid), "t_hash": fnv1a(t),
+                   "occ_hash": fnv1a(occ), "color_hash": fnv1a(color)}
+            if full:
+                np.savez_compressed(os.path.join(HERE, case + ".npz"), prim_id=pid, t=t, occ=occ, color=color)
+            else:
+                pix = np.sort(rng.choice(W * H, 4096, replace=False)).astype(np.uint32)
+                np.savez_compressed(os.path.join(HERE, case + ".npz"), pixels=pix, prim_id=pid[pix], t=t[pix],
+                                    occ=occ[pix], color=color[pix])
+            out[case] = rec
+            print(case, rec["hits"], rec["ao_occluded"], rec["occ_hash"], flush=True)
+
+
+def list_cases(out):
+    for case, scene, W, H, sb, frame in LIST_CASES:
+        with tempfile.TemporaryDirectory() as d:
+            r = subprocess.run([REF, "list", scene, d, str(W), str(H)] + [str(v) for v in sb] + [str(frame)],
+                               check=True, capture_output=True, text=True)
+            info = json.loads(r.stdout.strip().splitlines()[-1])
+            arr = {k: np.fromfile(os.path.join(d, k + ".bin"), dt) for k, dt in
+                   (("prim_id", np.uint32), ("t", np.float32), ("occ", np.uint8), ("leaf_pos", np.uint32))}
+            arr["color"] = np.fromfile(os.path.join(d, "color.bin"), np.float32).reshape(-1, 4)
+            for k in (0, 1):
+                arr[f"bvh{k}_nodes"] = np.fromfile(os.path.join(d, f"bvh{k}_nodes.bin"), np.uint32)
+                arr[f"bvh{k}_indices"] = np.fromfile(os.path.join(d, f"bvh{k}_indices.bin"), np.uint32)
+                arr[f"bvh{k}_prims"] = np.fromfile(os.path.join(d, f"bvh{k}_prims.bin"), np.uint8)
+            rec = {"scene": scene, "W": W, "H": H, "scissor": list(sb), "frame": frame, "hits": info["hits"],
+                   "ao_rays": info["ao_rays"], "ao_occluded": info["ao_occluded"],
+                   "primid_hash": fnv1a(arr["prim_id"]), "t_hash": fnv1a(arr["t"]), "occ_hash": fnv1a(arr["occ"]),
+                   "color_hash": fnv1a(arr["color"])}
+            for k in ("primid_hash", "t_hash", "color_hash"):
+                assert rec[k] == info[k], (case, k, rec[k], info[k])
+            np.savez_compressed(os.path.join(HERE, case + ".npz"), **arr)
+            out[case] = rec
+            print(case, rec["hits"], rec["ao_occluded"], flush=True)
+
+
 def sah_cases(out):
     rec = {}
     for scene in SAH_SCENES:
@@ -183,7 +251,7 @@ def sah_cases(out):
 def main():
     if not os.path.exists(REF):
         sys.exit("build the reference harness first: make -C oracle ref")
-    only_shade = any(f in sys.argv for f in ("--shade", "--multi", "--sah", "--whitted", "--mask"))
+    only_shade = any(f in sys.argv for f in ("--shade", "--multi", "--sah", "--whitted", "--mask", "--frames", "--list"))
     path = os.path.join(HERE, "golden.json")
     out = json.load(open(path)) if only_shade else {}
     rng = np.random.default_rng(12345)
@@ -215,7 +283,11 @@ def main():
                                     occ=occ[pix], color=color[pix])
             out[case] = rec
             print(case, rec["hits"], rec["ao_occluded"], rec["primid_hash"], flush=True)
-    if "--mask" in sys.argv:
+    if "--frames" in sys.argv:
+        frame_cases(out, np.random.default_rng(2468))
+    elif "--list" in sys.argv:
+        list_cases(out)
+    elif "--mask" in sys.argv:
         mask_cases(out)
     elif "--whitted" in sys.argv:
         whitted_cases(out, np.random.default_rng(777))
@@ -228,6 +300,8 @@ def main():
         sah_cases(out)
         whitted_cases(out, np.random.default_rng(777))
         mask_cases(out)
+        frame_cases(out, np.random.default_rng(2468))
+        list_cases(out)
     with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 

@@ -8,11 +8,13 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 AO_HIP = os.path.join(ROOT, "build", "examples", "ao_hip")
+AO_MULTI = os.path.join(ROOT, "build", "examples", "ao_multi_gpu")
 DROPIN = os.path.join(ROOT, "oracle", "_ref", "dropin_ref_api")
 
 
-def test_cpp_headers_compile_standalone(tmp_path):
-    src = os.path.join(ROOT, "examples", "ao_hip.cpp")
+@pytest.mark.parametrize("example", ["ao_hip.cpp", "ao_multi_gpu.cpp"])
+def test_cpp_headers_compile_standalone(tmp_path, example):
+    src = os.path.join(ROOT, "examples", example)
     subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), src],
                    check=True)
 
@@ -51,6 +53,18 @@ def test_cpp_example_matches_reference(golden, case, grid):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("case,grid,shards", [("hf200_320x180", 200, 0), ("hf200_320x180", 200, 3), ("hf1M", 708, 8)])
+def test_cpp_multi_gpu_example_matches_reference(golden, case, grid, shards):
+    """examples/ao_multi_gpu.cpp: a render group over every visible GPU (one on the test box, so
+    `shards` > 1 makes the one GPU render several shards and run the RCCL exchange with itself)."""
+    g = golden[case]
+    out = _run(AO_MULTI, grid, g["W"], g["H"], 2, shards)
+    assert out["matches_one_gpu"]
+    for k in ("primid_hash", "t_hash", "occ_hash", "color_hash"):
+        assert out[k] == g[k], k
+
+
+@pytest.mark.gpu
 @pytest.mark.skipif(not os.path.exists(DROPIN), reason="drop-in binary is built in the build container only")
 def test_reference_api_program_on_hip_backend(golden):
     g = golden["hf200_320x180"]
@@ -58,6 +72,18 @@ def test_reference_api_program_on_hip_backend(golden):
     for k in ("primid_hash", "t_hash", "occ_hash", "color_hash"):
         assert out[k] == g[k], k
     assert out["batch_ok"], "hip_sched::frames: a frame of the batch differs from its own frame()"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,grid,shards", [("hf200_320x180", 200, 0), ("hf200_320x180", 200, 3), ("hf1M", 708, 8)])
+def test_cpp_multi_gpu_example_matches_reference(golden, case, grid, shards):
+    """examples/ao_multi_gpu.cpp: a render group over every visible GPU (one on the test box, so
+    `shards` > 1 makes the one GPU render several shards and run the RCCL exchange with itself)."""
+    g = golden[case]
+    out = _run(AO_MULTI, grid, g["W"], g["H"], 2, shards)
+    assert out["matches_one_gpu"]
+    for k in ("primid_hash", "t_hash", "occ_hash", "color_hash"):
+        assert out[k] == g[k], k
 
 
 @pytest.mark.gpu

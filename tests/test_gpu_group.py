@@ -1,0 +1,147 @@
+"""GPU: multi-GPU render groups (vrh_group_* / vrh_render_sharded) on the one-GPU box.
+
+A one-rank group renders S > 1 image-tile shards on this GPU and runs the whole exchange of the
+N-GPU path -- packed shard renders, one ncclSend / ncclRecv pair per shard over RCCL (here rank 0
+sending to itself), the un-interleave on the root -- so the code bench.py runs at N > 1 runs here;
+only the peer index of each send / receive differs.  Bar: the gathered frame is bit-identical to the
+one-GPU frame and, for hf10M 1080p AO in 8 shards, its hashes equal the reference's own.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import visionaray_amd as va
+from visionaray_amd import _capi, scenes
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+_cache = {}
+
+
+def device_scene(ctx, name):
+    if name not in _cache:
+        prims = scenes.primitives(name)
+        b = va.build_index_bvh(prims)
+        _cache[name] = (b, va.hip_index_bvh(ctx, b, scenes.normals_for(prims)))
+    return _cache[name]
+
+
+@pytest.fixture(scope="module")
+def group(ctx):
+    g = va.render_group(ctx, 1, 0, va.render_group.unique_id())     # ncclCommInitRank, one rank
+    yield g
+    g.close()
+
+
+def single_frames(ctx, dev, kern, basis, W, H, frames, frame_num):
+    out = []
+    for f in range(frames):
+        rt = va.hip_buffer_rt(ctx, W, H)
+        va.render(ctx, dev, rt, basis, kern, None, frame_num=frame_num + f)
+        out.append(rt.download())
+        rt.close()
+    return out
+
+
+def sharded(ctx, group, dev, kern, basis, W, H, frames, frame_num, shards, fields):
+    dst = va.hip_buffer_rt(ctx, W, H * frames)
+    dst.clear_color_buffer((0, 0, 0, 0))
+    group.render(dev, kern, dst, [basis] * frames, frame_num=frame_num, shards=shards, fields=fields)
+    group.sync()
+    out = dst.download()
+    dst.close()
+    return out
+
+
+def test_hf10M_ao_in_8_shards_equals_reference_hashes(ctx, group, golden, oracle_mod):
+    g = golden["hf10M"]
+    host, dev = device_scene(ctx, "hf10M")
+    cam, W, H = scenes.scene_camera("hf10M")
+    fields = _capi.VRH_RT_COLOR | _capi.VRH_RT_PRIM_ID | _capi.VRH_RT_OCC | _capi.VRH_RT_T
+    out = sharded(ctx, group, dev, va.ao_kernel(dev), cam.basis(W, H), W, H, 1, 0, 8, fields)
+    O = oracle_mod
+    assert O.fnv1a(out["prim_id"]) == g["primid_hash"]
+    assert O.fnv1a(out["t"]) == g["t_hash"]
+    assert O.fnv1a(out["occ"]) == g["occ_hash"]
+    assert O.fnv1a(out["color"]) == g["color_hash"]
+
+
+@pytest.mark.parametrize("shards,frames", [(2, 1), (3, 4), (8, 2), (135, 1)])
+def test_sharded_frames_equal_single_gpu_frames(ctx, group, shards, frames):
+    """Frames in flight through the group (frame numbers 7, 8, ...), every buffer gathered."""
+    host, dev = device_scene(ctx, "hf200")
+    W, H = 320, 180
+    cam, _, _ = scenes.scene_camera("hf200", W, H)
+    basis = cam.basis(W, H)
+    kern = va.ao_kernel(dev)
+    out = sharded(ctx, group, dev, kern, basis, W, H, frames, 7, shards, _capi.VRH_RT_ALL)
+    n = W * H
+    for f, ref in enumerate(single_frames(ctx, dev, kern, basis, W, H, frames, 7)):
+        for k in ("prim_id", "t", "occ", "color"):
+            assert np.array_equal(out[k][f * n:(f + 1) * n].view(np.uint8), ref[k].view(np.uint8)), (k, f)
+
+
+def test_sharded_primary_spheres_and_shading_colour(ctx, group):
+    """Sphere primary visibility (colour re-derived from prim ids) and simple::kernel (RGBA32F
+    colour on the wire) through the group."""
+    host, dev = device_scene(ctx, "sph5000")
+    W, H = 256, 144
+    cam, _, _ = scenes.scene_camera("sph5000", W, H)
+    basis = cam.basis(W, H)
+    kern = va.closest_hit_kernel(dev)
+    out = sharded(ctx, group, dev, kern, basis, W, H, 1, 0, 5, _capi.VRH_RT_COLOR | _capi.VRH_RT_PRIM_ID)
+    ref = single_frames(ctx, dev, kern, basis, W, H, 1, 0)[0]
+    assert np.array_equal(out["prim_id"], ref["prim_id"])
+    assert np.array_equal(out["color"].view(np.uint32), ref["color"].view(np.uint32))
+
+    host, dev = device_scene(ctx, "hf64")
+    W, H = 160, 90
+    cam, _, _ = scenes.scene_camera("hf64", W, H)
+    basis = cam.basis(W, H)
+    mats = [va.plastic(cd=(0.8, 0.3, 0.2), ks=0.4, cs=(1, 1, 1), exp=32.0)]
+    lights = [va.point_light((1.0, 2.0, 1.0))]
+    sh = va.shading(ctx, mats, lights)
+    kern = va.simple_kernel(dev, sh)
+    out = sharded(ctx, group, dev, kern, basis, W, H, 1, 0, 3, _capi.VRH_RT_COLOR)
+    ref = single_frames(ctx, dev, kern, basis, W, H, 1, 0)[0]
+    assert np.array_equal(out["color"].view(np.uint32), ref["color"].view(np.uint32))
+
+
+def test_group_scissor_and_local_group(ctx):
+    """vrh_group_create_local (ncclCommInitAll over the visible device) and a scissor box: pixels
+    outside the box stay as the root's target was cleared."""
+    (g,) = va.render_group.local([ctx])
+    host, dev = device_scene(ctx, "hf64")
+    W, H = 160, 90
+    cam, _, _ = scenes.scene_camera("hf64", W, H)
+    basis = cam.basis(W, H)
+    basis.scissor[:] = [10, 20, 150, 61]
+    kern = va.ao_kernel(dev)
+    dst = va.hip_buffer_rt(ctx, W, H)
+    dst.clear_color_buffer((0.5, 0.5, 0.5, 1.0))
+    g.render(dev, kern, dst, [basis], shards=4)
+    g.sync()
+    out = dst.download()
+    rt = va.hip_buffer_rt(ctx, W, H)
+    rt.clear_color_buffer((0.5, 0.5, 0.5, 1.0))
+    va.render(ctx, dev, rt, basis, kern, None)
+    ref = rt.download()
+    for k in ("prim_id", "occ", "color"):
+        assert np.array_equal(out[k].view(np.uint8), ref[k].view(np.uint8)), k
+    inside = np.zeros((H, W), bool)
+    inside[20:61, 10:150] = True
+    assert (out["prim_id"].reshape(H, W)[~inside] == 0xFFFFFFFF).all()
+    g.close()
+
+
+def test_group_argument_errors(ctx, group):
+    host, dev = device_scene(ctx, "hf64")
+    cam, _, _ = scenes.scene_camera("hf64", 160, 90)
+    basis = cam.basis(160, 90)
+    small = va.hip_buffer_rt(ctx, 160, 45)
+    with pytest.raises(va.VrhError):          # the root's target must be W x (H * frames)
+        group.render(dev, va.ao_kernel(dev), small, [basis])
+    with pytest.raises(va.VrhError):          # AO masks of more than 8 samples do not fit a byte
+        group.render(dev, va.ao_kernel(dev, samples=12), va.hip_buffer_rt(ctx, 160, 90), [basis],
+                     fields=_capi.VRH_RT_OCC)

@@ -1,7 +1,7 @@
 """GPU: every traversal schedule and record width reaches the same bit-exact result.
 
 The kernel has several ways to organise a wave's work (vrh.h VRH_OPT_AO_SCHEDULE: whole descend-
-to-leaf steps, single items, items by vote, two-pass AO; VRH_OPT_WIDE_ANYHIT: 4-wide any-hit records).  Only
+to-leaf steps, single items for primary visibility; VRH_OPT_WIDE_ANYHIT: 4-wide any-hit records).  Only
 the defaults run in test_gpu_parity.py; here the parity cases are re-run under each non-default
 choice, on the same context, so none of the paths can drift from the reference.
 """
@@ -20,24 +20,19 @@ VARIANTS = {
     "step": {"ao_schedule": 3},
     "item": {"ao_schedule": 4},
     "item_refill1": {"ao_schedule": 4, "refill_min": 1},
-    "vote": {"ao_schedule": 5},
-    "vote_leafheavy": {"ao_schedule": 5, "vote_leaf": 64},
+    "global_queue": {"xcd_queues": 2},
     "step_wide": {"ao_schedule": 3, "wide_anyhit": 1},
     "step_wide_exact": {"ao_schedule": 3, "wide_anyhit": 1, "exact_minmax": 1},
     "step_cap1": {"ao_schedule": 3, "descent_cap": 1},
     "step_refill24": {"ao_schedule": 3, "refill_min": 24},
     "step_cap3_wide": {"ao_schedule": 3, "descent_cap": 3, "wide_anyhit": 1},
-    "two_pass": {"ao_schedule": 6},
-    "two_pass_wide_refill1": {"ao_schedule": 6, "wide_anyhit": 1, "refill_min": 1},
-    "two_pass_global_queue": {"ao_schedule": 6, "xcd_queues": 2},
     "step_pop_on_miss": {"ao_schedule": 3, "pop_on_miss": 1},
     "step_pop_cap2_wide": {"ao_schedule": 3, "pop_on_miss": 1, "descent_cap": 2, "wide_anyhit": 1},
     "coop": {"ao_schedule": 3, "coop_fetch": 1},
+    "coop_wide": {"ao_schedule": 3, "coop_fetch": 1, "wide_anyhit": 1},
     "coop_exact_pop_cap3": {"ao_schedule": 3, "coop_fetch": 1, "exact_minmax": 1, "pop_on_miss": 1, "descent_cap": 3},
-    "coop_two_pass": {"ao_schedule": 6, "coop_fetch": 1},
     "scalar_off": {"ao_schedule": 3, "scalar_fetch": 2},
     "scalar_off_pop_cap2": {"ao_schedule": 3, "scalar_fetch": 2, "pop_on_miss": 1, "descent_cap": 2},
-    "two_pass_occ5": {"ao_schedule": 6, "waves_per_simd": 5},
     "occ5": {"ao_schedule": 3, "waves_per_simd": 5},
     "occ6": {"ao_schedule": 3, "waves_per_simd": 6},
     # the primary-visibility defaults switched off (pop on miss, descent cap 8, item refill 32)
@@ -46,7 +41,7 @@ VARIANTS = {
     # scenes uploaded with the line-paired record layout (the option is read at upload)
     "pair_layout": {"pair_layout": 1},
 }
-OPTIONS = ("ao_schedule", "refill_min", "vote_leaf", "wide_anyhit", "exact_minmax", "descent_cap", "xcd_queues",
+OPTIONS = ("ao_schedule", "refill_min", "wide_anyhit", "exact_minmax", "descent_cap", "xcd_queues",
            "pop_on_miss", "coop_fetch", "scalar_fetch", "waves_per_simd", "pair_layout")
 
 

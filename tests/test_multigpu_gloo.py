@@ -1,7 +1,10 @@
-"""CPU, world_size 2 and 3 over gloo: the N>1 path of bench.py (band sharding, packed shard buffers,
-gather to rank 0, un-interleave, ray-count sum and max-over-ranks timing) reproduces the
-single-process frame bit for bit.  The per-rank renderer here is the oracle restricted to the
-rank's rows (the GPU box runs the same plumbing with libvrh shards over RCCL)."""
+"""CPU, world_size 2 and 3 over gloo: the protocol of libvrh's render groups (vrh_render_sharded,
+restated in visionaray_amd/multigpu.py) -- shard ownership s -> rank s % N, packed shard buffers
+of several frames on the wire as [prim ids | AO masks], point-to-point sends / receives paired in
+plan order, the root's un-interleave and colour re-derivation, the ray-count sum and max-over-ranks
+timing of bench.py -- reproduces the single-process frames bit for bit, including S > N shards.
+The per-rank renderer is the oracle restricted to the shard's rows; on the GPU box the same
+protocol runs inside libvrh over RCCL (tests/test_gpu_group.py: a one-rank group with S shards)."""
 import os
 import socket
 
@@ -13,7 +16,8 @@ import torch.multiprocessing as mp
 
 from visionaray_amd import multigpu
 
-SCENE, W, H = "hf64", 160, 90
+SCENE, W, H, FRAMES, FRAME0 = "hf64", 160, 90, 2, 4
+BG = (0.1, 0.2, 0.3, 1.0)
 
 
 def _free_port():
@@ -24,65 +28,97 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, shards, port, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from oracle import oracle as O
         sc = O.make_scene(SCENE)
         cam = O.scene_camera(SCENE, W, H)
-        rm = multigpu.rows_max(H, world)
-        rows = multigpu.packed_rows(H, rank, world)
-        loc_color = np.zeros((rm * W, 4), np.float32)
-        loc_pid = np.full(rm * W, 0xFFFFFFFF, np.uint32)
+        rm = multigpu.rows_max(H, shards)
+        lay, nbytes = multigpu.wire_layout(FRAMES, rm, W)
+        sends, recvs = multigpu.exchange_plan(rank, world, shards)
         rays = 0
-        for lr, y in enumerate(rows):
-            if y < 0:
-                continue
-            out = O.render(sc, cam, mode=O.VO_MODE_AO, rows=(int(y), int(y) + 1), threads=1)
-            loc_color[lr * W:(lr + 1) * W] = out["color"][y * W:(y + 1) * W]
-            loc_pid[lr * W:(lr + 1) * W] = out["prim_id"][y * W:(y + 1) * W]
-            rays += out["rays"]
-        tc = torch.from_numpy(loc_color)
-        tp = torch.from_numpy(loc_pid.view(np.int32))
-        outs = None
+        bufs = []
+        for s, _ in sends:                           # render every owned shard, packed
+            buf = np.zeros(nbytes, np.uint8)
+            pid = buf[lay["pid"][0]:lay["pid"][0] + lay["pid"][1]].view(np.uint32).reshape(FRAMES, rm * W)
+            occ = buf[lay["occ"][0]:lay["occ"][0] + lay["occ"][1]].reshape(FRAMES, rm * W)
+            pid[:] = 0xFFFFFFFF
+            for f in range(FRAMES):
+                for lr, y in enumerate(multigpu.packed_rows(H, s, shards)):
+                    if y < 0:
+                        continue
+                    out = O.render(sc, cam, mode=O.VO_MODE_AO, rows=(int(y), int(y) + 1), threads=1,
+                                   frame_num=FRAME0 + f)
+                    pid[f, lr * W:(lr + 1) * W] = out["prim_id"][y * W:(y + 1) * W]
+                    occ[f, lr * W:(lr + 1) * W] = out["occ"][y * W:(y + 1) * W]
+                    rays += out["rays"]
+            bufs.append(torch.from_numpy(buf))
+        # the exchange: sends to the root in plan order; the root receives shard s from s % N
+        gathered = np.zeros((shards, nbytes), np.uint8) if rank == 0 else None
+        reqs = [dist.isend(b, dst=0) for b, (s, peer) in zip(bufs, sends) if rank != 0]
         if rank == 0:
-            outs = [torch.empty((world,) + tuple(tc.shape), dtype=tc.dtype),
-                    torch.empty((world,) + tuple(tp.shape), dtype=tp.dtype)]
-        multigpu.gather_to_root(dist, [tc, tp], rank, world, outs)
+            mine = dict(zip([s for s, _ in sends], bufs))
+            for s, peer in recvs:
+                if peer == 0:
+                    gathered[s] = mine[s].numpy()
+                else:
+                    t = torch.empty(nbytes, dtype=torch.uint8)
+                    dist.recv(t, src=peer)
+                    gathered[s] = t.numpy()
+        for r in reqs:
+            r.wait()
         stats = torch.tensor([float(rank + 1), float(rays)], dtype=torch.float64)
         mx, sm = stats.clone(), stats.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         if rank == 0:
-            color = multigpu.unshard_host(outs[0].numpy(), W, H, world)
-            pid = multigpu.unshard_host(outs[1].numpy().view(np.uint32), W, H, world)
-            np.save(os.path.join(outdir, "color.npy"), color)
-            np.save(os.path.join(outdir, "pid.npy"), pid)
+            for f in range(FRAMES):
+                gp = gathered[:, lay["pid"][0]:lay["pid"][0] + lay["pid"][1]].view(np.uint32).reshape(shards, FRAMES, rm * W)[:, f]
+                go = gathered[:, lay["occ"][0]:lay["occ"][0] + lay["occ"][1]].reshape(shards, FRAMES, rm * W)[:, f]
+                pid = multigpu.unshard_host(gp, W, H, shards)
+                occ = multigpu.unshard_host(go, W, H, shards)
+                np.save(os.path.join(outdir, f"pid{f}.npy"), pid)
+                np.save(os.path.join(outdir, f"occ{f}.npy"), occ)
+                np.save(os.path.join(outdir, f"color{f}.npy"), multigpu.derive_colour(pid, occ, BG))
             np.save(os.path.join(outdir, "stats.npy"), np.array([mx[0].item(), sm[1].item()]))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_gather_equals_single_frame(tmp_path, oracle_mod, world):
+@pytest.mark.parametrize("world,shards", [(2, 2), (3, 3), (2, 5)])
+def test_sharded_exchange_equals_single_frames(tmp_path, oracle_mod, world, shards):
     O = oracle_mod
-    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, shards, _free_port(), str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
-    full = O.render(O.make_scene(SCENE), O.scene_camera(SCENE, W, H), mode=O.VO_MODE_AO)
-    color = np.load(tmp_path / "color.npy")
-    pid = np.load(tmp_path / "pid.npy")
     st = np.load(tmp_path / "stats.npy")
-    assert np.array_equal(pid, full["prim_id"])
-    assert np.array_equal(color.view(np.uint32), full["color"].view(np.uint32))
+    rays = 0
+    for f in range(FRAMES):
+        full = O.render(O.make_scene(SCENE), O.scene_camera(SCENE, W, H), mode=O.VO_MODE_AO, frame_num=FRAME0 + f)
+        rays += full["rays"]
+        assert np.array_equal(np.load(tmp_path / f"pid{f}.npy"), full["prim_id"])
+        assert np.array_equal(np.load(tmp_path / f"occ{f}.npy"), full["occ"])
+        assert np.array_equal(np.load(tmp_path / f"color{f}.npy").view(np.uint32), full["color"].view(np.uint32))
     assert st[0] == world                      # max over ranks
-    assert int(st[1]) == full["rays"]          # rays summed over ranks = whole frame
+    assert int(st[1]) == rays                  # rays summed over ranks = every frame
 
 
 def test_band_partition_covers_image_once():
     for Hh in (1, 17, 90, 1080):
-        for world in (1, 2, 3, 4, 8):
-            seen = np.concatenate([multigpu.packed_rows(Hh, r, world) for r in range(world)])
+        for shards in (1, 2, 3, 4, 8, 135):
+            seen = np.concatenate([multigpu.packed_rows(Hh, s, shards) for s in range(shards)])
             seen = seen[seen >= 0]
             assert np.array_equal(np.sort(seen), np.arange(Hh))
-            assert all(len(multigpu.packed_rows(Hh, r, world)) <= multigpu.rows_max(Hh, world) for r in range(world))
+            assert all(len(multigpu.packed_rows(Hh, s, shards)) <= multigpu.rows_max(Hh, shards) for s in range(shards))
+
+
+def test_exchange_plan_pairs_every_send_with_a_receive():
+    for world in (1, 2, 3, 8):
+        for shards in (1, world, world + 1, 3 * world):
+            recvs = multigpu.exchange_plan(0, world, shards)[1]
+            assert [s for s, _ in recvs] == list(range(shards))
+            for rank in range(world):
+                sends = multigpu.exchange_plan(rank, world, shards)[0]
+                # per peer, the root's receives from `rank` list the same shards in the same order
+                assert [s for s, _ in sends] == [s for s, p in recvs if p == rank]

@@ -63,7 +63,6 @@ for rnd in range(rounds):
         ctx.set_option("exact_minmax", v.get("exact_minmax", 0))
         ctx.set_option("xcd_queues", v.get("xcd_queues", 0))
         ctx.set_option("refill_min", v.get("refill_min", 0))
-        ctx.set_option("vote_leaf", v.get("vote_leaf", 0))
         ctx.set_option("wide_anyhit", v.get("wide_anyhit", 0))
         ctx.set_option("descent_cap", v.get("descent_cap", 0))
         ctx.set_option("pop_on_miss", v.get("pop_on_miss", 0))

@@ -23,7 +23,8 @@ VRH_RT_COLOR, VRH_RT_PRIM_ID, VRH_RT_T, VRH_RT_OCC, VRH_RT_ALL = 1, 2, 4, 8, 15
 
 class vrh_camera(C.Structure):
     _fields_ = [("eye", C.c_float * 3), ("cam_u", C.c_float * 3), ("cam_v", C.c_float * 3),
-                ("cam_w", C.c_float * 3), ("width", C.c_uint32), ("height", C.c_uint32)]
+                ("cam_w", C.c_float * 3), ("width", C.c_uint32), ("height", C.c_uint32),
+                ("scissor", C.c_uint32 * 4)]
 
 
 class vrh_kernel_desc(C.Structure):
@@ -47,10 +48,12 @@ VRH_KERNEL_COUNT_TESTS = 1
 VRH_BAND_ROWS = 8
 VRH_MAX_BATCH = 32
 VRH_OPT_BLOCK_THREADS, VRH_OPT_STACK_CAP, VRH_OPT_AO_SCHEDULE, VRH_OPT_BLOCKS_PER_CU = 1, 2, 3, 4
-VRH_OPT_WAVES_PER_SIMD, VRH_OPT_EXACT_MINMAX, VRH_OPT_XCD_QUEUES, VRH_OPT_REFILL_MIN, VRH_OPT_VOTE_LEAF = 5, 6, 7, 8, 9
+VRH_OPT_WAVES_PER_SIMD, VRH_OPT_EXACT_MINMAX, VRH_OPT_XCD_QUEUES, VRH_OPT_REFILL_MIN = 5, 6, 7, 8
 VRH_OPT_WIDE_ANYHIT, VRH_OPT_DESCENT_CAP, VRH_OPT_POP_ON_MISS, VRH_OPT_COOP_FETCH = 10, 11, 12, 13
 VRH_OPT_SCALAR_FETCH, VRH_OPT_PAIR_LAYOUT = 14, 15
 VRH_MAX_TIMED_FRAMES = 1024
+VRH_MAX_SCENE_LIST = 8
+VRH_GROUP_ID_BYTES = 128
 
 
 class vrh_accum_stats(C.Structure):
@@ -67,8 +70,10 @@ class vrh_frame_stats(C.Structure):
     _fields_ = [("kernel_ms", C.c_float), ("rays", C.c_uint64), ("hits", C.c_uint64), ("box_tests", C.c_uint64),
                 ("prim_tests", C.c_uint64), ("launches", C.c_uint32),
                 ("grid_blocks", C.c_uint32), ("block_threads", C.c_uint32), ("stack_depth", C.c_uint32),
+                ("frames", C.c_uint32),
                 ("wave_steps", C.c_uint64), ("busy_lane_steps", C.c_uint64), ("wave_box_iters", C.c_uint64),
-                ("wave_prim_iters", C.c_uint64), ("wave_box_uniform_iters", C.c_uint64)]
+                ("wave_prim_iters", C.c_uint64), ("wave_box_uniform_iters", C.c_uint64),
+                ("l1_lines", C.c_uint64), ("l1_segments", C.c_uint64), ("vmem_instrs", C.c_uint64)]
 
 
 class vrh_scene_info(C.Structure):
@@ -76,7 +81,7 @@ class vrh_scene_info(C.Structure):
                 ("prim_kind", C.c_uint32), ("max_depth", C.c_uint32), ("device_bytes", C.c_uint64),
                 ("wide_records", C.c_uint32), ("wide_depth", C.c_uint32), ("max_prim_id", C.c_uint32),
                 ("max_geom_id", C.c_uint32), ("vertex_normals", C.c_uint32), ("gpu_built", C.c_uint32),
-                ("build_ms", C.c_float)]
+                ("build_ms", C.c_float), ("num_bvhs", C.c_uint32)]
 
 
 class vrh_build_desc(C.Structure):
@@ -112,6 +117,7 @@ SIGNATURES = {
     "vrh_ctx_set_option": (C.c_int, [_vp, _u32, C.c_int64]),
     "vrh_scene_upload": (C.c_int, [_vp, _vp, _u32, _vp, _u32, _u32, _vp, _u32, _vp, C.POINTER(_vp)]),
     "vrh_scene_get_info": (C.c_int, [_vp, C.POINTER(vrh_scene_info)]),
+    "vrh_scene_list_create": (C.c_int, [_vp, C.POINTER(_vp), _u32, _vp, _u32, C.POINTER(_vp)]),
     "vrh_scene_free": (C.c_int, [_vp]),
     "vrh_scene_set_vertex_normals": (C.c_int, [_vp, _vp, _u32]),
     "vrh_shading_create": (C.c_int, [_vp, _vp, _u32, _vp, _u32, C.POINTER(_vp)]),
@@ -141,6 +147,14 @@ SIGNATURES = {
     "vrh_shard_bands": (C.c_uint32, [_u32, _u32, _u32]),
     "vrh_unshard": (C.c_int, [_vp, _u32, _u32, _u32, _vp, _vp, _vp, C.c_uint64, C.POINTER(vrh_kernel_desc), _vp]),
     "vrh_build_bvh": (C.c_int, [_vp, _u32, _u32, _vp, C.POINTER(_u32), _vp, C.POINTER(_u32)]),
+    "vrh_group_get_id": (C.c_int, [C.c_void_p]),
+    "vrh_group_join": (C.c_int, [_vp, _u32, _u32, C.c_void_p, C.POINTER(_vp)]),
+    "vrh_group_create_local": (C.c_int, [_u32, C.POINTER(_vp), C.POINTER(_vp)]),
+    "vrh_group_info": (C.c_int, [_vp, C.POINTER(_u32), C.POINTER(_u32)]),
+    "vrh_group_sync": (C.c_int, [_vp]),
+    "vrh_group_free": (C.c_int, [_vp]),
+    "vrh_render_sharded": (C.c_int, [_u32, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(vrh_kernel_desc), _vp, _u32,
+                                     C.POINTER(vrh_camera), _u32, _u32, _u32]),
     "vrh_gen_heightfield": (C.c_int, [_u32, _vp]),
     "vrh_gen_cornell": (C.c_int, [_vp]),
     "vrh_gen_spheres": (C.c_int, [_u32, _vp]),

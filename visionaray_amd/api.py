@@ -159,7 +159,7 @@ class Context:
                  "ao_schedule": capi.VRH_OPT_AO_SCHEDULE, "blocks_per_cu": capi.VRH_OPT_BLOCKS_PER_CU,
                  "waves_per_simd": capi.VRH_OPT_WAVES_PER_SIMD, "exact_minmax": capi.VRH_OPT_EXACT_MINMAX,
                  "xcd_queues": capi.VRH_OPT_XCD_QUEUES, "refill_min": capi.VRH_OPT_REFILL_MIN,
-                 "vote_leaf": capi.VRH_OPT_VOTE_LEAF, "wide_anyhit": capi.VRH_OPT_WIDE_ANYHIT,
+                 "wide_anyhit": capi.VRH_OPT_WIDE_ANYHIT,
                  "descent_cap": capi.VRH_OPT_DESCENT_CAP, "pop_on_miss": capi.VRH_OPT_POP_ON_MISS,
                  "coop_fetch": capi.VRH_OPT_COOP_FETCH, "scalar_fetch": capi.VRH_OPT_SCALAR_FETCH,
                  "pair_layout": capi.VRH_OPT_PAIR_LAYOUT}
@@ -249,6 +249,22 @@ class hip_index_bvh:
         h = C.c_void_p()
         desc = capi.vrh_build_desc(capi.VRH_BUILD_LBVH, max_leaf)
         capi.check("vrh_scene_build", ctx.handle, _p(prims), len(prims), kind, _p(nrm), C.byref(desc), C.byref(h))
+        self.handle = h
+        self._refresh_info()
+        return self
+
+    @classmethod
+    def scene_list(cls, ctx, members, normals=None):
+        """vrh_scene_list_create: a list of BVHs rendered as one scene -- closest_hit / any_hit over
+        [begin, end) of bvh_refs (traverse_linear.inl:76-141).  normals: (>= max prim_id + 1, 4)
+        float32 indexed by prim_id (AO)."""
+        self = cls.__new__(cls)
+        self.ctx = ctx
+        nrm = None if normals is None else np.ascontiguousarray(normals, np.float32)
+        arr = (C.c_void_p * len(members))(*[m.handle.value for m in members])
+        h = C.c_void_p()
+        capi.check("vrh_scene_list_create", ctx.handle, arr, len(members), _p(nrm), 0 if nrm is None else len(nrm),
+                   C.byref(h))
         self.handle = h
         self._refresh_info()
         return self
@@ -383,7 +399,9 @@ class sched_params:
             raise NotImplementedError("hip_sched supports pixel_sampler::uniform_type only")
         self.cam = cam          # stored by value in the reference (scheduler.h:72)
         self.rt = rt            # by reference (scheduler.h:73)
-        self.scissor_box = (0, 0, rt.width(), rt.height())
+        # scissor_box (scheduler.h:25-31, default recti(0, 0, w, h) at :175): x, y and the EXCLUSIVE
+        # right / bottom edges w, h, as cuda_sched.inl:71 reads them; None = the whole image
+        self.scissor_box = None
         # full image size; differs from the rt size only for a packed image-tile shard
         self.image_size = tuple(image_size) if image_size else (rt.width(), rt.height())
 
@@ -606,6 +624,8 @@ class hip_sched:
                             "callable cannot cross the C ABI")
         rt = sparams.rt
         cam = sparams.cam.basis(*sparams.image_size)
+        if sparams.scissor_box is not None:
+            cam.scissor[:] = [int(v) for v in sparams.scissor_box]
         sh = None
         if shard is not None:
             sh = capi.vrh_shard(shard[0], shard[1], 1 if shard[2] else 0, 0)
@@ -616,19 +636,20 @@ class hip_sched:
             rt.end_frame()
 
 
-def render(ctx, bvh, rt, cam_basis, kernel, shard=None):
+def render(ctx, bvh, rt, cam_basis, kernel, shard=None, frame_num=0):
     """Low-level frame with an explicit vrh_camera (full-image size) and optional vrh_shard."""
     capi.check("vrh_render", ctx.handle, bvh.handle, rt.handle, C.byref(cam_basis), C.byref(kernel.desc),
-               C.byref(shard) if shard is not None else None, 0)
+               C.byref(shard) if shard is not None else None, frame_num)
 
 
-def render_batch(ctx, bvh, rt, cam_bases, kernel, shard=None):
+def render_batch(ctx, bvh, rt, cam_bases, kernel, shard=None, frame_num=0):
     """vrh_render_batch: len(cam_bases) frames in one persistent launch (frames in flight); frame f
-    lands in rows [f * R, (f + 1) * R) of rt (R = image height, or rt height / frames when packed)."""
+    lands in rows [f * R, (f + 1) * R) of rt (R = image height, or rt height / frames when packed)
+    and has frame number frame_num + f."""
     n = len(cam_bases)
     cams = (capi.vrh_camera * n)(*cam_bases)
     capi.check("vrh_render_batch", ctx.handle, bvh.handle, rt.handle, cams, n, C.byref(kernel.desc),
-               C.byref(shard) if shard is not None else None, 0)
+               C.byref(shard) if shard is not None else None, frame_num)
 
 
 def shard_bands(height, index, count):
@@ -642,3 +663,80 @@ def unshard(ctx, width, height, count, dst_rt, color_ptr=0, prim_id_ptr=0, occ_p
     vp = lambda p: C.c_void_p(p) if p else None  # noqa: E731
     capi.check("vrh_unshard", ctx.handle, width, height, count, vp(color_ptr), vp(prim_id_ptr), vp(occ_ptr),
                int(shard_stride_bytes), C.byref(kernel.desc) if kernel is not None else None, dst_rt.handle)
+
+
+# ---- multi-GPU render groups (vrh.h vrh_group_*) -------------------------------------
+
+GROUP_ID_BYTES = capi.VRH_GROUP_ID_BYTES
+
+
+class render_group:
+    """One rank's membership of a multi-GPU render group (an RCCL communicator, vrh_group).
+
+    One process per GPU: rank 0 makes an id with render_group.unique_id(), every rank receives it
+    (any channel) and constructs render_group(ctx, nranks, rank, uid).  One process driving several
+    GPUs: render_group.local([ctx0, ctx1, ...]) returns one member per context; render the frames
+    with render_sharded(members, ...).  The exchange is libvrh's (ncclSend / ncclRecv on the
+    group's own stream); nothing of it goes through torch."""
+
+    def __init__(self, ctx, nranks, rank, uid):
+        if len(uid) != GROUP_ID_BYTES:
+            raise ValueError("render_group: the id is 128 bytes (vrh_group_id)")
+        self.ctx = ctx
+        buf = (C.c_char * GROUP_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        capi.check("vrh_group_join", ctx.handle, nranks, rank, C.cast(buf, C.c_void_p), C.byref(h))
+        self.handle = h
+        self.nranks, self.rank = nranks, rank
+
+    @staticmethod
+    def unique_id():
+        buf = (C.c_char * GROUP_ID_BYTES)()
+        capi.check("vrh_group_get_id", C.cast(buf, C.c_void_p))
+        return bytes(buf.raw)
+
+    @classmethod
+    def local(cls, ctxs):
+        n = len(ctxs)
+        hs = (C.c_void_p * n)()
+        capi.check("vrh_group_create_local", n, (C.c_void_p * n)(*[c.handle.value for c in ctxs]), hs)
+        out = []
+        for i, c in enumerate(ctxs):
+            g = cls.__new__(cls)
+            g.ctx, g.handle, g.nranks, g.rank = c, C.c_void_p(hs[i]), n, i
+            out.append(g)
+        return out
+
+    def render(self, scene, kernel, dst_rt, cam_bases, frame_num=0, shards=0, fields=None):
+        """vrh_render_sharded for this member alone (one process per GPU)."""
+        render_sharded([self], [scene], [kernel], dst_rt, cam_bases, frame_num, shards, fields)
+
+    def sync(self):
+        capi.check("vrh_group_sync", self.handle)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            capi.lib().vrh_group_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def render_sharded(groups, scenes_, kernels, dst_rt, cam_bases, frame_num=0, shards=0, fields=None):
+    """vrh_render_sharded: len(cam_bases) frames over the group; rank 0's dst_rt (W x H * frames)
+    receives them in image order (None on the other ranks).  fields: the vrh_rt_flags assembled on
+    the root (default: colour + prim id + AO mask, the same on every rank)."""
+    n = len(groups)
+    nf = len(cam_bases)
+    if fields is None:
+        fields = capi.VRH_RT_COLOR | capi.VRH_RT_PRIM_ID | capi.VRH_RT_OCC
+    gs = (C.c_void_p * n)(*[g.handle.value for g in groups])
+    ss = (C.c_void_p * n)(*[s.handle.value for s in scenes_])
+    ks = (capi.vrh_kernel_desc * n)(*[k.desc for k in kernels])
+    cams = (capi.vrh_camera * nf)(*cam_bases)
+    capi.check("vrh_render_sharded", n, gs, ss, ks, dst_rt.handle if dst_rt is not None else None, fields, cams, nf,
+               frame_num, shards)

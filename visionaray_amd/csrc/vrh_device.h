@@ -227,7 +227,42 @@ struct test_counts
     uint32_t it_box, it_prim;
     uint64_t w_steps, w_busy, w_box, w_prim;
     uint64_t w_uni;           // wave-level descent iterations whose active lanes all fetch one node
+    // vector-L1 coalescer model (counting variant): per wave-level vector-memory instruction of the
+    // traversal (node pair, primitive and normal loads, output stores), the distinct 128-B lines
+    // (`lines`) and 64-B segments (`segs`) its active lanes touch, and the instruction count
+    // (`vmem`); kept by the wave's first active lane, summed over lanes at the end
+    uint64_t lines, segs, vmem;
 };
+
+// distinct values of `key` over the active lanes (wave-uniform result)
+__device__ __forceinline__ uint32_t distinct_keys(uint64_t key)
+{
+    uint64_t rem = __ballot(true);
+    uint32_t n = 0;
+    while (rem)
+    {
+        const int first = __builtin_ctzll(rem);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, first);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(key >> 32), first);
+        rem &= ~__ballot(key == (((uint64_t)hi << 32) | lo));
+        ++n;
+    }
+    return n;
+}
+
+// one wave-level vector-memory instruction whose lanes access `bytes` (<= 16) at `p`: account for it
+// in the coalescer model (counting variant only; called by the active lanes)
+__device__ __forceinline__ void count_vmem(test_counts& c, const void* p, uint32_t times = 1u)
+{
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    const uint32_t l = distinct_keys(a >> 7), g = distinct_keys(a >> 6);
+    if (__lane_id() == (uint32_t)__builtin_ctzll(__ballot(true)))
+    {
+        c.lines += (uint64_t)l * times;
+        c.segs += (uint64_t)g * times;
+        c.vmem += times;
+    }
+}
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t v)
 {
@@ -280,6 +315,7 @@ __device__ __forceinline__ bool leaf_loop(const float4* __restrict__ prims, uint
         {
             const float4* q = prims + 3u * i;
             float4 a = q[0], b = q[1], c = q[2];
+            if (COUNT) { count_vmem(cnt, q); count_vmem(cnt, q + 1); count_vmem(cnt, q + 2); }
             h = isect_tri(r, a, b, c, t, hu, hv);
             pid = __float_as_uint(c.y);
             flags = __float_as_uint(c.w);
@@ -288,6 +324,7 @@ __device__ __forceinline__ bool leaf_loop(const float4* __restrict__ prims, uint
         {
             const float4* q = prims + 2u * i;
             float4 a = q[0], b = q[1];
+            if (COUNT) { count_vmem(cnt, q); count_vmem(cnt, q + 1); }
             h = isect_sphere(r, a, t);
             pid = __float_as_uint(b.x);
             flags = __float_as_uint(b.z);
@@ -368,6 +405,7 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
         {
             const float4* p = quads + 8u * link;
             const float4 xl = p[0], yl = p[1], zl = p[2], xh = p[3], yh = p[4], zh = p[5], lk = p[6];
+            if (COUNT) count_vmem(cnt, p, 7u);
             const uint32_t k0 = __float_as_uint(lk.x), k1 = __float_as_uint(lk.y);
             const uint32_t k2 = __float_as_uint(lk.z), k3 = __float_as_uint(lk.w);
             float d0, d1, d2, d3;
@@ -434,6 +472,7 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
             const float4* p = pairs + 4u * link;
             q0 = p[0]; q1 = p[1]; q2 = p[2];
             q3 = *reinterpret_cast<const float2*>(p + 3);
+            if (COUNT) count_vmem(cnt, p, 4u);      // one 64-B record: 4 loads, one line each
         }
         bool b0, b1;
         float tn0, tn1;
@@ -621,6 +660,8 @@ __device__ __forceinline__ bool item_step(const float4* __restrict__ pairs, cons
     constexpr uint32_t PF4 = KIND == KIND_TRI ? 3u : 2u;
     const float4* base = leaf ? prims + PF4 * idx : pairs + 4u * idx;
     const float4 q0 = base[0], q1 = base[1];
+    if (COUNT) { count_vmem(cnt, base); count_vmem(cnt, base + 1); count_vmem(cnt, base + 2, leaf && KIND != KIND_TRI ? 0u : 1u); }
+    if (COUNT && !leaf) count_vmem(cnt, base + 3);
     float4 q2 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), q3 = q2;
     if constexpr (KIND == KIND_TRI) q2 = base[2];
     if (!leaf)
@@ -758,13 +799,18 @@ __device__ __forceinline__ uint32_t wang(uint32_t a)
 }
 __device__ __forceinline__ float uniform01(uint32_t k) { return (float)(wang(k) >> 8) * (1.0f / 16777216.0f); }
 
+// per-frame sampler offset: the reference seeds its sampler anew every frame (cuda_sched.inl:38-45,
+// 79; ao/main.cpp passes ++frame_num, :245).  The Appendix-A counter of frame n is shifted by
+// n * 0x9E3779B1 (u32 wrap); frame 0 keeps the Appendix-A counter exactly (the parity fixtures).
+__host__ __device__ __forceinline__ uint32_t frame_salt(uint32_t frame_num) { return frame_num * 0x9E3779B1u; }
+
 // Appendix A Malley sample s of pixel p -> direction in the (u, v, n) basis (ao/main.cpp:218-226)
-__device__ __forceinline__ f3 ao_direction(uint32_t p, uint32_t s, f3 bu, f3 bv, f3 n)
+__device__ __forceinline__ f3 ao_direction(uint32_t p, uint32_t s, f3 bu, f3 bv, f3 n, uint32_t salt)
 {
     float sx = 0.0f, sy = 0.0f;
     for (uint32_t k = 0; k < 16; ++k)
     {
-        uint32_t ctr = ((p * 8u + s) * 16u + k) * 2u;
+        uint32_t ctr = ((p * 8u + s) * 16u + k) * 2u + salt;
         float xa = 2.0f * uniform01(ctr) - 1.0f;
         float ya = 2.0f * uniform01(ctr + 1u) - 1.0f;
         if (xa * xa + ya * ya < 1.0f) { sx = xa; sy = ya; break; }

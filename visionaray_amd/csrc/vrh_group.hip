@@ -1,0 +1,332 @@
+// visionaray_amd/csrc/vrh_group.hip -- multi-GPU render groups (include/vrh.h vrh_group_*,
+// vrh_render_sharded): image-tile shards rendered on every GPU of a group and gathered to rank 0
+// over RCCL (xGMI point-to-point), SURVEY.md §8e.
+//
+// The reference has no multi-GPU path; what is lifted across devices is tiled_sched's tile
+// distribution (tiled_sched.inl:24-25, 175-224: a frame's tiles handed to workers by an atomic
+// counter).  Here a frame's 8-row bands are dealt round-robin to shards (band b -> shard b % S,
+// interleaved so cheap sky rows and expensive terrain rows spread evenly), shard s is rendered by
+// rank s % N (inside a GPU the persistent kernel's own tile queues distribute its bands), every
+// shard is rendered packed (its bands back to back, vrh_render_batch with a packed vrh_shard), and
+// the packed shards travel to rank 0 -- one ncclSend per shard, one ncclRecv per shard on the root,
+// all in one ncclGroupStart/End -- where unshard_kernel lays the bands back into image order and
+// re-derives the RGBA32F colour of the built-in kernels from prim id + AO mask (5 B / pixel on the
+// wire instead of 20).  A rank may own several shards (S > N), so the whole path -- packed renders,
+// the RCCL exchange, the un-interleave -- runs on a one-GPU box with a one-rank group.
+//
+// Streams: the shards render on the context's stream; the exchange and the un-interleave run on
+// the group's own stream, ordered after the renders by an event, so frame batch k + 1 renders while
+// batch k's shards are still on the wire (two staging slots; a slot is reused only after its
+// previous exchange is done).  vrh_group_sync (or vrh_sync on the context after vrh_group_sync)
+// waits for everything.
+#include "vrh_objects.h"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+using namespace vrh;
+
+struct vrh_group
+{
+    vrh_ctx* ctx = nullptr;
+    ncclComm_t comm = nullptr;
+    uint32_t nranks = 1, rank = 0;
+    hipStream_t stream = nullptr;          // exchange + un-interleave
+    struct slot_t
+    {
+        hipEvent_t rendered = nullptr;     // on ctx->stream: this slot's shards are rendered
+        hipEvent_t done = nullptr;         // on the group stream: this slot's exchange + un-interleave done
+        uint8_t* send = nullptr;           // this rank's shards, back to back
+        uint8_t* recv = nullptr;           // root: every shard, [S][shard bytes]
+        size_t send_bytes = 0, recv_bytes = 0;
+        bool used = false;
+    } slot[2];
+    uint32_t next = 0;
+};
+
+namespace {
+
+#define VRH_NCCL(call)                                                                             \
+    do {                                                                                           \
+        ncclResult_t r_ = (call);                                                                  \
+        if (r_ != ncclSuccess) {                                                                   \
+            set_error(std::string(#call) + ": " + ncclGetErrorString(r_));                        \
+            return VRH_ERR_HIP;                                                                    \
+        }                                                                                          \
+    } while (0)
+
+int group_init_common(vrh_group* g)
+{
+    VRH_HIP(hipSetDevice(g->ctx->device));
+    VRH_HIP(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+    for (auto& s : g->slot)
+    {
+        VRH_HIP(hipEventCreateWithFlags(&s.rendered, hipEventDisableTiming));
+        VRH_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    }
+    return VRH_OK;
+}
+
+// what one pixel of a shard carries over the wire for a root target with buffers `fields`
+struct wire_layout
+{
+    bool pid = false, occ = false, t = false, color = false;
+    bool derive = false;                   // colour re-derived on the root from prim id (+ AO mask)
+    size_t bytes_per_px() const { return (pid ? 4 : 0) + (occ ? 1 : 0) + (t ? 4 : 0) + (color ? 16 : 0); }
+};
+
+wire_layout layout_for(uint32_t fields, const vrh_kernel_desc& k)
+{
+    wire_layout w;
+    const bool builtin_colour = k.kind <= VRH_KERNEL_AO && (k.kind != VRH_KERNEL_AO || k.samples <= 8);
+    w.derive = (fields & VRH_RT_COLOR) && builtin_colour;
+    w.color = (fields & VRH_RT_COLOR) && !builtin_colour;
+    w.pid = (fields & VRH_RT_PRIM_ID) || w.derive;
+    w.occ = k.kind == VRH_KERNEL_AO && (((fields & VRH_RT_OCC) && k.samples <= 8) || w.derive);
+    w.t = (fields & VRH_RT_T) != 0;
+    return w;
+}
+
+// (re)allocate a staging buffer; an exchange or render still using the old one is waited for first
+int grow(vrh_group* g, uint8_t*& p, size_t& have, size_t need)
+{
+    if (have >= need) return VRH_OK;
+    VRH_HIP(hipStreamSynchronize(g->ctx->stream));
+    VRH_HIP(hipStreamSynchronize(g->stream));
+    if (p) { VRH_HIP(hipFree(p)); p = nullptr; have = 0; }
+    VRH_HIP(hipMalloc(&p, need));
+    have = need;
+    return VRH_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+VRH_API int vrh_group_get_id(vrh_group_id* id)
+{
+    VRH_CHECK(id, "vrh_group_get_id: null");
+    static_assert(sizeof(vrh_group_id) == sizeof(ncclUniqueId), "group id = ncclUniqueId");
+    ncclUniqueId u;
+    VRH_NCCL(ncclGetUniqueId(&u));
+    std::memcpy(id, &u, sizeof(u));
+    return VRH_OK;
+}
+
+VRH_API int vrh_group_join(vrh_ctx* ctx, uint32_t nranks, uint32_t rank, const vrh_group_id* id, vrh_group** out)
+{
+    VRH_CHECK(ctx && id && out && nranks >= 1 && rank < nranks, "vrh_group_join: bad argument");
+    *out = nullptr;
+    auto* g = new (std::nothrow) vrh_group;
+    if (!g) { set_error("host allocation failed"); return VRH_ERR_OOM; }
+    g->ctx = ctx; g->nranks = nranks; g->rank = rank;
+    int rc = group_init_common(g);
+    if (rc == VRH_OK)
+    {
+        ncclUniqueId u;
+        std::memcpy(&u, id, sizeof(u));
+        ncclResult_t r = ncclCommInitRank(&g->comm, int(nranks), u, int(rank));
+        if (r != ncclSuccess) { set_error(std::string("vrh_group_join: ncclCommInitRank: ") + ncclGetErrorString(r)); rc = VRH_ERR_HIP; }
+    }
+    if (rc != VRH_OK) { vrh_group_free(g); return rc; }
+    *out = g;
+    return VRH_OK;
+}
+
+VRH_API int vrh_group_create_local(uint32_t ndev, vrh_ctx* const* ctxs, vrh_group** out)
+{
+    VRH_CHECK(ndev >= 1 && ctxs && out, "vrh_group_create_local: bad argument");
+    std::vector<int> devs(ndev);
+    for (uint32_t i = 0; i < ndev; ++i)
+    {
+        VRH_CHECK(ctxs[i], "vrh_group_create_local: null context");
+        devs[i] = ctxs[i]->device;
+        for (uint32_t j = 0; j < i; ++j) VRH_CHECK(devs[j] != devs[i], "vrh_group_create_local: one context per device");
+        out[i] = nullptr;
+    }
+    std::vector<ncclComm_t> comms(ndev, nullptr);
+    VRH_NCCL(ncclCommInitAll(comms.data(), int(ndev), devs.data()));
+    int rc = VRH_OK;
+    for (uint32_t i = 0; i < ndev && rc == VRH_OK; ++i)
+    {
+        auto* g = new (std::nothrow) vrh_group;
+        if (!g) { set_error("host allocation failed"); rc = VRH_ERR_OOM; break; }
+        g->ctx = ctxs[i]; g->comm = comms[i]; comms[i] = nullptr;
+        g->nranks = ndev; g->rank = i;
+        out[i] = g;
+        rc = group_init_common(g);
+    }
+    if (rc != VRH_OK)
+    {
+        for (uint32_t i = 0; i < ndev; ++i) { vrh_group_free(out[i]); out[i] = nullptr; if (comms[i]) ncclCommDestroy(comms[i]); }
+        return rc;
+    }
+    return VRH_OK;
+}
+
+VRH_API int vrh_group_info(const vrh_group* g, uint32_t* nranks, uint32_t* rank)
+{
+    VRH_CHECK(g, "vrh_group_info: null");
+    if (nranks) *nranks = g->nranks;
+    if (rank) *rank = g->rank;
+    return VRH_OK;
+}
+
+VRH_API int vrh_group_sync(vrh_group* g)
+{
+    VRH_CHECK(g, "vrh_group_sync: null");
+    VRH_HIP(hipSetDevice(g->ctx->device));
+    VRH_HIP(hipStreamSynchronize(g->ctx->stream));
+    VRH_HIP(hipStreamSynchronize(g->stream));
+    return VRH_OK;
+}
+
+VRH_API int vrh_group_free(vrh_group* g)
+{
+    if (!g) return VRH_OK;
+    if (g->ctx) (void)hipSetDevice(g->ctx->device);
+    if (g->stream) (void)hipStreamSynchronize(g->stream);
+    if (g->comm) (void)ncclCommDestroy(g->comm);
+    for (auto& s : g->slot)
+    {
+        if (s.rendered) (void)hipEventDestroy(s.rendered);
+        if (s.done) (void)hipEventDestroy(s.done);
+        if (s.send) (void)hipFree(s.send);
+        if (s.recv) (void)hipFree(s.recv);
+    }
+    if (g->stream) (void)hipStreamDestroy(g->stream);
+    delete g;
+    return VRH_OK;
+}
+
+VRH_API int vrh_render_sharded(uint32_t n, vrh_group* const* groups, const vrh_scene* const* scenes,
+                               const vrh_kernel_desc* kernels, vrh_rt* dst, uint32_t fields,
+                               const vrh_camera* cams, uint32_t num_frames, uint32_t frame_num, uint32_t shards)
+{
+    VRH_CHECK(n >= 1 && groups && scenes && kernels && cams, "vrh_render_sharded: null argument");
+    VRH_CHECK(num_frames >= 1 && num_frames <= VRH_MAX_BATCH, "vrh_render_sharded: 1..VRH_MAX_BATCH frames");
+    VRH_CHECK((fields & ~uint32_t(VRH_RT_ALL)) == 0 && fields != 0, "vrh_render_sharded: fields are vrh_rt_flags");
+    const uint32_t N = groups[0] ? groups[0]->nranks : 0;
+    const uint32_t S = shards ? shards : N;
+    const uint32_t W = cams[0].width, H = cams[0].height;
+    VRH_CHECK(S >= 1 && S <= 4096, "vrh_render_sharded: shard count");
+    int root = -1;
+    for (uint32_t i = 0; i < n; ++i)
+    {
+        VRH_CHECK(groups[i] && scenes[i] && groups[i]->nranks == N, "vrh_render_sharded: groups of one communicator");
+        VRH_CHECK(scenes[i]->ctx == groups[i]->ctx, "vrh_render_sharded: scene i must live on group i's context");
+        VRH_CHECK(kernels[i].kind == kernels[0].kind && kernels[i].samples == kernels[0].samples,
+                  "vrh_render_sharded: one kernel for every rank");
+        if (groups[i]->rank == 0) root = int(i);
+    }
+    const wire_layout wl = layout_for(fields, kernels[0]);
+    if (root >= 0)
+    {
+        VRH_CHECK(dst && dst->ctx == groups[root]->ctx, "vrh_render_sharded: the root needs a target on its context");
+        VRH_CHECK(dst->width == W && dst->height == H * num_frames, "vrh_render_sharded: target must be W x (H * frames)");
+        VRH_CHECK((!(fields & VRH_RT_COLOR) || dst->color) && (!(fields & VRH_RT_PRIM_ID) || dst->prim_id) &&
+                  (!(fields & VRH_RT_T) || dst->t) && (!(fields & VRH_RT_OCC) || dst->occ),
+                  "vrh_render_sharded: the target lacks a buffer named in fields");
+        VRH_CHECK(!(fields & VRH_RT_OCC) || kernels[0].kind != VRH_KERNEL_AO || kernels[0].samples <= 8,
+                  "vrh_render_sharded: an occlusion target records at most 8 AO samples");
+    }
+    // packed shard geometry: every shard uses shard 0's (largest) band count
+    const uint32_t rows = VRH_BAND_ROWS * vrh_shard_bands(H, 0, S);
+    const size_t px = size_t(rows) * W * num_frames;          // pixels of one shard (all frames)
+    const size_t shard_bytes = wl.bytes_per_px() * px;
+    VRH_CHECK(shard_bytes > 0, "vrh_render_sharded: nothing to gather");
+    const size_t o_pid = 0, o_occ = o_pid + (wl.pid ? 4 * px : 0), o_t = o_occ + (wl.occ ? px : 0),
+                 o_col = o_t + (wl.t ? 4 * px : 0);
+
+    // 1. every local group renders its shards into this call's staging slot (context stream)
+    std::vector<uint32_t> slot_of(n);
+    for (uint32_t i = 0; i < n; ++i)
+    {
+        vrh_group* g = groups[i];
+        vrh_ctx* ctx = g->ctx;
+        VRH_HIP(hipSetDevice(ctx->device));
+        const uint32_t si = g->next;
+        g->next ^= 1u;
+        slot_of[i] = si;
+        auto& sl = g->slot[si];
+        if (sl.used) VRH_HIP(hipStreamWaitEvent(ctx->stream, sl.done, 0));   // the slot's last exchange
+        const uint32_t mine = S > g->rank ? (S - g->rank + N - 1) / N : 0;    // shards s = rank, rank + N, ...
+        int rc = grow(g, sl.send, sl.send_bytes, std::max<size_t>(mine * shard_bytes, 1));
+        if (!rc && g->rank == 0) rc = grow(g, sl.recv, sl.recv_bytes, S * shard_bytes);
+        if (rc) return rc;
+        for (uint32_t j = 0; j < mine; ++j)
+        {
+            const uint32_t s = g->rank + j * N;
+            uint8_t* base = sl.send + size_t(j) * shard_bytes;
+            vrh_rt rt{};
+            rt.ctx = ctx; rt.width = W; rt.height = rows * num_frames; rt.owned = false;
+            rt.prim_id = wl.pid ? reinterpret_cast<uint32_t*>(base + o_pid) : nullptr;
+            rt.occ = wl.occ ? base + o_occ : nullptr;
+            rt.t = wl.t ? reinterpret_cast<float*>(base + o_t) : nullptr;
+            rt.color = wl.color ? reinterpret_cast<float4*>(base + o_col) : nullptr;
+            vrh_shard sh{ s, S, 1u, 0u };
+            rc = vrh_render_batch(ctx, scenes[i], &rt, cams, num_frames, &kernels[i], &sh, frame_num);
+            if (rc) return rc;
+        }
+        VRH_HIP(hipEventRecord(sl.rendered, ctx->stream));
+        VRH_HIP(hipStreamWaitEvent(g->stream, sl.rendered, 0));
+    }
+    // 2. the exchange: every shard to the root, one send / receive pair per shard
+    VRH_NCCL(ncclGroupStart());
+    for (uint32_t i = 0; i < n; ++i)
+    {
+        vrh_group* g = groups[i];
+        auto& sl = g->slot[slot_of[i]];
+        const uint32_t mine = S > g->rank ? (S - g->rank + N - 1) / N : 0;
+        for (uint32_t j = 0; j < mine; ++j)
+            VRH_NCCL(ncclSend(sl.send + size_t(j) * shard_bytes, shard_bytes, ncclUint8, 0, g->comm, g->stream));
+        if (g->rank == 0)
+            for (uint32_t s = 0; s < S; ++s)
+                VRH_NCCL(ncclRecv(sl.recv + size_t(s) * shard_bytes, shard_bytes, ncclUint8, int(s % N), g->comm, g->stream));
+    }
+    VRH_NCCL(ncclGroupEnd());
+    // 3. the root lays the bands back into image order, frame by frame
+    for (uint32_t i = 0; i < n; ++i)
+    {
+        vrh_group* g = groups[i];
+        auto& sl = g->slot[slot_of[i]];
+        VRH_HIP(hipSetDevice(g->ctx->device));
+        if (g->rank == 0)
+        {
+            const size_t fpx = size_t(rows) * W;               // pixels of one frame of one shard
+            for (uint32_t f = 0; f < num_frames; ++f)
+            {
+                unshard_params u{};
+                u.width = W; u.height = H; u.count = S; u.rows_per_shard = rows;
+                u.gpid = wl.pid ? reinterpret_cast<const char*>(sl.recv + o_pid + 4 * f * fpx) : nullptr;
+                u.gocc = wl.occ ? reinterpret_cast<const char*>(sl.recv + o_occ + f * fpx) : nullptr;
+                u.gt = wl.t ? reinterpret_cast<const char*>(sl.recv + o_t + 4 * f * fpx) : nullptr;
+                u.gcolor = wl.color ? reinterpret_cast<const char*>(sl.recv + o_col + 16 * f * fpx) : nullptr;
+                u.stride_pid = u.stride_occ = u.stride_t = u.stride_color = shard_bytes;
+                const size_t fo = size_t(f) * W * H;
+                u.color = (fields & VRH_RT_COLOR) ? dst->color + fo : nullptr;
+                u.pid = (fields & VRH_RT_PRIM_ID) ? dst->prim_id + fo : nullptr;
+                u.occ = (fields & VRH_RT_OCC) && wl.occ ? dst->occ + fo : nullptr;
+                u.t = (fields & VRH_RT_T) ? dst->t + fo : nullptr;
+                u.ao = kernels[i].kind == VRH_KERNEL_AO ? 1u : 0u;
+                u.samples = kernels[i].samples ? kernels[i].samples : 1u;
+                std::memcpy(u.bg, kernels[i].bg, 16);
+                const uint32_t* sb = cams[f].scissor;
+                const bool whole = sb[0] == 0 && sb[1] == 0 && sb[2] == 0 && sb[3] == 0;
+                u.clip[0] = whole ? 0u : std::min(sb[0], W); u.clip[1] = whole ? 0u : std::min(sb[1], H);
+                u.clip[2] = whole ? W : std::min(sb[2], W); u.clip[3] = whole ? H : std::min(sb[3], H);
+                VRH_HIP(launch_unshard(u, g->stream));
+            }
+        }
+        VRH_HIP(hipEventRecord(sl.done, g->stream));
+        sl.used = true;
+    }
+    return VRH_OK;
+}
+
+} // extern "C"

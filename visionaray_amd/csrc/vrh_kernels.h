@@ -9,14 +9,22 @@
 
 namespace vrh {
 
-struct frame_camera { float eye[3], cam_u[3], cam_v[3], cam_w[3]; };
+struct frame_camera
+{
+    float eye[3], cam_u[3], cam_v[3], cam_w[3];
+    uint32_t clip[4];         // scissor box clamped to the image: x0, y0, x1, y1 (exclusive)
+};
+
+constexpr uint32_t MAX_LIST = 8;   // BVHs of a scene list (VRH_MAX_SCENE_LIST)
 
 struct render_params
 {
     const float4* pairs;      // 4 float4 per inner node pair record
     const float4* prims;      // leaf-ordered primitives (3 float4 tri, 2 float4 sphere)
     const float4* normals;    // per prim_id
-    uint32_t root;            // root link (pair 0, or LEAF_BIT|0 for a single-leaf tree)
+    uint32_t root;            // root link (pair 0, or LEAF_BIT|0 for a single-leaf tree) = roots[0]
+    uint32_t roots[MAX_LIST]; // scene list (launch_config::sched 2): root link of each BVH
+    uint32_t num_roots;
     uint32_t step_limit;      // per-ray traversal step bound (nodes + primitives)
     uint32_t stack_cap;       // LDS stack entries per lane (>= BVH depth)
     uint32_t fast_ok;         // node bounds all finite: hardware min/max slab path allowed
@@ -25,6 +33,7 @@ struct render_params
 
     frame_camera cam[VRH_MAX_BATCH];   // pinhole basis of every frame of the launch
     uint32_t num_frames;      // frames rendered by this launch (vrh_render_batch)
+    uint32_t frame_num;       // frame number of frame 0 of the launch (frame f: frame_num + f), AO sampler offset
     uint32_t frame_rows;      // output rows per frame: frame f owns rows [f * frame_rows, (f + 1) * frame_rows)
     uint32_t width, height;
 
@@ -41,17 +50,17 @@ struct render_params
     uint8_t* occ;
 
     // counters (u64): [1] frame rays, [2] frame hits, [3] frame box tests, [4] frame primitive
-    // tests, [5] frame error flags (1 = traversal step guard tripped), [6] [7] [9] [10] SIMD
-    // utilisation (wave steps, busy lane-steps, wave descent / leaf iterations; counting variant
-    // only), [8 + 8q] tile queue head q
-    // (q = 0..7, one 64-B line each), [80 + 8q] hit records in list q and [144 + 8q] AO rays of
-    // list q handed out (two-pass AO) -- [0, COUNTERS_FRAME) reset per frame --
-    // [COUNTERS_TOTAL + 0/1] total rays / hits since vrh_stats_reset
+    // tests, [5] frame error flags (1 = traversal step guard tripped), [6] [7] [9] [10] [11] SIMD
+    // utilisation (wave steps, busy lane-steps, wave descent / leaf iterations, wave-uniform
+    // descents; counting variant only), [8 + 8q] tile queue head q (q = 0..7, one 64-B line each),
+    // [COUNTERS_LINES] vector-L1 line accesses and [COUNTERS_LINES + 1] wave-level vector-memory
+    // instructions of the traversal loads (counting variant: the coalescer model, vrh_device.h
+    // count_lines) -- [0, COUNTERS_FRAME) reset per frame -- [COUNTERS_TOTAL + 0/1] total rays / hits
+    // since vrh_stats_reset
     unsigned long long* counters;
     uint32_t xcd_queues;      // 1: per-XCD tile queues with stealing; 0: one global queue
     uint32_t refill_min;      // retire / refill once this many lanes are free (AO, item loops)
     uint32_t refill_min_primary;   // the same for the step loop's primary-only stream
-    uint32_t vote_leaf;       // vote schedule: leaf step when 8 * leaf lanes >= vote_leaf * node lanes
     uint32_t descent_cap;     // step loop: inner visits per step before a descent is resumed later
     uint32_t step_flags;      // step loop: bit 0 a descent that misses both children pops and continues;
                               // bit 1 wave-uniform pair records fetched through the scalar cache
@@ -61,18 +70,11 @@ struct render_params
     uint32_t num_bounces;     // VRH_KERNEL_WHITTED: loop iterations (eps = scene epsilon)
     uint32_t* mh_prim_id;     // [pixel][N] hit lists (render target side buffers)
     float* mh_t;
-    // two-pass AO (launch_config::sched 3): pass 1 publishes every primary hit as a 32-B record
-    // (isect pos, pixel index | face normal, output offset) into the hit list of its tile's queue
-    // (list q holds up to 64 records per tile of queue range q); pass 2 traces the lists' AO rays,
-    // one byte per ray into `aobits` ([record][sample]); the resolve pass folds them into colour
-    float4* hitrec;
-    uint8_t* aobits;
     dev::hit_mask_params hmask;   // mask intersector (vrh_hit_mask), hmask.mask == null: none
 };
 
 constexpr int COUNTERS_FRAME = 208;     // u64 words reset before every frame
-constexpr int COUNTERS_HITS = 80;       // [80 + 8q]: hit records of list q (two-pass AO)
-constexpr int COUNTERS_AOHEAD = 144;    // [144 + 8q]: AO rays of list q handed out
+constexpr int COUNTERS_LINES = 80;      // [80] L1 128-B lines, [81] wave-level vector-memory instructions, [82] 64-B segments (counting variant)
 constexpr int COUNTERS_TOTAL = 208;     // u64 words [208], [209]: totals
 constexpr int COUNTERS_WORDS = 256;
 
@@ -84,33 +86,31 @@ struct launch_config
     int block;         // threads per block (multiple of 64)
     int stack_cap;     // LDS stack entries per lane
     int occ;           // register budget: min waves per SIMD (1, 6 or 8)
-    int sched;         // 0: step loop (render_unified_kernel), 1: item loop, 2: vote loop (render_item_kernel),
-                       // 3: two-pass AO (primary pass publishing hit records, AO pass, resolve)
-    int epi;           // primary epilogue: 0 plain, 1 VRH_KERNEL_SIMPLE, 2 VRH_KERNEL_MULTI_HIT, 3 VRH_KERNEL_WHITTED (triangles),
-                       // 4 hit records for the two-pass AO
+    int sched;         // 0: step loop (render_unified_kernel), 1: item loop (render_item_kernel, primary only),
+                       // 2: step loop over a BVH list (render_unified_kernel<..., LIST>),
+                       // 3: step loop, frames in flight (render_unified_kernel<..., BATCH>: same code)
+    int epi;           // primary epilogue: 0 plain, 1 VRH_KERNEL_SIMPLE, 2 VRH_KERNEL_MULTI_HIT, 3 VRH_KERNEL_WHITTED (triangles)
     int max_hits;      // MULTI_HIT: N (LDS hit lists)
 };
 
 size_t render_lds_bytes(const launch_config& c);
 hipError_t launch_render(const render_params& p, const launch_config& c, int grid, hipStream_t s);
 int render_blocks_per_cu(const launch_config& c);
-// two-pass AO: pass 2 (AO rays of the hit lists) and the resolve pass (AO bytes -> colour, mask)
-size_t ao_pass_lds_bytes(const launch_config& c);
-hipError_t launch_ao_pass(const render_params& p, const launch_config& c, int grid, hipStream_t s);
-int ao_pass_blocks_per_cu(const launch_config& c);
-hipError_t launch_ao_resolve(const render_params& p, hipStream_t s);
 struct unshard_params
 {
     uint32_t width, height, count, rows_per_shard;
     const char* gcolor;          // gathered colour (float4), or null: re-derive from prim id + occ
     const char* gpid;            // gathered prim ids (u32)
     const char* gocc;            // gathered AO masks (u8)
-    uint64_t stride_color, stride_pid, stride_occ;   // bytes between consecutive shards
+    const char* gt;              // gathered closest-hit t (f32), or null
+    uint64_t stride_color, stride_pid, stride_occ, stride_t;   // bytes between consecutive shards
     float4* color;
     uint32_t* pid;
     uint8_t* occ;
+    float* t;
     uint32_t ao, samples;        // colour re-derivation (kernel kind, AO samples)
     float bg[4];
+    uint32_t clip[4];            // scissor box x0, y0, x1, y1: pixels outside are left untouched
 };
 hipError_t launch_unshard(const unshard_params& u, hipStream_t s);
 

@@ -51,7 +51,10 @@ __device__ __forceinline__ bool tile_pixel(const render_params& P, uint32_t id, 
     uint32_t in_band = lane >> 3;
     y = band * BAND + in_band;
     out_row = f * P.frame_rows + (P.packed ? lb * BAND + in_band : y);
-    return x < P.width && y < P.height;
+    // the frame's scissor box, clamped to the image on the host (cuda_sched.inl:71: x < sb.x,
+    // y < sb.y, x >= sb.w, y >= sb.h are skipped -- w / h are the exclusive right / bottom edges)
+    const frame_camera& c = P.cam[f];
+    return x >= c.clip[0] && y >= c.clip[1] && x < c.clip[2] && y < c.clip[3];
 }
 
 __device__ __forceinline__ bool tile_pixel(const render_params& P, uint32_t unit, uint32_t lane,
@@ -59,6 +62,46 @@ __device__ __forceinline__ bool tile_pixel(const render_params& P, uint32_t unit
 {
     uint32_t f;
     return tile_pixel(P, unit, lane, x, y, out_row, f);
+}
+
+// per-wave totals (rays, hits, test counts): one atomic set per wave, at the end of the kernel
+template <bool COUNT>
+__device__ __forceinline__ void flush_totals(const render_params& P, uint32_t lane, uint64_t rays_total,
+                                             uint64_t hits_total, const test_counts& cnt)
+{
+    unsigned long long rr = rays_total, hh = hits_total, b = cnt.box, q = cnt.prim, uni_sum = cnt.w_uni;
+    unsigned long long li = cnt.lines, sg = cnt.segs, vm = cnt.vmem;
+    for (int off = 32; off > 0; off >>= 1)
+    {
+        rr += __shfl_down(rr, off);
+        hh += __shfl_down(hh, off);
+        if (COUNT)
+        {
+            b += __shfl_down(b, off); q += __shfl_down(q, off); uni_sum += __shfl_down(uni_sum, off);
+            li += __shfl_down(li, off); sg += __shfl_down(sg, off); vm += __shfl_down(vm, off);
+        }
+    }
+    if (__ballot(cnt.aborted) != 0ull && lane == 0) atomicOr(P.counters + 5, 1ull);
+    if (lane == 0)
+    {
+        atomicAdd(P.counters + 1, rr);
+        atomicAdd(P.counters + 2, hh);
+        atomicAdd(P.counters + COUNTERS_TOTAL, rr);
+        atomicAdd(P.counters + COUNTERS_TOTAL + 1, hh);
+        if (COUNT)
+        {
+            atomicAdd(P.counters + 3, b);
+            atomicAdd(P.counters + 4, q);
+            atomicAdd(P.counters + 6, (unsigned long long)cnt.w_steps);    // wave-uniform values
+            atomicAdd(P.counters + 7, (unsigned long long)cnt.w_busy);
+            atomicAdd(P.counters + 9, (unsigned long long)cnt.w_box);
+            atomicAdd(P.counters + 10, (unsigned long long)cnt.w_prim);
+            atomicAdd(P.counters + 11, uni_sum);
+            atomicAdd(P.counters + COUNTERS_LINES, li);
+            atomicAdd(P.counters + COUNTERS_LINES + 1, vm);
+            atomicAdd(P.counters + COUNTERS_LINES + 2, sg);
+        }
+    }
 }
 
 // sched_common.h:130-150 make_primary_ray_impl (pinhole, uniform pixel sampler), frame f's camera
@@ -128,31 +171,60 @@ __device__ __forceinline__ uint32_t next_tile(const render_params& P, tile_queue
     return NONE;
 }
 
-// two-pass AO: hit list q holds up to 64 records per (frame, tile) of queue q; its first slot
-__device__ __forceinline__ uint32_t list_base(const render_params& P, uint32_t q, uint32_t nq)
-{
-    return 64u * P.num_frames * strip_lo(P, q, nq);
-}
-
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask)
 {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// AO ray s of hit slot `slot` whose pixel has global index p (ao/main.cpp:216-238 with the
-// Appendix-A sampler)
+// AO ray s of hit slot `slot` whose pixel has global index p in frame f of the launch
+// (ao/main.cpp:216-238 with the Appendix-A sampler, offset by the frame number)
+template <bool COUNT>
 __device__ __forceinline__ ray_t ao_ray(const render_params& P, const float* recs, uint32_t slot, uint32_t s,
-                                        uint32_t p)
+                                        uint32_t p, uint32_t f, test_counts& cnt)
 {
     const float* sr = recs + slot * AO_REC_WORDS;
     f3 pos = mk3(sr[0], sr[1], sr[2]);
-    const float4 nn = P.normals[__float_as_uint(sr[3])];              // get_normal.h:26-37
+    const float4* np = P.normals + __float_as_uint(sr[3]);
+    const float4 nn = *np;                                             // get_normal.h:26-37
+    if (COUNT) count_vmem(cnt, np);
     f3 n = mk3(nn.x, nn.y, nn.z);
     // vector3.inl:357-367 make_orthonormal_basis(u, v, w = n)
     f3 bv = fabsf(n.x) > fabsf(n.y) ? normalize(mk3(-n.z, 0.0f, n.x)) : normalize(mk3(0.0f, n.z, -n.y));
     f3 bu = cross(bv, n);
-    f3 d = ao_direction(p, s, bu, bv, n);
+    f3 d = ao_direction(p, s, bu, bv, n, frame_salt(P.frame_num + f));
     return make_ray(pos + d * P.eps, d);
+}
+
+// coalescer model of the output stores of one pixel (counting variant), by buffer: 1 colour,
+// 2 occlusion mask, 4 prim id, 8 t
+constexpr uint32_t ST_COLOR = 1u, ST_OCC = 2u, ST_PID = 4u, ST_T = 8u;
+__device__ __forceinline__ void count_stores(test_counts& cnt, const render_params& P, size_t o, uint32_t which)
+{
+    if ((which & ST_COLOR) && P.color) count_vmem(cnt, P.color + o);
+    if ((which & ST_OCC) && P.occ) count_vmem(cnt, P.occ + o);
+    if ((which & ST_PID) && P.prim_id) count_vmem(cnt, P.prim_id + o);
+    if ((which & ST_T) && P.t) count_vmem(cnt, P.t + o);
+}
+
+// BVH-ref lists (traverse_linear.inl:76-141): the ray's BVH `bk` is exhausted (rc < 0).  Every BVH
+// of the list is traversed on its own (fresh result, the same max_t), and its hit is merged into
+// the running result by update_if(result, hr, is_closer(hr, result, max_t)) (update_if.h:27-79,
+// hit_record.h:54-64: strictly closer only).  Any hit stops at the first BVH with a hit (rc > 0,
+// exit_traversal.h:49-56), so only exhausted BVHs come here.  Returns the new rc: 0 = the next BVH
+// was started, -1 = the list is done (best_t / best_prim hold the merged result).
+__device__ __forceinline__ int list_next(const render_params& P, bool any, uint32_t& bk, float& res_t, uint32_t& res_prim,
+                                         float& best_t, uint32_t& best_prim, lds_stack& st, uint32_t& resume)
+{
+    if (!any && best_t < res_t) { res_t = best_t; res_prim = best_prim; }
+    if (bk + 1u < P.num_roots)
+    {
+        bk += 1u;
+        best_t = FMAX; best_prim = 0;
+        st.reset(); st.push(P.roots[bk]); resume = NO_RESUME;
+        return 0;
+    }
+    best_t = res_t; best_prim = res_prim;
+    return -1;
 }
 
 // One refilling loop per wave.  Primary rays (one per pixel of the wave's tile)
@@ -162,8 +234,12 @@ __device__ __forceinline__ ray_t ao_ray(const render_params& P, const float* rec
 // streams pixels tile after tile and writes each pixel when its ray finishes.
 // EPI: primary-ray epilogue -- 0 colour = hit ? 1 : bg, 1 simple::kernel shading, 2 multi_hit<N>
 // hit lists + the multi_hit example's compositing, 3 whitted::kernel (the lane traces its pixel's
-// shadow and reflection rays one after the other before it takes the next pixel)
-template <int KIND, bool AO, bool COUNT, int OCC, int EPI = 0>
+// shadow and reflection rays one after the other before it takes the next pixel).
+// LIST: the scene is a list of BVHs (vrh_scene_list_create), traversed one after the other per ray
+// and merged as traverse_linear.inl:76-141 does (list_next); EPI 0 only.
+// BATCH: the same code, instantiated separately for launches of several frames (vrh_render_batch,
+// frames in flight) so that profiles tell them apart from one-frame launches (hip_sched::frame).
+template <int KIND, bool AO, bool COUNT, int OCC, int EPI = 0, bool LIST = false, bool BATCH = false>
 __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params P)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -192,16 +268,17 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     uint32_t best_prim = 0, steps = 0;
     bool any = false, quad = false, finite = true;
     uint32_t resume = NO_RESUME;
+    uint32_t bk = 0, res_prim = 0;                 // LIST: the ray's current BVH, merged result
+    float res_t = FMAX;
+    static_assert(!LIST || EPI == 0, "BVH lists: primary and AO kernels");
 
     if constexpr (!AO)
     {
         // ---- primary visibility: stream pixels, write each when its ray finishes ------------
         tile_queue tq = queue_init(P);
         uint32_t tile = next_tile(P, tq, lane);
-        uint32_t tile_q = tq.q;                    // the queue range `tile` came from (its hit list)
         uint32_t handed = 0;                       // pixels of `tile` handed out (wave-uniform)
         uint32_t out_o = 0;
-        uint32_t lane_q = 0, lane_px = 0;          // EPI 4: hit list and image pixel of the lane's ray
         hit_extra hx = { 0.0f, 0.0f, 0u };
         mh_list mh;
         mh.mem = smem;
@@ -219,7 +296,6 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 if (handed >= 64u && tile != NONE)
                 {
                     tile = next_tile(P, tq, lane);
-                    tile_q = tq.q;
                     handed = 0;
                 }
                 if (tile != NONE)
@@ -234,7 +310,6 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                             r = primary_ray(P, fr, x, y);
                             finite = finite_ray(r);
                             out_o = orow * P.width + x;
-                            if constexpr (EPI == 4) { lane_q = tile_q; lane_px = y * P.width + x; }
                             best_t = FMAX; best_prim = 0; steps = 0;
                             if constexpr (EPI == 2) mh.reset();
                             if constexpr (EPI == 3)
@@ -243,6 +318,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                                 max_t = FMAX; any = false; quad = false;
                             }
                             st.reset(); st.push(P.root); resume = NO_RESUME;
+                            bk = 0; res_t = FMAX; res_prim = 0;
                             mode = PRIMARY;
                             rays_total += 1;
                         }
@@ -255,7 +331,6 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 continue;
             }
             const bool busy = mode != IDLE;
-            bool publish = false;                  // EPI 4: this lane's primary hit becomes a record
             using ML = typename std::conditional<EPI == 2, mh_list, void>::type;
             constexpr bool UV = EPI == 1 || EPI == 3;
             const float mt = EPI == 3 ? max_t : FMAX;
@@ -271,6 +346,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 int rc = (COOP_FETCH && P.coop) ? rc_coop : (P.fast_ok && __ballot(!finite) == 0ull)
                     ? ray_step<KIND, COUNT, true, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, &hx, &mh, hm)
                     : ray_step<KIND, COUNT, false, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, &hx, &mh, hm);
+                if constexpr (LIST)
+                    if (rc != 0) rc = list_next(P, false, bk, res_t, res_prim, best_t, best_prim, st, resume);
                 if constexpr (EPI == 3)
                 {
                     if (rc != 0)
@@ -366,40 +443,12 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                         if (hit) c = shade_simple(P.shade, P.prims, P.normals, r, best_t, best_prim, hx);
                     if constexpr (EPI == 2)
                         c = shade_multi(P.shade, P.prims, P.normals, r, mh);
-                    // EPI 4: a hit pixel's colour and AO mask are written by the resolve pass
-                    if (P.color && (EPI != 4 || !hit)) P.color[out_o] = c;
+                    if (P.color) P.color[out_o] = c;
                     if (P.prim_id) P.prim_id[out_o] = hit ? best_prim : 0xFFFFFFFFu;
                     if (P.t) P.t[out_o] = hit ? best_t : -1.0f;
-                    if (P.occ && (EPI != 4 || !hit)) P.occ[out_o] = 0;
-                    if constexpr (EPI == 4) publish = hit;   // the ray state stays valid until the refill
+                    if (P.occ) P.occ[out_o] = 0;
+                    if (COUNT) count_stores(cnt, P, out_o, ST_COLOR | ST_OCC | ST_PID | ST_T);
                     mode = IDLE;
-                }
-            }
-            if constexpr (EPI == 4)
-            {
-                // append the finished hits to their tiles' lists (one atomic per list and step):
-                // record = (isect pos, image pixel) (face normal, output offset), ao/main.cpp:202,
-                // get_normal.h:26-37
-                uint64_t pend = __ballot(publish);
-                while (pend)
-                {
-                    const uint32_t first = (uint32_t)__builtin_ctzll(pend);
-                    const uint32_t q0 = __shfl(lane_q, first);
-                    const bool mine = publish && lane_q == q0;
-                    const uint64_t m = __ballot(mine);
-                    uint32_t j0 = 0;
-                    if (lane == first)
-                        j0 = atomicAdd(reinterpret_cast<uint32_t*>(P.counters + COUNTERS_HITS + 8u * q0), (uint32_t)__popcll(m));
-                    j0 = __shfl(j0, first);
-                    if (mine)
-                    {
-                        const uint32_t rec = list_base(P, q0, P.xcd_queues ? 8u : 1u) + j0 + lane_rank(m);
-                        const f3 pos = r.ori + r.dir * best_t;
-                        const float4 nn = P.normals[best_prim];
-                        P.hitrec[2u * rec] = make_float4(pos.x, pos.y, pos.z, __uint_as_float(lane_px));
-                        P.hitrec[2u * rec + 1u] = make_float4(nn.x, nn.y, nn.z, __uint_as_float(out_o));
-                    }
-                    pend &= ~m;
                 }
             }
             if (COUNT) count_wave(cnt, busy);
@@ -441,6 +490,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     const size_t o = (size_t)orow * P.width + x;
                     if (P.color) P.color[o] = make_float4(clr, clr, clr, 1.0f);
                     if (P.occ) P.occ[o] = (uint8_t)m;
+                    if (COUNT) count_stores(cnt, P, o, ST_COLOR | ST_OCC);
                 }
                 __builtin_amdgcn_wave_barrier();
                 tileD = NONE;
@@ -466,10 +516,11 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 if (mode == IDLE && cand < avail)
                 {
                     const uint32_t slot = cand / S, smp = cand - slot * S;
-                    uint32_t x, y, orow;
-                    tile_pixel(P, tileC, slot_px[parC * 64u + slot], x, y, orow);
-                    r = ao_ray(P, recs, slot, smp, y * P.width + x);
+                    uint32_t x, y, orow, fr;
+                    tile_pixel(P, tileC, slot_px[parC * 64u + slot], x, y, orow, fr);
+                    r = ao_ray<COUNT>(P, recs, slot, smp, y * P.width + x, fr, cnt);
                     best_t = FMAX; best_prim = 0; steps = 0; max_t = P.radius; any = true;
+                    bk = 0; res_t = FMAX; res_prim = 0;
                     finite = finite_ray(r);
                     quad = P.quad_ok && finite;
                     st.reset(); st.push(quad ? 0u : P.root); resume = NO_RESUME;
@@ -493,6 +544,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     finite = finite_ray(r);
                     best_t = FMAX; best_prim = 0; steps = 0; max_t = FMAX; any = false; quad = false;
                     st.reset(); st.push(P.root); resume = NO_RESUME;
+                    bk = 0; res_t = FMAX; res_prim = 0;
                     mode = PRIMARY;
                     tag = k;
                     rays_total += 1;
@@ -521,6 +573,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm)
                     : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm);
             }
+            if constexpr (LIST)
+                if (busy && rc < 0) rc = list_next(P, any, bk, res_t, res_prim, best_t, best_prim, st, resume);
             if (COUNT) count_wave(cnt, busy);
             // 5. finished AO rays: record occlusion, retire from their tile's in-flight count
             const bool ao_done = mode == AORAY && rc != 0;
@@ -541,6 +595,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     const size_t o = (size_t)orow * P.width + x;
                     if (P.prim_id) P.prim_id[o] = hit ? best_prim : 0xFFFFFFFFu;
                     if (P.t) P.t[o] = hit ? best_t : -1.0f;
+                    if (COUNT) count_stores(cnt, P, o, ST_PID | ST_T);
                     if (hit)
                     {
                         const uint32_t slot = pubC + lane_rank(hfin);
@@ -555,6 +610,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     {
                         if (P.color) P.color[o] = bg;
                         if (P.occ) P.occ[o] = 0;
+                        if (COUNT) count_stores(cnt, P, o, ST_COLOR | ST_OCC);
                     }
                 }
                 pubC += (uint32_t)__popcll(hfin);
@@ -567,194 +623,23 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         }
     }
 
-    // ---- per-wave totals: one atomic set per wave --------------------------------------------
-    unsigned long long rr = rays_total, hh = hits_total, b = cnt.box, q = cnt.prim, uni_sum = cnt.w_uni;
-    for (int off = 32; off > 0; off >>= 1)
-    {
-        rr += __shfl_down(rr, off);
-        hh += __shfl_down(hh, off);
-        if (COUNT) { b += __shfl_down(b, off); q += __shfl_down(q, off); uni_sum += __shfl_down(uni_sum, off); }
-    }
-    if (__ballot(cnt.aborted) != 0ull && lane == 0) atomicOr(P.counters + 5, 1ull);
-    if (lane == 0)
-    {
-        atomicAdd(P.counters + 1, rr);
-        atomicAdd(P.counters + 2, hh);
-        atomicAdd(P.counters + COUNTERS_TOTAL, rr);
-        atomicAdd(P.counters + COUNTERS_TOTAL + 1, hh);
-        if (COUNT)
-        {
-            atomicAdd(P.counters + 3, b);
-            atomicAdd(P.counters + 4, q);
-            atomicAdd(P.counters + 6, (unsigned long long)cnt.w_steps);    // wave-uniform values
-            atomicAdd(P.counters + 7, (unsigned long long)cnt.w_busy);
-            atomicAdd(P.counters + 9, (unsigned long long)cnt.w_box);
-            atomicAdd(P.counters + 10, (unsigned long long)cnt.w_prim);
-            atomicAdd(P.counters + 11, (unsigned long long)uni_sum);
-        }
-    }
+    flush_totals<COUNT>(P, lane, rays_total, hits_total, cnt);
 }
 
-// Two-pass AO, pass 2: the AO rays of the hit lists pass 1 published (render_unified_kernel,
-// EPI 4).  Ray g of list q = sample g % S of record g / S; lanes take rays straight from the list
-// heads (one atomic per refill for all idle lanes of the wave), so the frame's AO work is shared
-// out ray by ray instead of tile by tile: a shard of a few thousand tiles still keeps every wave
-// of the chip busy to the end.  A wave drains the list of its own XCD first (the strip whose BVH
-// nodes pass 1 left in that XCD's L2), then the others.  Same rays, same arithmetic and the same
-// any-hit traversal as the fused kernel (ao/main.cpp:216-238), so the occlusion bits are equal.
+// ITEM schedule (primary visibility): a wave iterates on single traversal items (item_step: one
+// node pair or one primitive per lane) instead of whole descend-to-leaf steps.  The vector-memory
+// unit charges every wave-level load instruction whatever its active lanes, so what counts is how
+// many lanes share each one: a lane that has reached a leaf tests its primitives while its
+// neighbours are still descending.  Finished rays are retired and idle lanes refilled only once at
+// least P.refill_min lanes are free (or none is busy), so the ray-generation code runs with many
+// lanes at once.  Measured faster than the step loop for sphere primary visibility (short leaves
+// of cheap tests), its auto default there; slower for AO, which always runs the step loop.
 template <int KIND, bool COUNT, int OCC>
-__global__ __launch_bounds__(256, OCC) void ao_pass_kernel(render_params P)
-{
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63u;
-    const uint32_t block = blockDim.x;
-
-    lds_stack st;
-    st.mem = smem;
-    st.base = tid;
-    st.stride = block;
-    st.top = tid;
-    st.end = tid + P.stack_cap * block;
-    test_counts cnt = {};
-    uint64_t rays_total = 0;
-    const hit_mask_params hml = P.hmask;          // a local copy: &P would spill the kernel arguments
-    const hit_mask_params* hm = &hml;             // ray_step tests hm->mask
-
-    const uint32_t S = P.samples;
-    const uint32_t nq = P.xcd_queues ? 8u : 1u;
-    uint32_t q = P.xcd_queues ? xcc_id() : 0u, tried = 0;
-    // hit records of list q: low word of the u64 counter COUNTERS_HITS + 8q (pass 1 is complete)
-    auto hits = [&](uint32_t qq) { return *reinterpret_cast<const uint32_t*>(P.counters + COUNTERS_HITS + 8u * qq); };
-    uint32_t total = hits(q) * S;                 // AO rays of list q
-
-    bool busy = false, quad = false, finite = true;
-    ray_t r;
-    float best_t = FMAX;
-    uint32_t best_prim = 0, steps = 0, resume = NO_RESUME, tag = 0;
-    for (;;)
-    {
-        uint64_t idle = __ballot(!busy);
-        if ((uint32_t)__popcll(idle) < P.refill_min && idle != ~0ull) idle = 0ull;
-        while (idle && tried < nq)
-        {
-            const uint32_t n = (uint32_t)__popcll(idle);
-            uint32_t a = 0;
-            if (lane == 0) a = atomicAdd(reinterpret_cast<uint32_t*>(P.counters + COUNTERS_AOHEAD + 8u * q), n);
-            a = __shfl(a, 0);
-            const uint32_t take = a < total ? min(n, total - a) : 0u;
-            const uint32_t cand = lane_rank(idle);
-            if (!busy && cand < take)
-            {
-                const uint32_t g = a + cand;
-                const uint32_t j = g / S, s = g - j * S;
-                const uint32_t rec = list_base(P, q, nq) + j;
-                const float4 r0 = P.hitrec[2u * rec], r1 = P.hitrec[2u * rec + 1u];
-                const f3 pos = mk3(r0.x, r0.y, r0.z), nrm = mk3(r1.x, r1.y, r1.z);
-                // vector3.inl:357-367 make_orthonormal_basis(u, v, w = n)
-                const f3 bv = fabsf(nrm.x) > fabsf(nrm.y) ? normalize(mk3(-nrm.z, 0.0f, nrm.x)) : normalize(mk3(0.0f, nrm.z, -nrm.y));
-                const f3 bu = cross(bv, nrm);
-                const f3 d = ao_direction(__float_as_uint(r0.w), s, bu, bv, nrm);
-                r = make_ray(pos + d * P.eps, d);
-                best_t = FMAX; best_prim = 0; steps = 0;
-                finite = finite_ray(r);
-                quad = P.quad_ok && finite;
-                st.reset(); st.push(quad ? 0u : P.root); resume = NO_RESUME;
-                tag = rec * S + s;
-                busy = true;
-                rays_total += 1;
-            }
-            if (take == n) break;
-            idle = __ballot(!busy);
-            q = (q + 1u) % nq;                    // list q is exhausted: move on to the next
-            tried += 1u;
-            if (tried < nq) total = hits(q) * S;
-        }
-        if (__ballot(busy) == 0ull) break;        // every list exhausted, no ray in flight
-        int rc = 0;
-        if (COOP_FETCH && P.coop)
-        {
-            rc = (P.fast_ok && __ballot(busy && !finite) == 0ull)
-                ? ray_step_coop<KIND, COUNT, true>(busy, P.pairs, P.prims, P.root, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm)
-                : ray_step_coop<KIND, COUNT, false>(busy, P.pairs, P.prims, P.root, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm);
-        }
-        else if (busy)
-        {
-            rc = (P.fast_ok && __ballot(!finite) == 0ull)
-                ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm)
-                : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, P.radius, true, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm);
-        }
-        if (COUNT) count_wave(cnt, busy);
-        if (busy && rc != 0)
-        {
-            P.aobits[tag] = rc > 0 ? 1u : 0u;
-            busy = false;
-        }
-    }
-
-    unsigned long long rr = rays_total, b = cnt.box, pq = cnt.prim, uni_sum = cnt.w_uni;
-    for (int off = 32; off > 0; off >>= 1)
-    {
-        rr += __shfl_down(rr, off);
-        if (COUNT) { b += __shfl_down(b, off); pq += __shfl_down(pq, off); uni_sum += __shfl_down(uni_sum, off); }
-    }
-    if (__ballot(cnt.aborted) != 0ull && lane == 0) atomicOr(P.counters + 5, 1ull);
-    if (lane == 0)
-    {
-        atomicAdd(P.counters + 1, rr);
-        atomicAdd(P.counters + COUNTERS_TOTAL, rr);
-        if (COUNT)
-        {
-            atomicAdd(P.counters + 3, b);
-            atomicAdd(P.counters + 4, pq);
-            atomicAdd(P.counters + 6, (unsigned long long)cnt.w_steps);
-            atomicAdd(P.counters + 7, (unsigned long long)cnt.w_busy);
-            atomicAdd(P.counters + 9, (unsigned long long)cnt.w_box);
-            atomicAdd(P.counters + 10, (unsigned long long)cnt.w_prim);
-            atomicAdd(P.counters + 11, (unsigned long long)uni_sum);
-        }
-    }
-}
-
-// Two-pass AO, resolve: record slot -> colour 1 - k/S over the occluded samples in sample order
-// (ao/main.cpp:234-238) and the sample mask, at the record's output offset
-__global__ void ao_resolve_kernel(render_params P)
-{
-    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
-    if (slot >= 64u * P.num_frames * P.num_tiles) return;
-    const uint32_t nq = P.xcd_queues ? 8u : 1u;
-    // list q owns record slots [64 F lo(q), 64 F lo(q + 1)), lo(q) = strip_lo(q), F = frames, so
-    // slot / (64 F) is a tile of strip q
-    const uint32_t tile = slot / (64u * P.num_frames);
-    const uint32_t q = (uint32_t)((((uint64_t)tile + 1u) * nq - 1u) / P.num_tiles);
-    const uint32_t j = slot - list_base(P, q, nq);
-    if (j >= *reinterpret_cast<const uint32_t*>(P.counters + COUNTERS_HITS + 8u * q)) return;
-    const uint32_t o = __float_as_uint(P.hitrec[2u * slot + 1u].w);
-    const uint32_t S = P.samples;
-    const uint8_t* bits = P.aobits + (size_t)slot * S;
-    float clr = 1.0f;
-    const float step = 1.0f / (float)S;
-    uint32_t m = 0;
-    for (uint32_t s = 0; s < S; ++s)
-        if (bits[s]) { clr = clr - step; m |= 1u << s; }
-    if (P.color) P.color[o] = make_float4(clr, clr, clr, 1.0f);
-    if (P.occ) P.occ[o] = (uint8_t)m;
-}
-
-// ITEM schedule: the same ray streams as render_unified_kernel (two tiles in flight for AO), but
-// a wave iterates on single traversal items (item_step: one node pair or one primitive per lane)
-// instead of whole descend-to-leaf steps.  The vector-memory unit charges every wave-level load
-// instruction whatever its active lanes, so what counts is how many lanes share each one: a lane
-// that has reached a leaf tests its primitives while its neighbours are still descending.
-// Finished rays are retired and idle lanes refilled only once at least P.refill_min lanes are
-// free (or none is busy), so the ray-generation code runs with many lanes at once.
-template <int KIND, bool AO, bool COUNT, int OCC, bool VOTE>
 __global__ __launch_bounds__(256, OCC) void render_item_kernel(render_params P)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
-    const uint32_t wave = tid >> 6;
     const uint32_t block = blockDim.x;
 
     lds_stack st;
@@ -763,238 +648,84 @@ __global__ __launch_bounds__(256, OCC) void render_item_kernel(render_params P)
     st.stride = block;
     st.top = tid;
     st.end = tid + P.stack_cap * block;
-    uint32_t* ao_area = smem + P.stack_cap * block + wave * AO_WAVE_WORDS;
-    float* recs = reinterpret_cast<float*>(ao_area);
-    uint32_t* masks = ao_area + AO_MASKS;
-    uint8_t* slot_px = reinterpret_cast<uint8_t*>(ao_area + AO_SLOT_PX);
     test_counts cnt = {};
     uint64_t rays_total = 0, hits_total = 0;
 
-    // lane state: mode = ray kind (PRIMARY / AORAY) | DONE once finished and not yet retired
-    constexpr uint32_t IDLE = 0, PRIMARY = 1, AORAY = 2, DONE = 4;
+    // lane state: BUSY while tracing, DONE once finished and not yet retired
+    constexpr uint32_t IDLE = 0, BUSY = 1, DONE = 2;
     uint32_t mode = IDLE;
     ray_t r;
-    float best_t = FMAX, max_t = FMAX;
+    float best_t = FMAX;
     uint32_t best_prim = 0, steps = 0, item = 0;
-    uint32_t tag = 0;        // PRIMARY: pixel lane k of tile C; AORAY: slot | s << 6 | parity << 11
-    bool any = false, occl = false, finite = true;
+    uint32_t out_o = 0;      // output pixel of the lane's ray
+    bool occl = false, finite = true;
 
-    const uint32_t S = AO ? P.samples : 1u;
     const float4 bg = make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
     tile_queue tq = queue_init(P);
-    uint32_t tileC = next_tile(P, tq, lane), parC = 0;
-    uint32_t handedC = 0, pendC = 0, pubC = 0, issC = 0;
-    uint32_t tileD = NONE, parD = 0, slotsD = 0;
-    uint32_t inflight0 = 0, inflight1 = 0;
+    uint32_t tileC = next_tile(P, tq, lane);
+    uint32_t handedC = 0;
 
     for (;;)
     {
-        uint64_t busy = __ballot(mode == PRIMARY || mode == AORAY);
+        uint64_t busy = __ballot(mode == BUSY);
         if (busy == 0ull || 64u - (uint32_t)__popcll(busy) >= P.refill_min)
         {
-            // ---- A1. retire finished rays ------------------------------------------------------
-            if constexpr (AO)
+            // ---- A1. retire finished rays ----------------------------------------------------------
+            if (mode == DONE)
             {
-                const bool ao_done = mode == (AORAY | DONE);
-                if (ao_done && occl) atomicOr(&masks[(tag >> 11) * 64u + (tag & 63u)], 1u << ((tag >> 6) & 31u));
-                inflight0 -= (uint32_t)__popcll(__ballot(ao_done && (tag >> 11) == 0u));
-                inflight1 -= (uint32_t)__popcll(__ballot(ao_done && (tag >> 11) != 0u));
-            }
-            const bool pr_done = mode == (PRIMARY | DONE);
-            const uint64_t fin = __ballot(pr_done);
-            if (fin)
-            {
-                const bool hit = pr_done && best_t != FMAX;
-                const uint64_t hfin = __ballot(hit);
-                if (pr_done)
-                {
-                    // AO: tile C is still the primary's tile (it cannot drain while primaries are
-                    // pending); primary only: tile C may have moved on, the lane kept its pixel
-                    size_t o = tag;
-                    if constexpr (AO)
-                    {
-                        uint32_t x, y, orow;
-                        tile_pixel(P, tileC, tag, x, y, orow);
-                        o = (size_t)orow * P.width + x;
-                    }
-                    if (P.prim_id) P.prim_id[o] = hit ? best_prim : 0xFFFFFFFFu;
-                    if (P.t) P.t[o] = hit ? best_t : -1.0f;
-                    if (AO && hit)
-                    {
-                        const uint32_t slot = pubC + lane_rank(hfin);
-                        const f3 pos = r.ori + r.dir * best_t;                   // ao/main.cpp:202
-                        float* rec = recs + slot * AO_REC_WORDS;
-                        rec[0] = pos.x; rec[1] = pos.y; rec[2] = pos.z;
-                        rec[3] = __uint_as_float(best_prim);
-                        masks[parC * 64u + slot] = 0u;
-                        slot_px[parC * 64u + slot] = (uint8_t)tag;
-                    }
-                    else
-                    {
-                        if (P.color) P.color[o] = hit ? make_float4(1.0f, 1.0f, 1.0f, 1.0f) : bg;
-                        if (P.occ) P.occ[o] = 0;
-                    }
-                }
-                if (AO) pubC += (uint32_t)__popcll(hfin);
-                pendC -= (uint32_t)__popcll(fin);
+                const bool hit = best_t != FMAX;
                 hits_total += hit ? 1 : 0;
+                if (P.prim_id) P.prim_id[out_o] = hit ? best_prim : 0xFFFFFFFFu;
+                if (P.t) P.t[out_o] = hit ? best_t : -1.0f;
+                if (P.color) P.color[out_o] = hit ? make_float4(1.0f, 1.0f, 1.0f, 1.0f) : bg;
+                if (P.occ) P.occ[out_o] = 0;
+                if (COUNT) count_stores(cnt, P, out_o, ST_COLOR | ST_OCC | ST_PID | ST_T);
+                mode = IDLE;
             }
-            if (mode & DONE) mode = IDLE;
-            if constexpr (AO)
+            if (tileC != NONE && handedC >= 64u)
             {
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                // ---- A2. the draining tile is done when its last AO ray is retired -------------
-                if (tileD != NONE && (parD ? inflight1 : inflight0) == 0u)
-                {
-                    if (lane < slotsD)
-                    {
-                        const uint32_t k = slot_px[parD * 64u + lane];
-                        const uint32_t m = masks[parD * 64u + lane];
-                        uint32_t x, y, orow;
-                        tile_pixel(P, tileD, k, x, y, orow);
-                        float clr = 1.0f;
-                        const float step = 1.0f / (float)S;
-                        for (uint32_t s2 = 0; s2 < S; ++s2)
-                            if ((m >> s2) & 1u) clr = clr - step;             // ao/main.cpp:234-238
-                        const size_t o = (size_t)orow * P.width + x;
-                        if (P.color) P.color[o] = make_float4(clr, clr, clr, 1.0f);
-                        if (P.occ) P.occ[o] = (uint8_t)m;
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    tileD = NONE;
-                }
-                // ---- A3. the current tile has handed out every ray: it drains, the next starts -
-                if (tileC != NONE && tileD == NONE && handedC >= 64u && pendC == 0u && issC >= pubC * S)
-                {
-                    tileD = tileC; parD = parC; slotsD = pubC;
-                    tileC = next_tile(P, tq, lane);
-                    parC ^= 1u;
-                    handedC = 0; pendC = 0; pubC = 0; issC = 0;
-                }
+                tileC = next_tile(P, tq, lane);
+                handedC = 0;
             }
-            else
-            {
-                if (tileC != NONE && handedC >= 64u)
-                {
-                    tileC = next_tile(P, tq, lane);
-                    handedC = 0;
-                }
-            }
-            // ---- A4. hand out rays to idle lanes: the current tile's AO rays, then primaries ---
-            uint64_t idle = __ballot(mode == IDLE);
-            if (AO && idle && issC < pubC * S)
-            {
-                const uint32_t avail = pubC * S;
-                const uint32_t cand = issC + lane_rank(idle);
-                const uint32_t n = min(avail - issC, (uint32_t)__popcll(idle));
-                if (mode == IDLE && cand < avail)
-                {
-                    const uint32_t slot = cand / S, smp = cand - slot * S;
-                    uint32_t x, y, orow;
-                    tile_pixel(P, tileC, slot_px[parC * 64u + slot], x, y, orow);
-                    r = ao_ray(P, recs, slot, smp, y * P.width + x);
-                    best_t = FMAX; best_prim = 0; steps = 0; max_t = P.radius; any = true; occl = false;
-                    item = P.root; st.reset();
-                    finite = finite_ray(r);
-                    mode = AORAY;
-                    tag = slot | (smp << 6) | (parC << 11);
-                    rays_total += 1;
-                }
-                issC += n;
-                if (parC) inflight1 += n; else inflight0 += n;
-                idle = __ballot(mode == IDLE);
-            }
-            if (idle && tileC != NONE && handedC < 64u)
+            // ---- A2. hand out the current tile's pixels to idle lanes ----------------------------
+            const uint64_t idle = __ballot(mode == IDLE);
+            if (idle && tileC != NONE)
             {
                 const uint32_t k = handedC + lane_rank(idle);
                 handedC = min(64u, handedC + (uint32_t)__popcll(idle));
                 uint32_t x, y, orow, fr;
-                bool started = false;
                 if (mode == IDLE && k < 64u && tile_pixel(P, tileC, k, x, y, orow, fr))
                 {
                     r = primary_ray(P, fr, x, y);
-                    best_t = FMAX; best_prim = 0; steps = 0; max_t = FMAX; any = false; occl = false;
+                    best_t = FMAX; best_prim = 0; steps = 0; occl = false;
                     item = P.root; st.reset();
                     finite = finite_ray(r);
-                    mode = PRIMARY;
-                    tag = AO ? k : orow * P.width + x;
+                    mode = BUSY;
+                    out_o = orow * P.width + x;
                     rays_total += 1;
-                    started = true;
                 }
-                pendC += (uint32_t)__popcll(__ballot(started));
             }
-            busy = __ballot(mode == PRIMARY || mode == AORAY);
+            busy = __ballot(mode == BUSY);
             if (busy == 0ull)
             {
-                if (tileC == NONE && tileD == NONE) break;
+                if (tileC == NONE) break;
                 continue;
             }
         }
         // ---- B. one traversal item for every busy lane -------------------------------------------
-        const bool my_busy = mode == PRIMARY || mode == AORAY;
-        if constexpr (VOTE)
+        const bool my_busy = mode == BUSY;
+        const bool fast = P.fast_ok && __ballot(my_busy && !finite) == 0ull;
+        if (my_busy)
         {
-            // the wave runs the node step or the primitive step, whichever more lanes wait for
-            // (weighted by P.vote_leaf / 8): lanes of the other kind keep their item meanwhile
-            const bool my_leaf = (item & LEAF_BIT) != 0u;
-            const uint32_t nl = (uint32_t)__popcll(__ballot(my_busy && my_leaf));
-            const uint32_t nn = (uint32_t)__popcll(__ballot(my_busy && !my_leaf));
-            const bool leaf_turn = nn == 0u || nl * P.vote_leaf >= nn * 8u;
-            bool done = false;
-            if (leaf_turn)
-            {
-                if (my_busy && my_leaf)
-                    done = prim_step<KIND, COUNT>(P.prims, r, max_t, any, st, item, best_t, best_prim, occl, cnt, steps, P.step_limit);
-            }
-            else
-            {
-                const bool fast = P.fast_ok && __ballot(my_busy && !my_leaf && !finite) == 0ull;
-                if (my_busy && !my_leaf)
-                    done = fast ? node_step<COUNT, true>(P.pairs, r, max_t, st, item, best_t, cnt, steps, P.step_limit)
-                                : node_step<COUNT, false>(P.pairs, r, max_t, st, item, best_t, cnt, steps, P.step_limit);
-            }
-            if (done) mode |= DONE;
-        }
-        else
-        {
-            const bool fast = P.fast_ok && __ballot(my_busy && !finite) == 0ull;
-            if (my_busy)
-            {
-                const bool done = fast
-                    ? item_step<KIND, COUNT, true>(P.pairs, P.prims, r, max_t, any, st, item, best_t, best_prim, occl, cnt, steps, P.step_limit)
-                    : item_step<KIND, COUNT, false>(P.pairs, P.prims, r, max_t, any, st, item, best_t, best_prim, occl, cnt, steps, P.step_limit);
-                if (done) mode |= DONE;
-            }
+            const bool done = fast
+                ? item_step<KIND, COUNT, true>(P.pairs, P.prims, r, FMAX, false, st, item, best_t, best_prim, occl, cnt, steps, P.step_limit)
+                : item_step<KIND, COUNT, false>(P.pairs, P.prims, r, FMAX, false, st, item, best_t, best_prim, occl, cnt, steps, P.step_limit);
+            if (done) mode = DONE;
         }
         if (COUNT) count_wave(cnt, my_busy);
     }
 
-    unsigned long long rr = rays_total, hh = hits_total, b = cnt.box, q = cnt.prim, uni_sum = cnt.w_uni;
-    for (int off = 32; off > 0; off >>= 1)
-    {
-        rr += __shfl_down(rr, off);
-        hh += __shfl_down(hh, off);
-        if (COUNT) { b += __shfl_down(b, off); q += __shfl_down(q, off); uni_sum += __shfl_down(uni_sum, off); }
-    }
-    if (__ballot(cnt.aborted) != 0ull && lane == 0) atomicOr(P.counters + 5, 1ull);
-    if (lane == 0)
-    {
-        atomicAdd(P.counters + 1, rr);
-        atomicAdd(P.counters + 2, hh);
-        atomicAdd(P.counters + COUNTERS_TOTAL, rr);
-        atomicAdd(P.counters + COUNTERS_TOTAL + 1, hh);
-        if (COUNT)
-        {
-            atomicAdd(P.counters + 3, b);
-            atomicAdd(P.counters + 4, q);
-            atomicAdd(P.counters + 6, (unsigned long long)cnt.w_steps);
-            atomicAdd(P.counters + 7, (unsigned long long)cnt.w_busy);
-            atomicAdd(P.counters + 9, (unsigned long long)cnt.w_box);
-            atomicAdd(P.counters + 10, (unsigned long long)cnt.w_prim);
-            atomicAdd(P.counters + 11, (unsigned long long)uni_sum);
-        }
-    }
+    flush_totals<COUNT>(P, lane, rays_total, hits_total, cnt);
 }
 
 // un-interleave gathered packed shards [count][rows_per_shard][W] into the full image; without a
@@ -1004,6 +735,7 @@ __global__ void unshard_kernel(unshard_params u)
     uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t y = blockIdx.y;
     if (x >= u.width || y >= u.height) return;
+    if (x < u.clip[0] || y < u.clip[1] || x >= u.clip[2] || y >= u.clip[3]) return;
     uint32_t band = y / BAND;
     uint32_t g = band % u.count;
     uint32_t lrow = (band / u.count) * BAND + (y % BAND);
@@ -1013,6 +745,7 @@ __global__ void unshard_kernel(unshard_params u)
     uint32_t occ = u.gocc ? (u.gocc + g * u.stride_occ)[src] : 0u;
     if (u.pid && u.gpid) u.pid[dst] = pid;
     if (u.occ && u.gocc) u.occ[dst] = (uint8_t)occ;
+    if (u.t && u.gt) u.t[dst] = reinterpret_cast<const float*>(u.gt + g * u.stride_t)[src];
     if (!u.color) return;
     if (u.gcolor) { u.color[dst] = reinterpret_cast<const float4*>(u.gcolor + g * u.stride_color)[src]; return; }
     float4 c = make_float4(u.bg[0], u.bg[1], u.bg[2], u.bg[3]);
@@ -1039,21 +772,20 @@ using kernel_fn = void (*)(render_params);
 template <int KIND, int OCC>
 static kernel_fn pick_occ(bool ao, bool count, int sched)
 {
-    if (sched == 1)
+    if (sched == 1 && !ao) return count ? dev::render_item_kernel<KIND, true, OCC> : dev::render_item_kernel<KIND, false, OCC>;
+    if (sched == 2)   // BVH list (step loop), at the default register budgets
     {
-        if (!ao) return count ? dev::render_item_kernel<KIND, false, true, OCC, false> : dev::render_item_kernel<KIND, false, false, OCC, false>;
-        return count ? dev::render_item_kernel<KIND, true, true, OCC, false> : dev::render_item_kernel<KIND, true, false, OCC, false>;
+        if (!ao) return count ? dev::render_unified_kernel<KIND, false, true, 6, 0, true> : dev::render_unified_kernel<KIND, false, false, 6, 0, true>;
+        return count ? dev::render_unified_kernel<KIND, true, true, 5, 0, true> : dev::render_unified_kernel<KIND, true, false, 5, 0, true>;
     }
-    if (sched == 2)
-    {
-        if (!ao) return count ? dev::render_item_kernel<KIND, false, true, OCC, true> : dev::render_item_kernel<KIND, false, false, OCC, true>;
-        return count ? dev::render_item_kernel<KIND, true, true, OCC, true> : dev::render_item_kernel<KIND, true, false, OCC, true>;
-    }
+    if (sched == 3)   // frames in flight (a distinct symbol for profiles), step loop
+        return ao ? dev::render_unified_kernel<KIND, true, false, OCC, 0, false, true>
+                  : dev::render_unified_kernel<KIND, false, false, OCC, 0, false, true>;
     if (!ao) return count ? dev::render_unified_kernel<KIND, false, true, OCC> : dev::render_unified_kernel<KIND, false, false, OCC>;
     return count ? dev::render_unified_kernel<KIND, true, true, OCC> : dev::render_unified_kernel<KIND, true, false, OCC>;
 }
 
-// simple::kernel / multi_hit epilogues: triangles, step loop
+// simple::kernel / multi_hit / whitted epilogues: triangles, step loop
 template <int OCC>
 static kernel_fn pick_shade(bool count, int epi)
 {
@@ -1076,27 +808,8 @@ static kernel_fn pick(bool ao, bool count, int occ, int sched)
     return pick_occ<KIND, 1>(ao, count, sched);
 }
 
-// two-pass AO, pass 1: primary visibility publishing hit records
-template <int KIND>
-static kernel_fn pick_publish(bool count, int occ)
-{
-    if (occ == 8) return count ? dev::render_unified_kernel<KIND, false, true, 8, 4> : dev::render_unified_kernel<KIND, false, false, 8, 4>;
-    if (occ == 6) return count ? dev::render_unified_kernel<KIND, false, true, 6, 4> : dev::render_unified_kernel<KIND, false, false, 6, 4>;
-    return count ? dev::render_unified_kernel<KIND, false, true, 1, 4> : dev::render_unified_kernel<KIND, false, false, 1, 4>;
-}
-
-template <int KIND>
-static kernel_fn pick_ao_pass(bool count, int occ)
-{
-    if (occ == 8) return count ? dev::ao_pass_kernel<KIND, true, 8> : dev::ao_pass_kernel<KIND, false, 8>;
-    if (occ == 6) return count ? dev::ao_pass_kernel<KIND, true, 6> : dev::ao_pass_kernel<KIND, false, 6>;
-    return count ? dev::ao_pass_kernel<KIND, true, 1> : dev::ao_pass_kernel<KIND, false, 1>;
-}
-
 static kernel_fn select_variant(const launch_config& c)
 {
-    if (c.epi == 4) return c.kind == dev::KIND_TRI ? pick_publish<dev::KIND_TRI>(c.count, c.occ)
-                                                   : pick_publish<dev::KIND_SPHERE>(c.count, c.occ);
     if (c.epi) return c.occ == 8 ? pick_shade<8>(c.count, c.epi) : c.occ == 6 ? pick_shade<6>(c.count, c.epi) : pick_shade<1>(c.count, c.epi);
     return c.kind == dev::KIND_TRI ? pick<dev::KIND_TRI>(c.ao, c.count, c.occ, c.sched)
                                    : pick<dev::KIND_SPHERE>(c.ao, c.count, c.occ, c.sched);
@@ -1121,34 +834,6 @@ int render_blocks_per_cu(const launch_config& c)
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, select_variant(c), c.block, render_lds_bytes(c)) != hipSuccess)
         return 1;
     return n > 0 ? n : 1;
-}
-
-size_t ao_pass_lds_bytes(const launch_config& c) { return size_t(c.stack_cap) * c.block * 4; }
-
-static kernel_fn ao_pass_variant(const launch_config& c)
-{
-    return c.kind == dev::KIND_TRI ? pick_ao_pass<dev::KIND_TRI>(c.count, c.occ) : pick_ao_pass<dev::KIND_SPHERE>(c.count, c.occ);
-}
-
-hipError_t launch_ao_pass(const render_params& p, const launch_config& c, int grid, hipStream_t s)
-{
-    hipLaunchKernelGGL(ao_pass_variant(c), dim3(grid), dim3(c.block), ao_pass_lds_bytes(c), s, p);
-    return hipGetLastError();
-}
-
-int ao_pass_blocks_per_cu(const launch_config& c)
-{
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ao_pass_variant(c), c.block, ao_pass_lds_bytes(c)) != hipSuccess)
-        return 1;
-    return n > 0 ? n : 1;
-}
-
-hipError_t launch_ao_resolve(const render_params& p, hipStream_t s)
-{
-    const uint32_t n = 64u * p.num_frames * p.num_tiles;
-    hipLaunchKernelGGL(dev::ao_resolve_kernel, dim3((n + 255u) / 256u), dim3(256), 0, s, p);
-    return hipGetLastError();
 }
 
 hipError_t launch_unshard(const unshard_params& u, hipStream_t s)

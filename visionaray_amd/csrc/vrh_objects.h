@@ -1,0 +1,91 @@
+// visionaray_amd/csrc/vrh_objects.h -- the opaque objects of the C-ABI (include/vrh.h), shared by
+// the runtime (vrh_runtime.hip) and the multi-GPU render groups (vrh_group.hip).
+#pragma once
+
+#include "vrh_internal.h"
+#include "vrh_kernels.h"
+
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+struct vrh_ctx
+{
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int num_cus = 0;
+    // device counters (u64), see render_params::counters; [0..7] reset per frame
+    unsigned long long* counters = nullptr;
+    // one hipEvent pair per frame since vrh_stats_reset (ring of VRH_MAX_TIMED_FRAMES)
+    std::vector<hipEvent_t> ev_start, ev_stop;
+    uint32_t frames = 0;
+    uint32_t last_slot = 0;
+    vrh_frame_stats last{};
+    bool have_frame = false;
+    // tuning options (0 = automatic), vrh_ctx_set_option
+    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_dcap = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0, opt_pop = 0, opt_coop = 0, opt_scalar = 0, opt_layout = 0;
+};
+
+struct vrh_scene
+{
+    vrh_ctx* ctx = nullptr;
+    float4* pairs = nullptr;
+    float4* prims = nullptr;
+    float4* normals = nullptr;
+    float4* quads = nullptr;     // 4-wide any-hit records (vrh_quad.cpp), null if the scene has none
+    float4* vnormals = nullptr;  // per-vertex normals (3 per prim_id), VRH_NORMALS_PER_VERTEX
+    vrh::node32* dnodes = nullptr;    // GPU-built scenes: the tree in the reference layout (download)
+    uint32_t* dindices = nullptr;
+    uint32_t roots[vrh::MAX_LIST] = {};   // root link of every BVH (one unless a scene list)
+    uint32_t num_roots = 1;
+    uint32_t num_pairs = 0;          // pair records in `pairs`
+    uint32_t quad_depth = 0;
+    bool finite_bounds = true;   // every node bound finite (enables the hardware min/max slab path)
+    vrh_scene_info info{};
+};
+
+struct vrh_shading
+{
+    vrh_ctx* ctx = nullptr;
+    vrh::dev::plastic_t* materials = nullptr;
+    vrh::dev::point_light_t* lights = nullptr;
+    uint32_t num_materials = 0, num_lights = 0;
+};
+
+struct vrh_hit_mask
+{
+    vrh_ctx* ctx = nullptr;
+    float2* tc = nullptr;         // 3 per prim_id
+    uint8_t* mask = nullptr;
+    uint32_t num_tc = 0, w = 0, h = 0;
+};
+
+struct vrh_rt
+{
+    vrh_ctx* ctx = nullptr;
+    uint32_t width = 0, height = 0;
+    float4* color = nullptr;
+    uint32_t* prim_id = nullptr;
+    float* t = nullptr;
+    uint8_t* occ = nullptr;
+    bool owned = false;
+    uint32_t* mh_prim_id = nullptr;   // multi_hit<N> lists [pixel][N] (always owned)
+    float* mh_t = nullptr;
+    uint32_t mh_n = 0;
+};
+
+// status plumbing shared by the C-ABI translation units: every HIP call is checked, nothing throws
+#define VRH_HIP(call)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (call);                                                                    \
+        if (e_ != hipSuccess) {                                                                    \
+            vrh::set_error(std::string(#call) + ": " + hipGetErrorString(e_));                    \
+            return e_ == hipErrorOutOfMemory ? VRH_ERR_OOM : VRH_ERR_HIP;                          \
+        }                                                                                          \
+    } while (0)
+
+#define VRH_CHECK(cond, msg)                                                                       \
+    do {                                                                                           \
+        if (!(cond)) { vrh::set_error(msg); return VRH_ERR_INVALID; }                              \
+    } while (0)

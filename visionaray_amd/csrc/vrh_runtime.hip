@@ -27,87 +27,7 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 
 using namespace vrh;
 
-#define VRH_HIP(call)                                                                              \
-    do {                                                                                           \
-        hipError_t e_ = (call);                                                                    \
-        if (e_ != hipSuccess) {                                                                    \
-            set_error(std::string(#call) + ": " + hipGetErrorString(e_));                         \
-            return e_ == hipErrorOutOfMemory ? VRH_ERR_OOM : VRH_ERR_HIP;                          \
-        }                                                                                          \
-    } while (0)
-
-#define VRH_CHECK(cond, msg)                                                                       \
-    do {                                                                                           \
-        if (!(cond)) { set_error(msg); return VRH_ERR_INVALID; }                                   \
-    } while (0)
-
-struct vrh_ctx
-{
-    int device = 0;
-    hipStream_t stream = nullptr;
-    bool own_stream = false;
-    int num_cus = 0;
-    // device counters (u64), see render_params::counters; [0..7] reset per frame
-    unsigned long long* counters = nullptr;
-    // one hipEvent pair per frame since vrh_stats_reset (ring of VRH_MAX_TIMED_FRAMES)
-    std::vector<hipEvent_t> ev_start, ev_stop;
-    uint32_t frames = 0;
-    uint32_t last_slot = 0;
-    vrh_frame_stats last{};
-    bool have_frame = false;
-    // tuning options (0 = automatic), vrh_ctx_set_option
-    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_vote = 0, opt_dcap = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0, opt_pop = 0, opt_coop = 0, opt_scalar = 0, opt_layout = 0;
-    // two-pass AO scratch (grown on demand): 32-B hit records and one byte per AO ray, per pixel slot
-    float4* hitrec = nullptr;
-    uint8_t* aobits = nullptr;
-    size_t hitrec_slots = 0, aobits_bytes = 0;
-};
-
-struct vrh_scene
-{
-    vrh_ctx* ctx = nullptr;
-    float4* pairs = nullptr;
-    float4* prims = nullptr;
-    float4* normals = nullptr;
-    float4* quads = nullptr;     // 4-wide any-hit records (vrh_quad.cpp), null if the scene has none
-    float4* vnormals = nullptr;  // per-vertex normals (3 per prim_id), VRH_NORMALS_PER_VERTEX
-    node32* dnodes = nullptr;    // GPU-built scenes: the tree in the reference layout (download)
-    uint32_t* dindices = nullptr;
-    uint32_t root = 0;
-    uint32_t quad_depth = 0;
-    bool finite_bounds = true;   // every node bound finite (enables the hardware min/max slab path)
-    vrh_scene_info info{};
-};
-
-struct vrh_shading
-{
-    vrh_ctx* ctx = nullptr;
-    dev::plastic_t* materials = nullptr;
-    dev::point_light_t* lights = nullptr;
-    uint32_t num_materials = 0, num_lights = 0;
-};
-
-struct vrh_hit_mask
-{
-    vrh_ctx* ctx = nullptr;
-    float2* tc = nullptr;         // 3 per prim_id
-    uint8_t* mask = nullptr;
-    uint32_t num_tc = 0, w = 0, h = 0;
-};
-
-struct vrh_rt
-{
-    vrh_ctx* ctx = nullptr;
-    uint32_t width = 0, height = 0;
-    float4* color = nullptr;
-    uint32_t* prim_id = nullptr;
-    float* t = nullptr;
-    uint8_t* occ = nullptr;
-    bool owned = false;
-    uint32_t* mh_prim_id = nullptr;   // multi_hit<N> lists [pixel][N] (always owned)
-    float* mh_t = nullptr;
-    uint32_t mh_n = 0;
-};
+#include "vrh_objects.h"
 
 namespace {
 
@@ -177,8 +97,6 @@ VRH_API int vrh_ctx_destroy(vrh_ctx* ctx)
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->counters) (void)hipFree(ctx->counters);
-    if (ctx->hitrec) (void)hipFree(ctx->hitrec);
-    if (ctx->aobits) (void)hipFree(ctx->aobits);
     for (auto e : ctx->ev_start) (void)hipEventDestroy(e);
     for (auto e : ctx->ev_stop) (void)hipEventDestroy(e);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -196,7 +114,7 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
         VRH_CHECK(value % 64 == 0, "vrh_ctx_set_option: block threads must be a multiple of 64");
         ctx->opt_block = int(value); break;
     case VRH_OPT_STACK_CAP: ctx->opt_stack = int(value); break;
-    case VRH_OPT_AO_SCHEDULE: VRH_CHECK(value == 0 || (value >= 3 && value <= 6), "vrh_ctx_set_option: schedule is 3 (step), 4 (item), 5 (vote) or 6 (two-pass AO)"); ctx->opt_sched = int(value); break;
+    case VRH_OPT_AO_SCHEDULE: VRH_CHECK(value == 0 || value == 3 || value == 4, "vrh_ctx_set_option: schedule is 3 (step loop) or 4 (item loop, primary visibility)"); ctx->opt_sched = int(value); break;
     case VRH_OPT_WIDE_ANYHIT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: wide any-hit is 1 (on) or 2 (off)"); ctx->opt_wide = int(value); break;
     case VRH_OPT_DESCENT_CAP: ctx->opt_dcap = int(value); break;
     case VRH_OPT_COOP_FETCH:
@@ -210,7 +128,6 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
     case VRH_OPT_POP_ON_MISS: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pop on miss is 1 (on) or 2 (off)"); ctx->opt_pop = int(value); break;
     case VRH_OPT_PAIR_LAYOUT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pair layout is 1 (line pairing) or 2 (builder order)"); ctx->opt_layout = int(value); break;
     case VRH_OPT_SCALAR_FETCH: VRH_CHECK(value <= 2, "vrh_ctx_set_option: scalar fetch is 1 (on) or 2 (off)"); ctx->opt_scalar = int(value); break;
-    case VRH_OPT_VOTE_LEAF: VRH_CHECK(value <= 64, "vrh_ctx_set_option: vote weight is 1..64"); ctx->opt_vote = int(value); break;
     case VRH_OPT_REFILL_MIN: VRH_CHECK(value <= 64, "vrh_ctx_set_option: refill threshold is 1..64"); ctx->opt_refill = int(value); break;
     case VRH_OPT_BLOCKS_PER_CU: ctx->opt_bpc = int(value); break;
     case VRH_OPT_WAVES_PER_SIMD: VRH_CHECK(value == 0 || value == 1 || value == 5 || value == 6 || value == 8, "vrh_ctx_set_option: waves per SIMD is 1, 5, 6 or 8"); ctx->opt_occ = int(value); break;
@@ -271,13 +188,15 @@ VRH_API int vrh_scene_upload(vrh_ctx* ctx, const void* nodes_v, uint32_t num_nod
     // depth (root depth 0) by iterative DFS over links
     uint32_t max_depth = 0;
     {
+        // every pair may be reached at most once: a pair reached twice (a DAG or a cycle) is rejected
         std::vector<std::pair<uint32_t, uint32_t>> st;
+        std::vector<uint8_t> seen(npairs, 0);
         if (!(root & 0x80000000u)) st.push_back({ root, 1u });
-        size_t visited = 0;
         while (!st.empty())
         {
             auto e = st.back(); st.pop_back();
-            if (++visited > npairs) { set_error("vrh_scene_upload: BVH is not a tree"); return VRH_ERR_INVALID; }
+            if (seen[e.first]) { set_error("vrh_scene_upload: BVH is not a tree (a node pair is reached twice)"); return VRH_ERR_INVALID; }
+            seen[e.first] = 1;
             max_depth = std::max(max_depth, e.second);
             uint32_t w[4];
             std::memcpy(w, &pairs[4 * e.first + 3], 16);
@@ -311,6 +230,7 @@ VRH_API int vrh_scene_upload(vrh_ctx* ctx, const void* nodes_v, uint32_t num_nod
         }
         for (uint32_t k = 0; k < npairs; ++k)
             if (perm[k] == 0xFFFFFFFFu) perm[k] = next++;      // unreachable records keep a slot
+        if (next != npairs) { set_error("vrh_scene_upload: pair layout: not a permutation"); return VRH_ERR_INVALID; }
         std::vector<float4> np(pairs.size());
         for (uint32_t k = 0; k < npairs; ++k)
         {
@@ -377,7 +297,8 @@ VRH_API int vrh_scene_upload(vrh_ctx* ctx, const void* nodes_v, uint32_t num_nod
     auto* sc = new (std::nothrow) vrh_scene;
     if (!sc) { set_error("host allocation failed"); return VRH_ERR_OOM; }
     sc->ctx = ctx;
-    sc->root = root;
+    sc->roots[0] = root;
+    sc->num_pairs = npairs;
     sc->finite_bounds = finite_bounds;
     auto fail = [&](hipError_t e, const char* what) {
         set_error(std::string(what) + ": " + hipGetErrorString(e));
@@ -407,6 +328,7 @@ VRH_API int vrh_scene_upload(vrh_ctx* ctx, const void* nodes_v, uint32_t num_nod
         bytes += size_t(num_prims) * sizeof(float4);
     }
     sc->info.num_nodes = num_nodes;
+    sc->info.num_bvhs = 1;
     sc->info.num_prims = num_prims;
     sc->info.num_indices = num_indices;
     sc->info.prim_kind = prim_kind;
@@ -440,6 +362,102 @@ VRH_API int vrh_scene_free(vrh_scene* sc)
     return VRH_OK;
 }
 
+namespace {
+// scene lists: the pair records of one member re-based into the combined arrays (inner links by
+// the member's first pair, leaf links by its first primitive)
+__global__ void rebase_links_kernel(float4* pairs, uint32_t n, uint32_t pair_off, uint32_t prim_off)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t* w = reinterpret_cast<uint32_t*>(pairs + 4u * size_t(i) + 3u);
+    for (int c = 0; c < 2; ++c)
+        w[c] = (w[c] & 0x80000000u) ? (0x80000000u | ((w[c] & 0x7FFFFFFFu) + prim_off)) : w[c] + pair_off;
+}
+} // namespace
+
+VRH_API int vrh_scene_list_create(vrh_ctx* ctx, const vrh_scene* const* scenes, uint32_t count,
+                                  const void* face_normals, uint32_t num_normals, vrh_scene** out)
+{
+    VRH_CHECK(ctx && scenes && out, "vrh_scene_list_create: null argument");
+    VRH_CHECK(count >= 1 && count <= VRH_MAX_SCENE_LIST, "vrh_scene_list_create: 1..VRH_MAX_SCENE_LIST scenes");
+    *out = nullptr;
+    uint64_t pairs = 0, prims = 0, nodes = 0, bytes = 0;
+    uint32_t kind = scenes[0] ? scenes[0]->info.prim_kind : 0u, depth = 0, max_pid = 0, max_gid = 0;
+    bool finite = true;
+    for (uint32_t i = 0; i < count; ++i)
+    {
+        const vrh_scene* m = scenes[i];
+        VRH_CHECK(m && m->ctx == ctx, "vrh_scene_list_create: scene missing or of another context");
+        VRH_CHECK(m->num_roots == 1, "vrh_scene_list_create: members must be single BVHs");
+        VRH_CHECK(m->info.prim_kind == kind, "vrh_scene_list_create: members must share one primitive type");
+        pairs += m->num_pairs;
+        prims += m->info.num_indices;
+        nodes += m->info.num_nodes;
+        depth = std::max(depth, m->info.max_depth);
+        max_pid = std::max(max_pid, m->info.max_prim_id);
+        max_gid = std::max(max_gid, m->info.max_geom_id);
+        finite = finite && m->finite_bounds;
+    }
+    VRH_CHECK(pairs < 0x80000000ull && prims < 0x80000000ull && nodes < 0xFFFFFFF0ull, "vrh_scene_list_create: list too large");
+    VRH_CHECK(!face_normals || uint64_t(num_normals) > max_pid, "vrh_scene_list_create: face normals must cover every prim_id");
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    auto* sc = new (std::nothrow) vrh_scene;
+    if (!sc) { set_error("host allocation failed"); return VRH_ERR_OOM; }
+    sc->ctx = ctx;
+    auto fail = [&](hipError_t e, const char* what) {
+        set_error(std::string("vrh_scene_list_create: ") + what + ": " + hipGetErrorString(e));
+        vrh_scene_free(sc);
+        return e == hipErrorOutOfMemory ? VRH_ERR_OOM : VRH_ERR_HIP;
+    };
+    const uint32_t f4_per = kind == VRH_PRIM_TRI64 ? 3u : 2u;
+    hipError_t e;
+    if ((e = hipMalloc(&sc->pairs, std::max<uint64_t>(pairs, 1) * 64)) != hipSuccess) return fail(e, "pairs");
+    if ((e = hipMalloc(&sc->prims, prims * f4_per * 16)) != hipSuccess) return fail(e, "prims");
+    uint32_t pair_off = 0, prim_off = 0;
+    for (uint32_t i = 0; i < count; ++i)
+    {
+        const vrh_scene* m = scenes[i];
+        if (m->num_pairs)
+        {
+            if ((e = hipMemcpyAsync(sc->pairs + 4u * size_t(pair_off), m->pairs, size_t(m->num_pairs) * 64,
+                                    hipMemcpyDeviceToDevice, ctx->stream)) != hipSuccess) return fail(e, "copy pairs");
+            hipLaunchKernelGGL(rebase_links_kernel, dim3((m->num_pairs + 255u) / 256u), dim3(256), 0, ctx->stream,
+                               sc->pairs + 4u * size_t(pair_off), m->num_pairs, pair_off, prim_off);
+            if ((e = hipGetLastError()) != hipSuccess) return fail(e, "rebase");
+        }
+        if ((e = hipMemcpyAsync(sc->prims + size_t(f4_per) * prim_off, m->prims, size_t(m->info.num_indices) * f4_per * 16,
+                                hipMemcpyDeviceToDevice, ctx->stream)) != hipSuccess) return fail(e, "copy prims");
+        const uint32_t r = m->roots[0];
+        sc->roots[i] = (r & 0x80000000u) ? (0x80000000u | ((r & 0x7FFFFFFFu) + prim_off)) : r + pair_off;
+        pair_off += m->num_pairs;
+        prim_off += m->info.num_indices;
+    }
+    bytes = std::max<uint64_t>(pairs, 1) * 64 + prims * f4_per * 16;
+    if (face_normals)
+    {
+        if ((e = hipMalloc(&sc->normals, size_t(num_normals) * 16)) != hipSuccess) return fail(e, "normals");
+        if ((e = hipMemcpyAsync(sc->normals, face_normals, size_t(num_normals) * 16, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+            return fail(e, "upload normals");
+        bytes += uint64_t(num_normals) * 16;
+    }
+    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return fail(e, "sync");
+    sc->num_roots = count;
+    sc->num_pairs = uint32_t(pairs);
+    sc->finite_bounds = finite;
+    sc->info.num_nodes = uint32_t(nodes);
+    sc->info.num_prims = uint32_t(prims);
+    sc->info.num_indices = uint32_t(prims);
+    sc->info.prim_kind = kind;
+    sc->info.max_depth = depth;
+    sc->info.max_prim_id = max_pid;
+    sc->info.max_geom_id = max_gid;
+    sc->info.device_bytes = bytes;
+    sc->info.num_bvhs = count;
+    *out = sc;
+    return VRH_OK;
+}
+
 VRH_API int vrh_scene_build(vrh_ctx* ctx, const void* prims, uint32_t num_prims, uint32_t prim_kind,
                             const void* face_normals, const vrh_build_desc* desc, vrh_scene** out)
 {
@@ -462,7 +480,8 @@ VRH_API int vrh_scene_build(vrh_ctx* ctx, const void* prims, uint32_t num_prims,
     }
     sc->ctx = ctx;
     sc->pairs = b.pairs; sc->prims = b.prims; sc->dnodes = b.nodes; sc->dindices = b.indices;
-    sc->root = b.root;
+    sc->roots[0] = b.root;
+    sc->num_pairs = b.num_pairs;
     sc->finite_bounds = b.finite;
     uint64_t bytes = uint64_t(std::max(b.num_pairs, 1u)) * 64 + uint64_t(num_prims) * (prim_kind == VRH_PRIM_TRI64 ? 48 : 32);
     if (face_normals)
@@ -486,6 +505,7 @@ VRH_API int vrh_scene_build(vrh_ctx* ctx, const void* prims, uint32_t num_prims,
     sc->info.max_prim_id = b.max_prim_id;
     sc->info.max_geom_id = b.max_geom_id;
     sc->info.gpu_built = 1;
+    sc->info.num_bvhs = 1;
     sc->info.build_ms = b.build_ms;
     *out = sc;
     return VRH_OK;
@@ -747,8 +767,8 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
                              uint32_t num_frames, const vrh_kernel_desc* k, const vrh_shard* shard,
                              uint32_t frame_num)
 {
-    (void)frame_num;  // the built-in kernels are deterministic; kept for cuda_sched::frame parity
     VRH_CHECK(ctx && sc && rt && cams && k, "vrh_render: null argument");
+    VRH_CHECK(rt->ctx == ctx && sc->ctx == ctx, "vrh_render: scene / render target of another context");
     VRH_CHECK(num_frames >= 1 && num_frames <= VRH_MAX_BATCH, "vrh_render_batch: 1..VRH_MAX_BATCH frames");
     const vrh_camera* cam = cams;
     for (uint32_t f = 1; f < num_frames; ++f)
@@ -759,6 +779,7 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     const bool multi = k->kind == VRH_KERNEL_MULTI_HIT;
     const bool whitted = k->kind == VRH_KERNEL_WHITTED;
     const bool shade = k->kind == VRH_KERNEL_SIMPLE || multi || whitted;
+    const bool list = sc->num_roots > 1;
     if (multi)
     {
         VRH_CHECK(k->max_hits >= 1 && k->max_hits <= VRH_MAX_HITS, "vrh_render: max_hits must be in [1, 16]");
@@ -768,6 +789,7 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     {
         VRH_CHECK(k->shading, "vrh_render: the shading kernels need a vrh_shading (materials, lights)");
         if (sc->info.prim_kind != VRH_PRIM_TRI64) { set_error("vrh_render: the shading kernels support triangles"); return VRH_ERR_UNSUPPORTED; }
+        if (list) { set_error("vrh_render: the shading kernels take a single BVH (scene lists: primary and AO kernels)"); return VRH_ERR_UNSUPPORTED; }
         VRH_CHECK(k->shading->num_materials > sc->info.max_geom_id, "vrh_render: a geom_id has no material");
         VRH_CHECK(k->normal_binding <= VRH_NORMALS_PER_VERTEX, "vrh_render: unknown normal binding");
         if (k->normal_binding == VRH_NORMALS_PER_FACE) VRH_CHECK(sc->normals, "vrh_render: per-face shading needs face normals");
@@ -776,7 +798,8 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     if (ao)
     {
         VRH_CHECK(k->samples >= 1 && k->samples <= 32, "vrh_render: AO samples must be in [1, 32]");
-        VRH_CHECK(sc->info.prim_kind != VRH_PRIM_TRI64 || sc->normals, "vrh_render: AO on triangles needs face normals");
+        // the occlusion target holds one bit per sample in a byte
+        VRH_CHECK(!rt->occ || k->samples <= 8, "vrh_render: a VRH_RT_OCC target records at most 8 AO samples");
         VRH_CHECK(sc->normals, "vrh_render: AO needs normals");
     }
     const vrh_hit_mask* hmask = k->hit_mask;
@@ -812,20 +835,22 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     lc.block = ctx->opt_block ? ctx->opt_block : 64;
     lc.stack_cap = int(cap);
     lc.epi = whitted ? 3 : multi ? 2 : shade ? 1 : 0;
-    // shading epilogues: no VGPR cap (their lane state spills at 6 waves/SIMD; measured faster at 4,
-    // profiles/r01_shade/shade_bench.jsonl); AO on the step loop: 5 waves/SIMD (96 VGPRs, no spills:
-    // 4-6 % faster than 6 with 18 spilled VGPRs); primary visibility: 6 (profiles/r01_ab_waves/)
-    lc.occ = ctx->opt_occ ? ctx->opt_occ : lc.epi ? 1 : (lc.ao && lc.sched == 0) ? 5 : 6;
     lc.max_hits = multi ? int(k->max_hits) : 0;
     // auto: the item loop for sphere primary visibility (short leaves of cheap tests, where the
     // step loop's leaf iterations run at ~20 % lane utilisation), the step loop otherwise
     if (ctx->opt_sched == 0) lc.sched = (lc.kind == 1 && !ao) ? 1 : 0;
-    else lc.sched = ctx->opt_sched == 4 ? 1 : ctx->opt_sched == 5 ? 2 : (ctx->opt_sched == 6 && ao) ? 3 : 0;
+    else lc.sched = (ctx->opt_sched == 4 && !ao) ? 1 : 0;
     if (shade) lc.sched = 0;   // the shading epilogue lives in the step loop
     if (hmask) lc.sched = 0;   // the mask test lives in the step loop's leaf test
-    // two-pass AO: pass 1 is the step loop's primary stream with the hit-record epilogue
-    launch_config lc1 = lc;
-    if (lc.sched == 3) { lc1.ao = false; lc1.epi = 4; lc1.sched = 0; }
+    if (list) lc.sched = 2;    // BVH lists: the step loop with the list merge
+    // frames in flight on the step loop (primary / AO, uncounted): the BATCH instantiation
+    if (lc.sched == 0 && num_frames > 1 && !lc.count && lc.epi == 0 && !hmask) lc.sched = 3;
+    // shading epilogues: no VGPR cap (their lane state spills at 6 waves/SIMD; measured faster at 4,
+    // profiles/r01_shade/shade_bench.jsonl); AO on the step loop: 5 waves/SIMD (96 VGPRs, no spills:
+    // 4-6 % faster than 6 with 18 spilled VGPRs); primary visibility: 6 (profiles/r01_ab_waves/);
+    // BVH lists run at these defaults
+    lc.occ = ctx->opt_occ ? ctx->opt_occ : lc.epi ? 1 : (lc.ao && lc.sched != 1) ? 5 : 6;
+    if (list) lc.occ = ao ? 5 : 6;
     if (render_lds_bytes(lc) > 160u * 1024u)
     {
         set_error("vrh_render: BVH depth " + std::to_string(sc->info.max_depth) + " needs more LDS stack than a CU has");
@@ -836,32 +861,42 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     if (rc) return rc;
 
     render_params p{};
-    p.pairs = sc->pairs; p.prims = sc->prims; p.normals = sc->normals; p.root = sc->root;
+    p.pairs = sc->pairs; p.prims = sc->prims; p.normals = sc->normals; p.root = sc->roots[0];
+    p.num_roots = sc->num_roots;
+    for (uint32_t i = 0; i < sc->num_roots; ++i) p.roots[i] = sc->roots[i];
     p.step_limit = sc->info.num_nodes + sc->info.num_indices + 16u;
     // measured: profiles/r01_ab (AO), profiles/r01_ab_primary (primary visibility: the item loop
     // refills at 32 free lanes; the step loop pops on a miss and caps a descent at 8 visits per
     // step, +6 % on hf1M and +36 % on hf10M; both hurt AO)
-    const bool primary_step = lc.sched == 0 && !lc.ao && lc.epi == 0;
-    p.refill_min = ctx->opt_refill ? uint32_t(ctx->opt_refill) : (lc.sched == 0 || (lc.sched == 1 && !lc.ao)) ? 32u : 16u;
+    const bool primary_step = lc.sched != 1 && !lc.ao && lc.epi == 0;
+    p.refill_min = ctx->opt_refill ? uint32_t(ctx->opt_refill) : 32u;
     p.refill_min_primary = ctx->opt_refill ? uint32_t(ctx->opt_refill) : 1u;
-    p.vote_leaf = ctx->opt_vote ? uint32_t(ctx->opt_vote) : 8u;
     p.descent_cap = ctx->opt_dcap ? uint32_t(ctx->opt_dcap) : primary_step ? 8u : 0xFFFFFFFFu;
     // shading epilogues (simple / multi_hit / whitted) pop on a miss too: +4-7 % (profiles/r01_shade/)
     const bool pop = ctx->opt_pop == 1 || (ctx->opt_pop == 0 && (primary_step || lc.epi != 0));
     p.step_flags = (pop ? 1u : 0u) | (ctx->opt_scalar == 2 ? 0u : 2u);
-    // cooperative pair fetch (step loop, binary records; the 4-wide any-hit records keep the
-    // per-lane fetch)
-    p.coop = (ctx->opt_coop == 1 && !p.quad_ok) ? 1u : 0u;
     p.stack_cap = cap;
     p.fast_ok = (sc->finite_bounds && !ctx->opt_exact_minmax) ? 1u : 0u;
     p.quads = sc->quads;
     p.quad_ok = (sc->quads && p.fast_ok && ctx->opt_wide == 1) ? 1u : 0u;   // auto: off (measured slower)
+    // cooperative pair fetch (step loop, binary records; the 4-wide any-hit records keep the
+    // per-lane fetch, so it is off whenever they are on)
+    p.coop = (ctx->opt_coop == 1 && !p.quad_ok) ? 1u : 0u;
     for (uint32_t f = 0; f < num_frames; ++f)
     {
         std::memcpy(p.cam[f].eye, cams[f].eye, 12); std::memcpy(p.cam[f].cam_u, cams[f].cam_u, 12);
         std::memcpy(p.cam[f].cam_v, cams[f].cam_v, 12); std::memcpy(p.cam[f].cam_w, cams[f].cam_w, 12);
+        // scissor_box (scheduler.h:25-31, default recti(0, 0, w, h) at :175): pixels x0 <= x < x1,
+        // y0 <= y < y1 are rendered, the rest of the target is left as it is (cuda_sched.inl:71)
+        const uint32_t* sb = cams[f].scissor;
+        const bool whole_image = sb[0] == 0 && sb[1] == 0 && sb[2] == 0 && sb[3] == 0;
+        p.cam[f].clip[0] = whole_image ? 0u : std::min(sb[0], cam->width);
+        p.cam[f].clip[1] = whole_image ? 0u : std::min(sb[1], cam->height);
+        p.cam[f].clip[2] = whole_image ? cam->width : std::min(sb[2], cam->width);
+        p.cam[f].clip[3] = whole_image ? cam->height : std::min(sb[3], cam->height);
     }
     p.num_frames = num_frames;
+    p.frame_num = frame_num;
     p.frame_rows = frame_rows;
     p.width = cam->width; p.height = cam->height;
     p.samples = ao ? k->samples : 0; p.radius = k->radius; p.eps = k->eps;
@@ -892,33 +927,11 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
         p.mh_t = rt->mh_t;
     }
 
-    const bool two_pass = lc.sched == 3;
-    int per_cu = render_blocks_per_cu(two_pass ? lc1 : lc);
+    int per_cu = render_blocks_per_cu(lc);
     if (ctx->opt_bpc) per_cu = std::min(per_cu, ctx->opt_bpc);
     const int waves_per_block = lc.block / 64;
     const uint64_t units = uint64_t(num_frames) * p.num_tiles;
     int grid = std::max(1, int(std::min<uint64_t>(uint64_t(ctx->num_cus) * per_cu, (units + waves_per_block - 1) / waves_per_block)));
-    int grid2 = 0;
-    if (two_pass)
-    {
-        // scratch: a 32-B record and `samples` AO bytes per pixel slot of the frame's tiles
-        const size_t slots = size_t(64) * units;
-        if (ctx->hitrec_slots < slots || ctx->aobits_bytes < slots * p.samples)
-        {
-            VRH_HIP(hipStreamSynchronize(ctx->stream));   // earlier frames may still read them
-            if (ctx->hitrec) { (void)hipFree(ctx->hitrec); ctx->hitrec = nullptr; ctx->hitrec_slots = 0; }
-            if (ctx->aobits) { (void)hipFree(ctx->aobits); ctx->aobits = nullptr; ctx->aobits_bytes = 0; }
-            VRH_HIP(hipMalloc(&ctx->hitrec, slots * 32));
-            ctx->hitrec_slots = slots;
-            VRH_HIP(hipMalloc(&ctx->aobits, slots * 32));   // room for the largest sample count
-            ctx->aobits_bytes = slots * 32;
-        }
-        p.hitrec = ctx->hitrec;
-        p.aobits = ctx->aobits;
-        int per_cu2 = ao_pass_blocks_per_cu(lc);
-        if (ctx->opt_bpc) per_cu2 = std::min(per_cu2, ctx->opt_bpc);
-        grid2 = std::max(1, ctx->num_cus * per_cu2);
-    }
 
     const uint32_t slot = ctx->frames % VRH_MAX_TIMED_FRAMES;
     while (ctx->ev_start.size() <= slot)
@@ -931,26 +944,17 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     }
     VRH_HIP(hipMemsetAsync(ctx->counters, 0, COUNTERS_FRAME * sizeof(unsigned long long), ctx->stream));
     VRH_HIP(hipEventRecord(ctx->ev_start[slot], ctx->stream));
-    if (p.num_tiles > 0)
-    {
-        if (two_pass)
-        {
-            VRH_HIP(launch_render(p, lc1, grid, ctx->stream));
-            VRH_HIP(launch_ao_pass(p, lc, grid2, ctx->stream));
-            VRH_HIP(launch_ao_resolve(p, ctx->stream));
-        }
-        else
-            VRH_HIP(launch_render(p, lc, grid, ctx->stream));
-    }
+    if (p.num_tiles > 0) VRH_HIP(launch_render(p, lc, grid, ctx->stream));
     VRH_HIP(hipEventRecord(ctx->ev_stop[slot], ctx->stream));
     ctx->last_slot = slot;
     ctx->frames++;
 
     ctx->last = vrh_frame_stats{};
-    ctx->last.launches = p.num_tiles > 0 ? (two_pass ? 3u : 1u) : 0u;
+    ctx->last.launches = p.num_tiles > 0 ? 1u : 0u;
     ctx->last.grid_blocks = uint32_t(grid);
     ctx->last.block_threads = uint32_t(lc.block);
     ctx->last.stack_depth = cap;
+    ctx->last.frames = num_frames;
     ctx->have_frame = true;
     return VRH_OK;
 }
@@ -971,7 +975,7 @@ VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats)
     VRH_HIP(hipEventSynchronize(ctx->ev_stop[ctx->last_slot]));
     float ms = 0.0f;
     VRH_HIP(hipEventElapsedTime(&ms, ctx->ev_start[ctx->last_slot], ctx->ev_stop[ctx->last_slot]));
-    unsigned long long c[12];
+    unsigned long long c[COUNTERS_LINES + 3];
     VRH_HIP(hipMemcpy(c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     ctx->last.kernel_ms = ms;
     ctx->last.rays = c[1];
@@ -983,6 +987,9 @@ VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats)
     ctx->last.wave_box_iters = c[9];
     ctx->last.wave_prim_iters = c[10];
     ctx->last.wave_box_uniform_iters = c[11];
+    ctx->last.l1_lines = c[COUNTERS_LINES];
+    ctx->last.vmem_instrs = c[COUNTERS_LINES + 1];
+    ctx->last.l1_segments = c[COUNTERS_LINES + 2];
     *stats = ctx->last;
     if (c[5] & 1ull) { set_error("traversal step guard tripped: corrupt BVH (rays were cut short)"); return VRH_ERR_HIP; }
     return VRH_OK;
@@ -1108,6 +1115,7 @@ VRH_API int vrh_unshard(vrh_ctx* ctx, uint32_t width, uint32_t height, uint32_t 
     u.stride_pid = stride ? stride : 4 * n;
     u.stride_occ = stride ? stride : n;
     u.color = dst->color; u.pid = dst->prim_id; u.occ = dst->occ;
+    u.clip[0] = 0; u.clip[1] = 0; u.clip[2] = width; u.clip[3] = height;
     if (k)
     {
         u.ao = k->kind == VRH_KERNEL_AO ? 1u : 0u;

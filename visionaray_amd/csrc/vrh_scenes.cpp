@@ -158,5 +158,6 @@ extern "C" VRH_API int vrh_make_camera(const float eye[3], const float center[3]
     }
     out->width = width;
     out->height = height;
+    for (int i = 0; i < 4; ++i) out->scissor[i] = 0u;   // whole image
     return VRH_OK;
 }
