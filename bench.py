@@ -27,13 +27,14 @@ ncclRecv on its own stream and un-interleaves them there (vrh_render_sharded).  
 fixed as N grows: scaling "strong".
 
 Rank 0 prints one JSON line (the contract of the task statement) with:
-  * roofline: the unit that binds the traversal kernel is the vector-memory path (L1 / TA / TD;
-    PMC: profiles/r02_pmc/), so `achieved` is the kernel's L1 line traffic -- distinct 128-B lines
-    per wave-level load / store (the coalescer model of the counting variant, vrh_frame_stats
-    l1_lines, cross-checked against rocprofv3 TCP_TOTAL_CACHE_ACCESSES) x 128 B per launch over
-    the hipEvent launch time -- and `peak` the same quantity measured on the access-shape
-    microbenchmark (tools/micro/l1_roof.hip -> profiles/l1_roof.json).  The SURVEY §8d
-    algorithmic HBM bytes are kept as roofline.hbm_algorithmic (informational);
+  * roofline: the unit that binds the traversal kernel is the vector-memory path (L1 / TA / TD:
+    TD busy 94 % of the launch, PMC in profiles/r02_*), so `achieved` is the kernel's vector-L1
+    request rate -- the distinct 16-B pieces its wave-level loads / stores request (the counting
+    variant's model, vrh_frame_stats.l1_requests, which equals rocprofv3's
+    TCP_TOTAL_CACHE_ACCESSES for these shapes) x 16 B per launch over the hipEvent launch time --
+    and `peak` the highest request rate of the kernel's access shape (per-lane dependent 64-B
+    record gathers) on the microbenchmark tools/micro/l1_roof.hip (profiles/l1_roof.json).  The
+    SURVEY §8d algorithmic HBM bytes are kept as roofline.hbm_algorithmic (informational);
   * cpu_baseline: the reference's own SSE4 tiled_sched path (oracle/_ref, built from
     /root/reference by oracle/Makefile) on a bounded sample, with the host's core count and model.
 """
@@ -54,7 +55,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
 TRI_BYTES, SPHERE_BYTES, INDEX_BYTES, NODE_BYTES = 64, 48, 4, 32
 OUT_BYTES_PRIMARY = 24          # RGBA32F + u32 prim_id + f32 t per primary ray
-L1_LINE_BYTES = 128
+L1_REQ_BYTES = 16               # one vector-L1 request (TCP access) = one lane's 16-B piece (tools/l1_roof.py)
 
 
 def parse():
@@ -333,15 +334,22 @@ def main():
         rays_launch = float(acc[rays_key]) / max(float(acc["timed_frames"]), 1.0)
         frame_share = rays_launch / n_rays                      # frames per launch on this rank (N > 1: a shard)
         roof = load_json(os.path.join(ROOT, "profiles", "l1_roof.json"))
-        lines_launch = float(cstats["l1_lines"]) * frame_share
-        achieved = lines_launch * L1_LINE_BYTES / (k_ms_mean * 1e-3) / 1e9
+        reqs_launch = float(cstats["l1_requests"]) * frame_share
+        achieved = reqs_launch * L1_REQ_BYTES / (k_ms_mean * 1e-3) / 1e9
         peak = roof.get("peak_gbs") if roof else None
         hbm_alg = bytes_per_ray * rays_launch / (k_ms_mean * 1e-3) / 1e9
+        # PMC of this exact configuration (tools/r02_session.sh + tools/pmc_bench.py): HBM bytes per
+        # launch (`traffic`), the L1 requests the hardware counted and how busy the TD unit was
         pmc = load_json(os.path.join(ROOT, "profiles", "pmc_traffic.json")) or {}
-        traffic = None
+        traffic, pmc_info = None, None
         if (pmc.get("scene") == args.scene and pmc.get("kernel") == kernel and world == 1
                 and pmc.get("frames_per_launch") == F):
             traffic = pmc.get("hbm_bytes_per_launch")
+            if pmc.get("l1_requests_per_launch"):
+                pmc_info = {"l1_requests_per_launch": pmc["l1_requests_per_launch"],
+                            "model_over_pmc": round(reqs_launch / pmc["l1_requests_per_launch"], 4),
+                            "td_busy_frac": round(pmc["td_busy_frac"], 4),
+                            "source": "profiles/pmc_traffic.json: " + pmc.get("command", "")}
         line = {
             "metric": "Mrays/s (primary + 8-sample AO)" if kernel == "ao" else "Mrays/s (primary)",
             "value": round(mrays, 3),
@@ -365,20 +373,22 @@ def main():
                 "frame_numbers": [first_timed, first_timed + args.steps - 1],
             },
             "roofline": {
-                "bound": "l1", "unit": "GB/s",
+                "bound": "vmem-l1", "unit": "GB/s",
                 "achieved": round(achieved, 1), "peak": peak,
                 "frac": round(achieved / peak, 4) if peak else None,
                 "traffic": traffic,
-                "what": "vector-L1 line traffic (distinct 128-B lines per wave-level load/store x 128 B) of the "
-                        "traversal launch over its hipEvent time; peak = the same on tools/micro/l1_roof.hip's "
-                        "per-lane dependent 64-B gathers (profiles/l1_roof.json)",
+                "what": "vector-L1 requests (TCP accesses: distinct 16-B pieces per wave-level load/store) x 16 B of "
+                        "the traversal launch over its hipEvent time; peak = the request rate of per-lane dependent "
+                        "64-B record gathers on tools/micro/l1_roof.hip (profiles/l1_roof.json)",
                 "kernel": "render_unified_kernel (traversal, frames in flight)" if F > 1 else "render_unified_kernel",
                 "kernel_ms_mean": round(k_ms_mean, 4), "frames_per_launch": F,
                 "kernel_ms_per_frame": round(k_ms_mean / F, 4),
-                "l1_lines_per_launch": round(lines_launch),
-                "l1_lines_per_ray": round(float(cstats["l1_lines"]) / n_rays, 3),
-                "l1_lines_per_vmem_instr": round(float(cstats["l1_lines"]) / max(float(cstats["vmem_instrs"]), 1.0), 3),
+                "l1_requests_per_launch": round(reqs_launch),
+                "l1_requests_per_ray": round(float(cstats["l1_requests"]) / n_rays, 3),
+                "l1_requests_per_vmem_instr": round(float(cstats["l1_requests"]) / max(float(cstats["vmem_instrs"]), 1.0), 3),
+                "l1_lines128_per_vmem_instr": round(float(cstats["l1_lines"]) / max(float(cstats["vmem_instrs"]), 1.0), 3),
                 "roof_source": roof.get("source") if roof else None,
+                "pmc": pmc_info,
                 "hbm_algorithmic": {
                     "bytes_per_ray": round(bytes_per_ray, 1), "box_tests_per_ray": round(n_box / n_rays, 3),
                     "prim_tests_per_ray": round(n_prim / n_rays, 3), "achieved_gbs": round(hbm_alg, 1),

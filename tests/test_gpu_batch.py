@@ -2,8 +2,9 @@
 the same frame rendered alone by vrh_render, for each kernel, traversal schedule and packed shard.
 
 A batch interleaves the frames' tiles in the work queues (vrh.h), so a wave moves from one frame's
-tile to another's; these tests pin that the per-frame cameras and output rows never mix.  Frames
-use distinct cameras (the eye moved along a small orbit), so a swapped camera or row is visible.
+tile to another's; these tests pin that the per-frame cameras, frame numbers (frame f of a launch
+has frame number frame_num + f: its own AO samples) and output rows never mix.  Frames use distinct
+cameras (the eye moved along a small orbit), so a swapped camera or row is visible.
 """
 import os
 import sys
@@ -39,29 +40,29 @@ def kernel_for(dev, kind):
     return va.ao_kernel(dev) if kind == "ao" else va.closest_hit_kernel(dev)
 
 
-def single(ctx, dev, W, rows, basis, kern, shard=None):
+def single(ctx, dev, W, rows, basis, kern, shard=None, frame_num=0):
     rt = va.hip_buffer_rt(ctx, W, rows)
     rt.clear_color_buffer((0, 0, 0, 0))
-    va.render(ctx, dev, rt, basis, kern, shard)
+    va.render(ctx, dev, rt, basis, kern, shard, frame_num=frame_num)
     out = rt.download()
     rt.close()
     return out
 
 
-def check_batch(ctx, name, W, H, kind, n, shard=None):
+def check_batch(ctx, name, W, H, kind, n, shard=None, frame_num=11):
     _, dev = base.device_scene(ctx, name)
     kern = kernel_for(dev, kind)
     bases = frame_cameras(name, W, H, n)
     rows = _capi.VRH_BAND_ROWS * va.shard_bands(H, shard.index, shard.count) if shard is not None and shard.packed else H
     rt = va.hip_buffer_rt(ctx, W, n * rows)
     rt.clear_color_buffer((0, 0, 0, 0))
-    va.render_batch(ctx, dev, rt, bases, kern, shard)
+    va.render_batch(ctx, dev, rt, bases, kern, shard, frame_num=frame_num)
     got = rt.download()
     stats = ctx.last_frame_stats()
     rt.close()
     rays = 0
     for f in range(n):
-        ref = single(ctx, dev, W, rows, bases[f], kern, shard)
+        ref = single(ctx, dev, W, rows, bases[f], kern, shard, frame_num=frame_num + f)
         rays += ctx.last_frame_stats()["rays"]
         sl = slice(f * rows * W, (f + 1) * rows * W)
         for k in ("prim_id", "occ"):
@@ -85,14 +86,16 @@ def test_batch_spheres(ctx, n):
     check_batch(ctx, "sph5000", 256, 144, "primary", n)
 
 
-@pytest.mark.parametrize("sched", [4, 5, 6])
-def test_batch_under_other_schedules(ctx, sched):
-    ctx.set_option("ao_schedule", sched)
+@pytest.mark.parametrize("opts", [{"ao_schedule": 3}, {"ao_schedule": 4}, {"xcd_queues": 2}, {"wide_anyhit": 1}])
+def test_batch_under_other_schedules(ctx, opts):
+    for k, v in opts.items():
+        ctx.set_option(k, v)
     try:
         check_batch(ctx, "hf200", 320, 180, "ao", 3)
         check_batch(ctx, "sph5000", 256, 144, "primary", 2)
     finally:
-        ctx.set_option("ao_schedule", 0)
+        for k in opts:
+            ctx.set_option(k, 0)
 
 
 @pytest.mark.parametrize("count,index,n", [(3, 0, 4), (3, 2, 4), (8, 5, 4), (8, 7, 32)])

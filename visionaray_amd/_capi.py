@@ -73,7 +73,7 @@ class vrh_frame_stats(C.Structure):
                 ("frames", C.c_uint32),
                 ("wave_steps", C.c_uint64), ("busy_lane_steps", C.c_uint64), ("wave_box_iters", C.c_uint64),
                 ("wave_prim_iters", C.c_uint64), ("wave_box_uniform_iters", C.c_uint64),
-                ("l1_lines", C.c_uint64), ("l1_segments", C.c_uint64), ("vmem_instrs", C.c_uint64)]
+                ("l1_lines", C.c_uint64), ("l1_requests", C.c_uint64), ("vmem_instrs", C.c_uint64)]
 
 
 class vrh_scene_info(C.Structure):

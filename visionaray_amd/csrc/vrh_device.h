@@ -227,11 +227,12 @@ struct test_counts
     uint32_t it_box, it_prim;
     uint64_t w_steps, w_busy, w_box, w_prim;
     uint64_t w_uni;           // wave-level descent iterations whose active lanes all fetch one node
-    // vector-L1 coalescer model (counting variant): per wave-level vector-memory instruction of the
-    // traversal (node pair, primitive and normal loads, output stores), the distinct 128-B lines
-    // (`lines`) and 64-B segments (`segs`) its active lanes touch, and the instruction count
+    // vector-L1 model (counting variant): per wave-level vector-memory instruction of the traversal
+    // (node pair, primitive and normal loads, output stores), the distinct 16-B pieces its active
+    // lanes request (`reqs`: what rocprofv3 TCP_TOTAL_CACHE_ACCESSES counts for these shapes,
+    // tools/micro/l1_roof.hip), the distinct 128-B lines (`lines`) and the instruction count
     // (`vmem`); kept by the wave's first active lane, summed over lanes at the end
-    uint64_t lines, segs, vmem;
+    uint64_t reqs, lines, vmem;
 };
 
 // distinct values of `key` over the active lanes (wave-uniform result)
@@ -255,11 +256,11 @@ __device__ __forceinline__ uint32_t distinct_keys(uint64_t key)
 __device__ __forceinline__ void count_vmem(test_counts& c, const void* p, uint32_t times = 1u)
 {
     const uint64_t a = (uint64_t)(uintptr_t)p;
-    const uint32_t l = distinct_keys(a >> 7), g = distinct_keys(a >> 6);
+    const uint32_t l = distinct_keys(a >> 7), q = distinct_keys(a >> 4);
     if (__lane_id() == (uint32_t)__builtin_ctzll(__ballot(true)))
     {
         c.lines += (uint64_t)l * times;
-        c.segs += (uint64_t)g * times;
+        c.reqs += (uint64_t)q * times;
         c.vmem += times;
     }
 }

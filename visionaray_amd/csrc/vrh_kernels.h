@@ -74,7 +74,7 @@ struct render_params
 };
 
 constexpr int COUNTERS_FRAME = 208;     // u64 words reset before every frame
-constexpr int COUNTERS_LINES = 80;      // [80] L1 128-B lines, [81] wave-level vector-memory instructions, [82] 64-B segments (counting variant)
+constexpr int COUNTERS_LINES = 80;      // [80] L1 128-B lines, [81] wave-level vector-memory instructions, [82] 16-B requests (counting variant)
 constexpr int COUNTERS_TOTAL = 208;     // u64 words [208], [209]: totals
 constexpr int COUNTERS_WORDS = 256;
 

@@ -70,7 +70,7 @@ __device__ __forceinline__ void flush_totals(const render_params& P, uint32_t la
                                              uint64_t hits_total, const test_counts& cnt)
 {
     unsigned long long rr = rays_total, hh = hits_total, b = cnt.box, q = cnt.prim, uni_sum = cnt.w_uni;
-    unsigned long long li = cnt.lines, sg = cnt.segs, vm = cnt.vmem;
+    unsigned long long li = cnt.lines, rq = cnt.reqs, vm = cnt.vmem;
     for (int off = 32; off > 0; off >>= 1)
     {
         rr += __shfl_down(rr, off);
@@ -78,7 +78,7 @@ __device__ __forceinline__ void flush_totals(const render_params& P, uint32_t la
         if (COUNT)
         {
             b += __shfl_down(b, off); q += __shfl_down(q, off); uni_sum += __shfl_down(uni_sum, off);
-            li += __shfl_down(li, off); sg += __shfl_down(sg, off); vm += __shfl_down(vm, off);
+            li += __shfl_down(li, off); rq += __shfl_down(rq, off); vm += __shfl_down(vm, off);
         }
     }
     if (__ballot(cnt.aborted) != 0ull && lane == 0) atomicOr(P.counters + 5, 1ull);
@@ -99,7 +99,7 @@ __device__ __forceinline__ void flush_totals(const render_params& P, uint32_t la
             atomicAdd(P.counters + 11, uni_sum);
             atomicAdd(P.counters + COUNTERS_LINES, li);
             atomicAdd(P.counters + COUNTERS_LINES + 1, vm);
-            atomicAdd(P.counters + COUNTERS_LINES + 2, sg);
+            atomicAdd(P.counters + COUNTERS_LINES + 2, rq);
         }
     }
 }

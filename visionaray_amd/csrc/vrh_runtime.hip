@@ -989,7 +989,7 @@ VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats)
     ctx->last.wave_box_uniform_iters = c[11];
     ctx->last.l1_lines = c[COUNTERS_LINES];
     ctx->last.vmem_instrs = c[COUNTERS_LINES + 1];
-    ctx->last.l1_segments = c[COUNTERS_LINES + 2];
+    ctx->last.l1_requests = c[COUNTERS_LINES + 2];
     *stats = ctx->last;
     if (c[5] & 1ull) { set_error("traversal step guard tripped: corrupt BVH (rays were cut short)"); return VRH_ERR_HIP; }
     return VRH_OK;
