@@ -334,8 +334,7 @@ def main():
         rays_launch = float(acc[rays_key]) / max(float(acc["timed_frames"]), 1.0)
         frame_share = rays_launch / n_rays                      # frames per launch on this rank (N > 1: a shard)
         roof = load_json(os.path.join(ROOT, "profiles", "l1_roof.json"))
-        reqs_launch = float(cstats["l1_requests"]) * frame_share
-        achieved = reqs_launch * L1_REQ_BYTES / (k_ms_mean * 1e-3) / 1e9
+        reqs_launch = float(cstats["l1_requests"]) * frame_share     # the counting variant's model
         peak = roof.get("peak_gbs") if roof else None
         hbm_alg = bytes_per_ray * rays_launch / (k_ms_mean * 1e-3) / 1e9
         # PMC of this exact configuration (tools/r02_session.sh + tools/pmc_bench.py): HBM bytes per
@@ -350,6 +349,10 @@ def main():
                             "model_over_pmc": round(reqs_launch / pmc["l1_requests_per_launch"], 4),
                             "td_busy_frac": round(pmc["td_busy_frac"], 4),
                             "source": "profiles/pmc_traffic.json: " + pmc.get("command", "")}
+        # achieved: the hardware-counted L1 requests of this launch shape when a PMC pass of this exact
+        # configuration is committed, else the counting variant's model; over the live hipEvent time
+        reqs_used = pmc_info["l1_requests_per_launch"] if pmc_info else reqs_launch
+        achieved = reqs_used * L1_REQ_BYTES / (k_ms_mean * 1e-3) / 1e9
         line = {
             "metric": "Mrays/s (primary + 8-sample AO)" if kernel == "ao" else "Mrays/s (primary)",
             "value": round(mrays, 3),
@@ -388,6 +391,7 @@ def main():
                 "l1_requests_per_vmem_instr": round(float(cstats["l1_requests"]) / max(float(cstats["vmem_instrs"]), 1.0), 3),
                 "l1_lines128_per_vmem_instr": round(float(cstats["l1_lines"]) / max(float(cstats["vmem_instrs"]), 1.0), 3),
                 "roof_source": roof.get("source") if roof else None,
+                "requests_source": "pmc (TCP_TOTAL_CACHE_ACCESSES of the committed pass)" if pmc_info else "model",
                 "pmc": pmc_info,
                 "hbm_algorithmic": {
                     "bytes_per_ray": round(bytes_per_ray, 1), "box_tests_per_ray": round(n_box / n_rays, 3),

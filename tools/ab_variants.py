@@ -2,7 +2,8 @@
 
     python tools/ab_variants.py [scene] [rounds]
 Each variant is also checked bit-exactly (prim_id / occ / colour hashes) against tests/golden.
-VRH_AB_BATCH = frames per launch (default 8, as bench.py); times are per frame.
+VRH_AB_BATCH = frames per launch (default 20, as the driver's bench command); times are per frame.
+Frame numbers advance with every frame (distinct AO samples); the parity check renders frame 0.
 """
 import json
 import os
@@ -48,42 +49,37 @@ cam, W, H = scenes.scene_camera(scene)
 basis = cam.basis(W, H)
 ao = prims.dtype == va.TRIANGLE_DTYPE and os.environ.get("VRH_AB_KERNEL", "ao") == "ao"
 kern = va.ao_kernel(dev) if ao else va.closest_hit_kernel(dev)
-F = int(os.environ.get("VRH_AB_BATCH", "8"))
+F = int(os.environ.get("VRH_AB_BATCH", "20"))
 rt = va.hip_buffer_rt(ctx, W, H * F)
 say(f"scene {scene} {len(prims)} prims depth {host.max_depth} ao={ao} wide records {dev.info['wide_records']} "
     f"(depth {dev.info['wide_depth']})")
+OPTIONS = ("block_threads", "stack_cap", "ao_schedule", "blocks_per_cu", "waves_per_simd", "exact_minmax", "xcd_queues",
+           "refill_min", "wide_anyhit", "descent_cap", "pop_on_miss", "coop_fetch", "scalar_fetch")
 res = {v["name"]: [] for v in VARIANTS}
+one = va.hip_buffer_rt(ctx, W, H)
+frame = 1
 for rnd in range(rounds):
     for v in VARIANTS:
-        ctx.set_option("block_threads", v.get("block_threads", 0))
-        ctx.set_option("stack_cap", v.get("stack_cap", 0))
-        ctx.set_option("ao_schedule", v.get("ao_schedule", 0))
-        ctx.set_option("blocks_per_cu", v.get("blocks_per_cu", 0))
-        ctx.set_option("waves_per_simd", v.get("waves_per_simd", 0))
-        ctx.set_option("exact_minmax", v.get("exact_minmax", 0))
-        ctx.set_option("xcd_queues", v.get("xcd_queues", 0))
-        ctx.set_option("refill_min", v.get("refill_min", 0))
-        ctx.set_option("wide_anyhit", v.get("wide_anyhit", 0))
-        ctx.set_option("descent_cap", v.get("descent_cap", 0))
-        ctx.set_option("pop_on_miss", v.get("pop_on_miss", 0))
-        ctx.set_option("coop_fetch", v.get("coop_fetch", 0))
-        ctx.set_option("scalar_fetch", v.get("scalar_fetch", 0))
+        for o in OPTIONS:
+            ctx.set_option(o, v.get(o, 0))
         ctx.stats_reset()
-        for _ in range(3):
-            va.render_batch(ctx, dev, rt, [basis] * F, kern)
+        for _ in range(3):                       # distinct frame numbers: every frame its own AO samples
+            va.render_batch(ctx, dev, rt, [basis] * F, kern, frame_num=frame)
+            frame += F
         a = ctx.accum_stats()
         st = ctx.last_frame_stats()
         ms = a["kernel_ms_min"] / F
         res[v["name"]].append((a["kernel_ms_total"] / a["timed_frames"] / F, ms, a["rays"] / a["frames"] / F))
         if rnd == 0 and g is not None:
-            out = {k: x[:W * H] for k, x in rt.download().items()}
+            va.render(ctx, dev, one, basis, kern, frame_num=0)      # the parity frame
+            out = one.download()
             ok = (O.fnv1a(out["prim_id"]) == g["primid_hash"] and O.fnv1a(out["t"]) == g["t_hash"]
                   and (not ao or (O.fnv1a(out["occ"]) == g["occ_hash"] and O.fnv1a(out["color"]) == g["color_hash"])))
             say(f"  {v['name']:24s} grid {st['grid_blocks']} x {st['block_threads']} stack {st['stack_depth']} "
                 f"parity {'OK' if ok else 'MISMATCH'}")
-say(f"{'variant':26s} {'mean ms':>9s} {'min ms':>9s} {'Mrays/s(min)':>13s}")
+say(f"{'variant':26s} {'mean ms':>9s} {'min ms':>9s} {'Mrays/s(min)':>13s} {'Mrays/s(mean)':>14s}")
 for name, vals in res.items():
     mean = float(np.median([x[0] for x in vals]))
     mn = float(np.min([x[1] for x in vals]))
     rays = vals[0][2]
-    say(f"{name:26s} {mean:9.4f} {mn:9.4f} {rays / mn / 1e3:13.1f}")
+    say(f"{name:26s} {mean:9.4f} {mn:9.4f} {rays / mn / 1e3:13.1f} {rays / mean / 1e3:14.1f}")

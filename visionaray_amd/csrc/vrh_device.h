@@ -251,12 +251,32 @@ __device__ __forceinline__ uint32_t distinct_keys(uint64_t key)
     return n;
 }
 
+// distinct values of `key` within each 16-lane quarter of the wave, summed (wave-uniform result):
+// the vector L1 merges the requests of lanes that ask for the same 16-B piece only inside a quarter
+// wave (tools/micro/l1_roof.hip: 64 lanes over 4 pieces of one record = 16 TCP accesses, 4 lanes per
+// piece = 16, one piece per lane = 64)
+__device__ __forceinline__ uint32_t distinct_keys_per_quarter(uint64_t key)
+{
+    uint64_t rem = __ballot(true);
+    uint32_t n = 0;
+    while (rem)
+    {
+        const int first = __builtin_ctzll(rem);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, first);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(key >> 32), first);
+        const uint64_t quarter = 0xFFFFull << (first & 48);
+        rem &= ~(__ballot(key == (((uint64_t)hi << 32) | lo)) & quarter);
+        ++n;
+    }
+    return n;
+}
+
 // one wave-level vector-memory instruction whose lanes access `bytes` (<= 16) at `p`: account for it
-// in the coalescer model (counting variant only; called by the active lanes)
+// in the L1 model (counting variant only; called by the active lanes)
 __device__ __forceinline__ void count_vmem(test_counts& c, const void* p, uint32_t times = 1u)
 {
     const uint64_t a = (uint64_t)(uintptr_t)p;
-    const uint32_t l = distinct_keys(a >> 7), q = distinct_keys(a >> 4);
+    const uint32_t l = distinct_keys(a >> 7), q = distinct_keys_per_quarter(a >> 4);
     if (__lane_id() == (uint32_t)__builtin_ctzll(__ballot(true)))
     {
         c.lines += (uint64_t)l * times;
