@@ -35,14 +35,14 @@ int main(int argc, char** argv)
     try
     {
         // scene + host BVH: build<index_bvh<P>> (build.inl:165-178)
-        std::vector<basic_triangle> tris(size_t(2) * grid * grid);
+        std::vector<basic_triangle<3, float>> tris(size_t(2) * grid * grid);
         hip_detail::check(vrh_gen_heightfield(grid, tris.data()), "vrh_gen_heightfield");
-        auto host_bvh = build<index_bvh<basic_triangle>>(tris.data(), tris.size());
+        auto host_bvh = build<index_bvh<basic_triangle<3, float>>>(tris.data(), tris.size());
         std::vector<vec4> normals(tris.size());
         hip_detail::check(vrh_face_normals(tris.data(), uint32_t(tris.size()), &normals[0].x), "vrh_face_normals");
 
         // device objects: cuda_index_bvh -> hip_index_bvh, gpu_buffer_rt -> hip_buffer_rt, cuda_sched -> hip_sched
-        hip_index_bvh<basic_triangle> device_bvh(host_bvh, normals.data());
+        hip_index_bvh<basic_triangle<3, float>> device_bvh(host_bvh, normals.data());
         hip_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> rt;
         rt.resize(W, H);
 

@@ -37,14 +37,14 @@ int main(int argc, char** argv)
     unsigned shards = argc > 5 ? unsigned(atoi(argv[5])) : 0u;
     try
     {
-        std::vector<basic_triangle> tris(size_t(2) * grid * grid);
+        std::vector<basic_triangle<3, float>> tris(size_t(2) * grid * grid);
         hip_detail::check(vrh_gen_heightfield(grid, tris.data()), "vrh_gen_heightfield");
-        auto host_bvh = build<index_bvh<basic_triangle>>(tris.data(), tris.size());
+        auto host_bvh = build<index_bvh<basic_triangle<3, float>>>(tris.data(), tris.size());
         std::vector<vec4> normals(tris.size());
         hip_detail::check(vrh_face_normals(tris.data(), uint32_t(tris.size()), &normals[0].x), "vrh_face_normals");
 
         hip_render_group group;                     // every visible GPU
-        std::vector<hip_index_bvh<basic_triangle>> replicas;
+        std::vector<hip_index_bvh<basic_triangle<3, float>>> replicas;
         std::vector<hip_builtin_kernel> kernels;
         for (size_t i = 0; i < group.size(); ++i)
             replicas.emplace_back(host_bvh, normals.data(), group.context(i));

@@ -1,4 +1,5 @@
-// visionaray_amd/csrc/vrh_device.h -- device-side data layout and traversal for gfx950.
+// include/visionaray_hip/detail/vrh_device.h -- device-side data layout and traversal for gfx950
+// (libvrh.so's kernels and the user kernels of visionaray_hip/hip_kernels.h share it).
 //
 // HBM layout (built once at vrh_scene_upload from the reference arrays):
 //

@@ -69,6 +69,14 @@ template <typename T> struct is_triangle<T, decltype((void)std::declval<T>().e2)
 template <typename SP, typename = void> struct has_scissor : std::false_type {};
 template <typename SP> struct has_scissor<SP, decltype((void)std::declval<SP>().scissor_box)> : std::true_type {};
 
+// user kernels (callables) are device code: visionaray_hip/hip_kernels.h, compiled by hipcc,
+// specialises this for them; without it hip_sched::frame accepts only the built-in kernels
+template <typename K, typename = void>
+struct user_kernels
+{
+    static constexpr bool available = false;
+};
+
 template <typename SP>
 void set_scissor(SP const& sp, vrh_camera& c)
 {
@@ -183,6 +191,16 @@ private:
 };
 
 //-------------------------------------------------------------------------------------------------
+// hip_bvh_ref: what hip_index_bvh::ref() hands to kernels -- the scene's device arrays
+// (vrh_scene_view); closest_hit / any_hit of visionaray_hip/hip_kernels.h traverse it
+//
+
+struct hip_bvh_ref
+{
+    vrh_scene_view view;
+};
+
+//-------------------------------------------------------------------------------------------------
 // hip_index_bvh<P>: device-resident copy of a host index BVH (the cuda_index_bvh copy-ctor)
 //
 
@@ -250,6 +268,16 @@ public:
 
     vrh_scene* handle() const { return scene_.get(); }
     hip_context& context() const { return *ctx_; }
+
+    // the device BVH a kernel traverses (cuda_index_bvh::ref(), bvh.h:344-350): a plain view of
+    // the device arrays, passed by value into user kernels (visionaray_hip/hip_kernels.h)
+    hip_bvh_ref ref() const
+    {
+        hip_bvh_ref r{};
+        hip_detail::check(vrh_scene_get_view(handle(), 0, &r.view), "vrh_scene_get_view");
+        return r;
+    }
+
     vrh_scene_info info() const
     {
         vrh_scene_info i{};
@@ -641,13 +669,32 @@ public:
 
     // frame(): rt.begin_frame() -> vrh_render -> rt.end_frame() (cuda_sched.inl:306-320; end_frame
     // syncs).  shard: optional image-tile shard (multi-GPU).
+    //
+    // K may also be a user kernel -- a callable R -> result_record (or (R, sampler&), (R, x, y)),
+    // as cuda_sched runs it (cuda_sched.inl:53-99, sched_common.h:78-120) -- when the translation
+    // unit includes visionaray_hip/hip_kernels.h and is compiled by hipcc: it then runs on the GPU
+    // over the pixels of the scissor box with the reference's primary rays.
     template <typename K, typename SP>
     void frame(K kernel, SP sparams, unsigned frame_num = 0, vrh_shard const* shard = nullptr)
     {
-        static_assert(std::is_same<K, hip_builtin_kernel>::value,
-                      "hip_sched runs the built-in kernels (make_hip_closest_hit_kernel / make_hip_ao_kernel / "
-                      "make_hip_simple_kernel / make_hip_multi_hit_kernel): "
-                      "an arbitrary callable cannot cross the C ABI");
+        if constexpr (!std::is_same<K, hip_builtin_kernel>::value)
+        {
+            static_assert(hip_detail::user_kernels<K>::available,
+                          "hip_sched runs the built-in kernels (make_hip_closest_hit_kernel / make_hip_ao_kernel / "
+                          "make_hip_simple_kernel / make_hip_multi_hit_kernel) through the C ABI; a user kernel "
+                          "(a callable) is device code: include visionaray_hip/hip_kernels.h and compile with hipcc");
+            if (shard) throw std::runtime_error("hip_sched::frame: user kernels render the whole image");
+            hip_detail::user_kernels<K>::frame(*ctx_, kernel, sparams, frame_num);
+            return;
+        }
+        else
+            frame_builtin(kernel, sparams, frame_num, shard);
+    }
+
+private:
+    template <typename SP>
+    void frame_builtin(hip_builtin_kernel const& kernel, SP& sparams, unsigned frame_num, vrh_shard const* shard)
+    {
         auto const& cam = sparams.cam;
         auto& rt = sparams.rt;
         float eye[3] = { cam.eye().x, cam.eye().y, cam.eye().z };
@@ -662,6 +709,8 @@ public:
                           "vrh_render");
         rt.end_frame();
     }
+
+public:
 
     // frames in flight (vrh_render_batch): ONE persistent launch renders cams.size() frames of
     // one scene and kernel (up to VRH_MAX_BATCH), camera f into rows [f * H, (f + 1) * H) of rt,

@@ -201,6 +201,9 @@ VRH_API int vrh_device_count(int* count);
 VRH_API int vrh_ctx_create(int hip_device, vrh_ctx** out);
 VRH_API int vrh_ctx_create_on_stream(int hip_device, void* hip_stream, vrh_ctx** out);
 VRH_API int vrh_ctx_destroy(vrh_ctx* ctx);
+/* the context's HIP device and stream (hipStream_t): user kernels (hip_kernels.h) launch on it, so
+ * they are ordered with the context's renders, uploads and downloads */
+VRH_API int vrh_ctx_get_stream(const vrh_ctx* ctx, int* hip_device, void** hip_stream);
 
 /* launch tuning (per context; 0 = automatic).  Results never depend on these. */
 enum vrh_option {
@@ -251,6 +254,26 @@ VRH_API int vrh_scene_upload(vrh_ctx* ctx, const void* nodes, uint32_t num_nodes
                              const uint32_t* indices, uint32_t num_indices,
                              const void* face_normals, vrh_scene** out);
 VRH_API int vrh_scene_get_info(const vrh_scene* scene, vrh_scene_info* info);
+
+/* Device view of BVH `bvh` of a scene (0 for a single BVH; i < num_bvhs for a list) <- the bvh_ref a
+ * device BVH hands to kernels (cuda_index_bvh::ref(), bvh.h:344-350, 443-448).  User kernels compiled
+ * with hipcc (include/visionaray_hip/hip_kernels.h) traverse it with their own intersectors.  The
+ * pointers are device addresses on the scene's context, valid until vrh_scene_free:
+ *   pairs : 64-B child-pair records (vrh_device.h layout), prims : leaf-ordered primitives (48-B
+ *   triangle / 32-B sphere records with END flags), normals : float4 face normal per prim_id or NULL.
+ * root = root link (pair index, or 0x80000000 | first primitive for a one-leaf tree). */
+typedef struct {
+    const void* pairs;
+    const void* prims;
+    const void* normals;
+    uint32_t root;
+    uint32_t max_depth;       /* traversal needs <= max_depth stack entries                     */
+    uint32_t prim_kind;       /* vrh_prim_kind                                                   */
+    uint32_t finite_bounds;   /* every node bound finite (the hardware min/max slab test is exact) */
+    uint32_t num_prims;       /* leaf-ordered primitive records                                  */
+    uint32_t reserved[3];
+} vrh_scene_view;
+VRH_API int vrh_scene_get_view(const vrh_scene* scene, uint32_t bvh, vrh_scene_view* out);
 
 /* A list of BVHs rendered as one scene <- closest_hit / any_hit over [begin, end) of bvh_refs
  * (traverse_linear.inl:76-141, 232-329; the kernels of ao/main.cpp:183 and the viewer pass such a

@@ -266,6 +266,32 @@ struct mask_intersector : basic_intersector<mask_intersector>
     int w = 0, h = 0;
 };
 
+//-------------------------------------------------------------------------------------------------
+// heart: the intersector example's procedural cut-out itself (examples/intersector/main.cpp:251-330:
+// tc -> (x, y) = 3 tc - 1.5, kept where (x^2 + y^2 - 1)^3 - x^2 y^3 < 0), evaluated per lane.  For
+// scalar rays the example's Mask(hits) is bool(bool[1]) -- a pointer, always true -- so the scalar
+// reference would cut nothing out; this restates what its SIMD rays compute, one lane at a time.
+//
+
+struct heart_intersector : basic_intersector<heart_intersector>
+{
+    using basic_intersector<heart_intersector>::operator();
+
+    template <typename R, typename S>
+    auto operator()(R const& ray, basic_triangle<3, S> const& tri) -> decltype( intersect(ray, tri) )
+    {
+        auto hr = intersect(ray, tri);
+        if (!hr.hit) return hr;
+        vec2 tc = get_tex_coord(tex_coords, hr, tri);
+        float x = tc.x * 3.0f - 1.5f;
+        float y = tc.y * 3.0f - 1.5f;
+        hr.hit &= (pow(x * x + y * y - 1.0f, 3.0f) - x * x * y * y * y) < 0.0f;
+        return hr;
+    }
+
+    vec2 const* tex_coords = nullptr;
+};
+
 // the parity AO sampler of SURVEY.md Appendix A, frame n offset by n * 0x9E3779B1 (the build's
 // stand-in for the reference's per-frame reseeding, cuda_sched.inl:38-45, 79; frame 0 = Appendix A):
 // Malley sample s of pixel p
@@ -910,6 +936,28 @@ int main(int argc, char** argv)
         isect.w = mw;
         isect.h = mh;
         return run_golden(d, t, normals, outdir, W, H, true, isect);
+    }
+    if (mode == "heart")
+    {
+        // heart <scene> <outdir> [W H]: primary closest hit with the procedural heart cut-out over
+        // the planar (x, z) tex coords of the mask mode
+        if (argc < 4 || d.spheres) return 2;
+        std::string outdir = argv[3];
+        int W = argc > 5 ? atoi(argv[4]) : d.W;
+        int H = argc > 5 ? atoi(argv[5]) : d.H;
+        aligned_vector<tri_t> t;
+        if (d.grid == 0) make_cornell(t); else if (d.layers) make_hfstack(d.grid, d.layers, t); else make_heightfield(d.grid, t);
+        std::vector<vec3> normals(t.size());
+        for (size_t i = 0; i < t.size(); ++i) normals[i] = normalize(cross(t[i].e1, t[i].e2));
+        std::vector<vec2> tc(3 * t.size());
+        for (auto const& tri : t)
+        {
+            vec3 c[3] = { tri.v1, tri.v1 + tri.e1, tri.v1 + tri.e2 };
+            for (int k = 0; k < 3; ++k) tc[3 * tri.prim_id + k] = vec2(c[k].x * 0.5f + 0.5f, c[k].z * 0.5f + 0.5f);
+        }
+        heart_intersector isect;
+        isect.tex_coords = tc.data();
+        return run_golden(d, t, normals, outdir, W, H, false, isect);
     }
     if (mode == "list")
     {

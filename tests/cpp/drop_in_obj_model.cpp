@@ -62,7 +62,7 @@ int main(int argc, char** argv)
         const unsigned W = 256, H = 160;
         try
         {
-            auto device_bvh = hip_index_bvh<basic_triangle>::gpu_build(mod.primitives, mod.geometric_normals);
+            auto device_bvh = hip_index_bvh<basic_triangle<3, float>>::gpu_build(mod.primitives, mod.geometric_normals);
             device_bvh.set_vertex_normals(mod.shading_normals);
             std::vector<vrh_point_light> lights(1);
             lights[0] = vrh_point_light{ { 0.5f, 2.0f, 1.5f }, { 1.0f, 1.0f, 1.0f }, 1.0f, 1.0f, 0.0f, 0.0f };

@@ -1,0 +1,267 @@
+// tests/cpp/user_kernels.hip -- user kernels and custom intersectors through hip_sched::frame
+// (include/visionaray_hip/hip_kernels.h), compiled by hipcc (visionaray_amd/Makefile `cpp_tests`).
+//
+//   user_kernels ao    <grid> <W> <H> <outdir> [frame]          AO kernel written as a device lambda,
+//                                                               default intersector
+//   user_kernels mask  <grid> <W> <H> <outdir> <mask.bin> <n>   the same kernel with a byte-mask
+//                                                               basic_intersector (the reference
+//                                                               harness's "mask" intersector)
+//   user_kernels heart <grid> <W> <H> <outdir>                  closest hit with the intersector
+//                                                               example's procedural heart cut-out
+//
+// The kernel is the reference harness's AO lambda (oracle/ref_harness.cpp run_golden, after
+// ao/main.cpp:183-246) as a user would port it to cuda_sched: closest_hit over the BVH refs, the
+// face normal, make_orthonormal_basis, 8 samples, any_hit with radius 0.1.  Its colour channels
+// carry the outputs the tests compare bit for bit with the reference's frames: x = prim id bits,
+// y = t, z = occlusion mask bits, w = the AO grey value (bg.w on a miss).  Writes prim_id.bin,
+// t.bin, occ.bin, color.bin (RGBA32F as the reference stores it) into outdir.
+#include <visionaray_hip/hip_kernels.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+using namespace visionaray;
+
+//-------------------------------------------------------------------------------------------------
+// a byte mask over the hit's texture coordinate (nearest texel), as the harness's mask_intersector
+//
+
+struct byte_mask_intersector : basic_intersector<byte_mask_intersector>
+{
+    using basic_intersector<byte_mask_intersector>::operator();
+
+    template <typename R, typename S>
+    __device__ auto operator()(R const& ray, basic_triangle<3, S> const& tri) -> decltype(intersect(ray, tri))
+    {
+        auto hr = intersect(ray, tri);
+        if (!hr.hit) return hr;
+        vec2 tc = get_tex_coord(tex_coords, hr);
+        hr.hit &= mask[texel(tc.y, h) * unsigned(w) + texel(tc.x, w)] != 0;
+        return hr;
+    }
+
+    __device__ static unsigned texel(float c, int n)
+    {
+        float x = (c > 0.0f ? c : 0.0f) * float(n);
+        return x < float(n) ? unsigned(x) : unsigned(n - 1);
+    }
+
+    vec2 const* tex_coords = nullptr;
+    uint8_t const* mask = nullptr;
+    int w = 0, h = 0;
+};
+
+//-------------------------------------------------------------------------------------------------
+// The intersector example's procedural cut-out, written in its width-generic style (the same code
+// serves float, float4 and float8 rays on the CPU): host code without VSNRAY_FUNC becomes device
+// code inside the force_cuda_host_device region.
+//
+
+#pragma clang force_cuda_host_device begin
+struct heart_intersector : basic_intersector<heart_intersector>
+{
+    using basic_intersector<heart_intersector>::operator();
+
+    template <typename R, typename S>
+    auto operator()(R const& ray, basic_triangle<3, S> const& tri) -> decltype(intersect(ray, tri))
+    {
+        using T = typename R::scalar_type;
+        static const int N = simd::num_elements<T>::value;
+        using Mask = simd::mask_type_t<T>;
+
+        assert(tex_coords);
+        auto hr = intersect(ray, tri);
+        if (!any(hr.hit))
+        {
+            return hr;
+        }
+        auto tc = get_tex_coord(tex_coords, hr);
+        auto hrs = unpack(hr);
+        auto tcs = unpack(tc);
+
+        bool keep[N];
+        memset(keep, 0, sizeof(keep));
+        for (int i = 0; i < N; ++i)
+        {
+            if (!hrs[i].hit) continue;
+            auto x = tcs[i].x * 3.0f - 1.5f;
+            auto y = tcs[i].y * 3.0f - 1.5f;
+            keep[i] = (pow(x * x + y * y - 1.0f, 3.0f) - x * x * y * y * y) < 0.0f;
+        }
+        hr.hit &= Mask(keep);
+        return hr;
+    }
+
+    vec2 const* tex_coords;
+};
+#pragma clang force_cuda_host_device end
+
+static void write_file(std::string const& path, const void* p, size_t n)
+{
+    FILE* f = fopen(path.c_str(), "wb");
+    if (!f || fwrite(p, 1, n, f) != n) { fprintf(stderr, "cannot write %s\n", path.c_str()); exit(3); }
+    fclose(f);
+}
+
+template <typename T>
+static T* to_device(std::vector<T> const& v)
+{
+    T* d = nullptr;
+    if (hipMalloc(&d, v.size() * sizeof(T)) != hipSuccess ||
+        hipMemcpy(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
+    {
+        fprintf(stderr, "device copy failed\n");
+        exit(4);
+    }
+    return d;
+}
+
+// primary closest hit + 8 AO samples with intersector `isect` (oracle/ref_harness.cpp run_golden)
+template <typename Isect>
+static auto ao_kernel(hip_bvh_ref ref, vec3 const* normals, Isect isect, unsigned W, unsigned frame_num)
+{
+    return [=] __device__ (ray r, unsigned x, unsigned y) mutable -> result_record<float>
+    {
+        result_record<float> result;
+        const vec4 bg(0.1f, 0.2f, 0.3f, 1.0f);
+        result.color = vec4(__uint_as_float(0xFFFFFFFFu), -1.0f, 0.0f, bg.w);
+        hip_bvh_ref const* begin = &ref;
+        auto hr = closest_hit(r, begin, begin + 1, isect);
+        result.hit = hr.hit;
+        if (!hr.hit) return result;
+        hr.isect_pos = r.ori + r.dir * hr.t;
+        float clr = 1.0f;
+        vec3 n = get_normal(normals, hr);
+        vec3 uu, vv, w = n;
+        make_orthonormal_basis(uu, vv, w);
+        unsigned mask = 0;
+        const unsigned p = y * W + x;
+        for (unsigned smp = 0; smp < 8; ++smp)
+        {
+            vec3 s = hip_ao_sample(p, smp, frame_num);
+            auto dir = normalize(s.x * uu + s.y * vv + s.z * w);
+            ray ao(hr.isect_pos + dir * 1E-3f, dir);
+            auto ar = any_hit(ao, begin, begin + 1, 0.1f, isect);
+            if (ar.hit) { clr = clr - 1.0f / 8; mask |= 1u << smp; }
+        }
+        result.color = vec4(__uint_as_float(unsigned(hr.prim_id)), hr.t, __uint_as_float(mask), clr);
+        return result;
+    };
+}
+
+// primary closest hit only: prim id and t
+template <typename Isect>
+static auto primary_kernel(hip_bvh_ref ref, Isect isect)
+{
+    return [=] __device__ (ray r) mutable -> result_record<float>
+    {
+        result_record<float> result;
+        result.color = vec4(__uint_as_float(0xFFFFFFFFu), -1.0f, 0.0f, 1.0f);
+        auto hr = closest_hit(r, &ref, &ref + 1, isect);
+        if (hr.hit) result.color = vec4(__uint_as_float(unsigned(hr.prim_id)), hr.t, 0.0f, 1.0f);
+        result.hit = hr.hit;
+        return result;
+    };
+}
+
+int main(int argc, char** argv)
+{
+    if (argc < 6) { fprintf(stderr, "usage: user_kernels ao|mask|heart grid W H outdir ...\n"); return 2; }
+    const std::string mode = argv[1];
+    const unsigned grid = unsigned(atoi(argv[2])), W = unsigned(atoi(argv[3])), H = unsigned(atoi(argv[4]));
+    const std::string outdir = argv[5];
+    using tri_t = basic_triangle<3, float>;
+    std::vector<tri_t> tris(size_t(2) * grid * grid);
+    if (vrh_gen_heightfield(grid, tris.data()) != VRH_OK) return 2;
+    auto host_bvh = build<index_bvh<tri_t>>(tris.data(), tris.size());
+    std::vector<vec4> normals(tris.size());
+    if (vrh_face_normals(tris.data(), uint32_t(tris.size()), &normals[0].x) != VRH_OK) return 2;
+    // planar (x, z) texture coordinates of every corner, per prim_id (as the harness's mask mode)
+    std::vector<vec2> tc(3 * tris.size());
+    for (auto const& t : tris)
+    {
+        vec3 c[3] = { t.v1, t.v1 + t.e1, t.v1 + t.e2 };
+        for (int k = 0; k < 3; ++k) tc[3 * t.prim_id + k] = vec2(c[k].x * 0.5f + 0.5f, c[k].z * 0.5f + 0.5f);
+    }
+
+    try
+    {
+        hip_index_bvh<tri_t> device_bvh(host_bvh, normals.data());
+        hip_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> rt;
+        rt.resize(W, H);
+        camera cam;
+        cam.perspective(45.0f * constants::degrees_to_radians<float>(), W / static_cast<float>(H), 0.001f, 1000.0f);
+        cam.look_at(vec3(0.0f, 0.9f, 1.4f), vec3(0.0f, 0.0f, 0.0f), vec3(0.0f, 1.0f, 0.0f));
+        hip_sched<ray> sched;
+        auto sparams = make_sched_params(pixel_sampler::uniform_type{}, cam, rt);
+        hip_bvh_ref ref = checked_ref(device_bvh.ref());
+        vec3 const* dnormals = static_cast<vec3 const*>(ref.view.normals);
+        vec2* dtc = to_device(tc);
+
+        if (mode == "ao")
+        {
+            unsigned frame_num = argc > 6 ? unsigned(strtoul(argv[6], nullptr, 10)) : 0u;
+            sched.frame(ao_kernel(ref, dnormals, default_intersector{}, W, frame_num), sparams, frame_num);
+        }
+        else if (mode == "mask")
+        {
+            if (argc < 8) return 2;
+            const int n = atoi(argv[7]);
+            std::vector<uint8_t> mask(size_t(n) * n);
+            FILE* f = fopen(argv[6], "rb");
+            if (!f || fread(mask.data(), 1, mask.size(), f) != mask.size()) return 3;
+            fclose(f);
+            byte_mask_intersector isect;
+            isect.tex_coords = dtc;
+            isect.mask = to_device(mask);
+            isect.w = n;
+            isect.h = n;
+            sched.frame(ao_kernel(ref, dnormals, isect, W, 0u), sparams);
+        }
+        else if (mode == "heart")
+        {
+            heart_intersector isect;
+            isect.tex_coords = dtc;
+            sched.frame(primary_kernel(ref, isect), sparams);
+        }
+        else
+            return 2;
+
+        const size_t npx = size_t(W) * H;
+        std::vector<float> out(4 * npx);
+        rt.download(out.data());
+        // decode the channels into the reference's four outputs
+        std::vector<uint32_t> pid(npx);
+        std::vector<float> t(npx), color(4 * npx);
+        std::vector<uint8_t> occ(npx);
+        for (size_t p = 0; p < npx; ++p)
+        {
+            uint32_t bits;
+            memcpy(&bits, &out[4 * p], 4);
+            pid[p] = bits;
+            t[p] = out[4 * p + 1];
+            memcpy(&bits, &out[4 * p + 2], 4);
+            occ[p] = uint8_t(bits);
+            const float g = out[4 * p + 3];
+            const bool hit = pid[p] != 0xFFFFFFFFu;
+            const float c[4] = { hit ? g : 0.1f, hit ? g : 0.2f, hit ? g : 0.3f, 1.0f };
+            memcpy(&color[4 * p], c, 16);
+        }
+        write_file(outdir + "/prim_id.bin", pid.data(), npx * 4);
+        write_file(outdir + "/t.bin", t.data(), npx * 4);
+        write_file(outdir + "/occ.bin", occ.data(), npx);
+        write_file(outdir + "/color.bin", color.data(), npx * 16);
+        size_t hits = 0;
+        for (auto p : pid) hits += p != 0xFFFFFFFFu;
+        printf("{\"mode\":\"%s\",\"W\":%u,\"H\":%u,\"hits\":%zu}\n", mode.c_str(), W, H, hits);
+    }
+    catch (std::exception const& e)
+    {
+        fprintf(stderr, "error: %s\n", e.what());
+        return 1;
+    }
+    return 0;
+}

@@ -10,6 +10,7 @@ Run in the build container (needs /root/reference to build the harness):
     python tests/golden/make_golden.py --mask                           (only the mask-intersector cases)
     python tests/golden/make_golden.py --frames                         (only the frame-number cases)
     python tests/golden/make_golden.py --list                           (only the BVH-list + scissor cases)
+    python tests/golden/make_golden.py --heart                          (only the procedural-heart cases)
 
 For every case the reference harness renders a full simple_sched<basic_ray<float>> frame
 (primary closest_hit + the Appendix-A AO kernel for triangle scenes) and this script stores:
@@ -80,6 +81,14 @@ WHITTED_CASES = [
 MASK_CASES = [
     ("mask_hf200_320x180", "hf200", 320, 180, 128),
     ("mask_hf64_160x90", "hf64", 160, 90, 37),
+]
+
+
+# procedural-heart cases (harness "heart" mode): primary closest hit with the intersector example's
+# procedural cut-out over planar (x, z) texture coordinates: name, scene, W, H
+HEART_CASES = [
+    ("heart_hf64_160x90", "hf64", 160, 90),
+    ("heart_hf200_320x180", "hf200", 320, 180),
 ]
 
 
@@ -191,6 +200,19 @@ def mask_cases(out):
             print(case, rec["hits"], rec["ao_occluded"], flush=True)
 
 
+def heart_cases(out):
+    for case, scene, W, H in HEART_CASES:
+        with tempfile.TemporaryDirectory() as d:
+            r = subprocess.run([REF, "heart", scene, d, str(W), str(H)], check=True, capture_output=True, text=True)
+            info = json.loads(r.stdout.strip().splitlines()[-1])
+            pid = np.fromfile(os.path.join(d, "prim_id.bin"), np.uint32)
+            t = np.fromfile(os.path.join(d, "t.bin"), np.float32)
+            rec = {"scene": scene, "W": W, "H": H, "hits": info["hits"], "primid_hash": fnv1a(pid), "t_hash": fnv1a(t)}
+            np.savez_compressed(os.path.join(HERE, case + ".npz"), prim_id=pid, t=t)
+            out[case] = rec
+            print(case, rec["hits"], flush=True)
+
+
 def frame_cases(out, rng):
     for case, scene, W, H, frame, full in FRAME_CASES:
         with tempfile.TemporaryDirectory() as d:
@@ -251,7 +273,8 @@ def sah_cases(out):
 def main():
     if not os.path.exists(REF):
         sys.exit("build the reference harness first: make -C oracle ref")
-    only_shade = any(f in sys.argv for f in ("--shade", "--multi", "--sah", "--whitted", "--mask", "--frames", "--list"))
+    only_shade = any(f in sys.argv for f in ("--shade", "--multi", "--sah", "--whitted", "--mask", "--frames", "--list",
+                                                "--heart"))
     path = os.path.join(HERE, "golden.json")
     out = json.load(open(path)) if only_shade else {}
     rng = np.random.default_rng(12345)
@@ -283,7 +306,9 @@ def main():
                                     occ=occ[pix], color=color[pix])
             out[case] = rec
             print(case, rec["hits"], rec["ao_occluded"], rec["primid_hash"], flush=True)
-    if "--frames" in sys.argv:
+    if "--heart" in sys.argv:
+        heart_cases(out)
+    elif "--frames" in sys.argv:
         frame_cases(out, np.random.default_rng(2468))
     elif "--list" in sys.argv:
         list_cases(out)

@@ -76,6 +76,12 @@ class vrh_frame_stats(C.Structure):
                 ("l1_lines", C.c_uint64), ("l1_requests", C.c_uint64), ("vmem_instrs", C.c_uint64)]
 
 
+class vrh_scene_view(C.Structure):
+    _fields_ = [("pairs", C.c_void_p), ("prims", C.c_void_p), ("normals", C.c_void_p), ("root", C.c_uint32),
+                ("max_depth", C.c_uint32), ("prim_kind", C.c_uint32), ("finite_bounds", C.c_uint32),
+                ("num_prims", C.c_uint32), ("reserved", C.c_uint32 * 3)]
+
+
 class vrh_scene_info(C.Structure):
     _fields_ = [("num_nodes", C.c_uint32), ("num_prims", C.c_uint32), ("num_indices", C.c_uint32),
                 ("prim_kind", C.c_uint32), ("max_depth", C.c_uint32), ("device_bytes", C.c_uint64),
@@ -114,9 +120,11 @@ SIGNATURES = {
     "vrh_ctx_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
     "vrh_ctx_create_on_stream": (C.c_int, [C.c_int, _vp, C.POINTER(_vp)]),
     "vrh_ctx_destroy": (C.c_int, [_vp]),
+    "vrh_ctx_get_stream": (C.c_int, [_vp, C.POINTER(C.c_int), C.POINTER(C.c_void_p)]),
     "vrh_ctx_set_option": (C.c_int, [_vp, _u32, C.c_int64]),
     "vrh_scene_upload": (C.c_int, [_vp, _vp, _u32, _vp, _u32, _u32, _vp, _u32, _vp, C.POINTER(_vp)]),
     "vrh_scene_get_info": (C.c_int, [_vp, C.POINTER(vrh_scene_info)]),
+    "vrh_scene_get_view": (C.c_int, [_vp, C.c_uint32, C.POINTER(vrh_scene_view)]),
     "vrh_scene_list_create": (C.c_int, [_vp, C.POINTER(_vp), _u32, _vp, _u32, C.POINTER(_vp)]),
     "vrh_scene_free": (C.c_int, [_vp]),
     "vrh_scene_set_vertex_normals": (C.c_int, [_vp, _vp, _u32]),

@@ -14,7 +14,7 @@
 //     AO rays share one refilling loop: a lane whose ray terminates takes the next ray of the tile
 //     at once (ballot + mbcnt compaction of the idle lanes), so the wave stays busy until the
 //     tile's ray pool is empty.
-#include "vrh_device.h"
+#include "visionaray_hip/detail/vrh_device.h"
 #include "vrh_kernels.h"
 
 namespace vrh {
@@ -810,7 +810,8 @@ static kernel_fn pick(bool ao, bool count, int occ, int sched)
 
 static kernel_fn select_variant(const launch_config& c)
 {
-    if (c.epi) return c.occ == 8 ? pick_shade<8>(c.count, c.epi) : c.occ == 6 ? pick_shade<6>(c.count, c.epi) : pick_shade<1>(c.count, c.epi);
+    if (c.epi) return c.occ == 8 ? pick_shade<8>(c.count, c.epi) : c.occ == 6 ? pick_shade<6>(c.count, c.epi)
+                    : c.occ == 5 ? pick_shade<5>(c.count, c.epi) : pick_shade<1>(c.count, c.epi);
     return c.kind == dev::KIND_TRI ? pick<dev::KIND_TRI>(c.ao, c.count, c.occ, c.sched)
                                    : pick<dev::KIND_SPHERE>(c.ao, c.count, c.occ, c.sched);
 }

@@ -91,6 +91,14 @@ VRH_API int vrh_ctx_create_on_stream(int hip_device, void* hip_stream, vrh_ctx**
 
 VRH_API int vrh_ctx_create(int hip_device, vrh_ctx** out) { return vrh_ctx_create_on_stream(hip_device, nullptr, out); }
 
+VRH_API int vrh_ctx_get_stream(const vrh_ctx* ctx, int* hip_device, void** hip_stream)
+{
+    VRH_CHECK(ctx, "vrh_ctx_get_stream: null context");
+    if (hip_device) *hip_device = ctx->device;
+    if (hip_stream) *hip_stream = ctx->stream;
+    return VRH_OK;
+}
+
 VRH_API int vrh_ctx_destroy(vrh_ctx* ctx)
 {
     if (!ctx) return VRH_OK;
@@ -344,6 +352,23 @@ VRH_API int vrh_scene_get_info(const vrh_scene* scene, vrh_scene_info* info)
 {
     VRH_CHECK(scene && info, "vrh_scene_get_info: null");
     *info = scene->info;
+    return VRH_OK;
+}
+
+VRH_API int vrh_scene_get_view(const vrh_scene* scene, uint32_t bvh, vrh_scene_view* out)
+{
+    VRH_CHECK(scene && out, "vrh_scene_get_view: null");
+    VRH_CHECK(bvh < scene->num_roots, "vrh_scene_get_view: bvh index out of range");
+    vrh_scene_view v{};
+    v.pairs = scene->pairs;
+    v.prims = scene->prims;
+    v.normals = scene->normals;
+    v.root = scene->roots[bvh];
+    v.max_depth = scene->info.max_depth;
+    v.prim_kind = scene->info.prim_kind;
+    v.finite_bounds = scene->finite_bounds ? 1u : 0u;
+    v.num_prims = scene->info.num_indices;
+    *out = v;
     return VRH_OK;
 }
 

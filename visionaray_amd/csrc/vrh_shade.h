@@ -9,7 +9,7 @@
 // relative tolerance (north star: 1e-5) while hit ids stay bit-exact.
 #pragma once
 
-#include "vrh_device.h"
+#include "visionaray_hip/detail/vrh_device.h"
 
 namespace vrh {
 namespace dev {
