@@ -224,21 +224,22 @@ enum vrh_option {
                                     queue (auto: 1)                                               */
     VRH_OPT_REFILL_MIN = 8,      /* free lanes (1..64) before finished rays are retired and idle
                                     lanes refilled (auto: 32)                                     */
-    VRH_OPT_WIDE_ANYHIT = 10,    /* 4-wide node records for any-hit (AO) rays (step loop): 1 = on
-                                    when the BVH passes the containment check, 2 = off (auto: off,
-                                    measured 6 % slower on hf1M AO than the binary records)      */
+    VRH_OPT_WIDE_ANYHIT = 10,    /* 4-wide node records for any-hit (AO / shadow) rays (step
+                                    loop): 1 = on when the BVH passes the containment check, 2 = off
+                                    (auto: on for the AO kernel, off for the shading kernels)     */
     VRH_OPT_DESCENT_CAP = 11,    /* step loop: inner visits per step before a lane's descent is
                                     resumed in the next step (1..1024; auto: 8 for primary
                                     visibility, unlimited for AO)                                 */
     VRH_OPT_POP_ON_MISS = 12,    /* step loop: a descent that misses both children pops its stack
-                                    and keeps descending in the same step: 1 = on, 2 = off (auto: on
-                                    for primary visibility and shading kernels, off for AO)       */
+                                    and keeps descending in the same step: 1 = on, 2 = off (auto: on) */
     VRH_OPT_COOP_FETCH = 13,     /* step loop: each quad of lanes fetches its four pair records
                                     together (one coalesced 64-B request per record) and transposes
                                     them with DPP: 1 = on, 2 = off (auto: off; 1 needs a build
                                     with -DVRH_COOP=1, else VRH_ERR_UNSUPPORTED)                  */
     VRH_OPT_SCALAR_FETCH = 14,   /* step loop: a pair record every active lane of a wave wants is
                                     fetched once through the scalar cache: 1 = on, 2 = off (auto: on) */
+    VRH_OPT_AO_GATE = 16,        /* AO step loop: a tile's AO rays are handed out only once all its
+                                    primaries have finished: 1 = on, 2 = off (auto: on)            */
     VRH_OPT_PAIR_LAYOUT = 15,    /* scene upload (read by vrh_scene_upload): 1 = node pairs in
                                     depth-first preorder, a pair's child-0 pair next to it in one
                                     128-B line; 2 = the builder's order (auto: 2; 1 measured

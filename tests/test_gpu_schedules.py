@@ -38,11 +38,15 @@ VARIANTS = {
     # the primary-visibility defaults switched off (pop on miss, descent cap 8, item refill 32)
     "no_pop_uncapped": {"pop_on_miss": 2, "descent_cap": 1024, "refill_min": 16},
     "pop_cap10": {"pop_on_miss": 1, "descent_cap": 10},
+    # the AO defaults switched off one by one (ao_gate + 4-wide any-hit + pop on miss)
+    "ao_round1": {"ao_gate": 2, "wide_anyhit": 2, "pop_on_miss": 2},
+    "ao_gate_binary": {"ao_gate": 1, "wide_anyhit": 2},
+    "ao_ungated_wide": {"ao_gate": 2, "wide_anyhit": 1},
     # scenes uploaded with the line-paired record layout (the option is read at upload)
     "pair_layout": {"pair_layout": 1},
 }
 OPTIONS = ("ao_schedule", "refill_min", "wide_anyhit", "exact_minmax", "descent_cap", "xcd_queues",
-           "pop_on_miss", "coop_fetch", "scalar_fetch", "waves_per_simd", "pair_layout")
+           "pop_on_miss", "coop_fetch", "scalar_fetch", "waves_per_simd", "pair_layout", "ao_gate")
 
 
 @pytest.fixture(params=sorted(VARIANTS))

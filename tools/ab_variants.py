@@ -53,7 +53,7 @@ F = int(os.environ.get("VRH_AB_BATCH", "20"))
 rt = va.hip_buffer_rt(ctx, W, H * F)
 say(f"scene {scene} {len(prims)} prims depth {host.max_depth} ao={ao} wide records {dev.info['wide_records']} "
     f"(depth {dev.info['wide_depth']})")
-OPTIONS = ("block_threads", "stack_cap", "ao_schedule", "blocks_per_cu", "waves_per_simd", "exact_minmax", "xcd_queues",
+OPTIONS = ("block_threads", "stack_cap", "ao_schedule", "blocks_per_cu", "waves_per_simd", "exact_minmax", "xcd_queues", "ao_gate",
            "refill_min", "wide_anyhit", "descent_cap", "pop_on_miss", "coop_fetch", "scalar_fetch")
 res = {v["name"]: [] for v in VARIANTS}
 one = va.hip_buffer_rt(ctx, W, H)

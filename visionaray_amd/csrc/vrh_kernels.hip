@@ -508,7 +508,11 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             //    many lanes at once
             uint64_t idle = __ballot(mode == IDLE);
             if ((uint32_t)__popcll(idle) < P.refill_min && idle != ~0ull) idle = 0ull;
-            if (idle && issC < pubC * S)
+            // ao_gate: a tile's AO rays wait until all its primaries have finished, so the waves'
+            // steps are mostly all-primary or all-AO (binary closest-hit and 4-wide any-hit descents
+            // then rarely share a step); +1 % alone, +6 % (hf1M) / +10 % (hf10M) with the 4-wide
+            // any-hit records (profiles/r02_ab/ab4_c4opts.log)
+            if (idle && issC < pubC * S && (!P.ao_gate || (pendC == 0u && handedC >= 64u)))
             {
                 const uint32_t avail = pubC * S;
                 const uint32_t cand = issC + lane_rank(idle);

@@ -133,6 +133,7 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
             return VRH_ERR_UNSUPPORTED;
         }
         ctx->opt_coop = int(value); break;
+    case VRH_OPT_AO_GATE: VRH_CHECK(value <= 2, "vrh_ctx_set_option: AO gate is 1 (on) or 2 (off)"); ctx->opt_gate = int(value); break;
     case VRH_OPT_POP_ON_MISS: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pop on miss is 1 (on) or 2 (off)"); ctx->opt_pop = int(value); break;
     case VRH_OPT_PAIR_LAYOUT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pair layout is 1 (line pairing) or 2 (builder order)"); ctx->opt_layout = int(value); break;
     case VRH_OPT_SCALAR_FETCH: VRH_CHECK(value <= 2, "vrh_ctx_set_option: scalar fetch is 1 (on) or 2 (off)"); ctx->opt_scalar = int(value); break;
@@ -898,12 +899,19 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     p.refill_min_primary = ctx->opt_refill ? uint32_t(ctx->opt_refill) : 1u;
     p.descent_cap = ctx->opt_dcap ? uint32_t(ctx->opt_dcap) : primary_step ? 8u : 0xFFFFFFFFu;
     // shading epilogues (simple / multi_hit / whitted) pop on a miss too: +4-7 % (profiles/r01_shade/)
-    const bool pop = ctx->opt_pop == 1 || (ctx->opt_pop == 0 && (primary_step || lc.epi != 0));
+    // AO (step loop): the tile's AO rays wait for its primaries (ao_gate), any-hit rays descend the
+    // 4-wide records and primaries pop on a miss -- together +6 % on hf1M and +10 % on hf10M
+    // (profiles/r02_ab/ab4_c4opts.log); each alone is within +-2 %
+    const bool ao_step = lc.ao && lc.sched != 1;
+    p.ao_gate = (ctx->opt_gate == 1 || (ctx->opt_gate == 0 && ao_step)) ? 1u : 0u;
+    const bool pop = ctx->opt_pop == 1 || (ctx->opt_pop == 0 && (primary_step || lc.epi != 0 || ao_step));
     p.step_flags = (pop ? 1u : 0u) | (ctx->opt_scalar == 2 ? 0u : 2u);
     p.stack_cap = cap;
     p.fast_ok = (sc->finite_bounds && !ctx->opt_exact_minmax) ? 1u : 0u;
     p.quads = sc->quads;
-    p.quad_ok = (sc->quads && p.fast_ok && ctx->opt_wide == 1) ? 1u : 0u;   // auto: off (measured slower)
+    // 4-wide any-hit records: auto on for the AO step loop (with ao_gate), off elsewhere
+    const bool wide = ctx->opt_wide == 1 || (ctx->opt_wide == 0 && ao_step);
+    p.quad_ok = (sc->quads && p.fast_ok && wide) ? 1u : 0u;
     // cooperative pair fetch (step loop, binary records; the 4-wide any-hit records keep the
     // per-lane fetch, so it is off whenever they are on)
     p.coop = (ctx->opt_coop == 1 && !p.quad_ok) ? 1u : 0u;
