@@ -28,13 +28,12 @@ fixed as N grows: scaling "strong".
 
 Rank 0 prints one JSON line (the contract of the task statement) with:
   * roofline: the unit that binds the traversal kernel is the vector-memory path (L1 / TA / TD:
-    TD busy 94 % of the launch, PMC in profiles/r02_*), so `achieved` is the kernel's vector-L1
-    request rate -- the distinct 16-B pieces its wave-level loads / stores request (the counting
-    variant's model, vrh_frame_stats.l1_requests, which equals rocprofv3's
-    TCP_TOTAL_CACHE_ACCESSES for these shapes) x 16 B per launch over the hipEvent launch time --
-    and `peak` the highest request rate of the kernel's access shape (per-lane dependent 64-B
-    record gathers) on the microbenchmark tools/micro/l1_roof.hip (profiles/l1_roof.json).  The
-    SURVEY §8d algorithmic HBM bytes are kept as roofline.hbm_algorithmic (informational);
+    TD busy 94-97 % of the launch, PMC in profiles/r02_*), so `achieved` is the kernel's vector-L1
+    request rate -- rocprofv3's TCP_TOTAL_CACHE_ACCESSES of the committed PMC pass of this exact
+    command (profiles/pmc_traffic.json) x 16 B per launch over the live hipEvent launch time -- and
+    `peak` the highest request rate of the kernel's access shape (per-lane dependent 64-B record
+    gathers) on the microbenchmark tools/micro/l1_roof.hip (profiles/l1_roof.json).  The SURVEY
+    §8d algorithmic HBM bytes are kept as roofline.hbm_algorithmic (informational);
   * cpu_baseline: the reference's own SSE4 tiled_sched path (oracle/_ref, built from
     /root/reference by oracle/Makefile) on a bounded sample, with the host's core count and model.
 """
@@ -334,7 +333,7 @@ def main():
         rays_launch = float(acc[rays_key]) / max(float(acc["timed_frames"]), 1.0)
         frame_share = rays_launch / n_rays                      # frames per launch on this rank (N > 1: a shard)
         roof = load_json(os.path.join(ROOT, "profiles", "l1_roof.json"))
-        reqs_launch = float(cstats["l1_requests"]) * frame_share     # the counting variant's model
+        pieces_launch = float(cstats["l1_requests"]) * frame_share    # counting variant: distinct 16-B pieces
         peak = roof.get("peak_gbs") if roof else None
         hbm_alg = bytes_per_ray * rays_launch / (k_ms_mean * 1e-3) / 1e9
         # PMC of this exact configuration (tools/r02_session.sh + tools/pmc_bench.py): HBM bytes per
@@ -346,13 +345,11 @@ def main():
             traffic = pmc.get("hbm_bytes_per_launch")
             if pmc.get("l1_requests_per_launch"):
                 pmc_info = {"l1_requests_per_launch": pmc["l1_requests_per_launch"],
-                            "model_over_pmc": round(reqs_launch / pmc["l1_requests_per_launch"], 4),
                             "td_busy_frac": round(pmc["td_busy_frac"], 4),
                             "source": "profiles/pmc_traffic.json: " + pmc.get("command", "")}
-        # achieved: the hardware-counted L1 requests of this launch shape when a PMC pass of this exact
-        # configuration is committed, else the counting variant's model; over the live hipEvent time
-        reqs_used = pmc_info["l1_requests_per_launch"] if pmc_info else reqs_launch
-        achieved = reqs_used * L1_REQ_BYTES / (k_ms_mean * 1e-3) / 1e9
+        # achieved: the hardware-counted L1 requests (TCP_TOTAL_CACHE_ACCESSES) of a committed PMC pass
+        # of this exact configuration, over the live hipEvent time; without one it is not reported
+        achieved = (pmc_info["l1_requests_per_launch"] * L1_REQ_BYTES / (k_ms_mean * 1e-3) / 1e9) if pmc_info else None
         line = {
             "metric": "Mrays/s (primary + 8-sample AO)" if kernel == "ao" else "Mrays/s (primary)",
             "value": round(mrays, 3),
@@ -377,8 +374,8 @@ def main():
             },
             "roofline": {
                 "bound": "vmem-l1", "unit": "GB/s",
-                "achieved": round(achieved, 1), "peak": peak,
-                "frac": round(achieved / peak, 4) if peak else None,
+                "achieved": round(achieved, 1) if achieved else None, "peak": peak,
+                "frac": round(achieved / peak, 4) if (peak and achieved) else None,
                 "traffic": traffic,
                 "what": "vector-L1 requests (TCP accesses: distinct 16-B pieces per wave-level load/store) x 16 B of "
                         "the traversal launch over its hipEvent time; peak = the request rate of per-lane dependent "
@@ -386,13 +383,16 @@ def main():
                 "kernel": "render_unified_kernel (traversal, frames in flight)" if F > 1 else "render_unified_kernel",
                 "kernel_ms_mean": round(k_ms_mean, 4), "frames_per_launch": F,
                 "kernel_ms_per_frame": round(k_ms_mean / F, 4),
-                "l1_requests_per_launch": round(reqs_launch),
-                "l1_requests_per_ray": round(float(cstats["l1_requests"]) / n_rays, 3),
-                "l1_requests_per_vmem_instr": round(float(cstats["l1_requests"]) / max(float(cstats["vmem_instrs"]), 1.0), 3),
-                "l1_lines128_per_vmem_instr": round(float(cstats["l1_lines"]) / max(float(cstats["vmem_instrs"]), 1.0), 3),
                 "roof_source": roof.get("source") if roof else None,
-                "requests_source": "pmc (TCP_TOTAL_CACHE_ACCESSES of the committed pass)" if pmc_info else "model",
+                "requests_source": ("pmc (TCP_TOTAL_CACHE_ACCESSES of the committed pass)" if pmc_info
+                                    else "no PMC pass of this configuration committed: achieved / frac not reported"),
                 "pmc": pmc_info,
+                # the counting variant's access-shape statistics of one frame (diagnostic; they count
+                # distinct 16-B pieces and 128-B lines per wave-level access, not TCP accesses)
+                "counted": {"distinct_16B_pieces_per_launch": round(pieces_launch),
+                            "distinct_16B_pieces_per_ray": round(float(cstats["l1_requests"]) / n_rays, 3),
+                            "vmem_instrs_per_ray": round(float(cstats["vmem_instrs"]) / n_rays, 3),
+                            "lines128_per_vmem_instr": round(float(cstats["l1_lines"]) / max(float(cstats["vmem_instrs"]), 1.0), 3)},
                 "hbm_algorithmic": {
                     "bytes_per_ray": round(bytes_per_ray, 1), "box_tests_per_ray": round(n_box / n_rays, 3),
                     "prim_tests_per_ray": round(n_prim / n_rays, 3), "achieved_gbs": round(hbm_alg, 1),

@@ -228,11 +228,11 @@ struct test_counts
     uint32_t it_box, it_prim;
     uint64_t w_steps, w_busy, w_box, w_prim;
     uint64_t w_uni;           // wave-level descent iterations whose active lanes all fetch one node
-    // vector-L1 model (counting variant): per wave-level vector-memory instruction of the traversal
+    // access shape (counting variant): per wave-level vector-memory instruction of the traversal
     // (node pair, primitive and normal loads, output stores), the distinct 16-B pieces its active
-    // lanes request (`reqs`: what rocprofv3 TCP_TOTAL_CACHE_ACCESSES counts for these shapes,
-    // tools/micro/l1_roof.hip), the distinct 128-B lines (`lines`) and the instruction count
-    // (`vmem`); kept by the wave's first active lane, summed over lanes at the end
+    // lanes request (`reqs`, merged within a 16-lane quarter), the distinct 128-B lines (`lines`) and
+    // the instruction count (`vmem`); kept by the wave's first active lane, summed over lanes at the
+    // end.  A divergence diagnostic -- the hardware's TCP access count is measured by PMC instead.
     uint64_t reqs, lines, vmem;
 };
 

@@ -163,12 +163,12 @@ typedef struct {
      * loops (lane-level: box_tests / 2 and prim_tests)                                          */
     uint64_t wave_steps, busy_lane_steps, wave_box_iters, wave_prim_iters;
     uint64_t wave_box_uniform_iters;  /* of wave_box_iters: those whose active lanes all fetch ONE node */
-    /* vector-L1 model (only with VRH_KERNEL_COUNT_TESTS): over every wave-level vector-memory
+    /* access shape (only with VRH_KERNEL_COUNT_TESTS): over every wave-level vector-memory
      * instruction of the traversal (node pair, primitive and normal loads, output stores), the
-     * distinct 128-B lines and the distinct 16-B pieces its active lanes touch -- l1_requests is
-     * what rocprofv3's TCP_TOTAL_CACHE_ACCESSES counts for these shapes (tools/micro/l1_roof.hip)
-     * -- and the number of such instructions: the per-launch work of the L1 / TA / TD path that
-     * bounds the kernel */
+     * distinct 128-B lines and the distinct 16-B pieces (merged within a 16-lane quarter) its
+     * active lanes touch, and the number of such instructions.  A diagnostic of the lanes'
+     * divergence; rocprofv3's TCP_TOTAL_CACHE_ACCESSES counts the hardware's own requests (about
+     * 2.2x l1_requests on the AO kernel, profiles/pmc_traffic.json) */
     uint64_t l1_lines, l1_requests, vmem_instrs;
 } vrh_frame_stats;
 

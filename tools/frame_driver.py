@@ -18,7 +18,7 @@ prims = scenes.primitives(scene)
 host = va.build_index_bvh(prims)
 ctx = va.Context(0)
 for opt in ("waves_per_simd", "block_threads", "exact_minmax", "xcd_queues", "ao_schedule", "wide_anyhit",
-            "refill_min", "descent_cap"):
+            "refill_min", "descent_cap", "ao_gate", "pop_on_miss"):
     v = os.environ.get("VRH_" + opt.upper())
     if v is not None:
         ctx.set_option(opt, int(v))
