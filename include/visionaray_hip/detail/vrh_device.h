@@ -202,20 +202,44 @@ __device__ __forceinline__ bool isect_sphere(const ray_t& r, float4 a, float& t)
     return valid;
 }
 
-// Per-lane LDS stack, column-major ([entry][lane]) so a wave's pushes/pops hit 64 distinct banks.
+// Per-lane stack, column-major ([entry][lane]) so a wave's pushes/pops hit 64 distinct LDS banks.
 // The top is kept as a word offset advanced by the block stride (no multiply per push/pop).
-struct lds_stack
+// SPILL = true: only the first (end - base) / stride entries live in LDS; deeper entries continue,
+// in the same column layout, in a global overflow block of the launch (`spill`), so a BVH deeper
+// than the LDS part is still exact -- used where LDS, not registers, would limit the waves per CU
+// (vrh_render; the check costs 2-4 % where it is not needed, so SPILL = false has none).
+template <bool SPILL>
+struct stack_t
 {
     uint32_t* mem;        // dynamic LDS base
     uint32_t base;        // this lane's column (word offset of entry 0)
     uint32_t top;         // word offset of the next free entry
     uint32_t stride;      // words between entries = threads per block
-    uint32_t end;         // base + capacity * stride
+    uint32_t end;         // base + LDS entries * stride
+    uint32_t lim;         // base + total entries * stride (LDS + overflow; = end without SPILL)
+    uint32_t* spill;      // SPILL: this block's overflow block (entry top >= end at spill[top - end + base])
     __device__ __forceinline__ void reset() { top = base; }
-    __device__ __forceinline__ void push(uint32_t v) { mem[top] = v; top += stride; }
-    __device__ __forceinline__ uint32_t pop() { top -= stride; return mem[top]; }
+    __device__ __forceinline__ void push(uint32_t v)
+    {
+        if constexpr (SPILL)
+        {
+            if (__builtin_expect(top < end, 1)) mem[top] = v;
+            else spill[top - end + base] = v;
+        }
+        else
+            mem[top] = v;
+        top += stride;
+    }
+    __device__ __forceinline__ uint32_t pop()
+    {
+        top -= stride;
+        if constexpr (SPILL)
+            if (__builtin_expect(top >= end, 0)) return spill[top - end + base];
+        return mem[top];
+    }
     __device__ __forceinline__ bool empty() const { return top == base; }
 };
+using lds_stack = stack_t<false>;
 
 // Test counts of the counting variant (VRH_KERNEL_COUNT_TESTS).  box / prim are per lane; the
 // step fields measure SIMD utilisation: `it_box` / `it_prim` are this lane's descent / leaf loop
@@ -395,10 +419,10 @@ __device__ __forceinline__ bool leaf_loop(const float4* __restrict__ prims, uint
 // records instead: the same set of leaves is reached (vrh_quad.cpp), the order does not matter
 // for an any-hit result, and the nearest hit entry is descended first.  If a record's hits could
 // overflow the stack, the ray restarts on the binary records from `root` (still exact).
-template <int KIND, bool COUNT, bool FAST, bool UV = false, class MultiList = void>
+template <int KIND, bool COUNT, bool FAST, bool UV = false, class MultiList = void, class Stack>
 __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const float4* __restrict__ prims,
                                         const float4* __restrict__ quads, uint32_t root, bool& quad,
-                                        const ray_t& r, float max_t, bool any, lds_stack& st,
+                                        const ray_t& r, float max_t, bool any, Stack& st,
                                         float& best_t, uint32_t& best_prim, test_counts& cnt,
                                         uint32_t& steps, uint32_t step_limit, uint32_t& resume, uint32_t cap,
                                         uint32_t flags, hit_extra* hx = nullptr, const MultiList* mh = nullptr,
@@ -437,7 +461,7 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
             const bool h3 = quad_entry(xl.w, yl.w, zl.w, xh.w, yh.w, zh.w, r, max_t, d3) & (k3 != QUAD_NONE);
             if (COUNT) cnt.box += 4;
             if (!(h0 | h1 | h2 | h3)) return st.empty() ? -1 : 0;
-            if (st.top + 3u * st.stride > st.end)
+            if (st.top + 3u * st.stride > st.lim)
             {
                 st.reset();
                 st.push(root);
@@ -555,9 +579,9 @@ __device__ __forceinline__ void quad_transpose(float& a0, float& a1, float& a2, 
 // ray_step with the cooperative pair fetch.  Called by EVERY lane of the wave (the quad exchanges
 // need all four lanes), `active` = the lane has a ray.  Per lane the sequence of box tests, stack
 // operations and leaf tests -- and the return value -- is exactly ray_step's (non-quad records).
-template <int KIND, bool COUNT, bool FAST, bool UV = false, class MultiList = void>
+template <int KIND, bool COUNT, bool FAST, bool UV = false, class MultiList = void, class Stack>
 __device__ __forceinline__ int ray_step_coop(bool active, const float4* __restrict__ pairs, const float4* __restrict__ prims,
-                                             uint32_t root, const ray_t& r, float max_t, bool any, lds_stack& st,
+                                             uint32_t root, const ray_t& r, float max_t, bool any, Stack& st,
                                              float& best_t, uint32_t& best_prim, test_counts& cnt,
                                              uint32_t& steps, uint32_t step_limit, uint32_t& resume, uint32_t cap,
                                              uint32_t flags, hit_extra* hx = nullptr, const MultiList* mh = nullptr,

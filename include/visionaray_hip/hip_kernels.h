@@ -267,6 +267,8 @@ __device__ inline vrh::dev::lds_stack user_stack()
     st.stride = nthreads;
     st.top = tid;
     st.end = tid + VRH_USER_STACK * nthreads;
+    st.lim = st.end;
+    st.spill = nullptr;          // checked_ref: the BVH fits the LDS stack
     return st;
 }
 

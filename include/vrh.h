@@ -208,8 +208,13 @@ VRH_API int vrh_ctx_get_stream(const vrh_ctx* ctx, int* hip_device, void** hip_s
 /* launch tuning (per context; 0 = automatic).  Results never depend on these. */
 enum vrh_option {
     VRH_OPT_BLOCK_THREADS = 1,   /* threads per block, multiple of 64 (auto: 64)                  */
-    VRH_OPT_STACK_CAP = 2,       /* LDS stack entries per lane, >= BVH depth (auto: depth rounded
-                                    up to a multiple of 4)                                        */
+    VRH_OPT_STACK_CAP = 2,       /* traversal stack entries per lane kept in LDS; entries beyond
+                                    them (up to the BVH depth) go to a global overflow block, so
+                                    any value is exact.  Primary / AO step loops at their default
+                                    register budgets only; other kernels keep the whole stack in
+                                    LDS (auto: the depth rounded up to a multiple of 4, lowered in
+                                    steps of 4 while LDS rather than registers limits the waves
+                                    per CU, and to at most 20 when the BVH is deeper than that) */
     VRH_OPT_AO_SCHEDULE = 3,     /* refilling loop of a wave: 3 = one descend-to-leaf step per
                                     iteration, 4 = one traversal item (node pair or primitive)
                                     per lane and iteration (primary visibility; AO always runs 3)

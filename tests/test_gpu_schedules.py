@@ -42,11 +42,15 @@ VARIANTS = {
     "ao_round1": {"ao_gate": 2, "wide_anyhit": 2, "pop_on_miss": 2},
     "ao_gate_binary": {"ao_gate": 1, "wide_anyhit": 2},
     "ao_ungated_wide": {"ao_gate": 2, "wide_anyhit": 1},
+    # the traversal stack mostly in the global overflow block (4 / 8 LDS entries per lane)
+    "stack_lds4": {"stack_cap": 4},
+    "stack_lds8_binary": {"stack_cap": 8, "wide_anyhit": 2},
     # scenes uploaded with the line-paired record layout (the option is read at upload)
     "pair_layout": {"pair_layout": 1},
 }
 OPTIONS = ("ao_schedule", "refill_min", "wide_anyhit", "exact_minmax", "descent_cap", "xcd_queues",
-           "pop_on_miss", "coop_fetch", "scalar_fetch", "waves_per_simd", "pair_layout", "ao_gate")
+           "pop_on_miss", "coop_fetch", "scalar_fetch", "waves_per_simd", "pair_layout", "ao_gate",
+           "stack_cap")
 
 
 @pytest.fixture(params=sorted(VARIANTS))
@@ -79,7 +83,7 @@ def test_edge_cases(vctx, oracle_mod):
 
 
 def test_deep_comb(vctx, oracle_mod):
-    base.test_deep_trees_wide_stack_and_rejection(vctx, oracle_mod, 90)
+    base.test_deep_trees_overflow_stack_and_rejection(vctx, oracle_mod, 90)
 
 
 def test_packed_shards(vctx):

@@ -26,7 +26,9 @@ struct render_params
     uint32_t roots[MAX_LIST]; // scene list (launch_config::sched 2): root link of each BVH
     uint32_t num_roots;
     uint32_t step_limit;      // per-ray traversal step bound (nodes + primitives)
-    uint32_t stack_cap;       // LDS stack entries per lane (>= BVH depth)
+    uint32_t stack_cap;       // LDS stack entries per lane
+    uint32_t stack_total;     // stack entries per lane in all (>= BVH depth): LDS + global overflow
+    uint32_t* stack_spill;    // overflow entries, (stack_total - stack_cap) x threads per block, per block
     uint32_t fast_ok;         // node bounds all finite: hardware min/max slab path allowed
     const float4* quads;      // 8 float4 per 4-wide any-hit record (vrh_quad.cpp)
     uint32_t quad_ok;         // any-hit rays with finite origin / inverse direction use `quads`
@@ -92,11 +94,13 @@ struct launch_config
                        // 3: step loop, frames in flight (render_unified_kernel<..., BATCH>: same code)
     int epi;           // primary epilogue: 0 plain, 1 VRH_KERNEL_SIMPLE, 2 VRH_KERNEL_MULTI_HIT, 3 VRH_KERNEL_WHITTED (triangles)
     int max_hits;      // MULTI_HIT: N (LDS hit lists)
+    bool spill;        // the traversal stack continues in a global overflow block (render_unified_kernel<..., SPILL>)
 };
 
 size_t render_lds_bytes(const launch_config& c);
 hipError_t launch_render(const render_params& p, const launch_config& c, int grid, hipStream_t s);
 int render_blocks_per_cu(const launch_config& c);
+bool render_spill_available(const launch_config& c);   // an overflow-stack instance exists for c
 struct unshard_params
 {
     uint32_t width, height, count, rows_per_shard;

@@ -15,6 +15,10 @@
 //     at once (ballot + mbcnt compaction of the idle lanes), so the wave stays busy until the
 //     tile's ray pool is empty.
 #include "visionaray_hip/detail/vrh_device.h"
+
+#include <map>
+#include <mutex>
+#include <tuple>
 #include "vrh_kernels.h"
 
 namespace vrh {
@@ -212,8 +216,9 @@ __device__ __forceinline__ void count_stores(test_counts& cnt, const render_para
 // hit_record.h:54-64: strictly closer only).  Any hit stops at the first BVH with a hit (rc > 0,
 // exit_traversal.h:49-56), so only exhausted BVHs come here.  Returns the new rc: 0 = the next BVH
 // was started, -1 = the list is done (best_t / best_prim hold the merged result).
+template <class Stack>
 __device__ __forceinline__ int list_next(const render_params& P, bool any, uint32_t& bk, float& res_t, uint32_t& res_prim,
-                                         float& best_t, uint32_t& best_prim, lds_stack& st, uint32_t& resume)
+                                         float& best_t, uint32_t& best_prim, Stack& st, uint32_t& resume)
 {
     if (!any && best_t < res_t) { res_t = best_t; res_prim = best_prim; }
     if (bk + 1u < P.num_roots)
@@ -239,7 +244,8 @@ __device__ __forceinline__ int list_next(const render_params& P, bool any, uint3
 // and merged as traverse_linear.inl:76-141 does (list_next); EPI 0 only.
 // BATCH: the same code, instantiated separately for launches of several frames (vrh_render_batch,
 // frames in flight) so that profiles tell them apart from one-frame launches (hip_sched::frame).
-template <int KIND, bool AO, bool COUNT, int OCC, int EPI = 0, bool LIST = false, bool BATCH = false>
+// SPILL: the traversal stack may continue in the global overflow block (stack_t<true>).
+template <int KIND, bool AO, bool COUNT, int OCC, int EPI = 0, bool LIST = false, bool BATCH = false, bool SPILL = false>
 __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params P)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -248,12 +254,14 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     const uint32_t wave = tid >> 6;
     const uint32_t block = blockDim.x;
 
-    lds_stack st;
+    stack_t<SPILL> st;
     st.mem = smem;
     st.base = tid;
     st.stride = block;
     st.top = tid;
     st.end = tid + P.stack_cap * block;
+    st.lim = SPILL ? tid + P.stack_total * block : st.end;
+    st.spill = SPILL ? P.stack_spill + size_t(blockIdx.x) * (P.stack_total - P.stack_cap) * block : nullptr;
     uint32_t* ao_area = smem + P.stack_cap * block + wave * AO_WAVE_WORDS;
     test_counts cnt = {};
     uint64_t rays_total = 0, hits_total = 0;
@@ -652,6 +660,8 @@ __global__ __launch_bounds__(256, OCC) void render_item_kernel(render_params P)
     st.stride = block;
     st.top = tid;
     st.end = tid + P.stack_cap * block;
+    st.lim = st.end;
+    st.spill = nullptr;
     test_counts cnt = {};
     uint64_t rays_total = 0, hits_total = 0;
 
@@ -785,6 +795,12 @@ static kernel_fn pick_occ(bool ao, bool count, int sched)
     if (sched == 3)   // frames in flight (a distinct symbol for profiles), step loop
         return ao ? dev::render_unified_kernel<KIND, true, false, OCC, 0, false, true>
                   : dev::render_unified_kernel<KIND, false, false, OCC, 0, false, true>;
+    if (sched == 4)   // sched 0 / 3 with the stack overflow block (launch_config::spill)
+        return ao ? dev::render_unified_kernel<KIND, true, false, OCC, 0, false, false, true>
+                  : dev::render_unified_kernel<KIND, false, false, OCC, 0, false, false, true>;
+    if (sched == 5)
+        return ao ? dev::render_unified_kernel<KIND, true, false, OCC, 0, false, true, true>
+                  : dev::render_unified_kernel<KIND, false, false, OCC, 0, false, true, true>;
     if (!ao) return count ? dev::render_unified_kernel<KIND, false, true, OCC> : dev::render_unified_kernel<KIND, false, false, OCC>;
     return count ? dev::render_unified_kernel<KIND, true, true, OCC> : dev::render_unified_kernel<KIND, true, false, OCC>;
 }
@@ -812,12 +828,34 @@ static kernel_fn pick(bool ao, bool count, int occ, int sched)
     return pick_occ<KIND, 1>(ao, count, sched);
 }
 
+// the overflow-stack instances exist at the default budgets only: AO 5 waves / SIMD (triangles),
+// primary visibility 6
+template <int KIND>
+static kernel_fn pick_spill(bool ao, int occ, int sched)
+{
+    const int s = sched == 3 ? 5 : 4;
+    if (ao && KIND == dev::KIND_TRI && occ == 5) return pick_occ<KIND, 5>(true, false, s);
+    if (!ao && occ == 6) return pick_occ<KIND, 6>(false, false, s);
+    return nullptr;
+}
+
 static kernel_fn select_variant(const launch_config& c)
 {
     if (c.epi) return c.occ == 8 ? pick_shade<8>(c.count, c.epi) : c.occ == 6 ? pick_shade<6>(c.count, c.epi)
                     : c.occ == 5 ? pick_shade<5>(c.count, c.epi) : pick_shade<1>(c.count, c.epi);
+    if (c.spill)
+        return c.kind == dev::KIND_TRI ? pick_spill<dev::KIND_TRI>(c.ao, c.occ, c.sched)
+                                       : pick_spill<dev::KIND_SPHERE>(c.ao, c.occ, c.sched);
     return c.kind == dev::KIND_TRI ? pick<dev::KIND_TRI>(c.ao, c.count, c.occ, c.sched)
                                    : pick<dev::KIND_SPHERE>(c.ao, c.count, c.occ, c.sched);
+}
+
+bool render_spill_available(const launch_config& c)
+{
+    if (c.epi || c.count || (c.sched != 0 && c.sched != 3)) return false;
+    launch_config s = c;
+    s.spill = true;
+    return select_variant(s) != nullptr;
 }
 
 size_t render_lds_bytes(const launch_config& c)
@@ -835,10 +873,22 @@ hipError_t launch_render(const render_params& p, const launch_config& c, int gri
 
 int render_blocks_per_cu(const launch_config& c)
 {
+    // cached per (variant, block, LDS bytes): vrh_render asks several times per frame
+    static std::mutex mu;
+    static std::map<std::tuple<const void*, int, size_t>, int> cache;
+    const auto key = std::make_tuple(reinterpret_cast<const void*>(select_variant(c)), c.block, render_lds_bytes(c));
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = cache.find(key);
+        if (it != cache.end()) return it->second;
+    }
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, select_variant(c), c.block, render_lds_bytes(c)) != hipSuccess)
         return 1;
-    return n > 0 ? n : 1;
+    n = n > 0 ? n : 1;
+    std::lock_guard<std::mutex> g(mu);
+    cache[key] = n;
+    return n;
 }
 
 hipError_t launch_unshard(const unshard_params& u, hipStream_t s)

@@ -17,6 +17,8 @@ struct vrh_ctx
     int num_cus = 0;
     // device counters (u64), see render_params::counters; [0..7] reset per frame
     unsigned long long* counters = nullptr;
+    void* spill = nullptr;          // traversal stack overflow blocks (vrh_render_batch), grown on demand
+    size_t spill_bytes = 0;
     // one hipEvent pair per frame since vrh_stats_reset (ring of VRH_MAX_TIMED_FRAMES)
     std::vector<hipEvent_t> ev_start, ev_stop;
     uint32_t frames = 0;

@@ -105,6 +105,7 @@ VRH_API int vrh_ctx_destroy(vrh_ctx* ctx)
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->counters) (void)hipFree(ctx->counters);
+    if (ctx->spill) (void)hipFree(ctx->spill);
     for (auto e : ctx->ev_start) (void)hipEventDestroy(e);
     for (auto e : ctx->ev_stop) (void)hipEventDestroy(e);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -850,10 +851,12 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     else VRH_CHECK(rt->height == cam->height * num_frames, "vrh_render: render target height != camera height x frames");
     VRH_CHECK(uint64_t(rt->height) * rt->width < (1ull << 32), "vrh_render: render target too large");
 
-    // a depth-first traversal holds at most `max_depth` stack entries (>= 1 for the root push)
+    // a depth-first traversal holds at most `max_depth` stack entries (>= 1 for the root push):
+    // `total` per lane, of which `cap` in LDS (the rest in a global overflow block, chosen below)
     const uint32_t need = std::max<uint32_t>(sc->info.max_depth, 1u);
-    uint32_t cap = ctx->opt_stack ? uint32_t(ctx->opt_stack) : ((need + 3u) & ~3u);
-    if (cap < need) { set_error("vrh_render: stack capacity option below the BVH depth"); return VRH_ERR_INVALID; }
+    const uint32_t total = std::max((need + 3u) & ~3u, uint32_t(ctx->opt_stack));
+    uint32_t cap = ctx->opt_stack ? uint32_t(ctx->opt_stack) : total;
+    VRH_CHECK(cap >= 1u, "vrh_render: stack capacity option must be >= 1");
     launch_config lc{};
     lc.kind = sc->info.prim_kind == VRH_PRIM_TRI64 ? 0 : 1;
     lc.ao = ao;
@@ -877,6 +880,29 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     // BVH lists run at these defaults
     lc.occ = ctx->opt_occ ? ctx->opt_occ : lc.epi ? 1 : (lc.ao && lc.sched != 1) ? 5 : 6;
     if (list) lc.occ = ao ? 5 : 6;
+    // auto: the LDS part of the stack shrinks (in steps of 4 entries) while LDS, not registers,
+    // limits the waves per CU -- a deep BVH (hf10M: depth 26) then keeps the register-bound
+    // occupancy and its few deepest entries go to the overflow block
+    // (the primary / AO step loops at their default register budgets have overflow-stack instances;
+    // every other kernel keeps its whole stack in LDS, as does an explicit VRH_OPT_STACK_CAP >= depth)
+    if (render_spill_available(lc) && (!ctx->opt_stack || cap < total))
+    {
+        lc.spill = true;
+        if (!ctx->opt_stack)
+        {
+            launch_config lo = lc;
+            lo.stack_cap = 4;
+            const int reg_bound = render_blocks_per_cu(lo);
+            while (lc.stack_cap > 4 && render_blocks_per_cu(lc) < reg_bound) lc.stack_cap -= 4;
+            // measured: hf10M AO 20 LDS entries +7 % over 24 at the same 20 waves / CU
+            // (profiles/r02_ab/ab6_stack.log); no BVH of depth <= 20 spills
+            if (total > 20u) lc.stack_cap = std::min(lc.stack_cap, 20);
+            cap = uint32_t(lc.stack_cap);
+        }
+        if (cap >= total) lc.spill = false;     // nothing overflows: the plain instance
+    }
+    else if (cap < total)
+        lc.stack_cap = int(cap = total);         // no overflow instance: the whole stack in LDS
     if (render_lds_bytes(lc) > 160u * 1024u)
     {
         set_error("vrh_render: BVH depth " + std::to_string(sc->info.max_depth) + " needs more LDS stack than a CU has");
@@ -907,6 +933,7 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     const bool pop = ctx->opt_pop == 1 || (ctx->opt_pop == 0 && (primary_step || lc.epi != 0 || ao_step));
     p.step_flags = (pop ? 1u : 0u) | (ctx->opt_scalar == 2 ? 0u : 2u);
     p.stack_cap = cap;
+    p.stack_total = lc.spill ? total : cap;
     p.fast_ok = (sc->finite_bounds && !ctx->opt_exact_minmax) ? 1u : 0u;
     p.quads = sc->quads;
     // 4-wide any-hit records: auto on for the AO step loop (with ao_gate), off elsewhere
@@ -966,6 +993,23 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     const uint64_t units = uint64_t(num_frames) * p.num_tiles;
     int grid = std::max(1, int(std::min<uint64_t>(uint64_t(ctx->num_cus) * per_cu, (units + waves_per_block - 1) / waves_per_block)));
 
+    // the stack overflow blocks of the persistent grid (grown on demand; the stream is drained
+    // first, so no launch still uses the old block)
+    if (lc.spill)
+    {
+        const size_t bytes = size_t(grid) * (p.stack_total - p.stack_cap) * size_t(lc.block) * sizeof(uint32_t);
+        if (bytes > ctx->spill_bytes)
+        {
+            VRH_HIP(hipStreamSynchronize(ctx->stream));
+            if (ctx->spill) (void)hipFree(ctx->spill);
+            ctx->spill = nullptr;
+            ctx->spill_bytes = 0;
+            VRH_HIP(hipMalloc(&ctx->spill, bytes));
+            ctx->spill_bytes = bytes;
+        }
+        p.stack_spill = static_cast<uint32_t*>(ctx->spill);
+    }
+
     const uint32_t slot = ctx->frames % VRH_MAX_TIMED_FRAMES;
     while (ctx->ev_start.size() <= slot)
     {
@@ -986,7 +1030,7 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     ctx->last.launches = p.num_tiles > 0 ? 1u : 0u;
     ctx->last.grid_blocks = uint32_t(grid);
     ctx->last.block_threads = uint32_t(lc.block);
-    ctx->last.stack_depth = cap;
+    ctx->last.stack_depth = p.stack_total;
     ctx->last.frames = num_frames;
     ctx->have_frame = true;
     return VRH_OK;
