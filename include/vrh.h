@@ -245,6 +245,9 @@ enum vrh_option {
                                     fetched once through the scalar cache: 1 = on, 2 = off (auto: on) */
     VRH_OPT_AO_GATE = 16,        /* AO step loop: a tile's AO rays are handed out only once all its
                                     primaries have finished: 1 = on, 2 = off (auto: on)            */
+    VRH_OPT_WAVE_TIMES = 19,     /* 1: the step-loop kernels record every wave's start / end time
+                                    (wall_clock64) for vrh_get_wave_times -- a launch-timeline
+                                    diagnostic (0 = off, the default)                              */
     VRH_OPT_PAIR_LAYOUT = 15,    /* scene upload (read by vrh_scene_upload): 1 = node pairs in
                                     depth-first preorder, a pair's child-0 pair next to it in one
                                     128-B line; 2 = the builder's order (auto: 2; 1 measured
@@ -338,6 +341,9 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* scene, vrh_rt* rt, c
                              uint32_t frame_num);
 VRH_API int vrh_sync(vrh_ctx* ctx);
 VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats);   /* syncs */
+/* VRH_OPT_WAVE_TIMES: (start, end) clock ticks of every wave of the last launch, 2 * count values
+ * into out (capacity values at most); ticks_per_ms = the constant wall clock's rate; syncs */
+VRH_API int vrh_get_wave_times(vrh_ctx* ctx, uint64_t* out, uint64_t capacity, uint64_t* count, double* ticks_per_ms);
 
 /* accumulation over every render since the last vrh_stats_reset (hipEvents per frame, kept in a
  * ring of VRH_MAX_TIMED_FRAMES; frames beyond that are counted in rays/hits but not timed) */

@@ -50,7 +50,7 @@ VRH_MAX_BATCH = 32
 VRH_OPT_BLOCK_THREADS, VRH_OPT_STACK_CAP, VRH_OPT_AO_SCHEDULE, VRH_OPT_BLOCKS_PER_CU = 1, 2, 3, 4
 VRH_OPT_WAVES_PER_SIMD, VRH_OPT_EXACT_MINMAX, VRH_OPT_XCD_QUEUES, VRH_OPT_REFILL_MIN = 5, 6, 7, 8
 VRH_OPT_WIDE_ANYHIT, VRH_OPT_DESCENT_CAP, VRH_OPT_POP_ON_MISS, VRH_OPT_COOP_FETCH = 10, 11, 12, 13
-VRH_OPT_SCALAR_FETCH, VRH_OPT_PAIR_LAYOUT, VRH_OPT_AO_GATE = 14, 15, 16
+VRH_OPT_SCALAR_FETCH, VRH_OPT_PAIR_LAYOUT, VRH_OPT_AO_GATE, VRH_OPT_WAVE_TIMES = 14, 15, 16, 19
 VRH_MAX_TIMED_FRAMES = 1024
 VRH_MAX_SCENE_LIST = 8
 VRH_GROUP_ID_BYTES = 128
@@ -125,6 +125,7 @@ SIGNATURES = {
     "vrh_scene_upload": (C.c_int, [_vp, _vp, _u32, _vp, _u32, _u32, _vp, _u32, _vp, C.POINTER(_vp)]),
     "vrh_scene_get_info": (C.c_int, [_vp, C.POINTER(vrh_scene_info)]),
     "vrh_scene_get_view": (C.c_int, [_vp, C.c_uint32, C.POINTER(vrh_scene_view)]),
+    "vrh_get_wave_times": (C.c_int, [_vp, _vp, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
     "vrh_scene_list_create": (C.c_int, [_vp, C.POINTER(_vp), _u32, _vp, _u32, C.POINTER(_vp)]),
     "vrh_scene_free": (C.c_int, [_vp]),
     "vrh_scene_set_vertex_normals": (C.c_int, [_vp, _vp, _u32]),

@@ -162,13 +162,26 @@ class Context:
                  "wide_anyhit": capi.VRH_OPT_WIDE_ANYHIT,
                  "descent_cap": capi.VRH_OPT_DESCENT_CAP, "pop_on_miss": capi.VRH_OPT_POP_ON_MISS,
                  "coop_fetch": capi.VRH_OPT_COOP_FETCH, "scalar_fetch": capi.VRH_OPT_SCALAR_FETCH,
-                 "pair_layout": capi.VRH_OPT_PAIR_LAYOUT, "ao_gate": capi.VRH_OPT_AO_GATE}
+                 "pair_layout": capi.VRH_OPT_PAIR_LAYOUT, "ao_gate": capi.VRH_OPT_AO_GATE, "wave_times": capi.VRH_OPT_WAVE_TIMES}
         capi.check("vrh_ctx_set_option", self.handle, names.get(option, option), int(value))
 
     def last_frame_stats(self):
         s = capi.vrh_frame_stats()
         capi.check("vrh_last_frame_stats", self.handle, C.byref(s))
         return {k: getattr(s, k) for k, _ in s._fields_}
+
+    def wave_times(self):
+        """(start, end) of every wave of the last launch in ms from the launch's first start, or
+        None (VRH_OPT_WAVE_TIMES off).  Diagnostic of the launch's ramp-up and tail."""
+        import numpy as np
+        n, rate = C.c_uint64(), C.c_double()
+        capi.check("vrh_get_wave_times", self.handle, None, 0, C.byref(n), C.byref(rate))
+        if n.value == 0:
+            return None
+        buf = np.zeros(2 * n.value, np.uint64)
+        capi.check("vrh_get_wave_times", self.handle, buf.ctypes.data_as(C.c_void_p), buf.size, C.byref(n), None)
+        t = buf.reshape(-1, 2).astype(np.float64)
+        return (t - t[:, 0].min()) / rate.value
 
     def stats_reset(self):
         capi.check("vrh_stats_reset", self.handle)

@@ -64,6 +64,7 @@ struct render_params
     uint32_t refill_min;      // retire / refill once this many lanes are free (AO, item loops)
     uint32_t refill_min_primary;   // the same for the step loop's primary-only stream
     uint32_t ao_gate;         // AO step loop: a tile's AO rays are handed out once its primaries are done
+    unsigned long long* wave_times;   // VRH_OPT_WAVE_TIMES: per wave (start, end) of wall_clock64(), else null
     uint32_t descent_cap;     // step loop: inner visits per step before a descent is resumed later
     uint32_t step_flags;      // step loop: bit 0 a descent that misses both children pops and continues;
                               // bit 1 wave-uniform pair records fetched through the scalar cache

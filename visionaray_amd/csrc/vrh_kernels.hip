@@ -267,6 +267,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     uint64_t rays_total = 0, hits_total = 0;
     const hit_mask_params hml = P.hmask;          // a local copy: &P would spill the kernel arguments
     const hit_mask_params* hm = &hml;             // ray_step tests hm->mask
+    const unsigned long long t_start = P.wave_times ? wall_clock64() : 0ull;
 
     // lane state: the ray it is stepping
     constexpr uint32_t IDLE = 0, PRIMARY = 1, AORAY = 2;
@@ -635,6 +636,12 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         }
     }
 
+    if (P.wave_times && lane == 0)
+    {
+        const size_t w = size_t(blockIdx.x) * (blockDim.x >> 6) + wave;
+        P.wave_times[2 * w] = t_start;
+        P.wave_times[2 * w + 1] = wall_clock64();
+    }
     flush_totals<COUNT>(P, lane, rays_total, hits_total, cnt);
 }
 

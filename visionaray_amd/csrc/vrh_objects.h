@@ -17,6 +17,8 @@ struct vrh_ctx
     int num_cus = 0;
     // device counters (u64), see render_params::counters; [0..7] reset per frame
     unsigned long long* counters = nullptr;
+    unsigned long long* wave_times = nullptr;   // VRH_OPT_WAVE_TIMES buffer (2 per resident wave)
+    size_t wave_times_n = 0, wave_times_used = 0;
     void* spill = nullptr;          // traversal stack overflow blocks (vrh_render_batch), grown on demand
     size_t spill_bytes = 0;
     // one hipEvent pair per frame since vrh_stats_reset (ring of VRH_MAX_TIMED_FRAMES)
@@ -26,7 +28,7 @@ struct vrh_ctx
     vrh_frame_stats last{};
     bool have_frame = false;
     // tuning options (0 = automatic), vrh_ctx_set_option
-    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_dcap = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0, opt_pop = 0, opt_coop = 0, opt_scalar = 0, opt_layout = 0, opt_gate = 0;
+    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_dcap = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0, opt_pop = 0, opt_coop = 0, opt_scalar = 0, opt_layout = 0, opt_gate = 0, opt_wave_times = 0;
 };
 
 struct vrh_scene

@@ -105,6 +105,7 @@ VRH_API int vrh_ctx_destroy(vrh_ctx* ctx)
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->counters) (void)hipFree(ctx->counters);
+    if (ctx->wave_times) (void)hipFree(ctx->wave_times);
     if (ctx->spill) (void)hipFree(ctx->spill);
     for (auto e : ctx->ev_start) (void)hipEventDestroy(e);
     for (auto e : ctx->ev_stop) (void)hipEventDestroy(e);
@@ -134,6 +135,7 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
             return VRH_ERR_UNSUPPORTED;
         }
         ctx->opt_coop = int(value); break;
+    case VRH_OPT_WAVE_TIMES: VRH_CHECK(value <= 1, "vrh_ctx_set_option: wave times is 1 (on) or 0 (off)"); ctx->opt_wave_times = int(value); break;
     case VRH_OPT_AO_GATE: VRH_CHECK(value <= 2, "vrh_ctx_set_option: AO gate is 1 (on) or 2 (off)"); ctx->opt_gate = int(value); break;
     case VRH_OPT_POP_ON_MISS: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pop on miss is 1 (on) or 2 (off)"); ctx->opt_pop = int(value); break;
     case VRH_OPT_PAIR_LAYOUT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pair layout is 1 (line pairing) or 2 (builder order)"); ctx->opt_layout = int(value); break;
@@ -1010,6 +1012,24 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
         p.stack_spill = static_cast<uint32_t*>(ctx->spill);
     }
 
+    // per-wave timeline of this launch (diagnostic, VRH_OPT_WAVE_TIMES)
+    ctx->wave_times_used = 0;
+    if (ctx->opt_wave_times && (lc.sched == 0 || lc.sched == 3))
+    {
+        const size_t n = size_t(grid) * waves_per_block;
+        if (n > ctx->wave_times_n)
+        {
+            VRH_HIP(hipStreamSynchronize(ctx->stream));
+            if (ctx->wave_times) (void)hipFree(ctx->wave_times);
+            ctx->wave_times = nullptr;
+            ctx->wave_times_n = 0;
+            VRH_HIP(hipMalloc(&ctx->wave_times, n * 2 * sizeof(unsigned long long)));
+            ctx->wave_times_n = n;
+        }
+        p.wave_times = ctx->wave_times;
+        ctx->wave_times_used = n;
+    }
+
     const uint32_t slot = ctx->frames % VRH_MAX_TIMED_FRAMES;
     while (ctx->ev_start.size() <= slot)
     {
@@ -1040,6 +1060,24 @@ VRH_API int vrh_sync(vrh_ctx* ctx)
 {
     VRH_CHECK(ctx, "vrh_sync: null");
     VRH_HIP(hipStreamSynchronize(ctx->stream));
+    return VRH_OK;
+}
+
+VRH_API int vrh_get_wave_times(vrh_ctx* ctx, uint64_t* out, uint64_t capacity, uint64_t* count, double* ticks_per_ms)
+{
+    VRH_CHECK(ctx && count, "vrh_get_wave_times: null");
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    VRH_HIP(hipStreamSynchronize(ctx->stream));
+    *count = ctx->wave_times_used;
+    if (ticks_per_ms)
+    {
+        int khz = 0;
+        VRH_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
+        *ticks_per_ms = double(khz);
+    }
+    if (out && ctx->wave_times_used)
+        VRH_HIP(hipMemcpy(out, ctx->wave_times, std::min<uint64_t>(capacity, 2 * ctx->wave_times_used) * 8, hipMemcpyDeviceToHost));
     return VRH_OK;
 }
 
