@@ -30,11 +30,6 @@
 #ifndef VRH_SCALAR_UNIFORM
 #define VRH_SCALAR_UNIFORM 1   // wave-uniform pair fetches through the scalar cache (ray_step)
 #endif
-#ifndef VRH_COOP
-// 1: the cooperative pair fetch (VRH_OPT_COOP_FETCH) is compiled into the kernels.  Off by default:
-// measured slower, and its mere presence costs 0.5-2.5 % (profiles/r01_ab_nocoop.log)
-#define VRH_COOP 0
-#endif
 #ifndef VRH_PACKED_SLABS
 #define VRH_PACKED_SLABS 0   // 1: slab distances with v_pk_add_f32 / v_pk_mul_f32
 #endif
@@ -43,7 +38,6 @@ namespace vrh {
 namespace dev {
 
 constexpr bool SCALAR_UNIFORM = VRH_SCALAR_UNIFORM != 0;
-constexpr bool COOP_FETCH = VRH_COOP != 0;
 constexpr uint32_t LEAF_BIT = 0x80000000u;
 constexpr uint32_t END_BIT = 1u;
 constexpr int KIND_TRI = 0;
@@ -544,137 +538,6 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
     }
     if (leaf_loop<KIND, COUNT, UV, MultiList>(prims, link, r, max_t, any, best_t, best_prim, cnt, hx, mh, hm)) return 1;
     return st.empty() ? -1 : 0;
-}
-
-// ---- cooperative pair fetch ----------------------------------------------------------------
-// The address coalescer takes a quad of consecutive lanes reading one contiguous 64-B record as ONE
-// request, but 64 lanes reading 64 different records as 64 (tools/micro/coop_fetch.hip: 2.4x the
-// record rate on L2-resident data).  So a quad fetches its four lanes' pair records together: in
-// load j lane 4k + m reads quarter m of lane 4k + j's record, then a 4x4 transpose inside the quad
-// (two DPP quad_perm exchange stages) hands every lane the four quarters of its own record.
-
-template <int CTRL>
-__device__ __forceinline__ uint32_t quad_dpp(uint32_t v)
-{
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
-}
-
-// a_j on quad lane m  ->  a_m on quad lane j
-__device__ __forceinline__ void quad_transpose(uint32_t& a0, uint32_t& a1, uint32_t& a2, uint32_t& a3, bool b1, bool b0)
-{
-    uint32_t s, r;
-    s = b1 ? a0 : a2; r = quad_dpp<0x4E>(s); if (b1) a0 = r; else a2 = r;    // quad_perm [2,3,0,1]
-    s = b1 ? a1 : a3; r = quad_dpp<0x4E>(s); if (b1) a1 = r; else a3 = r;
-    s = b0 ? a0 : a1; r = quad_dpp<0xB1>(s); if (b0) a0 = r; else a1 = r;    // quad_perm [1,0,3,2]
-    s = b0 ? a2 : a3; r = quad_dpp<0xB1>(s); if (b0) a2 = r; else a3 = r;
-}
-
-__device__ __forceinline__ void quad_transpose(float& a0, float& a1, float& a2, float& a3, bool b1, bool b0)
-{
-    uint32_t x0 = __float_as_uint(a0), x1 = __float_as_uint(a1), x2 = __float_as_uint(a2), x3 = __float_as_uint(a3);
-    quad_transpose(x0, x1, x2, x3, b1, b0);
-    a0 = __uint_as_float(x0); a1 = __uint_as_float(x1); a2 = __uint_as_float(x2); a3 = __uint_as_float(x3);
-}
-
-// ray_step with the cooperative pair fetch.  Called by EVERY lane of the wave (the quad exchanges
-// need all four lanes), `active` = the lane has a ray.  Per lane the sequence of box tests, stack
-// operations and leaf tests -- and the return value -- is exactly ray_step's (non-quad records).
-template <int KIND, bool COUNT, bool FAST, bool UV = false, class MultiList = void, class Stack>
-__device__ __forceinline__ int ray_step_coop(bool active, const float4* __restrict__ pairs, const float4* __restrict__ prims,
-                                             uint32_t root, const ray_t& r, float max_t, bool any, Stack& st,
-                                             float& best_t, uint32_t& best_prim, test_counts& cnt,
-                                             uint32_t& steps, uint32_t step_limit, uint32_t& resume, uint32_t cap,
-                                             uint32_t flags, hit_extra* hx = nullptr, const MultiList* mh = nullptr,
-                                             const hit_mask_params* hm = nullptr)
-{
-    (void)root;
-    const bool pop_on_miss = (flags & 1u) != 0u;
-    const bool scalar_uniform = SCALAR_UNIFORM && (flags & 2u) != 0u;
-    int rc = 0;
-    bool desc = false;
-    uint32_t link = 0u;
-    if (active)
-    {
-        if (resume != NO_RESUME) { link = resume; resume = NO_RESUME; desc = true; }
-        else if (st.empty()) rc = -1;
-        else if (++steps > step_limit) { cnt.aborted = true; rc = -1; }
-        else { link = st.pop(); desc = true; }
-    }
-    bool at_leaf = desc && (link & LEAF_BIT) != 0u;
-    desc = desc && !at_leaf;
-    const uint32_t lane = __lane_id();
-    const bool b1 = (lane & 2u) != 0u, b0 = (lane & 1u) != 0u;
-    const uint32_t quarter = lane & 3u;
-    uint32_t it = cap;
-    while (__ballot(desc) != 0ull)          // wave-uniform: all lanes run the fetch below
-    {
-        if (desc && it == 0u) { resume = link; desc = false; rc = 0; }
-        it -= desc ? 1u : 0u;
-        const uint64_t dm = __ballot(desc);
-        if (dm == 0ull) break;
-        const uint32_t fl = desc ? link : 0u;               // idle lanes fetch the root pair (cached)
-        const uint32_t lf = (uint32_t)__builtin_amdgcn_readlane((int)fl, (int)__builtin_ctzll(dm));
-        float4 q0, q1, q2;
-        float2 q3;
-        if (scalar_uniform && __ballot(desc && fl != lf) == 0ull)
-        {
-            typedef const __attribute__((address_space(4))) float cfloat;
-            cfloat* cp = (cfloat*)(const float*)(pairs) + 16u * lf;
-            q0 = make_float4(cp[0], cp[1], cp[2], cp[3]);
-            q1 = make_float4(cp[4], cp[5], cp[6], cp[7]);
-            q2 = make_float4(cp[8], cp[9], cp[10], cp[11]);
-            q3 = make_float2(cp[12], cp[13]);
-        }
-        else
-        {
-            uint32_t k0 = fl, k1 = fl, k2 = fl, k3 = fl;
-            quad_transpose(k0, k1, k2, k3, b1, b0);             // k_j = record of quad lane j
-            float4 a0 = pairs[4u * k0 + quarter], a1 = pairs[4u * k1 + quarter];
-            float4 a2 = pairs[4u * k2 + quarter], a3 = pairs[4u * k3 + quarter];
-            quad_transpose(a0.x, a1.x, a2.x, a3.x, b1, b0);
-            quad_transpose(a0.y, a1.y, a2.y, a3.y, b1, b0);
-            quad_transpose(a0.z, a1.z, a2.z, a3.z, b1, b0);
-            quad_transpose(a0.w, a1.w, a2.w, a3.w, b1, b0);
-            q0 = a0; q1 = a1; q2 = a2; q3 = make_float2(a3.x, a3.y);
-        }
-        if (COUNT)
-        {
-            const uint32_t uni = __ballot(desc && fl != lf) == 0ull ? 1u : 0u;
-            if (lane == (uint32_t)__builtin_ctzll(dm)) cnt.w_uni += uni;
-        }
-        if (desc)
-        {
-            bool c0, c1;
-            float tn0, tn1;
-            box_pair<FAST>(q0, q1, q2, r, best_t, max_t, c0, c1, tn0, tn1);
-            const uint32_t l0 = __float_as_uint(q3.x), l1 = __float_as_uint(q3.y);
-            if (COUNT) { cnt.box += 2; cnt.it_box += 1; }
-            const bool both = c0 & c1;
-            const bool go0 = both ? (tn0 < tn1) : c0;          // intersect.inl:84-101
-            if (both) st.push(go0 ? l1 : l0);
-            if (!(c0 | c1))
-            {
-                if (!pop_on_miss || st.empty()) { desc = false; rc = st.empty() ? -1 : 0; }
-                else if (++steps > step_limit) { cnt.aborted = true; desc = false; rc = -1; }
-                else
-                {
-                    link = st.pop();
-                    if (link & LEAF_BIT) { desc = false; at_leaf = true; }
-                }
-            }
-            else
-            {
-                link = go0 ? l0 : l1;
-                if (link & LEAF_BIT) { desc = false; at_leaf = true; }
-            }
-        }
-    }
-    if (at_leaf)
-    {
-        if (leaf_loop<KIND, COUNT, UV, MultiList>(prims, link, r, max_t, any, best_t, best_prim, cnt, hx, mh, hm)) return 1;
-        rc = st.empty() ? -1 : 0;
-    }
-    return rc;
 }
 
 __device__ __forceinline__ ray_t make_ray(f3 ori, f3 dir)

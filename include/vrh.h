@@ -237,10 +237,8 @@ enum vrh_option {
                                     visibility, unlimited for AO)                                 */
     VRH_OPT_POP_ON_MISS = 12,    /* step loop: a descent that misses both children pops its stack
                                     and keeps descending in the same step: 1 = on, 2 = off (auto: on) */
-    VRH_OPT_COOP_FETCH = 13,     /* step loop: each quad of lanes fetches its four pair records
-                                    together (one coalesced 64-B request per record) and transposes
-                                    them with DPP: 1 = on, 2 = off (auto: off; 1 needs a build
-                                    with -DVRH_COOP=1, else VRH_ERR_UNSUPPORTED)                  */
+    VRH_OPT_COOP_FETCH = 13,     /* removed in round 2 (the cooperative quad fetch measured slower):
+                                    0 / 2 accepted, 1 -> VRH_ERR_UNSUPPORTED                     */
     VRH_OPT_SCALAR_FETCH = 14,   /* step loop: a pair record every active lane of a wave wants is
                                     fetched once through the scalar cache: 1 = on, 2 = off (auto: on) */
     VRH_OPT_AO_GATE = 16,        /* AO step loop: a tile's AO rays are handed out only once all its

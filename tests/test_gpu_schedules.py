@@ -28,9 +28,6 @@ VARIANTS = {
     "step_cap3_wide": {"ao_schedule": 3, "descent_cap": 3, "wide_anyhit": 1},
     "step_pop_on_miss": {"ao_schedule": 3, "pop_on_miss": 1},
     "step_pop_cap2_wide": {"ao_schedule": 3, "pop_on_miss": 1, "descent_cap": 2, "wide_anyhit": 1},
-    "coop": {"ao_schedule": 3, "coop_fetch": 1},
-    "coop_wide": {"ao_schedule": 3, "coop_fetch": 1, "wide_anyhit": 1},
-    "coop_exact_pop_cap3": {"ao_schedule": 3, "coop_fetch": 1, "exact_minmax": 1, "pop_on_miss": 1, "descent_cap": 3},
     "scalar_off": {"ao_schedule": 3, "scalar_fetch": 2},
     "scalar_off_pop_cap2": {"ao_schedule": 3, "scalar_fetch": 2, "pop_on_miss": 1, "descent_cap": 2},
     "occ5": {"ao_schedule": 3, "waves_per_simd": 5},
@@ -49,14 +46,12 @@ VARIANTS = {
     "pair_layout": {"pair_layout": 1},
 }
 OPTIONS = ("ao_schedule", "refill_min", "wide_anyhit", "exact_minmax", "descent_cap", "xcd_queues",
-           "pop_on_miss", "coop_fetch", "scalar_fetch", "waves_per_simd", "pair_layout", "ao_gate",
+           "pop_on_miss", "scalar_fetch", "waves_per_simd", "pair_layout", "ao_gate",
            "stack_cap")
 
 
 @pytest.fixture(params=sorted(VARIANTS))
 def vctx(request, ctx):
-    if VARIANTS[request.param].get("coop_fetch") == 1 and not va.coop_fetch_available(ctx):
-        pytest.skip("cooperative fetch not compiled in (VRH_COOP=0, the default build)")
     for k, v in VARIANTS[request.param].items():
         ctx.set_option(k, v)
     yield ctx

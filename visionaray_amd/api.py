@@ -203,16 +203,6 @@ class Context:
             pass
 
 
-def coop_fetch_available(ctx):
-    """True if this libvrh build has the cooperative pair fetch compiled in (-DVRH_COOP=1)."""
-    try:
-        ctx.set_option("coop_fetch", 1)
-    except Exception:
-        return False
-    ctx.set_option("coop_fetch", 0)
-    return True
-
-
 def device_count():
     n = C.c_int(0)
     rc = capi.lib().vrh_device_count(C.byref(n))

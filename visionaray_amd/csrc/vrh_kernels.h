@@ -68,7 +68,6 @@ struct render_params
     uint32_t descent_cap;     // step loop: inner visits per step before a descent is resumed later
     uint32_t step_flags;      // step loop: bit 0 a descent that misses both children pops and continues;
                               // bit 1 wave-uniform pair records fetched through the scalar cache
-    uint32_t coop;            // step loop: quads of lanes fetch their pair records together (ray_step_coop)
     dev::shade_params shade;  // VRH_KERNEL_SIMPLE / MULTI_HIT: materials, lights, normal binding, ambient
     uint32_t max_hits;        // VRH_KERNEL_MULTI_HIT: N
     uint32_t num_bounces;     // VRH_KERNEL_WHITTED: loop iterations (eps = scene epsilon)

@@ -344,15 +344,9 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             constexpr bool UV = EPI == 1 || EPI == 3;
             const float mt = EPI == 3 ? max_t : FMAX;
             const bool an = EPI == 3 ? any : false;
-            // cooperative pair fetch: every lane takes part (quad exchanges), idle lanes included
-            int rc_coop = 0;
-            if (COOP_FETCH && P.coop)
-                rc_coop = (P.fast_ok && __ballot(busy && !finite) == 0ull)
-                    ? ray_step_coop<KIND, COUNT, true, UV, ML>(busy, P.pairs, P.prims, P.root, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, &hx, &mh, hm)
-                    : ray_step_coop<KIND, COUNT, false, UV, ML>(busy, P.pairs, P.prims, P.root, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, &hx, &mh, hm);
             if (mode != IDLE)
             {
-                int rc = (COOP_FETCH && P.coop) ? rc_coop : (P.fast_ok && __ballot(!finite) == 0ull)
+                int rc = (P.fast_ok && __ballot(!finite) == 0ull)
                     ? ray_step<KIND, COUNT, true, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, &hx, &mh, hm)
                     : ray_step<KIND, COUNT, false, UV, ML>(P.pairs, P.prims, P.quads, P.root, quad, r, mt, an, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, &hx, &mh, hm);
                 if constexpr (LIST)
@@ -573,14 +567,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             }
             // 4. one traversal step for every busy lane (same code for both ray kinds)
             int rc = 0;
-            if (COOP_FETCH && P.coop)
-            {
-                // cooperative pair fetch: every lane takes part (quad exchanges), idle lanes included
-                rc = (P.fast_ok && __ballot(busy && !finite) == 0ull)
-                    ? ray_step_coop<KIND, COUNT, true>(busy, P.pairs, P.prims, P.root, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm)
-                    : ray_step_coop<KIND, COUNT, false>(busy, P.pairs, P.prims, P.root, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm);
-            }
-            else if (busy)
+            if (busy)
             {
                 rc = (P.fast_ok && __ballot(!finite) == 0ull)
                     ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm)

@@ -128,13 +128,10 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
     case VRH_OPT_WIDE_ANYHIT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: wide any-hit is 1 (on) or 2 (off)"); ctx->opt_wide = int(value); break;
     case VRH_OPT_DESCENT_CAP: ctx->opt_dcap = int(value); break;
     case VRH_OPT_COOP_FETCH:
-        VRH_CHECK(value <= 2, "vrh_ctx_set_option: cooperative fetch is 1 (on) or 2 (off)");
-        if (value == 1 && !dev::COOP_FETCH)
-        {
-            set_error("vrh_ctx_set_option: cooperative fetch not compiled in (build with -DVRH_COOP=1)");
-            return VRH_ERR_UNSUPPORTED;
-        }
-        ctx->opt_coop = int(value); break;
+        // the cooperative quad fetch was removed in round 2 (measured slower, profiles/r01_ab_nocoop.log)
+        VRH_CHECK(value == 0 || value == 2, "vrh_ctx_set_option: cooperative fetch was removed (2 = off is accepted)");
+        if (value == 1) return VRH_ERR_UNSUPPORTED;
+        break;
     case VRH_OPT_WAVE_TIMES: VRH_CHECK(value <= 1, "vrh_ctx_set_option: wave times is 1 (on) or 0 (off)"); ctx->opt_wave_times = int(value); break;
     case VRH_OPT_AO_GATE: VRH_CHECK(value <= 2, "vrh_ctx_set_option: AO gate is 1 (on) or 2 (off)"); ctx->opt_gate = int(value); break;
     case VRH_OPT_POP_ON_MISS: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pop on miss is 1 (on) or 2 (off)"); ctx->opt_pop = int(value); break;
@@ -941,9 +938,6 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     // 4-wide any-hit records: auto on for the AO step loop (with ao_gate), off elsewhere
     const bool wide = ctx->opt_wide == 1 || (ctx->opt_wide == 0 && ao_step);
     p.quad_ok = (sc->quads && p.fast_ok && wide) ? 1u : 0u;
-    // cooperative pair fetch (step loop, binary records; the 4-wide any-hit records keep the
-    // per-lane fetch, so it is off whenever they are on)
-    p.coop = (ctx->opt_coop == 1 && !p.quad_ok) ? 1u : 0u;
     for (uint32_t f = 0; f < num_frames; ++f)
     {
         std::memcpy(p.cam[f].eye, cams[f].eye, 12); std::memcpy(p.cam[f].cam_u, cams[f].cam_u, 12);
