@@ -17,6 +17,8 @@
 // t.bin, occ.bin, color.bin (RGBA32F as the reference stores it) into outdir.
 #include <visionaray_hip/hip_kernels.h>
 
+#include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -205,6 +207,22 @@ int main(int argc, char** argv)
         {
             unsigned frame_num = argc > 6 ? unsigned(strtoul(argv[6], nullptr, 10)) : 0u;
             sched.frame(ao_kernel(ref, dnormals, default_intersector{}, W, frame_num), sparams, frame_num);
+        }
+        else if (mode == "bench")
+        {
+            // user-kernel throughput: the AO lambda over `frames` frames (one synchronous frame()
+            // each, as cuda_sched is driven), median wall time per frame
+            const int frames = argc > 6 ? atoi(argv[6]) : 10;
+            std::vector<double> ms;
+            for (int f = 0; f <= frames; ++f)
+            {
+                auto t0 = std::chrono::steady_clock::now();
+                sched.frame(ao_kernel(ref, dnormals, default_intersector{}, W, unsigned(f)), sparams, unsigned(f));
+                auto t1 = std::chrono::steady_clock::now();
+                if (f > 0) ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+            }
+            std::sort(ms.begin(), ms.end());
+            printf("{\"mode\":\"bench\",\"frame_ms_median\":%.4f,\"frames\":%d}\n", ms[ms.size() / 2], frames);
         }
         else if (mode == "mask")
         {
