@@ -556,19 +556,21 @@ struct user_kernels<K, typename std::enable_if<!std::is_same<K, hip_builtin_kern
         auto ref = rt.ref();
         f.color = reinterpret_cast<float4*>(ref.color);
         f.t = ref.t;
-        int dev = 0;
+        int dev = 0, prev = 0;
         void* stream = nullptr;
         check(vrh_ctx_get_stream(ctx.get(), &dev, &stream), "vrh_ctx_get_stream");
-        if (hipSetDevice(dev) != hipSuccess) throw hip_error("hipSetDevice", VRH_ERR_HIP);
+        if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(dev) != hipSuccess) throw hip_error("hipSetDevice", VRH_ERR_HIP);
         rt.begin_frame();
+        hipError_t e = hipSuccess;
         if (f.x1 > f.x0 && f.y1 > f.y0)
         {
             const dim3 grid((f.width + 7u) / 8u, (f.height + 7u) / 8u);
             const size_t lds = size_t(64) * VRH_USER_STACK * sizeof(uint32_t);
             hipLaunchKernelGGL(user_render<K>, grid, dim3(8, 8), lds, static_cast<hipStream_t>(stream), kernel, f);
-            hipError_t e = hipGetLastError();
-            if (e != hipSuccess) throw std::runtime_error(std::string("hip_sched::frame: user kernel launch: ") + hipGetErrorString(e));
+            e = hipGetLastError();
         }
+        (void)hipSetDevice(prev);        // the caller's current device is left as it was
+        if (e != hipSuccess) throw std::runtime_error(std::string("hip_sched::frame: user kernel launch: ") + hipGetErrorString(e));
         rt.end_frame();
     }
 };
