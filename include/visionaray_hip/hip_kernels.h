@@ -281,6 +281,9 @@ __device__ inline bvh_record traverse_bvh_slab(basic_ray<float> const& ray, vrh_
 {
     using HR = prim_record;
     hit_record_bvh<HR> result;
+    // the LDS stack holds VRH_USER_STACK entries: a deeper BVH (not passed through checked_ref)
+    // is not traversed -- a miss, never an out-of-bounds stack write
+    if (b.max_depth >= VRH_USER_STACK) return result;
     const vrh::dev::ray_t r = dev_ray(ray);
     const float4* pairs = static_cast<const float4*>(b.pairs);
     const float4* prims = static_cast<const float4*>(b.prims);
@@ -576,7 +579,8 @@ struct user_kernels<K, typename std::enable_if<!std::is_same<K, hip_builtin_kern
 };
 } // hip_detail
 
-// the user traversal stack holds VRH_USER_STACK entries: a deeper BVH cannot be traversed
+// the user traversal stack holds VRH_USER_STACK entries: a deeper BVH cannot be traversed (the
+// device code then reports a miss); checked_ref rejects it on the host instead
 inline hip_bvh_ref checked_ref(hip_bvh_ref r)
 {
     if (r.view.max_depth >= VRH_USER_STACK)
