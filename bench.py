@@ -189,6 +189,7 @@ def main():
 
     # ---- render paths -----------------------------------------------------------------------
     group = None
+    grouped = world > 1 or args.shards > 1     # one GPU with --shards S: a one-rank group (rehearsal)
     if world > 1:
         # the group id travels over torch.distributed once; the data path is libvrh + RCCL
         uid = torch.zeros(va.GROUP_ID_BYTES, dtype=torch.uint8, device="cuda")
@@ -196,12 +197,14 @@ def main():
             uid.copy_(torch.frombuffer(bytearray(va.render_group.unique_id()), dtype=torch.uint8))
         dist.broadcast(uid, 0)
         group = va.render_group(ctx, world, rank, bytes(uid.cpu().numpy().tobytes()))
+    elif grouped:
+        group = va.render_group(ctx, 1, 0, va.render_group.unique_id())
     full_rts = {}
 
     def target(b):
         """Full-image target of b frames (rank 0; every rank for N = 1)."""
         if b not in full_rts:
-            flags = _capi.VRH_RT_ALL if world == 1 else _capi.VRH_RT_COLOR | _capi.VRH_RT_PRIM_ID | _capi.VRH_RT_OCC
+            flags = _capi.VRH_RT_ALL if not grouped else _capi.VRH_RT_COLOR | _capi.VRH_RT_PRIM_ID | _capi.VRH_RT_OCC
             full_rts[b] = va.hip_buffer_rt(ctx, W, H * b, flags=flags) if (world == 1 or rank == 0) else None
         return full_rts[b]
 
@@ -210,7 +213,7 @@ def main():
     def run_batch(b):
         fn = next_frame[0]
         next_frame[0] += b
-        if world == 1:
+        if not grouped:
             va.render_batch(ctx, dev, target(b), [basis] * b, kern, None, frame_num=fn)
         else:
             group.render(dev, kern, target(b), [basis] * b, frame_num=fn, shards=args.shards)
@@ -340,7 +343,7 @@ def main():
         # launch (`traffic`), the L1 requests the hardware counted and how busy the TD unit was
         pmc = load_json(os.path.join(ROOT, "profiles", "pmc_traffic.json")) or {}
         traffic, pmc_info = None, None
-        if (pmc.get("scene") == args.scene and pmc.get("kernel") == kernel and world == 1
+        if (pmc.get("scene") == args.scene and pmc.get("kernel") == kernel and not grouped
                 and pmc.get("frames_per_launch") == F):
             traffic = pmc.get("hbm_bytes_per_launch")
             if pmc.get("l1_requests_per_launch"):
@@ -368,7 +371,8 @@ def main():
                 "scene": args.scene, "primitives": int(len(prims)), "bvh_nodes": int(len(host.nodes)),
                 "width": W, "height": H, "ao_samples": 8 if kernel == "ao" else 0,
                 "rays_per_frame": int(n_rays),
-                "parallelism": f"image-tile shard x{world}" + (" + RCCL gather (libvrh render group)" if world > 1 else ""),
+                "parallelism": f"image-tile shard x{world}" + (f" ({args.shards} shards)" if args.shards else "")
+                               + (" + RCCL gather (libvrh render group)" if grouped else ""),
                 "frames_per_launch": F, "launches": launches,
                 "frame_numbers": [first_timed, first_timed + args.steps - 1],
             },
@@ -408,9 +412,10 @@ def main():
         }
         print(json.dumps(line), flush=True)
 
-    if world > 1:
+    if group is not None:
         barrier()
         group.close()
+    if world > 1:
         dist.destroy_process_group()
 
 
