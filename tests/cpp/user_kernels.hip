@@ -8,6 +8,10 @@
 //                                                               harness's "mask" intersector)
 //   user_kernels heart <grid> <W> <H> <outdir>                  closest hit with the intersector
 //                                                               example's procedural heart cut-out
+//   user_kernels list  <grid> <W> <H> <outdir> x0 y0 x1 y1 f    the AO kernel over a list of two BVHs
+//                                                               (prim_id parity split), scissor box,
+//                                                               frame f (the harness's "list" mode)
+//   user_kernels bench <grid> <W> <H> <outdir> [frames]         throughput of the AO user kernel
 //
 // The kernel is the reference harness's AO lambda (oracle/ref_harness.cpp run_golden, after
 // ao/main.cpp:183-246) as a user would port it to cuda_sched: closest_hit over the BVH refs, the
@@ -121,17 +125,26 @@ static T* to_device(std::vector<T> const& v)
     return d;
 }
 
-// primary closest hit + 8 AO samples with intersector `isect` (oracle/ref_harness.cpp run_golden)
+// a short list of BVH refs, captured by value (the bvh_ref vector of ao/main.cpp:171-178)
+struct ref_list
+{
+    hip_bvh_ref r[2];
+    unsigned n;
+};
+
+// primary closest hit + 8 AO samples with intersector `isect` over the BVH list `refs`
+// (oracle/ref_harness.cpp run_golden / run_list)
 template <typename Isect>
-static auto ao_kernel(hip_bvh_ref ref, vec3 const* normals, Isect isect, unsigned W, unsigned frame_num)
+static auto ao_kernel(ref_list refs, vec3 const* normals, Isect isect, unsigned W, unsigned frame_num)
 {
     return [=] __device__ (ray r, unsigned x, unsigned y) mutable -> result_record<float>
     {
         result_record<float> result;
         const vec4 bg(0.1f, 0.2f, 0.3f, 1.0f);
         result.color = vec4(__uint_as_float(0xFFFFFFFFu), -1.0f, 0.0f, bg.w);
-        hip_bvh_ref const* begin = &ref;
-        auto hr = closest_hit(r, begin, begin + 1, isect);
+        hip_bvh_ref const* begin = refs.r;
+        hip_bvh_ref const* end = refs.r + refs.n;
+        auto hr = closest_hit(r, begin, end, isect);
         result.hit = hr.hit;
         if (!hr.hit) return result;
         hr.isect_pos = r.ori + r.dir * hr.t;
@@ -146,7 +159,7 @@ static auto ao_kernel(hip_bvh_ref ref, vec3 const* normals, Isect isect, unsigne
             vec3 s = hip_ao_sample(p, smp, frame_num);
             auto dir = normalize(s.x * uu + s.y * vv + s.z * w);
             ray ao(hr.isect_pos + dir * 1E-3f, dir);
-            auto ar = any_hit(ao, begin, begin + 1, 0.1f, isect);
+            auto ar = any_hit(ao, begin, end, 0.1f, isect);
             if (ar.hit) { clr = clr - 1.0f / 8; mask |= 1u << smp; }
         }
         result.color = vec4(__uint_as_float(unsigned(hr.prim_id)), hr.t, __uint_as_float(mask), clr);
@@ -202,11 +215,13 @@ int main(int argc, char** argv)
         hip_bvh_ref ref = checked_ref(device_bvh.ref());
         vec3 const* dnormals = static_cast<vec3 const*>(ref.view.normals);
         vec2* dtc = to_device(tc);
+        const ref_list one{ { ref, ref }, 1u };
+        int box[4] = { 0, 0, int(W), int(H) };      // list mode: the scissor box (x0, y0, x1, y1)
 
         if (mode == "ao")
         {
             unsigned frame_num = argc > 6 ? unsigned(strtoul(argv[6], nullptr, 10)) : 0u;
-            sched.frame(ao_kernel(ref, dnormals, default_intersector{}, W, frame_num), sparams, frame_num);
+            sched.frame(ao_kernel(one, dnormals, default_intersector{}, W, frame_num), sparams, frame_num);
         }
         else if (mode == "bench")
         {
@@ -217,7 +232,7 @@ int main(int argc, char** argv)
             for (int f = 0; f <= frames; ++f)
             {
                 auto t0 = std::chrono::steady_clock::now();
-                sched.frame(ao_kernel(ref, dnormals, default_intersector{}, W, unsigned(f)), sparams, unsigned(f));
+                sched.frame(ao_kernel(one, dnormals, default_intersector{}, W, unsigned(f)), sparams, unsigned(f));
                 auto t1 = std::chrono::steady_clock::now();
                 if (f > 0) ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
             }
@@ -237,7 +252,24 @@ int main(int argc, char** argv)
             isect.mask = to_device(mask);
             isect.w = n;
             isect.h = n;
-            sched.frame(ao_kernel(ref, dnormals, isect, W, 0u), sparams);
+            sched.frame(ao_kernel(one, dnormals, isect, W, 0u), sparams);
+        }
+        else if (mode == "list")
+        {
+            // the harness's list mode: the triangles split by prim_id parity into two BVHs, closest_hit
+            // / any_hit over the list of both, a scissor box, frame number `frame`
+            if (argc < 11) return 2;
+            for (int k = 0; k < 4; ++k) box[k] = atoi(argv[6 + k]);
+            const unsigned frame_num = unsigned(strtoul(argv[10], nullptr, 10));
+            std::vector<tri_t> part[2];
+            for (auto const& t : tris) part[t.prim_id % 2u].push_back(t);
+            auto h0 = build<index_bvh<tri_t>>(part[0].data(), part[0].size());
+            auto h1 = build<index_bvh<tri_t>>(part[1].data(), part[1].size());
+            hip_index_bvh<tri_t> d0(h0), d1(h1);
+            const ref_list two{ { checked_ref(d0.ref()), checked_ref(d1.ref()) }, 2u };
+            sparams.scissor_box = recti(box[0], box[1], box[2], box[3]);   // cuda_sched.inl:71 reading
+            rt.clear_color_buffer();
+            sched.frame(ao_kernel(two, dnormals, default_intersector{}, W, frame_num), sparams, frame_num);
         }
         else if (mode == "heart")
         {
@@ -267,6 +299,13 @@ int main(int argc, char** argv)
             const bool hit = pid[p] != 0xFFFFFFFFu;
             const float c[4] = { hit ? g : 0.1f, hit ? g : 0.2f, hit ? g : 0.3f, 1.0f };
             memcpy(&color[4 * p], c, 16);
+            const int px = int(p % W), py = int(p / W);
+            if (px < box[0] || py < box[1] || px >= box[2] || py >= box[3])
+            {
+                // outside the scissor box: the cleared target, as the reference leaves it
+                pid[p] = 0xFFFFFFFFu; t[p] = -1.0f; occ[p] = 0;
+                memset(&color[4 * p], 0, 16);
+            }
         }
         write_file(outdir + "/prim_id.bin", pid.data(), npx * 4);
         write_file(outdir + "/t.bin", t.data(), npx * 4);

@@ -9,7 +9,8 @@ tests/cpp/user_kernels.hip (built by visionaray_amd/Makefile `cpp_tests`) render
              mask_intersector);
   * heart -- closest hit with the intersector example's procedural cut-out, written in the example's
              width-generic style (unpack / simd::mask_type_t / Mask(bool[N]) / pow), against the
-             reference harness's "heart" mode (fixtures: heart_*).
+             reference harness's "heart" mode (fixtures: heart_*);
+  * list  -- the AO kernel over a list of two BVH refs with a scissor box (fixtures: list_*).
 """
 import os
 import subprocess
@@ -73,6 +74,17 @@ def test_user_heart_intersector_matches_reference(tmp_path, golden, case):
     assert diff == 0, f"{diff} pixels' prim id differ from the reference"
     assert np.array_equal(got["t"].view(np.uint32), ref["t"].view(np.uint32))
     assert int((got["prim_id"] != 0xFFFFFFFF).sum()) == g["hits"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["list_hf64_160x90", "list_hf200_320x180"])
+def test_user_kernel_over_bvh_list_with_scissor_matches_reference(tmp_path, golden, oracle_mod, case):
+    """closest_hit / any_hit over a list of two BVH refs (traverse_linear.inl:76-141) in a user lambda,
+    with the scissor box honoured by the user-kernel launch (cuda_sched.inl:71)."""
+    g = golden[case]
+    got = _run(tmp_path, "list", g["scene"], g["W"], g["H"], *g["scissor"], g["frame"])
+    _check_hashes(oracle_mod, got, g, [("prim_id", "primid_hash"), ("t", "t_hash"), ("occ", "occ_hash"),
+                                       ("color", "color_hash")])
 
 
 def test_user_kernel_header_needs_hipcc(tmp_path):
