@@ -30,7 +30,7 @@ Rank 0 prints one JSON line (the contract of the task statement) with:
   * roofline: the unit that binds the traversal kernel is the vector-memory path (L1 / TA / TD:
     TD busy 94-97 % of the launch, PMC in profiles/r02_*), so `achieved` is the kernel's vector-L1
     request rate -- rocprofv3's TCP_TOTAL_CACHE_ACCESSES of the committed PMC pass of this exact
-    command (profiles/pmc_traffic.json) x 16 B per launch over the live hipEvent launch time -- and
+    command (profiles/pmc_traffic_F<F>.json) x 16 B per launch over the live hipEvent launch time -- and
     `peak` the highest request rate of the kernel's access shape (per-lane dependent 64-B record
     gathers) on the microbenchmark tools/micro/l1_roof.hip (profiles/l1_roof.json).  The SURVEY
     §8d algorithmic HBM bytes are kept as roofline.hbm_algorithmic (informational);
@@ -341,7 +341,9 @@ def main():
         hbm_alg = bytes_per_ray * rays_launch / (k_ms_mean * 1e-3) / 1e9
         # PMC of this exact configuration (tools/r02_session.sh + tools/pmc_bench.py): HBM bytes per
         # launch (`traffic`), the L1 requests the hardware counted and how busy the TD unit was
-        pmc = load_json(os.path.join(ROOT, "profiles", "pmc_traffic.json")) or {}
+        # one committed pass per frames-per-launch value (the driver's --steps decides F)
+        pmc_name = f"pmc_traffic_F{F}.json"
+        pmc = load_json(os.path.join(ROOT, "profiles", pmc_name)) or {}
         traffic, pmc_info = None, None
         if (pmc.get("scene") == args.scene and pmc.get("kernel") == kernel and not grouped
                 and pmc.get("frames_per_launch") == F):
@@ -349,7 +351,7 @@ def main():
             if pmc.get("l1_requests_per_launch"):
                 pmc_info = {"l1_requests_per_launch": pmc["l1_requests_per_launch"],
                             "td_busy_frac": round(pmc["td_busy_frac"], 4),
-                            "source": "profiles/pmc_traffic.json: " + pmc.get("command", "")}
+                            "source": f"profiles/{pmc_name}: " + pmc.get("command", "")}
         # achieved: the hardware-counted L1 requests (TCP_TOTAL_CACHE_ACCESSES) of a committed PMC pass
         # of this exact configuration, over the live hipEvent time; without one it is not reported
         achieved = (pmc_info["l1_requests_per_launch"] * L1_REQ_BYTES / (k_ms_mean * 1e-3) / 1e9) if pmc_info else None

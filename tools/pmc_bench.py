@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc passes over the bench command into profiles/pmc_traffic.json.
+"""Summarise rocprofv3 --pmc passes over the bench command into profiles/pmc_traffic_F<F>.json
+(one file per frames-per-launch value F; bench.py reads the one of its own F).
 
     python tools/pmc_bench.py <session dir> [out.json] [scene] [kernel] [frames per launch] [command]
 

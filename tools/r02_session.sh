@@ -28,9 +28,13 @@ if [ -z "$SKIP_MICRO" ]; then
   step pmc_l1_roof 120 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD --output-format csv -d $OUT/pmc_l1_roof -o run -- tools/micro/l1_roof 16 20 512
 fi
 if [ -z "$SKIP_PMC" ]; then
-  step pmc_bench_tcp 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD --output-format csv -d $OUT/pmc_bench_tcp -o run -- python3 bench.py $BENCH --no-cpu-baseline
-  step pmc_bench_hbm 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_bench_hbm -o run -- python3 bench.py $BENCH --no-cpu-baseline
-  step pmc_bench_wr 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_bench_wr -o run -- python3 bench.py $BENCH --no-cpu-baseline
+  # the driver's command (--steps 20: F = 20) and the default one (--steps 64: F = 32)
+  for B in "$BENCH" ""; do
+    d=$OUT/pmc_F$( [ -n "$B" ] && echo 20 || echo 32 )
+    step $(basename $d)_tcp 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD --output-format csv -d $d/pmc_bench_tcp -o run -- python3 bench.py $B --no-cpu-baseline
+    step $(basename $d)_hbm 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $d/pmc_bench_hbm -o run -- python3 bench.py $B --no-cpu-baseline
+    step $(basename $d)_wr 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $d/pmc_bench_wr -o run -- python3 bench.py $B --no-cpu-baseline
+  done
 fi
 step trace_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_bench -o run -- python3 bench.py $BENCH
 exit 0
