@@ -22,7 +22,11 @@ from collections import defaultdict
 
 
 def batched(name):
-    return "render_unified_kernel" in name and name.rstrip(")").split("(")[0].rstrip(">").endswith("true")
+    """render_unified_kernel<KIND, AO, COUNT, OCC, EPI, LIST, BATCH[, SPILL]> with BATCH = true."""
+    if "render_unified_kernel<" not in name:
+        return False
+    args = [a.strip() for a in name.split("render_unified_kernel<", 1)[1].split(">", 1)[0].split(",")]
+    return len(args) >= 7 and args[6] == "true"
 
 
 def per_launch(d):
