@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--frames-in-flight", type=int, default=32,
                     help="max frames per persistent launch (vrh_render_batch, 1..32)")
     ap.add_argument("--single-frames", type=int, default=10, help="frames of the hip_sched::frame leg (median)")
+    ap.add_argument("--gather-ids", action="store_true",
+                    help="N > 1 / --shards: gather prim ids + AO masks with the colour (5 B per pixel on the wire, not 1)")
     ap.add_argument("--shards", type=int, default=0,
                     help="image-tile shards of the render group (0 = one per rank); > ranks: a rank renders several")
     return ap.parse_args()
@@ -140,6 +142,11 @@ def load_json(path):
 
 def main():
     args = parse()
+    # the JSON line is the only thing on stdout: native libraries (RCCL prints a version banner at
+    # communicator init) write to fd 1 directly, so fd 1 becomes stderr and the line goes to a dup
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -201,10 +208,15 @@ def main():
         group = va.render_group(ctx, 1, 0, va.render_group.unique_id())
     full_rts = {}
 
+    # N > 1: the root assembles the frame's colour (the AO example's product); its built-in colour
+    # crosses the wire as one byte per pixel (hit + occluded-sample count).  --gather-ids adds the
+    # prim ids and AO masks (5 B per pixel).
+    gather_fields = _capi.VRH_RT_COLOR | ((_capi.VRH_RT_PRIM_ID | _capi.VRH_RT_OCC) if args.gather_ids else 0)
+
     def target(b):
         """Full-image target of b frames (rank 0; every rank for N = 1)."""
         if b not in full_rts:
-            flags = _capi.VRH_RT_ALL if not grouped else _capi.VRH_RT_COLOR | _capi.VRH_RT_PRIM_ID | _capi.VRH_RT_OCC
+            flags = _capi.VRH_RT_ALL if not grouped else gather_fields
             full_rts[b] = va.hip_buffer_rt(ctx, W, H * b, flags=flags) if (world == 1 or rank == 0) else None
         return full_rts[b]
 
@@ -216,7 +228,7 @@ def main():
         if not grouped:
             va.render_batch(ctx, dev, target(b), [basis] * b, kern, None, frame_num=fn)
         else:
-            group.render(dev, kern, target(b), [basis] * b, frame_num=fn, shards=args.shards)
+            group.render(dev, kern, target(b), [basis] * b, frame_num=fn, shards=args.shards, fields=gather_fields)
         return fn
 
     def sync():
@@ -285,7 +297,8 @@ def main():
                       for k in ("color", "prim_id", "occ") if k in last)
         verify["timed_frames_match_single_frame_renders"] = bool(ok)
         if kernel == "ao" and F > 1:
-            verify["timed_frames_distinct"] = not np.array_equal(last["occ"][:n], last["occ"][(F - 1) * n:F * n])
+            key = "occ" if "occ" in last else "color"
+            verify["timed_frames_distinct"] = not np.array_equal(last[key][:n], last[key][(F - 1) * n:F * n])
         one.close()
     barrier()
 
@@ -412,7 +425,7 @@ def main():
             "host_build_s": round(build_s, 3),
             "verify": verify,
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
 
     if group is not None:
         barrier()

@@ -400,8 +400,10 @@ VRH_API int vrh_group_free(vrh_group* group);
  * mask objects on group i's context.  Every rank passes the same kernel, fields, cameras, frames
  * and shard count.  dst: rank 0's W x (H * num_frames) target (NULL on the other ranks); fields
  * (vrh_rt_flags) = the buffers assembled there (the same on every rank).  The built-in primary / AO
- * kernels' colour is re-derived on the root from prim id + AO mask (AO samples <= 8), so 4-5 B
- * per pixel cross xGMI; shading kernels gather their RGBA32F colour.  shards: S (0 = one per rank;
+ * kernels' colour is re-derived on the root (AO samples <= 8): without prim id / AO mask fields
+ * one byte per pixel crosses xGMI (0xFF miss, else the number of occluded samples -- the colour
+ * depends on nothing else, ao/main.cpp:234-238), with them 4-5 B; shading kernels gather their
+ * RGBA32F colour.  shards: S (0 = one per rank;
  * S > N: rank r renders shards r, r + N, ... -- so a one-rank group still runs the whole path).
  * Asynchronous: renders on each context's stream, the exchange and un-interleave on the group's
  * own stream (two staging slots: the next call's renders overlap this call's exchange);

@@ -67,6 +67,39 @@ def test_hf10M_ao_in_8_shards_equals_reference_hashes(ctx, group, golden, oracle
     assert O.fnv1a(out["color"]) == g["color_hash"]
 
 
+def test_hf10M_ao_colour_only_in_8_shards_equals_reference_hash(ctx, group, golden, oracle_mod):
+    """bench.py's N > 1 gather: a colour-only target, one code byte per pixel on the wire."""
+    host, dev = device_scene(ctx, "hf10M")
+    cam, W, H = scenes.scene_camera("hf10M")
+    dst = va.hip_buffer_rt(ctx, W, H, flags=_capi.VRH_RT_COLOR)
+    group.render(dev, va.ao_kernel(dev), dst, [cam.basis(W, H)], shards=8, fields=_capi.VRH_RT_COLOR)
+    group.sync()
+    out = dst.download()
+    dst.close()
+    assert set(out) == {"color"}
+    assert oracle_mod.fnv1a(out["color"]) == golden["hf10M"]["color_hash"]
+
+
+@pytest.mark.parametrize("kind,samples,shards,frames", [("ao", 8, 3, 2), ("ao", 3, 8, 1), ("ao", 5, 135, 1),
+                                                        ("primary", 0, 5, 2)])
+def test_colour_code_wire_equals_single_gpu_colour(ctx, group, kind, samples, shards, frames):
+    """Colour-only gathers re-derive the built-in colour from hit + occluded-sample count (any
+    sample count up to 8, and primary visibility)."""
+    host, dev = device_scene(ctx, "hf200")
+    W, H = 320, 180
+    cam, _, _ = scenes.scene_camera("hf200", W, H)
+    basis = cam.basis(W, H)
+    kern = va.ao_kernel(dev, samples=samples) if kind == "ao" else va.closest_hit_kernel(dev)
+    dst = va.hip_buffer_rt(ctx, W, H * frames, flags=_capi.VRH_RT_COLOR)
+    group.render(dev, kern, dst, [basis] * frames, frame_num=11, shards=shards, fields=_capi.VRH_RT_COLOR)
+    group.sync()
+    out = dst.download()
+    dst.close()
+    n = W * H
+    for f, ref in enumerate(single_frames(ctx, dev, kern, basis, W, H, frames, 11)):
+        assert np.array_equal(out["color"][f * n:(f + 1) * n].view(np.uint32), ref["color"].view(np.uint32)), f
+
+
 @pytest.mark.parametrize("shards,frames", [(2, 1), (3, 4), (8, 2), (135, 1)])
 def test_sharded_frames_equal_single_gpu_frames(ctx, group, shards, frames):
     """Frames in flight through the group (frame numbers 7, 8, ...), every buffer gathered."""

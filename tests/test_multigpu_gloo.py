@@ -1,6 +1,6 @@
 """CPU, world_size 2 and 3 over gloo: the protocol of libvrh's render groups (vrh_render_sharded,
 restated in visionaray_amd/multigpu.py) -- shard ownership s -> rank s % N, packed shard buffers
-of several frames on the wire as [prim ids | AO masks], point-to-point sends / receives paired in
+of several frames on the wire as [prim ids | AO masks] (or one colour code byte per pixel), point-to-point sends / receives paired in
 plan order, the root's un-interleave and colour re-derivation, the ray-count sum and max-over-ranks
 timing of bench.py -- reproduces the single-process frames bit for bit, including S > N shards.
 The per-rank renderer is the oracle restricted to the shard's rows; on the GPU box the same
@@ -28,7 +28,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, shards, port, outdir):
+def _worker(rank, world, shards, port, outdir, ids=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -36,14 +36,18 @@ def _worker(rank, world, shards, port, outdir):
         sc = O.make_scene(SCENE)
         cam = O.scene_camera(SCENE, W, H)
         rm = multigpu.rows_max(H, shards)
-        lay, nbytes = multigpu.wire_layout(FRAMES, rm, W)
+        lay, nbytes = multigpu.wire_layout(FRAMES, rm, W, ids=ids)
         sends, recvs = multigpu.exchange_plan(rank, world, shards)
         rays = 0
         bufs = []
         for s, _ in sends:                           # render every owned shard, packed
             buf = np.zeros(nbytes, np.uint8)
-            pid = buf[lay["pid"][0]:lay["pid"][0] + lay["pid"][1]].view(np.uint32).reshape(FRAMES, rm * W)
-            occ = buf[lay["occ"][0]:lay["occ"][0] + lay["occ"][1]].reshape(FRAMES, rm * W)
+            if ids:
+                pid = buf[lay["pid"][0]:lay["pid"][0] + lay["pid"][1]].view(np.uint32).reshape(FRAMES, rm * W)
+                occ = buf[lay["occ"][0]:lay["occ"][0] + lay["occ"][1]].reshape(FRAMES, rm * W)
+            else:   # rendered into a work buffer, then packed to the code byte
+                pid = np.empty((FRAMES, rm * W), np.uint32)
+                occ = np.zeros((FRAMES, rm * W), np.uint8)
             pid[:] = 0xFFFFFFFF
             for f in range(FRAMES):
                 for lr, y in enumerate(multigpu.packed_rows(H, s, shards)):
@@ -54,6 +58,8 @@ def _worker(rank, world, shards, port, outdir):
                     pid[f, lr * W:(lr + 1) * W] = out["prim_id"][y * W:(y + 1) * W]
                     occ[f, lr * W:(lr + 1) * W] = out["occ"][y * W:(y + 1) * W]
                     rays += out["rays"]
+            if not ids:
+                buf[:] = multigpu.pack_code(pid.reshape(-1), occ.reshape(-1))
             bufs.append(torch.from_numpy(buf))
         # the exchange: sends to the root in plan order; the root receives shard s from s % N
         gathered = np.zeros((shards, nbytes), np.uint8) if rank == 0 else None
@@ -75,6 +81,11 @@ def _worker(rank, world, shards, port, outdir):
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         if rank == 0:
             for f in range(FRAMES):
+                if not ids:
+                    gc = gathered.reshape(shards, FRAMES, rm * W)[:, f]
+                    code = multigpu.unshard_host(gc, W, H, shards)
+                    np.save(os.path.join(outdir, f"color{f}.npy"), multigpu.derive_colour_code(code, BG))
+                    continue
                 gp = gathered[:, lay["pid"][0]:lay["pid"][0] + lay["pid"][1]].view(np.uint32).reshape(shards, FRAMES, rm * W)[:, f]
                 go = gathered[:, lay["occ"][0]:lay["occ"][0] + lay["occ"][1]].reshape(shards, FRAMES, rm * W)[:, f]
                 pid = multigpu.unshard_host(gp, W, H, shards)
@@ -87,18 +98,20 @@ def _worker(rank, world, shards, port, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,shards", [(2, 2), (3, 3), (2, 5)])
-def test_sharded_exchange_equals_single_frames(tmp_path, oracle_mod, world, shards):
+@pytest.mark.parametrize("world,shards,ids", [(2, 2, True), (3, 3, True), (2, 5, True), (2, 3, False)])
+def test_sharded_exchange_equals_single_frames(tmp_path, oracle_mod, world, shards, ids):
+    """ids=False: a colour-only target, one code byte per pixel on the wire (bench.py's N > 1 default)."""
     O = oracle_mod
-    mp.start_processes(_worker, args=(world, shards, _free_port(), str(tmp_path)), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, shards, _free_port(), str(tmp_path), ids), nprocs=world, join=True,
                        start_method="spawn")
     st = np.load(tmp_path / "stats.npy")
     rays = 0
     for f in range(FRAMES):
         full = O.render(O.make_scene(SCENE), O.scene_camera(SCENE, W, H), mode=O.VO_MODE_AO, frame_num=FRAME0 + f)
         rays += full["rays"]
-        assert np.array_equal(np.load(tmp_path / f"pid{f}.npy"), full["prim_id"])
-        assert np.array_equal(np.load(tmp_path / f"occ{f}.npy"), full["occ"])
+        if ids:
+            assert np.array_equal(np.load(tmp_path / f"pid{f}.npy"), full["prim_id"])
+            assert np.array_equal(np.load(tmp_path / f"occ{f}.npy"), full["occ"])
         assert np.array_equal(np.load(tmp_path / f"color{f}.npy").view(np.uint32), full["color"].view(np.uint32))
     assert st[0] == world                      # max over ranks
     assert int(st[1]) == rays                  # rays summed over ranks = every frame

@@ -47,6 +47,8 @@ struct vrh_group
         bool used = false;
     } slot[2];
     uint32_t next = 0;
+    uint8_t* work = nullptr;               // colour-only gathers: one shard's prim ids + AO masks before packing
+    size_t work_bytes = 0;
 };
 
 namespace {
@@ -77,7 +79,8 @@ struct wire_layout
 {
     bool pid = false, occ = false, t = false, color = false;
     bool derive = false;                   // colour re-derived on the root from prim id (+ AO mask)
-    size_t bytes_per_px() const { return (pid ? 4 : 0) + (occ ? 1 : 0) + (t ? 4 : 0) + (color ? 16 : 0); }
+    bool code = false;                     // ... from one byte: 0xFF miss, else the occluded-sample count
+    size_t bytes_per_px() const { return (pid ? 4 : 0) + (occ ? 1 : 0) + (t ? 4 : 0) + (color ? 16 : 0) + (code ? 1 : 0); }
 };
 
 wire_layout layout_for(uint32_t fields, const vrh_kernel_desc& k)
@@ -89,6 +92,10 @@ wire_layout layout_for(uint32_t fields, const vrh_kernel_desc& k)
     w.pid = (fields & VRH_RT_PRIM_ID) || w.derive;
     w.occ = k.kind == VRH_KERNEL_AO && (((fields & VRH_RT_OCC) && k.samples <= 8) || w.derive);
     w.t = (fields & VRH_RT_T) != 0;
+    // a colour target without prim id / mask targets: the built-in colour depends only on hit and
+    // the number of occluded samples (ao/main.cpp:234-238), so 1 B per pixel crosses the wire, not 5
+    w.code = w.derive && !(fields & VRH_RT_PRIM_ID) && !(fields & VRH_RT_OCC);
+    if (w.code) w.pid = w.occ = false;
     return w;
 }
 
@@ -190,6 +197,7 @@ VRH_API int vrh_group_free(vrh_group* g)
 {
     if (!g) return VRH_OK;
     if (g->ctx) (void)hipSetDevice(g->ctx->device);
+    if (g->ctx) (void)hipStreamSynchronize(g->ctx->stream);
     if (g->stream) (void)hipStreamSynchronize(g->stream);
     if (g->comm) (void)ncclCommDestroy(g->comm);
     for (auto& s : g->slot)
@@ -199,6 +207,7 @@ VRH_API int vrh_group_free(vrh_group* g)
         if (s.send) (void)hipFree(s.send);
         if (s.recv) (void)hipFree(s.recv);
     }
+    if (g->work) (void)hipFree(g->work);
     if (g->stream) (void)hipStreamDestroy(g->stream);
     delete g;
     return VRH_OK;
@@ -241,7 +250,8 @@ VRH_API int vrh_render_sharded(uint32_t n, vrh_group* const* groups, const vrh_s
     const size_t shard_bytes = wl.bytes_per_px() * px;
     VRH_CHECK(shard_bytes > 0, "vrh_render_sharded: nothing to gather");
     const size_t o_pid = 0, o_occ = o_pid + (wl.pid ? 4 * px : 0), o_t = o_occ + (wl.occ ? px : 0),
-                 o_col = o_t + (wl.t ? 4 * px : 0);
+                 o_col = o_t + (wl.t ? 4 * px : 0), o_code = o_col + (wl.color ? 16 * px : 0);
+    const bool ao = kernels[0].kind == VRH_KERNEL_AO;
 
     // 1. every local group renders its shards into this call's staging slot (context stream)
     std::vector<uint32_t> slot_of(n);
@@ -258,6 +268,7 @@ VRH_API int vrh_render_sharded(uint32_t n, vrh_group* const* groups, const vrh_s
         const uint32_t mine = S > g->rank ? (S - g->rank + N - 1) / N : 0;    // shards s = rank, rank + N, ...
         int rc = grow(g, sl.send, sl.send_bytes, std::max<size_t>(mine * shard_bytes, 1));
         if (!rc && g->rank == 0) rc = grow(g, sl.recv, sl.recv_bytes, S * shard_bytes);
+        if (!rc && wl.code && mine) rc = grow(g, g->work, g->work_bytes, 5 * px);
         if (rc) return rc;
         for (uint32_t j = 0; j < mine; ++j)
         {
@@ -269,9 +280,18 @@ VRH_API int vrh_render_sharded(uint32_t n, vrh_group* const* groups, const vrh_s
             rt.occ = wl.occ ? base + o_occ : nullptr;
             rt.t = wl.t ? reinterpret_cast<float*>(base + o_t) : nullptr;
             rt.color = wl.color ? reinterpret_cast<float4*>(base + o_col) : nullptr;
+            if (wl.code)
+            {
+                // rendered into the work buffer, packed to one byte per pixel below (same stream,
+                // so the next shard's render starts after this pack)
+                rt.prim_id = reinterpret_cast<uint32_t*>(g->work);
+                rt.occ = ao ? g->work + 4 * px : nullptr;
+            }
             vrh_shard sh{ s, S, 1u, 0u };
             rc = vrh_render_batch(ctx, scenes[i], &rt, cams, num_frames, &kernels[i], &sh, frame_num);
             if (rc) return rc;
+            if (wl.code)
+                VRH_HIP(launch_pack_code(rt.prim_id, rt.occ, base + o_code, px, ctx->stream));
         }
         VRH_HIP(hipEventRecord(sl.rendered, ctx->stream));
         VRH_HIP(hipStreamWaitEvent(g->stream, sl.rendered, 0));
@@ -307,7 +327,8 @@ VRH_API int vrh_render_sharded(uint32_t n, vrh_group* const* groups, const vrh_s
                 u.gocc = wl.occ ? reinterpret_cast<const char*>(sl.recv + o_occ + f * fpx) : nullptr;
                 u.gt = wl.t ? reinterpret_cast<const char*>(sl.recv + o_t + 4 * f * fpx) : nullptr;
                 u.gcolor = wl.color ? reinterpret_cast<const char*>(sl.recv + o_col + 16 * f * fpx) : nullptr;
-                u.stride_pid = u.stride_occ = u.stride_t = u.stride_color = shard_bytes;
+                u.gcode = wl.code ? reinterpret_cast<const char*>(sl.recv + o_code + f * fpx) : nullptr;
+                u.stride_pid = u.stride_occ = u.stride_t = u.stride_color = u.stride_code = shard_bytes;
                 const size_t fo = size_t(f) * W * H;
                 u.color = (fields & VRH_RT_COLOR) ? dst->color + fo : nullptr;
                 u.pid = (fields & VRH_RT_PRIM_ID) ? dst->prim_id + fo : nullptr;

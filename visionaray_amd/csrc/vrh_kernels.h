@@ -108,7 +108,8 @@ struct unshard_params
     const char* gpid;            // gathered prim ids (u32)
     const char* gocc;            // gathered AO masks (u8)
     const char* gt;              // gathered closest-hit t (f32), or null
-    uint64_t stride_color, stride_pid, stride_occ, stride_t;   // bytes between consecutive shards
+    const char* gcode;           // gathered colour codes (u8: 0xFF miss, else occluded samples), or null
+    uint64_t stride_color, stride_pid, stride_occ, stride_t, stride_code;   // bytes between consecutive shards
     float4* color;
     uint32_t* pid;
     uint8_t* occ;
@@ -118,5 +119,8 @@ struct unshard_params
     uint32_t clip[4];            // scissor box x0, y0, x1, y1: pixels outside are left untouched
 };
 hipError_t launch_unshard(const unshard_params& u, hipStream_t s);
+// colour codes of n rendered pixels: 0xFF where prim_id is a miss, else the popcount of the AO mask
+// (occ null: 0)
+hipError_t launch_pack_code(const uint32_t* prim_id, const uint8_t* occ, uint8_t* code, size_t n, hipStream_t s);
 
 } // namespace vrh

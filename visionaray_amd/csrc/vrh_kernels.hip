@@ -751,6 +751,13 @@ __global__ void unshard_kernel(unshard_params u)
     size_t dst = (size_t)y * u.width + x;
     uint32_t pid = u.gpid ? reinterpret_cast<const uint32_t*>(u.gpid + g * u.stride_pid)[src] : 0xFFFFFFFFu;
     uint32_t occ = u.gocc ? (u.gocc + g * u.stride_occ)[src] : 0u;
+    uint32_t count = 0xFFFFFFFFu;                           // occluded samples, from a colour code
+    if (u.gcode)
+    {
+        const uint32_t c = (uint8_t)(u.gcode + g * u.stride_code)[src];
+        pid = c == 0xFFu ? 0xFFFFFFFFu : 0u;
+        count = c;
+    }
     if (u.pid && u.gpid) u.pid[dst] = pid;
     if (u.occ && u.gocc) u.occ[dst] = (uint8_t)occ;
     if (u.t && u.gt) u.t[dst] = reinterpret_cast<const float*>(u.gt + g * u.stride_t)[src];
@@ -764,11 +771,19 @@ __global__ void unshard_kernel(unshard_params u)
         {
             const float step = 1.0f / (float)u.samples;
             for (uint32_t s = 0; s < u.samples && s < 8u; ++s)
-                if ((occ >> s) & 1u) clr = clr - step;           // ao/main.cpp:234-238
+                if (count != 0xFFFFFFFFu ? s < count : ((occ >> s) & 1u) != 0u) clr = clr - step;   // ao/main.cpp:234-238
         }
         c = make_float4(clr, clr, clr, 1.0f);
     }
     u.color[dst] = c;
+}
+
+__global__ void pack_code_kernel(const uint32_t* __restrict__ pid, const uint8_t* __restrict__ occ,
+                                 uint8_t* __restrict__ code, size_t n)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    code[i] = pid[i] == 0xFFFFFFFFu ? (uint8_t)0xFFu : (uint8_t)(occ ? __popc((uint32_t)occ[i]) : 0);
 }
 
 } // namespace dev
@@ -883,6 +898,13 @@ int render_blocks_per_cu(const launch_config& c)
     std::lock_guard<std::mutex> g(mu);
     cache[key] = n;
     return n;
+}
+
+hipError_t launch_pack_code(const uint32_t* prim_id, const uint8_t* occ, uint8_t* code, size_t n, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(dev::pack_code_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, prim_id, occ, code, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_unshard(const unshard_params& u, hipStream_t s)

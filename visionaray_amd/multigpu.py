@@ -5,10 +5,12 @@ render groups run (vrh.h vrh_render_sharded, visionaray_amd/csrc/vrh_group.hip).
   terrain rows balance); shard s is rendered by rank s % N, packed: its bands back to back in a
   buffer of rows_max(H, S) rows (shard 0 owns the most bands).
 * On the wire one shard is [prim ids (u32) of every frame | AO masks (u8) of every frame | ...]
-  (wire_layout); rank r sends its shards r, r + N, ... in that order, the root receives shard s from
+  (wire_layout), or for a colour-only target one code byte per pixel (0xFF miss, else the number
+  of occluded AO samples, pack_code): the built-in colour depends on nothing else; rank r sends its shards r, r + N, ... in that order, the root receives shard s from
   rank s % N for s = 0, 1, ..., so sends and receives pair up in order per peer (exchange_plan).
 * The root un-interleaves every frame (unshard_host = vrh_unshard's mapping) and re-derives the
-  colour of the built-in kernels from prim id + AO mask.
+  colour of the built-in kernels from prim id + AO mask (derive_colour) or from the code
+  (derive_colour_code).
 
 libvrh runs this with ncclSend / ncclRecv on the GPU; the multi-process CPU tests run it with gloo
 point-to-point on oracle-rendered shards (tests/test_multigpu_gloo.py).
@@ -61,10 +63,13 @@ def exchange_plan(rank, nranks, shards):
     return sends, recvs
 
 
-def wire_layout(frames, rows, width, ao=True):
+def wire_layout(frames, rows, width, ao=True, ids=True):
     """Byte offsets of the fields of one packed shard of `frames` frames (built-in kernels with a
-    colour + prim id (+ AO mask) target): {'pid': (offset, bytes), 'occ': ...}, total bytes."""
+    colour + prim id (+ AO mask) target): {'pid': (offset, bytes), 'occ': ...}, total bytes.
+    ids=False (a colour-only target, vrh_group.hip wire_layout::code): {'code': (0, px)}."""
     px = frames * rows * width
+    if not ids:
+        return {"code": (0, px)}, px
     lay = {"pid": (0, 4 * px)}
     if ao:
         lay["occ"] = (4 * px, px)
@@ -96,6 +101,35 @@ def derive_colour(pid, occ, bg, samples=8, ao=True):
         for s in range(samples):
             occl = ((np.asarray(occ).astype(np.uint32) >> s) & 1).astype(bool)
             clr = np.where(occl, (clr - step).astype(np.float32), clr)
+    out[hit, 0] = out[hit, 1] = out[hit, 2] = clr[hit]
+    out[hit, 3] = 1.0
+    return out
+
+
+def pack_code(pid, occ=None):
+    """One byte per rendered pixel (pack_code_kernel): 0xFF on a miss, else the number of occluded
+    AO samples (0 without an AO mask)."""
+    pid = np.asarray(pid)
+    if occ is None:
+        code = np.zeros(len(pid), np.uint8)
+    else:
+        code = np.unpackbits(np.asarray(occ, np.uint8)[:, None], axis=1).sum(axis=1).astype(np.uint8)
+    code[pid == 0xFFFFFFFF] = 0xFF
+    return code
+
+
+def derive_colour_code(code, bg, samples=8, ao=True):
+    """derive_colour from the code byte: bg on 0xFF; 1 - k/samples (k subtractions) for k occluded
+    samples -- the same float sequence as subtracting in sample order."""
+    code = np.asarray(code)
+    out = np.empty((len(code), 4), np.float32)
+    out[:] = np.asarray(bg, np.float32)
+    hit = code != 0xFF
+    clr = np.ones(len(code), np.float32)
+    if ao:
+        step = np.float32(1.0) / np.float32(samples)
+        for s in range(samples):
+            clr = np.where(code.astype(np.uint32) > s, (clr - step).astype(np.float32), clr)
     out[hit, 0] = out[hit, 1] = out[hit, 2] = clr[hit]
     out[hit, 3] = 1.0
     return out
