@@ -548,155 +548,6 @@ __device__ __forceinline__ ray_t make_ray(f3 ori, f3 dir)
     return r;
 }
 
-// One traversal ITEM of the reference loop (detail/bvh/intersect.inl:66-130): `item` is either an
-// inner pair (both children box-tested: the near hit child becomes the next item, the far one is
-// pushed, none -> pop) or one primitive of a leaf (LEAF_BIT | leaf-ordered index: tested, then the
-// next primitive of the leaf or, after the leaf's last one, a pop).  The per-lane sequence of box
-// and primitive tests, best_t updates and stack operations is exactly ray_step's (and the
-// reference's); only the unit a wave iterates on is smaller, so a lane that reaches a leaf does
-// not idle while its neighbours keep descending, and the 3 loads a node and a triangle have in
-// common are issued once for the wave.  Returns true when the ray is finished (stack exhausted,
-// any-hit found -> `occluded`, or the step guard).
-template <int KIND, bool COUNT, bool FAST>
-__device__ __forceinline__ bool item_step(const float4* __restrict__ pairs, const float4* __restrict__ prims,
-                                          const ray_t& r, float max_t, bool any, lds_stack& st, uint32_t& item,
-                                          float& best_t, uint32_t& best_prim, bool& occluded, test_counts& cnt,
-                                          uint32_t& steps, uint32_t step_limit)
-{
-    if (++steps > step_limit) { cnt.aborted = true; return true; }
-    const bool leaf = (item & LEAF_BIT) != 0u;
-    const uint32_t idx = item & ~LEAF_BIT;
-    constexpr uint32_t PF4 = KIND == KIND_TRI ? 3u : 2u;
-    const float4* base = leaf ? prims + PF4 * idx : pairs + 4u * idx;
-    const float4 q0 = base[0], q1 = base[1];
-    if (COUNT) { count_vmem(cnt, base); count_vmem(cnt, base + 1); count_vmem(cnt, base + 2, leaf && KIND != KIND_TRI ? 0u : 1u); }
-    if (COUNT && !leaf) count_vmem(cnt, base + 3);
-    float4 q2 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), q3 = q2;
-    if constexpr (KIND == KIND_TRI) q2 = base[2];
-    if (!leaf)
-    {
-        if constexpr (KIND != KIND_TRI) q2 = base[2];
-        q3 = base[3];
-    }
-    bool pop;
-    if (!leaf)
-    {
-        bool b0, b1;
-        float tn0, tn1;
-        box_pair<FAST>(q0, q1, q2, r, best_t, max_t, b0, b1, tn0, tn1);
-        const uint32_t l0 = __float_as_uint(q3.x), l1 = __float_as_uint(q3.y);
-        if (COUNT) { cnt.box += 2; cnt.it_box = 1; }
-        const bool both = b0 & b1;
-        const bool go0 = both ? (tn0 < tn1) : b0;          // intersect.inl:84-101
-        if (both) st.push(go0 ? l1 : l0);
-        pop = !(b0 | b1);
-        item = go0 ? l0 : l1;
-    }
-    else
-    {
-        float t;
-        bool h;
-        uint32_t flags, pid;
-        if constexpr (KIND == KIND_TRI)
-        {
-            h = isect_tri(r, q0, q1, q2, t);
-            pid = __float_as_uint(q2.y);
-            flags = __float_as_uint(q2.w);
-        }
-        else
-        {
-            h = isect_sphere(r, q0, t);
-            pid = __float_as_uint(q1.x);
-            flags = __float_as_uint(q1.z);
-        }
-        if (COUNT) { cnt.prim += 1; cnt.it_prim = 1; }
-        if (h & (t >= 0.0f) & (t < best_t) & (t < max_t))      // update_if.h:48-56, 73-79
-        {
-            best_t = t;
-            best_prim = pid;
-            if (any) { occluded = true; return true; }           // exit_traversal.h:49-56
-        }
-        pop = (flags & END_BIT) != 0u;
-        item = item + 1u;
-    }
-    if (pop)
-    {
-        if (st.empty()) return true;
-        item = st.pop();
-    }
-    return false;
-}
-
-// item_step split by kind, for the VOTE schedule (a wave runs only one of the two per iteration).
-// node_step: `item` is an inner pair.  prim_step: `item` is LEAF_BIT | primitive.  Same return
-// convention and the same per-lane sequence of operations as item_step.
-__device__ __forceinline__ bool pop_or_done(lds_stack& st, uint32_t& item)
-{
-    if (st.empty()) return true;
-    item = st.pop();
-    return false;
-}
-
-template <bool COUNT, bool FAST>
-__device__ __forceinline__ bool node_step(const float4* __restrict__ pairs, const ray_t& r, float max_t, lds_stack& st,
-                                          uint32_t& item, float best_t, test_counts& cnt, uint32_t& steps,
-                                          uint32_t step_limit)
-{
-    if (++steps > step_limit) { cnt.aborted = true; return true; }
-    const float4* p = pairs + 4u * item;
-    const float4 q0 = p[0], q1 = p[1], q2 = p[2];
-    const float2 q3 = *reinterpret_cast<const float2*>(p + 3);     // links only (56 of 64 B)
-    bool b0, b1;
-    float tn0, tn1;
-    box_pair<FAST>(q0, q1, q2, r, best_t, max_t, b0, b1, tn0, tn1);
-    const uint32_t l0 = __float_as_uint(q3.x), l1 = __float_as_uint(q3.y);
-    if (COUNT) { cnt.box += 2; cnt.it_box = 1; }
-    const bool both = b0 & b1;
-    const bool go0 = both ? (tn0 < tn1) : b0;              // intersect.inl:84-101
-    if (both) st.push(go0 ? l1 : l0);
-    item = go0 ? l0 : l1;
-    if (!(b0 | b1)) return pop_or_done(st, item);
-    return false;
-}
-
-template <int KIND, bool COUNT>
-__device__ __forceinline__ bool prim_step(const float4* __restrict__ prims, const ray_t& r, float max_t, bool any,
-                                          lds_stack& st, uint32_t& item, float& best_t, uint32_t& best_prim,
-                                          bool& occluded, test_counts& cnt, uint32_t& steps, uint32_t step_limit)
-{
-    if (++steps > step_limit) { cnt.aborted = true; return true; }
-    const uint32_t idx = item & ~LEAF_BIT;
-    float t;
-    bool h;
-    uint32_t flags, pid;
-    if constexpr (KIND == KIND_TRI)
-    {
-        const float4* q = prims + 3u * idx;
-        const float4 a = q[0], b = q[1], c = q[2];
-        h = isect_tri(r, a, b, c, t);
-        pid = __float_as_uint(c.y);
-        flags = __float_as_uint(c.w);
-    }
-    else
-    {
-        const float4* q = prims + 2u * idx;
-        const float4 a = q[0], b = q[1];
-        h = isect_sphere(r, a, t);
-        pid = __float_as_uint(b.x);
-        flags = __float_as_uint(b.z);
-    }
-    if (COUNT) { cnt.prim += 1; cnt.it_prim = 1; }
-    if (h & (t >= 0.0f) & (t < best_t) & (t < max_t))          // update_if.h:48-56, 73-79
-    {
-        best_t = t;
-        best_prim = pid;
-        if (any) { occluded = true; return true; }               // exit_traversal.h:49-56
-    }
-    item = item + 1u;
-    if (flags & END_BIT) return pop_or_done(st, item);
-    return false;
-}
-
 // SURVEY.md Appendix A counter hash
 __device__ __forceinline__ uint32_t wang(uint32_t a)
 {

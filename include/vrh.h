@@ -216,11 +216,12 @@ enum vrh_option {
                                     steps of 4 while LDS rather than registers limits the waves
                                     per CU, and to at most 20 when the BVH is deeper than that) */
     VRH_OPT_AO_SCHEDULE = 3,     /* refilling loop of a wave: 3 = one descend-to-leaf step per
-                                    iteration, 4 = one traversal item (node pair or primitive)
-                                    per lane and iteration (primary visibility; AO always runs 3)
-                                    (auto: 4 for sphere primary visibility, else 3).  Round 1's
-                                    vote loop, item-loop AO and two-pass AO were removed: never
-                                    faster (profiles/r01_ab*)                                     */
+                                    iteration, the only schedule (auto: 3).  Round 1's vote loop,
+                                    item-loop AO and two-pass AO were removed (never faster,
+                                    profiles/r01_ab*), and in round 2 the primary-visibility item
+                                    loop (4, the old sphere default: 6-9 % slower than the step loop,
+                                    profiles/r02_ab/ab18_sphere_schedule.log); 4 returns
+                                    VRH_ERR_UNSUPPORTED                                             */
     VRH_OPT_BLOCKS_PER_CU = 4,   /* resident blocks per CU for the persistent grid (auto: max)     */
     VRH_OPT_WAVES_PER_SIMD = 5,  /* register budget of the unified kernel: 1 (none), 5, 6 or 8 (auto: 5 AO, 6 primary) */
     VRH_OPT_EXACT_MINMAX = 6,    /* 1 = always use the ternary min/max slab test (auto: hardware

@@ -66,7 +66,7 @@ def test_mask_intersector_matches_reference(ctx, golden, case):
     assert stats["rays"] == g["W"] * g["H"] + g["ao_rays"]
 
 
-@pytest.mark.parametrize("opts", [{"ao_schedule": 4}, {"xcd_queues": 2}, {"wide_anyhit": 1},
+@pytest.mark.parametrize("opts", [{"refill_min": 1}, {"xcd_queues": 2}, {"wide_anyhit": 1},
                                   {"exact_minmax": 1}, {"descent_cap": 2}])
 def test_mask_under_every_option(ctx, golden, opts):
     g, ref, tc, mask = case_inputs(golden, "mask_hf200_320x180")

@@ -1,7 +1,7 @@
 """GPU: every traversal schedule and record width reaches the same bit-exact result.
 
-The kernel has several ways to organise a wave's work (vrh.h VRH_OPT_AO_SCHEDULE: whole descend-
-to-leaf steps, single items for primary visibility; VRH_OPT_WIDE_ANYHIT: 4-wide any-hit records).  Only
+The kernel has several ways to organise a wave's work (descent caps, pop on miss, refill thresholds,
+the AO gate, VRH_OPT_WIDE_ANYHIT: 4-wide any-hit records, the stack's LDS share).  Only
 the defaults run in test_gpu_parity.py; here the parity cases are re-run under each non-default
 choice, on the same context, so none of the paths can drift from the reference.
 """
@@ -18,8 +18,7 @@ pytestmark = pytest.mark.gpu
 
 VARIANTS = {
     "step": {"ao_schedule": 3},
-    "item": {"ao_schedule": 4},
-    "item_refill1": {"ao_schedule": 4, "refill_min": 1},
+    "refill1": {"refill_min": 1},
     "global_queue": {"xcd_queues": 2},
     "step_wide": {"ao_schedule": 3, "wide_anyhit": 1},
     "step_wide_exact": {"ao_schedule": 3, "wide_anyhit": 1, "exact_minmax": 1},
@@ -32,7 +31,7 @@ VARIANTS = {
     "scalar_off_pop_cap2": {"ao_schedule": 3, "scalar_fetch": 2, "pop_on_miss": 1, "descent_cap": 2},
     "occ5": {"ao_schedule": 3, "waves_per_simd": 5},
     "occ6": {"ao_schedule": 3, "waves_per_simd": 6},
-    # the primary-visibility defaults switched off (pop on miss, descent cap 8, item refill 32)
+    # the primary-visibility defaults switched off (pop on miss, descent cap 8)
     "no_pop_uncapped": {"pop_on_miss": 2, "descent_cap": 1024, "refill_min": 16},
     "pop_cap10": {"pop_on_miss": 1, "descent_cap": 10},
     # the AO defaults switched off one by one (ao_gate + 4-wide any-hit + pop on miss)
@@ -83,3 +82,12 @@ def test_deep_comb(vctx, oracle_mod):
 
 def test_packed_shards(vctx):
     base.test_packed_shards_gather_to_identical_image(vctx, 3)
+
+
+def test_removed_schedules_are_refused(ctx):
+    """The item loop (round 2) and the cooperative fetch (round 1) were removed: asking for them is an
+    error, not a silent fallback."""
+    for opt, val in (("ao_schedule", 4), ("coop_fetch", 1)):
+        with pytest.raises(va.VrhError):
+            ctx.set_option(opt, val)
+        ctx.set_option(opt, 0)

@@ -61,7 +61,7 @@ struct render_params
     // since vrh_stats_reset
     unsigned long long* counters;
     uint32_t xcd_queues;      // 1: per-XCD tile queues with stealing; 0: one global queue
-    uint32_t refill_min;      // retire / refill once this many lanes are free (AO, item loops)
+    uint32_t refill_min;      // retire / refill once this many lanes are free (AO step loop)
     uint32_t refill_min_primary;   // the same for the step loop's primary-only stream
     uint32_t ao_gate;         // AO step loop: a tile's AO rays are handed out once its primaries are done
     unsigned long long* wave_times;   // VRH_OPT_WAVE_TIMES: per wave (start, end) of wall_clock64(), else null
@@ -89,7 +89,7 @@ struct launch_config
     int block;         // threads per block (multiple of 64)
     int stack_cap;     // LDS stack entries per lane
     int occ;           // register budget: min waves per SIMD (1, 6 or 8)
-    int sched;         // 0: step loop (render_unified_kernel), 1: item loop (render_item_kernel, primary only),
+    int sched;         // 0: step loop (render_unified_kernel),
                        // 2: step loop over a BVH list (render_unified_kernel<..., LIST>),
                        // 3: step loop, frames in flight (render_unified_kernel<..., BATCH>: same code)
     int epi;           // primary epilogue: 0 plain, 1 VRH_KERNEL_SIMPLE, 2 VRH_KERNEL_MULTI_HIT, 3 VRH_KERNEL_WHITTED (triangles)

@@ -632,110 +632,6 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     flush_totals<COUNT>(P, lane, rays_total, hits_total, cnt);
 }
 
-// ITEM schedule (primary visibility): a wave iterates on single traversal items (item_step: one
-// node pair or one primitive per lane) instead of whole descend-to-leaf steps.  The vector-memory
-// unit charges every wave-level load instruction whatever its active lanes, so what counts is how
-// many lanes share each one: a lane that has reached a leaf tests its primitives while its
-// neighbours are still descending.  Finished rays are retired and idle lanes refilled only once at
-// least P.refill_min lanes are free (or none is busy), so the ray-generation code runs with many
-// lanes at once.  Measured faster than the step loop for sphere primary visibility (short leaves
-// of cheap tests), its auto default there; slower for AO, which always runs the step loop.
-template <int KIND, bool COUNT, int OCC>
-__global__ __launch_bounds__(256, OCC) void render_item_kernel(render_params P)
-{
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63u;
-    const uint32_t block = blockDim.x;
-
-    lds_stack st;
-    st.mem = smem;
-    st.base = tid;
-    st.stride = block;
-    st.top = tid;
-    st.end = tid + P.stack_cap * block;
-    st.lim = st.end;
-    st.spill = nullptr;
-    test_counts cnt = {};
-    uint64_t rays_total = 0, hits_total = 0;
-
-    // lane state: BUSY while tracing, DONE once finished and not yet retired
-    constexpr uint32_t IDLE = 0, BUSY = 1, DONE = 2;
-    uint32_t mode = IDLE;
-    ray_t r;
-    float best_t = FMAX;
-    uint32_t best_prim = 0, steps = 0, item = 0;
-    uint32_t out_o = 0;      // output pixel of the lane's ray
-    bool occl = false, finite = true;
-
-    const float4 bg = make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
-    tile_queue tq = queue_init(P);
-    uint32_t tileC = next_tile(P, tq, lane);
-    uint32_t handedC = 0;
-
-    for (;;)
-    {
-        uint64_t busy = __ballot(mode == BUSY);
-        if (busy == 0ull || 64u - (uint32_t)__popcll(busy) >= P.refill_min)
-        {
-            // ---- A1. retire finished rays ----------------------------------------------------------
-            if (mode == DONE)
-            {
-                const bool hit = best_t != FMAX;
-                hits_total += hit ? 1 : 0;
-                if (P.prim_id) P.prim_id[out_o] = hit ? best_prim : 0xFFFFFFFFu;
-                if (P.t) P.t[out_o] = hit ? best_t : -1.0f;
-                if (P.color) P.color[out_o] = hit ? make_float4(1.0f, 1.0f, 1.0f, 1.0f) : bg;
-                if (P.occ) P.occ[out_o] = 0;
-                if (COUNT) count_stores(cnt, P, out_o, ST_COLOR | ST_OCC | ST_PID | ST_T);
-                mode = IDLE;
-            }
-            if (tileC != NONE && handedC >= 64u)
-            {
-                tileC = next_tile(P, tq, lane);
-                handedC = 0;
-            }
-            // ---- A2. hand out the current tile's pixels to idle lanes ----------------------------
-            const uint64_t idle = __ballot(mode == IDLE);
-            if (idle && tileC != NONE)
-            {
-                const uint32_t k = handedC + lane_rank(idle);
-                handedC = min(64u, handedC + (uint32_t)__popcll(idle));
-                uint32_t x, y, orow, fr;
-                if (mode == IDLE && k < 64u && tile_pixel(P, tileC, k, x, y, orow, fr))
-                {
-                    r = primary_ray(P, fr, x, y);
-                    best_t = FMAX; best_prim = 0; steps = 0; occl = false;
-                    item = P.root; st.reset();
-                    finite = finite_ray(r);
-                    mode = BUSY;
-                    out_o = orow * P.width + x;
-                    rays_total += 1;
-                }
-            }
-            busy = __ballot(mode == BUSY);
-            if (busy == 0ull)
-            {
-                if (tileC == NONE) break;
-                continue;
-            }
-        }
-        // ---- B. one traversal item for every busy lane -------------------------------------------
-        const bool my_busy = mode == BUSY;
-        const bool fast = P.fast_ok && __ballot(my_busy && !finite) == 0ull;
-        if (my_busy)
-        {
-            const bool done = fast
-                ? item_step<KIND, COUNT, true>(P.pairs, P.prims, r, FMAX, false, st, item, best_t, best_prim, occl, cnt, steps, P.step_limit)
-                : item_step<KIND, COUNT, false>(P.pairs, P.prims, r, FMAX, false, st, item, best_t, best_prim, occl, cnt, steps, P.step_limit);
-            if (done) mode = DONE;
-        }
-        if (COUNT) count_wave(cnt, my_busy);
-    }
-
-    flush_totals<COUNT>(P, lane, rays_total, hits_total, cnt);
-}
-
 // un-interleave gathered packed shards [count][rows_per_shard][W] into the full image; without a
 // gathered colour, re-derive it from prim id + AO mask exactly as the traversal kernel writes it
 __global__ void unshard_kernel(unshard_params u)
@@ -795,7 +691,6 @@ using kernel_fn = void (*)(render_params);
 template <int KIND, int OCC>
 static kernel_fn pick_occ(bool ao, bool count, int sched)
 {
-    if (sched == 1 && !ao) return count ? dev::render_item_kernel<KIND, true, OCC> : dev::render_item_kernel<KIND, false, OCC>;
     if (sched == 2)   // BVH list (step loop), at the default register budgets
     {
         if (!ao) return count ? dev::render_unified_kernel<KIND, false, true, 6, 0, true> : dev::render_unified_kernel<KIND, false, false, 6, 0, true>;

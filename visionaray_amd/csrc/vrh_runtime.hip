@@ -124,7 +124,10 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
         VRH_CHECK(value % 64 == 0, "vrh_ctx_set_option: block threads must be a multiple of 64");
         ctx->opt_block = int(value); break;
     case VRH_OPT_STACK_CAP: ctx->opt_stack = int(value); break;
-    case VRH_OPT_AO_SCHEDULE: VRH_CHECK(value == 0 || value == 3 || value == 4, "vrh_ctx_set_option: schedule is 3 (step loop) or 4 (item loop, primary visibility)"); ctx->opt_sched = int(value); break;
+    case VRH_OPT_AO_SCHEDULE:
+        // the item loop (4) was removed in round 2: the step loop measured faster for every kernel
+        if (value == 4) { set_error("vrh_ctx_set_option: the item-loop schedule was removed (the step loop is faster, profiles/r02_ab/ab18_sphere_schedule.log)"); return VRH_ERR_UNSUPPORTED; }
+        VRH_CHECK(value == 0 || value == 3, "vrh_ctx_set_option: schedule is 3 (step loop)"); ctx->opt_sched = int(value); break;
     case VRH_OPT_WIDE_ANYHIT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: wide any-hit is 1 (on) or 2 (off)"); ctx->opt_wide = int(value); break;
     case VRH_OPT_DESCENT_CAP: ctx->opt_dcap = int(value); break;
     case VRH_OPT_COOP_FETCH:
@@ -864,12 +867,10 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     lc.stack_cap = int(cap);
     lc.epi = whitted ? 3 : multi ? 2 : shade ? 1 : 0;
     lc.max_hits = multi ? int(k->max_hits) : 0;
-    // auto: the item loop for sphere primary visibility (short leaves of cheap tests, where the
-    // step loop's leaf iterations run at ~20 % lane utilisation), the step loop otherwise
-    if (ctx->opt_sched == 0) lc.sched = (lc.kind == 1 && !ao) ? 1 : 0;
-    else lc.sched = (ctx->opt_sched == 4 && !ao) ? 1 : 0;
-    if (shade) lc.sched = 0;   // the shading epilogue lives in the step loop
-    if (hmask) lc.sched = 0;   // the mask test lives in the step loop's leaf test
+    // every kernel runs the step loop (the round-1 item loop for sphere primary visibility measured
+    // 6-9 % slower than the step loop with its round-2 defaults, profiles/r02_ab/ab18_sphere_schedule.log,
+    // and was removed)
+    lc.sched = 0;
     if (list) lc.sched = 2;    // BVH lists: the step loop with the list merge
     // frames in flight on the step loop (primary / AO, uncounted): the BATCH instantiation
     if (lc.sched == 0 && num_frames > 1 && !lc.count && lc.epi == 0 && !hmask) lc.sched = 3;
@@ -877,7 +878,7 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     // profiles/r01_shade/shade_bench.jsonl); AO on the step loop: 5 waves/SIMD (96 VGPRs, no spills:
     // 4-6 % faster than 6 with 18 spilled VGPRs); primary visibility: 6 (profiles/r01_ab_waves/);
     // BVH lists run at these defaults
-    lc.occ = ctx->opt_occ ? ctx->opt_occ : lc.epi ? 1 : (lc.ao && lc.sched != 1) ? 5 : 6;
+    lc.occ = ctx->opt_occ ? ctx->opt_occ : lc.epi ? 1 : lc.ao ? 5 : 6;
     if (list) lc.occ = ao ? 5 : 6;
     // auto: the LDS part of the stack shrinks (in steps of 4 entries) while LDS, not registers,
     // limits the waves per CU -- a deep BVH (hf10M: depth 26) then keeps the register-bound
@@ -916,10 +917,10 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     p.num_roots = sc->num_roots;
     for (uint32_t i = 0; i < sc->num_roots; ++i) p.roots[i] = sc->roots[i];
     p.step_limit = sc->info.num_nodes + sc->info.num_indices + 16u;
-    // measured: profiles/r01_ab (AO), profiles/r01_ab_primary (primary visibility: the item loop
-    // refills at 32 free lanes; the step loop pops on a miss and caps a descent at 8 visits per
-    // step, +6 % on hf1M and +36 % on hf10M; both hurt AO)
-    const bool primary_step = lc.sched != 1 && !lc.ao && lc.epi == 0;
+    // measured: profiles/r01_ab (AO: refill at 32 free lanes), profiles/r01_ab_primary (primary
+    // visibility: pop on a miss and a cap of 8 visits per descent step, +6 % on hf1M and +36 % on
+    // hf10M; both hurt AO)
+    const bool primary_step = !lc.ao && lc.epi == 0;
     p.refill_min = ctx->opt_refill ? uint32_t(ctx->opt_refill) : 32u;
     p.refill_min_primary = ctx->opt_refill ? uint32_t(ctx->opt_refill) : 1u;
     p.descent_cap = ctx->opt_dcap ? uint32_t(ctx->opt_dcap) : primary_step ? 8u : 0xFFFFFFFFu;
@@ -927,7 +928,7 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     // AO (step loop): the tile's AO rays wait for its primaries (ao_gate), any-hit rays descend the
     // 4-wide records and primaries pop on a miss -- together +6 % on hf1M and +10 % on hf10M
     // (profiles/r02_ab/ab4_c4opts.log); each alone is within +-2 %
-    const bool ao_step = lc.ao && lc.sched != 1;
+    const bool ao_step = lc.ao;
     p.ao_gate = (ctx->opt_gate == 1 || (ctx->opt_gate == 0 && ao_step)) ? 1u : 0u;
     const bool pop = ctx->opt_pop == 1 || (ctx->opt_pop == 0 && (primary_step || lc.epi != 0 || ao_step));
     p.step_flags = (pop ? 1u : 0u) | (ctx->opt_scalar == 2 ? 0u : 2u);
