@@ -1,0 +1,18 @@
+#!/bin/bash
+# round-2 re-sweeps of launch defaults (tools/ab_builds.sh launch variants); logs under gpurun_out/
+#   ab19: primary (sph1M, hf1M) and AO (hf1M) knobs; ab20: the primary refill threshold, 20 and 1
+#   frames per launch; ab21: the new default against the old one
+case "${1:-ab21}" in
+ab19)
+  export VRH_AB='[{"name":"default"},{"name":"occ5","waves_per_simd":5},{"name":"occ8","waves_per_simd":8},{"name":"dcap4","descent_cap":4},{"name":"dcap16","descent_cap":16},{"name":"refill4","refill_min":4},{"name":"refill16","refill_min":16},{"name":"nopop","pop_on_miss":2},{"name":"scalar off","scalar_fetch":2},{"name":"global queue","xcd_queues":2}]'
+  SCENES="sph1M hf1M" KERNEL=primary REPS=1 ROUNDS=3 bash tools/ab_builds.sh > gpurun_out/ab19_primary.log 2>&1 || exit $?
+  export VRH_AB='[{"name":"default"},{"name":"refill16","refill_min":16},{"name":"refill24","refill_min":24},{"name":"refill40","refill_min":40},{"name":"refill48","refill_min":48},{"name":"occ6","waves_per_simd":6},{"name":"global queue","xcd_queues":2},{"name":"dcap8","descent_cap":8}]'
+  SCENES="hf1M" KERNEL=ao REPS=1 ROUNDS=3 bash tools/ab_builds.sh > gpurun_out/ab19_ao.log 2>&1 ;;
+ab20)
+  export VRH_AB='[{"name":"default"},{"name":"refill8","refill_min":8},{"name":"refill12","refill_min":12},{"name":"refill16","refill_min":16},{"name":"refill24","refill_min":24},{"name":"refill32","refill_min":32}]'
+  SCENES="sph1M hf1M hf10M" KERNEL=primary REPS=1 ROUNDS=3 bash tools/ab_builds.sh > gpurun_out/ab20_refill.log 2>&1 || exit $?
+  SCENES="sph1M hf1M" KERNEL=primary BATCH=1 REPS=1 ROUNDS=4 bash tools/ab_builds.sh > gpurun_out/ab20_refill_f1.log 2>&1 ;;
+ab21)
+  export VRH_AB='[{"name":"warm-up"},{"name":"default (16)"},{"name":"refill1 (old)","refill_min":1},{"name":"default again"}]'
+  SCENES="sph1M hf1M hf10M" KERNEL=primary REPS=1 ROUNDS=3 bash tools/ab_builds.sh > gpurun_out/ab21_refill_default.log 2>&1 ;;
+esac
