@@ -15,4 +15,7 @@ ab20)
 ab21)
   export VRH_AB='[{"name":"warm-up"},{"name":"default (16)"},{"name":"refill1 (old)","refill_min":1},{"name":"default again"}]'
   SCENES="sph1M hf1M hf10M" KERNEL=primary REPS=1 ROUNDS=3 bash tools/ab_builds.sh > gpurun_out/ab21_refill_default.log 2>&1 ;;
+ab22)
+  export VRH_AB='[{"name":"warm-up"},{"name":"default"},{"name":"refill24","refill_min":24},{"name":"refill40","refill_min":40},{"name":"dcap16","descent_cap":16},{"name":"occ6","waves_per_simd":6},{"name":"stack12","stack_cap":12},{"name":"stack16","stack_cap":16},{"name":"stack24","stack_cap":24},{"name":"nopop","pop_on_miss":2}]'
+  SCENES="hf10M" KERNEL=ao REPS=1 ROUNDS=3 bash tools/ab_builds.sh > gpurun_out/ab22_c4_defaults.log 2>&1 ;;
 esac
