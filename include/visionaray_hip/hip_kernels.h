@@ -43,7 +43,11 @@
 #include <utility>
 
 #ifndef VRH_USER_STACK
-#define VRH_USER_STACK 64   // traversal stack entries per thread (LDS), >= the deepest BVH traversed
+// traversal stack entries per thread (LDS), >= the deepest BVH traversed.  32 = the reference's own
+// detail::stack<32> (stack.h:17-51, usable depth 31); 64 entries (round 1) cost a 64-thread block
+// 16 KB of LDS, which held a CU to 10 resident waves (2.5 per SIMD) -- 32 lets the registers bound
+// it (4 waves per SIMD for the AO kernel)
+#define VRH_USER_STACK 32
 #endif
 
 namespace visionaray

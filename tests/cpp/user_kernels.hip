@@ -125,10 +125,12 @@ static T* to_device(std::vector<T> const& v)
     return d;
 }
 
-// a short list of BVH refs, captured by value (the bvh_ref vector of ao/main.cpp:171-178)
+// a short list of BVH refs (the bvh_ref vector of ao/main.cpp:171-178) in device memory, as the
+// reference's GPU programs hold them (a thrust::device_vector<bvh_ref> whose begin / end the kernel
+// captures; a by-value array in the lambda would be copied to scratch memory per thread)
 struct ref_list
 {
-    hip_bvh_ref r[2];
+    hip_bvh_ref const* r;
     unsigned n;
 };
 
@@ -215,7 +217,7 @@ int main(int argc, char** argv)
         hip_bvh_ref ref = checked_ref(device_bvh.ref());
         vec3 const* dnormals = static_cast<vec3 const*>(ref.view.normals);
         vec2* dtc = to_device(tc);
-        const ref_list one{ { ref, ref }, 1u };
+        const ref_list one{ to_device(std::vector<hip_bvh_ref>{ ref }), 1u };
         int box[4] = { 0, 0, int(W), int(H) };      // list mode: the scissor box (x0, y0, x1, y1)
 
         if (mode == "ao")
@@ -266,7 +268,7 @@ int main(int argc, char** argv)
             auto h0 = build<index_bvh<tri_t>>(part[0].data(), part[0].size());
             auto h1 = build<index_bvh<tri_t>>(part[1].data(), part[1].size());
             hip_index_bvh<tri_t> d0(h0), d1(h1);
-            const ref_list two{ { checked_ref(d0.ref()), checked_ref(d1.ref()) }, 2u };
+            const ref_list two{ to_device(std::vector<hip_bvh_ref>{ checked_ref(d0.ref()), checked_ref(d1.ref()) }), 2u };
             sparams.scissor_box = recti(box[0], box[1], box[2], box[3]);   // cuda_sched.inl:71 reading
             rt.clear_color_buffer();
             sched.frame(ao_kernel(two, dnormals, default_intersector{}, W, frame_num), sparams, frame_num);

@@ -923,9 +923,12 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     const bool primary_step = !lc.ao && lc.epi == 0;
     p.refill_min = ctx->opt_refill ? uint32_t(ctx->opt_refill) : 32u;
     // primary visibility with frames in flight refills once 16 lanes are free: +3 % sph1M, +2 % hf1M,
-    // +1.8 % hf10M at 20 frames per launch; one-frame launches and the shading epilogues keep 1
-    // (profiles/r02_ab/ab20_refill.log)
-    p.refill_min_primary = ctx->opt_refill ? uint32_t(ctx->opt_refill) : (primary_step && num_frames > 1) ? 16u : 1u;
+    // +1.8 % hf10M at 20 frames per launch (profiles/r02_ab/ab20_refill.log); simple::kernel and
+    // whitted once 8 are: +1-2.5 % / +1 % (profiles/r02_ab/shade_refill.jsonl); one-frame primary
+    // launches and multi_hit keep 1
+    const uint32_t refill_shade = (lc.epi == 1 || lc.epi == 3) ? 8u : 1u;
+    p.refill_min_primary = ctx->opt_refill ? uint32_t(ctx->opt_refill)
+                         : (primary_step && num_frames > 1) ? 16u : lc.epi ? refill_shade : 1u;
     p.descent_cap = ctx->opt_dcap ? uint32_t(ctx->opt_dcap) : primary_step ? 8u : 0xFFFFFFFFu;
     // shading epilogues (simple / multi_hit / whitted) pop on a miss too: +4-7 % (profiles/r01_shade/)
     // AO (step loop): the tile's AO rays wait for its primaries (ao_gate), any-hit rays descend the
