@@ -18,4 +18,7 @@ ab21)
 ab22)
   export VRH_AB='[{"name":"warm-up"},{"name":"default"},{"name":"refill24","refill_min":24},{"name":"refill40","refill_min":40},{"name":"dcap16","descent_cap":16},{"name":"occ6","waves_per_simd":6},{"name":"stack12","stack_cap":12},{"name":"stack16","stack_cap":16},{"name":"stack24","stack_cap":24},{"name":"nopop","pop_on_miss":2}]'
   SCENES="hf10M" KERNEL=ao REPS=1 ROUNDS=3 bash tools/ab_builds.sh > gpurun_out/ab22_c4_defaults.log 2>&1 ;;
+ab23)
+  export VRH_AB='[{"name":"warm-up"},{"name":"default"},{"name":"refill16","refill_min":16},{"name":"refill24","refill_min":24},{"name":"refill48","refill_min":48},{"name":"occ6","waves_per_simd":6},{"name":"ungated","ao_gate":2},{"name":"binary","wide_anyhit":2},{"name":"global queue","xcd_queues":2},{"name":"default again"}]'
+  SCENES="hf1M hf10M" KERNEL=ao BATCH=1 REPS=1 ROUNDS=5 bash tools/ab_builds.sh > gpurun_out/ab23_ao_single_frame.log 2>&1 ;;
 esac
