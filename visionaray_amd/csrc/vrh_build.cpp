@@ -7,13 +7,17 @@
 // Tree identity matters because closest-hit ties are resolved by traversal order.
 //
 // Structure differs from the reference: an explicit work stack instead of recursion, primitive
-// references kept as flat arrays, object splits only (no config uses spatial splits).
+// references kept as flat arrays, object splits only (no config uses spatial splits), and large
+// subtrees built on parallel threads and spliced back in the sequential numbering (build_fork).
 
 #include "vrh_internal.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cstring>
+#include <memory>
+#include <thread>
 #include <vector>
 
 namespace vrh {
@@ -127,6 +131,135 @@ bool try_split(std::vector<ref_t>& refs, size_t nrefs, const range_t& r, range_t
     return true;
 }
 
+// A subtree built on its own: nodes numbered as the sequential loop numbers them relative to the
+// subtree's root (local 0; its children pairs from 1, right subtree first), leaf primitive indices in
+// the order the sequential loop appends them, leaf `first` relative to the subtree's first index.
+struct subtree
+{
+    std::vector<node32> nodes;
+    std::vector<uint32_t> idx;
+    unsigned max_depth = 0;
+};
+
+// the sequential loop (build.inl:28-81 with an explicit stack) over refs[r.first, end)
+void build_local(std::vector<ref_t>& refs, range_t r, size_t end, subtree& out)
+{
+    size_t nrefs = end;      // refs beyond nrefs have been consumed by finished leaves
+    r.node = 0;
+    out.nodes.assign(1, node32{});
+    out.idx.clear();
+    out.max_depth = 0;
+    std::vector<range_t> work{ r };
+    while (!work.empty())
+    {
+        range_t w = work.back();
+        work.pop_back();
+        out.max_depth = std::max(out.max_depth, w.depth);
+        range_t left, right;
+        if (try_split(refs, nrefs, w, left, right))
+        {
+            const uint32_t c0 = static_cast<uint32_t>(out.nodes.size());
+            out.nodes.resize(c0 + 2u);
+            make_node(out.nodes[w.node], w.box, c0, 0);
+            left.node = c0; right.node = c0 + 1;
+            left.depth = right.depth = w.depth + 1;
+            work.push_back(left);    // popped after the whole right subtree
+            work.push_back(right);
+        }
+        else
+        {
+            const uint32_t cnt = static_cast<uint32_t>(nrefs - static_cast<size_t>(w.first));
+            make_node(out.nodes[w.node], w.box, static_cast<uint32_t>(out.idx.size()), cnt);
+            for (size_t i = static_cast<size_t>(w.first); i < nrefs; ++i) out.idx.push_back(static_cast<uint32_t>(refs[i].prim));
+            nrefs = static_cast<size_t>(w.first);
+        }
+    }
+}
+
+// Parallel build, same tree.  A range of at least kForkMin refs is split here (the same try_split
+// on the same refs: subtrees own disjoint ref ranges, [first, mid) and [mid, end), so the in-place
+// partitions do not interact); its right subtree is built on another thread while this one builds
+// the left.  Smaller ranges run the sequential loop into their own arrays.  assemble() then replays
+// the sequential order -- pair allocated, right subtree, then left -- and copies every node once.
+constexpr size_t kForkMin = size_t(1) << 15;
+
+struct fork_node
+{
+    bool split = false;
+    bounds3 box;
+    std::unique_ptr<fork_node> left, right;
+    subtree sub;                 // !split: the subtree built by build_local
+};
+
+struct fork_pool
+{
+    std::atomic<int> spare;      // threads that may still be started
+};
+
+void build_fork(std::vector<ref_t>& refs, const range_t& r, size_t end, fork_node& out, fork_pool& pool)
+{
+    range_t left, right;
+    if (end - static_cast<size_t>(r.first) >= kForkMin && try_split(refs, end, r, left, right))
+    {
+        out.split = true;
+        out.box = r.box;
+        out.sub.max_depth = r.depth;
+        out.left.reset(new fork_node);
+        out.right.reset(new fork_node);
+        left.depth = right.depth = r.depth + 1;
+        std::thread t;
+        if (pool.spare.fetch_sub(1) > 0)
+            t = std::thread([&] { build_fork(refs, right, end, *out.right, pool); });
+        else
+        {
+            pool.spare.fetch_add(1);
+            build_fork(refs, right, end, *out.right, pool);
+        }
+        build_fork(refs, left, static_cast<size_t>(right.first), *out.left, pool);
+        if (t.joinable())
+        {
+            t.join();
+            pool.spare.fetch_add(1);
+        }
+        return;
+    }
+    build_local(refs, r, end, out.sub);
+}
+
+struct assembly
+{
+    node32* nodes;
+    uint32_t* indices;
+    uint32_t num_nodes, num_idx;
+    unsigned max_depth;
+};
+
+void assemble(const fork_node& f, uint32_t slot, assembly& a)
+{
+    if (f.split)
+    {
+        const uint32_t c0 = a.num_nodes;
+        a.num_nodes += 2;
+        make_node(a.nodes[slot], f.box, c0, 0);
+        a.max_depth = std::max(a.max_depth, f.sub.max_depth);
+        assemble(*f.right, c0 + 1, a);
+        assemble(*f.left, c0, a);
+        return;
+    }
+    // local node c >= 1 -> a.num_nodes + c - 1; leaf first -> a.num_idx + first
+    const uint32_t node_shift = a.num_nodes - 1u, idx_shift = a.num_idx;
+    for (size_t i = 0; i < f.sub.nodes.size(); ++i)
+    {
+        node32 n = f.sub.nodes[i];
+        n.first += n.num_prims ? idx_shift : node_shift;
+        a.nodes[i == 0 ? slot : node_shift + static_cast<uint32_t>(i)] = n;
+    }
+    a.num_nodes += static_cast<uint32_t>(f.sub.nodes.size()) - 1u;
+    std::memcpy(a.indices + a.num_idx, f.sub.idx.data(), f.sub.idx.size() * sizeof(uint32_t));
+    a.num_idx += static_cast<uint32_t>(f.sub.idx.size());
+    a.max_depth = std::max(a.max_depth, f.sub.max_depth);
+}
+
 template <typename GetBox>
 int build_impl(size_t n, GetBox get_box, node32* nodes_out, uint32_t* num_nodes_out, uint32_t* indices_out,
                uint32_t* max_depth_out)
@@ -144,38 +277,15 @@ int build_impl(size_t n, GetBox get_box, node32* nodes_out, uint32_t* num_nodes_
         root.box.grow(refs[i].box);
         root.cbox.grow(c);
     }
-
-    size_t nrefs = n;        // refs beyond nrefs have been consumed by finished leaves
-    uint32_t num_nodes = 1;  // root slot
-    uint32_t num_idx = 0;
-    unsigned max_depth = 0;
-    std::vector<range_t> work{ root };
-    while (!work.empty())
-    {
-        range_t r = work.back();
-        work.pop_back();
-        max_depth = std::max(max_depth, r.depth);
-        range_t left, right;
-        if (try_split(refs, nrefs, r, left, right))
-        {
-            uint32_t c0 = num_nodes;
-            num_nodes += 2;
-            make_node(nodes_out[r.node], r.box, c0, 0);
-            left.node = c0; right.node = c0 + 1;
-            left.depth = right.depth = r.depth + 1;
-            work.push_back(left);    // popped after the whole right subtree
-            work.push_back(right);
-        }
-        else
-        {
-            uint32_t cnt = static_cast<uint32_t>(nrefs - static_cast<size_t>(r.first));
-            make_node(nodes_out[r.node], r.box, num_idx, cnt);
-            for (size_t i = static_cast<size_t>(r.first); i < nrefs; ++i) indices_out[num_idx++] = static_cast<uint32_t>(refs[i].prim);
-            nrefs = static_cast<size_t>(r.first);
-        }
-    }
-    *num_nodes_out = num_nodes;
-    if (max_depth_out) *max_depth_out = max_depth;
+    fork_pool pool;
+    const unsigned hw = std::thread::hardware_concurrency();
+    pool.spare = static_cast<int>(std::min(16u, hw ? hw : 1u)) - 1;   // the box's CPU share is 16 threads
+    fork_node top;
+    build_fork(refs, root, n, top, pool);
+    assembly a{ nodes_out, indices_out, 1u, 0u, 0u };
+    assemble(top, 0, a);
+    *num_nodes_out = a.num_nodes;
+    if (max_depth_out) *max_depth_out = a.max_depth;
     return VRH_OK;
 }
 
