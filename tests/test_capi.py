@@ -49,6 +49,16 @@ def test_scene_generators_and_builder_match_oracle(oracle_mod, name):
         assert va.face_normals(prims).tobytes() == O.face_normals(oprims).tobytes()
 
 
+@pytest.mark.parametrize("case", ["hf1M", "sph1M", "hf10M"])
+def test_parallel_builder_matches_reference_hashes_full_size(oracle_mod, golden, case):
+    """The product builder (subtrees of >= 32K refs on parallel threads) reproduces the reference
+    builder's node and index arrays at full size (hashes recorded from the reference)."""
+    g = golden[case]
+    b = va.build_index_bvh(scenes.primitives(g["scene"]))
+    assert oracle_mod.fnv1a(b.nodes) == g["bvh_hash"] and oracle_mod.fnv1a(b.indices) == g["idx_hash"]
+    assert len(b.nodes) == g["nodes"] and b.max_depth == g["max_depth"]
+
+
 def _soup(rng, n, spread=1.0):
     v1 = rng.uniform(-spread, spread, (n, 3)).astype(np.float32)
     e1 = rng.uniform(-0.2, 0.2, (n, 3)).astype(np.float32)
