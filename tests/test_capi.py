@@ -66,7 +66,7 @@ def _soup(rng, n, spread=1.0):
     return va.make_triangles(v1, e1, e2)
 
 
-@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 7, 17, 1000, 20000])
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 7, 17, 1000, 20000, 150000])
 def test_builder_random_soups_identical(oracle_mod, n):
     O = oracle_mod
     rng = np.random.default_rng(n)
@@ -74,6 +74,23 @@ def test_builder_random_soups_identical(oracle_mod, n):
     b = va.build_index_bvh(tris)
     on, oi, _ = O.build_bvh(tris, O.VO_TRI)
     assert b.nodes.tobytes() == on.tobytes() and np.array_equal(b.indices, oi)
+
+
+def test_parallel_builder_clustered_and_duplicate_inputs(oracle_mod):
+    """Inputs large enough to split on parallel threads (>= 32K refs per forked range) whose
+    subtrees differ a lot in size: tight clusters, many identical centroids, a long thin strip."""
+    O = oracle_mod
+    rng = np.random.default_rng(11)
+    centres = rng.uniform(-4, 4, (6, 3))
+    pts = np.concatenate([c + rng.normal(0, 0.01 * (k + 1), (20000 * (k + 1), 3)) for k, c in enumerate(centres)])
+    dup = np.repeat(rng.uniform(-1, 1, (500, 3)), 80, axis=0)
+    strip = np.stack([np.linspace(-50, 50, 60000), np.zeros(60000), np.zeros(60000)], 1)
+    for v in (pts, dup, strip):
+        v = v.astype(np.float32)
+        tris = va.make_triangles(v, np.full_like(v, 0.01), np.tile(np.float32([[0.01, -0.01, 0.005]]), (len(v), 1)))
+        b = va.build_index_bvh(tris)
+        on, oi, od = O.build_bvh(tris, O.VO_TRI)
+        assert b.nodes.tobytes() == on.tobytes() and np.array_equal(b.indices, oi) and b.max_depth == od
 
 
 def test_builder_degenerate_inputs_identical(oracle_mod):

@@ -168,6 +168,33 @@ def test_group_scissor_and_local_group(ctx):
     g.close()
 
 
+def test_colour_code_wire_with_scissor_box(ctx, group):
+    """Colour-only gather (1 B per pixel) with a scissor box: pixels inside equal the one-GPU frame,
+    pixels outside keep the root target's clear colour."""
+    host, dev = device_scene(ctx, "hf200")
+    W, H = 320, 180
+    cam, _, _ = scenes.scene_camera("hf200", W, H)
+    basis = cam.basis(W, H)
+    basis.scissor[:] = [17, 9, 301, 150]
+    kern = va.ao_kernel(dev)
+    clear = (0.25, 0.5, 0.75, 1.0)
+    dst = va.hip_buffer_rt(ctx, W, H, flags=_capi.VRH_RT_COLOR)
+    dst.clear_color_buffer(clear)
+    group.render(dev, kern, dst, [basis], frame_num=5, shards=6, fields=_capi.VRH_RT_COLOR)
+    group.sync()
+    out = dst.download()["color"].reshape(H, W, 4)
+    dst.close()
+    rt = va.hip_buffer_rt(ctx, W, H)
+    rt.clear_color_buffer(clear)
+    va.render(ctx, dev, rt, basis, kern, None, frame_num=5)
+    ref = rt.download()["color"].reshape(H, W, 4)
+    rt.close()
+    assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
+    inside = np.zeros((H, W), bool)
+    inside[9:150, 17:301] = True
+    assert (out[~inside] == np.float32(clear)).all()
+
+
 def test_group_argument_errors(ctx, group):
     host, dev = device_scene(ctx, "hf64")
     cam, _, _ = scenes.scene_camera("hf64", 160, 90)
