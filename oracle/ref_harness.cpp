@@ -866,6 +866,116 @@ static int run_list(scene_desc const& d, aligned_vector<tri_t> const& all, std::
     return 0;
 }
 
+//-------------------------------------------------------------------------------------------------
+// sampler: the reference's pixel samplers (sched_common.h:160-300 make_primary_rays for uniform,
+// jittered and ssaa<2/4/8>; :440-720 sample_pixel_impl: store, blend with 1/frame_num, ssaa's
+// store-zero-then-blend) driven pixel by pixel as simple_sched does, with the build's deterministic
+// stand-in for the scheduler's clock-seeded random_sampler: the jitter draws of pixel p in frame n
+// are U(c), U(c + 1) with c = p * 2 + 0x632BE5AB + n * 0x68E31DA4 (the AO samples keep Appendix A).
+// The target starts as `init` everywhere (what jittered_blend blends onto).
+//
+
+struct det_sampler
+{
+    uint32_t c;
+    float next() { return U(c++); }
+};
+
+template <typename P, typename SamplerT, typename MakeRays>
+static int run_sampler_impl(scene_desc const& d, aligned_vector<P>& prims, std::vector<vec3> const& normals,
+                            std::string const& outdir, int W, int H, bool do_ao, uint32_t frame_num, SamplerT st,
+                            MakeRays make_rays)
+{
+    auto bvh = build<index_bvh<P>>(prims.data(), prims.size());
+    camera cam = make_camera(d, W, H);
+    auto f = normalize(cam.eye() - cam.center());
+    auto s = normalize(cross(cam.up(), f));
+    auto u = cross(f, s);
+    vec3 cam_u = s * float(tan(cam.fovy() / 2.0f) * cam.aspect());
+    vec3 cam_v = u * float(tan(cam.fovy() / 2.0f));
+    vec3 cam_w = -f;
+    vec3 eye = cam.eye();
+
+    using bvh_ref = typename index_bvh<P>::bvh_ref;
+    std::vector<bvh_ref> bvhs{ bvh.ref() };
+    auto prims_begin = bvhs.data();
+    auto prims_end = bvhs.data() + bvhs.size();
+    const vec4 bg(0.1f, 0.2f, 0.3f, 1.0f);
+    const vec4 init(0.25f, 0.5f, 0.75f, 1.0f);
+    size_t npx = size_t(W) * H;
+    std::vector<uint32_t> prim_id(npx, 0xFFFFFFFFu);    // the last sub-sample's hit
+    std::vector<vec4> color(npx, init);
+    render_target_ref<PF_RGBA32F> rt_ref(color.data(), nullptr, size_t(W), size_t(H));
+
+    auto kernel = [&](ray r, unsigned x, unsigned y) -> result_record<float>
+    {
+        result_record<float> result;
+        result.color = bg;
+        auto hr = closest_hit(r, prims_begin, prims_end);
+        result.hit = hr.hit;
+        size_t p = size_t(y) * W + x;
+        prim_id[p] = hr.hit ? hr.prim_id : 0xFFFFFFFFu;
+        if (!hr.hit) return result;
+        if (!do_ao) { result.color = vec4(1.0f); return result; }
+        hr.isect_pos = r.ori + r.dir * hr.t;
+        vec4 clr(1.0f);
+        vec3 n = normals[hr.prim_id];
+        vec3 uu, vv, w = n;
+        make_orthonormal_basis(uu, vv, w);
+        for (int smp = 0; smp < 8; ++smp)
+        {
+            vec2 sxy = ao_sample(uint32_t(p), smp, frame_num);
+            float sx = sxy.x, sy = sxy.y;
+            float sz = sqrt(std::max(0.0f, 1.0f - sx * sx - sy * sy));
+            auto dir = normalize(sx * uu + sy * vv + sz * w);
+            ray ao;
+            ao.ori = hr.isect_pos + dir * 1E-3f;
+            ao.dir = dir;
+            auto ar = any_hit(ao, prims_begin, prims_end, 0.1f);
+            if (ar.hit) clr = clr - 1.0f / 8;
+        }
+        result.color = vec4(clr.xyz(), 1.0f);
+        return result;
+    };
+
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x)
+        {
+            det_sampler samp{ uint32_t(y * W + x) * 2u + 0x632BE5ABu + frame_num * 0x68E31DA4u };
+            auto rays = make_rays(samp, unsigned(x), unsigned(y), eye, cam_u, cam_v, cam_w);
+            visionaray::detail::sample_pixel_impl(kernel, st, rays, samp, frame_num, rt_ref, x, y, W, H);
+        }
+
+    write_file(outdir + "/prim_id.bin", prim_id.data(), npx * 4);
+    write_file(outdir + "/color.bin", color.data(), npx * 16);
+    fnv hp, hc;
+    for (size_t p = 0; p < npx; ++p) hp.u32(prim_id[p]);
+    hc.bytes(color.data(), npx * 16);
+    printf("{\"scene\":\"%s\",\"W\":%d,\"H\":%d,\"frame\":%u,\"primid_hash\":\"%016llx\",\"color_hash\":\"%016llx\"}\n",
+           d.name.c_str(), W, H, frame_num, (unsigned long long)hp.h, (unsigned long long)hc.h);
+    return 0;
+}
+
+template <typename P>
+static int run_sampler(scene_desc const& d, aligned_vector<P>& prims, std::vector<vec3> const& normals,
+                       std::string const& outdir, int W, int H, bool do_ao, std::string const& kind, uint32_t frame_num)
+{
+    auto rays_of = [&](auto st)
+    {
+        return [=](det_sampler& samp, unsigned x, unsigned y, vec3 eye, vec3 cu, vec3 cv, vec3 cw)
+        {
+            return visionaray::detail::make_primary_rays(ray{}, st, samp, x, y, size_t(W), size_t(H), eye, cu, cv, cw);
+        };
+    };
+    if (kind == "uniform")        return run_sampler_impl(d, prims, normals, outdir, W, H, do_ao, frame_num, pixel_sampler::uniform_type{}, rays_of(pixel_sampler::uniform_type{}));
+    if (kind == "jittered")       return run_sampler_impl(d, prims, normals, outdir, W, H, do_ao, frame_num, pixel_sampler::jittered_type{}, rays_of(pixel_sampler::jittered_type{}));
+    if (kind == "jittered_blend") return run_sampler_impl(d, prims, normals, outdir, W, H, do_ao, frame_num, pixel_sampler::jittered_blend_type{}, rays_of(pixel_sampler::jittered_type{}));
+    if (kind == "ssaa2")          return run_sampler_impl(d, prims, normals, outdir, W, H, do_ao, frame_num, pixel_sampler::ssaa_type<2>{}, rays_of(pixel_sampler::ssaa_type<2>{}));
+    if (kind == "ssaa4")          return run_sampler_impl(d, prims, normals, outdir, W, H, do_ao, frame_num, pixel_sampler::ssaa_type<4>{}, rays_of(pixel_sampler::ssaa_type<4>{}));
+    if (kind == "ssaa8")          return run_sampler_impl(d, prims, normals, outdir, W, H, do_ao, frame_num, pixel_sampler::ssaa_type<8>{}, rays_of(pixel_sampler::ssaa_type<8>{}));
+    return 2;
+}
+
 int main(int argc, char** argv)
 {
     if (argc < 3)
@@ -997,6 +1107,20 @@ int main(int argc, char** argv)
         std::vector<vec3> normals(t.size());
         for (size_t i = 0; i < t.size(); ++i) normals[i] = normalize(cross(t[i].e1, t[i].e2));
         return run_multi(d, t, normals, outdir, per_vertex, W, H);
+    }
+    if (mode == "sampler")
+    {
+        // sampler <scene> <outdir> <uniform|jittered|jittered_blend|ssaa2|ssaa4|ssaa8> <primary|ao> <frame> [W H]
+        if (argc < 7) return 2;
+        std::string outdir = argv[3], kind = argv[4];
+        bool do_ao = std::string(argv[5]) == "ao" && !d.spheres;
+        uint32_t frame_num = uint32_t(strtoul(argv[6], nullptr, 10));
+        int W = argc > 8 ? atoi(argv[7]) : d.W;
+        int H = argc > 8 ? atoi(argv[8]) : d.H;
+        return with_scene(d, [&](auto& prims, std::vector<vec3> const& normals)
+        {
+            return run_sampler(d, prims, normals, outdir, W, H, do_ao, kind, frame_num);
+        });
     }
     if (mode == "bench")
     {

@@ -11,6 +11,7 @@ Run in the build container (needs /root/reference to build the harness):
     python tests/golden/make_golden.py --frames                         (only the frame-number cases)
     python tests/golden/make_golden.py --list                           (only the BVH-list + scissor cases)
     python tests/golden/make_golden.py --heart                          (only the procedural-heart cases)
+    python tests/golden/make_golden.py --sampler                        (only the pixel-sampler cases)
 
 For every case the reference harness renders a full simple_sched<basic_ray<float>> frame
 (primary closest_hit + the Appendix-A AO kernel for triangle scenes) and this script stores:
@@ -260,6 +261,30 @@ def list_cases(out):
             print(case, rec["hits"], rec["ao_occluded"], flush=True)
 
 
+# (case, scene, kernel, sampler, frame, W, H): the reference's pixel samplers (harness `sampler` mode)
+SAMPLER_CASES = [(f"sampler_{k}_hf64_ao", "hf64", "ao", k, 3, 160, 90)
+                 for k in ("uniform", "jittered", "jittered_blend", "ssaa2", "ssaa4", "ssaa8")] + [
+    ("sampler_ssaa8_sph5000_primary", "sph5000", "primary", "ssaa8", 2, 128, 72),
+    ("sampler_jittered_blend_sph5000_primary", "sph5000", "primary", "jittered_blend", 2, 128, 72),
+]
+
+
+def sampler_cases(out):
+    for case, scene, kernel, kind, frame, W, H in SAMPLER_CASES:
+        with tempfile.TemporaryDirectory() as d:
+            r = subprocess.run([REF, "sampler", scene, d, kind, kernel, str(frame), str(W), str(H)], check=True,
+                               capture_output=True, text=True)
+            info = json.loads(r.stdout.strip().splitlines()[-1])
+            pid = np.fromfile(os.path.join(d, "prim_id.bin"), np.uint32)
+            color = np.fromfile(os.path.join(d, "color.bin"), np.float32).reshape(-1, 4)
+            rec = {"scene": scene, "kernel": kernel, "sampler": kind, "frame": frame, "W": W, "H": H,
+                   "primid_hash": fnv1a(pid), "color_hash": fnv1a(color)}
+            assert rec["primid_hash"] == info["primid_hash"] and rec["color_hash"] == info["color_hash"], case
+            np.savez_compressed(os.path.join(HERE, case + ".npz"), prim_id=pid, color=color)
+            out[case] = rec
+            print(case, rec["color_hash"], flush=True)
+
+
 def sah_cases(out):
     rec = {}
     for scene in SAH_SCENES:
@@ -274,7 +299,7 @@ def main():
     if not os.path.exists(REF):
         sys.exit("build the reference harness first: make -C oracle ref")
     only_shade = any(f in sys.argv for f in ("--shade", "--multi", "--sah", "--whitted", "--mask", "--frames", "--list",
-                                                "--heart"))
+                                                "--heart", "--sampler"))
     path = os.path.join(HERE, "golden.json")
     out = json.load(open(path)) if only_shade else {}
     rng = np.random.default_rng(12345)
@@ -308,6 +333,8 @@ def main():
             print(case, rec["hits"], rec["ao_occluded"], rec["primid_hash"], flush=True)
     if "--heart" in sys.argv:
         heart_cases(out)
+    elif "--sampler" in sys.argv:
+        sampler_cases(out)
     elif "--frames" in sys.argv:
         frame_cases(out, np.random.default_rng(2468))
     elif "--list" in sys.argv:
@@ -327,6 +354,7 @@ def main():
         mask_cases(out)
         frame_cases(out, np.random.default_rng(2468))
         list_cases(out)
+        sampler_cases(out)
     with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 
