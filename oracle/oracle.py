@@ -29,6 +29,9 @@ assert TRI_DTYPE.itemsize == 64 and SPHERE_DTYPE.itemsize == 48 and NODE_DTYPE.i
 VO_TRI, VO_SPHERE = 0, 1
 VO_MODE_PRIMARY, VO_MODE_AO, VO_MODE_SIMPLE, VO_MODE_MULTI_HIT, VO_MODE_WHITTED = 0, 1, 2, 3, 4
 VO_NORMALS_PER_FACE, VO_NORMALS_PER_VERTEX = 0, 1
+VO_SAMPLER_UNIFORM, VO_SAMPLER_JITTERED, VO_SAMPLER_JITTERED_BLEND, VO_SAMPLER_SSAA = 0, 1, 2, 3
+SAMPLERS = {"uniform": (0, 0), "jittered": (1, 0), "jittered_blend": (2, 0), "ssaa2": (3, 2), "ssaa4": (3, 4),
+            "ssaa8": (3, 8)}
 # plastic<float> / point_light<float> parameter records (vrh_oracle.h vo_plastic / vo_point_light)
 PLASTIC_DTYPE = np.dtype([("ca", "<f4", 3), ("ka", "<f4"), ("cd", "<f4", 3), ("kd", "<f4"), ("cs", "<f4", 3),
                           ("ks", "<f4"), ("exp", "<f4")])
@@ -100,6 +103,9 @@ def lib():
         L.vo_render_pixels.argtypes = [C.POINTER(_Scene), C.POINTER(_Camera), C.POINTER(_Kernel), vp, sz,
                                        vp, vp, vp, vp, C.c_int]
         L.vo_render_pixels.restype = C.c_uint64
+        L.vo_render_sampled.argtypes = [C.POINTER(_Scene), C.POINTER(_Camera), C.POINTER(_Kernel), C.c_int, C.c_int,
+                                        vp, vp, C.c_int]
+        L.vo_render_sampled.restype = C.c_int
         L.vo_fnv1a.argtypes = [vp, sz, C.c_uint64]; L.vo_fnv1a.restype = C.c_uint64
         L.vo_vertex_normals.argtypes = [vp, sz, vp]; L.vo_vertex_normals.restype = None
         L.vo_render_multi.argtypes = [C.POINTER(_Scene), C.POINTER(_Camera), C.POINTER(_Kernel), vp, vp, vp, C.c_int]
@@ -265,6 +271,20 @@ def render(scene, cam, mode=VO_MODE_AO, rows=None, threads=0, **kw):
     out["rays"] = int(rays)
     out["box_tests"] = int(cnt.box_tests)
     out["prim_tests"] = int(cnt.prim_tests)
+    return out
+
+
+def render_sampled(scene, cam, sampler, init=(0.25, 0.5, 0.75, 1.0), mode=VO_MODE_AO, threads=0, **kw):
+    """A frame through one of the reference's pixel samplers (SAMPLERS: uniform, jittered,
+    jittered_blend, ssaa2/4/8) onto a target filled with `init`: colour + the last sample's prim id."""
+    _, _, _, _, W, H = cam
+    kind, count = SAMPLERS[sampler]
+    out = {"color": np.tile(np.asarray(init, np.float32), (H * W, 1)), "prim_id": np.full(H * W, 0xFFFFFFFF, np.uint32)}
+    s, c, k = _structs(scene, cam, mode, **kw)
+    rc = lib().vo_render_sampled(C.byref(s), C.byref(c), C.byref(k), kind, count, _p(out["color"]), _p(out["prim_id"]),
+                                 threads)
+    if rc != 0:
+        raise ValueError("render_sampled: bad sampler")
     return out
 
 

@@ -598,10 +598,11 @@ out:
 /* ------------------------------------------------------------------------------------------ */
 /* Pixel pipeline + kernels                                                                    */
 
-/* sched_common.h:130-150 make_primary_ray_impl (pinhole) + :180-195 uniform sampler */
-static inline void primary_ray(const vo_camera* cam, unsigned x, unsigned y, v3* ori, v3* dir)
+/* sched_common.h:130-150 make_primary_ray_impl (pinhole) for the pixel position (x + ox, y + oy):
+ * the uniform sampler (:180-195) passes offset 0, jittered / ssaa (:196-300) their offsets */
+static inline void primary_ray_at(const vo_camera* cam, unsigned x, unsigned y, float ox, float oy, v3* ori, v3* dir)
 {
-    float fx = (float)x, fy = (float)y;
+    float fx = (float)x + ox, fy = (float)y + oy;
     float u = 2.0f * (fx + 0.5f) / (float)cam->width - 1.0f;
     float v = 2.0f * (fy + 0.5f) / (float)cam->height - 1.0f;
     v3 cu = mk(cam->cam_u[0], cam->cam_u[1], cam->cam_u[2]);
@@ -609,6 +610,11 @@ static inline void primary_ray(const vo_camera* cam, unsigned x, unsigned y, v3*
     v3 cw = mk(cam->cam_w[0], cam->cam_w[1], cam->cam_w[2]);
     *ori = mk(cam->eye[0], cam->eye[1], cam->eye[2]);
     *dir = normalize(add(add(muls(cu, u), muls(cv, v)), cw));
+}
+
+static inline void primary_ray(const vo_camera* cam, unsigned x, unsigned y, v3* ori, v3* dir)
+{
+    primary_ray_at(cam, x, y, 0.0f, 0.0f, ori, dir);
 }
 
 typedef struct { float color[4]; uint32_t prim_id; float t; uint8_t occ; uint32_t list_index; uint32_t rays; } px_out;
@@ -635,14 +641,14 @@ static void shade_whitted(const vo_scene* s, const vo_kernel* k, v3 ori, v3 dir,
                           uint32_t* rays, vo_counters* cnt);
 
 /* ao/main.cpp:183-246 with the deterministic sampler of SURVEY.md Appendix A */
-static px_out shade_pixel(const vo_scene* s, const vo_camera* cam, const vo_kernel* k, unsigned x, unsigned y,
-                          vo_counters* cnt)
+static px_out shade_pixel_at(const vo_scene* s, const vo_camera* cam, const vo_kernel* k, unsigned x, unsigned y,
+                             float ox, float oy, vo_counters* cnt)
 {
     px_out o;
     memcpy(o.color, k->bg, sizeof(o.color));
     o.prim_id = 0xFFFFFFFFu; o.t = -1.0f; o.occ = 0; o.list_index = 0xFFFFFFFFu; o.rays = 1;
     v3 ori, dir;
-    primary_ray(cam, x, y, &ori, &dir);
+    primary_ray_at(cam, x, y, ox, oy, &ori, &dir);
     float fo[3] = { ori.x, ori.y, ori.z }, fd[3] = { dir.x, dir.y, dir.z };
     vo_hit hr = trace(s, fo, fd, 0, FLT_MAX, cnt);
     if (!hr.hit) return o;
@@ -686,6 +692,12 @@ static px_out shade_pixel(const vo_scene* s, const vo_camera* cam, const vo_kern
     o.color[0] = o.color[1] = o.color[2] = clr;
     o.color[3] = 1.0f;
     return o;
+}
+
+static px_out shade_pixel(const vo_scene* s, const vo_camera* cam, const vo_kernel* k, unsigned x, unsigned y,
+                          vo_counters* cnt)
+{
+    return shade_pixel_at(s, cam, k, x, y, 0.0f, 0.0f, cnt);
 }
 
 /* get_surface (get_surface.h:336-376, 576-592) of a triangle hit: geometric + shading normal by
@@ -900,6 +912,74 @@ uint64_t vo_render_rows(const vo_scene* s, const vo_camera* cam, const vo_kernel
     }
     if (cnt) { cnt->box_tests += nbox; cnt->prim_tests += nprim; }
     return rays;
+}
+
+/* pixel samplers (sched_common.h:196-300 make_primary_rays, :440-720 sample_pixel_impl), pixel by
+ * pixel: uniform and jittered store the kernel's colour; jittered_blend blends it onto the target,
+ * dst = c * a + dst * (1 - a) with a = 1 / frame_num (pixel_access.h:1155-1176); ssaa<N> stores 0
+ * and then blends each of its N fixed-offset samples with a = 1 / N, 1 (the reference's offset
+ * tables, including its 8x entry 0.1825).  The jitter draws of pixel p in frame n are U(c) - 0.5,
+ * U(c + 1) - 0.5 with c = p * 2 + 0x632BE5AB + n * 0x68E31DA4 (the build's deterministic stand-in
+ * for the scheduler's clock-seeded random_sampler; the reference's jitter vector takes them in
+ * g++'s argument order: y the first, x the second).  prim_id: the last sample's hit. */
+static const float ssaa2[2][2] = { { -0.25f, -0.25f }, { 0.25f, 0.25f } };
+static const float ssaa4[4][2] = { { -0.125f, -0.375f }, { 0.375f, -0.125f }, { 0.125f, 0.375f }, { -0.375f, 0.125f } };
+static const float ssaa8[8][2] = { { -0.125f, -0.4375f }, { 0.375f, -0.3125f }, { -0.375f, -0.1875f }, { 0.125f, -0.0625f },
+                                   { -0.125f, 0.0625f }, { 0.375f, 0.1825f }, { -0.375f, 0.3125f }, { 0.125f, 0.4375f } };
+
+void vo_sampler_offsets(int kind, int count, unsigned x, unsigned y, unsigned width, uint32_t frame_num,
+                        int sub, float* ox, float* oy)
+{
+    *ox = 0.0f; *oy = 0.0f;
+    if (kind == VO_SAMPLER_JITTERED || kind == VO_SAMPLER_JITTERED_BLEND) {
+        /* vector<2, S> jitter(samp.next() - 0.5, samp.next() - 0.5) (sched_common.h:208): the two
+         * draws are constructor arguments, whose evaluation order C++ leaves unspecified; g++ on
+         * x86-64 (the reference build here) evaluates them right to left, so y takes the first draw */
+        uint32_t c = (y * width + x) * 2u + 0x632BE5ABu + frame_num * 0x68E31DA4u;
+        *oy = vo_uniform(c) - 0.5f;
+        *ox = vo_uniform(c + 1u) - 0.5f;
+    } else if (kind == VO_SAMPLER_SSAA) {
+        const float (*t)[2] = count == 2 ? ssaa2 : count == 4 ? ssaa4 : ssaa8;
+        *ox = t[sub][0]; *oy = t[sub][1];
+    }
+}
+
+int vo_render_sampled(const vo_scene* s, const vo_camera* cam, const vo_kernel* k, int kind, int count,
+                      float* color, uint32_t* prim_id, int threads)
+{
+    if (kind == VO_SAMPLER_SSAA && count != 2 && count != 4 && count != 8) return -1;
+    const int n = kind == VO_SAMPLER_SSAA ? count : 1;
+    int W = cam->width;
+#ifdef _OPENMP
+    if (threads <= 0) threads = omp_get_max_threads();
+#else
+    threads = 1;
+#endif
+    #pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
+    for (int y = 0; y < cam->height; ++y) {
+        for (int x = 0; x < W; ++x) {
+            size_t p = (size_t)y * W + x;
+            float* dst = color + 4 * p;
+            if (kind == VO_SAMPLER_SSAA) dst[0] = dst[1] = dst[2] = dst[3] = 0.0f;
+            for (int sub = 0; sub < n; ++sub) {
+                float ox, oy;
+                vo_sampler_offsets(kind, count, (unsigned)x, (unsigned)y, (unsigned)W, k->frame_num, sub, &ox, &oy);
+                px_out o = shade_pixel_at(s, cam, k, (unsigned)x, (unsigned)y, ox, oy, NULL);
+                prim_id[p] = o.prim_id;
+                if (kind == VO_SAMPLER_UNIFORM || kind == VO_SAMPLER_JITTERED) {
+                    memcpy(dst, o.color, 16);
+                } else {
+                    float a = kind == VO_SAMPLER_SSAA ? 1.0f / (float)n : 1.0f / (float)k->frame_num;
+                    float b = kind == VO_SAMPLER_SSAA ? 1.0f : 1.0f - a;
+                    for (int c = 0; c < 4; ++c) {
+                        float sc = o.color[c] * a, dc = dst[c] * b;
+                        dst[c] = sc + dc;
+                    }
+                }
+            }
+        }
+    }
+    return 0;
 }
 
 uint64_t vo_render_pixels(const vo_scene* s, const vo_camera* cam, const vo_kernel* k,

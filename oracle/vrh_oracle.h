@@ -145,6 +145,13 @@ uint64_t vo_render_multi(const vo_scene* s, const vo_camera* cam, const vo_kerne
                          uint32_t* mh_prim_id, float* mh_t, int threads);
 
 /* Same, for an explicit list of pixel indices (p = y*W + x); outputs are indexed by list position. */
+/* pixel samplers: VO_SAMPLER_* kind, count = ssaa samples (2, 4, 8); color is read (blend) and
+ * written for the whole image, prim_id = the last sample's hit.  Returns 0, -1 for a bad count. */
+enum { VO_SAMPLER_UNIFORM = 0, VO_SAMPLER_JITTERED = 1, VO_SAMPLER_JITTERED_BLEND = 2, VO_SAMPLER_SSAA = 3 };
+void vo_sampler_offsets(int kind, int count, unsigned x, unsigned y, unsigned width, uint32_t frame_num,
+                        int sub, float* ox, float* oy);
+int vo_render_sampled(const vo_scene* s, const vo_camera* cam, const vo_kernel* k, int kind, int count,
+                      float* color, uint32_t* prim_id, int threads);
 uint64_t vo_render_pixels(const vo_scene* s, const vo_camera* cam, const vo_kernel* k,
                           const uint32_t* pixels, size_t npix,
                           float* color, uint32_t* prim_id, float* t, uint8_t* occ, int threads);
