@@ -356,6 +356,30 @@ typedef struct {
 VRH_API int vrh_stats_reset(vrh_ctx* ctx);
 VRH_API int vrh_get_accum_stats(vrh_ctx* ctx, vrh_accum_stats* out);           /* syncs */
 
+/* Pixel samplers of sched_params (pixel_sampler::*, sched_common.h:160-300 make_primary_rays and
+ * :440-720 sample_pixel_impl) for the primary and AO kernels, one frame (`frame_num` as in
+ * vrh_render):
+ *   UNIFORM        = vrh_render;
+ *   JITTERED       the ray through (x + jx, y + jy), colour stored;
+ *   JITTERED_BLEND the same ray, colour blended onto the target: c / frame_num + dst (1 - 1 / frame_num)
+ *                  (pixel_access.h:1155-1176; the reference AO example's sampler, ao/main.cpp);
+ *   SSAA (count 2, 4, 8) the reference's fixed sub-pixel offsets (its 8x table as written, 0.1825
+ *                  included): colour 0, then each sample blended with 1 / count, 1, in order.
+ * The reference draws the jitter from the scheduler's clock-seeded random_sampler; here the draws of
+ * pixel p = y * width + x in frame n are U(c), U(c + 1) with c = p * 2 + 0x632BE5AB + n * 0x68E31DA4
+ * and U the Appendix-A hash; jy = U(c) - 0.5, jx = U(c + 1) - 0.5 (the reference's jitter vector takes
+ * its two draws in g++'s right-to-left argument order).  The AO samples of every sub-sample are the
+ * frame's.  Prim id / t / occ targets hold the last sample's values. */
+enum vrh_sampler_kind {
+    VRH_SAMPLER_UNIFORM = 0u, VRH_SAMPLER_JITTERED = 1u, VRH_SAMPLER_JITTERED_BLEND = 2u, VRH_SAMPLER_SSAA = 3u
+};
+typedef struct {
+    uint32_t kind;            /* vrh_sampler_kind                                         */
+    uint32_t count;           /* VRH_SAMPLER_SSAA: 2, 4 or 8 samples per pixel            */
+} vrh_pixel_sampler;
+VRH_API int vrh_render_sampled(vrh_ctx* ctx, const vrh_scene* scene, vrh_rt* rt, const vrh_camera* cam,
+                               const vrh_kernel_desc* kernel, const vrh_pixel_sampler* sampler, uint32_t frame_num);
+
 /* device -> host copies (any destination may be NULL); synchronous */
 VRH_API int vrh_rt_download(vrh_ctx* ctx, vrh_rt* rt, void* color, uint32_t* prim_id, float* t, uint8_t* occ);
 

@@ -12,7 +12,7 @@ from .api import (BVH_NODE_DTYPE, DEGREES_TO_RADIANS, GROUP_ID_BYTES, PLASTIC_DT
                   device_count, face_normals, hip_buffer_rt, hip_index_bvh, hip_sched,
                   hit_mask, index_bvh, load_obj, make_sched_params, make_spheres, make_triangles, model,
                   multi_hit_kernel, normals_per_face_binding, normals_per_vertex_binding, pixel_sampler, plastic,
-                  point_light, render, render_batch, render_group, render_sharded, sah_cost, shading, shard_bands,
+                  point_light, render, render_batch, render_group, render_sampled, render_sharded, sah_cost, shading, shard_bands,
                   simple_kernel, unshard, whitted_kernel, with_hit_mask)
 
 __all__ = [
@@ -21,6 +21,6 @@ __all__ = [
     "device_count", "face_normals", "hip_buffer_rt", "hip_index_bvh", "hip_sched",
     "hit_mask", "index_bvh", "load_obj", "make_sched_params", "make_spheres", "make_triangles", "model",
     "multi_hit_kernel", "normals_per_face_binding", "normals_per_vertex_binding", "pixel_sampler", "plastic",
-    "point_light", "render", "render_batch", "render_group", "render_sharded", "sah_cost", "shading",
+    "point_light", "render", "render_batch", "render_group", "render_sampled", "render_sharded", "sah_cost", "shading",
     "shard_bands", "simple_kernel", "unshard", "whitted_kernel", "with_hit_mask",
 ]

@@ -62,6 +62,13 @@ class vrh_accum_stats(C.Structure):
                 ("hits", C.c_uint64)]
 
 
+class vrh_pixel_sampler(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("count", C.c_uint32)]
+
+
+VRH_SAMPLER_UNIFORM, VRH_SAMPLER_JITTERED, VRH_SAMPLER_JITTERED_BLEND, VRH_SAMPLER_SSAA = 0, 1, 2, 3
+
+
 class vrh_shard(C.Structure):
     _fields_ = [("index", C.c_uint32), ("count", C.c_uint32), ("packed", C.c_uint32), ("reserved", C.c_uint32)]
 
@@ -147,6 +154,8 @@ SIGNATURES = {
                              C.POINTER(vrh_shard), _u32]),
     "vrh_render_batch": (C.c_int, [_vp, _vp, _vp, C.POINTER(vrh_camera), _u32, C.POINTER(vrh_kernel_desc),
                                    C.POINTER(vrh_shard), _u32]),
+    "vrh_render_sampled": (C.c_int, [_vp, _vp, _vp, C.POINTER(vrh_camera), C.POINTER(vrh_kernel_desc),
+                                     C.POINTER(vrh_pixel_sampler), _u32]),
     "vrh_sync": (C.c_int, [_vp]),
     "vrh_last_frame_stats": (C.c_int, [_vp, C.POINTER(vrh_frame_stats)]),
     "vrh_stats_reset": (C.c_int, [_vp]),

@@ -392,14 +392,40 @@ class hip_buffer_rt:
 # ---- scheduler ----------------------------------------------------------------------------------
 
 class pixel_sampler:
+    """pixel_sampler::* (sched_common.h:34-50): the sampler of make_sched_params."""
     class uniform_type:
-        pass
+        kind, count = 0, 0
+
+    class jittered_type:
+        kind, count = 1, 0
+
+    class jittered_blend_type:
+        kind, count = 2, 0
+
+    class ssaa2_type:
+        kind, count = 3, 2
+
+    class ssaa4_type:
+        kind, count = 3, 4
+
+    class ssaa8_type:
+        kind, count = 3, 8
+
+    @staticmethod
+    def ssaa_type(n):
+        """pixel_sampler::ssaa_type<N> for N in 1 (= uniform), 2, 4, 8."""
+        types = {1: pixel_sampler.uniform_type, 2: pixel_sampler.ssaa2_type, 4: pixel_sampler.ssaa4_type,
+                 8: pixel_sampler.ssaa8_type}
+        if n not in types:
+            raise ValueError("ssaa_type<N>: N is 1, 2, 4 or 8")
+        return types[n]
 
 
 class sched_params:
     def __init__(self, cam, rt, sampler=pixel_sampler.uniform_type, image_size=None):
-        if sampler is not pixel_sampler.uniform_type:
-            raise NotImplementedError("hip_sched supports pixel_sampler::uniform_type only")
+        if not hasattr(sampler, "kind"):
+            raise TypeError("sched_params: the sampler is one of the pixel_sampler types")
+        self.sampler = sampler
         self.cam = cam          # stored by value in the reference (scheduler.h:72)
         self.rt = rt            # by reference (scheduler.h:73)
         # scissor_box (scheduler.h:25-31, default recti(0, 0, w, h) at :175): x, y and the EXCLUSIVE
@@ -633,8 +659,17 @@ class hip_sched:
         if shard is not None:
             sh = capi.vrh_shard(shard[0], shard[1], 1 if shard[2] else 0, 0)
         rt.begin_frame()
-        capi.check("vrh_render", self.ctx.handle, kernel.bvh.handle, rt.handle, C.byref(cam), C.byref(kernel.desc),
-                   C.byref(sh) if sh is not None else None, frame_num)
+        sampler = getattr(sparams, "sampler", pixel_sampler.uniform_type)
+        if sampler.kind != pixel_sampler.uniform_type.kind:
+            # jittered / jittered_blend / ssaa<N> (sched_common.h:160-300, 440-720)
+            if sh is not None:
+                raise ValueError("hip_sched::frame: pixel samplers other than uniform render the whole image")
+            ps = capi.vrh_pixel_sampler(sampler.kind, sampler.count)
+            capi.check("vrh_render_sampled", self.ctx.handle, kernel.bvh.handle, rt.handle, C.byref(cam),
+                       C.byref(kernel.desc), C.byref(ps), frame_num)
+        else:
+            capi.check("vrh_render", self.ctx.handle, kernel.bvh.handle, rt.handle, C.byref(cam), C.byref(kernel.desc),
+                       C.byref(sh) if sh is not None else None, frame_num)
         if sync:
             rt.end_frame()
 
@@ -643,6 +678,13 @@ def render(ctx, bvh, rt, cam_basis, kernel, shard=None, frame_num=0):
     """Low-level frame with an explicit vrh_camera (full-image size) and optional vrh_shard."""
     capi.check("vrh_render", ctx.handle, bvh.handle, rt.handle, C.byref(cam_basis), C.byref(kernel.desc),
                C.byref(shard) if shard is not None else None, frame_num)
+
+
+def render_sampled(ctx, bvh, rt, cam_basis, kernel, sampler, frame_num=0):
+    """vrh_render_sampled: one frame through a pixel sampler (a pixel_sampler type)."""
+    ps = capi.vrh_pixel_sampler(sampler.kind, sampler.count)
+    capi.check("vrh_render_sampled", ctx.handle, bvh.handle, rt.handle, C.byref(cam_basis), C.byref(kernel.desc),
+               C.byref(ps), frame_num)
 
 
 def render_batch(ctx, bvh, rt, cam_bases, kernel, shard=None, frame_num=0):

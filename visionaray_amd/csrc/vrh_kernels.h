@@ -42,6 +42,12 @@ struct render_params
     uint32_t samples;
     float radius, eps;
     float bg[4];
+    // pixel sampler pass (vrh_render_sampled): primary rays through (x + px_off, y + px_off) or, with
+    // `jitter`, through the pixel's jittered position; colour stored (blend 0) or blended as
+    // c * blend_s + dst * blend_d with dst read (1) or taken as 0 (2: ssaa's first sample)
+    float px_off[2];
+    uint32_t jitter, blend;
+    float blend_s, blend_d;
 
     uint32_t shard_index, shard_count, packed;
     uint32_t tiles_x, num_tiles;   // tiles of ONE frame (the launch has num_frames x num_tiles units)
@@ -91,7 +97,8 @@ struct launch_config
     int occ;           // register budget: min waves per SIMD (1, 6 or 8)
     int sched;         // 0: step loop (render_unified_kernel),
                        // 2: step loop over a BVH list (render_unified_kernel<..., LIST>),
-                       // 3: step loop, frames in flight (render_unified_kernel<..., BATCH>: same code)
+                       // 3: step loop, frames in flight (render_unified_kernel<..., BATCH>: same code),
+                       // 6: a pixel-sampler pass (render_unified_kernel<..., SAMPLED>)
     int epi;           // primary epilogue: 0 plain, 1 VRH_KERNEL_SIMPLE, 2 VRH_KERNEL_MULTI_HIT, 3 VRH_KERNEL_WHITTED (triangles)
     int max_hits;      // MULTI_HIT: N (LDS hit lists)
     bool spill;        // the traversal stack continues in a global overflow block (render_unified_kernel<..., SPILL>)

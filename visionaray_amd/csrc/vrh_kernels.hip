@@ -109,10 +109,27 @@ __device__ __forceinline__ void flush_totals(const render_params& P, uint32_t la
 }
 
 // sched_common.h:130-150 make_primary_ray_impl (pinhole, uniform pixel sampler), frame f's camera
+template <bool SAMPLED = false>
 __device__ __forceinline__ ray_t primary_ray(const render_params& P, uint32_t f, uint32_t x, uint32_t y)
 {
     const frame_camera& c = P.cam[f];
     float fx = (float)x, fy = (float)y;
+    if constexpr (!SAMPLED) {}
+    else if (P.jitter)
+    {
+        // jittered samplers (sched_common.h:196-216): x + (U - 0.5), y + (U - 0.5) with the
+        // deterministic draws of vrh.h vrh_pixel_sampler -- y takes the first, as the reference's
+        // jitter vector evaluates its constructor arguments under g++ (oracle vo_sampler_offsets)
+        const uint32_t n = P.frame_num + f;
+        const uint32_t k = (y * P.width + x) * 2u + 0x632BE5ABu + n * 0x68E31DA4u;
+        fy = fy + (uniform01(k) - 0.5f);
+        fx = fx + (uniform01(k + 1u) - 0.5f);
+    }
+    else
+    {
+        fx = fx + P.px_off[0];                    // ssaa<N>: the sample's offset
+        fy = fy + P.px_off[1];
+    }
     float u = 2.0f * (fx + 0.5f) / (float)P.width - 1.0f;
     float v = 2.0f * (fy + 0.5f) / (float)P.height - 1.0f;
     f3 cu = mk3(c.cam_u[0], c.cam_u[1], c.cam_u[2]);
@@ -120,6 +137,20 @@ __device__ __forceinline__ ray_t primary_ray(const render_params& P, uint32_t f,
     f3 cw = mk3(c.cam_w[0], c.cam_w[1], c.cam_w[2]);
     f3 dir = normalize((cu * u + cv * v) + cw);
     return make_ray(mk3(c.eye[0], c.eye[1], c.eye[2]), dir);
+}
+
+// colour of output pixel o: stored, or blended onto the target (pixel_access.h:1155-1176:
+// dst = c * s + dst * d) for the jittered_blend / ssaa samplers
+template <bool SAMPLED>
+__device__ __forceinline__ void put_color(const render_params& P, size_t o, float4 c)
+{
+    if (SAMPLED && P.blend)
+    {
+        const float4 d = P.blend == 2u ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : P.color[o];
+        c = make_float4(c.x * P.blend_s + d.x * P.blend_d, c.y * P.blend_s + d.y * P.blend_d,
+                        c.z * P.blend_s + d.z * P.blend_d, c.w * P.blend_s + d.w * P.blend_d);
+    }
+    P.color[o] = c;
 }
 
 // Tile work queues.  A frame's tiles are split into 8 contiguous ranges (horizontal image strips);
@@ -245,7 +276,8 @@ __device__ __forceinline__ int list_next(const render_params& P, bool any, uint3
 // BATCH: the same code, instantiated separately for launches of several frames (vrh_render_batch,
 // frames in flight) so that profiles tell them apart from one-frame launches (hip_sched::frame).
 // SPILL: the traversal stack may continue in the global overflow block (stack_t<true>).
-template <int KIND, bool AO, bool COUNT, int OCC, int EPI = 0, bool LIST = false, bool BATCH = false, bool SPILL = false>
+template <int KIND, bool AO, bool COUNT, int OCC, int EPI = 0, bool LIST = false, bool BATCH = false, bool SPILL = false,
+          bool SAMPLED = false>
 __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params P)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -316,7 +348,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                         uint32_t x, y, orow, fr;
                         if (tile_pixel(P, tile, cand, x, y, orow, fr))
                         {
-                            r = primary_ray(P, fr, x, y);
+                            r = primary_ray<SAMPLED>(P, fr, x, y);
                             finite = finite_ray(r);
                             out_o = orow * P.width + x;
                             best_t = FMAX; best_prim = 0; steps = 0;
@@ -446,7 +478,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                         if (hit) c = shade_simple(P.shade, P.prims, P.normals, r, best_t, best_prim, hx);
                     if constexpr (EPI == 2)
                         c = shade_multi(P.shade, P.prims, P.normals, r, mh);
-                    if (P.color) P.color[out_o] = c;
+                    if (P.color) put_color<SAMPLED>(P, out_o, c);
                     if (P.prim_id) P.prim_id[out_o] = hit ? best_prim : 0xFFFFFFFFu;
                     if (P.t) P.t[out_o] = hit ? best_t : -1.0f;
                     if (P.occ) P.occ[out_o] = 0;
@@ -491,7 +523,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     for (uint32_t s2 = 0; s2 < S; ++s2)
                         if ((m >> s2) & 1u) clr = clr - step;                 // ao/main.cpp:234-238
                     const size_t o = (size_t)orow * P.width + x;
-                    if (P.color) P.color[o] = make_float4(clr, clr, clr, 1.0f);
+                    if (P.color) put_color<SAMPLED>(P, o, make_float4(clr, clr, clr, 1.0f));
                     if (P.occ) P.occ[o] = (uint8_t)m;
                     if (COUNT) count_stores(cnt, P, o, ST_COLOR | ST_OCC);
                 }
@@ -547,7 +579,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 bool started = false;
                 if (mode == IDLE && k < 64u && tile_pixel(P, tileC, k, x, y, orow, fr))
                 {
-                    r = primary_ray(P, fr, x, y);
+                    r = primary_ray<SAMPLED>(P, fr, x, y);
                     finite = finite_ray(r);
                     best_t = FMAX; best_prim = 0; steps = 0; max_t = FMAX; any = false; quad = false;
                     st.reset(); st.push(P.root); resume = NO_RESUME;
@@ -608,7 +640,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     }
                     else
                     {
-                        if (P.color) P.color[o] = bg;
+                        if (P.color) put_color<SAMPLED>(P, o, bg);
                         if (P.occ) P.occ[o] = 0;
                         if (COUNT) count_stores(cnt, P, o, ST_COLOR | ST_OCC);
                     }
@@ -695,6 +727,13 @@ static kernel_fn pick_occ(bool ao, bool count, int sched)
     {
         if (!ao) return count ? dev::render_unified_kernel<KIND, false, true, 6, 0, true> : dev::render_unified_kernel<KIND, false, false, 6, 0, true>;
         return count ? dev::render_unified_kernel<KIND, true, true, 5, 0, true> : dev::render_unified_kernel<KIND, true, false, 5, 0, true>;
+    }
+    if (sched == 6)   // a pixel-sampler pass (vrh_render_sampled): jittered / offset rays, blended colour
+    {
+        if constexpr (OCC == 5 || OCC == 6)
+            return ao ? dev::render_unified_kernel<KIND, true, false, OCC, 0, false, false, false, true>
+                      : dev::render_unified_kernel<KIND, false, false, OCC, 0, false, false, false, true>;
+        return nullptr;
     }
     if (sched == 3)   // frames in flight (a distinct symbol for profiles), step loop
         return ao ? dev::render_unified_kernel<KIND, true, false, OCC, 0, false, true>

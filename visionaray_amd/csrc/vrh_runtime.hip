@@ -792,9 +792,69 @@ VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_
     return vrh_render_batch(ctx, sc, rt, cam, 1, k, shard, frame_num);
 }
 
+namespace {
+// one pass of a pixel sampler (vrh_render_sampled); null = the uniform sampler, colour stored
+struct sampler_pass
+{
+    float off[2];
+    uint32_t jitter, blend;
+    float s, d;
+};
+int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_camera* cams, uint32_t num_frames,
+                      const vrh_kernel_desc* k, const vrh_shard* shard, uint32_t frame_num, const sampler_pass* sp);
+} // namespace
+
 VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_camera* cams,
                              uint32_t num_frames, const vrh_kernel_desc* k, const vrh_shard* shard,
                              uint32_t frame_num)
+{
+    return render_batch_impl(ctx, sc, rt, cams, num_frames, k, shard, frame_num, nullptr);
+}
+
+VRH_API int vrh_render_sampled(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_camera* cam,
+                               const vrh_kernel_desc* k, const vrh_pixel_sampler* ps, uint32_t frame_num)
+{
+    VRH_CHECK(ctx && sc && rt && cam && k && ps, "vrh_render_sampled: null argument");
+    VRH_CHECK(ps->kind <= VRH_SAMPLER_SSAA, "vrh_render_sampled: unknown pixel sampler");
+    if (ps->kind == VRH_SAMPLER_UNIFORM) return render_batch_impl(ctx, sc, rt, cam, 1, k, nullptr, frame_num, nullptr);
+    if (k->kind != VRH_KERNEL_PRIMARY && k->kind != VRH_KERNEL_AO)
+    {
+        set_error("vrh_render_sampled: jittered / ssaa samplers run the primary and AO kernels");
+        return VRH_ERR_UNSUPPORTED;
+    }
+    if (ps->kind != VRH_SAMPLER_SSAA)
+    {
+        // jittered: the pixel's jittered ray, colour stored; jittered_blend: blended with
+        // a = 1 / frame_num, 1 - a (sched_common.h:480-540)
+        sampler_pass p{ { 0.0f, 0.0f }, 1u, 0u, 1.0f, 0.0f };
+        if (ps->kind == VRH_SAMPLER_JITTERED_BLEND)
+        {
+            p.blend = 1u;
+            p.s = 1.0f / float(frame_num);
+            p.d = 1.0f - p.s;
+        }
+        return render_batch_impl(ctx, sc, rt, cam, 1, k, nullptr, frame_num, &p);
+    }
+    // ssaa<N> (sched_common.h:219-300, 640-720): colour 0, then every sample blended with 1 / N, 1
+    // in order -- one pass per sample on the context's stream
+    static const float off2[2][2] = { { -0.25f, -0.25f }, { 0.25f, 0.25f } };
+    static const float off4[4][2] = { { -0.125f, -0.375f }, { 0.375f, -0.125f }, { 0.125f, 0.375f }, { -0.375f, 0.125f } };
+    static const float off8[8][2] = { { -0.125f, -0.4375f }, { 0.375f, -0.3125f }, { -0.375f, -0.1875f }, { 0.125f, -0.0625f },
+                                      { -0.125f, 0.0625f }, { 0.375f, 0.1825f }, { -0.375f, 0.3125f }, { 0.125f, 0.4375f } };
+    VRH_CHECK(ps->count == 2 || ps->count == 4 || ps->count == 8, "vrh_render_sampled: ssaa takes 2, 4 or 8 samples");
+    const float (*tab)[2] = ps->count == 2 ? off2 : ps->count == 4 ? off4 : off8;
+    for (uint32_t i = 0; i < ps->count; ++i)
+    {
+        sampler_pass p{ { tab[i][0], tab[i][1] }, 0u, i == 0 ? 2u : 1u, 1.0f / float(ps->count), 1.0f };
+        const int rc = render_batch_impl(ctx, sc, rt, cam, 1, k, nullptr, frame_num, &p);
+        if (rc) return rc;
+    }
+    return VRH_OK;
+}
+
+namespace {
+int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_camera* cams, uint32_t num_frames,
+                      const vrh_kernel_desc* k, const vrh_shard* shard, uint32_t frame_num, const sampler_pass* sp)
 {
     VRH_CHECK(ctx && sc && rt && cams && k, "vrh_render: null argument");
     VRH_CHECK(rt->ctx == ctx && sc->ctx == ctx, "vrh_render: scene / render target of another context");
@@ -872,6 +932,12 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     // and was removed)
     lc.sched = 0;
     if (list) lc.sched = 2;    // BVH lists: the step loop with the list merge
+    if (sp)
+    {
+        // a pixel-sampler pass runs its own instance (the plain ones keep their code and registers)
+        if (list || lc.count) { set_error("vrh_render_sampled: pixel samplers take a single BVH and no test counting"); return VRH_ERR_UNSUPPORTED; }
+        lc.sched = 6;
+    }
     // frames in flight on the step loop (primary / AO, uncounted): the BATCH instantiation
     if (lc.sched == 0 && num_frames > 1 && !lc.count && lc.epi == 0 && !hmask) lc.sched = 3;
     // shading epilogues: no VGPR cap (their lane state spills at 6 waves/SIMD; measured faster at 4,
@@ -879,6 +945,7 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     // 4-6 % faster than 6 with 18 spilled VGPRs); primary visibility: 6 (profiles/r01_ab_waves/);
     // BVH lists run at these defaults
     lc.occ = ctx->opt_occ ? ctx->opt_occ : lc.epi ? 1 : lc.ao ? 5 : 6;
+    if (sp) lc.occ = lc.ao ? 5 : 6;                    // the sampler instances exist at the defaults
     if (list) lc.occ = ao ? 5 : 6;
     // auto: the LDS part of the stack shrinks (in steps of 4 entries) while LDS, not registers,
     // limits the waves per CU -- a deep BVH (hf10M: depth 26) then keeps the register-bound
@@ -964,6 +1031,11 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     p.width = cam->width; p.height = cam->height;
     p.samples = ao ? k->samples : 0; p.radius = k->radius; p.eps = k->eps;
     std::memcpy(p.bg, k->bg, 16);
+    if (sp)
+    {
+        p.px_off[0] = sp->off[0]; p.px_off[1] = sp->off[1];
+        p.jitter = sp->jitter; p.blend = sp->blend; p.blend_s = sp->s; p.blend_d = sp->d;
+    }
     p.shard_index = sh.index; p.shard_count = sh.count; p.packed = sh.packed ? 1u : 0u;
     p.tiles_x = (cam->width + 7u) / 8u;
     p.num_tiles = local_bands * p.tiles_x;        // a band is one row of 8x8 tiles
@@ -1056,6 +1128,7 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     ctx->have_frame = true;
     return VRH_OK;
 }
+} // namespace
 
 VRH_API int vrh_sync(vrh_ctx* ctx)
 {
