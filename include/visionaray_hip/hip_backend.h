@@ -37,6 +37,15 @@
 namespace visionaray
 {
 
+// the reference's pixel samplers (sched_common.h:34-50), declared here so that hip_sched can read
+// sched_params::pixel_sampler_type (defined by the reference's headers or by standalone.h)
+namespace pixel_sampler
+{
+template <size_t NumSamples> struct ssaa_type;
+struct jittered_type;
+struct jittered_blend_type;
+}
+
 // normal binding tags of make_kernel_params (tags.h:46-47), declared here so the shading kernel
 // factory can take them; the reference's (or standalone.h's) definitions complete them
 struct normals_per_face_binding;
@@ -76,6 +85,34 @@ struct user_kernels
 {
     static constexpr bool available = false;
 };
+
+// pixel sampler of a sched_params (sched_params::pixel_sampler_type; uniform when it has none) and
+// its vrh_pixel_sampler
+template <typename T> struct sampler_desc { static constexpr bool supported = false; static constexpr uint32_t kind = 0, count = 0; };
+template <size_t N> struct sampler_desc<pixel_sampler::ssaa_type<N>>
+{
+    static constexpr bool supported = N == 1 || N == 2 || N == 4 || N == 8;
+    static constexpr uint32_t kind = N == 1 ? VRH_SAMPLER_UNIFORM : VRH_SAMPLER_SSAA, count = uint32_t(N);
+};
+template <> struct sampler_desc<pixel_sampler::jittered_type>
+{
+    static constexpr bool supported = true;
+    static constexpr uint32_t kind = VRH_SAMPLER_JITTERED, count = 0;
+};
+template <> struct sampler_desc<pixel_sampler::jittered_blend_type>
+{
+    static constexpr bool supported = true;
+    static constexpr uint32_t kind = VRH_SAMPLER_JITTERED_BLEND, count = 0;
+};
+template <typename SP, typename = void> struct sampler_of { using type = pixel_sampler::ssaa_type<1>; };
+template <typename SP> struct sampler_of<SP, decltype((void)std::declval<typename SP::pixel_sampler_type*>())>
+{
+    using type = typename SP::pixel_sampler_type;
+};
+template <typename SP> constexpr bool uniform_sampler()
+{
+    return sampler_desc<typename sampler_of<SP>::type>::kind == VRH_SAMPLER_UNIFORM;
+}
 
 template <typename SP>
 void set_scissor(SP const& sp, vrh_camera& c)
@@ -638,6 +675,7 @@ public:
     template <typename SP>
     void frame(std::vector<hip_builtin_kernel> const& kernels, SP sparams, unsigned frame_num = 0)
     {
+        static_assert(hip_detail::uniform_sampler<SP>(), "hip_sched(group)::frame: render groups use pixel_sampler::uniform_type");
         if (!group_ || kernels.size() != group_->size())
             throw std::runtime_error("hip_sched::frame: one kernel per member of the render group");
         auto const& cam = sparams.cam;
@@ -695,6 +733,9 @@ private:
     template <typename SP>
     void frame_builtin(hip_builtin_kernel const& kernel, SP& sparams, unsigned frame_num, vrh_shard const* shard)
     {
+        using PS = hip_detail::sampler_desc<typename hip_detail::sampler_of<SP>::type>;
+        static_assert(PS::supported, "hip_sched: the pixel samplers are uniform_type, jittered_type, "
+                                     "jittered_blend_type and ssaa_type<2 / 4 / 8>");
         auto const& cam = sparams.cam;
         auto& rt = sparams.rt;
         float eye[3] = { cam.eye().x, cam.eye().y, cam.eye().z };
@@ -705,8 +746,17 @@ private:
                                           uint32_t(rt.height()), &c), "vrh_make_camera");
         hip_detail::set_scissor(sparams, c);
         rt.begin_frame();
-        hip_detail::check(vrh_render(ctx_->get(), kernel.scene, rt.handle(), &c, &kernel.desc, shard, frame_num),
-                          "vrh_render");
+        if constexpr (PS::kind == VRH_SAMPLER_UNIFORM)
+            hip_detail::check(vrh_render(ctx_->get(), kernel.scene, rt.handle(), &c, &kernel.desc, shard, frame_num),
+                              "vrh_render");
+        else
+        {
+            // jittered / jittered_blend / ssaa<N> (sched_common.h:160-300, 440-720)
+            if (shard) throw std::runtime_error("hip_sched::frame: pixel samplers other than uniform render the whole image");
+            const vrh_pixel_sampler ps{ PS::kind, PS::count };
+            hip_detail::check(vrh_render_sampled(ctx_->get(), kernel.scene, rt.handle(), &c, &kernel.desc, &ps, frame_num),
+                              "vrh_render_sampled");
+        }
         rt.end_frame();
     }
 

@@ -541,6 +541,8 @@ struct user_kernels<K, typename std::enable_if<!std::is_same<K, hip_builtin_kern
     template <typename SP>
     static void frame(hip_context& ctx, K const& kernel, SP& sparams, unsigned frame_num)
     {
+        static_assert(uniform_sampler<SP>(), "hip_sched: user kernels run with pixel_sampler::uniform_type (the "
+                                             "built-in primary / AO kernels take the jittered and ssaa samplers)");
         auto const& cam = sparams.cam;
         auto& rt = sparams.rt;
         user_frame f{};

@@ -266,9 +266,14 @@ private:
     float fovy_ = 0.785398f, aspect_ = 1.0f, z_near_ = 0.001f, z_far_ = 1000.0f;
 };
 
+// pixel samplers (sched_common.h:34-50)
 namespace pixel_sampler
 {
-struct uniform_type {};
+struct base_type {};
+template <size_t N> struct ssaa_type : base_type {};
+using uniform_type = ssaa_type<1>;
+struct jittered_type : base_type {};
+struct jittered_blend_type : jittered_type {};
 }
 
 // recti (math/rectangle.h): x, y, w, h; the scissor box cuda_sched reads (cuda_sched.inl:71)
@@ -281,18 +286,22 @@ struct recti
 
 // sched_params / make_sched_params (scheduler.h:52-75, 164-242): camera by value, rt by reference,
 // scissor box recti(0, 0, w, h) (scheduler.h:175)
-template <typename RT>
+template <typename RT, typename PxSamplerT = pixel_sampler::uniform_type>
 struct sched_params
 {
+    using rt_type = RT;
+    using pixel_sampler_type = PxSamplerT;
+
     camera cam;
     RT& rt;
     recti scissor_box;
 };
 
-template <typename RT>
-sched_params<RT> make_sched_params(pixel_sampler::uniform_type, camera const& cam, RT& rt)
+template <typename PxSamplerT, typename RT,
+          typename = typename std::enable_if<std::is_base_of<pixel_sampler::base_type, PxSamplerT>::value>::type>
+sched_params<RT, PxSamplerT> make_sched_params(PxSamplerT, camera const& cam, RT& rt)
 {
-    return sched_params<RT>{ cam, rt, recti(0, 0, int(rt.width()), int(rt.height())) };
+    return sched_params<RT, PxSamplerT>{ cam, rt, recti(0, 0, int(rt.width()), int(rt.height())) };
 }
 
 template <typename RT>

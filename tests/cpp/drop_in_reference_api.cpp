@@ -125,7 +125,25 @@ int main(int argc, char** argv)
             mask_hashes[2] = fnv1a(mo.data(), n);
             mask_hashes[3] = fnv1a(mc.data(), n * 16);
         }
-        printf("{\"mask_primid_hash\":\"%016llx\",\"mask_t_hash\":\"%016llx\",\"mask_occ_hash\":\"%016llx\","
+        // the reference AO example's own sampler (ao/main.cpp: pixel_sampler::jittered_blend_type) and
+        // 4x SSAA, frame 3, blended onto a target cleared to (0.25, 0.5, 0.75, 1)
+        unsigned long long sampler_hashes[2] = { 0, 0 };
+        {
+            hip_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> srt;
+            srt.resize(W, H);
+            std::vector<float> sc(4 * n);
+            srt.clear_color_buffer(vec4(0.25f, 0.5f, 0.75f, 1.0f));
+            sched.frame(kern, make_sched_params(pixel_sampler::jittered_blend_type{}, cam, srt), 3);
+            srt.download(sc.data(), nullptr, nullptr, nullptr);
+            sampler_hashes[0] = fnv1a(sc.data(), n * 16);
+            srt.clear_color_buffer(vec4(0.25f, 0.5f, 0.75f, 1.0f));
+            sched.frame(kern, make_sched_params(pixel_sampler::ssaa_type<4>{}, cam, srt), 3);
+            srt.download(sc.data(), nullptr, nullptr, nullptr);
+            sampler_hashes[1] = fnv1a(sc.data(), n * 16);
+        }
+        printf("{\"sampler_jittered_blend_color_hash\":\"%016llx\",\"sampler_ssaa4_color_hash\":\"%016llx\",",
+               sampler_hashes[0], sampler_hashes[1]);
+        printf("\"mask_primid_hash\":\"%016llx\",\"mask_t_hash\":\"%016llx\",\"mask_occ_hash\":\"%016llx\","
                "\"mask_color_hash\":\"%016llx\",", mask_hashes[0], mask_hashes[1], mask_hashes[2], mask_hashes[3]);
         printf("\"grid\":%u,\"W\":%u,\"H\":%u,\"rays\":%llu,\"primid_hash\":\"%016llx\",\"t_hash\":\"%016llx\","
                "\"occ_hash\":\"%016llx\",\"color_hash\":\"%016llx\",\"batch_ok\":%s}\n", grid, W, H, rays,

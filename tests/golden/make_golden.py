@@ -266,6 +266,8 @@ SAMPLER_CASES = [(f"sampler_{k}_hf64_ao", "hf64", "ao", k, 3, 160, 90)
                  for k in ("uniform", "jittered", "jittered_blend", "ssaa2", "ssaa4", "ssaa8")] + [
     ("sampler_ssaa8_sph5000_primary", "sph5000", "primary", "ssaa8", 2, 128, 72),
     ("sampler_jittered_blend_sph5000_primary", "sph5000", "primary", "jittered_blend", 2, 128, 72),
+    ("sampler_jittered_blend_hf200_ao", "hf200", "ao", "jittered_blend", 3, 320, 180),
+    ("sampler_ssaa4_hf200_ao", "hf200", "ao", "ssaa4", 3, 320, 180),
 ]
 
 

@@ -72,6 +72,9 @@ def test_reference_api_program_on_hip_backend(golden):
     for k in ("primid_hash", "t_hash", "occ_hash", "color_hash"):
         assert out[k] == g[k], k
     assert out["batch_ok"], "hip_sched::frames: a frame of the batch differs from its own frame()"
+    # make_sched_params(pixel_sampler::jittered_blend_type / ssaa_type<4>, cam, rt): the reference harness's frames
+    assert out["sampler_jittered_blend_color_hash"] == golden["sampler_jittered_blend_hf200_ao"]["color_hash"]
+    assert out["sampler_ssaa4_color_hash"] == golden["sampler_ssaa4_hf200_ao"]["color_hash"]
 
 
 @pytest.mark.gpu
