@@ -373,6 +373,11 @@ private:
 template <auto ColorFormat, auto DepthFormat>
 class hip_buffer_rt
 {
+    // the formats of the measured configurations; other formats are a
+    // compile error rather than a silent RGBA32F target (values as in pixel_format.h:15-60)
+    static_assert(int(ColorFormat) == 12, "hip_buffer_rt: colour format PF_RGBA32F");
+    static_assert(int(DepthFormat) == 0, "hip_buffer_rt: depth format PF_UNSPECIFIED (no depth buffer)");
+
 public:
     struct ref_type          // render_target_ref analogue: raw device pointers + size
     {

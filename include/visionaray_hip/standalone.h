@@ -29,7 +29,7 @@
 namespace visionaray
 {
 
-enum pixel_format { PF_UNSPECIFIED = 0, PF_RGBA32F = 1 };
+enum pixel_format { PF_UNSPECIFIED = 0, PF_RGBA32F = 12 };   // the reference's values (pixel_format.h:15-60)
 
 //-------------------------------------------------------------------------------------------------
 // vector<N, T> (math/vector.h): vec2 / vec3 / vec4 with the reference's member names.  vec3 is
