@@ -109,6 +109,11 @@ template <typename SP> struct sampler_of<SP, decltype((void)std::declval<typenam
 {
     using type = typename SP::pixel_sampler_type;
 };
+// sched_params with an intersector (scheduler.h:33-45, 177-193)
+template <typename SP, typename = void> struct has_sched_intersector : std::false_type {};
+template <typename SP> struct has_sched_intersector<SP, decltype((void)std::declval<typename SP::has_intersector*>())>
+    : std::true_type {};
+
 template <typename SP> constexpr bool uniform_sampler()
 {
     return sampler_desc<typename sampler_of<SP>::type>::kind == VRH_SAMPLER_UNIFORM;
@@ -741,6 +746,9 @@ private:
         using PS = hip_detail::sampler_desc<typename hip_detail::sampler_of<SP>::type>;
         static_assert(PS::supported, "hip_sched: the pixel samplers are uniform_type, jittered_type, "
                                      "jittered_blend_type and ssaa_type<2 / 4 / 8>");
+        static_assert(!hip_detail::has_sched_intersector<SP>::value,
+                      "hip_sched: a built-in kernel takes its intersector as data (with_intersector(kernel, "
+                      "hip_hit_mask)); sched_params with an intersector are for user kernels (hip_kernels.h)");
         auto const& cam = sparams.cam;
         auto& rt = sparams.rt;
         float eye[3] = { cam.eye().x, cam.eye().y, cam.eye().z };

@@ -506,6 +506,22 @@ __device__ inline auto invoke_kernel(K& kernel, basic_ray<float> const& r, S&, u
     return kernel(r, x, y);
 }
 
+// sched_params with an intersector (scheduler.h:33-45, 177-193: make_sched_params(sampler, cam, rt,
+// isect)): the kernel is called as kernel(isect, r ...) (sched_common.h:786-818
+// call_kernel_with_intersector); the intersector is copied into the launch (it holds device pointers)
+template <typename K, typename I>
+struct call_with_intersector
+{
+    K kernel;
+    I isect;
+
+    template <typename... A>
+    __device__ auto operator()(A&&... a) -> decltype(kernel(isect, std::forward<A>(a)...))
+    {
+        return kernel(isect, std::forward<A>(a)...);
+    }
+};
+
 template <typename T, typename = void> struct has_depth : std::false_type {};
 template <typename T> struct has_depth<T, decltype((void)std::declval<T>().depth)> : std::true_type {};
 
@@ -575,7 +591,15 @@ struct user_kernels<K, typename std::enable_if<!std::is_same<K, hip_builtin_kern
         {
             const dim3 grid((f.width + 7u) / 8u, (f.height + 7u) / 8u);
             const size_t lds = size_t(64) * VRH_USER_STACK * sizeof(uint32_t);
-            hipLaunchKernelGGL(user_render<K>, grid, dim3(8, 8), lds, static_cast<hipStream_t>(stream), kernel, f);
+            if constexpr (has_sched_intersector<SP>::value)
+            {
+                using I = typename std::decay<decltype(sparams.intersector)>::type;
+                using C = call_with_intersector<K, I>;
+                hipLaunchKernelGGL(user_render<C>, grid, dim3(8, 8), lds, static_cast<hipStream_t>(stream),
+                                   C{ kernel, sparams.intersector }, f);
+            }
+            else
+                hipLaunchKernelGGL(user_render<K>, grid, dim3(8, 8), lds, static_cast<hipStream_t>(stream), kernel, f);
             e = hipGetLastError();
         }
         (void)hipSetDevice(prev);        // the caller's current device is left as it was

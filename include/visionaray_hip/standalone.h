@@ -304,6 +304,22 @@ sched_params<RT, PxSamplerT> make_sched_params(PxSamplerT, camera const& cam, RT
     return sched_params<RT, PxSamplerT>{ cam, rt, recti(0, 0, int(rt.width()), int(rt.height())) };
 }
 
+// with an intersector (scheduler.h:33-45, 177-193): kernels are called as kernel(isect, r ...)
+template <typename RT, typename PxSamplerT, typename Intersector>
+struct sched_params_isect : sched_params<RT, PxSamplerT>
+{
+    using has_intersector = void;
+    Intersector& intersector;
+};
+
+template <typename PxSamplerT, typename RT, typename Intersector,
+          typename = typename std::enable_if<std::is_base_of<pixel_sampler::base_type, PxSamplerT>::value>::type>
+sched_params_isect<RT, PxSamplerT, Intersector> make_sched_params(PxSamplerT, camera const& cam, RT& rt, Intersector& isect)
+{
+    return sched_params_isect<RT, PxSamplerT, Intersector>{ { cam, rt, recti(0, 0, int(rt.width()), int(rt.height())) },
+                                                            isect };
+}
+
 template <typename RT>
 sched_params<RT> make_sched_params(camera const& cam, RT& rt)
 {

@@ -8,6 +8,8 @@
 //                                                               harness's "mask" intersector)
 //   user_kernels heart <grid> <W> <H> <outdir>                  closest hit with the intersector
 //                                                               example's procedural heart cut-out
+//   user_kernels isect <grid> <W> <H> <outdir> <mask.bin> <n>   the mask case with the intersector in the
+//                                                                sched params: kernel(isect, r, x, y)
 //   user_kernels list  <grid> <W> <H> <outdir> x0 y0 x1 y1 f    the AO kernel over a list of two BVHs
 //                                                               (prim_id parity split), scissor box,
 //                                                               frame f (the harness's "list" mode)
@@ -137,35 +139,42 @@ struct ref_list
 // primary closest hit + 8 AO samples with intersector `isect` over the BVH list `refs`
 // (oracle/ref_harness.cpp run_golden / run_list)
 template <typename Isect>
+__device__ static result_record<float> ao_body(ref_list refs, vec3 const* normals, Isect& isect, unsigned W,
+                                              unsigned frame_num, ray r, unsigned x, unsigned y)
+{
+    result_record<float> result;
+    const vec4 bg(0.1f, 0.2f, 0.3f, 1.0f);
+    result.color = vec4(__uint_as_float(0xFFFFFFFFu), -1.0f, 0.0f, bg.w);
+    hip_bvh_ref const* begin = refs.r;
+    hip_bvh_ref const* end = refs.r + refs.n;
+    auto hr = closest_hit(r, begin, end, isect);
+    result.hit = hr.hit;
+    if (!hr.hit) return result;
+    hr.isect_pos = r.ori + r.dir * hr.t;
+    float clr = 1.0f;
+    vec3 n = get_normal(normals, hr);
+    vec3 uu, vv, w = n;
+    make_orthonormal_basis(uu, vv, w);
+    unsigned mask = 0;
+    const unsigned p = y * W + x;
+    for (unsigned smp = 0; smp < 8; ++smp)
+    {
+        vec3 s = hip_ao_sample(p, smp, frame_num);
+        auto dir = normalize(s.x * uu + s.y * vv + s.z * w);
+        ray ao(hr.isect_pos + dir * 1E-3f, dir);
+        auto ar = any_hit(ao, begin, end, 0.1f, isect);
+        if (ar.hit) { clr = clr - 1.0f / 8; mask |= 1u << smp; }
+    }
+    result.color = vec4(__uint_as_float(unsigned(hr.prim_id)), hr.t, __uint_as_float(mask), clr);
+    return result;
+}
+
+template <typename Isect>
 static auto ao_kernel(ref_list refs, vec3 const* normals, Isect isect, unsigned W, unsigned frame_num)
 {
     return [=] __device__ (ray r, unsigned x, unsigned y) mutable -> result_record<float>
     {
-        result_record<float> result;
-        const vec4 bg(0.1f, 0.2f, 0.3f, 1.0f);
-        result.color = vec4(__uint_as_float(0xFFFFFFFFu), -1.0f, 0.0f, bg.w);
-        hip_bvh_ref const* begin = refs.r;
-        hip_bvh_ref const* end = refs.r + refs.n;
-        auto hr = closest_hit(r, begin, end, isect);
-        result.hit = hr.hit;
-        if (!hr.hit) return result;
-        hr.isect_pos = r.ori + r.dir * hr.t;
-        float clr = 1.0f;
-        vec3 n = get_normal(normals, hr);
-        vec3 uu, vv, w = n;
-        make_orthonormal_basis(uu, vv, w);
-        unsigned mask = 0;
-        const unsigned p = y * W + x;
-        for (unsigned smp = 0; smp < 8; ++smp)
-        {
-            vec3 s = hip_ao_sample(p, smp, frame_num);
-            auto dir = normalize(s.x * uu + s.y * vv + s.z * w);
-            ray ao(hr.isect_pos + dir * 1E-3f, dir);
-            auto ar = any_hit(ao, begin, end, 0.1f, isect);
-            if (ar.hit) { clr = clr - 1.0f / 8; mask |= 1u << smp; }
-        }
-        result.color = vec4(__uint_as_float(unsigned(hr.prim_id)), hr.t, __uint_as_float(mask), clr);
-        return result;
+        return ao_body(refs, normals, isect, W, frame_num, r, x, y);
     };
 }
 
@@ -181,6 +190,15 @@ static auto primary_kernel(hip_bvh_ref ref, Isect isect)
         if (hr.hit) result.color = vec4(__uint_as_float(unsigned(hr.prim_id)), hr.t, 0.0f, 1.0f);
         result.hit = hr.hit;
         return result;
+    };
+}
+
+// the AO kernel with the intersector taken from the sched params: kernel(isect, r, x, y)
+static auto ao_kernel_isect(ref_list refs, vec3 const* normals, unsigned W, unsigned frame_num)
+{
+    return [=] __device__ (byte_mask_intersector& isect, ray r, unsigned x, unsigned y) -> result_record<float>
+    {
+        return ao_body(refs, normals, isect, W, frame_num, r, x, y);
     };
 }
 
@@ -255,6 +273,24 @@ int main(int argc, char** argv)
             isect.w = n;
             isect.h = n;
             sched.frame(ao_kernel(one, dnormals, isect, W, 0u), sparams);
+        }
+        else if (mode == "isect")
+        {
+            // the mask intersector handed over in the sched params (make_sched_params(sampler, cam,
+            // rt, isect), scheduler.h:177-193): the kernel is called as kernel(isect, r, x, y)
+            if (argc < 8) return 2;
+            const int n = atoi(argv[7]);
+            std::vector<uint8_t> mask(size_t(n) * n);
+            FILE* f = fopen(argv[6], "rb");
+            if (!f || fread(mask.data(), 1, mask.size(), f) != mask.size()) return 3;
+            fclose(f);
+            byte_mask_intersector isect;
+            isect.tex_coords = dtc;
+            isect.mask = to_device(mask);
+            isect.w = n;
+            isect.h = n;
+            auto isparams = make_sched_params(pixel_sampler::uniform_type{}, cam, rt, isect);
+            sched.frame(ao_kernel_isect(one, dnormals, W, 0u), isparams);
         }
         else if (mode == "list")
         {

@@ -10,7 +10,8 @@ tests/cpp/user_kernels.hip (built by visionaray_amd/Makefile `cpp_tests`) render
   * heart -- closest hit with the intersector example's procedural cut-out, written in the example's
              width-generic style (unpack / simd::mask_type_t / Mask(bool[N]) / pow), against the
              reference harness's "heart" mode (fixtures: heart_*);
-  * list  -- the AO kernel over a list of two BVH refs with a scissor box (fixtures: list_*).
+  * list  -- the AO kernel over a list of two BVH refs with a scissor box (fixtures: list_*);
+  * isect -- the mask case with the intersector passed in the sched params (kernel(isect, r, x, y)).
 """
 import os
 import subprocess
@@ -60,6 +61,22 @@ def test_user_mask_intersector_matches_reference(tmp_path, golden, oracle_mod, c
         assert np.array_equal(got[k], ref[k]), f"{k}: {int((got[k] != ref[k]).sum())} pixels differ"
     for k in ("t", "color"):
         assert np.array_equal(got[k].view(np.uint32), ref[k].view(np.uint32)), k
+    _check_hashes(oracle_mod, got, g, [("prim_id", "primid_hash"), ("t", "t_hash"), ("occ", "occ_hash"),
+                                       ("color", "color_hash")])
+
+
+@pytest.mark.gpu
+def test_user_kernel_with_intersector_in_sched_params(tmp_path, golden, oracle_mod):
+    """make_sched_params(sampler, cam, rt, isect) (scheduler.h:177-193): hip_sched calls the kernel as
+    kernel(isect, r, x, y) (sched_common.h:786-818) -- the mask frames again."""
+    case = "mask_hf200_320x180"
+    g = golden[case]
+    ref = np.load(os.path.join(GOLDEN, case + ".npz"))
+    mpath = tmp_path / "mask.bin"
+    ref["mask"].astype(np.uint8).tofile(mpath)
+    got = _run(tmp_path, "isect", g["scene"], g["W"], g["H"], mpath, g["mask_size"])
+    for k in ("prim_id", "occ"):
+        assert np.array_equal(got[k], ref[k]), f"{k}: {int((got[k] != ref[k]).sum())} pixels differ"
     _check_hashes(oracle_mod, got, g, [("prim_id", "primid_hash"), ("t", "t_hash"), ("occ", "occ_hash"),
                                        ("color", "color_hash")])
 
