@@ -525,25 +525,80 @@ struct call_with_intersector
 template <typename T, typename = void> struct has_depth : std::false_type {};
 template <typename T> struct has_depth<T, decltype((void)std::declval<T>().depth)> : std::true_type {};
 
-template <typename K>
+template <typename K, uint32_t SK = VRH_SAMPLER_UNIFORM, uint32_t SN = 1>
 __global__ __launch_bounds__(64) void user_render(K kernel, user_frame f)
 {
     const uint32_t x = blockIdx.x * 8u + threadIdx.x;
     const uint32_t y = blockIdx.y * 8u + threadIdx.y;
     if (x < f.x0 || y < f.y0 || x >= f.x1 || y >= f.y1) return;
-    // sched_common.h:130-150 make_primary_ray_impl (uniform pixel sampler), as the built-in kernels
-    const float u = 2.0f * ((float)x + 0.5f) / (float)f.width - 1.0f;
-    const float v = 2.0f * ((float)y + 0.5f) / (float)f.height - 1.0f;
     const vec3 cu(f.cam.cam_u[0], f.cam.cam_u[1], f.cam.cam_u[2]);
     const vec3 cv(f.cam.cam_v[0], f.cam.cam_v[1], f.cam.cam_v[2]);
     const vec3 cw(f.cam.cam_w[0], f.cam.cam_w[1], f.cam.cam_w[2]);
-    basic_ray<float> r(vec3(f.cam.eye[0], f.cam.eye[1], f.cam.eye[2]), normalize((cu * u + cv * v) + cw));
+    const vec3 eye(f.cam.eye[0], f.cam.eye[1], f.cam.eye[2]);
     hip_sampler samp(y * f.width + x, f.frame_num);
-    auto res = invoke_kernel(kernel, r, samp, x, y, 0);
     const size_t o = size_t(y) * f.width + x;
-    if (f.color) f.color[o] = make_float4(res.color.x, res.color.y, res.color.z, res.color.w);
-    if constexpr (has_depth<decltype(res)>::value)
-        if (f.t) f.t[o] = res.depth;
+    if constexpr (SK == VRH_SAMPLER_UNIFORM)
+    {
+        // sched_common.h:130-150 make_primary_ray_impl (uniform pixel sampler), as the built-in kernels
+        const float u = 2.0f * ((float)x + 0.5f) / (float)f.width - 1.0f;
+        const float v = 2.0f * ((float)y + 0.5f) / (float)f.height - 1.0f;
+        basic_ray<float> r(eye, normalize((cu * u + cv * v) + cw));
+        auto res = invoke_kernel(kernel, r, samp, x, y, 0);
+        if (f.color) f.color[o] = make_float4(res.color.x, res.color.y, res.color.z, res.color.w);
+        if constexpr (has_depth<decltype(res)>::value)
+            if (f.t) f.t[o] = res.depth;
+    }
+    else
+    {
+        // the jittered / jittered_blend / ssaa<N> samplers (sched_common.h:196-300, 440-720), with the
+        // jitter draws and offset tables of vrh.h vrh_pixel_sampler
+        auto ray_at = [&](float ox, float oy)
+        {
+            const float u = 2.0f * (((float)x + ox) + 0.5f) / (float)f.width - 1.0f;
+            const float v = 2.0f * (((float)y + oy) + 0.5f) / (float)f.height - 1.0f;
+            return basic_ray<float>(eye, normalize((cu * u + cv * v) + cw));
+        };
+        if constexpr (SK == VRH_SAMPLER_SSAA)
+        {
+            constexpr float off2[2][2] = { { -0.25f, -0.25f }, { 0.25f, 0.25f } };
+            constexpr float off4[4][2] = { { -0.125f, -0.375f }, { 0.375f, -0.125f }, { 0.125f, 0.375f }, { -0.375f, 0.125f } };
+            constexpr float off8[8][2] = { { -0.125f, -0.4375f }, { 0.375f, -0.3125f }, { -0.375f, -0.1875f }, { 0.125f, -0.0625f },
+                                           { -0.125f, 0.0625f }, { 0.375f, 0.1825f }, { -0.375f, 0.3125f }, { 0.125f, 0.4375f } };
+            const float a = 1.0f / float(SN);
+            float4 d = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll 1
+            for (uint32_t i = 0; i < SN; ++i)
+            {
+                const float ox = SN == 2 ? off2[i][0] : SN == 4 ? off4[i][0] : off8[i][0];
+                const float oy = SN == 2 ? off2[i][1] : SN == 4 ? off4[i][1] : off8[i][1];
+                auto res = invoke_kernel(kernel, ray_at(ox, oy), samp, x, y, 0);
+                d = make_float4(res.color.x * a + d.x * 1.0f, res.color.y * a + d.y * 1.0f,
+                                res.color.z * a + d.z * 1.0f, res.color.w * a + d.w * 1.0f);
+                if constexpr (has_depth<decltype(res)>::value)
+                    if (f.t) f.t[o] = res.depth;
+            }
+            if (f.color) f.color[o] = d;
+        }
+        else
+        {
+            const uint32_t k = (y * f.width + x) * 2u + 0x632BE5ABu + f.frame_num * 0x68E31DA4u;
+            const float oy = vrh::dev::uniform01(k) - 0.5f, ox = vrh::dev::uniform01(k + 1u) - 0.5f;
+            auto res = invoke_kernel(kernel, ray_at(ox, oy), samp, x, y, 0);
+            float4 c = make_float4(res.color.x, res.color.y, res.color.z, res.color.w);
+            if constexpr (SK == VRH_SAMPLER_JITTERED_BLEND)
+            {
+                const float a = 1.0f / float(f.frame_num), b = 1.0f - a;
+                if (f.color)
+                {
+                    const float4 d = f.color[o];
+                    c = make_float4(c.x * a + d.x * b, c.y * a + d.y * b, c.z * a + d.z * b, c.w * a + d.w * b);
+                }
+            }
+            if (f.color) f.color[o] = c;
+            if constexpr (has_depth<decltype(res)>::value)
+                if (f.t) f.t[o] = res.depth;
+        }
+    }
 }
 } // hip_detail
 
@@ -557,8 +612,9 @@ struct user_kernels<K, typename std::enable_if<!std::is_same<K, hip_builtin_kern
     template <typename SP>
     static void frame(hip_context& ctx, K const& kernel, SP& sparams, unsigned frame_num)
     {
-        static_assert(uniform_sampler<SP>(), "hip_sched: user kernels run with pixel_sampler::uniform_type (the "
-                                             "built-in primary / AO kernels take the jittered and ssaa samplers)");
+        using PS = sampler_desc<typename sampler_of<SP>::type>;
+        static_assert(PS::supported, "hip_sched: the pixel samplers are uniform_type, jittered_type, "
+                                     "jittered_blend_type and ssaa_type<2 / 4 / 8>");
         auto const& cam = sparams.cam;
         auto& rt = sparams.rt;
         user_frame f{};
@@ -595,11 +651,12 @@ struct user_kernels<K, typename std::enable_if<!std::is_same<K, hip_builtin_kern
             {
                 using I = typename std::decay<decltype(sparams.intersector)>::type;
                 using C = call_with_intersector<K, I>;
-                hipLaunchKernelGGL(user_render<C>, grid, dim3(8, 8), lds, static_cast<hipStream_t>(stream),
-                                   C{ kernel, sparams.intersector }, f);
+                hipLaunchKernelGGL((user_render<C, PS::kind, PS::count>), grid, dim3(8, 8), lds,
+                                   static_cast<hipStream_t>(stream), C{ kernel, sparams.intersector }, f);
             }
             else
-                hipLaunchKernelGGL(user_render<K>, grid, dim3(8, 8), lds, static_cast<hipStream_t>(stream), kernel, f);
+                hipLaunchKernelGGL((user_render<K, PS::kind, PS::count>), grid, dim3(8, 8), lds,
+                                   static_cast<hipStream_t>(stream), kernel, f);
             e = hipGetLastError();
         }
         (void)hipSetDevice(prev);        // the caller's current device is left as it was

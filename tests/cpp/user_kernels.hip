@@ -10,6 +10,8 @@
 //                                                               example's procedural heart cut-out
 //   user_kernels isect <grid> <W> <H> <outdir> <mask.bin> <n>   the mask case with the intersector in the
 //                                                                sched params: kernel(isect, r, x, y)
+//   user_kernels sampler <grid> <W> <H> <outdir> <kind> <frame> the harness's sampler frames (jittered,
+//                                                                jittered_blend, ssaa2/4/8) with a user kernel
 //   user_kernels list  <grid> <W> <H> <outdir> x0 y0 x1 y1 f    the AO kernel over a list of two BVHs
 //                                                               (prim_id parity split), scissor box,
 //                                                               frame f (the harness's "list" mode)
@@ -193,6 +195,39 @@ static auto primary_kernel(hip_bvh_ref ref, Isect isect)
     };
 }
 
+// the reference harness's `sampler` kernel (oracle/ref_harness.cpp run_sampler_impl): bg on a miss,
+// (1 - k/8, 1 - k/8, 1 - k/8, 1) for k occluded AO samples on a hit; the last sample's prim id
+static auto sampler_kernel(ref_list refs, vec3 const* normals, uint32_t* pid, unsigned W, unsigned frame_num)
+{
+    return [=] __device__ (ray r, unsigned x, unsigned y) -> result_record<float>
+    {
+        result_record<float> result;
+        result.color = vec4(0.1f, 0.2f, 0.3f, 1.0f);
+        default_intersector isect;
+        hip_bvh_ref const* begin = refs.r;
+        hip_bvh_ref const* end = refs.r + refs.n;
+        auto hr = closest_hit(r, begin, end, isect);
+        result.hit = hr.hit;
+        const unsigned p = y * W + x;
+        pid[p] = hr.hit ? unsigned(hr.prim_id) : 0xFFFFFFFFu;
+        if (!hr.hit) return result;
+        hr.isect_pos = r.ori + r.dir * hr.t;
+        float clr = 1.0f;
+        vec3 n = get_normal(normals, hr);
+        vec3 uu, vv, w = n;
+        make_orthonormal_basis(uu, vv, w);
+        for (unsigned smp = 0; smp < 8; ++smp)
+        {
+            vec3 s = hip_ao_sample(p, smp, frame_num);
+            auto dir = normalize(s.x * uu + s.y * vv + s.z * w);
+            ray ao(hr.isect_pos + dir * 1E-3f, dir);
+            if (any_hit(ao, begin, end, 0.1f, isect).hit) clr = clr - 1.0f / 8;
+        }
+        result.color = vec4(clr, clr, clr, 1.0f);
+        return result;
+    };
+}
+
 // the AO kernel with the intersector taken from the sched params: kernel(isect, r, x, y)
 static auto ao_kernel_isect(ref_list refs, vec3 const* normals, unsigned W, unsigned frame_num)
 {
@@ -292,6 +327,26 @@ int main(int argc, char** argv)
             auto isparams = make_sched_params(pixel_sampler::uniform_type{}, cam, rt, isect);
             sched.frame(ao_kernel_isect(one, dnormals, W, 0u), isparams);
         }
+        else if (mode == "sampler")
+        {
+            // make_sched_params(pixel_sampler::<kind>{}, cam, rt) with a user kernel, frame `frame`, onto a
+            // target cleared to (0.25, 0.5, 0.75, 1): colour + the last sample's prim id
+            if (argc < 8) return 2;
+            const std::string kind = argv[6];
+            const unsigned frame_num = unsigned(strtoul(argv[7], nullptr, 10));
+            std::vector<uint32_t> hp(size_t(W) * H, 0xFFFFFFFFu);
+            uint32_t* dpid = to_device(hp);
+            auto k = sampler_kernel(one, dnormals, dpid, W, frame_num);
+            rt.clear_color_buffer(vec4(0.25f, 0.5f, 0.75f, 1.0f));
+            if (kind == "jittered") sched.frame(k, make_sched_params(pixel_sampler::jittered_type{}, cam, rt), frame_num);
+            else if (kind == "jittered_blend") sched.frame(k, make_sched_params(pixel_sampler::jittered_blend_type{}, cam, rt), frame_num);
+            else if (kind == "ssaa2") sched.frame(k, make_sched_params(pixel_sampler::ssaa_type<2>{}, cam, rt), frame_num);
+            else if (kind == "ssaa4") sched.frame(k, make_sched_params(pixel_sampler::ssaa_type<4>{}, cam, rt), frame_num);
+            else if (kind == "ssaa8") sched.frame(k, make_sched_params(pixel_sampler::ssaa_type<8>{}, cam, rt), frame_num);
+            else sched.frame(k, make_sched_params(pixel_sampler::uniform_type{}, cam, rt), frame_num);
+            if (hipMemcpy(hp.data(), dpid, hp.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return 4;
+            write_file(outdir + "/sampler_prim_id.bin", hp.data(), hp.size() * 4);
+        }
         else if (mode == "list")
         {
             // the harness's list mode: the triangles split by prim_id parity into two BVHs, closest_hit
@@ -321,6 +376,11 @@ int main(int argc, char** argv)
         const size_t npx = size_t(W) * H;
         std::vector<float> out(4 * npx);
         rt.download(out.data());
+        if (mode == "sampler")
+        {
+            write_file(outdir + "/sampler_color.bin", out.data(), out.size() * 4);    // RGBA32F as rendered
+            return 0;
+        }
         // decode the channels into the reference's four outputs
         std::vector<uint32_t> pid(npx);
         std::vector<float> t(npx), color(4 * npx);

@@ -66,6 +66,24 @@ def test_user_mask_intersector_matches_reference(tmp_path, golden, oracle_mod, c
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["jittered", "jittered_blend", "ssaa2", "ssaa4", "ssaa8"])
+def test_user_kernel_pixel_samplers_match_reference(tmp_path, golden, kind):
+    """make_sched_params(pixel_sampler::<kind>, cam, rt) with a user kernel: the reference harness's
+    sampler frames (colour blended onto the same initial target, the last sample's prim id)."""
+    case = f"sampler_{kind}_hf64_ao"
+    g = golden[case]
+    ref = np.load(os.path.join(GOLDEN, case + ".npz"))
+    out = tmp_path / "s"
+    out.mkdir()
+    subprocess.run([BIN, "sampler", str(GRID[g["scene"]]), str(g["W"]), str(g["H"]), str(out), kind, str(g["frame"])],
+                   check=True, capture_output=True, text=True, timeout=120)
+    pid = np.fromfile(out / "sampler_prim_id.bin", np.uint32)
+    color = np.fromfile(out / "sampler_color.bin", np.float32).reshape(-1, 4)
+    assert np.array_equal(pid, ref["prim_id"])
+    assert np.array_equal(color.view(np.uint32), ref["color"].view(np.uint32))
+
+
+@pytest.mark.gpu
 def test_user_kernel_with_intersector_in_sched_params(tmp_path, golden, oracle_mod):
     """make_sched_params(sampler, cam, rt, isect) (scheduler.h:177-193): hip_sched calls the kernel as
     kernel(isect, r, x, y) (sched_common.h:786-818) -- the mask frames again."""
