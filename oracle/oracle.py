@@ -64,7 +64,7 @@ _Scene._fields_ = [("nodes", C.c_void_p), ("indices", C.c_void_p), ("prims", C.c
 class _Camera(C.Structure):
     _fields_ = [("eye", C.c_float * 3), ("cam_u", C.c_float * 3), ("cam_v", C.c_float * 3),
                 ("cam_w", C.c_float * 3), ("width", C.c_int), ("height", C.c_int),
-                ("scissor", C.c_uint * 4)]
+                ("scissor", C.c_uint * 4), ("inv_view", C.c_void_p), ("inv_proj", C.c_void_p)]
 
 
 class _Kernel(C.Structure):
@@ -104,8 +104,9 @@ def lib():
                                        vp, vp, vp, vp, C.c_int]
         L.vo_render_pixels.restype = C.c_uint64
         L.vo_render_sampled.argtypes = [C.POINTER(_Scene), C.POINTER(_Camera), C.POINTER(_Kernel), C.c_int, C.c_int,
-                                        vp, vp, C.c_int]
+                                        vp, vp, vp, C.c_int]
         L.vo_render_sampled.restype = C.c_int
+        L.vo_inverse4.argtypes = [vp, vp]; L.vo_inverse4.restype = None
         L.vo_fnv1a.argtypes = [vp, sz, C.c_uint64]; L.vo_fnv1a.restype = C.c_uint64
         L.vo_vertex_normals.argtypes = [vp, sz, vp]; L.vo_vertex_normals.restype = None
         L.vo_render_multi.argtypes = [C.POINTER(_Scene), C.POINTER(_Camera), C.POINTER(_Kernel), vp, vp, vp, C.c_int]
@@ -274,15 +275,30 @@ def render(scene, cam, mode=VO_MODE_AO, rows=None, threads=0, **kw):
     return out
 
 
-def render_sampled(scene, cam, sampler, init=(0.25, 0.5, 0.75, 1.0), mode=VO_MODE_AO, threads=0, **kw):
+def inverse4(m):
+    """matrix4.inl:209-244 inverse of a column-major 4x4 float matrix (16 floats)."""
+    m = np.ascontiguousarray(m, np.float32).reshape(16)
+    out = np.zeros(16, np.float32)
+    lib().vo_inverse4(_p(m), _p(out))
+    return out
+
+
+def render_sampled(scene, cam, sampler, init=(0.25, 0.5, 0.75, 1.0), mode=VO_MODE_AO, threads=0, matrices=None,
+                   **kw):
     """A frame through one of the reference's pixel samplers (SAMPLERS: uniform, jittered,
-    jittered_blend, ssaa2/4/8) onto a target filled with `init`: colour + the last sample's prim id."""
+    jittered_blend, ssaa2/4/8) onto a target filled with `init`: colour + the last sample's prim id.
+    matrices=(view, proj): the camera as matrices (column-major 4x4), inverted as the scheduler does."""
     _, _, _, _, W, H = cam
     kind, count = SAMPLERS[sampler]
-    out = {"color": np.tile(np.asarray(init, np.float32), (H * W, 1)), "prim_id": np.full(H * W, 0xFFFFFFFF, np.uint32)}
+    out = {"color": np.tile(np.asarray(init, np.float32), (H * W, 1)), "prim_id": np.full(H * W, 0xFFFFFFFF, np.uint32),
+           "t": np.full(H * W, -1.0, np.float32)}
     s, c, k = _structs(scene, cam, mode, **kw)
+    if matrices is not None:
+        iv, ip = inverse4(matrices[0]), inverse4(matrices[1])
+        c.inv_view, c.inv_proj = _p(iv).value, _p(ip).value
+        render_sampled.keep = (iv, ip)
     rc = lib().vo_render_sampled(C.byref(s), C.byref(c), C.byref(k), kind, count, _p(out["color"]), _p(out["prim_id"]),
-                                 threads)
+                                 _p(out["t"]), threads)
     if rc != 0:
         raise ValueError("render_sampled: bad sampler")
     return out

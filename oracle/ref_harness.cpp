@@ -904,6 +904,7 @@ static int run_sampler_impl(scene_desc const& d, aligned_vector<P>& prims, std::
     const vec4 init(0.25f, 0.5f, 0.75f, 1.0f);
     size_t npx = size_t(W) * H;
     std::vector<uint32_t> prim_id(npx, 0xFFFFFFFFu);    // the last sub-sample's hit
+    std::vector<float> tval(npx, -1.0f);
     std::vector<vec4> color(npx, init);
     render_target_ref<PF_RGBA32F> rt_ref(color.data(), nullptr, size_t(W), size_t(H));
 
@@ -915,6 +916,7 @@ static int run_sampler_impl(scene_desc const& d, aligned_vector<P>& prims, std::
         result.hit = hr.hit;
         size_t p = size_t(y) * W + x;
         prim_id[p] = hr.hit ? hr.prim_id : 0xFFFFFFFFu;
+        tval[p] = hr.hit ? hr.t : -1.0f;
         if (!hr.hit) return result;
         if (!do_ao) { result.color = vec4(1.0f); return result; }
         hr.isect_pos = r.ori + r.dir * hr.t;
@@ -947,6 +949,7 @@ static int run_sampler_impl(scene_desc const& d, aligned_vector<P>& prims, std::
         }
 
     write_file(outdir + "/prim_id.bin", prim_id.data(), npx * 4);
+    write_file(outdir + "/t.bin", tval.data(), npx * 4);
     write_file(outdir + "/color.bin", color.data(), npx * 16);
     fnv hp, hc;
     for (size_t p = 0; p < npx; ++p) hp.u32(prim_id[p]);
@@ -958,12 +961,27 @@ static int run_sampler_impl(scene_desc const& d, aligned_vector<P>& prims, std::
 
 template <typename P>
 static int run_sampler(scene_desc const& d, aligned_vector<P>& prims, std::vector<vec3> const& normals,
-                       std::string const& outdir, int W, int H, bool do_ao, std::string const& kind, uint32_t frame_num)
+                       std::string const& outdir, int W, int H, bool do_ao, std::string const& kind, uint32_t frame_num,
+                       bool matrices = false)
 {
+    // matrices: the camera given as view / projection matrices (sched_params with MT, scheduler.h:77-95),
+    // rays from make_primary_ray_impl's matrix form (sched_common.h:152-176) with the inverses the
+    // scheduler computes (cuda_sched.inl:228-235, matrix4.inl:209-244); the matrices are written out
+    camera mcam = make_camera(d, W, H);
+    const mat4 view = mcam.get_view_matrix(), proj = mcam.get_proj_matrix();
+    const mat4 inv_view = inverse(view), inv_proj = inverse(proj);
+    if (matrices)
+    {
+        write_file(outdir + "/view.bin", &view, sizeof(view));
+        write_file(outdir + "/proj.bin", &proj, sizeof(proj));
+    }
     auto rays_of = [&](auto st)
     {
         return [=](det_sampler& samp, unsigned x, unsigned y, vec3 eye, vec3 cu, vec3 cv, vec3 cw)
         {
+            if (matrices)
+                return visionaray::detail::make_primary_rays(ray{}, st, samp, x, y, size_t(W), size_t(H), view, inv_view,
+                                                             proj, inv_proj);
             return visionaray::detail::make_primary_rays(ray{}, st, samp, x, y, size_t(W), size_t(H), eye, cu, cv, cw);
         };
     };
@@ -1110,16 +1128,18 @@ int main(int argc, char** argv)
     }
     if (mode == "sampler")
     {
-        // sampler <scene> <outdir> <uniform|jittered|jittered_blend|ssaa2|ssaa4|ssaa8> <primary|ao> <frame> [W H]
+        // sampler <scene> <outdir> <uniform|jittered|jittered_blend|ssaa2|ssaa4|ssaa8>[+matrix] <primary|ao> <frame> [W H]
         if (argc < 7) return 2;
         std::string outdir = argv[3], kind = argv[4];
+        bool matrices = false;
+        if (kind.size() > 7 && kind.substr(kind.size() - 7) == "+matrix") { matrices = true; kind.resize(kind.size() - 7); }
         bool do_ao = std::string(argv[5]) == "ao" && !d.spheres;
         uint32_t frame_num = uint32_t(strtoul(argv[6], nullptr, 10));
         int W = argc > 8 ? atoi(argv[7]) : d.W;
         int H = argc > 8 ? atoi(argv[8]) : d.H;
         return with_scene(d, [&](auto& prims, std::vector<vec3> const& normals)
         {
-            return run_sampler(d, prims, normals, outdir, W, H, do_ao, kind, frame_num);
+            return run_sampler(d, prims, normals, outdir, W, H, do_ao, kind, frame_num, matrices);
         });
     }
     if (mode == "bench")

@@ -600,11 +600,68 @@ out:
 
 /* sched_common.h:130-150 make_primary_ray_impl (pinhole) for the pixel position (x + ox, y + oy):
  * the uniform sampler (:180-195) passes offset 0, jittered / ssaa (:196-300) their offsets */
+static inline float det2(float m00, float m01, float m10, float m11) { return m00 * m11 - m10 * m01; }  /* math.h:493-496 */
+
+void vo_inverse4(const float m[16], float out[16])
+{
+#define M(r, c) m[(c) * 4 + (r)]
+    float s0 = det2(M(0, 0), M(0, 1), M(1, 0), M(1, 1));
+    float s1 = det2(M(0, 0), M(0, 2), M(1, 0), M(1, 2));
+    float s2 = det2(M(0, 0), M(0, 3), M(1, 0), M(1, 3));
+    float s3 = det2(M(0, 1), M(0, 2), M(1, 1), M(1, 2));
+    float s4 = det2(M(0, 1), M(0, 3), M(1, 1), M(1, 3));
+    float s5 = det2(M(0, 2), M(0, 3), M(1, 2), M(1, 3));
+    float c5 = det2(M(2, 2), M(2, 3), M(3, 2), M(3, 3));
+    float c4 = det2(M(2, 1), M(2, 3), M(3, 1), M(3, 3));
+    float c3 = det2(M(2, 1), M(2, 2), M(3, 1), M(3, 2));
+    float c2 = det2(M(2, 0), M(2, 3), M(3, 0), M(3, 3));
+    float c1 = det2(M(2, 0), M(2, 2), M(3, 0), M(3, 2));
+    float c0 = det2(M(2, 0), M(2, 1), M(3, 0), M(3, 1));
+    float det = s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0;
+    const float r[16] = {   /* the constructor's arguments, column by column */
+        (+ M(1, 1) * c5 - M(1, 2) * c4 + M(1, 3) * c3) / det,
+        (- M(1, 0) * c5 + M(1, 2) * c2 + M(1, 3) * c1) / det,
+        (+ M(1, 0) * c4 - M(1, 1) * c2 + M(1, 3) * c0) / det,
+        (- M(1, 0) * c3 + M(1, 1) * c1 + M(1, 2) * c0) / det,
+        (- M(0, 1) * c5 + M(0, 2) * c4 - M(0, 3) * c3) / det,
+        (+ M(0, 0) * c5 - M(0, 2) * c2 + M(0, 3) * c1) / det,
+        (- M(0, 0) * c4 + M(0, 1) * c2 - M(0, 3) * c0) / det,
+        (+ M(0, 0) * c3 - M(0, 1) * c1 + M(0, 2) * c0) / det,
+        (+ M(3, 1) * s5 - M(3, 2) * s4 + M(3, 3) * s3) / det,
+        (- M(3, 0) * s5 + M(3, 2) * s2 - M(3, 3) * s1) / det,
+        (+ M(3, 0) * s4 - M(3, 1) * s2 + M(3, 3) * s0) / det,
+        (- M(3, 0) * s3 + M(3, 1) * s1 - M(3, 2) * s0) / det,
+        (- M(2, 1) * s5 + M(2, 2) * s4 - M(2, 3) * s3) / det,
+        (+ M(2, 0) * s5 - M(2, 2) * s2 + M(2, 3) * s1) / det,
+        (- M(2, 0) * s4 + M(2, 1) * s2 - M(2, 3) * s0) / det,
+        (+ M(2, 0) * s3 - M(2, 1) * s1 + M(2, 2) * s0) / det };
+#undef M
+    memcpy(out, r, sizeof(r));
+}
+
+/* matrix4.inl:171-181 matrix * vector (column-major m[c * 4 + r]) */
+static inline void mat_vec(const float* m, const float v[4], float out[4])
+{
+    for (int r = 0; r < 4; ++r)
+        out[r] = m[0 * 4 + r] * v[0] + m[1 * 4 + r] * v[1] + m[2 * 4 + r] * v[2] + m[3 * 4 + r] * v[3];
+}
+
 static inline void primary_ray_at(const vo_camera* cam, unsigned x, unsigned y, float ox, float oy, v3* ori, v3* dir)
 {
     float fx = (float)x + ox, fy = (float)y + oy;
     float u = 2.0f * (fx + 0.5f) / (float)cam->width - 1.0f;
     float v = 2.0f * (fy + 0.5f) / (float)cam->height - 1.0f;
+    if (cam->inv_view) {
+        /* sched_common.h:152-176: o = inv_view (inv_proj (u, v, -1, 1)), d likewise at z = +1;
+         * ori = o.xyz / o.w, dir = normalize(d.xyz / d.w - ori) */
+        const float pn[4] = { u, v, -1.0f, 1.0f }, pf[4] = { u, v, 1.0f, 1.0f };
+        float a[4], o[4], b[4], d[4];
+        mat_vec(cam->inv_proj, pn, a); mat_vec(cam->inv_view, a, o);
+        mat_vec(cam->inv_proj, pf, b); mat_vec(cam->inv_view, b, d);
+        *ori = mk(o[0] / o[3], o[1] / o[3], o[2] / o[3]);
+        *dir = normalize(sub(mk(d[0] / d[3], d[1] / d[3], d[2] / d[3]), *ori));
+        return;
+    }
     v3 cu = mk(cam->cam_u[0], cam->cam_u[1], cam->cam_u[2]);
     v3 cv = mk(cam->cam_v[0], cam->cam_v[1], cam->cam_v[2]);
     v3 cw = mk(cam->cam_w[0], cam->cam_w[1], cam->cam_w[2]);
@@ -945,7 +1002,7 @@ void vo_sampler_offsets(int kind, int count, unsigned x, unsigned y, unsigned wi
 }
 
 int vo_render_sampled(const vo_scene* s, const vo_camera* cam, const vo_kernel* k, int kind, int count,
-                      float* color, uint32_t* prim_id, int threads)
+                      float* color, uint32_t* prim_id, float* t, int threads)
 {
     if (kind == VO_SAMPLER_SSAA && count != 2 && count != 4 && count != 8) return -1;
     const int n = kind == VO_SAMPLER_SSAA ? count : 1;
@@ -966,6 +1023,7 @@ int vo_render_sampled(const vo_scene* s, const vo_camera* cam, const vo_kernel* 
                 vo_sampler_offsets(kind, count, (unsigned)x, (unsigned)y, (unsigned)W, k->frame_num, sub, &ox, &oy);
                 px_out o = shade_pixel_at(s, cam, k, (unsigned)x, (unsigned)y, ox, oy, NULL);
                 prim_id[p] = o.prim_id;
+                if (t) t[p] = o.t;
                 if (kind == VO_SAMPLER_UNIFORM || kind == VO_SAMPLER_JITTERED) {
                     memcpy(dst, o.color, 16);
                 } else {

@@ -109,7 +109,13 @@ typedef struct {
     /* scissor box as cuda_sched reads it (cuda_sched.inl:71): pixels x0 <= x < x1, y0 <= y < y1 are
      * rendered, the others not written; all zero = whole image */
     unsigned scissor[4];
+    /* the camera as matrices (sched_params with view / projection matrices, scheduler.h:77-95): the
+     * inverses (column-major 4x4, vo_inverse4); NULL = the pinhole basis above */
+    const float* inv_view;
+    const float* inv_proj;
 } vo_camera;
+/* matrix4.inl:209-244 inverse of a column-major 4x4 matrix, the reference's cofactor formula */
+void vo_inverse4(const float m[16], float out[16]);
 typedef struct {
     int   mode;                           /* VO_MODE_PRIMARY | VO_MODE_AO | VO_MODE_SIMPLE */
     int   samples;                        /* AO samples (8) */
@@ -151,7 +157,7 @@ enum { VO_SAMPLER_UNIFORM = 0, VO_SAMPLER_JITTERED = 1, VO_SAMPLER_JITTERED_BLEN
 void vo_sampler_offsets(int kind, int count, unsigned x, unsigned y, unsigned width, uint32_t frame_num,
                         int sub, float* ox, float* oy);
 int vo_render_sampled(const vo_scene* s, const vo_camera* cam, const vo_kernel* k, int kind, int count,
-                      float* color, uint32_t* prim_id, int threads);
+                      float* color, uint32_t* prim_id, float* t, int threads);
 uint64_t vo_render_pixels(const vo_scene* s, const vo_camera* cam, const vo_kernel* k,
                           const uint32_t* pixels, size_t npix,
                           float* color, uint32_t* prim_id, float* t, uint8_t* occ, int threads);

@@ -268,6 +268,11 @@ SAMPLER_CASES = [(f"sampler_{k}_hf64_ao", "hf64", "ao", k, 3, 160, 90)
     ("sampler_jittered_blend_sph5000_primary", "sph5000", "primary", "jittered_blend", 2, 128, 72),
     ("sampler_jittered_blend_hf200_ao", "hf200", "ao", "jittered_blend", 3, 320, 180),
     ("sampler_ssaa4_hf200_ao", "hf200", "ao", "ssaa4", 3, 320, 180),
+    # the camera as view / projection matrices (sched_params with MT), alone and with samplers
+    ("matrix_uniform_hf64_ao", "hf64", "ao", "uniform+matrix", 3, 160, 90),
+    ("matrix_ssaa4_hf64_ao", "hf64", "ao", "ssaa4+matrix", 3, 160, 90),
+    ("matrix_jittered_blend_sph5000_primary", "sph5000", "primary", "jittered_blend+matrix", 2, 128, 72),
+    ("matrix_uniform_hf200_ao", "hf200", "ao", "uniform+matrix", 0, 320, 180),
 ]
 
 
@@ -278,11 +283,17 @@ def sampler_cases(out):
                                capture_output=True, text=True)
             info = json.loads(r.stdout.strip().splitlines()[-1])
             pid = np.fromfile(os.path.join(d, "prim_id.bin"), np.uint32)
+            t = np.fromfile(os.path.join(d, "t.bin"), np.float32)
             color = np.fromfile(os.path.join(d, "color.bin"), np.float32).reshape(-1, 4)
-            rec = {"scene": scene, "kernel": kernel, "sampler": kind, "frame": frame, "W": W, "H": H,
-                   "primid_hash": fnv1a(pid), "color_hash": fnv1a(color)}
+            sampler, _, cam = kind.partition("+")
+            rec = {"scene": scene, "kernel": kernel, "sampler": sampler, "camera": cam or "pinhole", "frame": frame,
+                   "W": W, "H": H, "primid_hash": fnv1a(pid), "t_hash": fnv1a(t), "color_hash": fnv1a(color)}
             assert rec["primid_hash"] == info["primid_hash"] and rec["color_hash"] == info["color_hash"], case
-            np.savez_compressed(os.path.join(HERE, case + ".npz"), prim_id=pid, color=color)
+            arrays = {"prim_id": pid, "t": t, "color": color}
+            if cam == "matrix":
+                arrays["view"] = np.fromfile(os.path.join(d, "view.bin"), np.float32)
+                arrays["proj"] = np.fromfile(os.path.join(d, "proj.bin"), np.float32)
+            np.savez_compressed(os.path.join(HERE, case + ".npz"), **arrays)
             out[case] = rec
             print(case, rec["color_hash"], flush=True)
 

@@ -239,5 +239,27 @@ def test_oracle_pixel_samplers_match_reference(oracle_mod, golden, case):
     mode = O.VO_MODE_AO if g["kernel"] == "ao" else O.VO_MODE_PRIMARY
     out = O.render_sampled(sc, cam, g["sampler"], mode=mode, frame_num=g["frame"])
     assert np.array_equal(out["prim_id"], ref["prim_id"])
+    assert np.array_equal(out["t"].view(np.uint32), ref["t"].view(np.uint32))
     assert np.array_equal(out["color"].view(np.uint32), ref["color"].view(np.uint32))
     assert O.fnv1a(out["color"]) == g["color_hash"]
+
+
+MATRIX_CASES = ["matrix_uniform_hf64_ao", "matrix_ssaa4_hf64_ao", "matrix_jittered_blend_sph5000_primary",
+                "matrix_uniform_hf200_ao"]
+
+
+@pytest.mark.parametrize("case", MATRIX_CASES)
+def test_oracle_matrix_camera_matches_reference(oracle_mod, golden, case):
+    """The camera as view / projection matrices (sched_params with MT): the scheduler's inverse
+    (matrix4.inl:209-244) and make_primary_ray_impl's matrix form (sched_common.h:152-176), alone and
+    under the pixel samplers, against the harness (prim id, t, colour of every pixel)."""
+    O = oracle_mod
+    g = golden[case]
+    ref = np.load(os.path.join(HERE, "golden", case + ".npz"))
+    sc = O.make_scene(g["scene"])
+    cam = O.scene_camera(g["scene"], g["W"], g["H"])
+    mode = O.VO_MODE_AO if g["kernel"] == "ao" else O.VO_MODE_PRIMARY
+    out = O.render_sampled(sc, cam, g["sampler"], mode=mode, frame_num=g["frame"], matrices=(ref["view"], ref["proj"]))
+    assert np.array_equal(out["prim_id"], ref["prim_id"])
+    assert np.array_equal(out["t"].view(np.uint32), ref["t"].view(np.uint32))
+    assert np.array_equal(out["color"].view(np.uint32), ref["color"].view(np.uint32))
