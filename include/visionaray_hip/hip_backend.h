@@ -28,6 +28,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -112,6 +113,11 @@ template <typename SP> struct sampler_of<SP, decltype((void)std::declval<typenam
 // sched_params with an intersector (scheduler.h:33-45, 177-193)
 template <typename SP, typename = void> struct has_sched_intersector : std::false_type {};
 template <typename SP> struct has_sched_intersector<SP, decltype((void)std::declval<typename SP::has_intersector*>())>
+    : std::true_type {};
+
+// sched_params with view / projection matrices instead of a camera (scheduler.h:76-96, 197-231)
+template <typename SP, typename = void> struct has_camera_matrices : std::false_type {};
+template <typename SP> struct has_camera_matrices<SP, decltype((void)std::declval<typename SP::has_camera_matrices*>())>
     : std::true_type {};
 
 template <typename SP> constexpr bool uniform_sampler()
@@ -686,6 +692,7 @@ public:
     void frame(std::vector<hip_builtin_kernel> const& kernels, SP sparams, unsigned frame_num = 0)
     {
         static_assert(hip_detail::uniform_sampler<SP>(), "hip_sched(group)::frame: render groups use pixel_sampler::uniform_type");
+        static_assert(!hip_detail::has_camera_matrices<SP>::value, "hip_sched(group)::frame: render groups take a camera");
         if (!group_ || kernels.size() != group_->size())
             throw std::runtime_error("hip_sched::frame: one kernel per member of the render group");
         auto const& cam = sparams.cam;
@@ -749,28 +756,51 @@ private:
         static_assert(!hip_detail::has_sched_intersector<SP>::value,
                       "hip_sched: a built-in kernel takes its intersector as data (with_intersector(kernel, "
                       "hip_hit_mask)); sched_params with an intersector are for user kernels (hip_kernels.h)");
-        auto const& cam = sparams.cam;
         auto& rt = sparams.rt;
-        float eye[3] = { cam.eye().x, cam.eye().y, cam.eye().z };
-        float center[3] = { cam.center().x, cam.center().y, cam.center().z };
-        float up[3] = { cam.up().x, cam.up().y, cam.up().z };
-        vrh_camera c{};
-        hip_detail::check(vrh_make_camera(eye, center, up, cam.fovy(), cam.aspect(), uint32_t(rt.width()),
-                                          uint32_t(rt.height()), &c), "vrh_make_camera");
-        hip_detail::set_scissor(sparams, c);
-        rt.begin_frame();
-        if constexpr (PS::kind == VRH_SAMPLER_UNIFORM)
-            hip_detail::check(vrh_render(ctx_->get(), kernel.scene, rt.handle(), &c, &kernel.desc, shard, frame_num),
-                              "vrh_render");
+        if constexpr (hip_detail::has_camera_matrices<SP>::value)
+        {
+            // make_sched_params(sampler, view_matrix, proj_matrix, rt) (scheduler.h:197-212):
+            // the matrix primary rays (sched_common.h:152-176), whole image
+            if (shard) throw std::runtime_error("hip_sched::frame: camera matrices render the whole image");
+            vrh_view_camera vc{};
+            std::memcpy(vc.view, sparams.view_matrix.data(), sizeof(vc.view));
+            std::memcpy(vc.proj, sparams.proj_matrix.data(), sizeof(vc.proj));
+            vc.width = uint32_t(rt.width());
+            vc.height = uint32_t(rt.height());
+            vrh_camera c{};
+            hip_detail::set_scissor(sparams, c);
+            std::memcpy(vc.scissor, c.scissor, sizeof(vc.scissor));
+            const vrh_pixel_sampler ps{ PS::kind, PS::count };
+            rt.begin_frame();
+            hip_detail::check(vrh_render_view(ctx_->get(), kernel.scene, rt.handle(), &vc, &kernel.desc, &ps, frame_num),
+                              "vrh_render_view");
+            rt.end_frame();
+            return;
+        }
         else
         {
-            // jittered / jittered_blend / ssaa<N> (sched_common.h:160-300, 440-720)
-            if (shard) throw std::runtime_error("hip_sched::frame: pixel samplers other than uniform render the whole image");
-            const vrh_pixel_sampler ps{ PS::kind, PS::count };
-            hip_detail::check(vrh_render_sampled(ctx_->get(), kernel.scene, rt.handle(), &c, &kernel.desc, &ps, frame_num),
-                              "vrh_render_sampled");
+            auto const& cam = sparams.cam;
+            float eye[3] = { cam.eye().x, cam.eye().y, cam.eye().z };
+            float center[3] = { cam.center().x, cam.center().y, cam.center().z };
+            float up[3] = { cam.up().x, cam.up().y, cam.up().z };
+            vrh_camera c{};
+            hip_detail::check(vrh_make_camera(eye, center, up, cam.fovy(), cam.aspect(), uint32_t(rt.width()),
+                                              uint32_t(rt.height()), &c), "vrh_make_camera");
+            hip_detail::set_scissor(sparams, c);
+            rt.begin_frame();
+            if constexpr (PS::kind == VRH_SAMPLER_UNIFORM)
+                hip_detail::check(vrh_render(ctx_->get(), kernel.scene, rt.handle(), &c, &kernel.desc, shard, frame_num),
+                                  "vrh_render");
+            else
+            {
+                // jittered / jittered_blend / ssaa<N> (sched_common.h:160-300, 440-720)
+                if (shard) throw std::runtime_error("hip_sched::frame: pixel samplers other than uniform render the whole image");
+                const vrh_pixel_sampler ps{ PS::kind, PS::count };
+                hip_detail::check(vrh_render_sampled(ctx_->get(), kernel.scene, rt.handle(), &c, &kernel.desc, &ps, frame_num),
+                                  "vrh_render_sampled");
+            }
+            rt.end_frame();
         }
-        rt.end_frame();
     }
 
 public:

@@ -484,7 +484,39 @@ struct user_frame
     float* t;
     uint32_t width, height, frame_num;
     uint32_t x0, y0, x1, y1;      // scissor box, exclusive right / bottom edges
+    uint32_t matrix_cam;          // sched_params with camera matrices: their inverses (column-major)
+    float inv_view[16], inv_proj[16];
 };
+
+// the primary ray through image position (fx, fy) (the pixel plus the sampler's offset):
+// sched_common.h:130-150 (pinhole basis) or :152-176 (camera matrices), the built-in kernels' arithmetic
+__device__ inline basic_ray<float> user_primary_ray(user_frame const& f, float fx, float fy)
+{
+    const float u = 2.0f * (fx + 0.5f) / (float)f.width - 1.0f;
+    const float v = 2.0f * (fy + 0.5f) / (float)f.height - 1.0f;
+    if (f.matrix_cam)
+    {
+        float a[4], b[4], o[4], d[4];
+        for (int r = 0; r < 4; ++r)
+        {
+            a[r] = f.inv_proj[r] * u + f.inv_proj[4 + r] * v + f.inv_proj[8 + r] * -1.0f + f.inv_proj[12 + r] * 1.0f;
+            b[r] = f.inv_proj[r] * u + f.inv_proj[4 + r] * v + f.inv_proj[8 + r] * 1.0f + f.inv_proj[12 + r] * 1.0f;
+        }
+        for (int r = 0; r < 4; ++r)
+        {
+            o[r] = f.inv_view[r] * a[0] + f.inv_view[4 + r] * a[1] + f.inv_view[8 + r] * a[2] + f.inv_view[12 + r] * a[3];
+            d[r] = f.inv_view[r] * b[0] + f.inv_view[4 + r] * b[1] + f.inv_view[8 + r] * b[2] + f.inv_view[12 + r] * b[3];
+        }
+        const vec3 ori(o[0] / o[3], o[1] / o[3], o[2] / o[3]);
+        const vec3 far(d[0] / d[3], d[1] / d[3], d[2] / d[3]);
+        return basic_ray<float>(ori, normalize(far - ori));
+    }
+    const vec3 cu(f.cam.cam_u[0], f.cam.cam_u[1], f.cam.cam_u[2]);
+    const vec3 cv(f.cam.cam_v[0], f.cam.cam_v[1], f.cam.cam_v[2]);
+    const vec3 cw(f.cam.cam_w[0], f.cam.cam_w[1], f.cam.cam_w[2]);
+    const vec3 eye(f.cam.eye[0], f.cam.eye[1], f.cam.eye[2]);
+    return basic_ray<float>(eye, normalize((cu * u + cv * v) + cw));
+}
 
 // sched_common.h:78-120 invoke_kernel: kernel(r), kernel(r, sampler) or kernel(r, x, y), in that
 // order of preference (the int / long / ... tag ranks the overloads)
@@ -531,19 +563,12 @@ __global__ __launch_bounds__(64) void user_render(K kernel, user_frame f)
     const uint32_t x = blockIdx.x * 8u + threadIdx.x;
     const uint32_t y = blockIdx.y * 8u + threadIdx.y;
     if (x < f.x0 || y < f.y0 || x >= f.x1 || y >= f.y1) return;
-    const vec3 cu(f.cam.cam_u[0], f.cam.cam_u[1], f.cam.cam_u[2]);
-    const vec3 cv(f.cam.cam_v[0], f.cam.cam_v[1], f.cam.cam_v[2]);
-    const vec3 cw(f.cam.cam_w[0], f.cam.cam_w[1], f.cam.cam_w[2]);
-    const vec3 eye(f.cam.eye[0], f.cam.eye[1], f.cam.eye[2]);
     hip_sampler samp(y * f.width + x, f.frame_num);
     const size_t o = size_t(y) * f.width + x;
     if constexpr (SK == VRH_SAMPLER_UNIFORM)
     {
-        // sched_common.h:130-150 make_primary_ray_impl (uniform pixel sampler), as the built-in kernels
-        const float u = 2.0f * ((float)x + 0.5f) / (float)f.width - 1.0f;
-        const float v = 2.0f * ((float)y + 0.5f) / (float)f.height - 1.0f;
-        basic_ray<float> r(eye, normalize((cu * u + cv * v) + cw));
-        auto res = invoke_kernel(kernel, r, samp, x, y, 0);
+        // sched_common.h:130-176 make_primary_ray_impl (uniform pixel sampler), as the built-in kernels
+        auto res = invoke_kernel(kernel, user_primary_ray(f, (float)x, (float)y), samp, x, y, 0);
         if (f.color) f.color[o] = make_float4(res.color.x, res.color.y, res.color.z, res.color.w);
         if constexpr (has_depth<decltype(res)>::value)
             if (f.t) f.t[o] = res.depth;
@@ -552,12 +577,7 @@ __global__ __launch_bounds__(64) void user_render(K kernel, user_frame f)
     {
         // the jittered / jittered_blend / ssaa<N> samplers (sched_common.h:196-300, 440-720), with the
         // jitter draws and offset tables of vrh.h vrh_pixel_sampler
-        auto ray_at = [&](float ox, float oy)
-        {
-            const float u = 2.0f * (((float)x + ox) + 0.5f) / (float)f.width - 1.0f;
-            const float v = 2.0f * (((float)y + oy) + 0.5f) / (float)f.height - 1.0f;
-            return basic_ray<float>(eye, normalize((cu * u + cv * v) + cw));
-        };
+        auto ray_at = [&](float ox, float oy) { return user_primary_ray(f, (float)x + ox, (float)y + oy); };
         if constexpr (SK == VRH_SAMPLER_SSAA)
         {
             constexpr float off2[2][2] = { { -0.25f, -0.25f }, { 0.25f, 0.25f } };
@@ -615,15 +635,26 @@ struct user_kernels<K, typename std::enable_if<!std::is_same<K, hip_builtin_kern
         using PS = sampler_desc<typename sampler_of<SP>::type>;
         static_assert(PS::supported, "hip_sched: the pixel samplers are uniform_type, jittered_type, "
                                      "jittered_blend_type and ssaa_type<2 / 4 / 8>");
-        auto const& cam = sparams.cam;
         auto& rt = sparams.rt;
         user_frame f{};
-        float eye[3] = { cam.eye().x, cam.eye().y, cam.eye().z };
-        float center[3] = { cam.center().x, cam.center().y, cam.center().z };
-        float up[3] = { cam.up().x, cam.up().y, cam.up().z };
-        check(vrh_make_camera(eye, center, up, cam.fovy(), cam.aspect(), uint32_t(rt.width()), uint32_t(rt.height()),
-                              &f.cam),
-              "vrh_make_camera");
+        if constexpr (has_camera_matrices<SP>::value)
+        {
+            // sched_params<Base, MT, RT, PxSamplerT> (scheduler.h:76-96): the host inverses of
+            // vrh_render_view (matrix4.inl:209-244)
+            f.matrix_cam = 1u;
+            vrh_matrix_inverse(sparams.view_matrix.data(), f.inv_view);
+            vrh_matrix_inverse(sparams.proj_matrix.data(), f.inv_proj);
+        }
+        else
+        {
+            auto const& cam = sparams.cam;
+            float eye[3] = { cam.eye().x, cam.eye().y, cam.eye().z };
+            float center[3] = { cam.center().x, cam.center().y, cam.center().z };
+            float up[3] = { cam.up().x, cam.up().y, cam.up().z };
+            check(vrh_make_camera(eye, center, up, cam.fovy(), cam.aspect(), uint32_t(rt.width()), uint32_t(rt.height()),
+                                  &f.cam),
+                  "vrh_make_camera");
+        }
         set_scissor(sparams, f.cam);
         f.width = uint32_t(rt.width());
         f.height = uint32_t(rt.height());

@@ -326,4 +326,55 @@ sched_params<RT> make_sched_params(camera const& cam, RT& rt)
     return sched_params<RT>{ cam, rt, recti(0, 0, int(rt.width()), int(rt.height())) };
 }
 
+// matrix<4, 4, float> (math/matrix.h:75-125): column-major storage, data() = m[col * 4 + row]
+template <size_t M, size_t N, typename T> class matrix;
+template <>
+class matrix<4, 4, float>
+{
+public:
+    matrix() = default;
+    explicit matrix(float const* col_major) { for (int i = 0; i < 16; ++i) m_[i] = col_major[i]; }
+    static matrix identity()
+    {
+        matrix r;
+        r.m_[0] = r.m_[5] = r.m_[10] = r.m_[15] = 1.0f;
+        return r;
+    }
+    float* data() { return m_; }
+    float const* data() const { return m_; }
+    float& operator()(int row, int col) { return m_[col * 4 + row]; }
+    float operator()(int row, int col) const { return m_[col * 4 + row]; }
+private:
+    float m_[16] = {};
+};
+using mat4 = matrix<4, 4, float>;
+
+// sched_params with camera matrices (scheduler.h:76-96, 197-231): view and projection matrix by
+// value instead of a camera
+template <typename RT, typename PxSamplerT = pixel_sampler::uniform_type>
+struct sched_params_matrices
+{
+    using has_camera_matrices = void;
+    using rt_type = RT;
+    using pixel_sampler_type = PxSamplerT;
+
+    mat4 view_matrix;
+    mat4 proj_matrix;
+    RT& rt;
+    recti scissor_box;
+};
+
+template <typename PxSamplerT, typename RT,
+          typename = typename std::enable_if<std::is_base_of<pixel_sampler::base_type, PxSamplerT>::value>::type>
+sched_params_matrices<RT, PxSamplerT> make_sched_params(PxSamplerT, mat4 const& view, mat4 const& proj, RT& rt)
+{
+    return sched_params_matrices<RT, PxSamplerT>{ view, proj, rt, recti(0, 0, int(rt.width()), int(rt.height())) };
+}
+
+template <typename RT>
+sched_params_matrices<RT> make_sched_params(mat4 const& view, mat4 const& proj, RT& rt)
+{
+    return sched_params_matrices<RT>{ view, proj, rt, recti(0, 0, int(rt.width()), int(rt.height())) };
+}
+
 } // visionaray

@@ -380,6 +380,27 @@ typedef struct {
 VRH_API int vrh_render_sampled(vrh_ctx* ctx, const vrh_scene* scene, vrh_rt* rt, const vrh_camera* cam,
                                const vrh_kernel_desc* kernel, const vrh_pixel_sampler* sampler, uint32_t frame_num);
 
+/* Camera matrices instead of a pinhole camera: sched_params<Base, MT, RT, PxSamplerT> as
+ * make_sched_params(sampler, view_matrix, proj_matrix, rt) builds it (scheduler.h:76-96, :197-212).
+ * Both matrices column-major (matrix<4, 4, float>: m[col * 4 + row]).  Their inverses are taken on
+ * the host with the reference's cofactor inverse (matrix4.inl:209-244, same float operations), and
+ * pixel (x, y) (plus the sampler's offset) gets the ray of sched_common.h:152-176:
+ *   u = 2 (x + 0.5) / width - 1, v = 2 (y + 0.5) / height - 1,
+ *   o = inv_view (inv_proj (u, v, -1, 1)), d = inv_view (inv_proj (u, v, 1, 1)),
+ *   origin = o.xyz / o.w, direction = normalize(d.xyz / d.w - origin).
+ * Samplers, frame_num and the scissor box as in vrh_render_sampled / vrh_camera; primary and AO
+ * kernels (the others: VRH_ERR_UNSUPPORTED). */
+typedef struct {
+    float    view[16];        /* view matrix, column-major                                  */
+    float    proj[16];        /* projection matrix, column-major                            */
+    uint32_t width, height;   /* image size (= the render target's)                         */
+    uint32_t scissor[4];      /* x, y, w, h (exclusive edges); all zero: whole image        */
+} vrh_view_camera;
+VRH_API int vrh_render_view(vrh_ctx* ctx, const vrh_scene* scene, vrh_rt* rt, const vrh_view_camera* cam,
+                            const vrh_kernel_desc* kernel, const vrh_pixel_sampler* sampler, uint32_t frame_num);
+/* the host inverse vrh_render_view applies (matrix4.inl:209-244 inverse()), for tests */
+VRH_API void vrh_matrix_inverse(const float m[16], float out[16]);
+
 /* device -> host copies (any destination may be NULL); synchronous */
 VRH_API int vrh_rt_download(vrh_ctx* ctx, vrh_rt* rt, void* color, uint32_t* prim_id, float* t, uint8_t* occ);
 

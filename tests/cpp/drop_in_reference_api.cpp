@@ -141,8 +141,22 @@ int main(int argc, char** argv)
             srt.download(sc.data(), nullptr, nullptr, nullptr);
             sampler_hashes[1] = fnv1a(sc.data(), n * 16);
         }
+        // the camera as view / projection matrices (make_sched_params(sampler, view, proj, rt),
+        // scheduler.h:197-212): the camera's own get_view_matrix() / get_proj_matrix(), frame 0
+        unsigned long long matrix_hashes[2] = { 0, 0 };
+        {
+            hip_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> vrt;
+            vrt.resize(W, H);
+            std::vector<float> vc(4 * n), vt(n);
+            vrt.clear_color_buffer(vec4(0.25f, 0.5f, 0.75f, 1.0f));
+            sched.frame(kern, make_sched_params(pixel_sampler::uniform_type{}, cam.get_view_matrix(), cam.get_proj_matrix(), vrt), 0);
+            vrt.download(vc.data(), nullptr, vt.data(), nullptr);
+            matrix_hashes[0] = fnv1a(vc.data(), n * 16);
+            matrix_hashes[1] = fnv1a(vt.data(), n * 4);
+        }
         printf("{\"sampler_jittered_blend_color_hash\":\"%016llx\",\"sampler_ssaa4_color_hash\":\"%016llx\",",
                sampler_hashes[0], sampler_hashes[1]);
+        printf("\"matrix_color_hash\":\"%016llx\",\"matrix_t_hash\":\"%016llx\",", matrix_hashes[0], matrix_hashes[1]);
         printf("\"mask_primid_hash\":\"%016llx\",\"mask_t_hash\":\"%016llx\",\"mask_occ_hash\":\"%016llx\","
                "\"mask_color_hash\":\"%016llx\",", mask_hashes[0], mask_hashes[1], mask_hashes[2], mask_hashes[3]);
         printf("\"grid\":%u,\"W\":%u,\"H\":%u,\"rays\":%llu,\"primid_hash\":\"%016llx\",\"t_hash\":\"%016llx\","

@@ -338,12 +338,30 @@ int main(int argc, char** argv)
             uint32_t* dpid = to_device(hp);
             auto k = sampler_kernel(one, dnormals, dpid, W, frame_num);
             rt.clear_color_buffer(vec4(0.25f, 0.5f, 0.75f, 1.0f));
-            if (kind == "jittered") sched.frame(k, make_sched_params(pixel_sampler::jittered_type{}, cam, rt), frame_num);
-            else if (kind == "jittered_blend") sched.frame(k, make_sched_params(pixel_sampler::jittered_blend_type{}, cam, rt), frame_num);
-            else if (kind == "ssaa2") sched.frame(k, make_sched_params(pixel_sampler::ssaa_type<2>{}, cam, rt), frame_num);
-            else if (kind == "ssaa4") sched.frame(k, make_sched_params(pixel_sampler::ssaa_type<4>{}, cam, rt), frame_num);
-            else if (kind == "ssaa8") sched.frame(k, make_sched_params(pixel_sampler::ssaa_type<8>{}, cam, rt), frame_num);
-            else sched.frame(k, make_sched_params(pixel_sampler::uniform_type{}, cam, rt), frame_num);
+            // optional argv[8]: view and projection matrix (32 floats, column-major) -- the camera
+            // matrices form make_sched_params(sampler, view, proj, rt) (scheduler.h:197-212)
+            const bool mats = argc > 8;
+            mat4 view, proj;
+            if (mats)
+            {
+                float m[32];
+                FILE* f = fopen(argv[8], "rb");
+                if (!f || fread(m, 4, 32, f) != 32) return 3;
+                fclose(f);
+                view = mat4(m);
+                proj = mat4(m + 16);
+            }
+            auto run = [&](auto ps)
+            {
+                if (mats) sched.frame(k, make_sched_params(ps, view, proj, rt), frame_num);
+                else sched.frame(k, make_sched_params(ps, cam, rt), frame_num);
+            };
+            if (kind == "jittered") run(pixel_sampler::jittered_type{});
+            else if (kind == "jittered_blend") run(pixel_sampler::jittered_blend_type{});
+            else if (kind == "ssaa2") run(pixel_sampler::ssaa_type<2>{});
+            else if (kind == "ssaa4") run(pixel_sampler::ssaa_type<4>{});
+            else if (kind == "ssaa8") run(pixel_sampler::ssaa_type<8>{});
+            else run(pixel_sampler::uniform_type{});
             if (hipMemcpy(hp.data(), dpid, hp.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return 4;
             write_file(outdir + "/sampler_prim_id.bin", hp.data(), hp.size() * 4);
         }

@@ -1,7 +1,8 @@
 """GPU: the reference's pixel samplers (pixel_sampler::jittered / jittered_blend / ssaa_type<2, 4, 8>,
 sched_common.h:160-300 and 440-720) through vrh_render_sampled and hip_sched.frame, bit for bit
 against the reference harness's `sampler` frames (tests/golden/sampler_*: colour blended onto a
-target filled with (0.25, 0.5, 0.75, 1), the last sample's prim id)."""
+target filled with (0.25, 0.5, 0.75, 1), the last sample's prim id and t) -- with the pinhole
+camera and with view / projection matrices (vrh_render_view, tests/golden/matrix_*)."""
 import os
 
 import numpy as np
@@ -31,6 +32,7 @@ def _scene(ctx, name):
 
 def _check(out, ref):
     assert np.array_equal(out["prim_id"], ref["prim_id"]), int((out["prim_id"] != ref["prim_id"]).sum())
+    assert np.array_equal(out["t"].view(np.uint32), ref["t"].view(np.uint32)), int((out["t"] != ref["t"]).sum())
     bad = int((out["color"].view(np.uint32) != ref["color"].view(np.uint32)).any(axis=1).sum())
     assert bad == 0, f"{bad} pixels' colour differ from the reference"
 
@@ -91,3 +93,65 @@ def test_progressive_jittered_blend_converges_and_shading_is_refused(ctx):
         va.render_sampled(ctx, dev, rt, basis, va.simple_kernel(dev, sh), va.pixel_sampler.ssaa_type(4))
     rt.close()
     one.close()
+
+
+MATRIX_CASES = ["matrix_uniform_hf64_ao", "matrix_ssaa4_hf64_ao", "matrix_jittered_blend_sph5000_primary",
+                "matrix_uniform_hf200_ao"]
+
+
+@pytest.mark.parametrize("case", MATRIX_CASES)
+def test_matrix_camera_matches_reference(ctx, golden, case):
+    """make_sched_params(sampler, view_matrix, proj_matrix, rt) (scheduler.h:197-212): the host inverse
+    and the matrix primary rays (sched_common.h:152-176), alone and under the samplers."""
+    g = golden[case]
+    ref = np.load(os.path.join(HERE, "golden", case + ".npz"))
+    dev = _scene(ctx, g["scene"])
+    kern = va.ao_kernel(dev) if g["kernel"] == "ao" else va.closest_hit_kernel(dev)
+    rt = va.hip_buffer_rt(ctx, g["W"], g["H"])
+    rt.clear_color_buffer(INIT)
+    vc = va.view_camera(ref["view"], ref["proj"], g["W"], g["H"])
+    va.render_view(ctx, dev, rt, vc, kern, SAMPLERS[g["sampler"]], frame_num=g["frame"])
+    ctx.sync()
+    _check(rt.download(), ref)
+    rt.close()
+
+
+@pytest.mark.parametrize("case", ["matrix_uniform_hf64_ao", "matrix_jittered_blend_sph5000_primary"])
+def test_matrix_camera_through_hip_sched(ctx, golden, case):
+    """hip_sched.frame(kernel, make_sched_params(sampler, view, proj, rt)); 4x4 [row, col] matrices
+    give the same frame as the column-major 16-vectors; a scissor box leaves the outside untouched."""
+    g = golden[case]
+    ref = np.load(os.path.join(HERE, "golden", case + ".npz"))
+    dev = _scene(ctx, g["scene"])
+    kern = va.ao_kernel(dev) if g["kernel"] == "ao" else va.closest_hit_kernel(dev)
+    rt = va.hip_buffer_rt(ctx, g["W"], g["H"])
+    rt.clear_color_buffer(INIT)
+    view = ref["view"].reshape(4, 4).T          # [row, col]
+    proj = ref["proj"].reshape(4, 4).T
+    sched = va.hip_sched(ctx)
+    sched.frame(kern, va.make_sched_params(SAMPLERS[g["sampler"]], view, proj, rt), frame_num=g["frame"])
+    _check(rt.download(), ref)
+    # scissor: only pixels x0 <= x < x1, y0 <= y < y1 are rendered
+    W, H = g["W"], g["H"]
+    box = (W // 4, H // 3, W // 2 + 7, H - 5)
+    rt.clear_color_buffer(INIT)
+    sp = va.make_sched_params(SAMPLERS[g["sampler"]], view, proj, rt)
+    sp.scissor_box = box
+    sched.frame(kern, sp, frame_num=g["frame"])
+    col = rt.download()["color"].reshape(H, W, 4)
+    refc = ref["color"].reshape(H, W, 4)
+    inside = np.zeros((H, W), bool)
+    inside[box[1]:box[3], box[0]:box[2]] = True
+    assert np.array_equal(col[inside].view(np.uint32), refc[inside].view(np.uint32))
+    assert np.all(col[~inside] == np.asarray(INIT, np.float32))
+    rt.close()
+
+
+def test_matrix_camera_refuses_shading_kernels(ctx):
+    dev = _scene(ctx, "hf64")
+    rt = va.hip_buffer_rt(ctx, 64, 32)
+    sh = va.shading(ctx, [va.plastic(cd=(0.8, 0.3, 0.2))], [va.point_light((1.0, 2.0, 1.0))])
+    vc = va.view_camera(np.eye(4), np.eye(4), 64, 32)
+    with pytest.raises(va.VrhError):
+        va.render_view(ctx, dev, rt, vc, va.simple_kernel(dev, sh))
+    rt.close()

@@ -84,6 +84,25 @@ def test_user_kernel_pixel_samplers_match_reference(tmp_path, golden, kind):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("case", ["matrix_uniform_hf64_ao", "matrix_ssaa4_hf64_ao"])
+def test_user_kernel_camera_matrices_match_reference(tmp_path, golden, case):
+    """make_sched_params(sampler, view_matrix, proj_matrix, rt) with a user kernel: the reference
+    harness's matrix-camera frames (sched_common.h:152-176)."""
+    g = golden[case]
+    ref = np.load(os.path.join(GOLDEN, case + ".npz"))
+    out = tmp_path / "m"
+    out.mkdir()
+    mpath = tmp_path / "mats.bin"
+    np.concatenate([ref["view"], ref["proj"]]).astype(np.float32).tofile(mpath)
+    subprocess.run([BIN, "sampler", str(GRID[g["scene"]]), str(g["W"]), str(g["H"]), str(out), g["sampler"],
+                    str(g["frame"]), str(mpath)], check=True, capture_output=True, text=True, timeout=120)
+    pid = np.fromfile(out / "sampler_prim_id.bin", np.uint32)
+    color = np.fromfile(out / "sampler_color.bin", np.float32).reshape(-1, 4)
+    assert np.array_equal(pid, ref["prim_id"])
+    assert np.array_equal(color.view(np.uint32), ref["color"].view(np.uint32))
+
+
+@pytest.mark.gpu
 def test_user_kernel_with_intersector_in_sched_params(tmp_path, golden, oracle_mod):
     """make_sched_params(sampler, cam, rt, isect) (scheduler.h:177-193): hip_sched calls the kernel as
     kernel(isect, r, x, y) (sched_common.h:786-818) -- the mask frames again."""

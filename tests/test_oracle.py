@@ -263,3 +263,19 @@ def test_oracle_matrix_camera_matches_reference(oracle_mod, golden, case):
     assert np.array_equal(out["prim_id"], ref["prim_id"])
     assert np.array_equal(out["t"].view(np.uint32), ref["t"].view(np.uint32))
     assert np.array_equal(out["color"].view(np.uint32), ref["color"].view(np.uint32))
+
+
+def test_library_matrix_inverse_matches_oracle(oracle_mod):
+    """vrh_matrix_inverse (host code of libvrh, no GPU) == the oracle's matrix4.inl inverse, bit for
+    bit, on the fixtures' matrices and random ones."""
+    import visionaray_amd as va
+    O = oracle_mod
+    rng = np.random.default_rng(7)
+    mats = [rng.standard_normal(16).astype(np.float32) for _ in range(64)]
+    for case in MATRIX_CASES:
+        ref = np.load(os.path.join(HERE, "golden", case + ".npz"))
+        mats += [ref["view"], ref["proj"]]
+    for m in mats:
+        a = va.matrix_inverse(m)
+        b = np.asarray(O.inverse4(m), np.float32)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))

@@ -69,6 +69,11 @@ class vrh_pixel_sampler(C.Structure):
 VRH_SAMPLER_UNIFORM, VRH_SAMPLER_JITTERED, VRH_SAMPLER_JITTERED_BLEND, VRH_SAMPLER_SSAA = 0, 1, 2, 3
 
 
+class vrh_view_camera(C.Structure):
+    _fields_ = [("view", C.c_float * 16), ("proj", C.c_float * 16), ("width", C.c_uint32), ("height", C.c_uint32),
+                ("scissor", C.c_uint32 * 4)]
+
+
 class vrh_shard(C.Structure):
     _fields_ = [("index", C.c_uint32), ("count", C.c_uint32), ("packed", C.c_uint32), ("reserved", C.c_uint32)]
 
@@ -156,6 +161,9 @@ SIGNATURES = {
                                    C.POINTER(vrh_shard), _u32]),
     "vrh_render_sampled": (C.c_int, [_vp, _vp, _vp, C.POINTER(vrh_camera), C.POINTER(vrh_kernel_desc),
                                      C.POINTER(vrh_pixel_sampler), _u32]),
+    "vrh_render_view": (C.c_int, [_vp, _vp, _vp, C.POINTER(vrh_view_camera), C.POINTER(vrh_kernel_desc),
+                                  C.POINTER(vrh_pixel_sampler), _u32]),
+    "vrh_matrix_inverse": (None, [_vp, _vp]),
     "vrh_sync": (C.c_int, [_vp]),
     "vrh_last_frame_stats": (C.c_int, [_vp, C.POINTER(vrh_frame_stats)]),
     "vrh_stats_reset": (C.c_int, [_vp]),

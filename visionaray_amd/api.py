@@ -421,13 +421,31 @@ class pixel_sampler:
         return types[n]
 
 
+def _matrix4(m):
+    """matrix<4, 4, float> in its memory order (column-major, m[col * 4 + row]): a flat 16-vector is
+    taken as that order, a 4x4 array as m[row, col]."""
+    a = np.asarray(m, dtype=np.float32)
+    if a.shape == (4, 4):
+        return np.ascontiguousarray(a.T).ravel()
+    if a.size != 16:
+        raise ValueError("a camera matrix has 4 x 4 entries")
+    return np.ascontiguousarray(a.ravel())
+
+
 class sched_params:
-    def __init__(self, cam, rt, sampler=pixel_sampler.uniform_type, image_size=None):
+    """sched_params (scheduler.h:53-96): a camera, or view / projection matrices (has_camera_matrices),
+    the render target, the pixel sampler and the scissor box."""
+
+    def __init__(self, cam, rt, sampler=pixel_sampler.uniform_type, image_size=None, view_matrix=None,
+                 proj_matrix=None):
         if not hasattr(sampler, "kind"):
             raise TypeError("sched_params: the sampler is one of the pixel_sampler types")
         self.sampler = sampler
         self.cam = cam          # stored by value in the reference (scheduler.h:72)
         self.rt = rt            # by reference (scheduler.h:73)
+        # the matrix form (scheduler.h:76-96), column-major float32[16], or None
+        self.view_matrix = None if view_matrix is None else _matrix4(view_matrix)
+        self.proj_matrix = None if proj_matrix is None else _matrix4(proj_matrix)
         # scissor_box (scheduler.h:25-31, default recti(0, 0, w, h) at :175): x, y and the EXCLUSIVE
         # right / bottom edges w, h, as cuda_sched.inl:71 reads them; None = the whole image
         self.scissor_box = None
@@ -436,14 +454,18 @@ class sched_params:
 
 
 def make_sched_params(*args, image_size=None):
-    """make_sched_params([pixel_sampler], camera, rt) -- scheduler.h:164-242."""
+    """make_sched_params([pixel_sampler], camera, rt) or make_sched_params([pixel_sampler], view_matrix,
+    proj_matrix, rt) -- scheduler.h:164-242."""
+    sampler = pixel_sampler.uniform_type
+    if args and hasattr(args[0], "kind"):
+        sampler, args = args[0], args[1:]
+    if len(args) == 2:
+        cam, rt = args
+        return sched_params(cam, rt, sampler, image_size)
     if len(args) == 3:
-        sampler, cam, rt = args
-    elif len(args) == 2:
-        sampler, (cam, rt) = pixel_sampler.uniform_type, args
-    else:
-        raise TypeError("make_sched_params([sampler,] camera, render_target)")
-    return sched_params(cam, rt, sampler, image_size)
+        view, proj, rt = args
+        return sched_params(None, rt, sampler, image_size, view_matrix=view, proj_matrix=proj)
+    raise TypeError("make_sched_params([sampler,] camera, render_target) or ([sampler,] view, proj, render_target)")
 
 
 class _builtin_kernel:
@@ -652,6 +674,19 @@ class hip_sched:
             raise TypeError("hip_sched runs built-in kernels only (closest_hit / ao / simple / multi_hit / whitted): an arbitrary "
                             "callable cannot cross the C ABI")
         rt = sparams.rt
+        sampler = getattr(sparams, "sampler", pixel_sampler.uniform_type)
+        if getattr(sparams, "view_matrix", None) is not None:
+            # camera matrices (sched_common.h:152-176): vrh_render_view, whole image
+            if shard is not None:
+                raise ValueError("hip_sched::frame: camera matrices render the whole image")
+            vc = view_camera(sparams.view_matrix, sparams.proj_matrix, *sparams.image_size)
+            if sparams.scissor_box is not None:
+                vc.scissor[:] = [int(v) for v in sparams.scissor_box]
+            rt.begin_frame()
+            render_view(self.ctx, kernel.bvh, rt, vc, kernel, sampler, frame_num)
+            if sync:
+                rt.end_frame()
+            return
         cam = sparams.cam.basis(*sparams.image_size)
         if sparams.scissor_box is not None:
             cam.scissor[:] = [int(v) for v in sparams.scissor_box]
@@ -659,7 +694,6 @@ class hip_sched:
         if shard is not None:
             sh = capi.vrh_shard(shard[0], shard[1], 1 if shard[2] else 0, 0)
         rt.begin_frame()
-        sampler = getattr(sparams, "sampler", pixel_sampler.uniform_type)
         if sampler.kind != pixel_sampler.uniform_type.kind:
             # jittered / jittered_blend / ssaa<N> (sched_common.h:160-300, 440-720)
             if sh is not None:
@@ -685,6 +719,30 @@ def render_sampled(ctx, bvh, rt, cam_basis, kernel, sampler, frame_num=0):
     ps = capi.vrh_pixel_sampler(sampler.kind, sampler.count)
     capi.check("vrh_render_sampled", ctx.handle, bvh.handle, rt.handle, C.byref(cam_basis), C.byref(kernel.desc),
                C.byref(ps), frame_num)
+
+
+def view_camera(view, proj, width, height):
+    """vrh_view_camera of view / projection matrices (column-major 16-vectors or 4x4 [row, col])."""
+    vc = capi.vrh_view_camera()
+    vc.view[:] = [float(x) for x in _matrix4(view)]
+    vc.proj[:] = [float(x) for x in _matrix4(proj)]
+    vc.width, vc.height = int(width), int(height)
+    return vc
+
+
+def render_view(ctx, bvh, rt, view_cam, kernel, sampler=pixel_sampler.uniform_type, frame_num=0):
+    """vrh_render_view: one frame from camera matrices (a vrh_view_camera) through a pixel sampler."""
+    ps = capi.vrh_pixel_sampler(sampler.kind, sampler.count)
+    capi.check("vrh_render_view", ctx.handle, bvh.handle, rt.handle, C.byref(view_cam), C.byref(kernel.desc),
+               C.byref(ps), frame_num)
+
+
+def matrix_inverse(m):
+    """vrh_matrix_inverse: the host inverse vrh_render_view applies (matrix4.inl:209-244)."""
+    a = _matrix4(m)
+    out = np.empty(16, np.float32)
+    capi.lib().vrh_matrix_inverse(a.ctypes.data, out.ctypes.data)
+    return out
 
 
 def render_batch(ctx, bvh, rt, cam_bases, kernel, shard=None, frame_num=0):

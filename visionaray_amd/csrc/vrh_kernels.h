@@ -48,6 +48,10 @@ struct render_params
     float px_off[2];
     uint32_t jitter, blend;
     float blend_s, blend_d;
+    // camera matrices (vrh_render_view; pixel-sampler instances only): the ray of pixel (x, y) runs
+    // through inv_view * (inv_proj * (u, v, -+1, 1)) instead of the pinhole basis of cam[f]
+    uint32_t matrix_cam;
+    float inv_view[16], inv_proj[16];   // column-major
 
     uint32_t shard_index, shard_count, packed;
     uint32_t tiles_x, num_tiles;   // tiles of ONE frame (the launch has num_frames x num_tiles units)

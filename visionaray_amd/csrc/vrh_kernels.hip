@@ -132,6 +132,27 @@ __device__ __forceinline__ ray_t primary_ray(const render_params& P, uint32_t f,
     }
     float u = 2.0f * (fx + 0.5f) / (float)P.width - 1.0f;
     float v = 2.0f * (fy + 0.5f) / (float)P.height - 1.0f;
+    if (SAMPLED && P.matrix_cam)
+    {
+        // sched_common.h:152-176 (camera matrices): o = inv_view (inv_proj (u, v, -1, 1)), d at
+        // z = +1; matrix * vector row by row, left to right (matrix4.inl:171-181)
+        const float* iv = P.inv_view;
+        const float* ip = P.inv_proj;
+        float a[4], b[4], o[4], d[4];
+        for (int r = 0; r < 4; ++r)
+        {
+            a[r] = ip[r] * u + ip[4 + r] * v + ip[8 + r] * -1.0f + ip[12 + r] * 1.0f;
+            b[r] = ip[r] * u + ip[4 + r] * v + ip[8 + r] * 1.0f + ip[12 + r] * 1.0f;
+        }
+        for (int r = 0; r < 4; ++r)
+        {
+            o[r] = iv[r] * a[0] + iv[4 + r] * a[1] + iv[8 + r] * a[2] + iv[12 + r] * a[3];
+            d[r] = iv[r] * b[0] + iv[4 + r] * b[1] + iv[8 + r] * b[2] + iv[12 + r] * b[3];
+        }
+        const f3 ori = mk3(o[0] / o[3], o[1] / o[3], o[2] / o[3]);
+        const f3 far = mk3(d[0] / d[3], d[1] / d[3], d[2] / d[3]);
+        return make_ray(ori, normalize(far - ori));
+    }
     f3 cu = mk3(c.cam_u[0], c.cam_u[1], c.cam_u[2]);
     f3 cv = mk3(c.cam_v[0], c.cam_v[1], c.cam_v[2]);
     f3 cw = mk3(c.cam_w[0], c.cam_w[1], c.cam_w[2]);

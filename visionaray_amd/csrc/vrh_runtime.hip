@@ -799,6 +799,7 @@ struct sampler_pass
     float off[2];
     uint32_t jitter, blend;
     float s, d;
+    const float* inv_mats;    // vrh_render_view: inverse view, inverse projection (32 floats), else null
 };
 int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_camera* cams, uint32_t num_frames,
                       const vrh_kernel_desc* k, const vrh_shard* shard, uint32_t frame_num, const sampler_pass* sp);
@@ -811,22 +812,25 @@ VRH_API int vrh_render_batch(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, cons
     return render_batch_impl(ctx, sc, rt, cams, num_frames, k, shard, frame_num, nullptr);
 }
 
-VRH_API int vrh_render_sampled(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_camera* cam,
-                               const vrh_kernel_desc* k, const vrh_pixel_sampler* ps, uint32_t frame_num)
+namespace {
+// the passes of a pixel sampler (vrh_render_sampled / vrh_render_view); inv_mats: camera matrices
+int render_sampled_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_camera* cam,
+                        const vrh_kernel_desc* k, const vrh_pixel_sampler* ps, uint32_t frame_num, const float* inv_mats)
 {
     VRH_CHECK(ctx && sc && rt && cam && k && ps, "vrh_render_sampled: null argument");
     VRH_CHECK(ps->kind <= VRH_SAMPLER_SSAA, "vrh_render_sampled: unknown pixel sampler");
-    if (ps->kind == VRH_SAMPLER_UNIFORM) return render_batch_impl(ctx, sc, rt, cam, 1, k, nullptr, frame_num, nullptr);
+    if (ps->kind == VRH_SAMPLER_UNIFORM && !inv_mats) return render_batch_impl(ctx, sc, rt, cam, 1, k, nullptr, frame_num, nullptr);
     if (k->kind != VRH_KERNEL_PRIMARY && k->kind != VRH_KERNEL_AO)
     {
-        set_error("vrh_render_sampled: jittered / ssaa samplers run the primary and AO kernels");
+        set_error(inv_mats ? "vrh_render_view: camera matrices run the primary and AO kernels"
+                           : "vrh_render_sampled: jittered / ssaa samplers run the primary and AO kernels");
         return VRH_ERR_UNSUPPORTED;
     }
     if (ps->kind != VRH_SAMPLER_SSAA)
     {
-        // jittered: the pixel's jittered ray, colour stored; jittered_blend: blended with
-        // a = 1 / frame_num, 1 - a (sched_common.h:480-540)
-        sampler_pass p{ { 0.0f, 0.0f }, 1u, 0u, 1.0f, 0.0f };
+        // uniform (camera matrices): the pixel's ray, colour stored; jittered: the pixel's jittered
+        // ray, colour stored; jittered_blend: blended with a = 1 / frame_num, 1 - a (sched_common.h:480-540)
+        sampler_pass p{ { 0.0f, 0.0f }, ps->kind == VRH_SAMPLER_UNIFORM ? 0u : 1u, 0u, 1.0f, 0.0f, inv_mats };
         if (ps->kind == VRH_SAMPLER_JITTERED_BLEND)
         {
             p.blend = 1u;
@@ -845,11 +849,56 @@ VRH_API int vrh_render_sampled(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, co
     const float (*tab)[2] = ps->count == 2 ? off2 : ps->count == 4 ? off4 : off8;
     for (uint32_t i = 0; i < ps->count; ++i)
     {
-        sampler_pass p{ { tab[i][0], tab[i][1] }, 0u, i == 0 ? 2u : 1u, 1.0f / float(ps->count), 1.0f };
+        sampler_pass p{ { tab[i][0], tab[i][1] }, 0u, i == 0 ? 2u : 1u, 1.0f / float(ps->count), 1.0f, inv_mats };
         const int rc = render_batch_impl(ctx, sc, rt, cam, 1, k, nullptr, frame_num, &p);
         if (rc) return rc;
     }
     return VRH_OK;
+}
+} // namespace
+
+VRH_API int vrh_render_sampled(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_camera* cam,
+                               const vrh_kernel_desc* k, const vrh_pixel_sampler* ps, uint32_t frame_num)
+{
+    return render_sampled_impl(ctx, sc, rt, cam, k, ps, frame_num, nullptr);
+}
+
+// matrix4.inl:209-244 inverse(): the 2x2 sub-determinants of rows 0-1 and 2-3
+// (det2(a, b, c, d) = a * d - c * b, math.h:493-496), the cofactor expansion, every entry / det
+VRH_API void vrh_matrix_inverse(const float m[16], float out[16])
+{
+    auto det2 = [](float a, float b, float c, float d) { return a * d - c * b; };
+    auto M = [m](int r, int c) { return m[c * 4 + r]; };
+    const float s0 = det2(M(0, 0), M(0, 1), M(1, 0), M(1, 1)), s1 = det2(M(0, 0), M(0, 2), M(1, 0), M(1, 2));
+    const float s2 = det2(M(0, 0), M(0, 3), M(1, 0), M(1, 3)), s3 = det2(M(0, 1), M(0, 2), M(1, 1), M(1, 2));
+    const float s4 = det2(M(0, 1), M(0, 3), M(1, 1), M(1, 3)), s5 = det2(M(0, 2), M(0, 3), M(1, 2), M(1, 3));
+    const float c5 = det2(M(2, 2), M(2, 3), M(3, 2), M(3, 3)), c4 = det2(M(2, 1), M(2, 3), M(3, 1), M(3, 3));
+    const float c3 = det2(M(2, 1), M(2, 2), M(3, 1), M(3, 2)), c2 = det2(M(2, 0), M(2, 3), M(3, 0), M(3, 3));
+    const float c1 = det2(M(2, 0), M(2, 2), M(3, 0), M(3, 2)), c0 = det2(M(2, 0), M(2, 1), M(3, 0), M(3, 1));
+    const float det = s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0;
+    const float r[16] = {
+        (M(1, 1) * c5 - M(1, 2) * c4 + M(1, 3) * c3) / det, (-M(1, 0) * c5 + M(1, 2) * c2 + M(1, 3) * c1) / det,
+        (M(1, 0) * c4 - M(1, 1) * c2 + M(1, 3) * c0) / det, (-M(1, 0) * c3 + M(1, 1) * c1 + M(1, 2) * c0) / det,
+        (-M(0, 1) * c5 + M(0, 2) * c4 - M(0, 3) * c3) / det, (M(0, 0) * c5 - M(0, 2) * c2 + M(0, 3) * c1) / det,
+        (-M(0, 0) * c4 + M(0, 1) * c2 - M(0, 3) * c0) / det, (M(0, 0) * c3 - M(0, 1) * c1 + M(0, 2) * c0) / det,
+        (M(3, 1) * s5 - M(3, 2) * s4 + M(3, 3) * s3) / det, (-M(3, 0) * s5 + M(3, 2) * s2 - M(3, 3) * s1) / det,
+        (M(3, 0) * s4 - M(3, 1) * s2 + M(3, 3) * s0) / det, (-M(3, 0) * s3 + M(3, 1) * s1 - M(3, 2) * s0) / det,
+        (-M(2, 1) * s5 + M(2, 2) * s4 - M(2, 3) * s3) / det, (M(2, 0) * s5 - M(2, 2) * s2 + M(2, 3) * s1) / det,
+        (-M(2, 0) * s4 + M(2, 1) * s2 - M(2, 3) * s0) / det, (M(2, 0) * s3 - M(2, 1) * s1 + M(2, 2) * s0) / det };
+    std::memcpy(out, r, sizeof(r));
+}
+
+VRH_API int vrh_render_view(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_view_camera* vc,
+                            const vrh_kernel_desc* k, const vrh_pixel_sampler* ps, uint32_t frame_num)
+{
+    VRH_CHECK(ctx && vc, "vrh_render_view: null argument");
+    vrh_camera cam{};
+    cam.width = vc->width; cam.height = vc->height;
+    std::memcpy(cam.scissor, vc->scissor, sizeof(cam.scissor));
+    float inv[32];
+    vrh_matrix_inverse(vc->view, inv);
+    vrh_matrix_inverse(vc->proj, inv + 16);
+    return render_sampled_impl(ctx, sc, rt, &cam, k, ps, frame_num, inv);
 }
 
 namespace {
@@ -1035,6 +1084,12 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     {
         p.px_off[0] = sp->off[0]; p.px_off[1] = sp->off[1];
         p.jitter = sp->jitter; p.blend = sp->blend; p.blend_s = sp->s; p.blend_d = sp->d;
+        if (sp->inv_mats)
+        {
+            p.matrix_cam = 1u;
+            std::memcpy(p.inv_view, sp->inv_mats, sizeof(p.inv_view));
+            std::memcpy(p.inv_proj, sp->inv_mats + 16, sizeof(p.inv_proj));
+        }
     }
     p.shard_index = sh.index; p.shard_count = sh.count; p.packed = sh.packed ? 1u : 0u;
     p.tiles_x = (cam->width + 7u) / 8u;
