@@ -44,10 +44,10 @@ int main(int argc, char** argv)
         hip_detail::check(vrh_face_normals(tris.data(), uint32_t(tris.size()), &normals[0].x), "vrh_face_normals");
 
         hip_render_group group;                     // every visible GPU
-        std::vector<hip_index_bvh<basic_triangle<3, float>>> replicas;
+        // the BVH goes to GPU 0 once and is broadcast from there to every member over RCCL
+        hip_index_bvh<basic_triangle<3, float>> root_bvh(host_bvh, normals.data(), group.context(0));
+        auto replicas = hip_index_bvh<basic_triangle<3, float>>::broadcast(group, &root_bvh);
         std::vector<hip_builtin_kernel> kernels;
-        for (size_t i = 0; i < group.size(); ++i)
-            replicas.emplace_back(host_bvh, normals.data(), group.context(i));
         for (auto const& r : replicas)
             kernels.push_back(make_hip_ao_kernel(r, vec4(0.1f, 0.2f, 0.3f, 1.0f), 8, 0.1f));
 

@@ -333,6 +333,23 @@ public:
         return i;
     }
 
+    // scene replication over a render group (vrh_group_broadcast_scene): the process
+    // holding rank 0 passes its BVH (on rank 0's context), the others nullptr; one replica per
+    // member this process drives, on that member's context, broadcast over RCCL instead of built
+    // or uploaded once per GPU
+    static std::vector<hip_index_bvh> broadcast(hip_render_group const& group, hip_index_bvh const* root_bvh)
+    {
+        std::vector<vrh_group*> g;
+        for (size_t i = 0; i < group.size(); ++i) g.push_back(group.handle(i));
+        std::vector<vrh_scene*> out(g.size(), nullptr);
+        hip_detail::check(vrh_group_broadcast_scene(uint32_t(g.size()), g.data(), root_bvh ? root_bvh->handle() : nullptr,
+                                                    out.data()),
+                          "vrh_group_broadcast_scene");
+        std::vector<hip_index_bvh> r;
+        for (size_t i = 0; i < g.size(); ++i) r.push_back(hip_index_bvh(out[i], group.context(i)));
+        return r;
+    }
+
 private:
     hip_index_bvh(vrh_scene* s, std::shared_ptr<hip_context> ctx) : ctx_(std::move(ctx))
     {

@@ -454,6 +454,13 @@ VRH_API int vrh_group_free(vrh_group* group);
  * Asynchronous: renders on each context's stream, the exchange and un-interleave on the group's
  * own stream (two staging slots: the next call's renders overlap this call's exchange);
  * vrh_group_sync waits for both. */
+/* Scene replication over a group (the scene is broadcast from rank 0 once, instead of
+ * every rank building it): rank 0 passes its scene (any kind: uploaded, GPU-built, a list, with
+ * vertex normals), the other ranks NULL; out[i] receives, on group i's context, a new scene holding
+ * the same device bytes (free it with vrh_scene_free; rank 0's own scene stays its caller's).  One
+ * ncclBroadcast per array over the group's communicator (xGMI), after a header with the array
+ * sizes.  n / groups as in vrh_render_sharded.  Collective; returns once every replica is complete. */
+VRH_API int vrh_group_broadcast_scene(uint32_t n, vrh_group* const* groups, const vrh_scene* root_scene, vrh_scene** out);
 VRH_API int vrh_render_sharded(uint32_t n, vrh_group* const* groups, const vrh_scene* const* scenes,
                                const vrh_kernel_desc* kernels, vrh_rt* dst, uint32_t fields,
                                const vrh_camera* cams, uint32_t num_frames, uint32_t frame_num, uint32_t shards);

@@ -205,3 +205,110 @@ def test_group_argument_errors(ctx, group):
     with pytest.raises(va.VrhError):          # AO masks of more than 8 samples do not fit a byte
         group.render(dev, va.ao_kernel(dev, samples=12), va.hip_buffer_rt(ctx, 160, 90), [basis],
                      fields=_capi.VRH_RT_OCC)
+
+
+def _frame(ctx, dev, kern, basis, W, H):
+    rt = va.hip_buffer_rt(ctx, W, H)
+    va.render(ctx, dev, rt, basis, kern, None, frame_num=2)
+    out = rt.download()
+    rt.close()
+    return out
+
+
+def _same(a, b):
+    for k in ("prim_id", "occ"):
+        assert np.array_equal(a[k], b[k]), k
+    for k in ("t", "color"):
+        assert np.array_equal(a[k].view(np.uint32), b[k].view(np.uint32)), k
+
+
+def test_broadcast_scene_replicas_render_identically(ctx, group, golden, oracle_mod):
+    """vrh_group_broadcast_scene (SURVEY.md §8e scene replication: ncclBroadcast from rank 0, here a
+    one-rank group broadcasting into a new scene): every scene kind -- uploaded triangles with the
+    4-wide records, spheres, a two-BVH list, a GPU-built scene with its reference-layout tree,
+    vertex normals for the shading kernels -- renders bit for bit as the original; hf10M's replica
+    reproduces the reference hashes."""
+    W, H = 320, 180
+    host, dev = device_scene(ctx, "hf200")
+    cam, _, _ = scenes.scene_camera("hf200", W, H)
+    basis = cam.basis(W, H)
+    rep = group.broadcast_scene(dev)
+    assert rep.handle.value != dev.handle.value
+    assert rep.info == dev.info
+    _same(_frame(ctx, rep, va.ao_kernel(rep), basis, W, H), _frame(ctx, dev, va.ao_kernel(dev), basis, W, H))
+    rep.close()
+
+    host, sdev = device_scene(ctx, "sph5000")
+    scam, _, _ = scenes.scene_camera("sph5000", W, H)
+    rep = group.broadcast_scene(sdev)
+    _same(_frame(ctx, rep, va.closest_hit_kernel(rep), scam.basis(W, H), W, H),
+          _frame(ctx, sdev, va.closest_hit_kernel(sdev), scam.basis(W, H), W, H))
+    rep.close()
+
+    # a list of two BVHs (prim ids split by parity), AO
+    prims = scenes.primitives("hf200")
+    halves = [va.hip_index_bvh(ctx, va.build_index_bvh(prims[prims["prim_id"] % 2 == p])) for p in (0, 1)]
+    lst = va.hip_index_bvh.scene_list(ctx, halves, scenes.normals_for(prims))
+    rep = group.broadcast_scene(lst)
+    assert rep.info["num_bvhs"] == 2
+    _same(_frame(ctx, rep, va.ao_kernel(rep), basis, W, H), _frame(ctx, lst, va.ao_kernel(lst), basis, W, H))
+    rep.close()
+
+    # GPU-built scene: the replica keeps the device tree (download_bvh) and renders the same
+    gb = va.hip_index_bvh.gpu_build(ctx, prims, scenes.normals_for(prims))
+    rep = group.broadcast_scene(gb)
+    n0, i0 = gb.download_bvh()
+    n1, i1 = rep.download_bvh()
+    assert n0.tobytes() == n1.tobytes() and np.array_equal(i0, i1)
+    _same(_frame(ctx, rep, va.ao_kernel(rep), basis, W, H), _frame(ctx, gb, va.ao_kernel(gb), basis, W, H))
+    rep.close()
+
+    # vertex normals: simple::kernel with per-vertex shading normals on the replica
+    O = oracle_mod
+    sprims = scenes.primitives("hf64")
+    fn = va.face_normals(sprims)
+    vdev = va.hip_index_bvh(ctx, va.build_index_bvh(sprims), fn)
+    vdev.set_vertex_normals(O.vertex_normals(fn))
+    rep = group.broadcast_scene(vdev)
+    assert rep.info["vertex_normals"] == 1
+    sh = va.shading(ctx, [va.plastic(cd=(0.8, 0.3, 0.2), ks=0.4, cs=(1, 1, 1), exp=32.0)], [va.point_light((1.0, 2.0, 1.0))])
+    vcam, _, _ = scenes.scene_camera("hf64", 160, 90)
+    kv = [va.simple_kernel(d, sh, binding=va.normals_per_vertex_binding) for d in (rep, vdev)]
+    _same(_frame(ctx, rep, kv[0], vcam.basis(160, 90), 160, 90), _frame(ctx, vdev, kv[1], vcam.basis(160, 90), 160, 90))
+    rep.close()
+
+    # hf10M: the replica renders the reference's frame
+    g = golden["hf10M"]
+    host, big = device_scene(ctx, "hf10M")
+    bcam, BW, BH = scenes.scene_camera("hf10M")
+    rep = group.broadcast_scene(big)
+    out = _frame_num0(ctx, rep, BW, BH, bcam.basis(BW, BH))
+    O = oracle_mod
+    assert O.fnv1a(out["prim_id"]) == g["primid_hash"]
+    assert O.fnv1a(out["occ"]) == g["occ_hash"]
+    assert O.fnv1a(out["color"]) == g["color_hash"]
+    rep.close()
+
+
+def _frame_num0(ctx, dev, W, H, basis):
+    rt = va.hip_buffer_rt(ctx, W, H)
+    va.render(ctx, dev, rt, basis, va.ao_kernel(dev), None, frame_num=0)
+    out = rt.download()
+    rt.close()
+    return out
+
+
+def test_broadcast_scene_local_group_and_errors(ctx):
+    """One process driving the group (vrh_group_create_local): the same call with every member;
+    rank 0 must pass its scene."""
+    (g,) = va.render_group.local([ctx])
+    host, dev = device_scene(ctx, "hf64")
+    W, H = 160, 90
+    cam, _, _ = scenes.scene_camera("hf64", W, H)
+    (rep,) = va.broadcast_scene([g], dev)
+    _same(_frame(ctx, rep, va.ao_kernel(rep), cam.basis(W, H), W, H),
+          _frame(ctx, dev, va.ao_kernel(dev), cam.basis(W, H), W, H))
+    rep.close()
+    with pytest.raises(va.VrhError):
+        va.broadcast_scene([g], None)
+    g.close()

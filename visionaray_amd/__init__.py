@@ -8,7 +8,7 @@ multi-GPU render groups (render_group, render_sharded: image-tile shards gathere
 from . import _capi
 from ._capi import VrhError
 from .api import (BVH_NODE_DTYPE, DEGREES_TO_RADIANS, GROUP_ID_BYTES, PLASTIC_DTYPE, POINT_LIGHT_DTYPE,
-                  SPHERE_DTYPE, TRIANGLE_DTYPE, Context, ao_kernel, build_index_bvh, camera, closest_hit_kernel,
+                  SPHERE_DTYPE, TRIANGLE_DTYPE, Context, ao_kernel, broadcast_scene, build_index_bvh, camera, closest_hit_kernel,
                   device_count, face_normals, hip_buffer_rt, hip_index_bvh, hip_sched,
                   hit_mask, index_bvh, load_obj, make_sched_params, make_spheres, make_triangles, matrix_inverse, model,
                   multi_hit_kernel, normals_per_face_binding, normals_per_vertex_binding, pixel_sampler, plastic,
@@ -17,7 +17,7 @@ from .api import (BVH_NODE_DTYPE, DEGREES_TO_RADIANS, GROUP_ID_BYTES, PLASTIC_DT
 
 __all__ = [
     "BVH_NODE_DTYPE", "DEGREES_TO_RADIANS", "GROUP_ID_BYTES", "PLASTIC_DTYPE", "POINT_LIGHT_DTYPE", "SPHERE_DTYPE",
-    "TRIANGLE_DTYPE", "Context", "VrhError", "_capi", "ao_kernel", "build_index_bvh", "camera", "closest_hit_kernel",
+    "TRIANGLE_DTYPE", "Context", "VrhError", "_capi", "ao_kernel", "broadcast_scene", "build_index_bvh", "camera", "closest_hit_kernel",
     "device_count", "face_normals", "hip_buffer_rt", "hip_index_bvh", "hip_sched",
     "hit_mask", "index_bvh", "load_obj", "make_sched_params", "make_spheres", "make_triangles", "matrix_inverse", "model",
     "multi_hit_kernel", "normals_per_face_binding", "normals_per_vertex_binding", "pixel_sampler", "plastic",

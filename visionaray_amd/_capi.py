@@ -179,6 +179,7 @@ SIGNATURES = {
     "vrh_group_info": (C.c_int, [_vp, C.POINTER(_u32), C.POINTER(_u32)]),
     "vrh_group_sync": (C.c_int, [_vp]),
     "vrh_group_free": (C.c_int, [_vp]),
+    "vrh_group_broadcast_scene": (C.c_int, [_u32, C.POINTER(_vp), _vp, C.POINTER(_vp)]),
     "vrh_render_sharded": (C.c_int, [_u32, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(vrh_kernel_desc), _vp, _u32,
                                      C.POINTER(vrh_camera), _u32, _u32, _u32]),
     "vrh_gen_heightfield": (C.c_int, [_u32, _vp]),

@@ -814,6 +814,11 @@ class render_group:
         """vrh_render_sharded for this member alone (one process per GPU)."""
         render_sharded([self], [scene], [kernel], dst_rt, cam_bases, frame_num, shards, fields)
 
+    def broadcast_scene(self, scene=None):
+        """vrh_group_broadcast_scene for this member alone (one process per GPU): rank 0 passes its
+        hip_index_bvh, the other ranks None; every rank gets a replica on its own context."""
+        return broadcast_scene([self], scene)[0]
+
     def sync(self):
         capi.check("vrh_group_sync", self.handle)
 
@@ -827,6 +832,23 @@ class render_group:
             self.close()
         except Exception:
             pass
+
+
+def broadcast_scene(groups, scene=None):
+    """vrh_group_broadcast_scene: rank 0's scene (a hip_index_bvh; None on the other ranks) replicated
+    over the group by RCCL broadcasts -- one new hip_index_bvh per member in `groups`, on its context
+    (the scene goes to every GPU once, instead of every rank building it)."""
+    n = len(groups)
+    out = (C.c_void_p * n)()
+    capi.check("vrh_group_broadcast_scene", n, (C.c_void_p * n)(*[g.handle.value for g in groups]),
+               scene.handle if scene is not None else None, out)
+    replicas = []
+    for i, g in enumerate(groups):
+        r = hip_index_bvh.__new__(hip_index_bvh)
+        r.ctx, r.handle = g.ctx, C.c_void_p(out[i])
+        r._refresh_info()
+        replicas.append(r)
+    return replicas
 
 
 def render_sharded(groups, scenes_, kernels, dst_rt, cam_bases, frame_num=0, shards=0, fields=None):

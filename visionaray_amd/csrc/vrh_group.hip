@@ -111,6 +111,34 @@ int grow(vrh_group* g, uint8_t*& p, size_t& have, size_t need)
     return VRH_OK;
 }
 
+// what a scene replica needs to know before its arrays arrive (vrh_group_broadcast_scene)
+struct scene_header
+{
+    uint64_t bytes[7];                 // pairs, prims, normals, quads, vnormals, dnodes, dindices
+    uint32_t roots[vrh::MAX_LIST];
+    uint32_t num_roots, num_pairs, quad_depth, finite_bounds;
+    vrh_scene_info info;
+};
+
+// the device arrays of a scene, in scene_header::bytes order
+inline void* const* scene_arrays(vrh_scene* sc, void* (&a)[7])
+{
+    a[0] = sc->pairs; a[1] = sc->prims; a[2] = sc->normals; a[3] = sc->quads;
+    a[4] = sc->vnormals; a[5] = sc->dnodes; a[6] = sc->dindices;
+    return a;
+}
+
+// allocation size of a device array (0 for null)
+int array_bytes(void* p, uint64_t& out)
+{
+    out = 0;
+    if (!p) return VRH_OK;
+    size_t n = 0;
+    VRH_HIP(hipMemPtrGetInfo(p, &n));
+    out = n;
+    return VRH_OK;
+}
+
 } // namespace
 
 extern "C" {
@@ -349,5 +377,125 @@ VRH_API int vrh_render_sharded(uint32_t n, vrh_group* const* groups, const vrh_s
     }
     return VRH_OK;
 }
+
+VRH_API int vrh_group_broadcast_scene(uint32_t n, vrh_group* const* groups, const vrh_scene* root_scene, vrh_scene** out)
+{
+    VRH_CHECK(n >= 1 && groups && out, "vrh_group_broadcast_scene: null argument");
+    int root = -1;
+    for (uint32_t i = 0; i < n; ++i)
+    {
+        VRH_CHECK(groups[i] && groups[i]->nranks == groups[0]->nranks, "vrh_group_broadcast_scene: groups of one communicator");
+        out[i] = nullptr;
+        if (groups[i]->rank == 0) root = int(i);
+    }
+    VRH_CHECK(root < 0 || (root_scene && root_scene->ctx == groups[root]->ctx),
+              "vrh_group_broadcast_scene: rank 0 passes its scene, on its context");
+    // 1. the header, from rank 0's host to every member (a small device buffer per member)
+    scene_header h{};
+    if (root >= 0)
+    {
+        vrh_scene* rs = const_cast<vrh_scene*>(root_scene);
+        void* a[7];
+        scene_arrays(rs, a);
+        for (int k = 0; k < 7; ++k)
+        {
+            const int rc = array_bytes(a[k], h.bytes[k]);
+            if (rc) return rc;
+        }
+        std::memcpy(h.roots, rs->roots, sizeof(h.roots));
+        h.num_roots = rs->num_roots; h.num_pairs = rs->num_pairs; h.quad_depth = rs->quad_depth;
+        h.finite_bounds = rs->finite_bounds ? 1u : 0u;
+        h.info = rs->info;
+        // the scene's own uploads / builds on its context stream finish before the broadcast reads it
+        VRH_HIP(hipSetDevice(rs->ctx->device));
+        VRH_HIP(hipStreamSynchronize(rs->ctx->stream));
+    }
+    std::vector<scene_header*> dh(n, nullptr);
+    auto free_headers = [&]() { for (uint32_t i = 0; i < n; ++i) if (dh[i]) { (void)hipSetDevice(groups[i]->ctx->device); (void)hipFree(dh[i]); } };
+    int rc = VRH_OK;
+    for (uint32_t i = 0; i < n && rc == VRH_OK; ++i)
+    {
+        vrh_group* g = groups[i];
+        if (hipSetDevice(g->ctx->device) != hipSuccess || hipMalloc(&dh[i], sizeof(scene_header)) != hipSuccess ||
+            (int(i) == root && hipMemcpy(dh[i], &h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess))
+        { set_error("vrh_group_broadcast_scene: header buffer"); rc = VRH_ERR_HIP; }
+    }
+    if (rc == VRH_OK)
+    {
+        ncclResult_t r = ncclGroupStart();
+        for (uint32_t i = 0; i < n && r == ncclSuccess; ++i)
+            r = ncclBroadcast(dh[i], dh[i], sizeof(scene_header), ncclUint8, 0, groups[i]->comm, groups[i]->stream);
+        const ncclResult_t r2 = ncclGroupEnd();
+        if (r == ncclSuccess) r = r2;
+        if (r != ncclSuccess) { set_error(std::string("vrh_group_broadcast_scene: header: ") + ncclGetErrorString(r)); rc = VRH_ERR_HIP; }
+    }
+    std::vector<scene_header> hh(n);
+    for (uint32_t i = 0; i < n && rc == VRH_OK; ++i)
+    {
+        vrh_group* g = groups[i];
+        if (hipSetDevice(g->ctx->device) != hipSuccess || hipStreamSynchronize(g->stream) != hipSuccess ||
+            hipMemcpy(&hh[i], dh[i], sizeof(scene_header), hipMemcpyDeviceToHost) != hipSuccess)
+        { set_error("vrh_group_broadcast_scene: header download"); rc = VRH_ERR_HIP; }
+    }
+    free_headers();
+    if (rc) return rc;
+    // 2. every member allocates its replica (rank 0 too: the replica is a new scene everywhere)
+    auto free_out = [&]() { for (uint32_t i = 0; i < n; ++i) { vrh_scene_free(out[i]); out[i] = nullptr; } };
+    for (uint32_t i = 0; i < n; ++i)
+        VRH_CHECK(hh[i].num_roots >= 1 && hh[i].num_roots <= vrh::MAX_LIST, "vrh_group_broadcast_scene: bad header");
+    for (uint32_t i = 0; i < n; ++i)
+    {
+        const scene_header& x = hh[i];
+        auto* sc = new (std::nothrow) vrh_scene;
+        if (!sc) { free_out(); set_error("host allocation failed"); return VRH_ERR_OOM; }
+        out[i] = sc;
+        sc->ctx = groups[i]->ctx;
+        std::memcpy(sc->roots, x.roots, sizeof(sc->roots));
+        sc->num_roots = x.num_roots; sc->num_pairs = x.num_pairs; sc->quad_depth = x.quad_depth;
+        sc->finite_bounds = x.finite_bounds != 0;
+        sc->info = x.info;
+        void** dst[7] = { reinterpret_cast<void**>(&sc->pairs), reinterpret_cast<void**>(&sc->prims),
+                          reinterpret_cast<void**>(&sc->normals), reinterpret_cast<void**>(&sc->quads),
+                          reinterpret_cast<void**>(&sc->vnormals), reinterpret_cast<void**>(&sc->dnodes),
+                          reinterpret_cast<void**>(&sc->dindices) };
+        if (hipSetDevice(sc->ctx->device) != hipSuccess) { free_out(); set_error("hipSetDevice"); return VRH_ERR_HIP; }
+        for (int k = 0; k < 7; ++k)
+            if (x.bytes[k])
+            {
+                const hipError_t e = hipMalloc(dst[k], x.bytes[k]);
+                if (e != hipSuccess)
+                {
+                    free_out();
+                    set_error(std::string("vrh_group_broadcast_scene: hipMalloc: ") + hipGetErrorString(e));
+                    return e == hipErrorOutOfMemory ? VRH_ERR_OOM : VRH_ERR_HIP;
+                }
+            }
+    }
+    // 3. the arrays: one broadcast per array from rank 0's scene into every replica
+    {
+        void* src[7] = {};
+        if (root >= 0) scene_arrays(const_cast<vrh_scene*>(root_scene), src);
+        ncclResult_t r = ncclGroupStart();
+        for (uint32_t i = 0; i < n && r == ncclSuccess; ++i)
+        {
+            void* d[7];
+            scene_arrays(out[i], d);
+            for (int k = 0; k < 7 && r == ncclSuccess; ++k)
+                if (hh[i].bytes[k])
+                    r = ncclBroadcast(int(i) == root ? src[k] : d[k], d[k], hh[i].bytes[k], ncclUint8, 0, groups[i]->comm,
+                                      groups[i]->stream);
+        }
+        const ncclResult_t r2 = ncclGroupEnd();
+        if (r == ncclSuccess) r = r2;
+        if (r != ncclSuccess) { free_out(); set_error(std::string("vrh_group_broadcast_scene: ") + ncclGetErrorString(r)); return VRH_ERR_HIP; }
+    }
+    for (uint32_t i = 0; i < n; ++i)
+    {
+        if (hipSetDevice(groups[i]->ctx->device) != hipSuccess || hipStreamSynchronize(groups[i]->stream) != hipSuccess)
+        { free_out(); set_error("vrh_group_broadcast_scene: sync"); return VRH_ERR_HIP; }
+    }
+    return VRH_OK;
+}
+
 
 } // extern "C"
