@@ -86,7 +86,8 @@ def test_batch_spheres(ctx, n):
     check_batch(ctx, "sph5000", 256, 144, "primary", n)
 
 
-@pytest.mark.parametrize("opts", [{"ao_schedule": 3}, {"refill_min": 1}, {"xcd_queues": 2}, {"wide_anyhit": 1}])
+@pytest.mark.parametrize("opts", [{"ao_schedule": 3}, {"refill_min": 1}, {"xcd_queues": 2}, {"xcd_queues": 1},
+                                  {"wide_anyhit": 1}])
 def test_batch_under_other_schedules(ctx, opts):
     for k, v in opts.items():
         ctx.set_option(k, v)

@@ -20,6 +20,7 @@ VARIANTS = {
     "step": {"ao_schedule": 3},
     "refill1": {"refill_min": 1},
     "global_queue": {"xcd_queues": 2},
+    "band_interleaved_queues": {"xcd_queues": 3},
     "step_wide": {"ao_schedule": 3, "wide_anyhit": 1},
     "step_wide_exact": {"ao_schedule": 3, "wide_anyhit": 1, "exact_minmax": 1},
     "step_cap1": {"ao_schedule": 3, "descent_cap": 1},

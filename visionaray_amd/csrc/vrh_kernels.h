@@ -70,7 +70,8 @@ struct render_params
     // count_lines) -- [0, COUNTERS_FRAME) reset per frame -- [COUNTERS_TOTAL + 0/1] total rays / hits
     // since vrh_stats_reset
     unsigned long long* counters;
-    uint32_t xcd_queues;      // 1: per-XCD tile queues with stealing; 0: one global queue
+    uint32_t xcd_queues;      // 1: per-XCD tile queues (strips) with stealing; 2: per-XCD queues over
+                              // band-interleaved (band, frame) units; 0: one global queue
     uint32_t refill_min;      // retire / refill once this many lanes are free (AO step loop)
     uint32_t refill_min_primary;   // the same for the step loop's primary-only stream
     uint32_t ao_gate;         // AO step loop: a tile's AO rays are handed out once its primaries are done

@@ -174,9 +174,13 @@ __device__ __forceinline__ void put_color(const render_params& P, size_t o, floa
     P.color[o] = c;
 }
 
-// Tile work queues.  A frame's tiles are split into 8 contiguous ranges (horizontal image strips);
-// queue q hands out strip q of frame 0, then strip q of frame 1, ... (frames of one launch,
-// vrh_render_batch).  A wave first drains the queue of the XCD it runs on (hardware register
+// Tile work queues.  One frame per launch: a frame's tiles are split into 8 contiguous ranges
+// (horizontal image strips), queue q hands out strip q.  Frames in flight (vrh_render_batch): the
+// launch's (band, frame) units go round robin to the queues in band-major order, so the 8 XCDs
+// sweep the image together, each on other frames of the same bands (+4 % hf10M AO, +10 % hf10M
+// primary against strip q of every frame per queue, profiles/r02_ab/ab28_tile_order_*.log: the
+// MALL then holds the bands' working set once for all XCDs).  A wave first drains the queue of the
+// XCD it runs on (hardware register
 // XCC_ID), so the BVH nodes of a strip stay in that XCD's L2, then steals from the other queues in
 // turn -- a wave never idles while another frame of the launch still has tiles.  Which XCD a wave
 // lands on only changes speed: every (frame, tile) is handed out exactly once by one of the 8
@@ -209,6 +213,33 @@ __device__ __forceinline__ uint32_t strip_lo(const render_params& P, uint32_t q,
 __device__ __forceinline__ uint32_t next_tile(const render_params& P, tile_queue& tq, uint32_t lane)
 {
     const uint32_t nq = P.xcd_queues ? 8u : 1u;
+    if (P.xcd_queues == 2u)
+    {
+        // band-interleaved (frames in flight): the launch's (band, frame) units in band-major order,
+        // unit u = band * num_frames + frame dealt to queue u % 8 -- all 8 XCDs sweep the image's
+        // bands together, each on other frames of the same band, so the nodes and triangles under
+        // a band are fetched from HBM once for every XCD and frame in flight (the MALL and each
+        // L2 hold the band's working set) instead of once per XCD strip
+        const uint32_t tx = P.tiles_x;
+        const uint32_t units = (P.num_tiles / tx) * P.num_frames;
+        while (tq.tried < 8u)
+        {
+            uint32_t t = 0;
+            if (lane == 0) t = atomicAdd(reinterpret_cast<uint32_t*>(P.counters + 8u + 8u * tq.q), 1u);
+            t = __shfl(t, 0);
+            const uint32_t k = t / tx;
+            const uint32_t u = k * 8u + tq.q;
+            if (u < units)
+            {
+                const uint32_t band = u / P.num_frames;
+                const uint32_t f = u - band * P.num_frames;
+                return (f << TILE_FRAME_SHIFT) | (band * tx + (t - k * tx));
+            }
+            tq.q = (tq.q + 1u) & 7u;
+            tq.tried += 1u;
+        }
+        return NONE;
+    }
     while (tq.tried < nq)
     {
         const uint32_t lo = strip_lo(P, tq.q, nq);

@@ -144,7 +144,7 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
     case VRH_OPT_BLOCKS_PER_CU: ctx->opt_bpc = int(value); break;
     case VRH_OPT_WAVES_PER_SIMD: VRH_CHECK(value == 0 || value == 1 || value == 5 || value == 6 || value == 8, "vrh_ctx_set_option: waves per SIMD is 1, 5, 6 or 8"); ctx->opt_occ = int(value); break;
     case VRH_OPT_EXACT_MINMAX: ctx->opt_exact_minmax = value ? 1 : 0; break;
-    case VRH_OPT_XCD_QUEUES: VRH_CHECK(value <= 2, "vrh_ctx_set_option: xcd queues is 1 (on) or 2 (off)"); ctx->opt_xcd_queues = int(value); break;
+    case VRH_OPT_XCD_QUEUES: VRH_CHECK(value <= 3, "vrh_ctx_set_option: xcd queues is 1 (strips), 2 (off) or 3 (band-interleaved)"); ctx->opt_xcd_queues = int(value); break;
     default: set_error("vrh_ctx_set_option: unknown option"); return VRH_ERR_INVALID;
     }
     return VRH_OK;
@@ -1097,7 +1097,9 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     VRH_CHECK(uint64_t(p.num_tiles) * 64u * num_frames < (1ull << 32) && p.num_tiles < (1u << 26), "vrh_render: image too large");
     p.color = rt->color; p.prim_id = rt->prim_id; p.t = rt->t; p.occ = rt->occ;
     p.counters = ctx->counters;
-    p.xcd_queues = ctx->opt_xcd_queues == 2 ? 0u : 1u;
+    // tile queues: per-XCD strips; with frames in flight the band-interleaved order (auto)
+    p.xcd_queues = ctx->opt_xcd_queues == 2 ? 0u : ctx->opt_xcd_queues == 1 ? 1u
+                 : ctx->opt_xcd_queues == 3 ? 2u : (num_frames > 1 ? 2u : 1u);
     if (shade)
     {
         p.shade.materials = k->shading->materials;
