@@ -37,4 +37,11 @@ ab30)
   export VRH_AB='[{"name":"warm-up"},{"name":"strips (auto)"},{"name":"band-interleaved","xcd_queues":3},{"name":"strips again","xcd_queues":1},{"name":"band-interleaved again","xcd_queues":3}]'
   SCENES="hf1M hf10M" KERNEL=ao BATCH=1 REPS=1 ROUNDS=5 bash tools/ab_builds.sh > gpurun_out/ab30_tile_order_f1_ao.log 2>&1 || exit $?
   SCENES="sph1M hf1M" KERNEL=primary BATCH=1 REPS=1 ROUNDS=5 bash tools/ab_builds.sh > gpurun_out/ab30_tile_order_f1_primary.log 2>&1 ;;
+ab31)
+  # tile order with frames in flight and a moving camera (0.5 deg of orbit per frame): no two frames
+  # of a launch share primary rays, so band-interleaving gets no credit from coinciding frames
+  export VRH_AB='[{"name":"warm-up"},{"name":"band-interleaved (auto)"},{"name":"strips","xcd_queues":1},{"name":"band-interleaved again","xcd_queues":3},{"name":"strips again","xcd_queues":1}]'
+  export VRH_AB_ORBIT=0.5
+  SCENES="hf1M hf10M" KERNEL=ao REPS=1 ROUNDS=3 bash tools/ab_builds.sh > gpurun_out/ab31_tile_order_orbit_ao.log 2>&1 || exit $?
+  SCENES="hf1M hf10M" KERNEL=primary REPS=1 ROUNDS=3 bash tools/ab_builds.sh > gpurun_out/ab31_tile_order_orbit_primary.log 2>&1 ;;
 esac

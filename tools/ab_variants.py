@@ -4,6 +4,9 @@
 Each variant is also checked bit-exactly (prim_id / occ / colour hashes) against tests/golden.
 VRH_AB_BATCH = frames per launch (default 20, as the driver's bench command); times are per frame.
 Frame numbers advance with every frame (distinct AO samples); the parity check renders frame 0.
+VRH_AB_ORBIT = degrees the camera orbits the scene centre per frame (default 0: every frame of a
+launch shares the camera, as bench.py's frames do); with it, no two frames of a launch trace the
+same primary rays.
 """
 import json
 import os
@@ -47,15 +50,35 @@ ctx = va.Context(0)
 dev = va.hip_index_bvh(ctx, host, scenes.normals_for(prims))
 cam, W, H = scenes.scene_camera(scene)
 basis = cam.basis(W, H)
+ORBIT = float(os.environ.get("VRH_AB_ORBIT", "0"))
+
+
+def frame_bases(first, n):
+    """Camera of frames first..first+n-1: the scene camera orbited ORBIT degrees per frame about +y."""
+    if ORBIT == 0.0:
+        return [basis] * n
+    out = []
+    ex, ey, ez = cam.eye
+    for i in range(n):
+        a = np.radians(ORBIT * (first + i))
+        c = va.camera()
+        c.perspective(cam.fovy, cam.aspect, 0.001, 1000.0)
+        c.look_at((ex * np.cos(a) + ez * np.sin(a), ey, -ex * np.sin(a) + ez * np.cos(a)), cam.center, cam.up)
+        out.append(c.basis(W, H))
+    return out
+
+
 ao = prims.dtype == va.TRIANGLE_DTYPE and os.environ.get("VRH_AB_KERNEL", "ao") == "ao"
 kern = va.ao_kernel(dev) if ao else va.closest_hit_kernel(dev)
 F = int(os.environ.get("VRH_AB_BATCH", "20"))
 rt = va.hip_buffer_rt(ctx, W, H * F)
+say(f"orbit {ORBIT} deg/frame, {F} frames per launch")
 say(f"scene {scene} {len(prims)} prims depth {host.max_depth} ao={ao} wide records {dev.info['wide_records']} "
     f"(depth {dev.info['wide_depth']})")
 OPTIONS = ("block_threads", "stack_cap", "ao_schedule", "blocks_per_cu", "waves_per_simd", "exact_minmax", "xcd_queues", "ao_gate",
            "refill_min", "wide_anyhit", "descent_cap", "pop_on_miss", "coop_fetch", "scalar_fetch")
 res = {v["name"]: [] for v in VARIANTS}
+bases = [frame_bases(1 + k * F, F) for k in range(3)]     # the same camera path for every variant
 one = va.hip_buffer_rt(ctx, W, H)
 frame = 1
 for rnd in range(rounds):
@@ -64,7 +87,7 @@ for rnd in range(rounds):
             ctx.set_option(o, v.get(o, 0))
         ctx.stats_reset()
         for _ in range(3):                       # distinct frame numbers: every frame its own AO samples
-            va.render_batch(ctx, dev, rt, [basis] * F, kern, frame_num=frame)
+            va.render_batch(ctx, dev, rt, bases[_], kern, frame_num=frame)
             frame += F
         a = ctx.accum_stats()
         st = ctx.last_frame_stats()

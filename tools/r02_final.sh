@@ -3,7 +3,7 @@
 # tests, smoke, the driver's bench command, PMC passes at 20 and 32 frames per launch, kernel trace;
 # the L1 roof is not re-measured) and bench.py on C2 / C4 / C5.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-export OUT=gpurun_out/r02_final SKIP_MICRO=1
+export OUT=${OUT:-gpurun_out/r02_final} SKIP_MICRO=1
 bash tools/r02_session.sh || exit $?
 for s in "hf1M --kernel primary" "hf10M" "sph1M"; do
   n=$(echo $s | tr ' ' '_' | tr -d '-')
