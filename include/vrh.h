@@ -228,7 +228,7 @@ enum vrh_option {
                                     min/max where provably identical, see vrh_device.h)           */
     VRH_OPT_XCD_QUEUES = 7,      /* tile queues: 1 = one per XCD (image strips) with stealing,
                                     2 = one global queue, 3 = one per XCD over band-interleaved
-                                    (band, frame) units (auto: 3 with frames in flight, else 1)   */
+                                    (band, frame) units (auto: 3 with frames in flight for AO or scenes > 256 MB, else 1) */
     VRH_OPT_REFILL_MIN = 8,      /* free lanes (1..64) before finished rays are retired and idle
                                     lanes refilled (auto: 32)                                     */
     VRH_OPT_WIDE_ANYHIT = 10,    /* 4-wide node records for any-hit (AO / shadow) rays (step

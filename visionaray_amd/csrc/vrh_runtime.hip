@@ -1097,9 +1097,14 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     VRH_CHECK(uint64_t(p.num_tiles) * 64u * num_frames < (1ull << 32) && p.num_tiles < (1u << 26), "vrh_render: image too large");
     p.color = rt->color; p.prim_id = rt->prim_id; p.t = rt->t; p.occ = rt->occ;
     p.counters = ctx->counters;
-    // tile queues: per-XCD strips; with frames in flight the band-interleaved order (auto)
+    // tile queues: per-XCD strips; with frames in flight the band-interleaved order (auto) for AO
+    // and for scenes larger than the 256 MB Infinity Cache.  Measured with a camera orbiting 0.5 deg
+    // per frame (profiles/r02_ab/ab31_tile_order_orbit_*.log): band order hf10M AO +3.5 %, hf10M
+    // primary +10 %, hf1M AO +0.3 %, but hf1M primary -2.8 % (its scene fits the MALL, and a
+    // strip's primaries then keep their XCD's L2); one-frame launches keep strips (ab30)
+    const bool band_auto = num_frames > 1 && (lc.ao || sc->info.device_bytes > (256ull << 20));
     p.xcd_queues = ctx->opt_xcd_queues == 2 ? 0u : ctx->opt_xcd_queues == 1 ? 1u
-                 : ctx->opt_xcd_queues == 3 ? 2u : (num_frames > 1 ? 2u : 1u);
+                 : ctx->opt_xcd_queues == 3 ? 2u : (band_auto ? 2u : 1u);
     if (shade)
     {
         p.shade.materials = k->shading->materials;
