@@ -19,6 +19,8 @@ Frames in flight: the K timed frames run as K / F persistent launches of F frame
 tail is paid once per launch.  `value` is K frames' rays over the wall time of the timed region.
 The hip_sched::frame path -- one synchronous launch per frame, as the reference's scheduler
 issues frames -- is measured separately over --single-frames frames (median): single_frame_*.
+The timed frames share the scene camera (their AO samples differ); moving_camera_* repeats the
+timed launches with the eye orbiting --moving-camera degrees per frame (no shared primary rays).
 
 N > 1: one process per GPU, one libvrh render group over RCCL (vrh_group_join, the id broadcast
 by torch.distributed): each rank renders its image-tile shard (8-row bands, band b -> rank b % N,
@@ -70,6 +72,8 @@ def parse():
     ap.add_argument("--frames-in-flight", type=int, default=32,
                     help="max frames per persistent launch (vrh_render_batch, 1..32)")
     ap.add_argument("--single-frames", type=int, default=10, help="frames of the hip_sched::frame leg (median)")
+    ap.add_argument("--moving-camera", type=float, default=0.5,
+                    help="degrees of camera orbit per frame in the moving-camera leg (0: skip the leg)")
     ap.add_argument("--gather-ids", action="store_true",
                     help="N > 1 / --shards: gather prim ids + AO masks with the colour (5 B per pixel on the wire, not 1)")
     ap.add_argument("--shards", type=int, default=0,
@@ -325,6 +329,29 @@ def main():
                   "path": "hip_sched::frame -> vrh_render + vrh_sync (one launch per frame)"}
         rt_s.close()
 
+    # ---- moving-camera leg (N = 1, untimed by the driver's clock): the timed launches' shape with
+    # the eye orbiting --moving-camera degrees per frame, so no two frames of a launch share primary
+    # rays (the timed frames share the scene camera, as the reference viewer's frames do at rest)
+    moving = None
+    if world == 1 and not grouped and args.moving_camera > 0:
+        nl = 3
+        bases = scenes.orbit_bases(args.scene, args.moving_camera, F * nl)
+        rt_m = target(F)
+        va.render_batch(ctx, dev, rt_m, bases[:F], kern, None, frame_num=next_frame[0])   # warm-up
+        next_frame[0] += F
+        sync()
+        ctx.stats_reset()
+        for k in range(nl):
+            va.render_batch(ctx, dev, rt_m, bases[k * F:(k + 1) * F], kern, None, frame_num=next_frame[0])
+            next_frame[0] += F
+        sync()
+        am = ctx.accum_stats()
+        moving = {"degrees_per_frame": args.moving_camera, "frames_per_launch": F, "launches": nl,
+                  "kernel_ms_per_frame": round(am["kernel_ms_total"] / (nl * F), 4),
+                  "mrays_kernel": round(am[rays_key] / am["kernel_ms_total"] / 1e3, 3),
+                  "what": "same launches as the timed region, eye orbiting the scene centre per frame "
+                          "(scenes.orbit_bases); kernel time from hipEvents"}
+
     # ---- aggregate over ranks -------------------------------------------------------------------
     local_vals = torch.tensor([elapsed, float(acc[rays_key]), acc["kernel_ms_total"], float(acc["timed_frames"])],
                               dtype=torch.float64, device="cuda")
@@ -421,6 +448,8 @@ def main():
             },
             "single_frame": single,
             "single_frame_mrays": single["mrays_kernel"] if single else None,
+            "moving_camera": moving,
+            "moving_camera_mrays": moving["mrays_kernel"] if moving else None,
             "cpu_baseline": cpu,
             "host_build_s": round(build_s, 3),
             "verify": verify,

@@ -57,15 +57,7 @@ def frame_bases(first, n):
     """Camera of frames first..first+n-1: the scene camera orbited ORBIT degrees per frame about +y."""
     if ORBIT == 0.0:
         return [basis] * n
-    out = []
-    ex, ey, ez = cam.eye
-    for i in range(n):
-        a = np.radians(ORBIT * (first + i))
-        c = va.camera()
-        c.perspective(cam.fovy, cam.aspect, 0.001, 1000.0)
-        c.look_at((ex * np.cos(a) + ez * np.sin(a), ey, -ex * np.sin(a) + ez * np.cos(a)), cam.center, cam.up)
-        out.append(c.basis(W, H))
-    return out
+    return scenes.orbit_bases(scene, ORBIT, first + n, W, H)[first:]
 
 
 ao = prims.dtype == va.TRIANGLE_DTYPE and os.environ.get("VRH_AB_KERNEL", "ao") == "ao"
