@@ -248,6 +248,10 @@ enum vrh_option {
     VRH_OPT_WAVE_TIMES = 19,     /* 1: the step-loop kernels record every wave's start / end time
                                     (wall_clock64) for vrh_get_wave_times -- a launch-timeline
                                     diagnostic (0 = off, the default)                              */
+    VRH_OPT_AO_CUT = 20,         /* AO step loop: any-hit rays start below the top of the 4-wide tree,
+                                    at a per-tile cut of at most 8 records whose boxes meet the
+                                    tile's AO reach (every hit position +- eps + radius): 1 = on,
+                                    2 = off (auto: on)                                             */
     VRH_OPT_PAIR_LAYOUT = 15,    /* scene upload (read by vrh_scene_upload): 1 = node pairs in
                                     depth-first preorder, a pair's child-0 pair next to it in one
                                     128-B line; 2 = the builder's order (auto: 2; 1 measured

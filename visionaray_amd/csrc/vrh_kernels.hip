@@ -36,7 +36,15 @@ constexpr int AO_REC_WORDS = 4;                         // pos xyz, prim id (its
                                                         // 512 B less LDS per wave = 24 instead of 22 waves/CU)
 constexpr int AO_MASKS = 64 * AO_REC_WORDS;             // u32 masks[2][64]
 constexpr int AO_SLOT_PX = AO_MASKS + 2 * 64;           // u8 slot_px[2][64]: pixel (lane) of a hit slot
-constexpr int AO_WAVE_WORDS = AO_SLOT_PX + 2 * 64 / 4;
+#ifndef VRH_AO_CUT
+#define VRH_AO_CUT 1    // compile the AO entry cut in (render_params::ao_cut switches it per launch)
+#endif
+constexpr int AO_CUT = AO_SLOT_PX + 2 * 64 / 4;         // the current tile's entry cut (ao_cut_build)
+#ifndef VRH_AO_CUT_MAX
+#define VRH_AO_CUT_MAX 8
+#endif
+constexpr uint32_t CUT_MAX = VRH_AO_CUT_MAX;            // records of a cut
+constexpr int AO_WAVE_WORDS = AO_CUT + 2 * 8 * CUT_MAX; // two levels x entries of box lo xyz, hi xyz, link, pad
 
 // tile id (next_tile: frame f << TILE_FRAME_SHIFT | tile of that frame) -> (x, y) of lane, plus the
 // output row (frame f's rows start at f * frame_rows; packed shards).  A band is one row of tiles.
@@ -280,6 +288,128 @@ __device__ __forceinline__ ray_t ao_ray(const render_params& P, const float* rec
     f3 bu = cross(bv, n);
     f3 d = ao_direction(p, s, bu, bv, n, frame_salt(P.frame_num + f));
     return make_ray(pos + d * P.eps, d);
+}
+
+// Entry cut of the 4-wide any-hit tree for the AO rays of one tile (render_params::ao_cut).
+// R = the box of the tile's hit positions grown by the AO reach (eps + radius, plus a margin of
+// 1e-4 (1 + |coordinate|), orders of magnitude above the float error of a slab test).  Starting at
+// the root, every record of the frontier is replaced by its children whose boxes meet R, level by
+// level, while the frontier holds at most CUT_MAX entries.  An AO ray then starts with the cut
+// entries whose boxes it passes (quad_entry, the test its parent record would apply) on its stack.
+// Exact: (1) a leaf the any-hit traversal reaches passes its own box test, so its box comes within
+// float error of the ray segment, which lies in R -- the leaf box, and every ancestor box (they
+// contain it), meets R, so the leaf lies under a cut entry; (2) the slab test is monotone in the box
+// bounds under round-to-nearest, so a ray that passes a cut entry's box passes every ancestor's, and
+// the traversal from the root would reach that entry too.  Both traversals therefore reach the same
+// leaves, and an any-hit result does not depend on the order.  Returns the
+// number of entries written to `cut` (0: no AO ray of the tile can reach a leaf), or NONE when the
+// root's children do not fit (the rays then start at the root).
+__device__ __forceinline__ float wave_min(float v)
+{
+    for (int o = 32; o >= 1; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v)
+{
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+// The cut is built with wave-uniform values only: records through the scalar cache (s_load on a
+// wave-uniform address, as ray_step's uniform pair fetch), frontier entries in LDS (two halves,
+// one level each), so it needs no vector registers beyond the rays the other lanes are tracing.
+typedef const __attribute__((address_space(4))) float cut_cfloat;
+__device__ __forceinline__ float ufl(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
+__device__ __forceinline__ uint32_t uu(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+// the children of 4-wide record `k` whose boxes meet [lo, hi] (bit c = entry c)
+__device__ __forceinline__ uint32_t cut_children(const float4* quads, uint32_t k, const float* lo, const float* hi)
+{
+    cut_cfloat* q = (cut_cfloat*)(const float*)(quads) + 32u * k;
+    uint32_t m = 0u;
+#pragma unroll
+    for (uint32_t c = 0; c < 4u; ++c)
+    {
+        const bool meet = (__float_as_uint(q[24u + c]) != QUAD_NONE) & (q[c] <= hi[0]) & (q[12u + c] >= lo[0])
+                        & (q[4u + c] <= hi[1]) & (q[16u + c] >= lo[1]) & (q[8u + c] <= hi[2]) & (q[20u + c] >= lo[2]);
+        m |= meet ? (1u << c) : 0u;
+    }
+    return uu(m);
+}
+template <bool COUNT>
+__device__ __forceinline__ uint32_t ao_cut_build(const render_params& P, const float* recs, uint32_t nslots, float* cut,
+                                                 uint32_t lane, test_counts& cnt)
+{
+    const bool v = lane < nslots;
+    float lo[3], hi[3];
+    float mag = 0.0f;
+    for (int a = 0; a < 3; ++a)
+    {
+        const float x = recs[(v ? lane : 0u) * AO_REC_WORDS + a];
+        lo[a] = ufl(wave_min(v ? x : INFINITY));
+        hi[a] = ufl(wave_max(v ? x : -INFINITY));
+        mag = fmaxf(mag, fmaxf(fabsf(lo[a]), fabsf(hi[a])));
+    }
+    const float ext = ufl((P.eps + P.radius) * 1.001f + 1e-4f * (1.0f + mag));
+    if (!(ext < INFINITY)) return NONE;
+    for (int a = 0; a < 3; ++a) { lo[a] -= ext; hi[a] += ext; }
+    auto put = [&](float* e, cut_cfloat* q, uint32_t c) {           // entry c of record q -> e
+        if (lane < 7u) e[lane] = q[lane < 6u ? 4u * lane + c : 24u + c];
+    };
+    // level 0: the root record's children
+    float* cur = cut;
+    float* nxt = cut + 8u * CUT_MAX;
+    {
+        const uint32_t ok = cut_children(P.quads, 0u, lo, hi);
+        cut_cfloat* q = (cut_cfloat*)(const float*)(P.quads);
+        uint32_t n = 0;
+        for (uint32_t c = 0; c < 4u; ++c)
+            if (ok & (1u << c)) { put(cur + 8u * n, q, c); n += 1u; }
+        if (COUNT && lane == 0u) cnt.box += 4u;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        // deeper levels while the frontier fits
+#pragma unroll 1
+        for (uint32_t level = 0; level < 32u; ++level)
+        {
+            uint32_t total = 0, inner = 0;
+#pragma unroll 1
+            for (uint32_t j = 0; j < n; ++j)
+            {
+                const uint32_t k = uu(__float_as_uint(cur[8u * j + 6u]));
+                if (k & LEAF_BIT) { total += 1u; continue; }
+                inner += 1u;
+                total += (uint32_t)__popc(cut_children(P.quads, k, lo, hi));
+            }
+            if (inner == 0u || total > CUT_MAX) break;
+            uint32_t o = 0;
+#pragma unroll 1
+            for (uint32_t j = 0; j < n; ++j)
+            {
+                const uint32_t k = uu(__float_as_uint(cur[8u * j + 6u]));
+                if (k & LEAF_BIT)
+                {
+                    if (lane < 7u) nxt[8u * o + lane] = cur[8u * j + lane];
+                    o += 1u;
+                    continue;
+                }
+                const uint32_t ok = cut_children(P.quads, k, lo, hi);
+                if (COUNT && lane == 0u) cnt.box += 4u;
+                cut_cfloat* q = (cut_cfloat*)(const float*)(P.quads) + 32u * k;
+                for (uint32_t c = 0; c < 4u; ++c)
+                    if (ok & (1u << c)) { put(nxt + 8u * o, q, c); o += 1u; }
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            float* t = cur; cur = nxt; nxt = t;
+            n = total;
+        }
+        if (cur != cut)
+        {
+            if (lane < 8u * n) cut[lane] = cur[lane];
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        }
+        return n;
+    }
 }
 
 // coalescer model of the output stores of one pixel (counting variant), by buffer: 1 colour,
@@ -548,6 +678,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         float* recs = reinterpret_cast<float*>(ao_area);
         uint32_t* masks = ao_area + AO_MASKS;
         uint8_t* slot_px = reinterpret_cast<uint8_t*>(ao_area + AO_SLOT_PX);
+        float* cut = reinterpret_cast<float*>(ao_area + AO_CUT);
+        uint32_t cutN = NONE;                                 // entries of tile C's cut (NONE: root)
         const float4 bg = make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
         tile_queue tq = queue_init(P);
         // wave-uniform tile state
@@ -602,6 +734,18 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             if (idle && issC < pubC * S && (!P.ao_gate || (pendC == 0u && handedC >= 64u)))
             {
                 const uint32_t avail = pubC * S;
+                // the cut is compiled into the instances for BVHs of depth <= the LDS stack (no SPILL):
+                // measured +5.5 % on hf1M (depth 20), while the deep-BVH instance (hf10M, depth 26)
+                // lost 0.2-0.7 % with it and 1.6 % to its extra registers
+                // (profiles/r02_ab/ab32_ao_cut*.log)
+                constexpr bool CUT = !LIST && !SPILL && VRH_AO_CUT;
+                if constexpr (CUT)
+                    if (P.ao_cut && issC == 0u)
+                    {
+                        // the tile's first AO hand-out: all its hits are published (ao_gate)
+                        cutN = ao_cut_build<COUNT>(P, recs, pubC, cut, lane, cnt);
+                        if (cutN != NONE && cutN + 4u > P.stack_cap) cutN = NONE;
+                    }
                 const uint32_t cand = issC + lane_rank(idle);
                 const uint32_t n = min(avail - issC, (uint32_t)__popcll(idle));
                 if (mode == IDLE && cand < avail)
@@ -614,7 +758,28 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     bk = 0; res_t = FMAX; res_prim = 0;
                     finite = finite_ray(r);
                     quad = P.quad_ok && finite;
-                    st.reset(); st.push(quad ? 0u : P.root); resume = NO_RESUME;
+                    st.reset(); resume = NO_RESUME;
+                    if (!LIST && !SPILL && VRH_AO_CUT && quad && cutN != NONE)
+                    {
+                        // start at the tile's cut: the entries whose boxes this ray passes
+#pragma unroll 1
+                        for (uint32_t j = 0; j < cutN; ++j)
+                        {
+                            // quad_entry's test, one axis at a time (max / min of non-NaN values
+                            // are exact in any order: the same tn / tf, fewer live registers)
+                            const float* e = cut + 8u * j;
+                            float t1 = (e[0] - r.ori.x) * r.inv.x, t2 = (e[3] - r.ori.x) * r.inv.x;
+                            float tn = __builtin_fminf(t1, t2), tf = __builtin_fmaxf(t1, t2);
+                            t1 = (e[1] - r.ori.y) * r.inv.y; t2 = (e[4] - r.ori.y) * r.inv.y;
+                            tn = __builtin_fmaxf(tn, __builtin_fminf(t1, t2)); tf = __builtin_fminf(tf, __builtin_fmaxf(t1, t2));
+                            t1 = (e[2] - r.ori.z) * r.inv.z; t2 = (e[5] - r.ori.z) * r.inv.z;
+                            tn = __builtin_fmaxf(tn, __builtin_fminf(t1, t2)); tf = __builtin_fminf(tf, __builtin_fmaxf(t1, t2));
+                            if ((tf >= tn) & (tn < FMAX) & (tf >= 0.0f) & (tn < max_t)) st.push(__float_as_uint(e[6]));
+                        }
+                        if (COUNT) cnt.box += cutN;
+                    }
+                    else
+                        st.push(quad ? 0u : P.root);
                     mode = AORAY;
                     tag = slot | (smp << 6) | (parC << 11);
                     rays_total += 1;
