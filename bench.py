@@ -20,7 +20,7 @@ tail is paid once per launch.  `value` is K frames' rays over the wall time of t
 The hip_sched::frame path -- one synchronous launch per frame, as the reference's scheduler
 issues frames -- is measured separately over --single-frames frames (median): single_frame_*.
 The timed frames share the scene camera (their AO samples differ); moving_camera_* repeats the
-timed launches with the eye orbiting --moving-camera degrees per frame (no shared primary rays).
+timed launches with the eye orbiting --moving-camera degrees per frame (no shared primary rays; opt-in).
 
 N > 1: one process per GPU, one libvrh render group over RCCL (vrh_group_join, the id broadcast
 by torch.distributed): each rank renders its image-tile shard (8-row bands, band b -> rank b % N,
@@ -72,8 +72,10 @@ def parse():
     ap.add_argument("--frames-in-flight", type=int, default=32,
                     help="max frames per persistent launch (vrh_render_batch, 1..32)")
     ap.add_argument("--single-frames", type=int, default=10, help="frames of the hip_sched::frame leg (median)")
-    ap.add_argument("--moving-camera", type=float, default=0.5,
-                    help="degrees of camera orbit per frame in the moving-camera leg (0: skip the leg)")
+    ap.add_argument("--moving-camera", type=float, default=0.0,
+                    help="degrees of camera orbit per frame in an extra moving-camera leg (0: no such leg, the "
+                         "default, so the kernel's launches in a profile of the default command are the timed "
+                         "shape only; tools/r02_final.sh runs it with 0.5)")
     ap.add_argument("--gather-ids", action="store_true",
                     help="N > 1 / --shards: gather prim ids + AO masks with the colour (5 B per pixel on the wire, not 1)")
     ap.add_argument("--shards", type=int, default=0,

@@ -39,6 +39,8 @@ VARIANTS = {
     "ao_round1": {"ao_gate": 2, "wide_anyhit": 2, "pop_on_miss": 2},
     "ao_gate_binary": {"ao_gate": 1, "wide_anyhit": 2},
     "ao_ungated_wide": {"ao_gate": 2, "wide_anyhit": 1},
+    "ao_cut_off": {"ao_cut": 2},
+    "ao_cut_refill1_cap1": {"ao_cut": 1, "refill_min": 1, "descent_cap": 1},
     # the traversal stack mostly in the global overflow block (4 / 8 LDS entries per lane)
     "stack_lds4": {"stack_cap": 4},
     "stack_lds8_binary": {"stack_cap": 8, "wide_anyhit": 2},
@@ -47,7 +49,7 @@ VARIANTS = {
 }
 OPTIONS = ("ao_schedule", "refill_min", "wide_anyhit", "exact_minmax", "descent_cap", "xcd_queues",
            "pop_on_miss", "scalar_fetch", "waves_per_simd", "pair_layout", "ao_gate",
-           "stack_cap")
+           "stack_cap", "ao_cut")
 
 
 @pytest.fixture(params=sorted(VARIANTS))

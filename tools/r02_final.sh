@@ -10,4 +10,9 @@ for s in "hf1M --kernel primary" "hf10M" "sph1M"; do
   timeout -k 10 300 python bench.py --scene $s --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench_$n.json 2> $OUT/bench_$n.err || { echo "bench $s failed"; exit 1; }
   cut -c1-160 $OUT/bench_$n.json
 done
+# the moving-camera leg (eye orbiting 0.5 deg per frame) on C3 and C4
+for s in "hf1M" "hf10M"; do
+  timeout -k 10 300 python bench.py --scene $s --steps 20 --warmup 5 --no-cpu-baseline --single-frames 0 --moving-camera 0.5 > $OUT/bench_moving_$s.json 2> $OUT/bench_moving_$s.err || { echo "bench moving $s failed"; exit 1; }
+  cut -c1-160 $OUT/bench_moving_$s.json
+done
 exit 0
