@@ -250,8 +250,9 @@ enum vrh_option {
                                     diagnostic (0 = off, the default)                              */
     VRH_OPT_AO_CUT = 20,         /* AO step loop: any-hit rays start below the top of the 4-wide tree,
                                     at a per-tile cut of at most 8 records whose boxes meet the
-                                    tile's AO reach (every hit position +- eps + radius): 1 = on,
-                                    2 = off (auto: on)                                             */
+                                    tile's AO reach (every hit position +- eps + radius), pushed
+                                    so that the entry nearest the tile is popped first: 1 = on,
+                                    2 = off, 3 = on with the entries in cut order (auto: on)      */
     VRH_OPT_PAIR_LAYOUT = 15,    /* scene upload (read by vrh_scene_upload): 1 = node pairs in
                                     depth-first preorder, a pair's child-0 pair next to it in one
                                     128-B line; 2 = the builder's order (auto: 2; 1 measured

@@ -36,7 +36,7 @@ def _check(got, ref, n=None):
 
 
 @pytest.mark.parametrize("radius", [0.002, 0.03, 0.1, 0.6, 8.0])
-@pytest.mark.parametrize("cut", [0, 2])
+@pytest.mark.parametrize("cut", [0, 2, 3])
 def test_ao_cut_matches_oracle(ctx, oracle_mod, scene, radius, cut):
     O = oracle_mod
     dev, cam, osc = scene
@@ -57,4 +57,4 @@ def test_ao_cut_matches_oracle(ctx, oracle_mod, scene, radius, cut):
 
 def test_ao_cut_option_range(ctx):
     with pytest.raises(Exception):
-        ctx.set_option("ao_cut", 3)
+        ctx.set_option("ao_cut", 4)

@@ -75,6 +75,7 @@ struct render_params
     uint32_t refill_min;      // retire / refill once this many lanes are free (AO step loop)
     uint32_t refill_min_primary;   // the same for the step loop's primary-only stream
     uint32_t ao_cut;          // AO step loop: any-hit rays start at the tile's cut of the 4-wide tree
+                              // (1: entries in cut order, 2: nearest-first)
     uint32_t ao_gate;         // AO step loop: a tile's AO rays are handed out once its primaries are done
     unsigned long long* wave_times;   // VRH_OPT_WAVE_TIMES: per wave (start, end) of wall_clock64(), else null
     uint32_t descent_cap;     // step loop: inner visits per step before a descent is resumed later

@@ -402,6 +402,30 @@ __device__ __forceinline__ uint32_t ao_cut_build(const render_params& P, const f
             float* t = cur; cur = nxt; nxt = t;
             n = total;
         }
+        if (P.ao_cut == 2u && n > 1u)
+        {
+            // order the entries by the distance of their box centre to R's centre, farthest first:
+            // the nearest is pushed last and popped first (an AO occluder is usually near the hit)
+            float key = -1.0f;
+            if (lane < n)
+            {
+                const float* e = cur + 8u * lane;
+                const float dx = (e[0] + e[3]) - (lo[0] + hi[0]), dy = (e[1] + e[4]) - (lo[1] + hi[1]);
+                const float dz = (e[2] + e[5]) - (lo[2] + hi[2]);
+                key = dx * dx + dy * dy + dz * dz;
+            }
+            uint32_t rank = 0;
+            for (uint32_t j = 0; j < n; ++j)
+            {
+                const float kj = __shfl(key, (int)j);
+                rank += ((kj > key) | ((kj == key) & (j < lane))) ? 1u : 0u;
+            }
+            for (uint32_t w = 0; w < 7u; ++w)
+                if (lane < n) nxt[8u * rank + w] = cur[8u * lane + w];
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            float* t = cur; cur = nxt; nxt = t;
+        }
         if (cur != cut)
         {
             if (lane < 8u * n) cut[lane] = cur[lane];

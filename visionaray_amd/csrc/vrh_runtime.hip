@@ -136,7 +136,7 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
         if (value == 1) return VRH_ERR_UNSUPPORTED;
         break;
     case VRH_OPT_WAVE_TIMES: VRH_CHECK(value <= 1, "vrh_ctx_set_option: wave times is 1 (on) or 0 (off)"); ctx->opt_wave_times = int(value); break;
-    case VRH_OPT_AO_CUT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: AO cut is 1 (on) or 2 (off)"); ctx->opt_cut = int(value); break;
+    case VRH_OPT_AO_CUT: VRH_CHECK(value <= 3, "vrh_ctx_set_option: AO cut is 1 (on, entries nearest-first), 2 (off) or 3 (on, entries in cut order)"); ctx->opt_cut = int(value); break;
     case VRH_OPT_AO_GATE: VRH_CHECK(value <= 2, "vrh_ctx_set_option: AO gate is 1 (on) or 2 (off)"); ctx->opt_gate = int(value); break;
     case VRH_OPT_POP_ON_MISS: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pop on miss is 1 (on) or 2 (off)"); ctx->opt_pop = int(value); break;
     case VRH_OPT_PAIR_LAYOUT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pair layout is 1 (line pairing) or 2 (builder order)"); ctx->opt_layout = int(value); break;
@@ -1063,7 +1063,8 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     const bool wide = ctx->opt_wide == 1 || (ctx->opt_wide == 0 && ao_step);
     p.quad_ok = (sc->quads && p.fast_ok && wide) ? 1u : 0u;
     // per-tile entry cut of the 4-wide tree for AO rays (needs the gate: the tile's hits are known)
-    p.ao_cut = (p.quad_ok && p.ao_gate && ctx->opt_cut != 2) ? 1u : 0u;
+    // entries nearest-first (+3.5 % over the cut order, profiles/r02_ab/ab33_ao_cut_order*.log)
+    p.ao_cut = (p.quad_ok && p.ao_gate && ctx->opt_cut != 2) ? (ctx->opt_cut == 3 ? 1u : 2u) : 0u;
     for (uint32_t f = 0; f < num_frames; ++f)
     {
         std::memcpy(p.cam[f].eye, cams[f].eye, 12); std::memcpy(p.cam[f].cam_u, cams[f].cam_u, 12);
