@@ -40,6 +40,9 @@ constexpr int AO_SLOT_PX = AO_MASKS + 2 * 64;           // u8 slot_px[2][64]: pi
 #define VRH_AO_CUT 1    // compile the AO entry cut in (render_params::ao_cut switches it per launch)
 #endif
 constexpr int AO_CUT = AO_SLOT_PX + 2 * 64 / 4;         // the current tile's entry cut (ao_cut_build)
+#ifndef VRH_AO_CUT_SPILL
+#define VRH_AO_CUT_SPILL 1   // 0: the cut only in the instances whose stack fits LDS (A/B)
+#endif
 #ifndef VRH_AO_CUT_MAX
 #define VRH_AO_CUT_MAX 8
 #endif
@@ -762,7 +765,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 // measured +5.5 % on hf1M (depth 20), while the deep-BVH instance (hf10M, depth 26)
                 // lost 0.2-0.7 % with it and 1.6 % to its extra registers
                 // (profiles/r02_ab/ab32_ao_cut*.log)
-                constexpr bool CUT = !LIST && !SPILL && VRH_AO_CUT;
+                constexpr bool CUT = !LIST && (!SPILL || VRH_AO_CUT_SPILL) && VRH_AO_CUT;
                 if constexpr (CUT)
                     if (P.ao_cut && issC == 0u)
                     {
@@ -783,7 +786,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     finite = finite_ray(r);
                     quad = P.quad_ok && finite;
                     st.reset(); resume = NO_RESUME;
-                    if (!LIST && !SPILL && VRH_AO_CUT && quad && cutN != NONE)
+                    if (!LIST && (!SPILL || VRH_AO_CUT_SPILL) && VRH_AO_CUT && quad && cutN != NONE)
                     {
                         // start at the tile's cut: the entries whose boxes this ray passes
 #pragma unroll 1
