@@ -761,10 +761,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             if (idle && issC < pubC * S && (!P.ao_gate || (pendC == 0u && handedC >= 64u)))
             {
                 const uint32_t avail = pubC * S;
-                // the cut is compiled into the instances for BVHs of depth <= the LDS stack (no SPILL):
-                // measured +5.5 % on hf1M (depth 20), while the deep-BVH instance (hf10M, depth 26)
-                // lost 0.2-0.7 % with it and 1.6 % to its extra registers
-                // (profiles/r02_ab/ab32_ao_cut*.log)
+                // measured with entries nearest-first: hf1M +9 %, hf10M +4.8 %
+                // (profiles/r02_ab/ab32_*, ab33_*, ab34_ao_cut_spill.log)
                 constexpr bool CUT = !LIST && (!SPILL || VRH_AO_CUT_SPILL) && VRH_AO_CUT;
                 if constexpr (CUT)
                     if (P.ao_cut && issC == 0u)
