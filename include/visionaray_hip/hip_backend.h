@@ -248,6 +248,15 @@ struct hip_bvh_ref
     vrh_scene_view view;
 };
 
+// the typed ref hip_index_bvh<P>::ref() returns (index_bvh_ref_t<P>, bvh.h:190-235): the same view,
+// plus the primitive type, which the reference's traversal templates read as BVH::primitive_type
+// when visionaray_hip/reference.h brings them to the device
+template <typename Primitive>
+struct hip_bvh_ref_t : hip_bvh_ref
+{
+    using primitive_type = Primitive;
+};
+
 //-------------------------------------------------------------------------------------------------
 // hip_index_bvh<P>: device-resident copy of a host index BVH (the cuda_index_bvh copy-ctor)
 //
@@ -319,9 +328,9 @@ public:
 
     // the device BVH a kernel traverses (cuda_index_bvh::ref(), bvh.h:344-350): a plain view of
     // the device arrays, passed by value into user kernels (visionaray_hip/hip_kernels.h)
-    hip_bvh_ref ref() const
+    hip_bvh_ref_t<Primitive> ref() const
     {
-        hip_bvh_ref r{};
+        hip_bvh_ref_t<Primitive> r{};
         hip_detail::check(vrh_scene_get_view(handle(), 0, &r.view), "vrh_scene_get_view");
         return r;
     }

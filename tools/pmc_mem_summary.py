@@ -10,22 +10,34 @@ import os
 import sys
 from collections import defaultdict
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_bench import batched  # noqa: E402
+
+
+def counting(name):
+    """render_unified_kernel<KIND, AO, COUNT, ...> with COUNT = true (bench.py's untimed counting pass)."""
+    args = [a.strip() for a in name.split("render_unified_kernel<", 1)[1].split(">", 1)[0].split(",")]
+    return len(args) > 2 and args[2] == "true"
+
 
 def main():
     d, out = sys.argv[1], sys.argv[2]
     scene = sys.argv[3] if len(sys.argv) > 3 else "hf1M"
     kernel = sys.argv[4] if len(sys.argv) > 4 else "ao"
     fpl = int(sys.argv[5]) if len(sys.argv) > 5 else 8
-    agg = defaultdict(list)
+    rows = []
     for name in sorted(os.listdir(d)):
         p = os.path.join(d, name, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
-        for r in csv.DictReader(open(p)):
-            k = r["Kernel_Name"]
-            if "render_unified_kernel" not in k or "true, true" in k:    # the traversal kernel, not the counting pass
-                continue
-            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        rows += [r for r in csv.DictReader(open(p)) if "render_unified_kernel" in r["Kernel_Name"]
+                 and not counting(r["Kernel_Name"])]             # the traversal kernel, not the counting pass
+    # over bench.py's command: only the frames-in-flight launches (the timed shape), as tools/pmc_bench.py
+    if any(batched(r["Kernel_Name"]) for r in rows):
+        rows = [r for r in rows if batched(r["Kernel_Name"])]
+    agg = defaultdict(list)
+    for r in rows:
+        agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
     c = {k: sum(v) / len(v) for k, v in agg.items()}
     cus = 256
     cycles = c["GRBM_GUI_ACTIVE"] / 8            # GRBM_GUI_ACTIVE is summed over the 8 XCDs
@@ -39,6 +51,7 @@ def main():
         "l1_to_l2_reads_per_access": c["TCP_TCC_READ_REQ_sum"] / c["TCP_TOTAL_CACHE_ACCESSES_sum"],
         "l2_read_latency_cycles": c["TCP_TCC_READ_REQ_LATENCY_sum"] / c["TCP_TCC_READ_REQ_sum"],
         "td_stalled_on_l1_frac": (c["TD_TC_STALL_sum"] / c["TD_TD_BUSY_sum"]) if "TD_TC_STALL_sum" in c else None,
+        "l2_hit_frac": (c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])) if "TCC_HIT_sum" in c else None,
         "l1_pending_stall_frac": (c["TCP_PENDING_STALL_CYCLES_sum"] / (cus * cycles))
                                  if "TCP_PENDING_STALL_CYCLES_sum" in c else None,
         "note": "TA/TD busy = fraction of kernel cycles the vector-memory address / data units of the 256 CUs "
