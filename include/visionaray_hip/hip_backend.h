@@ -255,6 +255,14 @@ template <typename Primitive>
 struct hip_bvh_ref_t : hip_bvh_ref
 {
     using primitive_type = Primitive;
+#if defined(__HIP__)
+    __host__ __device__ size_t num_primitives() const { return view.num_prims; }   // index_bvh_ref_t::num_primitives
+    // primitive i in leaf order (index_bvh_ref_t::primitive, bvh.h:226-229: the device copy holds the
+    // primitives already permuted by the index list), device code; defined in visionaray_hip/hip_kernels.h
+    __host__ __device__ Primitive primitive(size_t i) const;
+#else
+    size_t num_primitives() const { return view.num_prims; }
+#endif
 };
 
 //-------------------------------------------------------------------------------------------------
@@ -266,6 +274,7 @@ class hip_index_bvh
 {
 public:
     using primitive_type = Primitive;
+    using bvh_ref = hip_bvh_ref_t<Primitive>;      // cuda_index_bvh<P>::bvh_ref (bvh.h:344)
     static_assert(hip_detail::is_triangle<Primitive>::value || hip_detail::is_sphere<Primitive>::value,
                   "hip_index_bvh supports basic_triangle<3,float> and basic_sphere<float>");
 

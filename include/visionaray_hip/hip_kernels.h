@@ -3,23 +3,34 @@
 // hip_sched::frame runs the built-in kernels through the C ABI.  A translation unit compiled by
 // hipcc that includes this header can also hand it its OWN kernel -- any callable
 //
-//     result_record<float> kernel(ray r)                    (or (ray, hip_sampler&) / (ray, x, y))
+//     result_record<float> kernel(ray r)     (or (ray, random_sampler<float>&) / (ray, x, y))
 //
 // as cuda_sched runs one (cuda_sched.inl:53-153, sched_common.h:78-120): one GPU thread per pixel of
 // the scissor box, the reference's pinhole primary ray, the returned colour stored in the render
-// target.  Inside, the reference's traversal intrinsics work on the device BVHs:
+// target.  A kernel taking a sampler gets a random_sampler<float> seeded per pixel (below).
+// Inside, the reference's traversal intrinsics work on the device BVHs:
 //
 //     closest_hit(ray, begin, end [, isect])     traverse_linear.inl:286-329
 //     any_hit(ray, begin, end, max_t [, isect])  traverse_linear.inl:232-283
+//     multi_hit<N>(ray, begin, end [, isect])    traverse_linear.inl:333-380 (reference headers)
 //
 // over a range of hip_bvh_ref (hip_index_bvh::ref(), the bvh_ref of bvh.h:344-350) or of plain
 // primitives (basic_triangle<3,float> / basic_sphere<float> arrays in device memory), with the
-// default intersector or a basic_intersector subclass (intersector.h:24-119) -- e.g. the
-// intersector example's mask_intersector (examples/intersector/main.cpp:251-330) compiles unchanged
-// against these types.  The BVH walk is libvrh's (visionaray_hip/detail/vrh_device.h: the 64-B pair
-// records, box_pair's slab test, near child first with ties to child 1, far child pushed, leaf
-// primitives in index order), with the primitive test handed to the intersector, so the default
-// intersector gives the built-in kernels' bits.
+// default intersector or a basic_intersector subclass (intersector.h:24-119).
+//
+// Two vocabularies:
+//   * with visionaray_hip/reference.h included first, the REFERENCE'S OWN headers are device code:
+//     its types, closest_hit / any_hit / multi_hit, update_if, basic_intersector, get_normal,
+//     random_sampler<float>, cosine_sample_hemisphere, kernels<> ...  This header then only adds the
+//     device BVH as one more BVH type of the reference's traversal (is_index_bvh<hip_bvh_ref_t<P>>
+//     and its intersect<Traversal>(), below): a kernel written for cuda_sched compiles unchanged.
+//   * without it, visionaray_hip/standalone.h's minimal restatement of the same names (this header
+//     adds the kernel-side ones: hit records, intersect(), basic_intersector, random_sampler<float>,
+//     cosine_sample_hemisphere, ...), for programs that do not have the Visionaray headers.
+// Either way the BVH walk is libvrh's (visionaray_hip/detail/vrh_device.h: the 64-B pair records,
+// box_pair's slab test, near child first with ties to child 1, far child pushed, leaf primitives in
+// index order), with the primitive test handed to the intersector, so the default intersector gives
+// the built-in kernels' bits.
 //
 // Device lambdas capture by value ([=]): they run on the GPU.  The traversal stack lives in LDS
 // (VRH_USER_STACK entries per thread); BVHs deeper than that are rejected by hip_bvh_ref checks.
@@ -31,7 +42,14 @@
 
 #include <hip/hip_runtime.h>
 
+#if defined(VRH_REFERENCE_HEADERS)
+#include "hip_backend.h"
+#ifndef VRH_FUNC
+#define VRH_FUNC __host__ __device__
+#endif
+#else
 #include "standalone.h"
+#endif
 #include "detail/vrh_device.h"
 
 #include <array>
@@ -52,6 +70,19 @@
 
 namespace visionaray
 {
+
+namespace hip_detail
+{
+__device__ inline vrh::dev::ray_t dev_ray(basic_ray<float> const& r)
+{
+    return vrh::dev::make_ray(vrh::dev::mk3(r.ori.x, r.ori.y, r.ori.z), vrh::dev::mk3(r.dir.x, r.dir.y, r.dir.z));
+}
+} // hip_detail
+
+#if !defined(VRH_REFERENCE_HEADERS)
+// ================================================================================================
+// standalone vocabulary (the reference headers define all of this themselves)
+// ================================================================================================
 
 //-------------------------------------------------------------------------------------------------
 // SIMD vocabulary at width 1 (math/simd/type_traits.h): the reference's kernels are written for
@@ -153,14 +184,6 @@ VRH_FUNC inline std::array<T, 1> unpack(T const& v) { return std::array<T, 1>{ {
 // ray / primitive tests (math/intersect.h:122-221): libvrh's arithmetic, the reference's record
 //
 
-namespace hip_detail
-{
-__device__ inline vrh::dev::ray_t dev_ray(basic_ray<float> const& r)
-{
-    return vrh::dev::make_ray(vrh::dev::mk3(r.ori.x, r.ori.y, r.ori.z), vrh::dev::mk3(r.dir.x, r.dir.y, r.dir.z));
-}
-} // hip_detail
-
 __device__ inline hit_record<basic_ray<float>, primitive<unsigned>> intersect(basic_ray<float> const& ray,
                                                                                basic_triangle<3, float, unsigned> const& tri)
 {
@@ -226,36 +249,96 @@ struct default_intersector : basic_intersector<default_intersector>
 };
 
 //-------------------------------------------------------------------------------------------------
-// BVH traversal with an intersector: intersect<ClosestHit / AnyHit>(ray, bvh, isect)
-// (detail/bvh/intersect.inl:25-134) over libvrh's device layout
+// random_sampler<float> (random_sampler.h:24-57): std::default_random_engine -- libstdc++'s
+// minstd_rand0, x <- 16807 x mod (2^31 - 1), seeded with seed mod (2^31 - 1) (1 for 0) -- under
+// std::uniform_real_distribution<float>(0, 1), i.e. generate_canonical<float, 24> (random.tcc:
+// one engine call; (x - 1) as float over float(2^31 - 1 + 1) = 2^31; 1.0 clamped to the float below 1)
+// times (1 - 0) plus 0.  Bit-identical to the reference's CPU sampler (tests/test_gpu_ref_kernels.py).
+//
+
+template <typename T> class random_sampler;
+
+template <>
+class random_sampler<float>
+{
+public:
+    using value_type = float;
+
+    VRH_FUNC random_sampler() = default;
+    VRH_FUNC random_sampler(unsigned seed) : x_(seed % 2147483647u == 0u ? 1u : seed % 2147483647u) {}
+
+    VRH_FUNC float next()
+    {
+        x_ = uint32_t((uint64_t(x_) * 16807u) % 2147483647u);
+        float r = float(x_ - 1u) / 2147483648.0f;
+        if (r >= 1.0f) r = 0.99999994f;             // std::nextafter(1.0f, 0.0f)
+        return r * (1.0f - 0.0f) + 0.0f;
+    }
+
+private:
+    uint32_t x_ = 1u;                               // default_seed
+};
+
+// sampling.h:49-71 (math/detail/math.h:241 two_pi; max(x, y) = x < y ? y : x)
+template <typename T>
+VRH_FUNC inline vector<3, T> uniform_sample_hemisphere(T u1, T u2)
+{
+    auto m = T(1.0) - u1 * u1;
+    auto r = std::sqrt(T(0.0) < m ? m : T(0.0));
+    auto phi = T(6.28318530717958647692528676656e+00) * u2;
+    return vector<3, T>(r * std::cos(phi), r * std::sin(phi), u1);
+}
+
+template <typename T>
+VRH_FUNC inline vector<3, T> cosine_sample_hemisphere(T u1, T u2)
+{
+    auto r = std::sqrt(u1);
+    auto theta = T(6.28318530717958647692528676656e+00) * u2;
+    auto x = r * std::cos(theta);
+    auto y = r * std::sin(theta);
+    auto m = T(1.0) - u1;
+    auto z = std::sqrt(T(0.0) < m ? m : T(0.0));
+    return vector<3, T>(x, y, z);
+}
+
+#endif // !VRH_REFERENCE_HEADERS
+
+//-------------------------------------------------------------------------------------------------
+// The BVH walk over libvrh's device layout (detail/bvh/intersect.inl:60-134), shared by both
+// vocabularies: near child first (ties -> child 1), the far child pushed, a node pair culled against
+// the running result's t (cull_t(): is_closer(box, result, max_t), update_if.h:60-88), a leaf's
+// primitives handed in index order to `leaf(i)`, which tests and merges one primitive and returns
+// true to end the traversal (exit_traversal<AnyHit>).
 //
 
 namespace hip_detail
 {
-// the leaf primitive i of the device layout, rebuilt as the reference's primitive object
-__device__ inline basic_triangle<3, float> leaf_triangle(const float4* prims, uint32_t i, uint32_t& flags)
+// the leaf primitive i of the device layout, rebuilt as a primitive object of type P (the
+// reference's basic_triangle<3,float> / basic_sphere<float>, or standalone.h's of the same layout)
+template <typename P>
+__device__ inline P leaf_primitive(const float4* prims, uint32_t i, uint32_t& flags)
 {
-    const float4 a = prims[3u * i], b = prims[3u * i + 1u], c = prims[3u * i + 2u];
-    basic_triangle<3, float> t;
-    t.v1 = vec3(a.x, a.y, a.z);
-    t.e1 = vec3(a.w, b.x, b.y);
-    t.e2 = vec3(b.z, b.w, c.x);
-    t.prim_id = __float_as_uint(c.y);
-    t.geom_id = __float_as_uint(c.z);
-    flags = __float_as_uint(c.w);
-    return t;
-}
-
-__device__ inline basic_sphere<float> leaf_sphere(const float4* prims, uint32_t i, uint32_t& flags)
-{
-    const float4 a = prims[2u * i], b = prims[2u * i + 1u];
-    basic_sphere<float> s;
-    s.center = vec3(a.x, a.y, a.z);
-    s.radius = a.w;
-    s.prim_id = __float_as_uint(b.x);
-    s.geom_id = __float_as_uint(b.y);
-    flags = __float_as_uint(b.z);
-    return s;
+    P p;
+    if constexpr (is_sphere<P>::value)
+    {
+        const float4 a = prims[2u * i], b = prims[2u * i + 1u];
+        p.center = decltype(p.center)(a.x, a.y, a.z);
+        p.radius = a.w;
+        p.prim_id = __float_as_uint(b.x);
+        p.geom_id = __float_as_uint(b.y);
+        flags = __float_as_uint(b.z);
+    }
+    else
+    {
+        const float4 a = prims[3u * i], b = prims[3u * i + 1u], c = prims[3u * i + 2u];
+        p.v1 = decltype(p.v1)(a.x, a.y, a.z);
+        p.e1 = decltype(p.e1)(a.w, b.x, b.y);
+        p.e2 = decltype(p.e2)(b.z, b.w, c.x);
+        p.prim_id = __float_as_uint(c.y);
+        p.geom_id = __float_as_uint(c.z);
+        flags = __float_as_uint(c.w);
+    }
+    return p;
 }
 
 // the per-thread traversal stack: a column of the block's dynamic LDS (hip_sched's user-kernel
@@ -276,21 +359,10 @@ __device__ inline vrh::dev::lds_stack user_stack()
     return st;
 }
 
-// the hit record of intersect(ray, primitive) -- and of every intersector built on it
-using prim_record = hit_record<basic_ray<float>, primitive<unsigned>>;
-using bvh_record = hit_record_bvh<prim_record>;
-
-template <bool Any, bool FAST, typename Isect>
-__device__ inline bvh_record traverse_bvh_slab(basic_ray<float> const& ray, vrh_scene_view const& b, Isect& isect, float max_t)
+template <bool FAST, typename CullT, typename Leaf>
+__device__ inline void walk_slab(vrh_scene_view const& b, vrh::dev::ray_t const& r, float max_t, CullT const& cull_t, Leaf&& leaf)
 {
-    using HR = prim_record;
-    hit_record_bvh<HR> result;
-    // the LDS stack holds VRH_USER_STACK entries: a deeper BVH (not passed through checked_ref)
-    // is not traversed -- a miss, never an out-of-bounds stack write
-    if (b.max_depth >= VRH_USER_STACK) return result;
-    const vrh::dev::ray_t r = dev_ray(ray);
     const float4* pairs = static_cast<const float4*>(b.pairs);
-    const float4* prims = static_cast<const float4*>(b.prims);
     vrh::dev::lds_stack st = user_stack();
     st.push(b.root);
     while (!st.empty())
@@ -304,7 +376,7 @@ __device__ inline bvh_record traverse_bvh_slab(basic_ray<float> const& ray, vrh_
             const float2 q3 = *reinterpret_cast<const float2*>(p + 3);
             bool b0, b1;
             float tn0, tn1;
-            vrh::dev::box_pair<FAST>(q0, q1, q2, r, result.t, max_t, b0, b1, tn0, tn1);
+            vrh::dev::box_pair<FAST>(q0, q1, q2, r, cull_t(), max_t, b0, b1, tn0, tn1);
             const uint32_t l0 = __float_as_uint(q3.x), l1 = __float_as_uint(q3.y);
             if (!(b0 | b1)) { at_leaf = false; break; }                               // pop
             const bool go0 = (b0 & b1) ? (tn0 < tn1) : b0;                             // ties -> child 1
@@ -312,42 +384,161 @@ __device__ inline bvh_record traverse_bvh_slab(basic_ray<float> const& ray, vrh_
             link = go0 ? l0 : l1;
         }
         if (!at_leaf) continue;
-        // the leaf: every primitive in index order, is_closer / update_if (intersect.inl:103-128)
         for (uint32_t i = link & ~vrh::dev::LEAF_BIT;; ++i)
         {
-            uint32_t flags;
-            HR hr;
-            if (b.prim_kind == VRH_PRIM_TRI64) hr = isect(ray, leaf_triangle(prims, i, flags));
-            else hr = isect(ray, leaf_sphere(prims, i, flags));
-            if (is_closer(hr, static_cast<HR const&>(result), max_t))
-            {
-                result = hit_record_bvh<HR>(hr, i);
-                if (Any) return result;                   // exit_traversal.h:49-56
-            }
+            uint32_t flags = 0;
+            if (leaf(i, flags)) return;
             if (flags & vrh::dev::END_BIT) break;
         }
     }
-    return result;
 }
 
-template <bool Any, typename Isect>
-__device__ inline bvh_record traverse_bvh(basic_ray<float> const& ray, vrh_scene_view const& b, Isect& isect, float max_t)
+// the LDS stack holds VRH_USER_STACK entries: a deeper BVH (not passed through checked_ref) is not
+// traversed -- a miss, never an out-of-bounds stack write.  The hardware min/max slab test where it is
+// provably identical (vrh_device.h box_pair).
+template <typename Ray, typename CullT, typename Leaf>
+__device__ inline void walk(vrh_scene_view const& b, Ray const& ray, float max_t, CullT const& cull_t, Leaf&& leaf)
 {
-    // the hardware min/max slab test where it is provably identical (vrh_device.h box_pair)
-    if (b.finite_bounds && vrh::dev::finite_ray(dev_ray(ray)))
-        return traverse_bvh_slab<Any, true>(ray, b, isect, max_t);
-    return traverse_bvh_slab<Any, false>(ray, b, isect, max_t);
+    if (b.max_depth >= VRH_USER_STACK) return;
+    const vrh::dev::ray_t r = dev_ray(ray);
+    if (b.finite_bounds && vrh::dev::finite_ray(r)) walk_slab<true>(b, r, max_t, cull_t, leaf);
+    else walk_slab<false>(b, r, max_t, cull_t, leaf);
 }
 
 template <typename It>
 using range_value_t = typename std::decay<decltype(*std::declval<It>())>::type;
+template <typename It>
+using is_bvh_ref_range = std::is_base_of<hip_bvh_ref, range_value_t<It>>;
+} // hip_detail
+
+template <typename P>
+__host__ __device__ inline P hip_bvh_ref_t<P>::primitive(size_t i) const
+{
+    uint32_t flags;
+    return hip_detail::leaf_primitive<P>(static_cast<const float4*>(view.prims), uint32_t(i), flags);
+}
+
+#if defined(VRH_REFERENCE_HEADERS)
+// ================================================================================================
+// The reference's traversal over the device BVH.  hip_bvh_ref_t<P> is one more index BVH for the
+// reference's templates: closest_hit / any_hit / multi_hit over [begin, end) of refs run the
+// reference's own traverse() (traverse_linear.inl:76-141), which calls the intersector's BVH
+// overloads (intersector.h:38-106), which call intersect<Traversal>(ray, ref, isect, max_t, cond)
+// below: libvrh's walk with the reference's leaf step -- HR(isect(ray, prim), i), update_cond,
+// update_if, exit_traversal<Traversal> (intersect.inl:103-128) -- so the result records, the
+// multi-hit insertion and any custom intersector are the reference's code.
+// ================================================================================================
+
+template <typename P>
+struct is_index_bvh<hip_bvh_ref_t<P>> : std::true_type {};
+
+namespace hip_detail
+{
+// is_closer(box record, result, max_t) compares the box's tnear with result.t, or for a multi-hit
+// array with every entry's t (multi_hit.h: any entry) -- i.e. with the largest
+template <typename RT>
+__device__ inline float cull_of(RT const& r) { return r.t; }
+template <typename HR, size_t N>
+__device__ inline float cull_of(array<HR, N> const& r)
+{
+    float m = r[0].t;
+    for (size_t k = 1; k < N; ++k) m = m < r[k].t ? r[k].t : m;
+    return m;
+}
+} // hip_detail
+
+template <
+    detail::traversal_type Traversal,
+    size_t MultiHitMax = 1,
+    typename P,
+    typename Intersector,
+    typename Cond = is_closer_t
+    >
+VRH_FUNC inline auto intersect(
+        basic_ray<float> const& ray,
+        hip_bvh_ref_t<P> const& b,
+        Intersector&            isect,
+        float                   max_t = numeric_limits<float>::max(),
+        Cond                    update_cond = Cond()
+        )
+    -> typename detail::traversal_result<
+            hit_record_bvh<basic_ray<float>, hip_bvh_ref_t<P>, decltype(isect(ray, std::declval<P>()))>,
+            Traversal, MultiHitMax>::type
+{
+    using HR = hit_record_bvh<basic_ray<float>, hip_bvh_ref_t<P>, decltype(isect(ray, std::declval<P>()))>;
+    using RT = typename detail::traversal_result<HR, Traversal, MultiHitMax>::type;
+    RT result;
+    const float4* prims = static_cast<const float4*>(b.view.prims);
+    hip_detail::walk(b.view, ray, max_t, [&]() { return hip_detail::cull_of(result); },
+                     [&](uint32_t i, uint32_t& flags) -> bool
+                     {
+                         const P prim = hip_detail::leaf_primitive<P>(prims, i, flags);
+                         auto hr = HR(isect(ray, prim), int(i));
+                         auto closer = update_cond(hr, result, max_t);
+                         if (!any(closer)) return false;
+                         update_if(result, hr, closer);
+                         detail::exit_traversal<Traversal> early_exit;
+                         return early_exit.check(result);
+                     });
+    return result;
+}
+
+// the default (closest hit) overloads, intersect.inl:140-189
+template <typename P, typename Intersector, typename Cond = is_closer_t>
+VRH_FUNC inline auto intersect(basic_ray<float> const& ray, hip_bvh_ref_t<P> const& b, Intersector& isect,
+                                 Cond update_cond = Cond())
+    -> hit_record_bvh<basic_ray<float>, hip_bvh_ref_t<P>, decltype(isect(ray, std::declval<P>()))>
+{
+    return intersect<detail::ClosestHit>(ray, b, isect, numeric_limits<float>::max(), update_cond);
+}
+
+template <typename P>
+VRH_FUNC inline auto intersect(basic_ray<float> const& ray, hip_bvh_ref_t<P> const& b)
+    -> hit_record_bvh<basic_ray<float>, hip_bvh_ref_t<P>, decltype(intersect(ray, std::declval<P>()))>
+{
+    default_intersector isect;
+    return intersect<detail::ClosestHit>(ray, b, isect, numeric_limits<float>::max(), is_closer_t());
+}
+
+#else
+// ================================================================================================
+// standalone: closest_hit / any_hit over hip_bvh_ref ranges and primitive arrays
+// ================================================================================================
+
+namespace hip_detail
+{
+// the hit record of intersect(ray, primitive) -- and of every intersector built on it
+using prim_record = hit_record<basic_ray<float>, primitive<unsigned>>;
+using bvh_record = hit_record_bvh<prim_record>;
+
+template <bool Any, typename Isect>
+__device__ inline bvh_record traverse_bvh(basic_ray<float> const& ray, vrh_scene_view const& b, Isect& isect, float max_t)
+{
+    using HR = prim_record;
+    bvh_record result;
+    const float4* prims = static_cast<const float4*>(b.prims);
+    // the leaf: every primitive in index order, is_closer / update_if (intersect.inl:103-128)
+    walk(b, ray, max_t, [&]() { return result.t; },
+         [&](uint32_t i, uint32_t& flags) -> bool
+         {
+             HR hr;
+             if (b.prim_kind == VRH_PRIM_TRI64) hr = isect(ray, leaf_primitive<basic_triangle<3, float>>(prims, i, flags));
+             else hr = isect(ray, leaf_primitive<basic_sphere<float>>(prims, i, flags));
+             if (is_closer(hr, static_cast<HR const&>(result), max_t))
+             {
+                 result = bvh_record(hr, i);
+                 if (Any) return true;                     // exit_traversal.h:49-56
+             }
+             return false;
+         });
+    return result;
+}
 } // hip_detail
 
 // closest_hit / any_hit over [begin, end) of hip_bvh_ref (traverse_linear.inl:76-141): every BVH on
 // its own with the same max_t, merged by update_if(result, hr, is_closer(hr, result, max_t));
 // any_hit stops at the first BVH with a hit
-template <typename It, typename Isect,
-          typename = typename std::enable_if<std::is_same<hip_detail::range_value_t<It>, hip_bvh_ref>::value>::type>
+template <typename It, typename Isect, typename = typename std::enable_if<hip_detail::is_bvh_ref_range<It>::value>::type>
 __device__ inline hip_detail::bvh_record closest_hit(basic_ray<float> const& ray, It begin, It end, Isect& isect)
 {
     hip_detail::bvh_record result;
@@ -359,8 +550,7 @@ __device__ inline hip_detail::bvh_record closest_hit(basic_ray<float> const& ray
     return result;
 }
 
-template <typename It, typename Isect,
-          typename = typename std::enable_if<std::is_same<hip_detail::range_value_t<It>, hip_bvh_ref>::value>::type>
+template <typename It, typename Isect, typename = typename std::enable_if<hip_detail::is_bvh_ref_range<It>::value>::type>
 __device__ inline hip_detail::bvh_record any_hit(basic_ray<float> const& ray, It begin, It end, float max_t, Isect& isect)
 {
     hip_detail::bvh_record result;
@@ -374,8 +564,7 @@ __device__ inline hip_detail::bvh_record any_hit(basic_ray<float> const& ray, It
 }
 
 // the same over [begin, end) of primitives (traverse_linear.inl:25-62): a linear scan
-template <typename It, typename Isect,
-          typename = typename std::enable_if<!std::is_same<hip_detail::range_value_t<It>, hip_bvh_ref>::value>::type,
+template <typename It, typename Isect, typename = typename std::enable_if<!hip_detail::is_bvh_ref_range<It>::value>::type,
           typename = void>
 __device__ inline auto closest_hit(basic_ray<float> const& ray, It begin, It end, Isect& isect)
 {
@@ -389,8 +578,7 @@ __device__ inline auto closest_hit(basic_ray<float> const& ray, It begin, It end
     return result;
 }
 
-template <typename It, typename Isect,
-          typename = typename std::enable_if<!std::is_same<hip_detail::range_value_t<It>, hip_bvh_ref>::value>::type,
+template <typename It, typename Isect, typename = typename std::enable_if<!hip_detail::is_bvh_ref_range<It>::value>::type,
           typename = void>
 __device__ inline auto any_hit(basic_ray<float> const& ray, It begin, It end, float max_t, Isect& isect)
 {
@@ -434,25 +622,42 @@ VRH_FUNC inline vec3 get_normal(Normals normals, HR const& hr)
 {
     return normals[hr.prim_id];
 }
+#endif // VRH_REFERENCE_HEADERS
 
 //-------------------------------------------------------------------------------------------------
-// Samplers.  The reference seeds a random_sampler per pixel from the clock (cuda_sched.inl:38-45,
-// 79); here every draw is the SURVEY.md Appendix-A counter hash, so frames are reproducible:
-//   hip_sampler::next()        uniform [0, 1) from the counter (pixel, frame number, draw)
-//   hip_ao_sample(p, s, frame) the built-in AO kernel's cosine-hemisphere sample s of pixel p
-//                              (Malley disk point, z = sqrt(1 - x^2 - y^2)) -- the same sample set
-//                              as VRH_KERNEL_AO, so a user AO kernel reproduces its frames.
+// Samplers.  A kernel taking a sampler, kernel(ray, random_sampler<float>& samp), gets the
+// reference's random_sampler<float> (random_sampler.h:24-57) seeded per pixel as cuda_sched seeds it
+// (cuda_sched.inl:20-45: cuda_hash(tic() + y * w + x)), with the clock tic() replaced by
+// frame_num * W * H so that frames are reproducible and the seeds of consecutive frames distinct:
+//
+//     seed(x, y) = cuda_hash(frame_num * W * H + y * W + x)        (32-bit unsigned arithmetic)
+//
+// The reference CPU path run with the same seeds draws the same numbers bit for bit
+// (oracle/ref_harness.cpp `rsampler`, tests/test_gpu_ref_kernels.py).
+//   hip_ao_sample(p, s, frame) is the built-in AO kernel's cosine-hemisphere sample s of pixel p
+//   (Malley disk point, z = sqrt(1 - x^2 - y^2)) -- the same sample set as VRH_KERNEL_AO, so a user
+//   AO kernel can reproduce the built-in kernel's frames.
 //
 
-struct hip_sampler
+namespace hip_detail
 {
-    uint32_t ctr;
-    __device__ explicit hip_sampler(uint32_t pixel, uint32_t frame_num)
-        : ctr(vrh::dev::wang(pixel * 0x9E3779B1u ^ vrh::dev::frame_salt(frame_num + 1u)))
-    {
-    }
-    __device__ float next() { return vrh::dev::uniform01(ctr++); }
-};
+// cuda_sched.inl:27-36 (the integer hash of thrust's monte_carlo example)
+__device__ inline unsigned seed_hash(unsigned a)
+{
+    a = (a + 0x7ed55d16u) + (a << 12);
+    a = (a ^ 0xc761c23cu) ^ (a >> 19);
+    a = (a + 0x165667b1u) + (a << 5);
+    a = (a + 0xd3a2646cu) ^ (a << 9);
+    a = (a + 0xfd7046c5u) + (a << 3);
+    a = (a ^ 0xb55a4f09u) ^ (a >> 16);
+    return a;
+}
+
+__device__ inline unsigned pixel_seed(unsigned x, unsigned y, unsigned w, unsigned h, unsigned frame_num)
+{
+    return seed_hash(frame_num * w * h + y * w + x);
+}
+} // hip_detail
 
 __device__ inline vec3 hip_ao_sample(uint32_t pixel, uint32_t s, uint32_t frame_num)
 {
@@ -563,7 +768,7 @@ __global__ __launch_bounds__(64) void user_render(K kernel, user_frame f)
     const uint32_t x = blockIdx.x * 8u + threadIdx.x;
     const uint32_t y = blockIdx.y * 8u + threadIdx.y;
     if (x < f.x0 || y < f.y0 || x >= f.x1 || y >= f.y1) return;
-    hip_sampler samp(y * f.width + x, f.frame_num);
+    random_sampler<float> samp(pixel_seed(x, y, f.width, f.height, f.frame_num));
     const size_t o = size_t(y) * f.width + x;
     if constexpr (SK == VRH_SAMPLER_UNIFORM)
     {
@@ -699,7 +904,8 @@ struct user_kernels<K, typename std::enable_if<!std::is_same<K, hip_builtin_kern
 
 // the user traversal stack holds VRH_USER_STACK entries: a deeper BVH cannot be traversed (the
 // device code then reports a miss); checked_ref rejects it on the host instead
-inline hip_bvh_ref checked_ref(hip_bvh_ref r)
+template <typename Ref>
+inline Ref checked_ref(Ref r)
 {
     if (r.view.max_depth >= VRH_USER_STACK)
         throw hip_error("hip_bvh_ref: BVH deeper than VRH_USER_STACK", VRH_ERR_UNSUPPORTED);

@@ -22,6 +22,10 @@
 //                                    shade-mode scene, hit lists (prim_id / t) + the compositing
 //                                    kernel of examples/multi_hit/main.cpp:166-235 (restated on the
 //                                    reference's get_surface / plastic::shade).
+//   rsampler <scene> <outdir> <W> <H> <frame> [samples]
+//                                  : ao/main.cpp:183-246 verbatim (random_sampler<float> +
+//                                    cosine_sample_hemisphere) with hip_sched's per-pixel seeds
+//                                    (built by clang++: vsnray_ref_clang)
 //   bench  <scene> <threads> <frames> [W H] [samples]
 //                                  : the reference SSE4 CPU path, tiled_sched<basic_ray<simd::float4>>
 //                                    (tiled_sched.inl:365-391) running the ao/main.cpp:183-246 kernel
@@ -994,6 +998,108 @@ static int run_sampler(scene_desc const& d, aligned_vector<P>& prims, std::vecto
     return 2;
 }
 
+//-------------------------------------------------------------------------------------------------
+// rsampler: the ao/main.cpp:183-246 kernel verbatim -- random_sampler<float> (random_sampler.h:24-57)
+// draws, cosine_sample_hemisphere(samp.next(), samp.next()) (sampling.h:61-71), closest_hit /
+// any_hit over the bvh_ref list, get_normal(normals, hit, index_bvh<P>{}, normals_per_face_binding{})
+// -- with the per-pixel sampler seeded as hip_sched seeds it (visionaray_hip/hip_kernels.h:
+// cuda_sched's cuda_hash(tic() + y * w + x), cuda_sched.inl:20-45, with tic() = frame * W * H).
+// The pixel loop is simple_sched's (simple_sched.inl:139-151, kernel form (ray, x, y)); the sampler
+// is built per pixel from the seed instead of once per frame from the clock.  Also records draws
+// 0, 1, 2 and 15 of every pixel's sampler (a copy, before the kernel draws).
+// Built for these fixtures by clang++ (oracle/Makefile vsnray_ref_clang): the order in which the two
+// samp.next() arguments are evaluated is the compiler's (g++ right to left, clang and hipcc left to
+// right), and the GPU side is compiled by hipcc.
+//
+
+static unsigned rs_hash(unsigned a)
+{
+    a = (a + 0x7ed55d16u) + (a << 12);
+    a = (a ^ 0xc761c23cu) ^ (a >> 19);
+    a = (a + 0x165667b1u) + (a << 5);
+    a = (a + 0xd3a2646cu) ^ (a << 9);
+    a = (a + 0xfd7046c5u) + (a << 3);
+    a = (a ^ 0xb55a4f09u) ^ (a >> 16);
+    return a;
+}
+
+static int run_rsampler(scene_desc const& d, aligned_vector<tri_t>& prims, std::vector<vec3> const& normals,
+                        std::string const& outdir, int W, int H, uint32_t frame_num, int AO_Samples)
+{
+    using R = ray;
+    using S = float;
+    using C = vec4;
+    using V = vec3;
+    auto bvh = build<index_bvh<tri_t>>(prims.data(), prims.size());
+    camera cam = make_camera(d, W, H);
+    using bvh_ref = index_bvh<tri_t>::bvh_ref;
+    std::vector<bvh_ref> bvhs{ bvh.ref() };
+    auto prims_begin = bvhs.data();
+    auto prims_end = bvhs.data() + bvhs.size();
+    const vec4 bgcolor(0.1f, 0.2f, 0.3f, 1.0f);
+    const S AO_Radius = 0.1f;
+    size_t npx = size_t(W) * H;
+    std::vector<float> draws(4 * npx), tval(npx, -1.0f);
+    simple_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> rt;
+    rt.resize(W, H);
+    auto sparams = make_sched_params(pixel_sampler::uniform_type{}, cam, rt);
+    simple_sched<R> sched;
+    sched.frame([&](R ray, unsigned x, unsigned y) -> result_record<S>
+    {
+        random_sampler<S> samp(rs_hash(frame_num * unsigned(W) * unsigned(H) + y * unsigned(W) + x));
+        size_t p = size_t(y) * W + x;
+        {
+            random_sampler<S> c = samp;
+            float dd[16];
+            for (int k = 0; k < 16; ++k) dd[k] = c.next();
+            draws[4 * p] = dd[0]; draws[4 * p + 1] = dd[1]; draws[4 * p + 2] = dd[2]; draws[4 * p + 3] = dd[15];
+        }
+        // ao/main.cpp:185-242
+        result_record<S> result;
+        result.color = C(bgcolor.xyz(), 1.0f);
+        auto hit_rec = closest_hit(ray, prims_begin, prims_end);
+        result.hit = hit_rec.hit;
+        if (any(hit_rec.hit))
+        {
+            tval[p] = hit_rec.t;
+            hit_rec.isect_pos = ray.ori + ray.dir * hit_rec.t;
+            result.isect_pos = hit_rec.isect_pos;
+            C clr(1.0);
+            auto n = get_normal(normals.data(), hit_rec, index_bvh<tri_t>{}, normals_per_face_binding{});
+            V u;
+            V v;
+            V w = n;
+            make_orthonormal_basis(u, v, w);
+            S radius = AO_Radius;
+            for (int i = 0; i < AO_Samples; ++i)
+            {
+                auto sp = cosine_sample_hemisphere(samp.next(), samp.next());
+                auto dir = normalize(sp.x * u + sp.y * v + sp.z * w);
+                R ao_ray;
+                ao_ray.ori = hit_rec.isect_pos + dir * S(1E-3f);
+                ao_ray.dir = dir;
+                auto ao_rec = any_hit(ao_ray, prims_begin, prims_end, radius);
+                clr = select(ao_rec.hit, clr - S(1.0f / AO_Samples), clr);
+            }
+            result.color = select(hit_rec.hit, C(clr.xyz(), S(1.0)), result.color);
+        }
+        return result;
+    }, sparams);
+    write_file(outdir + "/draws.bin", draws.data(), draws.size() * 4);
+    write_file(outdir + "/t.bin", tval.data(), npx * 4);
+    write_file(outdir + "/color.bin", rt.color(), npx * 16);
+    fnv hd, ht, hc;
+    uint64_t hits = 0;
+    for (size_t p = 0; p < npx; ++p) { ht.u32(fbits(tval[p])); hits += tval[p] >= 0.0f; }
+    hd.bytes(draws.data(), draws.size() * 4);
+    hc.bytes(rt.color(), npx * 16);
+    printf("{\"scene\":\"%s\",\"W\":%d,\"H\":%d,\"frame\":%u,\"samples\":%d,\"hits\":%llu,\"draws_hash\":\"%016llx\","
+           "\"t_hash\":\"%016llx\",\"color_hash\":\"%016llx\"}\n",
+           d.name.c_str(), W, H, frame_num, AO_Samples, (unsigned long long)hits, (unsigned long long)hd.h,
+           (unsigned long long)ht.h, (unsigned long long)hc.h);
+    return 0;
+}
+
 int main(int argc, char** argv)
 {
     if (argc < 3)
@@ -1141,6 +1247,21 @@ int main(int argc, char** argv)
         {
             return run_sampler(d, prims, normals, outdir, W, H, do_ao, kind, frame_num, matrices);
         });
+    }
+    if (mode == "rsampler")
+    {
+        // rsampler <scene> <outdir> <W> <H> <frame> [samples]: the AO example's kernel with per-pixel
+        // seeded random_sampler<float> (triangle scenes)
+        if (argc < 7 || d.spheres) return 2;
+        std::string outdir = argv[3];
+        int W = atoi(argv[4]), H = atoi(argv[5]);
+        uint32_t frame_num = uint32_t(strtoul(argv[6], nullptr, 10));
+        int samples = argc > 7 ? atoi(argv[7]) : 8;
+        aligned_vector<tri_t> t;
+        if (d.grid == 0) make_cornell(t); else if (d.layers) make_hfstack(d.grid, d.layers, t); else make_heightfield(d.grid, t);
+        std::vector<vec3> normals(t.size());
+        for (size_t i = 0; i < t.size(); ++i) normals[i] = normalize(cross(t[i].e1, t[i].e2));
+        return run_rsampler(d, t, normals, outdir, W, H, frame_num, samples);
     }
     if (mode == "bench")
     {

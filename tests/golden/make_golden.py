@@ -12,6 +12,7 @@ Run in the build container (needs /root/reference to build the harness):
     python tests/golden/make_golden.py --list                           (only the BVH-list + scissor cases)
     python tests/golden/make_golden.py --heart                          (only the procedural-heart cases)
     python tests/golden/make_golden.py --sampler                        (only the pixel-sampler cases)
+    python tests/golden/make_golden.py --rsampler                       (only the random_sampler AO cases)
 
 For every case the reference harness renders a full simple_sched<basic_ray<float>> frame
 (primary closest_hit + the Appendix-A AO kernel for triangle scenes) and this script stores:
@@ -35,6 +36,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 REF = os.path.join(ROOT, "oracle", "_ref", "vsnray_ref")
+REF_CLANG = os.path.join(ROOT, "oracle", "_ref", "vsnray_ref_clang")    # the harness built by clang++ (rsampler)
 
 # (case name, scene, W, H, full dump?)
 CASES = [
@@ -298,6 +300,39 @@ def sampler_cases(out):
             print(case, rec["color_hash"], flush=True)
 
 
+# (case, scene, W, H, frame): the AO example's kernel verbatim with random_sampler<float> seeded per pixel
+# as hip_sched seeds it (harness `rsampler` mode, built by clang++): draws 0, 1, 2, 15 of every pixel's
+# sampler, the closest-hit t, the AO colour.  Stored: hashes over the whole frame, the occluded-sample
+# count per pixel (255 = miss), and 4096 sampled pixels' draws and t.
+RSAMPLER_CASES = [
+    ("rs_hf64_160x90_f0", "hf64", 160, 90, 0),
+    ("rs_hf200_320x180_f3", "hf200", 320, 180, 3),
+    ("rs_hf1M_f1", "hf1M", 1920, 1080, 1),
+]
+
+
+def rsampler_cases(out):
+    rng = np.random.default_rng(97531)
+    for case, scene, W, H, frame in RSAMPLER_CASES:
+        with tempfile.TemporaryDirectory() as d:
+            r = subprocess.run([REF_CLANG, "rsampler", scene, d, str(W), str(H), str(frame)], check=True,
+                               capture_output=True, text=True)
+            info = json.loads(r.stdout.strip().splitlines()[-1])
+            draws = np.fromfile(os.path.join(d, "draws.bin"), np.float32).reshape(-1, 4)
+            t = np.fromfile(os.path.join(d, "t.bin"), np.float32)
+            color = np.fromfile(os.path.join(d, "color.bin"), np.float32).reshape(-1, 4)
+            hit = t >= 0.0
+            k = np.where(hit, np.rint((1.0 - color[:, 0]) * 8.0), 255).astype(np.uint8)
+            rec = {"scene": scene, "W": W, "H": H, "frame": frame, "samples": 8, "hits": int(hit.sum()),
+                   "draws_hash": fnv1a(draws), "t_hash": fnv1a(t), "color_hash": fnv1a(color),
+                   "occluded_samples": int(k[hit].astype(np.int64).sum())}
+            assert rec["draws_hash"] == info["draws_hash"] and rec["color_hash"] == info["color_hash"], case
+            pix = np.sort(rng.choice(W * H, 4096, replace=False)).astype(np.uint32)
+            np.savez_compressed(os.path.join(HERE, case + ".npz"), ao_count=k, pixels=pix, draws=draws[pix], t=t[pix])
+            out[case] = rec
+            print(case, rec["hits"], rec["occluded_samples"], rec["draws_hash"], flush=True)
+
+
 def sah_cases(out):
     rec = {}
     for scene in SAH_SCENES:
@@ -312,7 +347,7 @@ def main():
     if not os.path.exists(REF):
         sys.exit("build the reference harness first: make -C oracle ref")
     only_shade = any(f in sys.argv for f in ("--shade", "--multi", "--sah", "--whitted", "--mask", "--frames", "--list",
-                                                "--heart", "--sampler"))
+                                                "--heart", "--sampler", "--rsampler"))
     path = os.path.join(HERE, "golden.json")
     out = json.load(open(path)) if only_shade else {}
     rng = np.random.default_rng(12345)
@@ -346,6 +381,8 @@ def main():
             print(case, rec["hits"], rec["ao_occluded"], rec["primid_hash"], flush=True)
     if "--heart" in sys.argv:
         heart_cases(out)
+    elif "--rsampler" in sys.argv:
+        rsampler_cases(out)
     elif "--sampler" in sys.argv:
         sampler_cases(out)
     elif "--frames" in sys.argv:
@@ -368,6 +405,7 @@ def main():
         frame_cases(out, np.random.default_rng(2468))
         list_cases(out)
         sampler_cases(out)
+        rsampler_cases(out)
     with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 
