@@ -533,6 +533,10 @@ hip_builtin_kernel make_hip_ao_kernel(BVH const& bvh, Vec4 const& bg, unsigned s
     k.desc.radius = radius;
     k.desc.eps = eps;
     k.desc.bg[0] = bg.x; k.desc.bg[1] = bg.y; k.desc.bg[2] = bg.z; k.desc.bg[3] = bg.w;
+    // ao/main.cpp takes AO_Samples from its command line (main.cpp:85, 115): with more than 8 the
+    // per-sample mask no longer fits hip_buffer_rt's occlusion byte, which is then left untouched
+    // (the colour carries the result, as in the reference, which has no such buffer)
+    if (samples > 8u) k.desc.flags |= VRH_KERNEL_NO_OCC;
     return k;
 }
 
@@ -750,7 +754,9 @@ public:
         }
         rt.begin_frame();
         hip_detail::check(vrh_render_sharded(uint32_t(g.size()), g.data(), sc.data(), kd.data(),
-                                             group_->has_root() ? rt.handle() : nullptr, VRH_RT_ALL, &c, 1, frame_num,
+                                             group_->has_root() ? rt.handle() : nullptr,
+                                             (kd[0].flags & VRH_KERNEL_NO_OCC) ? (VRH_RT_ALL & ~uint32_t(VRH_RT_OCC)) : VRH_RT_ALL,
+                                             &c, 1, frame_num,
                                              shards_),
                           "vrh_render_sharded");
         group_->sync();

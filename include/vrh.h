@@ -116,7 +116,8 @@ typedef struct vrh_hit_mask vrh_hit_mask;   /* see vrh_hit_mask_create          
 typedef struct {
     uint32_t kind;            /* vrh_kernel_kind                                          */
     uint32_t samples;         /* AO samples per hit pixel (ao/main.cpp default 8, <= 32; a
-                                 VRH_RT_OCC target records at most 8)                        */
+                                 VRH_RT_OCC target records at most 8: with more, set
+                                 VRH_KERNEL_NO_OCC or use a target without the buffer)       */
     float    radius;          /* AO any_hit max_t (default 0.1)                            */
     float    eps;             /* AO origin offset along the sample direction (1e-3); the
                                  whitted kernel's scene epsilon                              */
@@ -132,8 +133,11 @@ typedef struct {
 } vrh_kernel_desc;
 
 enum vrh_kernel_flags {
-    VRH_KERNEL_COUNT_TESTS = 1u   /* instrumented variant: count box / primitive tests (slower;
+    VRH_KERNEL_COUNT_TESTS = 1u,  /* instrumented variant: count box / primitive tests (slower;
                                      feeds the algorithmic-bytes roofline)    */
+    VRH_KERNEL_NO_OCC = 2u        /* leave the target's VRH_RT_OCC buffer untouched (AO kernels of
+                                     more than 8 samples, whose masks do not fit its bytes, render
+                                     into a target that has one)                              */
 };
 
 /* Image-tile sharding: the image is cut into bands of VRH_BAND_ROWS = 8 rows (one
@@ -253,6 +257,13 @@ enum vrh_option {
                                     tile's AO reach (every hit position +- eps + radius), pushed
                                     so that the entry nearest the tile is popped first: 1 = on,
                                     2 = off, 3 = on with the entries in cut order (auto: on)      */
+    VRH_OPT_AO_STEAL = 21,       /* AO step loop: the tiles a wave takes when fewer than about one per
+                                    wave remain in its queue (the launch's last round) publish their
+                                    hits to a launch-wide stash instead of tracing their AO rays
+                                    alone, and every wave that runs out of tiles traces stash AO
+                                    rays, 64 at a time, so the launch's tail is shared by all waves:
+                                    1 = on, 2 = off, 4..4096: on with value / 16 tiles per wave
+                                    (and queue) counted as the last round (auto: on, 16 = 1 tile)   */
     VRH_OPT_PAIR_LAYOUT = 15,    /* scene upload (read by vrh_scene_upload): 1 = node pairs in
                                     depth-first preorder, a pair's child-0 pair next to it in one
                                     128-B line; 2 = the builder's order (auto: 2; 1 measured
@@ -470,6 +481,36 @@ VRH_API int vrh_group_broadcast_scene(uint32_t n, vrh_group* const* groups, cons
 VRH_API int vrh_render_sharded(uint32_t n, vrh_group* const* groups, const vrh_scene* const* scenes,
                                const vrh_kernel_desc* kernels, vrh_rt* dst, uint32_t fields,
                                const vrh_camera* cams, uint32_t num_frames, uint32_t frame_num, uint32_t shards);
+
+/* The render-group plan vrh_render_sharded runs, as host functions (no device needed; the same code
+ * the group calls -- visionaray_amd/csrc/vrh_plan.h -- so a multi-process test can drive the protocol):
+ *   vrh_group_shards_of   : the shards rank `rank` of `nranks` renders, in the order it sends them
+ *                           (s = rank, rank + N, ...); returns their count (written up to cap)
+ *   vrh_group_shard_owner : the rank the root receives shard s from (it receives s = 0, 1, ... in order)
+ *   vrh_group_wire_layout : the bytes of one packed shard of `frames` frames on the wire for a root
+ *                           target with buffers `fields` and kernel k (offsets UINT64_MAX: absent)
+ *   vrh_shard_packed_rows : image row of every packed row of shard s (-1: padding past the image);
+ *                           rows_out holds wire.rows entries
+ *   vrh_pack_codes_host   : the one-byte colour code of rendered pixels (0xFF miss, else the number
+ *                           of occluded AO samples; occ may be NULL)
+ *   vrh_unshard_host      : the root's un-interleave of frame f from S gathered shards (host memory,
+ *                           `wire` layout, shard s at gathered + s * wire.shard_bytes) into full-image
+ *                           buffers (any may be NULL), colour re-derived as the GPU kernel does */
+typedef struct {
+    uint64_t prim_id, occ, t, color, code;   /* byte offsets inside a shard (UINT64_MAX: not sent)   */
+    uint64_t shard_bytes;                    /* one packed shard, every frame                        */
+    uint32_t rows;                           /* packed rows per shard and frame                      */
+    uint32_t derive;                         /* the root re-derives the colour (prim ids / codes)    */
+} vrh_wire_layout;
+VRH_API uint32_t vrh_group_shards_of(uint32_t nranks, uint32_t rank, uint32_t shards, uint32_t* out, uint32_t cap);
+VRH_API uint32_t vrh_group_shard_owner(uint32_t nranks, uint32_t shard);
+VRH_API int vrh_group_wire_layout(uint32_t fields, const vrh_kernel_desc* k, uint32_t width, uint32_t height,
+                                  uint32_t frames, uint32_t shards, vrh_wire_layout* out);
+VRH_API int vrh_shard_packed_rows(uint32_t height, uint32_t shard, uint32_t shards, int32_t* rows_out);
+VRH_API int vrh_pack_codes_host(const uint32_t* prim_id, const uint8_t* occ, uint8_t* code, uint64_t n);
+VRH_API int vrh_unshard_host(const void* gathered, const vrh_wire_layout* wire, uint32_t width, uint32_t height,
+                             uint32_t shards, uint32_t frame, uint32_t fields, const vrh_kernel_desc* k,
+                             void* color, uint32_t* prim_id, uint8_t* occ, float* t);
 
 /* GPU BVH construction: a linear BVH (Morton order, Karras 2012 hierarchy,
  * leaves of up to max_leaf primitives) built on the device straight into a scene -- no host build,

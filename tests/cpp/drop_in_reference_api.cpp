@@ -154,7 +154,19 @@ int main(int argc, char** argv)
             matrix_hashes[0] = fnv1a(vc.data(), n * 16);
             matrix_hashes[1] = fnv1a(vt.data(), n * 4);
         }
-        printf("{\"sampler_jittered_blend_color_hash\":\"%016llx\",\"sampler_ssaa4_color_hash\":\"%016llx\",",
+        // AO_Samples = 16 (ao/main.cpp:85, 115 take it from the command line): the frame renders into the
+        // same target, whose occlusion byte cannot hold 16 masks and is left as it was
+        unsigned long long ao16_hash = 0;
+        {
+            hip_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> art;
+            art.resize(W, H);
+            std::vector<float> ac(4 * n);
+            sched.frame(make_hip_ao_kernel(device_bvh, vec4(0.1f, 0.2f, 0.3f, 1.0f), 16), make_sched_params(pixel_sampler::uniform_type{}, cam, art));
+            art.download(ac.data(), nullptr, nullptr, nullptr);
+            ao16_hash = fnv1a(ac.data(), n * 16);
+        }
+        printf("{\"ao16_color_hash\":\"%016llx\",", ao16_hash);
+        printf("\"sampler_jittered_blend_color_hash\":\"%016llx\",\"sampler_ssaa4_color_hash\":\"%016llx\",",
                sampler_hashes[0], sampler_hashes[1]);
         printf("\"matrix_color_hash\":\"%016llx\",\"matrix_t_hash\":\"%016llx\",", matrix_hashes[0], matrix_hashes[1]);
         printf("\"mask_primid_hash\":\"%016llx\",\"mask_t_hash\":\"%016llx\",\"mask_occ_hash\":\"%016llx\","

@@ -16,6 +16,11 @@
 //                                                               (prim_id parity split), scissor box,
 //                                                               frame f (the harness's "list" mode)
 //   user_kernels bench <grid> <W> <H> <outdir> [frames]         throughput of the AO user kernel
+//   user_kernels draws <grid> <W> <H> <outdir> <frame>          kernel(r, random_sampler<float>&): draws
+//                                                                0, 1, 2, 15 of the pixel's sampler as colour
+//   user_kernels rsao  <grid> <W> <H> <outdir> <frame>          the AO example's kernel (ao/main.cpp:183-246)
+//                                                                with standalone.h's random_sampler and
+//                                                                cosine_sample_hemisphere; depth = hit t
 //
 // The kernel is the reference harness's AO lambda (oracle/ref_harness.cpp run_golden, after
 // ao/main.cpp:183-246) as a user would port it to cuda_sched: closest_hit over the BVH refs, the
@@ -277,6 +282,58 @@ int main(int argc, char** argv)
         {
             unsigned frame_num = argc > 6 ? unsigned(strtoul(argv[6], nullptr, 10)) : 0u;
             sched.frame(ao_kernel(one, dnormals, default_intersector{}, W, frame_num), sparams, frame_num);
+        }
+        else if (mode == "draws")
+        {
+            const unsigned frame_num = unsigned(strtoul(argv[6], nullptr, 10));
+            sched.frame([=] __device__ (ray r, random_sampler<float>& samp) -> result_record<float>
+            {
+                result_record<float> result;
+                float d[16];
+                for (int k = 0; k < 16; ++k) d[k] = samp.next();
+                result.color = vec4(d[0], d[1], d[2], d[15]);
+                return result;
+            }, sparams, frame_num);
+            std::vector<float> out(4 * size_t(W) * H);
+            rt.download(out.data());
+            write_file(outdir + "/color.bin", out.data(), out.size() * 4);
+            return 0;
+        }
+        else if (mode == "rsao")
+        {
+            const unsigned frame_num = unsigned(strtoul(argv[6], nullptr, 10));
+            hip_bvh_ref const* begin = one.r;
+            hip_bvh_ref const* end = one.r + one.n;
+            sched.frame([=] __device__ (ray r, random_sampler<float>& samp) -> result_record<float>
+            {
+                result_record<float> result;
+                result.color = vec4(0.1f, 0.2f, 0.3f, 1.0f);
+                auto hr = closest_hit(r, begin, end);
+                result.hit = hr.hit;
+                if (hr.hit)
+                {
+                    hr.isect_pos = r.ori + r.dir * hr.t;
+                    result.depth = hr.t;
+                    vec4 clr(1.0f);
+                    vec3 n = get_normal(dnormals, hr);
+                    vec3 u, v, w = n;
+                    make_orthonormal_basis(u, v, w);
+                    for (int i = 0; i < 8; ++i)
+                    {
+                        auto sp = cosine_sample_hemisphere(samp.next(), samp.next());
+                        auto dir = normalize(sp.x * u + sp.y * v + sp.z * w);
+                        ray ao(hr.isect_pos + dir * 1E-3f, dir);
+                        if (any_hit(ao, begin, end, 0.1f).hit) clr = clr - 1.0f / 8;
+                    }
+                    result.color = vec4(clr.x, clr.y, clr.z, 1.0f);
+                }
+                return result;
+            }, sparams, frame_num);
+            std::vector<float> out(4 * size_t(W) * H), t(size_t(W) * H);
+            rt.download(out.data(), nullptr, t.data());
+            write_file(outdir + "/color.bin", out.data(), out.size() * 4);
+            write_file(outdir + "/t.bin", t.data(), t.size() * 4);
+            return 0;
         }
         else if (mode == "bench")
         {

@@ -77,6 +77,8 @@ def test_reference_api_program_on_hip_backend(golden):
     assert out["sampler_ssaa4_color_hash"] == golden["sampler_ssaa4_hf200_ao"]["color_hash"]
     # make_sched_params(pixel_sampler::uniform_type, cam.get_view_matrix(), cam.get_proj_matrix(), rt)
     assert out["matrix_color_hash"] == golden["matrix_uniform_hf200_ao"]["color_hash"]
+    # make_hip_ao_kernel(bvh, bg, 16) into a hip_buffer_rt (which has an occlusion byte): renders
+    assert out["ao16_color_hash"] != "0000000000000000"
     assert out["matrix_t_hash"] == golden["matrix_uniform_hf200_ao"]["t_hash"]
 
 

@@ -167,11 +167,23 @@ def test_scissor_leaves_outside_pixels_untouched(ctx, oracle_mod):
     assert (out["prim_id"] == 0xFFFFFFFF).all()
 
 
-def test_occlusion_target_rejects_more_than_8_samples(ctx):
+def test_occlusion_target_with_more_than_8_samples(ctx):
+    """An occlusion byte holds 8 sample bits: a kernel asked to write masks of 9 samples into one is
+    rejected; by default such a kernel leaves the buffer untouched (VRH_KERNEL_NO_OCC) and its colour
+    equals a render into a target without the buffer."""
     host, dev = device_scene(ctx, "hf64")
     cam, _, _ = scenes.scene_camera("hf64", 160, 90)
     rt = va.hip_buffer_rt(ctx, 160, 90)
+    sp = va.make_sched_params(va.pixel_sampler.uniform_type, cam, rt)
     with pytest.raises(_capi.VrhError):
-        va.hip_sched(ctx).frame(va.ao_kernel(dev, samples=9), va.make_sched_params(va.pixel_sampler.uniform_type, cam, rt))
+        va.hip_sched(ctx).frame(va.ao_kernel(dev, samples=9, occ=True), sp)
+    before = rt.download()["occ"].copy()
+    va.hip_sched(ctx).frame(va.ao_kernel(dev, samples=16), sp)
+    out = rt.download()
+    assert np.array_equal(out["occ"], before)
     rt2 = va.hip_buffer_rt(ctx, 160, 90, flags=_capi.VRH_RT_COLOR | _capi.VRH_RT_PRIM_ID)
     va.hip_sched(ctx).frame(va.ao_kernel(dev, samples=16), va.make_sched_params(va.pixel_sampler.uniform_type, cam, rt2))
+    out2 = rt2.download()
+    assert np.array_equal(out["color"].view(np.uint32), out2["color"].view(np.uint32))
+    assert np.array_equal(out["prim_id"], out2["prim_id"])
+    assert len(np.unique(out2["color"][out2["prim_id"] != 0xFFFFFFFF][:, 0])) > 8   # 16-sample grey levels

@@ -100,7 +100,9 @@ def test_mask_in_batched_and_sharded_launches(ctx, golden):
         pid = np.full(rows * W, 0xFFFFFFFF, np.uint32)
         pid[:n] = o["prim_id"][n:]                                  # frame 1 of the batch
         parts.append(pid)
-    full = multigpu.unshard_host(np.stack(parts), W, H, 3)
+    wire = multigpu.wire_layout(_capi.VRH_RT_PRIM_ID, W, H, 1, 3)
+    gathered = np.stack([p.view(np.uint8) for p in parts])
+    full = multigpu.unshard(gathered, wire, _capi.VRH_RT_PRIM_ID, W, H, 3, 0)["prim_id"]
     assert np.array_equal(full, ref["prim_id"])
 
 

@@ -78,6 +78,34 @@ def test_reference_ao_kernel_on_hip_sched(tmp_path, golden, oracle_mod, case):
     assert abs(tot - g["occluded_samples"]) <= max(8, g["occluded_samples"] // 1000)
 
 
+UK_BIN = os.path.join(ROOT, "build", "tests", "user_kernels")
+GRID = {"hf64": 64, "hf200": 200, "hf1M": 708}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["rs_hf64_160x90_f0", "rs_hf1M_f1"])
+def test_standalone_random_sampler_and_ao_kernel(tmp_path, golden, oracle_mod, case):
+    """Without the reference headers (hip_kernels.h + standalone.h): the restated random_sampler<float>
+    draws bit-exact, the AO example's kernel with the restated cosine_sample_hemisphere on the same bar
+    as the reference-header build."""
+    g = golden[case]
+    ref = np.load(os.path.join(GOLDEN, case + ".npz"))
+    d = tmp_path / "d"
+    d.mkdir()
+    args = [str(GRID[g["scene"]]), str(g["W"]), str(g["H"]), str(d), str(g["frame"])]
+    subprocess.run([UK_BIN, "draws", *args], check=True, capture_output=True, timeout=120)
+    draws = np.fromfile(d / "color.bin", np.float32).reshape(-1, 4)
+    assert oracle_mod.fnv1a(draws) == g["draws_hash"]
+    subprocess.run([UK_BIN, "rsao", *args], check=True, capture_output=True, timeout=120)
+    color = np.fromfile(d / "color.bin", np.float32).reshape(-1, 4)
+    t = np.fromfile(d / "t.bin", np.float32)
+    hit = ~np.all(color == BG, axis=1)
+    assert np.array_equal(hit, ref["ao_count"] != 255)
+    assert oracle_mod.fnv1a(np.where(hit, t, np.float32(-1.0)).astype(np.float32)) == g["t_hash"]
+    k = np.where(hit, np.rint((1.0 - color[:, 0]) * 8.0), 255).astype(np.uint8)
+    assert float(np.mean(k == ref["ao_count"])) >= 0.999
+
+
 @pytest.mark.gpu
 @needs_bin
 @pytest.mark.parametrize("case,mode", [("shade_hf64_face", "shade"), ("shade_hf64_vertex", "shade"),

@@ -67,8 +67,9 @@ rt = va.hip_buffer_rt(ctx, W, H * F)
 say(f"orbit {ORBIT} deg/frame, {F} frames per launch")
 say(f"scene {scene} {len(prims)} prims depth {host.max_depth} ao={ao} wide records {dev.info['wide_records']} "
     f"(depth {dev.info['wide_depth']})")
-OPTIONS = ("block_threads", "stack_cap", "ao_schedule", "blocks_per_cu", "waves_per_simd", "exact_minmax", "xcd_queues", "ao_gate",
-           "refill_min", "wide_anyhit", "descent_cap", "pop_on_miss", "coop_fetch", "scalar_fetch", "ao_cut")
+# the options the variants set (reset to 0 = auto between variants); a library without one of them
+# (an older build, VRH_LIB) is then only asked for the ones its variants use
+OPTIONS = sorted({k for v in VARIANTS for k in v if k != "name"})
 res = {v["name"]: [] for v in VARIANTS}
 bases = [frame_bases(1 + k * F, F) for k in range(3)]     # the same camera path for every variant
 one = va.hip_buffer_rt(ctx, W, H)

@@ -45,6 +45,7 @@ class vrh_point_light(C.Structure):
 
 
 VRH_KERNEL_COUNT_TESTS = 1
+VRH_KERNEL_NO_OCC = 2
 VRH_BAND_ROWS = 8
 VRH_MAX_BATCH = 32
 VRH_OPT_BLOCK_THREADS, VRH_OPT_STACK_CAP, VRH_OPT_AO_SCHEDULE, VRH_OPT_BLOCKS_PER_CU = 1, 2, 3, 4
@@ -52,6 +53,7 @@ VRH_OPT_WAVES_PER_SIMD, VRH_OPT_EXACT_MINMAX, VRH_OPT_XCD_QUEUES, VRH_OPT_REFILL
 VRH_OPT_WIDE_ANYHIT, VRH_OPT_DESCENT_CAP, VRH_OPT_POP_ON_MISS, VRH_OPT_COOP_FETCH = 10, 11, 12, 13
 VRH_OPT_SCALAR_FETCH, VRH_OPT_PAIR_LAYOUT, VRH_OPT_AO_GATE, VRH_OPT_WAVE_TIMES = 14, 15, 16, 19
 VRH_OPT_AO_CUT = 20
+VRH_OPT_AO_STEAL = 21
 VRH_MAX_TIMED_FRAMES = 1024
 VRH_MAX_SCENE_LIST = 8
 VRH_GROUP_ID_BYTES = 128
@@ -115,6 +117,14 @@ class vrh_obj_info(C.Structure):
                 ("num_tex_coords", C.c_uint32), ("num_materials", C.c_uint32), ("num_degenerate", C.c_uint32),
                 ("num_unknown_materials", C.c_uint32), ("num_missing_files", C.c_uint32),
                 ("reserved", C.c_uint32), ("bbox_min", C.c_float * 3), ("bbox_max", C.c_float * 3)]
+
+
+class vrh_wire_layout(C.Structure):
+    _fields_ = [("prim_id", C.c_uint64), ("occ", C.c_uint64), ("t", C.c_uint64), ("color", C.c_uint64),
+                ("code", C.c_uint64), ("shard_bytes", C.c_uint64), ("rows", C.c_uint32), ("derive", C.c_uint32)]
+
+
+VRH_WIRE_ABSENT = (1 << 64) - 1
 
 
 class VrhError(RuntimeError):
@@ -183,6 +193,14 @@ SIGNATURES = {
     "vrh_group_broadcast_scene": (C.c_int, [_u32, C.POINTER(_vp), _vp, C.POINTER(_vp)]),
     "vrh_render_sharded": (C.c_int, [_u32, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(vrh_kernel_desc), _vp, _u32,
                                      C.POINTER(vrh_camera), _u32, _u32, _u32]),
+    "vrh_group_shards_of": (C.c_uint32, [_u32, _u32, _u32, C.POINTER(_u32), _u32]),
+    "vrh_group_shard_owner": (C.c_uint32, [_u32, _u32]),
+    "vrh_group_wire_layout": (C.c_int, [_u32, C.POINTER(vrh_kernel_desc), _u32, _u32, _u32, _u32,
+                                        C.POINTER(vrh_wire_layout)]),
+    "vrh_shard_packed_rows": (C.c_int, [_u32, _u32, _u32, C.POINTER(C.c_int32)]),
+    "vrh_pack_codes_host": (C.c_int, [_vp, _vp, _vp, C.c_uint64]),
+    "vrh_unshard_host": (C.c_int, [_vp, C.POINTER(vrh_wire_layout), _u32, _u32, _u32, _u32, _u32,
+                                   C.POINTER(vrh_kernel_desc), _vp, _vp, _vp, _vp]),
     "vrh_gen_heightfield": (C.c_int, [_u32, _vp]),
     "vrh_gen_cornell": (C.c_int, [_vp]),
     "vrh_gen_spheres": (C.c_int, [_u32, _vp]),

@@ -20,6 +20,7 @@
 // previous exchange is done).  vrh_group_sync (or vrh_sync on the context after vrh_group_sync)
 // waits for everything.
 #include "vrh_objects.h"
+#include "vrh_plan.h"
 
 #include <rccl/rccl.h>
 
@@ -74,30 +75,8 @@ int group_init_common(vrh_group* g)
     return VRH_OK;
 }
 
-// what one pixel of a shard carries over the wire for a root target with buffers `fields`
-struct wire_layout
-{
-    bool pid = false, occ = false, t = false, color = false;
-    bool derive = false;                   // colour re-derived on the root from prim id (+ AO mask)
-    bool code = false;                     // ... from one byte: 0xFF miss, else the occluded-sample count
-    size_t bytes_per_px() const { return (pid ? 4 : 0) + (occ ? 1 : 0) + (t ? 4 : 0) + (color ? 16 : 0) + (code ? 1 : 0); }
-};
-
-wire_layout layout_for(uint32_t fields, const vrh_kernel_desc& k)
-{
-    wire_layout w;
-    const bool builtin_colour = k.kind <= VRH_KERNEL_AO && (k.kind != VRH_KERNEL_AO || k.samples <= 8);
-    w.derive = (fields & VRH_RT_COLOR) && builtin_colour;
-    w.color = (fields & VRH_RT_COLOR) && !builtin_colour;
-    w.pid = (fields & VRH_RT_PRIM_ID) || w.derive;
-    w.occ = k.kind == VRH_KERNEL_AO && (((fields & VRH_RT_OCC) && k.samples <= 8) || w.derive);
-    w.t = (fields & VRH_RT_T) != 0;
-    // a colour target without prim id / mask targets: the built-in colour depends only on hit and
-    // the number of occluded samples (ao/main.cpp:234-238), so 1 B per pixel crosses the wire, not 5
-    w.code = w.derive && !(fields & VRH_RT_PRIM_ID) && !(fields & VRH_RT_OCC);
-    if (w.code) w.pid = w.occ = false;
-    return w;
-}
+using plan::wire_layout;
+using plan::layout_for;
 
 // (re)allocate a staging buffer; an exchange or render still using the old one is waited for first
 int grow(vrh_group* g, uint8_t*& p, size_t& have, size_t need)
@@ -273,12 +252,12 @@ VRH_API int vrh_render_sharded(uint32_t n, vrh_group* const* groups, const vrh_s
                   "vrh_render_sharded: an occlusion target records at most 8 AO samples");
     }
     // packed shard geometry: every shard uses shard 0's (largest) band count
-    const uint32_t rows = VRH_BAND_ROWS * vrh_shard_bands(H, 0, S);
+    const uint32_t rows = VRH_BAND_ROWS * plan::shard_bands(H, 0, S);
     const size_t px = size_t(rows) * W * num_frames;          // pixels of one shard (all frames)
-    const size_t shard_bytes = wl.bytes_per_px() * px;
+    const plan::wire_offsets wo = plan::offsets_for(wl, px);
+    const size_t shard_bytes = wo.shard_bytes;
     VRH_CHECK(shard_bytes > 0, "vrh_render_sharded: nothing to gather");
-    const size_t o_pid = 0, o_occ = o_pid + (wl.pid ? 4 * px : 0), o_t = o_occ + (wl.occ ? px : 0),
-                 o_col = o_t + (wl.t ? 4 * px : 0), o_code = o_col + (wl.color ? 16 * px : 0);
+    const size_t o_pid = wo.pid, o_occ = wo.occ, o_t = wo.t, o_col = wo.col, o_code = wo.code;
     const bool ao = kernels[0].kind == VRH_KERNEL_AO;
 
     // 1. every local group renders its shards into this call's staging slot (context stream)
@@ -293,14 +272,14 @@ VRH_API int vrh_render_sharded(uint32_t n, vrh_group* const* groups, const vrh_s
         slot_of[i] = si;
         auto& sl = g->slot[si];
         if (sl.used) VRH_HIP(hipStreamWaitEvent(ctx->stream, sl.done, 0));   // the slot's last exchange
-        const uint32_t mine = S > g->rank ? (S - g->rank + N - 1) / N : 0;    // shards s = rank, rank + N, ...
+        const uint32_t mine = plan::owned_count(S, N, g->rank);              // shards s = rank, rank + N, ...
         int rc = grow(g, sl.send, sl.send_bytes, std::max<size_t>(mine * shard_bytes, 1));
         if (!rc && g->rank == 0) rc = grow(g, sl.recv, sl.recv_bytes, S * shard_bytes);
         if (!rc && wl.code && mine) rc = grow(g, g->work, g->work_bytes, 5 * px);
         if (rc) return rc;
         for (uint32_t j = 0; j < mine; ++j)
         {
-            const uint32_t s = g->rank + j * N;
+            const uint32_t s = plan::owned_shard(g->rank, N, j);
             uint8_t* base = sl.send + size_t(j) * shard_bytes;
             vrh_rt rt{};
             rt.ctx = ctx; rt.width = W; rt.height = rows * num_frames; rt.owned = false;
@@ -325,19 +304,24 @@ VRH_API int vrh_render_sharded(uint32_t n, vrh_group* const* groups, const vrh_s
         VRH_HIP(hipStreamWaitEvent(g->stream, sl.rendered, 0));
     }
     // 2. the exchange: every shard to the root, one send / receive pair per shard
+    // (an error inside the group still closes it: the thread's next RCCL call must not join a stale group)
     VRH_NCCL(ncclGroupStart());
-    for (uint32_t i = 0; i < n; ++i)
+    ncclResult_t xr = ncclSuccess;
+    for (uint32_t i = 0; i < n && xr == ncclSuccess; ++i)
     {
         vrh_group* g = groups[i];
         auto& sl = g->slot[slot_of[i]];
-        const uint32_t mine = S > g->rank ? (S - g->rank + N - 1) / N : 0;
-        for (uint32_t j = 0; j < mine; ++j)
-            VRH_NCCL(ncclSend(sl.send + size_t(j) * shard_bytes, shard_bytes, ncclUint8, 0, g->comm, g->stream));
+        const uint32_t mine = plan::owned_count(S, N, g->rank);
+        for (uint32_t j = 0; j < mine && xr == ncclSuccess; ++j)
+            xr = ncclSend(sl.send + size_t(j) * shard_bytes, shard_bytes, ncclUint8, 0, g->comm, g->stream);
         if (g->rank == 0)
-            for (uint32_t s = 0; s < S; ++s)
-                VRH_NCCL(ncclRecv(sl.recv + size_t(s) * shard_bytes, shard_bytes, ncclUint8, int(s % N), g->comm, g->stream));
+            for (uint32_t s = 0; s < S && xr == ncclSuccess; ++s)
+                xr = ncclRecv(sl.recv + size_t(s) * shard_bytes, shard_bytes, ncclUint8, int(plan::shard_owner(s, N)),
+                              g->comm, g->stream);
     }
-    VRH_NCCL(ncclGroupEnd());
+    const ncclResult_t xe = ncclGroupEnd();
+    if (xr == ncclSuccess) xr = xe;
+    if (xr != ncclSuccess) { set_error(std::string("vrh_render_sharded: exchange: ") + ncclGetErrorString(xr)); return VRH_ERR_HIP; }
     // 3. the root lays the bands back into image order, frame by frame
     for (uint32_t i = 0; i < n; ++i)
     {
@@ -346,35 +330,101 @@ VRH_API int vrh_render_sharded(uint32_t n, vrh_group* const* groups, const vrh_s
         VRH_HIP(hipSetDevice(g->ctx->device));
         if (g->rank == 0)
         {
-            const size_t fpx = size_t(rows) * W;               // pixels of one frame of one shard
             for (uint32_t f = 0; f < num_frames; ++f)
             {
-                unshard_params u{};
-                u.width = W; u.height = H; u.count = S; u.rows_per_shard = rows;
-                u.gpid = wl.pid ? reinterpret_cast<const char*>(sl.recv + o_pid + 4 * f * fpx) : nullptr;
-                u.gocc = wl.occ ? reinterpret_cast<const char*>(sl.recv + o_occ + f * fpx) : nullptr;
-                u.gt = wl.t ? reinterpret_cast<const char*>(sl.recv + o_t + 4 * f * fpx) : nullptr;
-                u.gcolor = wl.color ? reinterpret_cast<const char*>(sl.recv + o_col + 16 * f * fpx) : nullptr;
-                u.gcode = wl.code ? reinterpret_cast<const char*>(sl.recv + o_code + f * fpx) : nullptr;
-                u.stride_pid = u.stride_occ = u.stride_t = u.stride_color = u.stride_code = shard_bytes;
-                const size_t fo = size_t(f) * W * H;
-                u.color = (fields & VRH_RT_COLOR) ? dst->color + fo : nullptr;
-                u.pid = (fields & VRH_RT_PRIM_ID) ? dst->prim_id + fo : nullptr;
-                u.occ = (fields & VRH_RT_OCC) && wl.occ ? dst->occ + fo : nullptr;
-                u.t = (fields & VRH_RT_T) ? dst->t + fo : nullptr;
-                u.ao = kernels[i].kind == VRH_KERNEL_AO ? 1u : 0u;
-                u.samples = kernels[i].samples ? kernels[i].samples : 1u;
-                std::memcpy(u.bg, kernels[i].bg, 16);
-                const uint32_t* sb = cams[f].scissor;
-                const bool whole = sb[0] == 0 && sb[1] == 0 && sb[2] == 0 && sb[3] == 0;
-                u.clip[0] = whole ? 0u : std::min(sb[0], W); u.clip[1] = whole ? 0u : std::min(sb[1], H);
-                u.clip[2] = whole ? W : std::min(sb[2], W); u.clip[3] = whole ? H : std::min(sb[3], H);
+                const unshard_params u = plan::frame_params(wl, wo, sl.recv, W, H, S, rows, f, fields, kernels[i],
+                                                            dst->color, dst->prim_id, dst->occ, dst->t, cams[f].scissor);
                 VRH_HIP(launch_unshard(u, g->stream));
             }
+            // the target is written on the group's stream: its context's downloads, clears, renders
+            // and vrh_sync wait for this event (rt_wait) without a host synchronisation
+            VRH_HIP(mark_written(dst, g->stream));
         }
         VRH_HIP(hipEventRecord(sl.done, g->stream));
         sl.used = true;
     }
+    return VRH_OK;
+}
+
+// ---- the plan as host functions (vrh.h; tests/test_multigpu_gloo.py drives them) ----------------
+
+VRH_API uint32_t vrh_group_shards_of(uint32_t nranks, uint32_t rank, uint32_t shards, uint32_t* out, uint32_t cap)
+{
+    if (nranks == 0 || rank >= nranks) return 0;
+    const uint32_t n = plan::owned_count(shards, nranks, rank);
+    for (uint32_t j = 0; j < n && j < cap && out; ++j) out[j] = plan::owned_shard(rank, nranks, j);
+    return n;
+}
+
+VRH_API uint32_t vrh_group_shard_owner(uint32_t nranks, uint32_t shard)
+{
+    return nranks ? plan::shard_owner(shard, nranks) : 0u;
+}
+
+VRH_API int vrh_group_wire_layout(uint32_t fields, const vrh_kernel_desc* k, uint32_t width, uint32_t height,
+                                  uint32_t frames, uint32_t shards, vrh_wire_layout* out)
+{
+    VRH_CHECK(k && out && shards >= 1 && frames >= 1, "vrh_group_wire_layout: bad argument");
+    const wire_layout wl = layout_for(fields, *k);
+    const uint32_t rows = VRH_BAND_ROWS * plan::shard_bands(height, 0, shards);
+    const plan::wire_offsets o = plan::offsets_for(wl, size_t(rows) * width * frames);
+    const uint64_t none = ~0ull;
+    out->prim_id = wl.pid ? o.pid : none;
+    out->occ = wl.occ ? o.occ : none;
+    out->t = wl.t ? o.t : none;
+    out->color = wl.color ? o.col : none;
+    out->code = wl.code ? o.code : none;
+    out->shard_bytes = o.shard_bytes;
+    out->rows = rows;
+    out->derive = wl.derive ? 1u : 0u;
+    return VRH_OK;
+}
+
+VRH_API int vrh_shard_packed_rows(uint32_t height, uint32_t shard, uint32_t shards, int32_t* rows_out)
+{
+    VRH_CHECK(rows_out && shards >= 1 && shard < shards, "vrh_shard_packed_rows: bad argument");
+    const uint32_t rows = VRH_BAND_ROWS * plan::shard_bands(height, 0, shards);
+    for (uint32_t r = 0; r < rows; ++r) rows_out[r] = -1;
+    // the inverse of the kernel's packed row (tile_pixel: band lb * S + s, row lb * BAND + in_band),
+    // from the root's side: every image row whose home is this shard
+    for (uint32_t y = 0; y < height; ++y)
+    {
+        uint32_t s, lrow;
+        plan::row_home(y, shards, s, lrow);
+        if (s == shard && lrow < rows) rows_out[lrow] = int32_t(y);
+    }
+    return VRH_OK;
+}
+
+VRH_API int vrh_pack_codes_host(const uint32_t* prim_id, const uint8_t* occ, uint8_t* code, uint64_t n)
+{
+    VRH_CHECK((prim_id && code) || n == 0, "vrh_pack_codes_host: null argument");
+    for (uint64_t i = 0; i < n; ++i) code[i] = plan::pack_code(prim_id[i], occ, size_t(i));
+    return VRH_OK;
+}
+
+VRH_API int vrh_unshard_host(const void* gathered, const vrh_wire_layout* wire, uint32_t width, uint32_t height,
+                             uint32_t shards, uint32_t frame, uint32_t fields, const vrh_kernel_desc* k,
+                             void* color, uint32_t* prim_id, uint8_t* occ, float* t)
+{
+    VRH_CHECK(gathered && wire && k && shards >= 1, "vrh_unshard_host: bad argument");
+    const wire_layout wl = layout_for(fields, *k);
+    const uint32_t rows = VRH_BAND_ROWS * plan::shard_bands(height, 0, shards);
+    VRH_CHECK(wire->rows == rows, "vrh_unshard_host: wire layout of another geometry");
+    const size_t frames = rows ? size_t(wire->shard_bytes / (wl.bytes_per_px() * size_t(rows) * width)) : 0;
+    VRH_CHECK(frame < frames, "vrh_unshard_host: frame out of range");
+    const plan::wire_offsets o = plan::offsets_for(wl, size_t(rows) * width * frames);
+    const uint32_t whole[4] = { 0, 0, 0, 0 };
+    // the destination buffers hold this one frame: frame_params offsets them by f * W * H, so step back
+    const size_t fo = size_t(frame) * width * height;
+    float4* c = color ? static_cast<float4*>(color) - fo : nullptr;
+    uint32_t* p = prim_id ? prim_id - fo : nullptr;
+    uint8_t* q = occ ? occ - fo : nullptr;
+    float* tt = t ? t - fo : nullptr;
+    const unshard_params u = plan::frame_params(wl, o, static_cast<const uint8_t*>(gathered), width, height, shards, rows,
+                                                frame, fields, *k, c, p, q, tt, whole);
+    for (uint32_t y = 0; y < height; ++y)
+        for (uint32_t x = 0; x < width; ++x) plan::unshard_pixel(u, x, y);
     return VRH_OK;
 }
 

@@ -7,6 +7,7 @@
 
 #include "vrh_internal.h"
 #include "vrh_kernels.h"
+#include "vrh_plan.h"
 #include "vrh_lbvh.h"
 
 #include <hip/hip_runtime.h>
@@ -37,7 +38,13 @@ int select_device(vrh_ctx* ctx)
     return VRH_OK;
 }
 
-uint32_t bands_of(uint32_t height) { return (height + VRH_BAND_ROWS - 1u) / VRH_BAND_ROWS; }
+// a render group's root writes its target on the group's stream (vrh_render_sharded): work on the
+// target's context stream waits for that (an event wait, no host synchronisation)
+int rt_wait(vrh_ctx* ctx, vrh_rt* rt)
+{
+    if (rt && rt->written_pending) VRH_HIP(hipStreamWaitEvent(ctx->stream, rt->written, 0));
+    return VRH_OK;
+}
 
 } // namespace
 
@@ -107,6 +114,7 @@ VRH_API int vrh_ctx_destroy(vrh_ctx* ctx)
     if (ctx->counters) (void)hipFree(ctx->counters);
     if (ctx->wave_times) (void)hipFree(ctx->wave_times);
     if (ctx->spill) (void)hipFree(ctx->spill);
+    if (ctx->steal) (void)hipFree(ctx->steal);
     for (auto e : ctx->ev_start) (void)hipEventDestroy(e);
     for (auto e : ctx->ev_stop) (void)hipEventDestroy(e);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -135,8 +143,9 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
         VRH_CHECK(value == 0 || value == 2, "vrh_ctx_set_option: cooperative fetch was removed (2 = off is accepted)");
         if (value == 1) return VRH_ERR_UNSUPPORTED;
         break;
-    case VRH_OPT_WAVE_TIMES: VRH_CHECK(value <= 1, "vrh_ctx_set_option: wave times is 1 (on) or 0 (off)"); ctx->opt_wave_times = int(value); break;
+    case VRH_OPT_WAVE_TIMES: VRH_CHECK(value <= 2, "vrh_ctx_set_option: wave times is 1 (on), 2 (on + AO stash diagnostics) or 0 (off)"); ctx->opt_wave_times = int(value); break;
     case VRH_OPT_AO_CUT: VRH_CHECK(value <= 3, "vrh_ctx_set_option: AO cut is 1 (on, entries nearest-first), 2 (off) or 3 (on, entries in cut order)"); ctx->opt_cut = int(value); break;
+    case VRH_OPT_AO_STEAL: VRH_CHECK(value <= 2 || (value >= 4 && value <= 4096), "vrh_ctx_set_option: AO steal is 1 (on), 2 (off) or 4..4096 (tiles per wave and queue x 16 counted as the last round)"); ctx->opt_steal = int(value); break;
     case VRH_OPT_AO_GATE: VRH_CHECK(value <= 2, "vrh_ctx_set_option: AO gate is 1 (on) or 2 (off)"); ctx->opt_gate = int(value); break;
     case VRH_OPT_POP_ON_MISS: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pop on miss is 1 (on) or 2 (off)"); ctx->opt_pop = int(value); break;
     case VRH_OPT_PAIR_LAYOUT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pair layout is 1 (line pairing) or 2 (builder order)"); ctx->opt_layout = int(value); break;
@@ -748,6 +757,13 @@ VRH_API int vrh_rt_free(vrh_rt* rt)
         if (rt->mh_prim_id) (void)hipFree(rt->mh_prim_id);
         if (rt->mh_t) (void)hipFree(rt->mh_t);
     }
+    if (rt->written)
+    {
+        if (rt->ctx) (void)hipSetDevice(rt->ctx->device);
+        (void)hipEventSynchronize(rt->written);
+        if (rt->ctx && rt->ctx->group_written == rt->written) rt->ctx->group_written = nullptr;
+        (void)hipEventDestroy(rt->written);
+    }
     delete rt;
     return VRH_OK;
 }
@@ -772,6 +788,8 @@ VRH_API int vrh_rt_clear(vrh_ctx* ctx, vrh_rt* rt, const float color[4])
     if (rc) return rc;
     size_t n = size_t(rt->width) * rt->height;
     float4 c = color ? make_float4(color[0], color[1], color[2], color[3]) : make_float4(0, 0, 0, 0);
+    rc = rt_wait(ctx, rt);
+    if (rc) return rc;
     hipLaunchKernelGGL(fill_rt_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, ctx->stream,
                        rt->color, rt->prim_id, rt->t, rt->occ, n, c);
     VRH_HIP(hipGetLastError());
@@ -782,9 +800,7 @@ VRH_API int vrh_rt_clear(vrh_ctx* ctx, vrh_rt* rt, const float color[4])
 
 VRH_API uint32_t vrh_shard_bands(uint32_t height, uint32_t index, uint32_t count)
 {
-    uint32_t bands = bands_of(height);
-    if (count == 0 || index >= count || index >= bands) return 0;
-    return (bands - index + count - 1) / count;
+    return plan::shard_bands(height, index, count);
 }
 
 VRH_API int vrh_render(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_camera* cam,
@@ -938,7 +954,8 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     {
         VRH_CHECK(k->samples >= 1 && k->samples <= 32, "vrh_render: AO samples must be in [1, 32]");
         // the occlusion target holds one bit per sample in a byte
-        VRH_CHECK(!rt->occ || k->samples <= 8, "vrh_render: a VRH_RT_OCC target records at most 8 AO samples");
+        VRH_CHECK(!rt->occ || k->samples <= 8 || (k->flags & VRH_KERNEL_NO_OCC),
+                  "vrh_render: a VRH_RT_OCC target records at most 8 AO samples (VRH_KERNEL_NO_OCC leaves it out)");
         VRH_CHECK(sc->normals, "vrh_render: AO needs normals");
     }
     const vrh_hit_mask* hmask = k->hit_mask;
@@ -1028,6 +1045,8 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
 
     int rc = select_device(ctx);
     if (rc) return rc;
+    rc = rt_wait(ctx, rt);
+    if (rc) return rc;
 
     render_params p{};
     p.pairs = sc->pairs; p.prims = sc->prims; p.normals = sc->normals; p.root = sc->roots[0];
@@ -1099,7 +1118,8 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     p.tiles_x = (cam->width + 7u) / 8u;
     p.num_tiles = local_bands * p.tiles_x;        // a band is one row of 8x8 tiles
     VRH_CHECK(uint64_t(p.num_tiles) * 64u * num_frames < (1ull << 32) && p.num_tiles < (1u << 26), "vrh_render: image too large");
-    p.color = rt->color; p.prim_id = rt->prim_id; p.t = rt->t; p.occ = rt->occ;
+    p.color = rt->color; p.prim_id = rt->prim_id; p.t = rt->t;
+    p.occ = (k->flags & VRH_KERNEL_NO_OCC) ? nullptr : rt->occ;
     p.counters = ctx->counters;
     // tile queues: per-XCD strips; with frames in flight the band-interleaved order (auto) for AO
     // and for scenes larger than the 256 MB Infinity Cache.  Measured with a camera orbiting 0.5 deg
@@ -1151,6 +1171,46 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
         p.stack_spill = static_cast<uint32_t*>(ctx->spill);
     }
 
+    // AO tail stealing (VRH_OPT_AO_STEAL, vrh_kernels.hip steal_publish): tiles handed out while fewer
+    // than steal_rem remain in their queue (about one per wave: the launch's last round) publish their
+    // hits to a stash whose AO rays every wave without tiles traces.  The stash holds every hit those
+    // tiles can have; a tile that finds it full traces its AO rays itself.
+    if (lc.ao && !lc.count && lc.epi == 0 && !list && !sp && p.samples > 0 && ctx->opt_steal != 2)
+    {
+        const uint64_t nwaves = uint64_t(grid) * uint64_t(waves_per_block);
+        const uint32_t nq = p.xcd_queues ? 8u : 1u;
+        const uint64_t per16 = ctx->opt_steal >= 4 ? uint64_t(ctx->opt_steal) : 16u;
+        p.steal_rem = uint32_t(std::min<uint64_t>((nwaves * per16 / 16u + nq - 1u) / nq, 0xFFFFFFFFull));
+        const uint64_t final_tiles = std::min<uint64_t>(units, uint64_t(p.steal_rem) * nq + nq);
+        const size_t need = size_t(final_tiles) * 64u;
+        if (need > ctx->steal_records)
+        {
+            VRH_HIP(hipStreamSynchronize(ctx->stream));
+            if (ctx->steal) (void)hipFree(ctx->steal);
+            ctx->steal = nullptr;
+            ctx->steal_records = 0;
+            // uncached (MTYPE UC): written on one XCD, read on another within the launch -- the XCDs'
+            // L2s are not coherent with each other for cached device memory
+            VRH_HIP(hipExtMallocWithFlags(&ctx->steal, need * (32u + 8u + 4u), hipDeviceMallocUncached));
+            VRH_HIP(hipMemset(ctx->steal, 0, need * (32u + 8u + 4u)));     // ready flags: no epoch
+            ctx->steal_records = need;
+            ctx->steal_epoch = 0;
+        }
+        if (++ctx->steal_epoch == 0u)
+        {
+            VRH_HIP(hipMemsetAsync(static_cast<char*>(ctx->steal) + ctx->steal_records * 40u, 0, ctx->steal_records * 4u,
+                                   ctx->stream));
+            ctx->steal_epoch = 1u;
+        }
+        char* base = static_cast<char*>(ctx->steal);
+        p.steal_rec = reinterpret_cast<float4*>(base);
+        p.steal_state = reinterpret_cast<unsigned long long*>(base + ctx->steal_records * 32u);
+        p.steal_ready = reinterpret_cast<uint32_t*>(base + ctx->steal_records * 40u);
+        p.steal_cap = uint32_t(std::min<size_t>(ctx->steal_records, 0xFFFFFFFFu));
+        p.steal_epoch = ctx->steal_epoch;
+        p.ao_steal = 1u;
+    }
+
     // per-wave timeline of this launch (diagnostic, VRH_OPT_WAVE_TIMES)
     ctx->wave_times_used = 0;
     if (ctx->opt_wave_times && (lc.sched == 0 || lc.sched == 3))
@@ -1162,11 +1222,17 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
             if (ctx->wave_times) (void)hipFree(ctx->wave_times);
             ctx->wave_times = nullptr;
             ctx->wave_times_n = 0;
-            VRH_HIP(hipMalloc(&ctx->wave_times, n * 2 * sizeof(unsigned long long)));
+            VRH_HIP(hipMalloc(&ctx->wave_times, n * 10 * sizeof(unsigned long long)));
             ctx->wave_times_n = n;
         }
         p.wave_times = ctx->wave_times;
         ctx->wave_times_used = n;
+        if (ctx->opt_wave_times == 2 && p.ao_steal)
+        {
+            // AO stash diagnostics: 8 words per wave after the (start, end) pairs
+            p.steal_dbg = ctx->wave_times + 2 * n;
+            VRH_HIP(hipMemsetAsync(p.steal_dbg, 0, n * 8 * sizeof(unsigned long long), ctx->stream));
+        }
     }
 
     const uint32_t slot = ctx->frames % VRH_MAX_TIMED_FRAMES;
@@ -1199,6 +1265,7 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
 VRH_API int vrh_sync(vrh_ctx* ctx)
 {
     VRH_CHECK(ctx, "vrh_sync: null");
+    if (ctx->group_written) VRH_HIP(hipEventSynchronize(ctx->group_written));
     VRH_HIP(hipStreamSynchronize(ctx->stream));
     return VRH_OK;
 }
@@ -1217,7 +1284,9 @@ VRH_API int vrh_get_wave_times(vrh_ctx* ctx, uint64_t* out, uint64_t capacity, u
         *ticks_per_ms = double(khz);
     }
     if (out && ctx->wave_times_used)
-        VRH_HIP(hipMemcpy(out, ctx->wave_times, std::min<uint64_t>(capacity, 2 * ctx->wave_times_used) * 8, hipMemcpyDeviceToHost));
+        VRH_HIP(hipMemcpy(out, ctx->wave_times,
+                          std::min<uint64_t>(capacity, (ctx->opt_wave_times == 2 ? 10 : 2) * ctx->wave_times_used) * 8,
+                          hipMemcpyDeviceToHost));
     return VRH_OK;
 }
 
@@ -1294,6 +1363,8 @@ VRH_API int vrh_rt_download(vrh_ctx* ctx, vrh_rt* rt, void* color, uint32_t* pri
     int rc = select_device(ctx);
     if (rc) return rc;
     size_t n = size_t(rt->width) * rt->height;
+    rc = rt_wait(ctx, rt);
+    if (rc) return rc;
     VRH_HIP(hipStreamSynchronize(ctx->stream));
     if (color) { VRH_CHECK(rt->color, "vrh_rt_download: target has no colour buffer"); VRH_HIP(hipMemcpy(color, rt->color, n * 16, hipMemcpyDeviceToHost)); }
     if (prim_id) { VRH_CHECK(rt->prim_id, "vrh_rt_download: target has no prim_id buffer"); VRH_HIP(hipMemcpy(prim_id, rt->prim_id, n * 4, hipMemcpyDeviceToHost)); }
@@ -1325,6 +1396,8 @@ VRH_API int vrh_rt_download_multi_hit(vrh_ctx* ctx, vrh_rt* rt, uint32_t* prim_i
     int rc = select_device(ctx);
     if (rc) return rc;
     const size_t n = size_t(rt->width) * rt->height * rt->mh_n;
+    rc = rt_wait(ctx, rt);
+    if (rc) return rc;
     VRH_HIP(hipStreamSynchronize(ctx->stream));
     if (prim_ids) VRH_HIP(hipMemcpy(prim_ids, rt->mh_prim_id, n * 4, hipMemcpyDeviceToHost));
     if (t) VRH_HIP(hipMemcpy(t, rt->mh_t, n * 4, hipMemcpyDeviceToHost));
@@ -1338,6 +1411,8 @@ VRH_API int vrh_rt_upload(vrh_ctx* ctx, vrh_rt* rt, const void* color, const uin
     int rc = select_device(ctx);
     if (rc) return rc;
     size_t n = size_t(rt->width) * rt->height;
+    rc = rt_wait(ctx, rt);
+    if (rc) return rc;
     VRH_HIP(hipStreamSynchronize(ctx->stream));
     if (color) { VRH_CHECK(rt->color, "vrh_rt_upload: target has no colour buffer"); VRH_HIP(hipMemcpy(rt->color, color, n * 16, hipMemcpyHostToDevice)); }
     if (prim_id) { VRH_CHECK(rt->prim_id, "vrh_rt_upload: target has no prim_id buffer"); VRH_HIP(hipMemcpy(rt->prim_id, prim_id, n * 4, hipMemcpyHostToDevice)); }
