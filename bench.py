@@ -20,7 +20,8 @@ tail is paid once per launch.  `value` is K frames' rays over the wall time of t
 The hip_sched::frame path -- one synchronous launch per frame, as the reference's scheduler
 issues frames -- is measured separately over --single-frames frames (median): single_frame_*.
 The timed frames share the scene camera (their AO samples differ); moving_camera_* repeats the
-timed launches with the eye orbiting --moving-camera degrees per frame (no shared primary rays; opt-in).
+timed launches with the eye orbiting --moving-camera degrees per frame (default 0.5: no two frames
+share primary rays), reported beside the headline.
 
 N > 1: one process per GPU, one libvrh render group over RCCL (vrh_group_join, the id broadcast
 by torch.distributed): each rank renders its image-tile shard (8-row bands, band b -> rank b % N,
@@ -37,7 +38,8 @@ Rank 0 prints one JSON line (the contract of the task statement) with:
     gathers) on the microbenchmark tools/micro/l1_roof.hip (profiles/l1_roof.json).  The SURVEY
     §8d algorithmic HBM bytes are kept as roofline.hbm_algorithmic (informational);
   * cpu_baseline: the reference's own SSE4 tiled_sched path (oracle/_ref, built from
-    /root/reference by oracle/Makefile) on a bounded sample, with the host's core count and model.
+    /root/reference by oracle/Makefile) on a bounded sample, best of a worker-thread sweep, with the
+    host's core count, cgroup quota and model, and the retries / stall seconds of tiled_sched stalls.
 """
 from __future__ import annotations
 
@@ -67,15 +69,15 @@ def parse():
     ap.add_argument("--scene", default="hf1M", help="hf1M (C3, default) | hf10M (C4) | sph1M (C5)")
     ap.add_argument("--kernel", default=None, choices=["ao", "primary"], help="default: ao for triangles")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="host threads for the CPU baseline (default: the best of a 16/64/128/256 sweep)")
     ap.add_argument("--no-verify", action="store_true", help="skip the untimed checks against the fixtures")
     ap.add_argument("--frames-in-flight", type=int, default=32,
                     help="max frames per persistent launch (vrh_render_batch, 1..32)")
     ap.add_argument("--single-frames", type=int, default=10, help="frames of the hip_sched::frame leg (median)")
-    ap.add_argument("--moving-camera", type=float, default=0.0,
-                    help="degrees of camera orbit per frame in an extra moving-camera leg (0: no such leg, the "
-                         "default, so the kernel's launches in a profile of the default command are the timed "
-                         "shape only; tools/r02_final.sh runs it with 0.5)")
+    ap.add_argument("--moving-camera", type=float, default=0.5,
+                    help="degrees of camera orbit per frame in an extra moving-camera leg after the timed region "
+                         "(0: no such leg); its launches have the timed launches' shape")
     ap.add_argument("--gather-ids", action="store_true",
                     help="N > 1 / --shards: gather prim ids + AO masks with the colour (5 B per pixel on the wire, not 1)")
     ap.add_argument("--shards", type=int, default=0,
@@ -100,25 +102,68 @@ def host_info():
     return {"cpu_model": model, "host_cpus": os.cpu_count(), "cpus_available": avail}
 
 
-def cpu_baseline(scene, kernel, threads):
-    """Reference SSE4 tiled_sched<ray4> (oracle/_ref/vsnray_ref_bench) on a bounded sample:
-    the same scene and camera at full resolution, 1 warm-up + 3 timed frames (~2-10 s)."""
+def cgroup_cpu_quota():
+    """CPUs the cgroup lets this process use (cpu.max quota / period), or None without a quota."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+CPU_SWEEP = (16, 64, 128, 256)
+CPU_ATTEMPT_TIMEOUT_S = 60
+
+
+def cpu_baseline(scene, kernel, threads=None):
+    """Reference SSE4 tiled_sched<ray4> (oracle/_ref/vsnray_ref_bench) on a bounded sample: the same
+    scene and camera at full resolution, 1 warm-up + 3 timed frames per run.  Without --cpu-threads
+    the worker count is swept over CPU_SWEEP (capped at the CPUs this process may run on) and the
+    best is reported, with every point of the sweep.  tiled_sched can lose a worker's wake-up
+    (tiled_sched.inl:181 waits without a predicate against the notify_all at :386) and stall a frame
+    for good: a run that passes CPU_ATTEMPT_TIMEOUT_S is killed and tried once more, and the line
+    records the retries and the seconds lost to stalls."""
     from oracle import oracle as O
     samples = 8 if kernel == "ao" else 0
     info = host_info()
+    info["cgroup_cpu_quota"] = cgroup_cpu_quota()
     if os.path.exists(O.REF_BENCH_BIN):
-        print(f"cpu baseline: reference tiled_sched, {threads} threads ...", file=sys.stderr, flush=True)
-        try:
-            r = O.ref_bench(scene, threads, 3, 1920, 1080, samples, timeout=150)
-        except subprocess.TimeoutExpired:
-            # tiled_sched's lost-wakeup race (SURVEY.md §5) can stall a frame: one more try (CPU only)
-            print("cpu baseline: timed out, retrying once", file=sys.stderr, flush=True)
-            r = O.ref_bench(scene, threads, 3, 1920, 1080, samples, timeout=150)
-        return {"value": round(r["mrays_per_s"], 3), "unit": "Mrays/s", "cores": threads, "kind": "reference",
+        avail = info["cpus_available"] or 1
+        counts = [threads] if threads else sorted({min(t, avail) for t in CPU_SWEEP})
+        sweep, retries, stall_s = [], 0, 0.0
+        for n in counts:
+            print(f"cpu baseline: reference tiled_sched, {n} threads ...", file=sys.stderr, flush=True)
+            point = {"threads": n, "value": None, "retries": 0, "stall_s": 0.0}
+            for attempt in range(2):
+                t0 = time.perf_counter()
+                try:
+                    r = O.ref_bench(scene, n, 3, 1920, 1080, samples, timeout=CPU_ATTEMPT_TIMEOUT_S)
+                except subprocess.TimeoutExpired:
+                    lost = time.perf_counter() - t0
+                    print(f"cpu baseline: {n} threads stalled ({lost:.0f} s, tiled_sched lost wake-up)",
+                          file=sys.stderr, flush=True)
+                    point["stall_s"] = round(point["stall_s"] + lost, 1)
+                    if attempt == 0:
+                        point["retries"] += 1
+                    continue
+                point["value"] = round(r["mrays_per_s"], 3)
+                point["rays_per_frame"] = r["rays_per_frame"]
+                break
+            retries += point["retries"]
+            stall_s += point["stall_s"]
+            sweep.append(point)
+        done = [p for p in sweep if p["value"] is not None]
+        if not done:
+            raise RuntimeError(f"every reference run stalled: {sweep}")
+        best = max(done, key=lambda p: p["value"])
+        return {"value": best["value"], "unit": "Mrays/s", "cores": best["threads"], "kind": "reference",
                 "sample": f"{scene} 1920x1080, {samples} AO spp, tiled_sched<basic_ray<simd::float4>> -O3 -msse4.1, "
-                          f"{threads} worker threads, median of 3 frames after 1 warm-up ({r['rays_per_frame']} rays/frame)",
-                **info}
+                          f"best of a worker-thread sweep {counts}, each the median of 3 frames after 1 warm-up "
+                          f"({best['rays_per_frame']} rays/frame)",
+                "sweep": sweep, "retries": retries, "stall_s": round(stall_s, 1), **info}
     # fallback: the plain-C restatement (scalar, OpenMP rows) on 1/8 of the image rows
+    threads = threads or min(16, info["cpus_available"] or 1)
     sc = O.make_scene(scene)
     cam = O.scene_camera(scene)
     mode = O.VO_MODE_AO if kernel == "ao" else O.VO_MODE_PRIMARY
@@ -129,7 +174,7 @@ def cpu_baseline(scene, kernel, threads):
     dt = time.perf_counter() - t0
     return {"value": round(out["rays"] / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{scene} rows {rows[0]}-{rows[1]} of 1920x1080 ({out['rays']} rays), scalar C restatement",
-            **info}
+            "retries": 0, "stall_s": 0.0, **info}
 
 
 def frames_per_launch(steps, cap):
@@ -181,7 +226,7 @@ def main():
         try:
             cpu = cpu_baseline(args.scene, kernel, args.cpu_threads)
         except Exception as e:  # reported, never fatal for the GPU measurement
-            cpu = {"value": None, "unit": "Mrays/s", "cores": args.cpu_threads, "kind": "reference",
+            cpu = {"value": None, "unit": "Mrays/s", "cores": args.cpu_threads or 0, "kind": "reference",
                    "sample": f"failed: {e}", **host_info()}
 
     # ---- scene: host build, upload (excluded from timing) --------------------------------------

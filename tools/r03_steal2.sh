@@ -24,5 +24,6 @@ VRH_AB='[{"name":"steal on"},{"name":"steal off","ao_steal":2}]' VRH_AB_BATCH=20
 VRH_AB='[{"name":"steal on"},{"name":"steal off","ao_steal":2},{"name":"steal x2","ao_steal":32},{"name":"steal x0.5","ao_steal":8}]' VRH_AB_BATCH=1 step steal_f1 300 python tools/ab_variants.py hf1M 5
 VRH_AB='[{"name":"steal on"},{"name":"steal off","ao_steal":2}]' VRH_AB_BATCH=1 step steal_f1_hf10M 300 python tools/ab_variants.py hf10M 3
 step timeline 200 python tools/wave_timeline.py hf1M 1 20
+step bench_default 400 python bench.py
 TAIL=4 step pytest_gpu 600 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
 exit 0
