@@ -851,11 +851,25 @@ public:
     // whose height is cams.size() * H, with frame number frame_num + f.  Every frame equals its
     // own frame() call; the launch's tail is paid once instead of once per frame.  Synchronous
     // like frame().
+    // A user kernel (hip_kernels.h, hipcc) renders its frames in one persistent launch the same way.
     template <typename K, typename Camera, typename RT>
     void frames(K kernel, std::vector<Camera> const& cams, RT& rt, unsigned frame_num = 0)
     {
-        static_assert(std::is_same<K, hip_builtin_kernel>::value,
-                      "hip_sched runs the built-in kernels: an arbitrary callable cannot cross the C ABI");
+        if constexpr (!std::is_same<K, hip_builtin_kernel>::value)
+        {
+            static_assert(hip_detail::user_kernels<K>::available,
+                          "hip_sched::frames: a user kernel (a callable) is device code: include "
+                          "visionaray_hip/hip_kernels.h and compile with hipcc");
+            hip_detail::user_kernels<K>::frames(*ctx_, kernel, cams, rt, frame_num);
+        }
+        else
+            frames_builtin(kernel, cams, rt, frame_num);
+    }
+
+private:
+    template <typename Camera, typename RT>
+    void frames_builtin(hip_builtin_kernel const& kernel, std::vector<Camera> const& cams, RT& rt, unsigned frame_num)
+    {
         if (cams.empty() || rt.height() % cams.size() != 0)
             throw std::runtime_error("hip_sched::frames: render target height must be frames x image height");
         const uint32_t W = uint32_t(rt.width()), H = uint32_t(rt.height() / cams.size());
@@ -875,6 +889,7 @@ public:
         rt.end_frame();
     }
 
+public:
     hip_context& context() const { return *ctx_; }
 
 private:

@@ -393,15 +393,76 @@ __device__ inline void walk_slab(vrh_scene_view const& b, vrh::dev::ray_t const&
     }
 }
 
+// An any-hit ray over the scene's 4-wide records (vrh_scene_view::quads, vrh_quad.cpp): the records
+// hold the grandchildren of every binary node, so a ray reaches exactly the leaves the binary walk
+// reaches -- before its first accepted hit an any-hit ray's box tests compare against constants, so
+// whether it finds a hit does not depend on the order -- in half the dependent steps, nearest entry
+// first (as the built-in AO / shadow rays, vrh_device.h ray_step).  Returns false when a record's hits
+// would overflow the stack; the caller then walks the binary records from the root (nothing was
+// accepted so far, so the result is unchanged).
+template <typename Leaf>
+__device__ inline bool walk_quads(vrh_scene_view const& b, vrh::dev::ray_t const& r, float max_t, Leaf&& leaf)
+{
+    using vrh::dev::QUAD_NONE;
+    const float4* quads = static_cast<const float4*>(b.quads);
+    vrh::dev::lds_stack st = user_stack();
+    st.push(0u);
+    while (!st.empty())
+    {
+        uint32_t link = st.pop();
+        bool at_leaf = true;
+        while (!(link & vrh::dev::LEAF_BIT))
+        {
+            const float4* p = quads + 8u * link;
+            const float4 xl = p[0], yl = p[1], zl = p[2], xh = p[3], yh = p[4], zh = p[5], lk = p[6];
+            const uint32_t k0 = __float_as_uint(lk.x), k1 = __float_as_uint(lk.y);
+            const uint32_t k2 = __float_as_uint(lk.z), k3 = __float_as_uint(lk.w);
+            float d0, d1, d2, d3;
+            const bool h0 = vrh::dev::quad_entry(xl.x, yl.x, zl.x, xh.x, yh.x, zh.x, r, max_t, d0) & (k0 != QUAD_NONE);
+            const bool h1 = vrh::dev::quad_entry(xl.y, yl.y, zl.y, xh.y, yh.y, zh.y, r, max_t, d1) & (k1 != QUAD_NONE);
+            const bool h2 = vrh::dev::quad_entry(xl.z, yl.z, zl.z, xh.z, yh.z, zh.z, r, max_t, d2) & (k2 != QUAD_NONE);
+            const bool h3 = vrh::dev::quad_entry(xl.w, yl.w, zl.w, xh.w, yh.w, zh.w, r, max_t, d3) & (k3 != QUAD_NONE);
+            if (!(h0 | h1 | h2 | h3)) { at_leaf = false; break; }
+            if (st.top + 3u * st.stride > st.lim) return false;
+            d0 = h0 ? d0 : INFINITY; d1 = h1 ? d1 : INFINITY; d2 = h2 ? d2 : INFINITY; d3 = h3 ? d3 : INFINITY;
+            const bool a01 = d1 < d0, a23 = d3 < d2;
+            const float m01 = a01 ? d1 : d0, m23 = a23 ? d3 : d2;
+            const uint32_t j = (m23 < m01) ? (a23 ? 3u : 2u) : (a01 ? 1u : 0u);
+            if (h0 & (j != 0u)) st.push(k0);
+            if (h1 & (j != 1u)) st.push(k1);
+            if (h2 & (j != 2u)) st.push(k2);
+            if (h3 & (j != 3u)) st.push(k3);
+            link = j == 0u ? k0 : j == 1u ? k1 : j == 2u ? k2 : k3;
+        }
+        if (!at_leaf) continue;
+        for (uint32_t i = link & ~vrh::dev::LEAF_BIT;; ++i)
+        {
+            uint32_t flags = 0;
+            if (leaf(i, flags)) return true;
+            if (flags & vrh::dev::END_BIT) break;
+        }
+    }
+    return true;
+}
+
 // the LDS stack holds VRH_USER_STACK entries: a deeper BVH (not passed through checked_ref) is not
 // traversed -- a miss, never an out-of-bounds stack write.  The hardware min/max slab test where it is
-// provably identical (vrh_device.h box_pair).
-template <typename Ray, typename CullT, typename Leaf>
+// provably identical (vrh_device.h box_pair).  ANY: an any-hit walk (the leaf ends it at the first
+// accepted hit), which takes the 4-wide records where the scene has them and the ray is finite --
+// the hit / miss answer is the binary walk's; WHICH hit ends the ray may differ, as any hit may
+// (VRH_USER_BINARY_ANYHIT=1 keeps the reference's binary order, and so its first-found hit record).
+#ifndef VRH_USER_BINARY_ANYHIT
+#define VRH_USER_BINARY_ANYHIT 0
+#endif
+template <bool ANY = false, typename Ray, typename CullT, typename Leaf>
 __device__ inline void walk(vrh_scene_view const& b, Ray const& ray, float max_t, CullT const& cull_t, Leaf&& leaf)
 {
     if (b.max_depth >= VRH_USER_STACK) return;
     const vrh::dev::ray_t r = dev_ray(ray);
-    if (b.finite_bounds && vrh::dev::finite_ray(r)) walk_slab<true>(b, r, max_t, cull_t, leaf);
+    const bool fast = b.finite_bounds && vrh::dev::finite_ray(r);
+    if constexpr (ANY && !VRH_USER_BINARY_ANYHIT)
+        if (fast && b.quads && walk_quads(b, r, max_t, leaf)) return;
+    if (fast) walk_slab<true>(b, r, max_t, cull_t, leaf);
     else walk_slab<false>(b, r, max_t, cull_t, leaf);
 }
 
@@ -469,7 +530,7 @@ VRH_FUNC inline auto intersect(
     using RT = typename detail::traversal_result<HR, Traversal, MultiHitMax>::type;
     RT result;
     const float4* prims = static_cast<const float4*>(b.view.prims);
-    hip_detail::walk(b.view, ray, max_t, [&]() { return hip_detail::cull_of(result); },
+    hip_detail::walk<Traversal == detail::AnyHit>(b.view, ray, max_t, [&]() { return hip_detail::cull_of(result); },
                      [&](uint32_t i, uint32_t& flags) -> bool
                      {
                          const P prim = hip_detail::leaf_primitive<P>(prims, i, flags);
@@ -518,7 +579,7 @@ __device__ inline bvh_record traverse_bvh(basic_ray<float> const& ray, vrh_scene
     bvh_record result;
     const float4* prims = static_cast<const float4*>(b.prims);
     // the leaf: every primitive in index order, is_closer / update_if (intersect.inl:103-128)
-    walk(b, ray, max_t, [&]() { return result.t; },
+    walk<Any>(b, ray, max_t, [&]() { return result.t; },
          [&](uint32_t i, uint32_t& flags) -> bool
          {
              HR hr;
@@ -675,27 +736,36 @@ __device__ inline vec3 hip_ao_sample(uint32_t pixel, uint32_t s, uint32_t frame_
 }
 
 //-------------------------------------------------------------------------------------------------
-// The launch: one thread per pixel, 8 x 8 threads (one wave) per block, dynamic LDS for the
-// traversal stacks; cuda_sched.inl:53-99 with sample_pixel's uniform store (colour, and the depth
-// into the target's t buffer when the result carries one).
+// The launch: a persistent grid of one-wave blocks (8 x 8 threads = one 8 x 8 pixel tile, dynamic
+// LDS for the traversal stacks) sized to what is resident on the GPU; the waves take tiles from
+// eight per-XCD queues (vrh_ctx_user_queues) until every tile of every frame is done -- the tiles of
+// a queue are a contiguous strip of each frame (BVH nodes stay in that XCD's L2), a wave drains its
+// own XCD's queue first and then the others in turn.  Per pixel it is cuda_sched.inl:53-99 with
+// sample_pixel's uniform store (colour, and the depth into the target's t buffer when the result
+// carries one).  frames(): several frames per launch (frames in flight), frame f with its own camera
+// and frame number into rows [f * H, (f + 1) * H) of the target, so the launch's tail is paid once.
 //
 
 namespace hip_detail
 {
-struct user_frame
+template <uint32_t NC>
+struct user_frames
 {
-    vrh_camera cam;
+    vrh_camera cam[NC];
     float4* color;
     float* t;
-    uint32_t width, height, frame_num;
+    uint32_t width, height, frame_num, nframes;
     uint32_t x0, y0, x1, y1;      // scissor box, exclusive right / bottom edges
+    uint32_t tiles_x, tiles;      // 8 x 8 tiles of the box per row / per frame
+    uint32_t* queues;             // vrh_ctx_user_queues: 8 heads, VRH_USER_QUEUE_STRIDE words apart
     uint32_t matrix_cam;          // sched_params with camera matrices: their inverses (column-major)
     float inv_view[16], inv_proj[16];
 };
 
-// the primary ray through image position (fx, fy) (the pixel plus the sampler's offset):
+// the primary ray through image position (fx, fy) (the pixel plus the sampler's offset) of camera c:
 // sched_common.h:130-150 (pinhole basis) or :152-176 (camera matrices), the built-in kernels' arithmetic
-__device__ inline basic_ray<float> user_primary_ray(user_frame const& f, float fx, float fy)
+template <uint32_t NC>
+__device__ inline basic_ray<float> user_primary_ray(user_frames<NC> const& f, uint32_t c, float fx, float fy)
 {
     const float u = 2.0f * (fx + 0.5f) / (float)f.width - 1.0f;
     const float v = 2.0f * (fy + 0.5f) / (float)f.height - 1.0f;
@@ -716,10 +786,11 @@ __device__ inline basic_ray<float> user_primary_ray(user_frame const& f, float f
         const vec3 far(d[0] / d[3], d[1] / d[3], d[2] / d[3]);
         return basic_ray<float>(ori, normalize(far - ori));
     }
-    const vec3 cu(f.cam.cam_u[0], f.cam.cam_u[1], f.cam.cam_u[2]);
-    const vec3 cv(f.cam.cam_v[0], f.cam.cam_v[1], f.cam.cam_v[2]);
-    const vec3 cw(f.cam.cam_w[0], f.cam.cam_w[1], f.cam.cam_w[2]);
-    const vec3 eye(f.cam.eye[0], f.cam.eye[1], f.cam.eye[2]);
+    vrh_camera const& cam = f.cam[c];
+    const vec3 cu(cam.cam_u[0], cam.cam_u[1], cam.cam_u[2]);
+    const vec3 cv(cam.cam_v[0], cam.cam_v[1], cam.cam_v[2]);
+    const vec3 cw(cam.cam_w[0], cam.cam_w[1], cam.cam_w[2]);
+    const vec3 eye(cam.eye[0], cam.eye[1], cam.eye[2]);
     return basic_ray<float>(eye, normalize((cu * u + cv * v) + cw));
 }
 
@@ -762,18 +833,17 @@ struct call_with_intersector
 template <typename T, typename = void> struct has_depth : std::false_type {};
 template <typename T> struct has_depth<T, decltype((void)std::declval<T>().depth)> : std::true_type {};
 
-template <typename K, uint32_t SK = VRH_SAMPLER_UNIFORM, uint32_t SN = 1>
-__global__ __launch_bounds__(64) void user_render(K kernel, user_frame f)
+// pixel (x, y) of frame c of the launch
+template <typename K, uint32_t SK, uint32_t SN, uint32_t NC>
+__device__ inline void user_pixel(K& kernel, user_frames<NC> const& f, uint32_t c, uint32_t x, uint32_t y)
 {
-    const uint32_t x = blockIdx.x * 8u + threadIdx.x;
-    const uint32_t y = blockIdx.y * 8u + threadIdx.y;
-    if (x < f.x0 || y < f.y0 || x >= f.x1 || y >= f.y1) return;
-    random_sampler<float> samp(pixel_seed(x, y, f.width, f.height, f.frame_num));
-    const size_t o = size_t(y) * f.width + x;
+    const uint32_t frame_num = f.frame_num + c;
+    random_sampler<float> samp(pixel_seed(x, y, f.width, f.height, frame_num));
+    const size_t o = (size_t(c) * f.height + y) * f.width + x;
     if constexpr (SK == VRH_SAMPLER_UNIFORM)
     {
         // sched_common.h:130-176 make_primary_ray_impl (uniform pixel sampler), as the built-in kernels
-        auto res = invoke_kernel(kernel, user_primary_ray(f, (float)x, (float)y), samp, x, y, 0);
+        auto res = invoke_kernel(kernel, user_primary_ray(f, c, (float)x, (float)y), samp, x, y, 0);
         if (f.color) f.color[o] = make_float4(res.color.x, res.color.y, res.color.z, res.color.w);
         if constexpr (has_depth<decltype(res)>::value)
             if (f.t) f.t[o] = res.depth;
@@ -782,7 +852,7 @@ __global__ __launch_bounds__(64) void user_render(K kernel, user_frame f)
     {
         // the jittered / jittered_blend / ssaa<N> samplers (sched_common.h:196-300, 440-720), with the
         // jitter draws and offset tables of vrh.h vrh_pixel_sampler
-        auto ray_at = [&](float ox, float oy) { return user_primary_ray(f, (float)x + ox, (float)y + oy); };
+        auto ray_at = [&](float ox, float oy) { return user_primary_ray(f, c, (float)x + ox, (float)y + oy); };
         if constexpr (SK == VRH_SAMPLER_SSAA)
         {
             constexpr float off2[2][2] = { { -0.25f, -0.25f }, { 0.25f, 0.25f } };
@@ -806,24 +876,81 @@ __global__ __launch_bounds__(64) void user_render(K kernel, user_frame f)
         }
         else
         {
-            const uint32_t k = (y * f.width + x) * 2u + 0x632BE5ABu + f.frame_num * 0x68E31DA4u;
+            const uint32_t k = (y * f.width + x) * 2u + 0x632BE5ABu + frame_num * 0x68E31DA4u;
             const float oy = vrh::dev::uniform01(k) - 0.5f, ox = vrh::dev::uniform01(k + 1u) - 0.5f;
             auto res = invoke_kernel(kernel, ray_at(ox, oy), samp, x, y, 0);
-            float4 c = make_float4(res.color.x, res.color.y, res.color.z, res.color.w);
+            float4 cl = make_float4(res.color.x, res.color.y, res.color.z, res.color.w);
             if constexpr (SK == VRH_SAMPLER_JITTERED_BLEND)
             {
-                const float a = 1.0f / float(f.frame_num), b = 1.0f - a;
+                const float a = 1.0f / float(frame_num), b = 1.0f - a;
                 if (f.color)
                 {
                     const float4 d = f.color[o];
-                    c = make_float4(c.x * a + d.x * b, c.y * a + d.y * b, c.z * a + d.z * b, c.w * a + d.w * b);
+                    cl = make_float4(cl.x * a + d.x * b, cl.y * a + d.y * b, cl.z * a + d.z * b, cl.w * a + d.w * b);
                 }
             }
-            if (f.color) f.color[o] = c;
+            if (f.color) f.color[o] = cl;
             if constexpr (has_depth<decltype(res)>::value)
                 if (f.t) f.t[o] = res.depth;
         }
     }
+}
+
+__device__ inline uint32_t xcc_id()
+{
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & 7u;
+}
+
+// the persistent loop: queue q hands out strip q (tiles [tiles * q / 8, tiles * (q + 1) / 8)) of
+// every frame, frame-major; every (frame, tile) is handed out exactly once by one of the 8 heads, so
+// which XCD a wave runs on changes only speed.  Every wave leaves once all 8 queues are empty.
+template <typename K, uint32_t SK = VRH_SAMPLER_UNIFORM, uint32_t SN = 1, uint32_t NC = 1>
+__global__ __launch_bounds__(64) void user_render(K kernel, user_frames<NC> f)
+{
+    const uint32_t lane = threadIdx.y * 8u + threadIdx.x;
+    uint32_t q = xcc_id();
+    for (uint32_t tried = 0; tried < 8u; ++tried, q = (q + 1u) & 7u)
+    {
+        const uint32_t lo = uint32_t((uint64_t(f.tiles) * q) / 8u);
+        const uint32_t len = uint32_t((uint64_t(f.tiles) * (q + 1u)) / 8u) - lo;
+        const uint32_t n = len * f.nframes;
+        for (;;)
+        {
+            uint32_t t = 0;
+            if (lane == 0) t = atomicAdd(f.queues + q * VRH_USER_QUEUE_STRIDE, 1u);
+            t = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)t, 0));
+            if (t >= n) break;
+            const uint32_t c = t / len;
+            const uint32_t tile = lo + (t - c * len);
+            const uint32_t ty = tile / f.tiles_x;
+            const uint32_t x = f.x0 + (tile - ty * f.tiles_x) * 8u + threadIdx.x;
+            const uint32_t y = f.y0 + ty * 8u + threadIdx.y;
+            if (x < f.x1 && y < f.y1) user_pixel<K, SK, SN, NC>(kernel, f, c, x, y);
+        }
+    }
+}
+
+// launch `kern` over f on the context's stream: the queues zeroed first, then a grid of as many
+// one-wave blocks as the GPU holds at once (the kernel's own occupancy), at most one per tile
+template <typename K, uint32_t SK, uint32_t SN, uint32_t NC>
+inline hipError_t launch_user_render(hip_context& ctx, K const& kernel, user_frames<NC>& f, hipStream_t stream)
+{
+    const size_t lds = size_t(64) * VRH_USER_STACK * sizeof(uint32_t);
+    auto fn = user_render<K, SK, SN, NC>;
+    check(vrh_ctx_user_queues(ctx.get(), &f.queues), "vrh_ctx_user_queues");
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, lds);
+    if (e != hipSuccess) return e;
+    const uint64_t work = uint64_t(f.tiles) * f.nframes;
+    const uint64_t resident = uint64_t(cus > 0 ? cus : 1) * uint64_t(per_cu > 0 ? per_cu : 1);
+    const uint32_t grid = uint32_t(work < resident ? work : resident);
+    if ((e = hipMemsetAsync(f.queues, 0, 8u * VRH_USER_QUEUE_STRIDE * sizeof(uint32_t), stream)) != hipSuccess) return e;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(8, 8), lds, stream, kernel, f);
+    return hipGetLastError();
 }
 } // hip_detail
 
@@ -841,7 +968,7 @@ struct user_kernels<K, typename std::enable_if<!std::is_same<K, hip_builtin_kern
         static_assert(PS::supported, "hip_sched: the pixel samplers are uniform_type, jittered_type, "
                                      "jittered_blend_type and ssaa_type<2 / 4 / 8>");
         auto& rt = sparams.rt;
-        user_frame f{};
+        user_frames<1> f{};
         if constexpr (has_camera_matrices<SP>::value)
         {
             // sched_params<Base, MT, RT, PxSamplerT> (scheduler.h:76-96): the host inverses of
@@ -857,19 +984,58 @@ struct user_kernels<K, typename std::enable_if<!std::is_same<K, hip_builtin_kern
             float center[3] = { cam.center().x, cam.center().y, cam.center().z };
             float up[3] = { cam.up().x, cam.up().y, cam.up().z };
             check(vrh_make_camera(eye, center, up, cam.fovy(), cam.aspect(), uint32_t(rt.width()), uint32_t(rt.height()),
-                                  &f.cam),
+                                  &f.cam[0]),
                   "vrh_make_camera");
         }
-        set_scissor(sparams, f.cam);
+        set_scissor(sparams, f.cam[0]);
+        if constexpr (has_sched_intersector<SP>::value)
+        {
+            using I = typename std::decay<decltype(sparams.intersector)>::type;
+            using C = call_with_intersector<K, I>;
+            run<C, PS::kind, PS::count>(ctx, C{ kernel, sparams.intersector }, f, rt, 1u, uint32_t(rt.height()), frame_num);
+        }
+        else
+            run<K, PS::kind, PS::count>(ctx, kernel, f, rt, 1u, uint32_t(rt.height()), frame_num);
+    }
+
+    // frames in flight: camera f into rows [f * H, (f + 1) * H) of rt (height = cams.size() * H),
+    // frame number frame_num + f; every frame equals its own frame() call
+    template <typename Camera, typename RT>
+    static void frames(hip_context& ctx, K const& kernel, std::vector<Camera> const& cams, RT& rt, unsigned frame_num)
+    {
+        if (cams.empty() || cams.size() > VRH_MAX_BATCH || rt.height() % cams.size() != 0)
+            throw std::runtime_error("hip_sched::frames: 1..VRH_MAX_BATCH cameras, render target height = frames x image height");
+        const uint32_t W = uint32_t(rt.width()), H = uint32_t(rt.height() / cams.size());
+        user_frames<VRH_MAX_BATCH> f{};
+        for (size_t c = 0; c < cams.size(); ++c)
+        {
+            auto const& cam = cams[c];
+            float eye[3] = { cam.eye().x, cam.eye().y, cam.eye().z };
+            float center[3] = { cam.center().x, cam.center().y, cam.center().z };
+            float up[3] = { cam.up().x, cam.up().y, cam.up().z };
+            check(vrh_make_camera(eye, center, up, cam.fovy(), cam.aspect(), W, H, &f.cam[c]), "vrh_make_camera");
+        }
+        run<K, VRH_SAMPLER_UNIFORM, 1>(ctx, kernel, f, rt, uint32_t(cams.size()), H, frame_num);
+    }
+
+private:
+    template <typename KK, uint32_t SK, uint32_t SN, uint32_t NC, typename RT>
+    static void run(hip_context& ctx, KK const& kk, user_frames<NC>& f, RT& rt, uint32_t nframes, uint32_t H,
+                    unsigned frame_num)
+    {
         f.width = uint32_t(rt.width());
-        f.height = uint32_t(rt.height());
+        f.height = H;
         f.frame_num = frame_num;
-        const uint32_t* sc = f.cam.scissor;
+        f.nframes = nframes;
+        const uint32_t* sc = f.cam[0].scissor;
         const bool whole = sc[0] == 0 && sc[1] == 0 && sc[2] == 0 && sc[3] == 0;
         f.x0 = whole ? 0u : sc[0];
         f.y0 = whole ? 0u : sc[1];
         f.x1 = whole ? f.width : (sc[2] < f.width ? sc[2] : f.width);
         f.y1 = whole ? f.height : (sc[3] < f.height ? sc[3] : f.height);
+        const bool any = f.x1 > f.x0 && f.y1 > f.y0;
+        f.tiles_x = any ? (f.x1 - f.x0 + 7u) / 8u : 0u;
+        f.tiles = any ? f.tiles_x * ((f.y1 - f.y0 + 7u) / 8u) : 0u;
         auto ref = rt.ref();
         f.color = reinterpret_cast<float4*>(ref.color);
         f.t = ref.t;
@@ -879,22 +1045,7 @@ struct user_kernels<K, typename std::enable_if<!std::is_same<K, hip_builtin_kern
         if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(dev) != hipSuccess) throw hip_error("hipSetDevice", VRH_ERR_HIP);
         rt.begin_frame();
         hipError_t e = hipSuccess;
-        if (f.x1 > f.x0 && f.y1 > f.y0)
-        {
-            const dim3 grid((f.width + 7u) / 8u, (f.height + 7u) / 8u);
-            const size_t lds = size_t(64) * VRH_USER_STACK * sizeof(uint32_t);
-            if constexpr (has_sched_intersector<SP>::value)
-            {
-                using I = typename std::decay<decltype(sparams.intersector)>::type;
-                using C = call_with_intersector<K, I>;
-                hipLaunchKernelGGL((user_render<C, PS::kind, PS::count>), grid, dim3(8, 8), lds,
-                                   static_cast<hipStream_t>(stream), C{ kernel, sparams.intersector }, f);
-            }
-            else
-                hipLaunchKernelGGL((user_render<K, PS::kind, PS::count>), grid, dim3(8, 8), lds,
-                                   static_cast<hipStream_t>(stream), kernel, f);
-            e = hipGetLastError();
-        }
+        if (any) e = launch_user_render<KK, SK, SN, NC>(ctx, kk, f, static_cast<hipStream_t>(stream));
         (void)hipSetDevice(prev);        // the caller's current device is left as it was
         if (e != hipSuccess) throw std::runtime_error(std::string("hip_sched::frame: user kernel launch: ") + hipGetErrorString(e));
         rt.end_frame();

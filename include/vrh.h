@@ -257,13 +257,8 @@ enum vrh_option {
                                     tile's AO reach (every hit position +- eps + radius), pushed
                                     so that the entry nearest the tile is popped first: 1 = on,
                                     2 = off, 3 = on with the entries in cut order (auto: on)      */
-    VRH_OPT_AO_STEAL = 21,       /* AO step loop: the tiles a wave takes when fewer than about one per
-                                    wave remain in its queue (the launch's last round) publish their
-                                    hits to a launch-wide stash instead of tracing their AO rays
-                                    alone, and every wave that runs out of tiles traces stash AO
-                                    rays, 64 at a time, so the launch's tail is shared by all waves:
-                                    1 = on, 2 = off, 4..4096: on with value / 16 tiles per wave
-                                    (and queue) counted as the last round (auto: on, 16 = 1 tile)   */
+    VRH_OPT_AO_STEAL = 21,       /* removed in round 3 (the AO tail stash measured slower, DESIGN.md
+                                    "Negative results"): 0 / 2 accepted, 1 -> VRH_ERR_UNSUPPORTED  */
     VRH_OPT_PAIR_LAYOUT = 15,    /* scene upload (read by vrh_scene_upload): 1 = node pairs in
                                     depth-first preorder, a pair's child-0 pair next to it in one
                                     128-B line; 2 = the builder's order (auto: 2; 1 measured
@@ -296,7 +291,11 @@ typedef struct {
     uint32_t prim_kind;       /* vrh_prim_kind                                                   */
     uint32_t finite_bounds;   /* every node bound finite (the hardware min/max slab test is exact) */
     uint32_t num_prims;       /* leaf-ordered primitive records                                  */
-    uint32_t reserved[3];
+    uint32_t quad_depth;      /* levels of the 4-wide records (0: none)                          */
+    uint32_t reserved[2];
+    const void* quads;        /* 4-wide any-hit records (128 B each, vrh_quad.cpp) of a single-BVH
+                                 scene with finite bounds, else NULL: any_hit of a user kernel
+                                 descends them (hip_kernels.h walk_quads)                          */
 } vrh_scene_view;
 VRH_API int vrh_scene_get_view(const vrh_scene* scene, uint32_t bvh, vrh_scene_view* out);
 
@@ -360,6 +359,12 @@ VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats);   /* syn
 /* VRH_OPT_WAVE_TIMES: (start, end) clock ticks of every wave of the last launch, 2 * count values
  * into out (capacity values at most); ticks_per_ms = the constant wall clock's rate; syncs */
 VRH_API int vrh_get_wave_times(vrh_ctx* ctx, uint64_t* out, uint64_t capacity, uint64_t* count, double* ticks_per_ms);
+
+/* Device memory of the context for the user-kernel launches of visionaray_hip/hip_kernels.h: eight
+ * tile-queue heads (one per XCD, 64 B apart: VRH_USER_QUEUE_STRIDE words) that the launch zeroes on
+ * the context's stream before it starts.  Valid until vrh_ctx_destroy. */
+#define VRH_USER_QUEUE_STRIDE 16u
+VRH_API int vrh_ctx_user_queues(vrh_ctx* ctx, uint32_t** queues);
 
 /* accumulation over every render since the last vrh_stats_reset (hipEvents per frame, kept in a
  * ring of VRH_MAX_TIMED_FRAMES; frames beyond that are counted in rays/hits but not timed) */

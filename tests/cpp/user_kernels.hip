@@ -15,7 +15,10 @@
 //   user_kernels list  <grid> <W> <H> <outdir> x0 y0 x1 y1 f    the AO kernel over a list of two BVHs
 //                                                               (prim_id parity split), scissor box,
 //                                                               frame f (the harness's "list" mode)
-//   user_kernels bench <grid> <W> <H> <outdir> [frames]         throughput of the AO user kernel
+//   user_kernels bench <grid> <W> <H> <outdir> [launches] [F]   throughput of the AO user kernel (F > 1:
+//                                                                F frames per hip_sched::frames launch)
+//   user_kernels frames <grid> <W> <H> <outdir> [frame]         frames in flight: three cameras in one
+//                                                                frames() launch equal three frame() calls
 //   user_kernels draws <grid> <W> <H> <outdir> <frame>          kernel(r, random_sampler<float>&): draws
 //                                                                0, 1, 2, 15 of the pixel's sampler as colour
 //   user_kernels rsao  <grid> <W> <H> <outdir> <frame>          the AO example's kernel (ao/main.cpp:183-246)
@@ -35,6 +38,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -337,19 +341,109 @@ int main(int argc, char** argv)
         }
         else if (mode == "bench")
         {
-            // user-kernel throughput: the AO lambda over `frames` frames (one synchronous frame()
-            // each, as cuda_sched is driven), median wall time per frame
-            const int frames = argc > 6 ? atoi(argv[6]) : 10;
+            // user-kernel throughput, median wall time per frame over `launches` synchronous launches:
+            //   F = 1: the AO lambda (hip_ao_sample, the built-in sample set), one frame() per frame as
+            //          cuda_sched is driven;
+            //   F > 1: the AO lambda drawing its directions from the per-pixel random_sampler (distinct
+            //          samples per frame number), F frames per frames() launch
+            const int launches = argc > 6 ? atoi(argv[6]) : 10;
+            const int F = argc > 7 ? atoi(argv[7]) : 1;
+            hip_bvh_ref const* begin = one.r;
+            hip_bvh_ref const* end = one.r + one.n;
+            auto rs_ao = [=] __device__ (ray r, random_sampler<float>& samp) -> result_record<float>
+            {
+                result_record<float> result;
+                result.color = vec4(0.1f, 0.2f, 0.3f, 1.0f);
+                auto hr = closest_hit(r, begin, end);
+                result.hit = hr.hit;
+                if (hr.hit)
+                {
+                    hr.isect_pos = r.ori + r.dir * hr.t;
+                    float clr = 1.0f;
+                    vec3 n = get_normal(dnormals, hr);
+                    vec3 u, v, w = n;
+                    make_orthonormal_basis(u, v, w);
+                    for (int i = 0; i < 8; ++i)
+                    {
+                        auto sp = cosine_sample_hemisphere(samp.next(), samp.next());
+                        auto dir = normalize(sp.x * u + sp.y * v + sp.z * w);
+                        ray ao(hr.isect_pos + dir * 1E-3f, dir);
+                        if (any_hit(ao, begin, end, 0.1f).hit) clr = clr - 1.0f / 8;
+                    }
+                    result.color = vec4(clr, clr, clr, 1.0f);
+                }
+                return result;
+            };
+            hip_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> rtF;
+            rtF.resize(W, H * unsigned(F));
+            std::vector<camera> cams(size_t(F), cam);
             std::vector<double> ms;
-            for (int f = 0; f <= frames; ++f)
+            for (int l = 0; l <= launches; ++l)
             {
                 auto t0 = std::chrono::steady_clock::now();
-                sched.frame(ao_kernel(one, dnormals, default_intersector{}, W, unsigned(f)), sparams, unsigned(f));
+                if (F == 1) sched.frame(ao_kernel(one, dnormals, default_intersector{}, W, unsigned(l)), sparams, unsigned(l));
+                else sched.frames(rs_ao, cams, rtF, unsigned(l * F));
                 auto t1 = std::chrono::steady_clock::now();
-                if (f > 0) ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+                if (l > 0) ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count() / F);
             }
             std::sort(ms.begin(), ms.end());
-            printf("{\"mode\":\"bench\",\"frame_ms_median\":%.4f,\"frames\":%d}\n", ms[ms.size() / 2], frames);
+            printf("{\"mode\":\"bench\",\"frame_ms_median\":%.4f,\"launches\":%d,\"frames_per_launch\":%d,"
+                   "\"kernel\":\"%s\"}\n", ms[ms.size() / 2], launches, F, F == 1 ? "ao lambda" : "random_sampler ao lambda");
+        }
+        else if (mode == "frames")
+        {
+            // frames in flight with a user kernel: three cameras (the eye raised twice) in one frames()
+            // launch equal their own frame() calls with frame numbers frame_num + f
+            const unsigned frame_num = argc > 6 ? unsigned(strtoul(argv[6], nullptr, 10)) : 5u;
+            hip_bvh_ref const* begin = one.r;
+            hip_bvh_ref const* end = one.r + one.n;
+            auto k = [=] __device__ (ray r, random_sampler<float>& samp) -> result_record<float>
+            {
+                result_record<float> result;
+                result.color = vec4(0.1f, 0.2f, 0.3f, 1.0f);
+                auto hr = closest_hit(r, begin, end);
+                result.hit = hr.hit;
+                if (hr.hit)
+                {
+                    result.depth = hr.t;
+                    hr.isect_pos = r.ori + r.dir * hr.t;
+                    float clr = 1.0f;
+                    vec3 n = get_normal(dnormals, hr);
+                    vec3 u, v, w = n;
+                    make_orthonormal_basis(u, v, w);
+                    for (int i = 0; i < 8; ++i)
+                    {
+                        auto sp = cosine_sample_hemisphere(samp.next(), samp.next());
+                        auto dir = normalize(sp.x * u + sp.y * v + sp.z * w);
+                        ray ao(hr.isect_pos + dir * 1E-3f, dir);
+                        if (any_hit(ao, begin, end, 0.1f).hit) clr = clr - 1.0f / 8;
+                    }
+                    result.color = vec4(clr, clr, float(hr.prim_id), 1.0f);
+                }
+                return result;
+            };
+            std::vector<camera> cams(3, cam);
+            cams[1].look_at(vec3(0.0f, 1.0f, 1.4f), vec3(0.0f), vec3(0.0f, 1.0f, 0.0f));
+            cams[2].look_at(vec3(0.0f, 1.1f, 1.4f), vec3(0.0f), vec3(0.0f, 1.0f, 0.0f));
+            hip_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> rt3;
+            rt3.resize(W, 3 * H);
+            sched.frames(k, cams, rt3, frame_num);
+            const size_t n = size_t(W) * H;
+            std::vector<float> c3(12 * n), t3(3 * n), c1(4 * n), t1(n);
+            rt3.download(c3.data(), nullptr, t3.data());
+            bool ok = true, distinct = false;
+            for (size_t f = 0; f < 3; ++f)
+            {
+                auto sp = make_sched_params(pixel_sampler::uniform_type{}, cams[f], rt);
+                sched.frame(k, sp, frame_num + unsigned(f));
+                rt.download(c1.data(), nullptr, t1.data());
+                ok = ok && std::memcmp(c1.data(), c3.data() + 4 * f * n, 16 * n) == 0
+                        && std::memcmp(t1.data(), t3.data() + f * n, 4 * n) == 0;
+                if (f > 0) distinct = distinct || std::memcmp(c3.data(), c3.data() + 4 * f * n, 16 * n) != 0;
+            }
+            printf("{\"mode\":\"frames\",\"frames_ok\":%s,\"distinct\":%s}\n", ok ? "true" : "false",
+                   distinct ? "true" : "false");
+            return ok && distinct ? 0 : 1;
         }
         else if (mode == "mask")
         {

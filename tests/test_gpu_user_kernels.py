@@ -141,6 +141,18 @@ def test_user_kernel_over_bvh_list_with_scissor_matches_reference(tmp_path, gold
                                        ("color", "color_hash")])
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene,W,H", [("hf64", 160, 90), ("hf200", 333, 181)])
+def test_user_kernel_frames_in_flight_equal_single_frames(tmp_path, scene, W, H):
+    """hip_sched::frames with a user kernel (one persistent launch, three cameras, frame numbers
+    f0 .. f0 + 2) equals three frame() calls bit for bit, and the frames differ (ragged width and
+    height: partial tiles at the right and bottom edges)."""
+    r = subprocess.run([BIN, "frames", str(GRID[scene]), str(W), str(H), str(tmp_path), "7"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert '"frames_ok":true' in r.stdout and '"distinct":true' in r.stdout
+
+
 def test_user_kernel_header_needs_hipcc(tmp_path):
     """hip_kernels.h is device code: a host compiler gets a clear error, not a silent host path."""
     src = tmp_path / "host.cpp"

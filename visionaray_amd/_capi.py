@@ -94,7 +94,8 @@ class vrh_frame_stats(C.Structure):
 class vrh_scene_view(C.Structure):
     _fields_ = [("pairs", C.c_void_p), ("prims", C.c_void_p), ("normals", C.c_void_p), ("root", C.c_uint32),
                 ("max_depth", C.c_uint32), ("prim_kind", C.c_uint32), ("finite_bounds", C.c_uint32),
-                ("num_prims", C.c_uint32), ("reserved", C.c_uint32 * 3)]
+                ("num_prims", C.c_uint32), ("quad_depth", C.c_uint32), ("reserved", C.c_uint32 * 2),
+                ("quads", C.c_void_p)]
 
 
 class vrh_scene_info(C.Structure):
@@ -149,6 +150,7 @@ SIGNATURES = {
     "vrh_scene_get_info": (C.c_int, [_vp, C.POINTER(vrh_scene_info)]),
     "vrh_scene_get_view": (C.c_int, [_vp, C.c_uint32, C.POINTER(vrh_scene_view)]),
     "vrh_get_wave_times": (C.c_int, [_vp, _vp, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
+    "vrh_ctx_user_queues": (C.c_int, [_vp, C.POINTER(_vp)]),
     "vrh_scene_list_create": (C.c_int, [_vp, C.POINTER(_vp), _u32, _vp, _u32, C.POINTER(_vp)]),
     "vrh_scene_free": (C.c_int, [_vp]),
     "vrh_scene_set_vertex_normals": (C.c_int, [_vp, _vp, _u32]),
@@ -224,6 +226,8 @@ def lib():
             raise ImportError(f"{LIB_PATH} not built: run `make -C {_HERE}` (or __graft_entry__.build())")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("VRH_LIB") and not hasattr(L, name):
+                continue            # an older library under A/B (tools/ab_variants.py): what it has
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

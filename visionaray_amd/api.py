@@ -162,7 +162,7 @@ class Context:
                  "wide_anyhit": capi.VRH_OPT_WIDE_ANYHIT,
                  "descent_cap": capi.VRH_OPT_DESCENT_CAP, "pop_on_miss": capi.VRH_OPT_POP_ON_MISS,
                  "coop_fetch": capi.VRH_OPT_COOP_FETCH, "scalar_fetch": capi.VRH_OPT_SCALAR_FETCH,
-                 "pair_layout": capi.VRH_OPT_PAIR_LAYOUT, "ao_gate": capi.VRH_OPT_AO_GATE, "ao_cut": capi.VRH_OPT_AO_CUT, "ao_steal": capi.VRH_OPT_AO_STEAL, "wave_times": capi.VRH_OPT_WAVE_TIMES}
+                 "pair_layout": capi.VRH_OPT_PAIR_LAYOUT, "ao_gate": capi.VRH_OPT_AO_GATE, "ao_cut": capi.VRH_OPT_AO_CUT, "wave_times": capi.VRH_OPT_WAVE_TIMES}
         capi.check("vrh_ctx_set_option", self.handle, names.get(option, option), int(value))
 
     def last_frame_stats(self):
@@ -182,21 +182,6 @@ class Context:
         capi.check("vrh_get_wave_times", self.handle, buf.ctypes.data_as(C.c_void_p), buf.size, C.byref(n), None)
         t = buf.reshape(-1, 2).astype(np.float64)
         return (t - t[:, 0].min()) / rate.value
-
-    def steal_diag(self):
-        """VRH_OPT_WAVE_TIMES = 2: per wave (start, end) in ms and the 8 AO-stash diagnostic words
-        (vrh_kernels.hip STEAL_DBG; clock words in ms from the launch's first start)."""
-        import numpy as np
-        n, rate = C.c_uint64(), C.c_double()
-        capi.check("vrh_get_wave_times", self.handle, None, 0, C.byref(n), C.byref(rate))
-        buf = np.zeros(10 * n.value, np.uint64)
-        capi.check("vrh_get_wave_times", self.handle, buf.ctypes.data_as(C.c_void_p), buf.size, C.byref(n), None)
-        t = buf[:2 * n.value].reshape(-1, 2).astype(np.float64)
-        d = buf[2 * n.value:].reshape(-1, 8).astype(np.float64)
-        t0 = t[:, 0].min()
-        for k in (3, 4, 5, 7):
-            d[:, k] = np.where(d[:, k] > 0, (d[:, k] - t0) / rate.value, np.nan)
-        return (t - t0) / rate.value, d
 
     def stats_reset(self):
         capi.check("vrh_stats_reset", self.handle)

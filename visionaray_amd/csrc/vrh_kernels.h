@@ -87,22 +87,11 @@ struct render_params
     uint32_t* mh_prim_id;     // [pixel][N] hit lists (render target side buffers)
     float* mh_t;
     dev::hit_mask_params hmask;   // mask intersector (vrh_hit_mask), hmask.mask == null: none
-    // AO tail stealing (VRH_OPT_AO_STEAL): a tile handed out while fewer than steal_rem tiles remain in
-    // its queue publishes its hit records (pos, prim id, output pixel, sampler pixel, frame) to the
-    // stash once its primaries are done; waves without tiles claim stash records and trace their AO
-    // rays; the last sample of a record writes its pixel (state: occlusion mask | finished samples << 32).
-    // A record is valid when ready[r] == steal_epoch (flags of earlier launches hold older epochs).
-    uint32_t ao_steal, steal_rem, steal_epoch, steal_cap;
-    float4* steal_rec;                 // 2 float4 per record
-    unsigned long long* steal_state;   // per record
-    uint32_t* steal_ready;             // per record
-    unsigned long long* steal_dbg;     // VRH_OPT_WAVE_TIMES = 2: 8 diagnostic words per wave, else null
 };
 
 constexpr int COUNTERS_FRAME = 208;     // u64 words reset before every frame
 constexpr int COUNTERS_LINES = 80;      // [80] L1 128-B lines, [81] wave-level vector-memory instructions, [82] 16-B requests (counting variant)
 constexpr int COUNTERS_TOTAL = 208;     // u64 words [208], [209]: totals
-constexpr int COUNTERS_STEAL = 96;      // [96] stash records reserved, [104] claimed, [112] producers not yet published (one 64-B line each)
 constexpr int COUNTERS_WORDS = 256;
 
 struct launch_config

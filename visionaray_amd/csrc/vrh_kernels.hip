@@ -202,7 +202,6 @@ struct tile_queue
 {
     uint32_t q;       // range currently drained (wave-uniform)
     uint32_t tried;   // ranges found empty so far
-    uint32_t rem;     // tiles left in queue q after the one next_tile returned (AO tail stealing)
 };
 
 __device__ __forceinline__ uint32_t xcc_id()
@@ -214,7 +213,7 @@ __device__ __forceinline__ uint32_t xcc_id()
 
 __device__ __forceinline__ tile_queue queue_init(const render_params& P)
 {
-    return tile_queue{ P.xcd_queues ? xcc_id() : 0u, 0u, 0u };
+    return tile_queue{ P.xcd_queues ? xcc_id() : 0u, 0u };
 }
 
 // first tile of strip q of a frame (num_tiles * q / nq)
@@ -246,8 +245,6 @@ __device__ __forceinline__ uint32_t next_tile(const render_params& P, tile_queue
             {
                 const uint32_t band = u / P.num_frames;
                 const uint32_t f = u - band * P.num_frames;
-                const uint32_t units_q = (units - tq.q + 7u) / 8u;          // units of queue q
-                tq.rem = (units_q - 1u - k) * tx + (tx - 1u - (t - k * tx));
                 return (f << TILE_FRAME_SHIFT) | (band * tx + (t - k * tx));
             }
             tq.q = (tq.q + 1u) & 7u;
@@ -265,7 +262,6 @@ __device__ __forceinline__ uint32_t next_tile(const render_params& P, tile_queue
         if (t < len * P.num_frames)
         {
             const uint32_t f = t / len;
-            tq.rem = len * P.num_frames - 1u - t;
             return (f << TILE_FRAME_SHIFT) | (lo + t - f * len);
         }
         tq.q = (tq.q + 1u) % nq;
@@ -475,152 +471,6 @@ __device__ __forceinline__ int list_next(const render_params& P, bool any, uint3
     }
     best_t = res_t; best_prim = res_prim;
     return -1;
-}
-
-// AO tail stealing (render_params::ao_steal, VRH_OPT_AO_STEAL).  A one-frame launch ends with a
-// ragged tail: the tile a wave takes last commits it to that tile's 64 primaries and up to 64 x 8 AO
-// rays, while waves whose last tile was sky are already done (round 2's launch timeline: the tile pool
-// drains at 1.28 ms, the waves end between 1.28 and 1.70 ms).  So a tile taken in the launch's last
-// round (fewer than steal_rem tiles left in its queue) does not trace its AO rays alone: once its
-// primaries are done it publishes its hit records to a launch-wide stash, and every wave that has run
-// out of tiles claims stash records, 64 / S at a time, and traces their AO rays with the same step
-// loop, entry cut included.  The sample that completes a record writes its pixel (colour and mask as
-// the local path writes them).  Results are unchanged: the same rays, only traced by other waves.
-//
-// Memory protocol.  The 8 XCDs have their own L2s, so agent-scope acquire / release would write back
-// or invalidate a whole L2 (buffer_wbl2 / buffer_inv sc1: measured 1,000x slower launches).  The stash
-// lives in uncached device memory (hipDeviceMallocUncached) and the counters are read with atomic
-// RMWs, so every access is served at the coherence point, never from a stale L2 line.  Slots are reserved with an atomic add on counters[COUNTERS_STEAL]
-// (reservations beyond steal_cap hold no record: a tile that does not fit keeps those AO rays), the
-// records written, and -- after s_waitcnt vmcnt(0), so the record stores are complete -- published per
-// record by storing ready[r] = steal_epoch; claims CAS counters[COUNTERS_STEAL + 8] up to the reserved
-// count and poll each ready flag before reading the record.  counters[COUNTERS_STEAL +
-// 16] counts the waves holding a last-round tile that has not published yet; a wave without tiles
-// stops claiming once that count is 0 and every reserved record is claimed.  Waves never wait for
-// waves that are not resident: a wave that publishes claims its own records after its tiles too, so
-// every record is traced even if the other waves have left.  Every wait is bounded.
-constexpr uint32_t STEAL_SPIN_LIMIT = 1u << 22;
-// AO stash diagnostics (VRH_OPT_WAVE_TIMES = 2): per wave [0] claims, [1] traversal steps, [2]
-// publishes, [3] clock when the tile queues ran dry, [4] clock when the stash was seen finished,
-// [5] clock of the last claim, [6] records published, [7] clock of the first claim
-#define STEAL_DBG(k, op) do { if (P.steal_dbg && lane == 0u) { unsigned long long* d_ = P.steal_dbg + size_t(8) * (size_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) + (k); op; } } while (0)
-#ifndef VRH_STEAL_PARTS
-#define VRH_STEAL_PARTS 15
-#endif
-
-template <typename T>
-__device__ __forceinline__ T coh_ld(const T* p)
-{
-    return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename T>
-__device__ __forceinline__ void coh_st(T* p, T v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// word k (0..7) of stash record i
-__device__ __forceinline__ uint32_t rec_word(const float4* srec, size_t i, uint32_t k)
-{
-    return coh_ld(reinterpret_cast<const uint32_t*>(srec) + 8u * i + k);
-}
-__device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// a counter of ctx->counters (cached device memory) read at the coherence point: an atomic RMW
-// (a plain or sc1 load may hit a stale copy in this XCD's L2)
-__device__ __forceinline__ unsigned long long coh_rd(unsigned long long* p)
-{
-    return __hip_atomic_fetch_or(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// publish hit slots [0, n) of tile `tile` (records in LDS `recs`, slot -> pixel lane `spx`, slot ->
-// output pixel `sout`); whole wave.  A record is (pos, prim id) (output pixel, tile, pixel lane, 0):
-// the claimer re-derives the sampler pixel and frame with tile_pixel, as for its own tiles.  Returns
-// the number of slots published -- the LAST ones, [n - m, n): a stash with room for fewer than n
-// records takes what fits and the tile traces the rest itself.  Not inlined (as steal_claim): both
-// run once per tile, and inlined they cost the step loop registers.
-__device__ __noinline__ uint32_t steal_publish(unsigned long long* ctr, uint32_t cap, float4* srec,
-                                               unsigned long long* sstate, uint32_t* sready, uint32_t epoch,
-                                               const float* recs, const uint8_t* spx, const uint32_t* sout,
-                                               uint32_t tile, uint32_t n, uint32_t lane)
-{
-    uint32_t base = 0;
-    if (lane == 0u) base = (uint32_t)__hip_atomic_fetch_add(ctr, (unsigned long long)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    base = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)base, 0));
-    const uint32_t m = base >= cap ? 0u : min(n, cap - base);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane < m)
-    {
-        const uint32_t slot = n - m + lane;
-        const float* r = recs + slot * AO_REC_WORDS;
-        const size_t i = size_t(base) + lane;
-        uint32_t* w = reinterpret_cast<uint32_t*>(srec) + 8u * i;
-        coh_st(w + 0, __float_as_uint(r[0])); coh_st(w + 1, __float_as_uint(r[1]));
-        coh_st(w + 2, __float_as_uint(r[2])); coh_st(w + 3, __float_as_uint(r[3]));
-        coh_st(w + 4, sout[slot]); coh_st(w + 5, tile); coh_st(w + 6, (uint32_t)spx[slot]);
-        coh_st(sstate + i, 0ull);
-        wait_stores();                                   // the record is complete before its flag
-        coh_st(sready + i, epoch);
-    }
-    return m;
-}
-
-// claim up to k stash records and copy their (pos, prim id) into LDS `recs` (whole wave): returns
-// got | fin << 16 | base << 17 ... as two values: (got, fin) in the low word (got in bits 0-15, fin in
-// bit 16) and the first record in the high word.  got > 0: records [base, base + got), whose ready
-// flags it waits for (acquire); got = 0: none available now; fin = 1: none will ever be (no active
-// producer and every reserved record -- up to the stash's capacity -- is claimed)
-__device__ __noinline__ unsigned long long steal_claim(unsigned long long* ctr, uint32_t cap, uint32_t k,
-                                                       const uint32_t* sready, uint32_t epoch, const float4* srec,
-                                                       float* recs, uint32_t lane)
-{
-    uint32_t got = 0, b = 0;
-    int done = 0;
-    if (lane == 0u)
-    {
-        unsigned long long c = coh_rd(ctr + 8);
-        for (;;)
-        {
-            // no active producer => every reservation made so far is in `reserved` (a producer's
-            // reservation returned before it left the active count; the two loads complete in order)
-            const bool all = coh_rd(ctr + 16) == 0ull;
-            unsigned long long r = coh_rd(ctr);
-            r = r < cap ? r : cap;                         // reservations beyond the stash hold no record
-            if (c >= r)
-            {
-                done = all ? 1 : 0;
-                break;
-            }
-            const unsigned long long n = r - c < k ? r - c : k;
-            if (__hip_atomic_compare_exchange_strong(ctr + 8, &c, c + n, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT))
-            {
-                got = (uint32_t)n;
-                b = (uint32_t)c;
-                break;
-            }
-        }
-    }
-    got = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)got, 0));
-    b = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)b, 0));
-    done = __builtin_amdgcn_readfirstlane(__shfl(done, 0));
-    if (got)
-    {
-        // the records' ready flags (their producers set them right after reserving)
-        uint32_t spin = 0;
-        bool ok = true;
-        if (lane < got)
-            while (coh_ld(sready + b + lane) != epoch)
-            {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spin > STEAL_SPIN_LIMIT) { ok = false; break; }
-            }
-        if (lane < got)
-        {
-            float* rc4 = recs + lane * AO_REC_WORDS;
-            for (uint32_t k = 0; k < 4u; ++k) rc4[k] = __uint_as_float(rec_word(srec, size_t(b) + lane, k));
-        }
-        if (__ballot(!ok)) done |= 2;                      // a wait ran out: error flag
-    }
-    return (unsigned long long)got | ((unsigned long long)done << 16) | ((unsigned long long)b << 32);
 }
 
 // One refilling loop per wave.  Primary rays (one per pixel of the wave's tile)
@@ -860,26 +710,12 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         uint32_t cutN = NONE;                                 // entries of tile C's cut (NONE: root)
         const float4 bg = make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
         tile_queue tq = queue_init(P);
-        // AO tail stealing: instances without lists, test counts or pixel samplers
-        constexpr bool STEAL = !LIST && !COUNT && !SAMPLED && EPI == 0;
         // wave-uniform tile state
         uint32_t tileC = next_tile(P, tq, lane), parC = 0;
-        bool finalC = STEAL && P.ao_steal && tileC != NONE && tq.rem < P.steal_rem;   // tile C publishes its hits
-        unsigned long long* steal_active = P.counters + COUNTERS_STEAL + 16;           // producers not yet published
-        if (finalC && lane == 0u) __hip_atomic_fetch_add(steal_active, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t handedC = 0, pendC = 0, pubC = 0, issC = 0;  // primaries handed / in flight, slots, AO rays handed
         uint32_t tileD = NONE, parD = 0, slotsD = 0;
         uint32_t inflight0 = 0, inflight1 = 0;                // AO rays in flight per buffer parity
-        // AO tail stealing: once the tile queues are empty, tile C may be a claim of stash records
-        // (STASH): its AO rays are handed out like a tile's, their results go to the records' states
-        constexpr uint32_t STASH = 0xFFFFFFFEu;
-        constexpr uint32_t STASH_BIT = 1u << 12;
-        uint32_t sbase0 = 0, sbase1 = 0;                      // stash record of slot 0 of a STASH tile, per parity
-        bool stash_fin = !(STEAL && P.ao_steal);              // no stash records will come any more
-        uint32_t backoff = 0, waits = 0;
-        const uint32_t claim_k = S >= 64u ? 1u : 64u / S;     // records per claim: 64 rays
         // lane state: PRIMARY tag = pixel lane k of tile C; AORAY tag = slot | s << 6 | parity << 11
-        // (| STASH_BIT for a ray of a stash record)
         uint32_t tag = 0;
         for (;;)
         {
@@ -909,62 +745,11 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             // 2. the current tile has handed out all its rays: it drains, the next tile starts
             if (tileC != NONE && tileD == NONE && handedC >= 64u && pendC == 0u && issC >= pubC * S)
             {
-                tileD = tileC; parD = parC; slotsD = tileC == STASH ? 0u : pubC;   // stash pixels: written per record
-                if (finalC && lane == 0u)        // a last-round tile without hits published nothing
-                    __hip_atomic_fetch_add(steal_active, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                tileD = tileC; parD = parC; slotsD = pubC;
                 tileC = next_tile(P, tq, lane);
-                if (tileC == NONE) STEAL_DBG(3, if (*d_ == 0ull) *d_ = wall_clock64());
-                finalC = STEAL && P.ao_steal && tileC != NONE && tq.rem < P.steal_rem;
-                if (finalC && lane == 0u) __hip_atomic_fetch_add(steal_active, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 parC ^= 1u;
                 handedC = 0; pendC = 0; pubC = 0; issC = 0;
             }
-            // 2b. a last-round tile whose primaries are done publishes its hits to the stash (its
-            //     AO rays are then traced by whichever waves run out of tiles first)
-            if constexpr (STEAL && (VRH_STEAL_PARTS & 1))
-                if (finalC && pubC > 0u && issC == 0u && pendC == 0u && handedC >= 64u)
-                {
-                    const uint32_t m = steal_publish(P.counters + COUNTERS_STEAL, P.steal_cap, P.steal_rec, P.steal_state,
-                                                     P.steal_ready, P.steal_epoch, recs, slot_px + parC * 64u,
-                                                     masks + parC * 64u, tileC, pubC, lane);
-                    pubC -= m;
-                    if (lane < pubC) masks[parC * 64u + lane] = 0u;          // slots the stash had no room for
-                    STEAL_DBG(2, *d_ += 1ull);
-                    STEAL_DBG(6, *d_ += m);
-                    finalC = false;
-                    // published (its reservation and ready flags ordered before by the release)
-                    if (lane == 0u) __hip_atomic_fetch_add(steal_active, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            // 2c. no tile left: claim stash records as the next tile C (polling every few steps)
-            if constexpr (STEAL && (VRH_STEAL_PARTS & 2))
-                if (tileC == NONE && !stash_fin)
-                {
-                    if (backoff) backoff -= 1u;
-                    else
-                    {
-                        const unsigned long long cl = steal_claim(P.counters + COUNTERS_STEAL, P.steal_cap, claim_k, P.steal_ready,
-                                                                  P.steal_epoch, P.steal_rec, recs, lane);
-                        const uint32_t got = (uint32_t)cl & 0xFFFFu, fl = ((uint32_t)cl >> 16) & 3u;
-                        const uint32_t b = (uint32_t)(cl >> 32);
-                        stash_fin = (fl & 1u) != 0u;
-                        if (fl & 2u) cnt.aborted = true;
-                        if (stash_fin) STEAL_DBG(4, *d_ = wall_clock64());
-                        if (got) STEAL_DBG(7, if (*d_ == 0ull) *d_ = wall_clock64());
-                        if (got)
-                        {
-                            STEAL_DBG(0, *d_ += 1ull);
-                            STEAL_DBG(5, *d_ = wall_clock64());
-                            __builtin_amdgcn_wave_barrier();
-                            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                            tileC = STASH;
-                            if (parC) sbase1 = b; else sbase0 = b;
-                            handedC = 64u; pendC = 0u; pubC = got; issC = 0u;
-                            backoff = 0u;
-                        }
-                        else
-                            backoff = 8u;
-                    }
-                }
             // 3. hand out rays to idle lanes: the current tile's AO rays, then its primaries --
             //    once P.refill_min lanes are idle (or none is busy), so ray generation runs with
             //    many lanes at once
@@ -992,17 +777,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 if (mode == IDLE && cand < avail)
                 {
                     const uint32_t slot = cand / S, smp = cand - slot * S;
-                    uint32_t rtile = tileC, rk = slot_px[parC * 64u + slot];
-                    const bool stashed = STEAL && (VRH_STEAL_PARTS & 4) && tileC == STASH;
-                    if (stashed)
-                    {
-                        // a stash record's tile and pixel lane (steal_publish)
-                        const size_t ri = size_t(parC ? sbase1 : sbase0) + slot;
-                        rtile = rec_word(P.steal_rec, ri, 5u);
-                        rk = rec_word(P.steal_rec, ri, 6u);
-                    }
                     uint32_t x, y, orow, fr;
-                    tile_pixel(P, rtile, rk, x, y, orow, fr);
+                    tile_pixel(P, tileC, slot_px[parC * 64u + slot], x, y, orow, fr);
                     r = ao_ray<COUNT>(P, recs, slot, smp, y * P.width + x, fr, cnt);
                     best_t = FMAX; best_prim = 0; steps = 0; max_t = P.radius; any = true;
                     bk = 0; res_t = FMAX; res_prim = 0;
@@ -1031,7 +807,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     else
                         st.push(quad ? 0u : P.root);
                     mode = AORAY;
-                    tag = slot | (smp << 6) | (parC << 11) | (stashed ? STASH_BIT : 0u);
+                    tag = slot | (smp << 6) | (parC << 11);
                     rays_total += 1;
                 }
                 issC += n;
@@ -1061,17 +837,10 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             const bool busy = mode != IDLE;
             if (__ballot(busy) == 0ull)
             {
-                if (tileC == NONE && tileD == NONE)
-                {
-                    if (stash_fin) break;
-                    // nothing to trace until a stash record comes: other waves are still producing
-                    __builtin_amdgcn_s_sleep(4);
-                    if (++waits > STEAL_SPIN_LIMIT) { cnt.aborted = true; break; }
-                }
+                if (tileC == NONE && tileD == NONE) break;
                 continue;
             }
             // 4. one traversal step for every busy lane (same code for both ray kinds)
-            STEAL_DBG(1, *d_ += 1ull);
             int rc = 0;
             if (busy)
             {
@@ -1084,31 +853,9 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             if (COUNT) count_wave(cnt, busy);
             // 5. finished AO rays: record occlusion, retire from their tile's in-flight count
             const bool ao_done = mode == AORAY && rc != 0;
-            const uint32_t tpar = (tag >> 11) & 1u;
-            if (ao_done && rc > 0 && !(tag & STASH_BIT)) atomicOr(&masks[tpar * 64u + (tag & 63u)], 1u << ((tag >> 6) & 31u));
-            if constexpr (STEAL && (VRH_STEAL_PARTS & 8))
-                if (ao_done && (tag & STASH_BIT))
-                {
-                    // a stash record's state: occlusion bits | finished samples << 32; its last sample
-                    // writes the pixel (ao/main.cpp:234-242, as step 1 does for a tile's slots)
-                    const size_t rec = size_t(tpar ? sbase1 : sbase0) + (tag & 63u);
-                    const unsigned long long add = (1ull << 32) | (rc > 0 ? (1ull << ((tag >> 6) & 31u)) : 0ull);
-                    const unsigned long long old = __hip_atomic_fetch_add(P.steal_state + rec, add, __ATOMIC_RELAXED,
-                                                                          __HIP_MEMORY_SCOPE_AGENT);
-                    if ((uint32_t)(old >> 32) == S - 1u)
-                    {
-                        const uint32_t m = (uint32_t)(old + add);
-                        const uint32_t o = rec_word(P.steal_rec, rec, 4u);
-                        float clr = 1.0f;
-                        const float stp = 1.0f / (float)S;
-                        for (uint32_t s2 = 0; s2 < S; ++s2)
-                            if ((m >> s2) & 1u) clr = clr - stp;
-                        if (P.color) put_color<SAMPLED>(P, o, make_float4(clr, clr, clr, 1.0f));
-                        if (P.occ) P.occ[o] = (uint8_t)m;
-                    }
-                }
-            inflight0 -= (uint32_t)__popcll(__ballot(ao_done && tpar == 0u));
-            inflight1 -= (uint32_t)__popcll(__ballot(ao_done && tpar != 0u));
+            if (ao_done && rc > 0) atomicOr(&masks[(tag >> 11) * 64u + (tag & 63u)], 1u << ((tag >> 6) & 31u));
+            inflight0 -= (uint32_t)__popcll(__ballot(ao_done && (tag >> 11) == 0u));
+            inflight1 -= (uint32_t)__popcll(__ballot(ao_done && (tag >> 11) != 0u));
             // 6. finished primaries: write prim id / t (and a miss's colour), publish hits as slots
             const bool pr_done = mode == PRIMARY && rc != 0;
             const uint64_t fin = __ballot(pr_done);
@@ -1131,9 +878,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                         float* rec = recs + slot * AO_REC_WORDS;
                         rec[0] = pos.x; rec[1] = pos.y; rec[2] = pos.z;
                         rec[3] = __uint_as_float(best_prim);
-                        // a last-round tile keeps the output pixel in the (then unused) mask word
-                        // until it publishes (2b); a tile that traces its own AO rays starts at 0
-                        masks[parC * 64u + slot] = (STEAL && finalC) ? (uint32_t)o : 0u;
+                        masks[parC * 64u + slot] = 0u;
                         slot_px[parC * 64u + slot] = (uint8_t)tag;
                     }
                     else
@@ -1151,7 +896,6 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             }
             if (rc != 0) mode = IDLE;
         }
-
     }
 
     if (P.wave_times && lane == 0)

@@ -18,13 +18,11 @@ struct vrh_ctx
     hipEvent_t group_written = nullptr;   // the last render-group unshard into one of this context's targets
     // device counters (u64), see render_params::counters; [0..7] reset per frame
     unsigned long long* counters = nullptr;
+    uint32_t* user_queues = nullptr;            // vrh_ctx_user_queues (8 heads x 64 B)
     unsigned long long* wave_times = nullptr;   // VRH_OPT_WAVE_TIMES buffer (2 per resident wave)
     size_t wave_times_n = 0, wave_times_used = 0;
     void* spill = nullptr;          // traversal stack overflow blocks (vrh_render_batch), grown on demand
     size_t spill_bytes = 0;
-    void* steal = nullptr;          // AO tail stash (records, states, ready flags), grown on demand
-    size_t steal_records = 0;
-    uint32_t steal_epoch = 0;       // ready-flag value of the last launch (flags of older launches differ)
     // one hipEvent pair per frame since vrh_stats_reset (ring of VRH_MAX_TIMED_FRAMES)
     std::vector<hipEvent_t> ev_start, ev_stop;
     uint32_t frames = 0;
@@ -32,7 +30,7 @@ struct vrh_ctx
     vrh_frame_stats last{};
     bool have_frame = false;
     // tuning options (0 = automatic), vrh_ctx_set_option
-    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_dcap = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0, opt_pop = 0, opt_scalar = 0, opt_layout = 0, opt_gate = 0, opt_wave_times = 0, opt_cut = 0, opt_steal = 0;
+    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_dcap = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0, opt_pop = 0, opt_scalar = 0, opt_layout = 0, opt_gate = 0, opt_wave_times = 0, opt_cut = 0;
 };
 
 struct vrh_scene

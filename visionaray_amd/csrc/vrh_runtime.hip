@@ -113,8 +113,8 @@ VRH_API int vrh_ctx_destroy(vrh_ctx* ctx)
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->counters) (void)hipFree(ctx->counters);
     if (ctx->wave_times) (void)hipFree(ctx->wave_times);
+    if (ctx->user_queues) (void)hipFree(ctx->user_queues);
     if (ctx->spill) (void)hipFree(ctx->spill);
-    if (ctx->steal) (void)hipFree(ctx->steal);
     for (auto e : ctx->ev_start) (void)hipEventDestroy(e);
     for (auto e : ctx->ev_stop) (void)hipEventDestroy(e);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -143,9 +143,9 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
         VRH_CHECK(value == 0 || value == 2, "vrh_ctx_set_option: cooperative fetch was removed (2 = off is accepted)");
         if (value == 1) return VRH_ERR_UNSUPPORTED;
         break;
-    case VRH_OPT_WAVE_TIMES: VRH_CHECK(value <= 2, "vrh_ctx_set_option: wave times is 1 (on), 2 (on + AO stash diagnostics) or 0 (off)"); ctx->opt_wave_times = int(value); break;
+    case VRH_OPT_WAVE_TIMES: VRH_CHECK(value <= 1, "vrh_ctx_set_option: wave times is 1 (on) or 0 (off)"); ctx->opt_wave_times = int(value); break;
     case VRH_OPT_AO_CUT: VRH_CHECK(value <= 3, "vrh_ctx_set_option: AO cut is 1 (on, entries nearest-first), 2 (off) or 3 (on, entries in cut order)"); ctx->opt_cut = int(value); break;
-    case VRH_OPT_AO_STEAL: VRH_CHECK(value <= 2 || (value >= 4 && value <= 4096), "vrh_ctx_set_option: AO steal is 1 (on), 2 (off) or 4..4096 (tiles per wave and queue x 16 counted as the last round)"); ctx->opt_steal = int(value); break;
+    case VRH_OPT_AO_STEAL: VRH_CHECK(value != 1, "vrh_ctx_set_option: the AO tail stash was removed (it measured slower)"); return VRH_OK;
     case VRH_OPT_AO_GATE: VRH_CHECK(value <= 2, "vrh_ctx_set_option: AO gate is 1 (on) or 2 (off)"); ctx->opt_gate = int(value); break;
     case VRH_OPT_POP_ON_MISS: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pop on miss is 1 (on) or 2 (off)"); ctx->opt_pop = int(value); break;
     case VRH_OPT_PAIR_LAYOUT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pair layout is 1 (line pairing) or 2 (builder order)"); ctx->opt_layout = int(value); break;
@@ -382,6 +382,11 @@ VRH_API int vrh_scene_get_view(const vrh_scene* scene, uint32_t bvh, vrh_scene_v
     v.prim_kind = scene->info.prim_kind;
     v.finite_bounds = scene->finite_bounds ? 1u : 0u;
     v.num_prims = scene->info.num_indices;
+    if (scene->quads && scene->num_roots == 1 && scene->finite_bounds)
+    {
+        v.quads = scene->quads;
+        v.quad_depth = scene->quad_depth;
+    }
     *out = v;
     return VRH_OK;
 }
@@ -1171,46 +1176,6 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
         p.stack_spill = static_cast<uint32_t*>(ctx->spill);
     }
 
-    // AO tail stealing (VRH_OPT_AO_STEAL, vrh_kernels.hip steal_publish): tiles handed out while fewer
-    // than steal_rem remain in their queue (about one per wave: the launch's last round) publish their
-    // hits to a stash whose AO rays every wave without tiles traces.  The stash holds every hit those
-    // tiles can have; a tile that finds it full traces its AO rays itself.
-    if (lc.ao && !lc.count && lc.epi == 0 && !list && !sp && p.samples > 0 && ctx->opt_steal != 2)
-    {
-        const uint64_t nwaves = uint64_t(grid) * uint64_t(waves_per_block);
-        const uint32_t nq = p.xcd_queues ? 8u : 1u;
-        const uint64_t per16 = ctx->opt_steal >= 4 ? uint64_t(ctx->opt_steal) : 16u;
-        p.steal_rem = uint32_t(std::min<uint64_t>((nwaves * per16 / 16u + nq - 1u) / nq, 0xFFFFFFFFull));
-        const uint64_t final_tiles = std::min<uint64_t>(units, uint64_t(p.steal_rem) * nq + nq);
-        const size_t need = size_t(final_tiles) * 64u;
-        if (need > ctx->steal_records)
-        {
-            VRH_HIP(hipStreamSynchronize(ctx->stream));
-            if (ctx->steal) (void)hipFree(ctx->steal);
-            ctx->steal = nullptr;
-            ctx->steal_records = 0;
-            // uncached (MTYPE UC): written on one XCD, read on another within the launch -- the XCDs'
-            // L2s are not coherent with each other for cached device memory
-            VRH_HIP(hipExtMallocWithFlags(&ctx->steal, need * (32u + 8u + 4u), hipDeviceMallocUncached));
-            VRH_HIP(hipMemset(ctx->steal, 0, need * (32u + 8u + 4u)));     // ready flags: no epoch
-            ctx->steal_records = need;
-            ctx->steal_epoch = 0;
-        }
-        if (++ctx->steal_epoch == 0u)
-        {
-            VRH_HIP(hipMemsetAsync(static_cast<char*>(ctx->steal) + ctx->steal_records * 40u, 0, ctx->steal_records * 4u,
-                                   ctx->stream));
-            ctx->steal_epoch = 1u;
-        }
-        char* base = static_cast<char*>(ctx->steal);
-        p.steal_rec = reinterpret_cast<float4*>(base);
-        p.steal_state = reinterpret_cast<unsigned long long*>(base + ctx->steal_records * 32u);
-        p.steal_ready = reinterpret_cast<uint32_t*>(base + ctx->steal_records * 40u);
-        p.steal_cap = uint32_t(std::min<size_t>(ctx->steal_records, 0xFFFFFFFFu));
-        p.steal_epoch = ctx->steal_epoch;
-        p.ao_steal = 1u;
-    }
-
     // per-wave timeline of this launch (diagnostic, VRH_OPT_WAVE_TIMES)
     ctx->wave_times_used = 0;
     if (ctx->opt_wave_times && (lc.sched == 0 || lc.sched == 3))
@@ -1222,17 +1187,11 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
             if (ctx->wave_times) (void)hipFree(ctx->wave_times);
             ctx->wave_times = nullptr;
             ctx->wave_times_n = 0;
-            VRH_HIP(hipMalloc(&ctx->wave_times, n * 10 * sizeof(unsigned long long)));
+            VRH_HIP(hipMalloc(&ctx->wave_times, n * 2 * sizeof(unsigned long long)));
             ctx->wave_times_n = n;
         }
         p.wave_times = ctx->wave_times;
         ctx->wave_times_used = n;
-        if (ctx->opt_wave_times == 2 && p.ao_steal)
-        {
-            // AO stash diagnostics: 8 words per wave after the (start, end) pairs
-            p.steal_dbg = ctx->wave_times + 2 * n;
-            VRH_HIP(hipMemsetAsync(p.steal_dbg, 0, n * 8 * sizeof(unsigned long long), ctx->stream));
-        }
     }
 
     const uint32_t slot = ctx->frames % VRH_MAX_TIMED_FRAMES;
@@ -1270,6 +1229,19 @@ VRH_API int vrh_sync(vrh_ctx* ctx)
     return VRH_OK;
 }
 
+VRH_API int vrh_ctx_user_queues(vrh_ctx* ctx, uint32_t** queues)
+{
+    VRH_CHECK(ctx && queues, "vrh_ctx_user_queues: null");
+    if (!ctx->user_queues)
+    {
+        int rc = select_device(ctx);
+        if (rc) return rc;
+        VRH_HIP(hipMalloc(&ctx->user_queues, 8u * VRH_USER_QUEUE_STRIDE * sizeof(uint32_t)));
+    }
+    *queues = ctx->user_queues;
+    return VRH_OK;
+}
+
 VRH_API int vrh_get_wave_times(vrh_ctx* ctx, uint64_t* out, uint64_t capacity, uint64_t* count, double* ticks_per_ms)
 {
     VRH_CHECK(ctx && count, "vrh_get_wave_times: null");
@@ -1285,7 +1257,7 @@ VRH_API int vrh_get_wave_times(vrh_ctx* ctx, uint64_t* out, uint64_t capacity, u
     }
     if (out && ctx->wave_times_used)
         VRH_HIP(hipMemcpy(out, ctx->wave_times,
-                          std::min<uint64_t>(capacity, (ctx->opt_wave_times == 2 ? 10 : 2) * ctx->wave_times_used) * 8,
+                          std::min<uint64_t>(capacity, 2 * ctx->wave_times_used) * 8,
                           hipMemcpyDeviceToHost));
     return VRH_OK;
 }
