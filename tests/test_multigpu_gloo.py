@@ -123,6 +123,59 @@ def test_sharded_exchange_equals_single_frames(tmp_path, oracle_mod, world, shar
     assert int(st[1]) == rays                  # rays summed over ranks = every frame
 
 
+def test_plan_known_values():
+    """libvrh's plan against hand-derived values (8-row bands dealt round-robin):
+    an off-by-one anywhere in vrh_plan.h changes one of these."""
+    # H = 36: 5 bands (the last one 4 rows); S = 2: shard 0 owns bands 0, 2, 4, shard 1 bands 1, 3
+    assert [multigpu.shard_bands(36, s, 2) for s in range(2)] == [3, 2]
+    assert multigpu.rows_max(36, 2) == 24
+    assert multigpu.packed_rows(36, 0, 2).tolist() == list(range(0, 8)) + list(range(16, 24)) + \
+        list(range(32, 36)) + [-1] * 4
+    assert multigpu.packed_rows(36, 1, 2).tolist() == list(range(8, 16)) + list(range(24, 32)) + [-1] * 8
+    # S = 8 over 2 bands: shards 2..7 own nothing
+    assert [multigpu.shard_bands(16, s, 8) for s in range(8)] == [1, 1, 0, 0, 0, 0, 0, 0]
+    # N = 3 ranks, S = 5 shards: rank r sends r, r + 3; the root receives s from s % 3
+    assert [multigpu.owned_shards(r, 3, 5) for r in range(3)] == [[0, 3], [1, 4], [2]]
+    assert [multigpu.shard_owner(s, 3) for s in range(5)] == [0, 1, 2, 0, 1]
+    # N = 3, S = 2: rank 2 owns nothing
+    assert multigpu.owned_shards(2, 3, 2) == []
+    # 4 x 36 image, 2 shards of 24 rows, 3 frames: [prim ids | masks | t] of 288 pixels
+    w = multigpu.wire_layout(FIELDS_ALL, 4, 36, 3, 2)
+    px = 3 * 24 * 4
+    assert (w.rows, w.prim_id, w.occ, w.t, w.shard_bytes) == (24, 0, 4 * px, 5 * px, 9 * px)
+    assert (w.color, w.code) == (_capi.VRH_WIRE_ABSENT, _capi.VRH_WIRE_ABSENT) and w.derive == 1
+    w = multigpu.wire_layout(FIELDS_COLOR, 4, 36, 3, 2)
+    assert (w.code, w.shard_bytes, w.prim_id) == (0, px, _capi.VRH_WIRE_ABSENT)
+
+
+def test_unshard_of_synthetic_shards():
+    """vrh_unshard_host on shards whose prim ids encode (frame, image row, x): every pixel lands on
+    its own row; colour re-derived from the code byte."""
+    Wd, Hd, S, F = 5, 37, 3, 2
+    w = multigpu.wire_layout(FIELDS_IDS, Wd, Hd, F, S, bg=BG)
+    g = np.zeros((S, w.shard_bytes), np.uint8)
+    for s in range(S):
+        rows = multigpu.packed_rows(Hd, s, S)
+        pid = multigpu.field(g[s], w, "prim_id", F, Wd, np.uint32)
+        occ = multigpu.field(g[s], w, "occ", F, Wd, np.uint8)
+        for f in range(F):
+            for lr, y in enumerate(rows):
+                pid[f, lr * Wd:(lr + 1) * Wd] = 0xFFFFFFFF if y < 0 else (f * 1000 + y) * 8 + np.arange(Wd)
+                occ[f, lr * Wd:(lr + 1) * Wd] = 0 if y < 0 else (y * 7 + f) & 0xFF
+    for f in range(F):
+        out = multigpu.unshard(g, w, FIELDS_IDS, Wd, Hd, S, f, bg=BG)
+        y, x = np.divmod(np.arange(Wd * Hd), Wd)
+        assert np.array_equal(out["prim_id"], ((f * 1000 + y) * 8 + x).astype(np.uint32))
+        assert np.array_equal(out["occ"], ((y * 7 + f) & 0xFF).astype(np.uint8))
+        k = np.array([bin(v).count("1") for v in out["occ"]])
+        grey = np.float32(1.0)
+        levels = [grey]
+        for _ in range(8):
+            grey = np.float32(grey - np.float32(1.0 / 8))
+            levels.append(grey)
+        assert np.array_equal(out["color"][:, 0], np.array(levels, np.float32)[k])
+
+
 def test_wire_layout_fields():
     """What crosses the wire per target (vrh_plan.h layout_for): colour-only -> 1 code byte;
     colour + ids -> prim id + mask (colour re-derived); t adds 4 B; >8 AO samples carry no mask."""
