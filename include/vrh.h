@@ -251,7 +251,8 @@ enum vrh_option {
                                     primaries have finished: 1 = on, 2 = off (auto: on)            */
     VRH_OPT_WAVE_TIMES = 19,     /* 1: the step-loop kernels record every wave's start / end time
                                     (wall_clock64) for vrh_get_wave_times -- a launch-timeline
-                                    diagnostic (0 = off, the default)                              */
+                                    diagnostic (0 = off, the default); 2: also the tile timeline of
+                                    counting one-frame AO launches (vrh_get_tile_times)            */
     VRH_OPT_AO_CUT = 20,         /* AO step loop: any-hit rays start below the top of the 4-wide tree,
                                     at a per-tile cut of at most 8 records whose boxes meet the
                                     tile's AO reach (every hit position +- eps + radius), pushed
@@ -359,6 +360,9 @@ VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats);   /* syn
 /* VRH_OPT_WAVE_TIMES: (start, end) clock ticks of every wave of the last launch, 2 * count values
  * into out (capacity values at most); ticks_per_ms = the constant wall clock's rate; syncs */
 VRH_API int vrh_get_wave_times(vrh_ctx* ctx, uint64_t* out, uint64_t capacity, uint64_t* count, double* ticks_per_ms);
+/* VRH_OPT_WAVE_TIMES = 2: per 8x8 tile of the last counting (VRH_KERNEL_COUNT_TESTS) one-frame AO
+ * launch, wall_clock64() at (hand-out, primaries done, pixels written); count = tiles (3 words each) */
+VRH_API int vrh_get_tile_times(vrh_ctx* ctx, uint64_t* out, uint64_t capacity, uint64_t* count);
 
 /* Device memory of the context for the user-kernel launches of visionaray_hip/hip_kernels.h: eight
  * tile-queue heads (one per XCD, 64 B apart: VRH_USER_QUEUE_STRIDE words) that the launch zeroes on

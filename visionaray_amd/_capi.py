@@ -150,6 +150,7 @@ SIGNATURES = {
     "vrh_scene_get_info": (C.c_int, [_vp, C.POINTER(vrh_scene_info)]),
     "vrh_scene_get_view": (C.c_int, [_vp, C.c_uint32, C.POINTER(vrh_scene_view)]),
     "vrh_get_wave_times": (C.c_int, [_vp, _vp, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
+    "vrh_get_tile_times": (C.c_int, [_vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "vrh_ctx_user_queues": (C.c_int, [_vp, C.POINTER(_vp)]),
     "vrh_scene_list_create": (C.c_int, [_vp, C.POINTER(_vp), _u32, _vp, _u32, C.POINTER(_vp)]),
     "vrh_scene_free": (C.c_int, [_vp]),

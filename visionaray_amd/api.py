@@ -183,6 +183,20 @@ class Context:
         t = buf.reshape(-1, 2).astype(np.float64)
         return (t - t[:, 0].min()) / rate.value
 
+    def tile_times(self):
+        """(hand-out, primaries done, pixels written) of every tile of the last counting one-frame AO
+        launch (VRH_OPT_WAVE_TIMES = 2) in ms from the first hand-out, or None."""
+        import numpy as np
+        n, rate = C.c_uint64(), C.c_double()
+        capi.check("vrh_get_wave_times", self.handle, None, 0, C.byref(C.c_uint64()), C.byref(rate))
+        capi.check("vrh_get_tile_times", self.handle, None, 0, C.byref(n))
+        if n.value == 0:
+            return None
+        buf = np.zeros(3 * n.value, np.uint64)
+        capi.check("vrh_get_tile_times", self.handle, buf.ctypes.data_as(C.c_void_p), buf.size, C.byref(n))
+        t = buf.reshape(-1, 3).astype(np.float64)
+        return (t - t[:, 0][t[:, 0] > 0].min()) / rate.value
+
     def stats_reset(self):
         capi.check("vrh_stats_reset", self.handle)
 

@@ -78,6 +78,9 @@ struct render_params
                               // (1: entries in cut order, 2: nearest-first)
     uint32_t ao_gate;         // AO step loop: a tile's AO rays are handed out once its primaries are done
     unsigned long long* wave_times;   // VRH_OPT_WAVE_TIMES: per wave (start, end) of wall_clock64(), else null
+    // VRH_OPT_WAVE_TIMES = 2, counting kernels of one-frame AO launches: per tile (hand-out, primaries
+    // done, pixels written) of wall_clock64() -- where a launch's tail comes from
+    unsigned long long* tile_times;
     uint32_t descent_cap;     // step loop: inner visits per step before a descent is resumed later
     uint32_t step_flags;      // step loop: bit 0 a descent that misses both children pops and continues;
                               // bit 1 wave-uniform pair records fetched through the scalar cache

@@ -712,6 +712,12 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         tile_queue tq = queue_init(P);
         // wave-uniform tile state
         uint32_t tileC = next_tile(P, tq, lane), parC = 0;
+        // tile timeline (counting instance only): [3 t] hand-out, [3 t + 1] primaries done, [3 t + 2] written
+        auto tile_mark = [&](uint32_t id, uint32_t k) {
+            if constexpr (COUNT)
+                if (P.tile_times && id != NONE && lane == 0u) P.tile_times[3u * (id & TILE_MASK) + k] = wall_clock64();
+        };
+        tile_mark(tileC, 0u);
         uint32_t handedC = 0, pendC = 0, pubC = 0, issC = 0;  // primaries handed / in flight, slots, AO rays handed
         uint32_t tileD = NONE, parD = 0, slotsD = 0;
         uint32_t inflight0 = 0, inflight1 = 0;                // AO rays in flight per buffer parity
@@ -740,6 +746,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     if (COUNT) count_stores(cnt, P, o, ST_COLOR | ST_OCC);
                 }
                 __builtin_amdgcn_wave_barrier();
+                tile_mark(tileD, 2u);
                 tileD = NONE;
             }
             // 2. the current tile has handed out all its rays: it drains, the next tile starts
@@ -747,6 +754,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             {
                 tileD = tileC; parD = parC; slotsD = pubC;
                 tileC = next_tile(P, tq, lane);
+                tile_mark(tileC, 0u);
                 parC ^= 1u;
                 handedC = 0; pendC = 0; pubC = 0; issC = 0;
             }
@@ -890,6 +898,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 }
                 pubC += (uint32_t)__popcll(hfin);
                 pendC -= (uint32_t)__popcll(fin);
+                if (pendC == 0u && handedC >= 64u) tile_mark(tileC, 1u);
                 hits_total += hit ? 1 : 0;
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -19,6 +19,8 @@ struct vrh_ctx
     // device counters (u64), see render_params::counters; [0..7] reset per frame
     unsigned long long* counters = nullptr;
     uint32_t* user_queues = nullptr;            // vrh_ctx_user_queues (8 heads x 64 B)
+    unsigned long long* tile_times = nullptr;   // VRH_OPT_WAVE_TIMES = 2 (counting kernels): 3 per tile
+    size_t tile_times_n = 0, tile_times_used = 0;
     unsigned long long* wave_times = nullptr;   // VRH_OPT_WAVE_TIMES buffer (2 per resident wave)
     size_t wave_times_n = 0, wave_times_used = 0;
     void* spill = nullptr;          // traversal stack overflow blocks (vrh_render_batch), grown on demand

@@ -114,6 +114,7 @@ VRH_API int vrh_ctx_destroy(vrh_ctx* ctx)
     if (ctx->counters) (void)hipFree(ctx->counters);
     if (ctx->wave_times) (void)hipFree(ctx->wave_times);
     if (ctx->user_queues) (void)hipFree(ctx->user_queues);
+    if (ctx->tile_times) (void)hipFree(ctx->tile_times);
     if (ctx->spill) (void)hipFree(ctx->spill);
     for (auto e : ctx->ev_start) (void)hipEventDestroy(e);
     for (auto e : ctx->ev_stop) (void)hipEventDestroy(e);
@@ -143,7 +144,7 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
         VRH_CHECK(value == 0 || value == 2, "vrh_ctx_set_option: cooperative fetch was removed (2 = off is accepted)");
         if (value == 1) return VRH_ERR_UNSUPPORTED;
         break;
-    case VRH_OPT_WAVE_TIMES: VRH_CHECK(value <= 1, "vrh_ctx_set_option: wave times is 1 (on) or 0 (off)"); ctx->opt_wave_times = int(value); break;
+    case VRH_OPT_WAVE_TIMES: VRH_CHECK(value <= 2, "vrh_ctx_set_option: wave times is 1 (on), 2 (on + tile times of counting one-frame AO launches) or 0 (off)"); ctx->opt_wave_times = int(value); break;
     case VRH_OPT_AO_CUT: VRH_CHECK(value <= 3, "vrh_ctx_set_option: AO cut is 1 (on, entries nearest-first), 2 (off) or 3 (on, entries in cut order)"); ctx->opt_cut = int(value); break;
     case VRH_OPT_AO_STEAL: VRH_CHECK(value != 1, "vrh_ctx_set_option: the AO tail stash was removed (it measured slower)"); return VRH_OK;
     case VRH_OPT_AO_GATE: VRH_CHECK(value <= 2, "vrh_ctx_set_option: AO gate is 1 (on) or 2 (off)"); ctx->opt_gate = int(value); break;
@@ -1193,6 +1194,22 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
         p.wave_times = ctx->wave_times;
         ctx->wave_times_used = n;
     }
+    ctx->tile_times_used = 0;
+    if (ctx->opt_wave_times == 2 && lc.count && lc.ao && num_frames == 1 && p.num_tiles > 0)
+    {
+        if (p.num_tiles > ctx->tile_times_n)
+        {
+            VRH_HIP(hipStreamSynchronize(ctx->stream));
+            if (ctx->tile_times) (void)hipFree(ctx->tile_times);
+            ctx->tile_times = nullptr;
+            ctx->tile_times_n = 0;
+            VRH_HIP(hipMalloc(&ctx->tile_times, size_t(p.num_tiles) * 3 * sizeof(unsigned long long)));
+            ctx->tile_times_n = p.num_tiles;
+        }
+        VRH_HIP(hipMemsetAsync(ctx->tile_times, 0, size_t(p.num_tiles) * 3 * sizeof(unsigned long long), ctx->stream));
+        p.tile_times = ctx->tile_times;
+        ctx->tile_times_used = p.num_tiles;
+    }
 
     const uint32_t slot = ctx->frames % VRH_MAX_TIMED_FRAMES;
     while (ctx->ev_start.size() <= slot)
@@ -1226,6 +1243,16 @@ VRH_API int vrh_sync(vrh_ctx* ctx)
     VRH_CHECK(ctx, "vrh_sync: null");
     if (ctx->group_written) VRH_HIP(hipEventSynchronize(ctx->group_written));
     VRH_HIP(hipStreamSynchronize(ctx->stream));
+    return VRH_OK;
+}
+
+VRH_API int vrh_get_tile_times(vrh_ctx* ctx, uint64_t* out, uint64_t capacity, uint64_t* count)
+{
+    VRH_CHECK(ctx && count, "vrh_get_tile_times: null");
+    VRH_HIP(hipStreamSynchronize(ctx->stream));
+    *count = ctx->tile_times_used;
+    if (out && ctx->tile_times_used)
+        VRH_HIP(hipMemcpy(out, ctx->tile_times, std::min<uint64_t>(capacity, 3 * ctx->tile_times_used) * 8, hipMemcpyDeviceToHost));
     return VRH_OK;
 }
 
