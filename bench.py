@@ -432,8 +432,10 @@ def main():
         pmc_name = f"pmc_traffic_F{F}.json"
         pmc = load_json(os.path.join(ROOT, "profiles", pmc_name)) or {}
         traffic, pmc_info = None, None
+        from visionaray_amd.buildinfo import kernel_source_sha256
+        pmc_build_ok = pmc.get("kernel_source_sha256") == kernel_source_sha256()
         if (pmc.get("scene") == args.scene and pmc.get("kernel") == kernel and not grouped
-                and pmc.get("frames_per_launch") == F):
+                and pmc.get("frames_per_launch") == F and pmc_build_ok):
             traffic = pmc.get("hbm_bytes_per_launch")
             if pmc.get("l1_requests_per_launch"):
                 pmc_info = {"l1_requests_per_launch": pmc["l1_requests_per_launch"],
@@ -478,6 +480,8 @@ def main():
                 "kernel_ms_per_frame": round(k_ms_mean / F, 4),
                 "roof_source": roof.get("source") if roof else None,
                 "requests_source": ("pmc (TCP_TOTAL_CACHE_ACCESSES of the committed pass)" if pmc_info
+                                    else "the committed PMC pass is of another kernel build (kernel_source_sha256 "
+                                         "differs): achieved / frac / traffic not reported" if pmc and not pmc_build_ok
                                     else "no PMC pass of this configuration committed: achieved / frac not reported"),
                 "pmc": pmc_info,
                 # the counting variant's access-shape statistics of one frame (diagnostic; they count

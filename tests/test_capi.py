@@ -163,3 +163,23 @@ def test_sah_cost_matches_reference(golden, name):
     b = va.build_index_bvh(scenes.primitives(name))
     c = np.float32(va.sah_cost(b.nodes)).view(np.uint32)
     assert "%08x" % int(c) == golden["sah_cost_bits"][name]
+
+
+def test_kernel_source_hash_identifies_the_build(tmp_path):
+    """bench.py reports a committed PMC pass only for the kernel sources it was measured on
+    (visionaray_amd/buildinfo.py): the hash covers every kernel source and changes with any of them."""
+    import os
+    from visionaray_amd import buildinfo
+    files = buildinfo.kernel_sources()
+    assert all(os.path.exists(p) for p in files)
+    assert any(p.endswith("vrh_kernels.hip") for p in files) and any(p.endswith("vrh_device.h") for p in files)
+    h = buildinfo.kernel_source_sha256()
+    assert len(h) == 64 and h == buildinfo.kernel_source_sha256()
+    orig = buildinfo.kernel_sources
+    extra = tmp_path / "x.h"
+    extra.write_text("// x\n")
+    try:
+        buildinfo.kernel_sources = lambda: orig() + [str(extra)]
+        assert buildinfo.kernel_source_sha256() != h
+    finally:
+        buildinfo.kernel_sources = orig

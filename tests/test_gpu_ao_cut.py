@@ -37,11 +37,17 @@ def _check(got, ref, n=None):
 
 @pytest.mark.parametrize("radius", [0.002, 0.03, 0.1, 0.6, 8.0])
 @pytest.mark.parametrize("cut", [0, 2, 3])
-def test_ao_cut_matches_oracle(ctx, oracle_mod, scene, radius, cut):
+@pytest.mark.parametrize("stack", [0, 12])
+def test_ao_cut_matches_oracle(ctx, oracle_mod, scene, radius, cut, stack):
+    """stack 12: an LDS stack of 12 entries, shallower than the BVH, so the overflow-block (spilling)
+    kernel instances run -- with the cut (cutN + 4 <= 12) and without it."""
     O = oracle_mod
     dev, cam, osc = scene
+    if stack:
+        assert dev.info["max_depth"] > stack
     ref = O.render(osc, O.scene_camera(NAME, W, H), mode=O.VO_MODE_AO, radius=radius)
     ctx.set_option("ao_cut", cut)
+    ctx.set_option("stack_cap", stack)
     try:
         rt = va.hip_buffer_rt(ctx, W, H)
         va.hip_sched(ctx).frame(va.ao_kernel(dev, radius=radius), va.make_sched_params(cam, rt))
@@ -53,6 +59,7 @@ def test_ao_cut_matches_oracle(ctx, oracle_mod, scene, radius, cut):
         _check(rtb.download(), ref, W * H)
     finally:
         ctx.set_option("ao_cut", 0)
+        ctx.set_option("stack_cap", 0)
 
 
 def test_ao_cut_option_range(ctx):

@@ -59,8 +59,10 @@ def main():
         v, n = per_launch(os.path.join(d, sub))
         c.update(v)
         name = name or n
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from visionaray_amd.buildinfo import kernel_source_sha256
     res = {"scene": scene, "kernel": kernel, "gpus": 1, "frames_per_launch": fpl, "kernel_name": name,
-           "command": cmd, "counters_per_launch": c}
+           "command": cmd, "counters_per_launch": c, "kernel_source_sha256": kernel_source_sha256()}
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         read = c["FETCH_SIZE"] * 1024 * 2
         write = c["WRITE_SIZE"] * 1024
