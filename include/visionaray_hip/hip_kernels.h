@@ -359,6 +359,49 @@ __device__ inline vrh::dev::lds_stack user_stack()
     return st;
 }
 
+// A record every active lane of the wave wants (the upper tree levels, for the rays of one 8 x 8
+// tile) is fetched once through the scalar cache, as the built-in kernels fetch wave-uniform pairs
+// (vrh_device.h ray_step); otherwise per lane.  Same bytes either way.
+#ifndef VRH_USER_SCALAR_FETCH
+#define VRH_USER_SCALAR_FETCH 1
+#endif
+typedef const __attribute__((address_space(4))) float user_cfloat;
+__device__ inline void fetch_pair(const float4* pairs, uint32_t link, float4& q0, float4& q1, float4& q2, float2& q3)
+{
+    const uint32_t lf = (uint32_t)__builtin_amdgcn_readfirstlane((int)link);
+    if (VRH_USER_SCALAR_FETCH && __ballot(link != lf) == 0ull)
+    {
+        user_cfloat* cp = (user_cfloat*)(const float*)(pairs) + 16u * lf;
+        q0 = make_float4(cp[0], cp[1], cp[2], cp[3]);
+        q1 = make_float4(cp[4], cp[5], cp[6], cp[7]);
+        q2 = make_float4(cp[8], cp[9], cp[10], cp[11]);
+        q3 = make_float2(cp[12], cp[13]);
+    }
+    else
+    {
+        const float4* p = pairs + 4u * link;
+        q0 = p[0]; q1 = p[1]; q2 = p[2];
+        q3 = *reinterpret_cast<const float2*>(p + 3);
+    }
+}
+
+__device__ inline void fetch_quad(const float4* quads, uint32_t link, float4 (&q)[7])
+{
+    const uint32_t lf = (uint32_t)__builtin_amdgcn_readfirstlane((int)link);
+    if (VRH_USER_SCALAR_FETCH && __ballot(link != lf) == 0ull)
+    {
+        user_cfloat* cp = (user_cfloat*)(const float*)(quads) + 32u * lf;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) q[k] = make_float4(cp[4 * k], cp[4 * k + 1], cp[4 * k + 2], cp[4 * k + 3]);
+    }
+    else
+    {
+        const float4* p = quads + 8u * link;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) q[k] = p[k];
+    }
+}
+
 template <bool FAST, typename CullT, typename Leaf>
 __device__ inline void walk_slab(vrh_scene_view const& b, vrh::dev::ray_t const& r, float max_t, CullT const& cull_t, Leaf&& leaf)
 {
@@ -371,9 +414,9 @@ __device__ inline void walk_slab(vrh_scene_view const& b, vrh::dev::ray_t const&
         bool at_leaf = true;
         while (!(link & vrh::dev::LEAF_BIT))
         {
-            const float4* p = pairs + 4u * link;
-            const float4 q0 = p[0], q1 = p[1], q2 = p[2];
-            const float2 q3 = *reinterpret_cast<const float2*>(p + 3);
+            float4 q0, q1, q2;
+            float2 q3;
+            fetch_pair(pairs, link, q0, q1, q2, q3);
             bool b0, b1;
             float tn0, tn1;
             vrh::dev::box_pair<FAST>(q0, q1, q2, r, cull_t(), max_t, b0, b1, tn0, tn1);
@@ -413,8 +456,9 @@ __device__ inline bool walk_quads(vrh_scene_view const& b, vrh::dev::ray_t const
         bool at_leaf = true;
         while (!(link & vrh::dev::LEAF_BIT))
         {
-            const float4* p = quads + 8u * link;
-            const float4 xl = p[0], yl = p[1], zl = p[2], xh = p[3], yh = p[4], zh = p[5], lk = p[6];
+            float4 qr[7];
+            fetch_quad(quads, link, qr);
+            const float4 xl = qr[0], yl = qr[1], zl = qr[2], xh = qr[3], yh = qr[4], zh = qr[5], lk = qr[6];
             const uint32_t k0 = __float_as_uint(lk.x), k1 = __float_as_uint(lk.y);
             const uint32_t k2 = __float_as_uint(lk.z), k3 = __float_as_uint(lk.w);
             float d0, d1, d2, d3;
@@ -448,11 +492,13 @@ __device__ inline bool walk_quads(vrh_scene_view const& b, vrh::dev::ray_t const
 // the LDS stack holds VRH_USER_STACK entries: a deeper BVH (not passed through checked_ref) is not
 // traversed -- a miss, never an out-of-bounds stack write.  The hardware min/max slab test where it is
 // provably identical (vrh_device.h box_pair).  ANY: an any-hit walk (the leaf ends it at the first
-// accepted hit), which takes the 4-wide records where the scene has them and the ray is finite --
-// the hit / miss answer is the binary walk's; WHICH hit ends the ray may differ, as any hit may
-// (VRH_USER_BINARY_ANYHIT=1 keeps the reference's binary order, and so its first-found hit record).
+// accepted hit).  By default it is the binary walk in the reference's order, so the hit record an
+// any_hit returns is the reference's first-found one; VRH_USER_BINARY_ANYHIT=0 takes the 4-wide
+// records where the scene has them and the ray is finite (the hit / miss answer is the same, WHICH
+// hit ends the ray may differ).  Measured on the AO lambda (C3, profiles/r03_ab/user/): the binary
+// walk with the scalar fetch of wave-uniform pairs is 2-3 % faster than the 4-wide one.
 #ifndef VRH_USER_BINARY_ANYHIT
-#define VRH_USER_BINARY_ANYHIT 0
+#define VRH_USER_BINARY_ANYHIT 1
 #endif
 template <bool ANY = false, typename Ray, typename CullT, typename Leaf>
 __device__ inline void walk(vrh_scene_view const& b, Ray const& ray, float max_t, CullT const& cull_t, Leaf&& leaf)
@@ -906,8 +952,17 @@ __device__ inline uint32_t xcc_id()
 // the persistent loop: queue q hands out strip q (tiles [tiles * q / 8, tiles * (q + 1) / 8)) of
 // every frame, frame-major; every (frame, tile) is handed out exactly once by one of the 8 heads, so
 // which XCD a wave runs on changes only speed.  Every wave leaves once all 8 queues are empty.
+// VRH_USER_WAVES: waves per SIMD the register allocation targets (0: the compiler's choice)
+#ifndef VRH_USER_WAVES
+#define VRH_USER_WAVES 0
+#endif
+#if VRH_USER_WAVES
+#define VRH_USER_OCC __attribute__((amdgpu_waves_per_eu(VRH_USER_WAVES)))
+#else
+#define VRH_USER_OCC
+#endif
 template <typename K, uint32_t SK = VRH_SAMPLER_UNIFORM, uint32_t SN = 1, uint32_t NC = 1>
-__global__ __launch_bounds__(64) void user_render(K kernel, user_frames<NC> f)
+__global__ __launch_bounds__(64) VRH_USER_OCC void user_render(K kernel, user_frames<NC> f)
 {
     const uint32_t lane = threadIdx.y * 8u + threadIdx.x;
     uint32_t q = xcc_id();

@@ -24,6 +24,10 @@
 #include <deque>
 #include <unordered_map>
 
+#ifndef VRH_QUAD_ORDER
+#define VRH_QUAD_ORDER 0      // record order: 0 = breadth-first, 1 = depth-first (sibling groups)
+#endif
+
 namespace vrh {
 
 namespace {
@@ -57,8 +61,15 @@ bool build_quads(const node32* nodes, uint32_t num_nodes, std::vector<float>& ou
     out.resize(32, 0.0f);
     while (!queue.empty())
     {
+#if VRH_QUAD_ORDER == 1
+        // depth-first: a record's inner entries get consecutive indices (as in breadth-first), and
+        // the first of them is expanded next, so a descent's records lie close together
+        const uint32_t n = queue.back().first, depth = queue.back().second;
+        queue.pop_back();
+#else
         const uint32_t n = queue.front().first, depth = queue.front().second;
         queue.pop_front();
+#endif
         quad_depth = std::max(quad_depth, depth);
         const uint32_t q = index[n];
         uint32_t entries[4];
@@ -102,6 +113,10 @@ bool build_quads(const node32* nodes, uint32_t num_nodes, std::vector<float>& ou
                 }
             }
         }
+#if VRH_QUAD_ORDER == 1
+        // the entries were queued in order; depth-first expands the first one next
+        std::reverse(queue.end() - std::count_if(links, links + ne, [](uint32_t l) { return !(l & 0x80000000u); }), queue.end());
+#endif
         float* rec = &out[size_t(q) * 32];
         for (uint32_t e = 0; e < 4; ++e)
         {
