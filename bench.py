@@ -429,7 +429,9 @@ def main():
         # PMC of this exact configuration (tools/r02_session.sh + tools/pmc_bench.py): HBM bytes per
         # launch (`traffic`), the L1 requests the hardware counted and how busy the TD unit was
         # one committed pass per frames-per-launch value (the driver's --steps decides F)
-        pmc_name = f"pmc_traffic_F{F}.json"
+        pmc_name = f"pmc_traffic_F{F}_{args.scene}.json"
+        if not os.path.exists(os.path.join(ROOT, "profiles", pmc_name)):
+            pmc_name = f"pmc_traffic_F{F}.json"
         pmc = load_json(os.path.join(ROOT, "profiles", pmc_name)) or {}
         traffic, pmc_info = None, None
         from visionaray_amd.buildinfo import kernel_source_sha256
