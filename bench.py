@@ -446,6 +446,19 @@ def main():
         # achieved: the hardware-counted L1 requests (TCP_TOTAL_CACHE_ACCESSES) of a committed PMC pass
         # of this exact configuration, over the live hipEvent time; without one it is not reported
         achieved = (pmc_info["l1_requests_per_launch"] * L1_REQ_BYTES / (k_ms_mean * 1e-3) / 1e9) if pmc_info else None
+        # the roof of the kernel's own access shape: the fastest microbenchmark mode whose loads are
+        # at least as merged as the kernel's (TCP accesses per wave-level load <= 1.25 x the kernel's,
+        # PMC) -- for ~17.6 that is "quad-bcast" (4 lanes per address, 16 accesses per load); the
+        # max-rate `peak` mode is per-lane gathers at 64 accesses per load
+        shape = None
+        if roof and pmc and pmc.get("l1_requests_per_vmem_load") and pmc_info:
+            apl = pmc["l1_requests_per_vmem_load"]
+            cands = {k: v for k, v in roof["modes"].items() if v["tcp_accesses_per_load"] <= 1.25 * apl} or roof["modes"]
+            name, m = max(cands.items(), key=lambda kv: kv[1]["requests_per_s"])
+            sp = m["requests_per_s"] * L1_REQ_BYTES / 1e9
+            shape = {"mode": name, "accesses_per_load": round(m["tcp_accesses_per_load"], 2),
+                     "kernel_accesses_per_load": round(apl, 2), "peak": round(sp, 1),
+                     "frac": round(achieved / sp, 4)}
         line = {
             "metric": "Mrays/s (primary + 8-sample AO)" if kernel == "ao" else "Mrays/s (primary)",
             "value": round(mrays, 3),
@@ -473,6 +486,7 @@ def main():
                 "bound": "vmem-l1", "unit": "GB/s",
                 "achieved": round(achieved, 1) if achieved else None, "peak": peak,
                 "frac": round(achieved / peak, 4) if (peak and achieved) else None,
+                "own_shape": shape,
                 "traffic": traffic,
                 "what": "vector-L1 requests (TCP accesses: distinct 16-B pieces per wave-level load/store) x 16 B of "
                         "the traversal launch over its hipEvent time; peak = the request rate of per-lane dependent "
