@@ -538,6 +538,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         mh.n = EPI == 2 ? P.max_hits : 1u;
         whitted_lane w;
         w.shadow = 0; w.depth = 0;
+        w.sm = reinterpret_cast<float*>(smem); w.base = P.stack_cap * block + tid; w.stride = block;   // EPI 3 LDS words
         for (;;)
         {
             uint64_t idle = __ballot(mode == IDLE);
@@ -641,11 +642,12 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                             {
                                 // color += shaded * throughput; the reflection ray is traced only
                                 // if the next loop test can pass (its result is unused otherwise)
-                                w.color = w.color + w.shaded * w.thr;
+                                w.color = w.color + w.ld3(WL_SHADED) * w.thr;
                                 const float thr2 = w.thr * 0.1f;
                                 if (thr2 > P.eps && w.depth < P.num_bounces)
                                 {
-                                    r = make_ray(w.pos + w.rdir * P.eps, w.rdir);
+                                    const f3 rdir = whitted_reflect(w);
+                                    r = make_ray(w.ld3(WL_POS) + rdir * P.eps, rdir);
                                     w.thr = thr2; w.shadow = 0;
                                     max_t = FMAX; any = false; quad = false;
                                     finite = finite_ray(r);
@@ -1021,7 +1023,8 @@ bool render_spill_available(const launch_config& c)
 size_t render_lds_bytes(const launch_config& c)
 {
     size_t words = size_t(c.stack_cap) * c.block + (c.ao ? size_t(c.block / 64) * dev::AO_WAVE_WORDS : 0)
-                 + (c.epi == 2 ? size_t(5) * c.max_hits * c.block : 0);
+                 + (c.epi == 2 ? size_t(5) * c.max_hits * c.block : 0)
+                 + (c.epi == 3 ? size_t(dev::WL_WORDS) * c.block : 0);
     return words * 4;
 }
 

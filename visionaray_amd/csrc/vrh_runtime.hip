@@ -1014,10 +1014,11 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     // frames in flight on the step loop (primary / AO, uncounted): the BATCH instantiation
     if (lc.sched == 0 && num_frames > 1 && !lc.count && lc.epi == 0 && !hmask) lc.sched = 3;
     // shading epilogues: no VGPR cap (their lane state spills at 6 waves/SIMD; measured faster at 4,
-    // profiles/r01_shade/shade_bench.jsonl); AO on the step loop: 5 waves/SIMD (96 VGPRs, no spills:
-    // 4-6 % faster than 6 with 18 spilled VGPRs); primary visibility: 6 (profiles/r01_ab_waves/);
-    // BVH lists run at these defaults
-    lc.occ = ctx->opt_occ ? ctx->opt_occ : lc.epi ? 1 : lc.ao ? 5 : 6;
+    // profiles/r01_shade/shade_bench.jsonl), except whitted, whose bounce surface lives in LDS (vrh_shade.h):
+    // 96 VGPRs without spills, 5 waves/SIMD, +0.7-2.1 % over 4 (profiles/r03_ab/whitted/); AO on the
+    // step loop: 5 waves/SIMD (96 VGPRs, no spills: 4-6 % faster than 6 with 18 spilled VGPRs); primary
+    // visibility: 6 (profiles/r01_ab_waves/); BVH lists run at these defaults
+    lc.occ = ctx->opt_occ ? ctx->opt_occ : whitted ? 5 : lc.epi ? 1 : lc.ao ? 5 : 6;
     if (sp) lc.occ = lc.ao ? 5 : 6;                    // the sampler instances exist at the defaults
     if (list) lc.occ = ao ? 5 : 6;
     // auto: the LDS part of the stack shrinks (in steps of 4 entries) while LDS, not registers,
@@ -1143,6 +1144,7 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
         p.shade.per_vertex = k->normal_binding == VRH_NORMALS_PER_VERTEX ? 1u : 0u;
         p.shade.vnormals = sc->vnormals;
         std::memcpy(p.shade.ambient, k->ambient, 16);
+        for (int i = 0; i < 3; ++i) p.shade.amb[i] = p.shade.ambient[i] * p.shade.ambient[3];   // plastic.inl:13-16
     }
     p.num_bounces = whitted ? k->num_bounces : 0u;
     if (hmask && sc->info.prim_kind == VRH_PRIM_TRI64)

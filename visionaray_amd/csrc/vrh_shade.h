@@ -26,6 +26,7 @@ struct shade_params
     uint32_t per_vertex;          // normals_per_vertex_binding
     const float4* vnormals;       // 3 per prim_id
     float ambient[4];
+    float amb[3];                 // ambient[i] * ambient[3], computed on the host (the same IEEE products)
 };
 
 __device__ __forceinline__ f3 neg(f3 a) { return mk3(-a.x, -a.y, -a.z); }
@@ -99,7 +100,7 @@ __device__ inline float4 shade_simple(const shade_params& S, const float4* __res
     const f3 pos = r.ori + r.dir * t;                                  // simple.inl:37
     const surface_t sf = get_surface(S, prims, normals, prim_id, hx.li, hx.u, hx.v);
     // plastic.inl:13-16 ambient() = ca * ka, times from_rgba(ambient_color) (spectrum.inl:375-378)
-    const f3 amb = mk3(S.ambient[0] * S.ambient[3], S.ambient[1] * S.ambient[3], S.ambient[2] * S.ambient[3]);
+    const f3 amb = mk3(S.amb[0], S.amb[1], S.amb[2]);
     f3 shaded = (mk3(sf.m.ca[0], sf.m.ca[1], sf.m.ca[2]) * sf.m.ka) * amb;
     const f3 view = neg(r.dir);
     const f3 n = dot(sf.gn, view) < 0.0f ? neg(sf.sn) : sf.sn;       // faceforward, vector.inl:674-681
@@ -112,37 +113,51 @@ __device__ inline float4 shade_simple(const shade_params& S, const float4* __res
 // (primary or reflection) that hits sets up the surface, then one any-hit shadow ray per light
 // (max_t = distance to the light), then the reflection ray of the plastic fall-through bounce
 // (reflect(view, shading normal), kr = 0.1, whitted.inl:64-77).  The lane keeps what the loop body
-// carries between those rays.
+// carries between those rays.  The bounce's surface (isect_pos, two-sided shading normal,
+// view_dir, shaded_clr: 12 words) is read only when a ray of the bounce ends, so it lives in LDS
+// after the traversal stack ([word][lane], conflict-free), not in registers: the kernel then fits
+// 96 VGPRs without spills, 5 waves / SIMD instead of 4 at 124.
 struct whitted_lane
 {
     f3 color;        // accumulated radiance (`color`)
-    f3 shaded;       // this bounce: ambient + unshadowed lights (`shaded_clr`)
-    f3 pos, n, view; // isect_pos, two-sided shading normal, view_dir
-    f3 rdir;         // reflected direction of this bounce
     float thr;       // throughput
     uint32_t depth;  // loop iterations entered
     uint32_t li;     // light of the shadow ray in flight
     uint32_t mi;     // material (geom_id)
     uint32_t shadow; // 1 while a shadow ray is traced
+    float* sm;       // LDS base of the surface words: word k of this lane at sm[base + k * stride]
+    uint32_t base, stride;
+    __device__ __forceinline__ float& at(uint32_t k) const { return sm[base + k * stride]; }
+    __device__ __forceinline__ f3 ld3(uint32_t k) const { return mk3(at(k), at(k + 1u), at(k + 2u)); }
+    __device__ __forceinline__ void st3(uint32_t k, f3 v) const { at(k) = v.x; at(k + 1u) = v.y; at(k + 2u) = v.z; }
 };
+constexpr uint32_t WL_POS = 0, WL_N = 3, WL_VIEW = 6, WL_SHADED = 9, WL_WORDS = 12;   // LDS words per lane
 
 // loop body up to the light loop (whitted.inl:225-233), for a hit at t of ray r
 __device__ inline void whitted_surface(const shade_params& S, const float4* __restrict__ prims,
                                        const float4* __restrict__ normals, whitted_lane& w, const ray_t& r, float t,
                                        uint32_t prim_id, const hit_extra& hx)
 {
-    w.pos = r.ori + r.dir * t;
+    w.st3(WL_POS, r.ori + r.dir * t);
     const surface_t sf = get_surface(S, prims, normals, prim_id, hx.li, hx.u, hx.v);
     w.mi = sf.mi;
-    const f3 amb = mk3(S.ambient[0] * S.ambient[3], S.ambient[1] * S.ambient[3], S.ambient[2] * S.ambient[3]);
-    w.shaded = (mk3(sf.m.ca[0], sf.m.ca[1], sf.m.ca[2]) * sf.m.ka) * amb;
-    w.view = neg(r.dir);
-    w.n = dot(sf.gn, w.view) < 0.0f ? neg(sf.sn) : sf.sn;           // faceforward
-    // specular_bounce(plastic) = reflect(view_dir, shading_normal): 2 * dot(n, i) * n - i
-    // (vector.inl:683-689), with the un-flipped shading normal (whitted.inl:262)
-    const float d2 = 2.0f * dot(sf.sn, w.view);
-    w.rdir = mk3(d2 * sf.sn.x, d2 * sf.sn.y, d2 * sf.sn.z) - w.view;
+    const f3 amb = mk3(S.amb[0], S.amb[1], S.amb[2]);
+    w.st3(WL_SHADED, (mk3(sf.m.ca[0], sf.m.ca[1], sf.m.ca[2]) * sf.m.ka) * amb);
+    const f3 view = neg(r.dir);
+    w.st3(WL_VIEW, view);
+    w.st3(WL_N, dot(sf.gn, view) < 0.0f ? neg(sf.sn) : sf.sn);      // faceforward
     w.li = 0;
+}
+
+// specular_bounce(plastic) = reflect(view_dir, shading_normal): 2 * dot(n, i) * n - i
+// (vector.inl:683-689, whitted.inl:262) with the un-flipped shading normal sn.  Computed from the
+// stored two-sided normal n = +-sn: dot(-sn, v) = -dot(sn, v) and (-d) * (-x) = d * x exactly under
+// round-to-nearest, so the result is bit-identical.
+__device__ inline f3 whitted_reflect(const whitted_lane& w)
+{
+    const f3 n = w.ld3(WL_N), view = w.ld3(WL_VIEW);
+    const float d2 = 2.0f * dot(n, view);
+    return mk3(d2 * n.x, d2 * n.y, d2 * n.z) - view;
 }
 
 // shadow ray of light w.li (whitted.inl:237-252): origin pushed along the light direction, any hit
@@ -151,17 +166,19 @@ __device__ inline ray_t whitted_shadow_ray(const shade_params& S, const whitted_
 {
     const point_light_t& L = S.lights[w.li];
     const f3 lpos = mk3(L.position[0], L.position[1], L.position[2]);
-    const f3 ldir = normalize(lpos - w.pos);
-    const f3 dv = w.pos - lpos;
+    const f3 pos = w.ld3(WL_POS);
+    const f3 ldir = normalize(lpos - pos);
+    const f3 dv = pos - lpos;
     max_t = __builtin_sqrtf(dot(dv, dv));                              // length(isect_pos - position)
-    return make_ray(w.pos + ldir * eps, ldir);
+    return make_ray(pos + ldir * eps, ldir);
 }
 
 // a shadow ray ended: add the light's plastic::shade unless occluded (select(active, clr, 0))
 __device__ inline void whitted_light_done(const shade_params& S, whitted_lane& w, bool occluded)
 {
-    const f3 c = occluded ? mk3(0.0f, 0.0f, 0.0f) : plastic_shade(S.materials[w.mi], w.n, w.view, w.pos, S.lights[w.li]);
-    w.shaded = w.shaded + c;
+    const f3 c = occluded ? mk3(0.0f, 0.0f, 0.0f)
+               : plastic_shade(S.materials[w.mi], w.ld3(WL_N), w.ld3(WL_VIEW), w.ld3(WL_POS), S.lights[w.li]);
+    w.st3(WL_SHADED, w.ld3(WL_SHADED) + c);
     w.li += 1u;
 }
 
