@@ -512,6 +512,166 @@ __device__ inline void walk(vrh_scene_view const& b, Ray const& ray, float max_t
     else walk_slab<false>(b, r, max_t, cull_t, leaf);
 }
 
+// Shared any-hit walk (VRH_USER_ANYHIT_SHARE=1).  A user kernel calls any_hit from one thread per
+// pixel, and the wave runs each call until its slowest lane is done: on the AO lambda (C3) 55 % of
+// the lane-steps of the any_hit calls are idle lanes waiting (CPU replay of sampled tiles).  Here the
+// lanes that called any_hit together share the work: a lane whose ray is done (miss, or another
+// lane found its hit) takes the oldest stack entry -- the largest unvisited subtree -- of a lane
+// still traversing, with that lane's ray, and walks it; whoever finds a hit for a ray ends it for
+// every lane working on it, and the ray's owner receives that lane's hit record.  The hit / miss
+// answer is exactly the reference's: before its first accepted hit an any-hit ray's box tests
+// compare against constants (best_t = max(), its max_t), so the set of leaves it can reach does not
+// depend on the order in which they are visited (the argument of vrh_device.h's 4-wide records).
+// WHICH hit a ray reports may differ from the reference's first one in its traversal order (the
+// reference's own SIMD packets already report other first hits than its scalar path), so this is
+// opt-in.  The stack is a ring of VRH_USER_STACK entries (pops at the top, steals at the bottom);
+// a lane never holds more live entries than the BVH is deep (checked_ref).
+#ifndef VRH_USER_ANYHIT_SHARE
+#define VRH_USER_ANYHIT_SHARE 0
+#endif
+
+// position of the n-th set bit (n from 0) of m, for n < popcount(m)
+__device__ __forceinline__ uint32_t nth_bit(uint64_t m, uint32_t n)
+{
+    uint32_t p = 0;
+#pragma unroll
+    for (uint32_t w = 32; w; w >>= 1)
+    {
+        const uint32_t c = (uint32_t)__popcll(m & ((1ull << w) - 1ull));
+        if (n >= c) { n -= c; m >>= w; p += w; }
+    }
+    return p;
+}
+
+// leaf2(ray, max_t, i, flags, rec): test primitive i for `ray` into the record `rec` (update_if),
+// true = rec holds the hit that ends the ray
+template <bool FAST, typename RT, typename Leaf2>
+__device__ inline void walk_shared(vrh_scene_view const& b, vrh::dev::ray_t const& r0, float max_t0, RT& result, Leaf2&& leaf2)
+{
+    using namespace vrh::dev;
+    static_assert(sizeof(RT) % 4 == 0 && std::is_trivially_copyable<RT>::value, "hit record words move between lanes");
+    constexpr uint32_t CAP = VRH_USER_STACK, NOTASK = 0xFFFFFFFFu;
+    constexpr uint32_t RW = sizeof(RT) / 4;
+    extern __shared__ uint32_t vrh_user_smem[];
+    const float4* pairs = static_cast<const float4*>(b.pairs);
+    const uint32_t nthreads = blockDim.x * blockDim.y * blockDim.z;
+    const uint32_t tid = threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z);
+    const uint32_t lane = __lane_id();
+    auto slot = [&](uint32_t k) -> uint32_t& { return vrh_user_smem[tid + (k % CAP) * nthreads]; };
+    uint32_t task = lane;                 // the lane whose ray this lane traverses (NOTASK: idle)
+    ray_t tr = r0;
+    float tmax = max_t0;
+    uint32_t bot = 0, top = 0;            // live stack entries [bot, top) of the ring
+    slot(top++) = b.root;
+    uint64_t found = 0ull;                // lanes whose ray has its hit (wave-uniform)
+    for (;;)
+    {
+        if (task != NOTASK && ((found >> task) & 1ull)) task = NOTASK;
+        if (task != NOTASK && top == bot) task = NOTASK;
+        const uint64_t busy = __ballot(task != NOTASK);
+        if (busy == 0ull) break;
+        // 1. idle lanes take the bottom entry of a lane with two or more (k-th idle <- k-th donor):
+        //    the donor writes that entry and its ray into the idle lane's LDS column (an idle lane's
+        //    stack is empty), which the idle lane then reads -- no cross-lane register traffic
+        const uint64_t idle = __ballot(task == NOTASK);
+        const uint64_t donors = __ballot(task != NOTASK && top - bot >= 2u);
+        if (idle != 0ull && donors != 0ull)
+        {
+            const uint32_t n = min((uint32_t)__popcll(idle), (uint32_t)__popcll(donors));
+            const uint32_t dr = (uint32_t)__popcll(donors & ((1ull << lane) - 1ull));
+            if (((donors >> lane) & 1ull) && dr < n)
+            {
+                uint32_t* c = vrh_user_smem + (tid - lane + nth_bit(idle, dr));
+                c[0] = __float_as_uint(tr.ori.x); c[nthreads] = __float_as_uint(tr.ori.y); c[2 * nthreads] = __float_as_uint(tr.ori.z);
+                c[3 * nthreads] = __float_as_uint(tr.dir.x); c[4 * nthreads] = __float_as_uint(tr.dir.y); c[5 * nthreads] = __float_as_uint(tr.dir.z);
+                c[6 * nthreads] = __float_as_uint(tr.inv.x); c[7 * nthreads] = __float_as_uint(tr.inv.y); c[8 * nthreads] = __float_as_uint(tr.inv.z);
+                c[9 * nthreads] = __float_as_uint(tmax); c[10 * nthreads] = task; c[11 * nthreads] = slot(bot++);
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            const uint32_t ir = (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+            if (((idle >> lane) & 1ull) && ir < n)
+            {
+                const uint32_t* c = vrh_user_smem + tid;
+                tr.ori = mk3(__uint_as_float(c[0]), __uint_as_float(c[nthreads]), __uint_as_float(c[2 * nthreads]));
+                tr.dir = mk3(__uint_as_float(c[3 * nthreads]), __uint_as_float(c[4 * nthreads]), __uint_as_float(c[5 * nthreads]));
+                tr.inv = mk3(__uint_as_float(c[6 * nthreads]), __uint_as_float(c[7 * nthreads]), __uint_as_float(c[8 * nthreads]));
+                tmax = __uint_as_float(c[9 * nthreads]);
+                task = c[10 * nthreads];
+                bot = 11u; top = 12u;                         // the entry is ring slot 11
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        // 2. one descent (pop, down to a leaf or a miss) and the leaf's primitives
+        bool hit = false;
+        RT rec;
+        if (task != NOTASK)
+        {
+            uint32_t link = slot(--top);
+            bool at_leaf = true;
+            while (!(link & LEAF_BIT))
+            {
+                float4 q0, q1, q2;
+                float2 q3;
+                fetch_pair(pairs, link, q0, q1, q2, q3);
+                bool b0, b1;
+                float tn0, tn1;
+                box_pair<FAST>(q0, q1, q2, tr, FMAX, tmax, b0, b1, tn0, tn1);
+                const uint32_t l0 = __float_as_uint(q3.x), l1 = __float_as_uint(q3.y);
+                if (!(b0 | b1)) { at_leaf = false; break; }
+                const bool go0 = (b0 & b1) ? (tn0 < tn1) : b0;                 // ties -> child 1
+                if (b0 & b1) slot(top++) = go0 ? l1 : l0;
+                link = go0 ? l0 : l1;
+            }
+            if (at_leaf)
+                for (uint32_t i = link & ~LEAF_BIT;; ++i)
+                {
+                    uint32_t flags = 0;
+                    if (leaf2(tr, tmax, i, flags, rec)) { hit = true; break; }
+                    if (flags & END_BIT) break;
+                }
+        }
+        // 3. a hit ends its ray on every lane; the ray's owner takes the record of the lowest lane
+        //    that found one in this step
+        uint64_t hl = __ballot(hit);
+        if (hl != 0ull)
+        {
+            uint32_t winner = NOTASK;
+            while (hl != 0ull)
+            {
+                const uint32_t l = (uint32_t)__builtin_ctzll(hl);
+                hl &= hl - 1ull;
+                const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)task, (int)l);
+                if (!((found >> o) & 1ull))
+                {
+                    found |= 1ull << o;
+                    if (lane == o) winner = l;
+                }
+            }
+            // the winner's stack is dead (its ray ended): its record goes to the first words of its
+            // own LDS column, where the owner reads it
+            if (hit)
+            {
+                uint32_t w[RW];
+                __builtin_memcpy(w, &rec, sizeof(RT));
+#pragma unroll
+                for (uint32_t k = 0; k < RW; ++k) vrh_user_smem[tid + k * nthreads] = w[k];
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            if (winner != NOTASK)
+            {
+                uint32_t got[RW];
+#pragma unroll
+                for (uint32_t k = 0; k < RW; ++k) got[k] = vrh_user_smem[tid - lane + winner + k * nthreads];
+                __builtin_memcpy(&result, got, sizeof(RT));
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (hit) task = NOTASK;
+        }
+    }
+}
+
 template <typename It>
 using range_value_t = typename std::decay<decltype(*std::declval<It>())>::type;
 template <typename It>
@@ -576,6 +736,29 @@ VRH_FUNC inline auto intersect(
     using RT = typename detail::traversal_result<HR, Traversal, MultiHitMax>::type;
     RT result;
     const float4* prims = static_cast<const float4*>(b.view.prims);
+    if constexpr (Traversal == detail::AnyHit && VRH_USER_ANYHIT_SHARE)
+    {
+        // the shared any-hit walk (hip_detail::walk_shared): the same leaf step on the ray being
+        // traversed, into the record of this visit
+        if (b.view.max_depth >= VRH_USER_STACK) return result;
+        const vrh::dev::ray_t r = hip_detail::dev_ray(ray);
+        auto leaf2 = [&](vrh::dev::ray_t const& tr, float tmax, uint32_t i, uint32_t& flags, RT& rec) -> bool
+        {
+            const basic_ray<float> ray2(vector<3, float>(tr.ori.x, tr.ori.y, tr.ori.z), vector<3, float>(tr.dir.x, tr.dir.y, tr.dir.z));
+            const P prim = hip_detail::leaf_primitive<P>(prims, i, flags);
+            auto hr = HR(isect(ray2, prim), int(i));
+            auto closer = update_cond(hr, rec, tmax);
+            if (!any(closer)) return false;
+            update_if(rec, hr, closer);
+            detail::exit_traversal<Traversal> early_exit;
+            return early_exit.check(rec);
+        };
+        if (b.view.finite_bounds && __ballot(!vrh::dev::finite_ray(r)) == 0ull)
+            hip_detail::walk_shared<true>(b.view, r, max_t, result, leaf2);
+        else
+            hip_detail::walk_shared<false>(b.view, r, max_t, result, leaf2);
+        return result;
+    }
     hip_detail::walk<Traversal == detail::AnyHit>(b.view, ray, max_t, [&]() { return hip_detail::cull_of(result); },
                      [&](uint32_t i, uint32_t& flags) -> bool
                      {
@@ -624,6 +807,24 @@ __device__ inline bvh_record traverse_bvh(basic_ray<float> const& ray, vrh_scene
     using HR = prim_record;
     bvh_record result;
     const float4* prims = static_cast<const float4*>(b.prims);
+    if constexpr (Any && VRH_USER_ANYHIT_SHARE)
+    {
+        if (b.max_depth >= VRH_USER_STACK) return result;
+        const vrh::dev::ray_t r = dev_ray(ray);
+        auto leaf2 = [&](vrh::dev::ray_t const& tr, float tmax, uint32_t i, uint32_t& flags, bvh_record& rec) -> bool
+        {
+            const basic_ray<float> ray2(vec3(tr.ori.x, tr.ori.y, tr.ori.z), vec3(tr.dir.x, tr.dir.y, tr.dir.z));
+            HR hr;
+            if (b.prim_kind == VRH_PRIM_TRI64) hr = isect(ray2, leaf_primitive<basic_triangle<3, float>>(prims, i, flags));
+            else hr = isect(ray2, leaf_primitive<basic_sphere<float>>(prims, i, flags));
+            if (!is_closer(hr, static_cast<HR const&>(rec), tmax)) return false;
+            rec = bvh_record(hr, i);
+            return true;                                      // exit_traversal.h:49-56
+        };
+        if (b.finite_bounds && __ballot(!vrh::dev::finite_ray(r)) == 0ull) walk_shared<true>(b, r, max_t, result, leaf2);
+        else walk_shared<false>(b, r, max_t, result, leaf2);
+        return result;
+    }
     // the leaf: every primitive in index order, is_closer / update_if (intersect.inl:103-128)
     walk<Any>(b, ray, max_t, [&]() { return result.t; },
          [&](uint32_t i, uint32_t& flags) -> bool

@@ -15,12 +15,13 @@ tests/cpp/user_kernels.hip (built by visionaray_amd/Makefile `cpp_tests`) render
 """
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BIN = os.path.join(ROOT, "build", "tests", "user_kernels")
+BIN = os.environ.get("VRH_USER_BIN") or os.path.join(ROOT, "build", "tests", "user_kernels")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 GRID = {"hf64": 64, "hf200": 200}
 
@@ -43,6 +44,22 @@ def _check_hashes(oracle_mod, got, g, keys):
 @pytest.mark.gpu
 @pytest.mark.parametrize("case,frame", [("hf200_320x180", 0), ("frame1_hf200_320x180", 1)])
 def test_user_ao_kernel_matches_reference(tmp_path, golden, oracle_mod, case, frame):
+    g = golden[case]
+    got = _run(tmp_path, "ao", g["scene"], g["W"], g["H"], frame)
+    _check_hashes(oracle_mod, got, g, [("prim_id", "primid_hash"), ("t", "t_hash"), ("occ", "occ_hash"),
+                                       ("color", "color_hash")])
+
+
+SHARE_BIN = os.path.join(ROOT, "build", "tests", "uk_share")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,frame", [("hf200_320x180", 0), ("frame1_hf200_320x180", 1)])
+def test_user_ao_kernel_shared_anyhit_matches_reference(tmp_path, golden, oracle_mod, case, frame, monkeypatch):
+    """VRH_USER_ANYHIT_SHARE=1: idle lanes walk subtrees of other lanes' any-hit rays; every ray's
+    hit / miss -- so every AO mask and colour -- is still the reference's."""
+    assert os.path.exists(SHARE_BIN), "run __graft_entry__.build() (make -C visionaray_amd cpp_tests)"
+    monkeypatch.setattr(sys.modules[__name__], "BIN", SHARE_BIN)
     g = golden[case]
     got = _run(tmp_path, "ao", g["scene"], g["W"], g["H"], frame)
     _check_hashes(oracle_mod, got, g, [("prim_id", "primid_hash"), ("t", "t_hash"), ("occ", "occ_hash"),
