@@ -75,3 +75,33 @@ def test_whitted_zero_bounces_is_black(ctx, oracle_mod):
     hit = out["prim_id"] != 0xFFFFFFFF
     assert hit.any()
     assert np.array_equal(out["color"][hit], np.tile([0.0, 0.0, 0.0, 1.0], (int(hit.sum()), 1)).astype(np.float32))
+
+
+@pytest.mark.parametrize("occ", [0, 1])
+def test_whitted_frames_in_flight_equal_single_frames(ctx, oracle_mod, occ):
+    """whitted::kernel with three frames in one launch (vrh_render_batch, as hip_sched::frames): every
+    frame bit-identical to its own single-frame render -- at the default 5 waves/SIMD (the bounce
+    surface in LDS after the stack) and at 4 (waves_per_simd 1)."""
+    O = oracle_mod
+    name, W, H = "hfstack32x24", 96, 64
+    dev = product_scene(ctx, O, name)
+    m, lt, amb, bg = O.whitted_spec()
+    sh = va.shading(ctx, m.view(va.PLASTIC_DTYPE), lt.view(va.POINT_LIGHT_DTYPE))
+    k = va.whitted_kernel(dev, sh, bg=bg, ambient=amb, num_bounces=4, epsilon=1e-3)
+    cam = camera_of(O, name, W, H)
+    ctx.set_option("waves_per_simd", occ)
+    try:
+        one = va.hip_buffer_rt(ctx, W, H)
+        va.render(ctx, dev, one, cam, k)
+        single = one.download()
+        three = va.hip_buffer_rt(ctx, W, 3 * H)
+        va.render_batch(ctx, dev, three, [cam] * 3, k)
+        got = three.download()
+    finally:
+        ctx.set_option("waves_per_simd", 0)
+    assert (single["prim_id"] != 0xFFFFFFFF).any()
+    n = W * H
+    for f in range(3):
+        for key in ("prim_id", "t", "color"):
+            a, b = got[key][f * n:(f + 1) * n], single[key]
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (f, key)

@@ -2,7 +2,10 @@
 and multi_hit<16> at 1080p on hf1M, rays/s from the device counters over K timed frames, for each
 waves-per-SIMD register budget.  Prints one JSON line per (kernel, occ).
 
-    python tools/shade_bench.py [--scene hf1M] [--frames 10]
+    python tools/shade_bench.py [--scene hf1M] [--frames 10] [--frames-per-launch F]
+
+--frames-per-launch F > 1: the frames run as frames/F persistent launches of F frames each
+(vrh_render_batch, frames in flight, as hip_sched::frames) instead of one hip_sched::frame each.
 """
 import argparse
 import json
@@ -18,6 +21,7 @@ def main():
     ap.add_argument("--scene", default="hf1M")
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--occ", default="0,1,6,8")
+    ap.add_argument("--frames-per-launch", type=int, default=1)
     ap.add_argument("--variants", default=None,
                     help='JSON list of option dicts, e.g. [{"pop_on_miss": 1, "descent_cap": 8}] (replaces --occ)')
     a = ap.parse_args()
@@ -53,6 +57,18 @@ def main():
     }
     sched = va.hip_sched(ctx)
     sp = va.make_sched_params(va.pixel_sampler.uniform_type, cam, rt)
+    F = a.frames_per_launch
+    if F > 1:
+        assert a.frames % F == 0, "--frames must be a multiple of --frames-per-launch"
+        rtF = va.hip_buffer_rt(ctx, W, H * F)
+        rtF.alloc_multi_hit(16)
+        basis = cam.basis(W, H)
+
+    def launch(k, n):
+        if F == 1:
+            sched.frame(k, sp, sync=False)
+        else:
+            va.render_batch(ctx, dev, rtF, [basis] * F, k, None, frame_num=n)
     variants = json.loads(a.variants) if a.variants else [{"waves_per_simd": int(x)} for x in a.occ.split(",")]
     for name, k in kernels.items():
         for v in variants:
@@ -60,18 +76,20 @@ def main():
                 ctx.set_option(opt, val)
             occ = v.get("waves_per_simd", 0)
             try:
-                for _ in range(2):
-                    sched.frame(k, sp)
+                for i in range(2):
+                    launch(k, i)
+                    ctx.sync()
                 ctx.stats_reset()
                 ctx.sync()
                 t0 = time.perf_counter()
-                for _ in range(a.frames):
-                    sched.frame(k, sp, sync=False)
+                for i in range(a.frames // F):
+                    launch(k, i)
                 ctx.sync()
                 dt = time.perf_counter() - t0
                 st = ctx.accum_stats()
                 rays = int(st["rays"])
                 print(json.dumps({"kernel": name, "occ": occ, "options": v, "scene": a.scene, "W": W, "H": H,
+                                  "frames_per_launch": F,
                                   "ms_per_frame": round(dt / a.frames * 1e3, 3),
                                   "rays_per_frame": rays // a.frames,
                                   "Mrays_per_s": round(rays / dt / 1e6, 1)}), flush=True)
