@@ -20,6 +20,7 @@ within the north star's 1e-5 relative (device powf), hit lists bit-exact.
 """
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -57,9 +58,14 @@ def test_random_sampler_draws_bit_exact(tmp_path, golden, oracle_mod, case):
 @pytest.mark.gpu
 @needs_bin
 @pytest.mark.parametrize("case", ["rs_hf64_160x90_f0", "rs_hf200_320x180_f3", "rs_hf1M_f1"])
-def test_reference_ao_kernel_on_hip_sched(tmp_path, golden, oracle_mod, case):
+@pytest.mark.parametrize("share", [False, True])
+def test_reference_ao_kernel_on_hip_sched(tmp_path, golden, oracle_mod, case, share, monkeypatch):
     """ao/main.cpp's kernel, compiled from the reference's headers by hipcc: hits and t bit-exact, the
-    AO count equal on >= 99.9 % of the pixels (device vs host libm sin / cos)."""
+    AO count equal on >= 99.9 % of the pixels (device vs host libm sin / cos).  share: the build with
+    the shared any-hit walk (VRH_USER_ANYHIT_SHARE=1, oracle/_ref/ref_kernels_share)."""
+    if share:
+        assert os.path.exists(BIN + "_share"), "oracle/Makefile builds ref_kernels_share next to ref_kernels"
+        monkeypatch.setattr(sys.modules[__name__], "BIN", BIN + "_share")
     g = golden[case]
     ref = np.load(os.path.join(GOLDEN, case + ".npz"))
     out = _run(tmp_path, "ao", g["scene"], g["W"], g["H"], g["frame"])
