@@ -260,6 +260,11 @@ enum vrh_option {
                                     2 = off, 3 = on with the entries in cut order (auto: on)      */
     VRH_OPT_AO_STEAL = 21,       /* removed in round 3 (the AO tail stash measured slower, DESIGN.md
                                     "Negative results"): 0 / 2 accepted, 1 -> VRH_ERR_UNSUPPORTED  */
+    VRH_OPT_AO_SHARE = 22,       /* AO step loop, tail sharing: once the tile queues are dry, a wave's
+                                    last tile's AO rays are handed out through an LDS counter that
+                                    idle waves of the same block claim from (blocks of 4 waves):
+                                    1 = on, 2 = off (auto: off -- measured 2-3 % slower on one-frame
+                                    C3 / C4 launches, profiles/r03_ab/ao_share/)                    */
     VRH_OPT_PAIR_LAYOUT = 15,    /* scene upload (read by vrh_scene_upload): 1 = node pairs in
                                     depth-first preorder, a pair's child-0 pair next to it in one
                                     128-B line; 2 = the builder's order (auto: 2; 1 measured

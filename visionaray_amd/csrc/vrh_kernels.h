@@ -77,6 +77,7 @@ struct render_params
     uint32_t ao_cut;          // AO step loop: any-hit rays start at the tile's cut of the 4-wide tree
                               // (1: entries in cut order, 2: nearest-first)
     uint32_t ao_gate;         // AO step loop: a tile's AO rays are handed out once its primaries are done
+    uint32_t ao_share;        // AO step loop, blocks of several waves: tail sharing of the last tiles' AO rays
     unsigned long long* wave_times;   // VRH_OPT_WAVE_TIMES: per wave (start, end) of wall_clock64(), else null
     // VRH_OPT_WAVE_TIMES = 2, counting kernels of one-frame AO launches: per tile (hand-out, primaries
     // done, pixels written) of wall_clock64() -- where a launch's tail comes from
@@ -112,6 +113,7 @@ struct launch_config
     int epi;           // primary epilogue: 0 plain, 1 VRH_KERNEL_SIMPLE, 2 VRH_KERNEL_MULTI_HIT, 3 VRH_KERNEL_WHITTED (triangles)
     int max_hits;      // MULTI_HIT: N (LDS hit lists)
     bool spill;        // the traversal stack continues in a global overflow block (render_unified_kernel<..., SPILL>)
+    bool share;        // AO tail sharing (render_unified_kernel<..., SHARE>): one-frame AO launches at 5 waves / SIMD
 };
 
 size_t render_lds_bytes(const launch_config& c);

@@ -48,7 +48,19 @@ constexpr int AO_CUT = AO_SLOT_PX + 2 * 64 / 4;         // the current tile's en
 #define VRH_AO_CUT_MAX 8
 #endif
 constexpr uint32_t CUT_MAX = VRH_AO_CUT_MAX;            // records of a cut
-constexpr int AO_WAVE_WORDS = AO_CUT + 2 * 8 * CUT_MAX; // two levels x entries of box lo xyz, hi xyz, link, pad
+constexpr int AO_SH = AO_CUT + 2 * 8 * CUT_MAX;        // two levels x entries of box lo xyz, hi xyz, link, pad
+// Tail sharing (render_params::ao_share, blocks of several waves): once the tile queues are dry, a
+// wave publishes its last tile's AO rays in a header of its LDS area and hands them out through an
+// LDS counter, so idle sibling waves of the block trace some of them.  Header words: the published
+// tile (NONE: none), its buffer parity, the next AO ray to hand out (LDS atomic), the tile's AO rays,
+// rays in flight on sibling waves (LDS atomic), the tile's cut size; word SH_DRY of wave 0: the block
+// has seen the queues run dry.
+constexpr int AO_WAVE_WORDS = AO_SH + 8;
+constexpr uint32_t SH_TILE = 0, SH_PAR = 1, SH_NEXT = 2, SH_AVAIL = 3, SH_HELP = 4, SH_CUTN = 5, SH_DRY = 6;
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // tile id (next_tile: frame f << TILE_FRAME_SHIFT | tile of that frame) -> (x, y) of lane, plus the
 // output row (frame f's rows start at f * frame_rows; packed shards).  A band is one row of tiles.
@@ -487,7 +499,7 @@ __device__ __forceinline__ int list_next(const render_params& P, bool any, uint3
 // frames in flight) so that profiles tell them apart from one-frame launches (hip_sched::frame).
 // SPILL: the traversal stack may continue in the global overflow block (stack_t<true>).
 template <int KIND, bool AO, bool COUNT, int OCC, int EPI = 0, bool LIST = false, bool BATCH = false, bool SPILL = false,
-          bool SAMPLED = false>
+          bool SAMPLED = false, bool SHARE = false>
 __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params P)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -710,10 +722,25 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         uint8_t* slot_px = reinterpret_cast<uint8_t*>(ao_area + AO_SLOT_PX);
         float* cut = reinterpret_cast<float*>(ao_area + AO_CUT);
         uint32_t cutN = NONE;                                 // entries of tile C's cut (NONE: root)
+        uint32_t* const ao_base = smem + P.stack_cap * block; // wave w's AO area: ao_base + w * AO_WAVE_WORDS
+        uint32_t* const sh = ao_area + AO_SH;
+        const uint32_t nwaves = block >> 6;
+        const bool share = SHARE && !LIST && P.ao_share && nwaves > 1u;
+        bool shC = false, shD = false;                        // tile C / D published to the sibling waves
+        uint32_t* const dry = ao_base + AO_SH + SH_DRY;       // wave 0's word: the block saw the queues dry
+        if (share)
+        {
+            if (lane == 0u) { sh[SH_TILE] = NONE; sh[SH_HELP] = 0u; sh[SH_NEXT] = 0u; sh[SH_AVAIL] = 0u; sh[SH_DRY] = 0u; }
+            __syncthreads();
+        }
+        auto mark_dry = [&](uint32_t tile) {
+            if (share && tile == NONE && lane == 0u) __hip_atomic_store(dry, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        };
         const float4 bg = make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
         tile_queue tq = queue_init(P);
         // wave-uniform tile state
         uint32_t tileC = next_tile(P, tq, lane), parC = 0;
+        mark_dry(tileC);
         // tile timeline (counting instance only): [3 t] hand-out, [3 t + 1] primaries done, [3 t + 2] written
         auto tile_mark = [&](uint32_t id, uint32_t k) {
             if constexpr (COUNT)
@@ -723,15 +750,54 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         uint32_t handedC = 0, pendC = 0, pubC = 0, issC = 0;  // primaries handed / in flight, slots, AO rays handed
         uint32_t tileD = NONE, parD = 0, slotsD = 0;
         uint32_t inflight0 = 0, inflight1 = 0;                // AO rays in flight per buffer parity
-        // lane state: PRIMARY tag = pixel lane k of tile C; AORAY tag = slot | s << 6 | parity << 11
+        // lane state: PRIMARY tag = pixel lane k of tile C; AORAY tag = slot | s << 6 | parity << 11 |
+        // owner wave << 12 (the wave whose tile the ray belongs to: this one unless it helps a sibling)
         uint32_t tag = 0;
+        // AO ray `cand` (slot-major: slot cand / S, sample cand % S) of the tile `tile` whose hit records,
+        // slot pixels and cut are recs_ / spx / cut_, cutn (this wave's, or a sibling's it helps)
+        auto start_ao = [&](const float* recs_, const uint8_t* spx, const float* cut_, uint32_t cutn, uint32_t tile,
+                            uint32_t par, uint32_t cand, uint32_t owner) {
+            const uint32_t slot = cand / S, smp = cand - slot * S;
+            uint32_t x, y, orow, fr;
+            tile_pixel(P, tile, spx[par * 64u + slot], x, y, orow, fr);
+            r = ao_ray<COUNT>(P, recs_, slot, smp, y * P.width + x, fr, cnt);
+            best_t = FMAX; best_prim = 0; steps = 0; max_t = P.radius; any = true;
+            bk = 0; res_t = FMAX; res_prim = 0;
+            finite = finite_ray(r);
+            quad = P.quad_ok && finite;
+            st.reset(); resume = NO_RESUME;
+            if (!LIST && (!SPILL || VRH_AO_CUT_SPILL) && VRH_AO_CUT && quad && cutn != NONE)
+            {
+                // start at the tile's cut: the entries whose boxes this ray passes
+#pragma unroll 1
+                for (uint32_t j = 0; j < cutn; ++j)
+                {
+                    // quad_entry's test, one axis at a time (max / min of non-NaN values
+                    // are exact in any order: the same tn / tf, fewer live registers)
+                    const float* e = cut_ + 8u * j;
+                    float t1 = (e[0] - r.ori.x) * r.inv.x, t2 = (e[3] - r.ori.x) * r.inv.x;
+                    float tn = __builtin_fminf(t1, t2), tf = __builtin_fmaxf(t1, t2);
+                    t1 = (e[1] - r.ori.y) * r.inv.y; t2 = (e[4] - r.ori.y) * r.inv.y;
+                    tn = __builtin_fmaxf(tn, __builtin_fminf(t1, t2)); tf = __builtin_fminf(tf, __builtin_fmaxf(t1, t2));
+                    t1 = (e[2] - r.ori.z) * r.inv.z; t2 = (e[5] - r.ori.z) * r.inv.z;
+                    tn = __builtin_fmaxf(tn, __builtin_fminf(t1, t2)); tf = __builtin_fminf(tf, __builtin_fmaxf(t1, t2));
+                    if ((tf >= tn) & (tn < FMAX) & (tf >= 0.0f) & (tn < max_t)) st.push(__float_as_uint(e[6]));
+                }
+                if (COUNT) cnt.box += cutn;
+            }
+            else
+                st.push(quad ? 0u : P.root);
+            mode = AORAY;
+            tag = slot | (smp << 6) | (par << 11) | (SHARE ? owner << 12 : 0u);
+            rays_total += 1;
+        };
         for (;;)
         {
             // 1. the draining tile is done when its last AO ray is: write its hit pixels
-            if (tileD != NONE && (parD ? inflight1 : inflight0) == 0u)
+            if (tileD != NONE && (parD ? inflight1 : inflight0) == 0u && (!shD || lds_ld(&sh[SH_HELP]) == 0u))
             {
                 __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // the siblings' mask bits
                 if (lane < slotsD)
                 {
                     const uint32_t k = slot_px[parD * 64u + lane];
@@ -750,12 +816,16 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 __builtin_amdgcn_wave_barrier();
                 tile_mark(tileD, 2u);
                 tileD = NONE;
+                if (shD && lane == 0u) __hip_atomic_store(&sh[SH_TILE], NONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                shD = false;
             }
             // 2. the current tile has handed out all its rays: it drains, the next tile starts
             if (tileC != NONE && tileD == NONE && handedC >= 64u && pendC == 0u && issC >= pubC * S)
             {
                 tileD = tileC; parD = parC; slotsD = pubC;
+                shD = shC; shC = false;
                 tileC = next_tile(P, tq, lane);
+                mark_dry(tileC);
                 tile_mark(tileC, 0u);
                 parC ^= 1u;
                 handedC = 0; pendC = 0; pubC = 0; issC = 0;
@@ -782,45 +852,31 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                         cutN = ao_cut_build<COUNT>(P, recs, pubC, cut, lane, cnt);
                         if (cutN != NONE && cutN + 4u > P.stack_cap) cutN = NONE;
                     }
-                const uint32_t cand = issC + lane_rank(idle);
-                const uint32_t n = min(avail - issC, (uint32_t)__popcll(idle));
-                if (mode == IDLE && cand < avail)
+                // once the block's queues are dry, the tile's AO rays are handed out through the LDS
+                // counter of its header, which idle sibling waves claim from too (step 3b)
+                if (share && !shC && lds_ld(dry) != 0u)
                 {
-                    const uint32_t slot = cand / S, smp = cand - slot * S;
-                    uint32_t x, y, orow, fr;
-                    tile_pixel(P, tileC, slot_px[parC * 64u + slot], x, y, orow, fr);
-                    r = ao_ray<COUNT>(P, recs, slot, smp, y * P.width + x, fr, cnt);
-                    best_t = FMAX; best_prim = 0; steps = 0; max_t = P.radius; any = true;
-                    bk = 0; res_t = FMAX; res_prim = 0;
-                    finite = finite_ray(r);
-                    quad = P.quad_ok && finite;
-                    st.reset(); resume = NO_RESUME;
-                    if (!LIST && (!SPILL || VRH_AO_CUT_SPILL) && VRH_AO_CUT && quad && cutN != NONE)
+                    if (lane == 0u)
                     {
-                        // start at the tile's cut: the entries whose boxes this ray passes
-#pragma unroll 1
-                        for (uint32_t j = 0; j < cutN; ++j)
-                        {
-                            // quad_entry's test, one axis at a time (max / min of non-NaN values
-                            // are exact in any order: the same tn / tf, fewer live registers)
-                            const float* e = cut + 8u * j;
-                            float t1 = (e[0] - r.ori.x) * r.inv.x, t2 = (e[3] - r.ori.x) * r.inv.x;
-                            float tn = __builtin_fminf(t1, t2), tf = __builtin_fmaxf(t1, t2);
-                            t1 = (e[1] - r.ori.y) * r.inv.y; t2 = (e[4] - r.ori.y) * r.inv.y;
-                            tn = __builtin_fmaxf(tn, __builtin_fminf(t1, t2)); tf = __builtin_fminf(tf, __builtin_fmaxf(t1, t2));
-                            t1 = (e[2] - r.ori.z) * r.inv.z; t2 = (e[5] - r.ori.z) * r.inv.z;
-                            tn = __builtin_fmaxf(tn, __builtin_fminf(t1, t2)); tf = __builtin_fminf(tf, __builtin_fmaxf(t1, t2));
-                            if ((tf >= tn) & (tn < FMAX) & (tf >= 0.0f) & (tn < max_t)) st.push(__float_as_uint(e[6]));
-                        }
-                        if (COUNT) cnt.box += cutN;
+                        sh[SH_PAR] = parC; sh[SH_NEXT] = issC; sh[SH_AVAIL] = avail; sh[SH_CUTN] = cutN; sh[SH_HELP] = 0u;
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        __hip_atomic_store(&sh[SH_TILE], tileC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
-                    else
-                        st.push(quad ? 0u : P.root);
-                    mode = AORAY;
-                    tag = slot | (smp << 6) | (parC << 11);
-                    rays_total += 1;
+                    shC = true;
                 }
-                issC += n;
+                uint32_t base = issC;
+                const uint32_t want = (uint32_t)__popcll(idle);
+                if (shC)
+                {
+                    uint32_t b = 0u;
+                    if (lane == 0u) b = atomicAdd(&sh[SH_NEXT], want);
+                    base = uu((uint32_t)__shfl((int)b, 0));
+                }
+                const uint32_t cand = base + lane_rank(idle);
+                const uint32_t n = base < avail ? min(avail - base, want) : 0u;
+                if (mode == IDLE && cand < avail)
+                    start_ao(recs, slot_px, cut, cutN, tileC, parC, cand, wave);
+                issC = shC ? min(avail, base + want) : issC + n;
                 if (parC) inflight1 += n; else inflight0 += n;
                 idle = __ballot(mode == IDLE);
             }
@@ -844,6 +900,45 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 }
                 pendC += (uint32_t)__popcll(__ballot(started));
             }
+            // 3b. nothing of its own left to hand out once the queues are dry: idle lanes claim AO
+            //     rays of a sibling wave's published tile (their occlusion bits go to the sibling's
+            //     masks, the sibling writes the pixels once its helpers' rays are done)
+            if (share && tileC == NONE)
+            {
+                uint64_t hidle = __ballot(mode == IDLE);
+                if (hidle != 0ull && ((uint32_t)__popcll(hidle) >= P.refill_min || hidle == ~0ull))
+                {
+#pragma unroll 1
+                    for (uint32_t k = 1; k < nwaves && hidle != 0ull; ++k)
+                    {
+                        const uint32_t o = (wave + k) % nwaves;
+                        uint32_t* const ao_o = ao_base + o * AO_WAVE_WORDS;
+                        uint32_t* const so = ao_o + AO_SH;
+                        const uint32_t t = uu(lds_ld(&so[SH_TILE]));
+                        if (t == NONE) continue;
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // the header words
+                        const uint32_t avail = uu(lds_ld(&so[SH_AVAIL]));
+                        if (uu(lds_ld(&so[SH_NEXT])) >= avail) continue;
+                        const uint32_t want = (uint32_t)__popcll(hidle);
+                        uint32_t b = 0u;
+                        if (lane == 0u)
+                        {
+                            atomicAdd(&so[SH_HELP], want);            // before the claim: the owner waits
+                            b = atomicAdd(&so[SH_NEXT], want);
+                        }
+                        b = uu((uint32_t)__shfl((int)b, 0));
+                        const uint32_t got = b < avail ? min(avail - b, want) : 0u;
+                        if (lane == 0u && got < want) atomicSub(&so[SH_HELP], want - got);
+                        if (got == 0u) continue;
+                        const uint32_t rk = lane_rank(hidle);
+                        if (mode == IDLE && rk < got)
+                            start_ao(reinterpret_cast<const float*>(ao_o), reinterpret_cast<const uint8_t*>(ao_o + AO_SLOT_PX),
+                                     reinterpret_cast<const float*>(ao_o + AO_CUT), uu(lds_ld(&so[SH_CUTN])), t,
+                                     uu(lds_ld(&so[SH_PAR])), b + rk, o);
+                        hidle = __ballot(mode == IDLE);
+                    }
+                }
+            }
             const bool busy = mode != IDLE;
             if (__ballot(busy) == 0ull)
             {
@@ -863,9 +958,22 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             if (COUNT) count_wave(cnt, busy);
             // 5. finished AO rays: record occlusion, retire from their tile's in-flight count
             const bool ao_done = mode == AORAY && rc != 0;
-            if (ao_done && rc > 0) atomicOr(&masks[(tag >> 11) * 64u + (tag & 63u)], 1u << ((tag >> 6) & 31u));
-            inflight0 -= (uint32_t)__popcll(__ballot(ao_done && (tag >> 11) == 0u));
-            inflight1 -= (uint32_t)__popcll(__ballot(ao_done && (tag >> 11) != 0u));
+            const uint32_t own = SHARE ? tag >> 12 : wave;    // the wave whose tile the ray belongs to
+            const bool mine = own == wave;
+            uint32_t* const mk = mine ? masks : ao_base + own * AO_WAVE_WORDS + AO_MASKS;
+            if (ao_done && rc > 0) atomicOr(&mk[((tag >> 11) & 1u) * 64u + (tag & 63u)], 1u << ((tag >> 6) & 31u));
+            inflight0 -= (uint32_t)__popcll(__ballot(ao_done && mine && ((tag >> 11) & 1u) == 0u));
+            inflight1 -= (uint32_t)__popcll(__ballot(ao_done && mine && ((tag >> 11) & 1u) != 0u));
+            if (share && __ballot(ao_done && !mine) != 0ull)
+            {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");     // mask bits before the count
+#pragma unroll 1
+                for (uint32_t o = 0; o < nwaves; ++o)
+                {
+                    const uint32_t c = (uint32_t)__popcll(__ballot(ao_done && !mine && own == o));
+                    if (c != 0u && lane == 0u) atomicSub(&ao_base[o * AO_WAVE_WORDS + AO_SH + SH_HELP], c);
+                }
+            }
             // 6. finished primaries: write prim id / t (and a miss's colour), publish hits as slots
             const bool pr_done = mode == PRIMARY && rc != 0;
             const uint64_t fin = __ballot(pr_done);
@@ -1001,8 +1109,20 @@ static kernel_fn pick_spill(bool ao, int occ, int sched)
     return nullptr;
 }
 
+// AO tail sharing instances: one-frame AO launches (sched 0) at the default 5 waves / SIMD, with and
+// without the stack overflow block
+template <int KIND>
+static kernel_fn pick_share(const launch_config& c)
+{
+    if (!c.ao || c.count || c.epi || c.occ != 5 || c.sched != 0) return nullptr;
+    return c.spill ? dev::render_unified_kernel<KIND, true, false, 5, 0, false, false, true, false, true>
+                   : dev::render_unified_kernel<KIND, true, false, 5, 0, false, false, false, false, true>;
+}
+
 static kernel_fn select_variant(const launch_config& c)
 {
+    if (c.share)
+        if (kernel_fn f = c.kind == dev::KIND_TRI ? pick_share<dev::KIND_TRI>(c) : pick_share<dev::KIND_SPHERE>(c)) return f;
     if (c.epi) return c.occ == 8 ? pick_shade<8>(c.count, c.epi) : c.occ == 6 ? pick_shade<6>(c.count, c.epi)
                     : c.occ == 5 ? pick_shade<5>(c.count, c.epi) : pick_shade<1>(c.count, c.epi);
     if (c.spill)

@@ -147,6 +147,7 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
     case VRH_OPT_WAVE_TIMES: VRH_CHECK(value <= 2, "vrh_ctx_set_option: wave times is 1 (on), 2 (on + tile times of counting one-frame AO launches) or 0 (off)"); ctx->opt_wave_times = int(value); break;
     case VRH_OPT_AO_CUT: VRH_CHECK(value <= 3, "vrh_ctx_set_option: AO cut is 1 (on, entries nearest-first), 2 (off) or 3 (on, entries in cut order)"); ctx->opt_cut = int(value); break;
     case VRH_OPT_AO_STEAL: VRH_CHECK(value != 1, "vrh_ctx_set_option: the AO tail stash was removed (it measured slower)"); return VRH_OK;
+    case VRH_OPT_AO_SHARE: VRH_CHECK(value <= 2, "vrh_ctx_set_option: AO tail sharing is 1 (on) or 2 (off)"); ctx->opt_share = int(value); break;
     case VRH_OPT_AO_GATE: VRH_CHECK(value <= 2, "vrh_ctx_set_option: AO gate is 1 (on) or 2 (off)"); ctx->opt_gate = int(value); break;
     case VRH_OPT_POP_ON_MISS: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pop on miss is 1 (on) or 2 (off)"); ctx->opt_pop = int(value); break;
     case VRH_OPT_PAIR_LAYOUT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pair layout is 1 (line pairing) or 2 (builder order)"); ctx->opt_layout = int(value); break;
@@ -996,7 +997,10 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     lc.kind = sc->info.prim_kind == VRH_PRIM_TRI64 ? 0 : 1;
     lc.ao = ao;
     lc.count = (k->flags & VRH_KERNEL_COUNT_TESTS) != 0;
-    lc.block = ctx->opt_block ? ctx->opt_block : 64;
+    // AO tail sharing needs several waves per block (they share LDS): 4 unless the block is set
+    const bool ao_share = ctx->opt_share == 1 && ao && !list;
+    lc.block = ctx->opt_block ? ctx->opt_block : ao_share ? 256 : 64;
+    lc.share = ao_share;
     lc.stack_cap = int(cap);
     lc.epi = whitted ? 3 : multi ? 2 : shade ? 1 : 0;
     lc.max_hits = multi ? int(k->max_hits) : 0;
@@ -1091,6 +1095,7 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     // per-tile entry cut of the 4-wide tree for AO rays (needs the gate: the tile's hits are known)
     // entries nearest-first (+3.5 % over the cut order, profiles/r02_ab/ab33_ao_cut_order*.log)
     p.ao_cut = (p.quad_ok && p.ao_gate && ctx->opt_cut != 2) ? (ctx->opt_cut == 3 ? 1u : 2u) : 0u;
+    p.ao_share = (ao_share && lc.block > 64) ? 1u : 0u;
     for (uint32_t f = 0; f < num_frames; ++f)
     {
         std::memcpy(p.cam[f].eye, cams[f].eye, 12); std::memcpy(p.cam[f].cam_u, cams[f].cam_u, 12);
