@@ -552,6 +552,8 @@ __device__ inline void walk_shared(vrh_scene_view const& b, vrh::dev::ray_t cons
     static_assert(sizeof(RT) % 4 == 0 && std::is_trivially_copyable<RT>::value, "hit record words move between lanes");
     constexpr uint32_t CAP = VRH_USER_STACK, NOTASK = 0xFFFFFFFFu;
     constexpr uint32_t RW = sizeof(RT) / 4;
+    // a finished lane's LDS column carries a hit record (RW words) or a stolen entry with its ray (12)
+    static_assert(RW <= CAP && CAP >= 12u, "VRH_USER_ANYHIT_SHARE: the stack column must hold a hit record and a ray");
     extern __shared__ uint32_t vrh_user_smem[];
     const float4* pairs = static_cast<const float4*>(b.pairs);
     const uint32_t nthreads = blockDim.x * blockDim.y * blockDim.z;
