@@ -6,6 +6,8 @@
 #          frac / traffic), the driver's command itself, and its rocprofv3 kernel trace
 #   c4     the same passes for C4 (hf10M, 20 frames per launch) + L2 / TD passes, its bench line;
 #          C2 and C5 bench lines
+#   f32    the same PMC passes for the no-argument command (64 frames, 32 per launch), C3 and C4, and
+#          their bench lines
 # Every GPU step has its own time limit; after a fault / abort / timeout nothing else touches the GPU.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
@@ -49,5 +51,14 @@ if has c4; then
   step bench_c4 600 python3 bench.py --scene hf10M --steps 20 --warmup 5 --no-cpu-baseline
   step bench_c2 600 python3 bench.py --scene hf1M --kernel primary --steps 20 --warmup 5 --no-cpu-baseline
   step bench_c5 600 python3 bench.py --scene sph1M --steps 20 --warmup 5 --no-cpu-baseline
+fi
+if has f32; then
+  # the no-argument bench command (--steps 64 --warmup 32: two launches of 32 frames)
+  passes $OUT/c3_f32 python3 bench.py --steps 64 --warmup 32 $Q
+  python3 tools/pmc_bench.py $OUT/c3_f32 $OUT/pmc_traffic_F32.json hf1M ao 32 "python3 bench.py --steps 64 --warmup 32 $Q" && cp $OUT/pmc_traffic_F32.json profiles/
+  passes $OUT/c4_f32 python3 bench.py --scene hf10M --steps 64 --warmup 32 $Q
+  python3 tools/pmc_bench.py $OUT/c4_f32 $OUT/pmc_traffic_F32_hf10M.json hf10M ao 32 "python3 bench.py --scene hf10M --steps 64 --warmup 32 $Q" && cp $OUT/pmc_traffic_F32_hf10M.json profiles/
+  step bench_f32 600 python3 bench.py
+  step bench_c4_f32 600 python3 bench.py --scene hf10M --no-cpu-baseline
 fi
 exit 0
