@@ -234,7 +234,7 @@ enum vrh_option {
                                     2 = one global queue, 3 = one per XCD over band-interleaved
                                     (band, frame) units (auto: 3 with frames in flight for AO or scenes > 256 MB, else 1) */
     VRH_OPT_REFILL_MIN = 8,      /* free lanes (1..64) before finished rays are retired and idle
-                                    lanes refilled (auto: 32)                                     */
+                                    lanes refilled (auto: AO 24, 28 for scenes above 256 MB)      */
     VRH_OPT_WIDE_ANYHIT = 10,    /* 4-wide node records for any-hit (AO / shadow) rays (step
                                     loop): 1 = on when the BVH passes the containment check, 2 = off
                                     (auto: on for the AO kernel, off for the shading kernels)     */

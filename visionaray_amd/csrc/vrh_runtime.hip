@@ -1068,7 +1068,10 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     // visibility: pop on a miss and a cap of 8 visits per descent step, +6 % on hf1M and +36 % on
     // hf10M; both hurt AO)
     const bool primary_step = !lc.ao && lc.epi == 0;
-    p.refill_min = ctx->opt_refill ? uint32_t(ctx->opt_refill) : 32u;
+    // AO step loop: refill once 24 lanes are free for scenes the 256 MB Infinity Cache holds, 28 above
+    // (profiles/r03_ab/refill/, 3 repetitions at 20 frames per launch: hf1M 24 vs 32 +0.6 %, hf10M
+    // 28 vs 32 +0.3 % and 24 -0.6 %)
+    p.refill_min = ctx->opt_refill ? uint32_t(ctx->opt_refill) : sc->info.device_bytes > (256ull << 20) ? 28u : 24u;
     // primary visibility with frames in flight refills once 16 lanes are free: +3 % sph1M, +2 % hf1M,
     // +1.8 % hf10M at 20 frames per launch (profiles/r02_ab/ab20_refill.log); simple::kernel and
     // whitted once 8 are: +1-2.5 % / +1 % (profiles/r02_ab/shade_refill.jsonl); one-frame primary
