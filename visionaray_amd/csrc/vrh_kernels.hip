@@ -444,7 +444,12 @@ __device__ __forceinline__ uint32_t ao_cut_build(const render_params& P, const f
         }
         if (cur != cut)
         {
-            if (lane < 8u * n) cut[lane] = cur[lane];
+            if constexpr (CUT_MAX <= 8u)
+            {
+                if (lane < 8u * n) cut[lane] = cur[lane];
+            }
+            else
+                for (uint32_t k = lane; k < 8u * n; k += 64u) cut[k] = cur[k];   // more words than lanes
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         }
