@@ -209,16 +209,19 @@ struct stack_t
     uint32_t base;        // this lane's column (word offset of entry 0)
     uint32_t top;         // word offset of the next free entry
     uint32_t stride;      // words between entries = threads per block
-    uint32_t end;         // base + LDS entries * stride
-    uint32_t lim;         // base + total entries * stride (LDS + overflow; = end without SPILL)
-    uint32_t* spill;      // SPILL: this block's overflow block (entry top >= end at spill[top - end + base])
+    uint32_t end;         // SPILL: base + LDS entries * stride (unused otherwise)
+    uint32_t lim_off;     // total entries * stride (LDS + overflow; wave-uniform)
+    uint32_t* spill;      // SPILL: this block's overflow block minus LDS entries * stride (wave-uniform):
+                          // the entry at top >= end lives at spill[top] (= block[top - end + base])
     __device__ __forceinline__ void reset() { top = base; }
+    // k more entries fit (lim_off is uniform, so no per-lane limit register stays live)
+    __device__ __forceinline__ bool room(uint32_t k) const { return top + k * stride <= base + lim_off; }
     __device__ __forceinline__ void push(uint32_t v)
     {
         if constexpr (SPILL)
         {
             if (__builtin_expect(top < end, 1)) mem[top] = v;
-            else spill[top - end + base] = v;
+            else spill[top] = v;
         }
         else
             mem[top] = v;
@@ -228,7 +231,7 @@ struct stack_t
     {
         top -= stride;
         if constexpr (SPILL)
-            if (__builtin_expect(top >= end, 0)) return spill[top - end + base];
+            if (__builtin_expect(top >= end, 0)) return spill[top];
         return mem[top];
     }
     __device__ __forceinline__ bool empty() const { return top == base; }
@@ -455,7 +458,7 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
             const bool h3 = quad_entry(xl.w, yl.w, zl.w, xh.w, yh.w, zh.w, r, max_t, d3) & (k3 != QUAD_NONE);
             if (COUNT) cnt.box += 4;
             if (!(h0 | h1 | h2 | h3)) return st.empty() ? -1 : 0;
-            if (st.top + 3u * st.stride > st.lim)
+            if (!st.room(3u))
             {
                 st.reset();
                 st.push(root);

@@ -51,6 +51,7 @@
 #include "standalone.h"
 #endif
 #include "detail/vrh_device.h"
+#include "detail/vrh_libm.h"
 
 #include <array>
 #include <cassert>
@@ -279,6 +280,28 @@ private:
     uint32_t x_ = 1u;                               // default_seed
 };
 
+// float sin / cos as the host C library computes them (detail/vrh_libm.h restates glibc's sinf / cosf,
+// equal to it on every float input), so the samplers below draw the reference CPU run's directions on
+// the device too; other types keep std::sin / std::cos
+VRH_FUNC inline float libm_cos(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return ::vrh::libm::cosf(x);
+#else
+    return ::cosf(x);
+#endif
+}
+VRH_FUNC inline float libm_sin(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return ::vrh::libm::sinf(x);
+#else
+    return ::sinf(x);
+#endif
+}
+template <typename T> VRH_FUNC inline T libm_cos(T x) { return std::cos(x); }
+template <typename T> VRH_FUNC inline T libm_sin(T x) { return std::sin(x); }
+
 // sampling.h:49-71 (math/detail/math.h:241 two_pi; max(x, y) = x < y ? y : x)
 template <typename T>
 VRH_FUNC inline vector<3, T> uniform_sample_hemisphere(T u1, T u2)
@@ -286,7 +309,7 @@ VRH_FUNC inline vector<3, T> uniform_sample_hemisphere(T u1, T u2)
     auto m = T(1.0) - u1 * u1;
     auto r = std::sqrt(T(0.0) < m ? m : T(0.0));
     auto phi = T(6.28318530717958647692528676656e+00) * u2;
-    return vector<3, T>(r * std::cos(phi), r * std::sin(phi), u1);
+    return vector<3, T>(r * libm_cos(phi), r * libm_sin(phi), u1);
 }
 
 template <typename T>
@@ -294,8 +317,8 @@ VRH_FUNC inline vector<3, T> cosine_sample_hemisphere(T u1, T u2)
 {
     auto r = std::sqrt(u1);
     auto theta = T(6.28318530717958647692528676656e+00) * u2;
-    auto x = r * std::cos(theta);
-    auto y = r * std::sin(theta);
+    auto x = r * libm_cos(theta);
+    auto y = r * libm_sin(theta);
     auto m = T(1.0) - u1;
     auto z = std::sqrt(T(0.0) < m ? m : T(0.0));
     return vector<3, T>(x, y, z);
@@ -354,7 +377,7 @@ __device__ inline vrh::dev::lds_stack user_stack()
     st.stride = nthreads;
     st.top = tid;
     st.end = tid + VRH_USER_STACK * nthreads;
-    st.lim = st.end;
+    st.lim_off = VRH_USER_STACK * nthreads;
     st.spill = nullptr;          // checked_ref: the BVH fits the LDS stack
     return st;
 }
@@ -467,7 +490,7 @@ __device__ inline bool walk_quads(vrh_scene_view const& b, vrh::dev::ray_t const
             const bool h2 = vrh::dev::quad_entry(xl.z, yl.z, zl.z, xh.z, yh.z, zh.z, r, max_t, d2) & (k2 != QUAD_NONE);
             const bool h3 = vrh::dev::quad_entry(xl.w, yl.w, zl.w, xh.w, yh.w, zh.w, r, max_t, d3) & (k3 != QUAD_NONE);
             if (!(h0 | h1 | h2 | h3)) { at_leaf = false; break; }
-            if (st.top + 3u * st.stride > st.lim) return false;
+            if (!st.room(3u)) return false;
             d0 = h0 ? d0 : INFINITY; d1 = h1 ? d1 : INFINITY; d2 = h2 ? d2 : INFINITY; d3 = h3 ? d3 : INFINITY;
             const bool a01 = d1 < d0, a23 = d3 < d2;
             const float m01 = a01 ? d1 : d0, m23 = a23 ? d3 : d2;

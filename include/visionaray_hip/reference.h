@@ -9,7 +9,8 @@
 // basic_intersector, get_normal / get_tex_coord / get_surface, the materials and lights, simple::
 // and whitted::kernel, random_sampler<float> (std::default_random_engine +
 // std::uniform_real_distribution<float>, so its draws on the GPU are the CPU's bit for bit) and
-// cosine_sample_hemisphere (sampling.h:61-71).  No reference source is changed or copied, and no
+// cosine_sample_hemisphere (sampling.h:61-71, whose float sin / cos are the host library's on the device
+// too: detail/vrh_libm.h).  No reference source is changed or copied, and no
 // CUDA macro is defined: `__CUDACC__` / `__CUDA_ARCH__` stay undefined, so the reference takes the
 // same (CPU) code paths it takes under g++.
 //
@@ -77,9 +78,43 @@
 #include <immintrin.h>
 #endif
 
+#include "detail/vrh_libm.h"
+
 #pragma clang force_cuda_host_device begin
 #include <random>
 #include <visionaray/math/math.h>
+// sampling.h's sin / cos (cosine_sample_hemisphere, uniform_sample_hemisphere: sampling.h:51-71) on a
+// float return what the host C library returns -- on the device through the restatement of glibc's
+// sinf / cosf (detail/vrh_libm.h, equal to the host library on every float input), on the host the
+// library itself -- so a device AO kernel draws the reference CPU run's directions bit for bit.  Every
+// other argument type keeps the reference's own overloads.  sampling.h is included here, first, with
+// its two calls renamed; its include guard keeps later includes (brdf.h, kernels.h) from repeating it.
+namespace visionaray
+{
+inline float vrh_libm_cos(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return ::vrh::libm::cosf(x);
+#else
+    return ::cosf(x);
+#endif
+}
+inline float vrh_libm_sin(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return ::vrh::libm::sinf(x);
+#else
+    return ::sinf(x);
+#endif
+}
+template <typename T> inline auto vrh_libm_cos(T const& x) -> decltype(cos(x)) { return cos(x); }
+template <typename T> inline auto vrh_libm_sin(T const& x) -> decltype(sin(x)) { return sin(x); }
+} // visionaray
+#define cos vrh_libm_cos
+#define sin vrh_libm_sin
+#include <visionaray/sampling.h>
+#undef cos
+#undef sin
 #include <visionaray/aligned_vector.h>
 #include <visionaray/bvh.h>
 #include <visionaray/camera.h>

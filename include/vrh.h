@@ -232,7 +232,11 @@ enum vrh_option {
                                     min/max where provably identical, see vrh_device.h)           */
     VRH_OPT_XCD_QUEUES = 7,      /* tile queues: 1 = one per XCD (image strips) with stealing,
                                     2 = one global queue, 3 = one per XCD over band-interleaved
-                                    (band, frame) units (auto: 3 with frames in flight for AO or scenes > 256 MB, else 1) */
+                                    (band, frame) units, 4 = one per XCD over image strips in cluster
+                                    order (cluster, frame, tile: the frames in flight of a cluster
+                                    back to back) (auto: 4 with frames in flight for AO, 3 with frames
+                                    in flight for scenes > 256 MB, else 1)                         */
+    VRH_OPT_CLUSTER_TILES = 23,  /* VRH_OPT_XCD_QUEUES 4: 8x8 tiles per cluster, 1..1024 (auto: 8) */
     VRH_OPT_REFILL_MIN = 8,      /* free lanes (1..64) before finished rays are retired and idle
                                     lanes refilled (auto: AO 24, 28 for scenes above 256 MB)      */
     VRH_OPT_WIDE_ANYHIT = 10,    /* 4-wide node records for any-hit (AO / shadow) rays (step

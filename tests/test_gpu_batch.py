@@ -87,7 +87,8 @@ def test_batch_spheres(ctx, n):
 
 
 @pytest.mark.parametrize("opts", [{"ao_schedule": 3}, {"refill_min": 1}, {"xcd_queues": 2}, {"xcd_queues": 1},
-                                  {"wide_anyhit": 1}])
+                                  {"wide_anyhit": 1}, {"xcd_queues": 4}, {"xcd_queues": 4, "cluster_tiles": 3},
+                                  {"xcd_queues": 4, "cluster_tiles": 1}, {"xcd_queues": 4, "cluster_tiles": 1024}])
 def test_batch_under_other_schedules(ctx, opts):
     for k, v in opts.items():
         ctx.set_option(k, v)
@@ -102,6 +103,17 @@ def test_batch_under_other_schedules(ctx, opts):
 @pytest.mark.parametrize("count,index,n", [(3, 0, 4), (3, 2, 4), (8, 5, 4), (8, 7, 32)])
 def test_batch_packed_shards(ctx, count, index, n):
     check_batch(ctx, "hf200", 320, 180, "ao", n, shard=_capi.vrh_shard(index, count, 1, 0))
+
+
+@pytest.mark.parametrize("count,index,n", [(3, 1, 5), (8, 7, 20)])
+def test_batch_packed_shards_cluster_order(ctx, count, index, n):
+    ctx.set_option("xcd_queues", 4)
+    ctx.set_option("cluster_tiles", 7)
+    try:
+        check_batch(ctx, "hf200", 320, 180, "ao", n, shard=_capi.vrh_shard(index, count, 1, 0))
+    finally:
+        ctx.set_option("xcd_queues", 0)
+        ctx.set_option("cluster_tiles", 0)
 
 
 def test_batch_arguments_are_checked(ctx):

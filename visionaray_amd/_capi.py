@@ -54,6 +54,7 @@ VRH_OPT_WIDE_ANYHIT, VRH_OPT_DESCENT_CAP, VRH_OPT_POP_ON_MISS, VRH_OPT_COOP_FETC
 VRH_OPT_SCALAR_FETCH, VRH_OPT_PAIR_LAYOUT, VRH_OPT_AO_GATE, VRH_OPT_WAVE_TIMES = 14, 15, 16, 19
 VRH_OPT_AO_CUT = 20
 VRH_OPT_AO_SHARE = 22
+VRH_OPT_CLUSTER_TILES = 23
 VRH_OPT_AO_STEAL = 21
 VRH_MAX_TIMED_FRAMES = 1024
 VRH_MAX_SCENE_LIST = 8

@@ -38,8 +38,13 @@ struct render_params
     uint32_t frame_num;       // frame number of frame 0 of the launch (frame f: frame_num + f), AO sampler offset
     uint32_t frame_rows;      // output rows per frame: frame f owns rows [f * frame_rows, (f + 1) * frame_rows)
     uint32_t width, height;
+    float width_f, height_f;  // (float)width, (float)height (sched_common.h:137-138 divides by them)
 
     uint32_t samples;
+    // ceil(2^20 / samples): (c * samples_recip) >> 20 == c / samples for every c < 2048 (the error
+    // c * (recip - 2^20 / samples) / 2^20 stays below 2048 / 2^20 < 1 / samples for samples <= 32),
+    // a multiply instead of a division whose reciprocal the compiler kept in a spilled VGPR
+    uint32_t samples_recip;
     float radius, eps;
     float bg[4];
     // pixel sampler pass (vrh_render_sampled): primary rays through (x + px_off, y + px_off) or, with
@@ -71,7 +76,9 @@ struct render_params
     // since vrh_stats_reset
     unsigned long long* counters;
     uint32_t xcd_queues;      // 1: per-XCD tile queues (strips) with stealing; 2: per-XCD queues over
-                              // band-interleaved (band, frame) units; 0: one global queue
+                              // band-interleaved (band, frame) units; 3: per-XCD strips in cluster
+                              // order (cluster, frame, tile); 0: one global queue
+    uint32_t cluster;         // xcd_queues 3: tiles per cluster (>= 1)
     uint32_t refill_min;      // retire / refill once this many lanes are free (AO step loop)
     uint32_t refill_min_primary;   // the same for the step loop's primary-only stream
     uint32_t ao_cut;          // AO step loop: any-hit rays start at the tile's cut of the 4-wide tree

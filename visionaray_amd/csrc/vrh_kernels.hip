@@ -154,8 +154,10 @@ __device__ __forceinline__ ray_t primary_ray(const render_params& P, uint32_t f,
         fx = fx + P.px_off[0];                    // ssaa<N>: the sample's offset
         fy = fy + P.px_off[1];
     }
-    float u = 2.0f * (fx + 0.5f) / (float)P.width - 1.0f;
-    float v = 2.0f * (fy + 0.5f) / (float)P.height - 1.0f;
+    // (float)width / (float)height converted on the host (the same value: the conversion is exact
+    // below 2^24): a device conversion of the uniform value was hoisted into a spilled VGPR
+    float u = 2.0f * (fx + 0.5f) / P.width_f - 1.0f;
+    float v = 2.0f * (fy + 0.5f) / P.height_f - 1.0f;
     if (SAMPLED && P.matrix_cam)
     {
         // sched_common.h:152-176 (camera matrices): o = inv_view (inv_proj (u, v, -1, 1)), d at
@@ -237,6 +239,39 @@ __device__ __forceinline__ uint32_t strip_lo(const render_params& P, uint32_t q,
 __device__ __forceinline__ uint32_t next_tile(const render_params& P, tile_queue& tq, uint32_t lane)
 {
     const uint32_t nq = P.xcd_queues ? 8u : 1u;
+    if (P.xcd_queues == 3u)
+    {
+        // cluster order (frames in flight): queue q owns strip q of the launch's bands; a band is cut
+        // into clusters of P.cluster tiles, and the units of a strip are (cluster, frame, tile) with
+        // the tile fastest, then the frame -- the F frames of one cluster are handed out back to back,
+        // so the waves in flight on one XCD trace the same few clusters of the image in every frame
+        // in flight and their nodes and triangles stay in that XCD's L2
+        const uint32_t tx = P.tiles_x, F = P.num_frames, C = P.cluster;
+        const uint32_t nb = P.num_tiles / tx;
+        while (tq.tried < 8u)
+        {
+            const uint32_t b0 = (uint32_t)(((uint64_t)nb * tq.q) >> 3);
+            const uint32_t b1 = (uint32_t)(((uint64_t)nb * (tq.q + 1u)) >> 3);
+            uint32_t t = 0;
+            if (lane == 0) t = atomicAdd(reinterpret_cast<uint32_t*>(P.counters + 8u + 8u * tq.q), 1u);
+            t = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl(t, 0));
+            const uint32_t per_band = tx * F;
+            if (t < (b1 - b0) * per_band)
+            {
+                const uint32_t lb = t / per_band;
+                const uint32_t r = t - lb * per_band;
+                const uint32_t c = r / (C * F);                 // cluster of the band (the last may be narrower)
+                const uint32_t r2 = r - c * C * F;
+                const uint32_t cw = min(C, tx - c * C);
+                const uint32_t f = r2 / cw;
+                const uint32_t j = r2 - f * cw;
+                return (f << TILE_FRAME_SHIFT) | ((b0 + lb) * tx + c * C + j);
+            }
+            tq.q = (tq.q + 1u) & 7u;
+            tq.tried += 1u;
+        }
+        return NONE;
+    }
     if (P.xcd_queues == 2u)
     {
         // band-interleaved (frames in flight): the launch's (band, frame) units in band-major order,
@@ -368,7 +403,16 @@ __device__ __forceinline__ uint32_t ao_cut_build(const render_params& P, const f
     if (!(ext < INFINITY)) return NONE;
     for (int a = 0; a < 3; ++a) { lo[a] -= ext; hi[a] += ext; }
     auto put = [&](float* e, cut_cfloat* q, uint32_t c) {           // entry c of record q -> e
-        if (lane < 7u) e[lane] = q[lane < 6u ? 4u * lane + c : 24u + c];
+        // seven wave-uniform (scalar) loads, lane k keeps word k: no per-lane record address stays
+        // live across the kernel (it was spilled to scratch)
+        float w = q[c];
+        w = lane == 1u ? q[4u + c] : w;
+        w = lane == 2u ? q[8u + c] : w;
+        w = lane == 3u ? q[12u + c] : w;
+        w = lane == 4u ? q[16u + c] : w;
+        w = lane == 5u ? q[20u + c] : w;
+        w = lane == 6u ? q[24u + c] : w;
+        if (lane < 7u) e[lane] = w;
     };
     // level 0: the root record's children
     float* cur = cut;
@@ -519,14 +563,18 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     st.stride = block;
     st.top = tid;
     st.end = tid + P.stack_cap * block;
-    st.lim = SPILL ? tid + P.stack_total * block : st.end;
-    st.spill = SPILL ? P.stack_spill + size_t(blockIdx.x) * (P.stack_total - P.stack_cap) * block : nullptr;
+    st.lim_off = (SPILL ? P.stack_total : P.stack_cap) * block;
+    // the overflow entries of lane tid start at entry stack_cap: word top - stack_cap * block of this
+    // block's overflow area, i.e. spill[top] with the pointer moved back by stack_cap * block words
+    st.spill = SPILL ? P.stack_spill + size_t(blockIdx.x) * (P.stack_total - P.stack_cap) * block - size_t(P.stack_cap) * block
+                     : nullptr;
     uint32_t* ao_area = smem + P.stack_cap * block + wave * AO_WAVE_WORDS;
     test_counts cnt = {};
     uint64_t rays_total = 0, hits_total = 0;
     const hit_mask_params hml = P.hmask;          // a local copy: &P would spill the kernel arguments
     const hit_mask_params* hm = &hml;             // ray_step tests hm->mask
-    const unsigned long long t_start = P.wave_times ? wall_clock64() : 0ull;
+    if (P.wave_times && lane == 0)      // the start is stored at once: nothing stays live across the loop
+        P.wave_times[2 * (size_t(blockIdx.x) * (blockDim.x >> 6) + wave)] = wall_clock64();
 
     // lane state: the ray it is stepping
     constexpr uint32_t IDLE = 0, PRIMARY = 1, AORAY = 2;
@@ -762,7 +810,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         // slot pixels and cut are recs_ / spx / cut_, cutn (this wave's, or a sibling's it helps)
         auto start_ao = [&](const float* recs_, const uint8_t* spx, const float* cut_, uint32_t cutn, uint32_t tile,
                             uint32_t par, uint32_t cand, uint32_t owner) {
-            const uint32_t slot = cand / S, smp = cand - slot * S;
+            // cand / S by the host's reciprocal (exact: cand < 64 S <= 2048, S <= 32, vrh_kernels.h)
+            const uint32_t slot = (cand * P.samples_recip) >> 20, smp = cand - slot * S;
             uint32_t x, y, orow, fr;
             tile_pixel(P, tile, spx[par * 64u + slot], x, y, orow, fr);
             r = ao_ray<COUNT>(P, recs_, slot, smp, y * P.width + x, fr, cnt);
@@ -1023,11 +1072,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     }
 
     if (P.wave_times && lane == 0)
-    {
-        const size_t w = size_t(blockIdx.x) * (blockDim.x >> 6) + wave;
-        P.wave_times[2 * w] = t_start;
-        P.wave_times[2 * w + 1] = wall_clock64();
-    }
+        P.wave_times[2 * (size_t(blockIdx.x) * (blockDim.x >> 6) + wave) + 1] = wall_clock64();
     flush_totals<COUNT>(P, lane, rays_total, hits_total, cnt);
 }
 

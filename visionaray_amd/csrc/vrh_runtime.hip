@@ -146,7 +146,10 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
         break;
     case VRH_OPT_WAVE_TIMES: VRH_CHECK(value <= 2, "vrh_ctx_set_option: wave times is 1 (on), 2 (on + tile times of counting one-frame AO launches) or 0 (off)"); ctx->opt_wave_times = int(value); break;
     case VRH_OPT_AO_CUT: VRH_CHECK(value <= 3, "vrh_ctx_set_option: AO cut is 1 (on, entries nearest-first), 2 (off) or 3 (on, entries in cut order)"); ctx->opt_cut = int(value); break;
-    case VRH_OPT_AO_STEAL: VRH_CHECK(value != 1, "vrh_ctx_set_option: the AO tail stash was removed (it measured slower)"); return VRH_OK;
+    case VRH_OPT_AO_STEAL:
+        // the AO tail stash was removed in round 3 (measured slower)
+        if (value == 1) { set_error("vrh_ctx_set_option: the AO tail stash was removed (it measured slower)"); return VRH_ERR_UNSUPPORTED; }
+        return VRH_OK;
     case VRH_OPT_AO_SHARE: VRH_CHECK(value <= 2, "vrh_ctx_set_option: AO tail sharing is 1 (on) or 2 (off)"); ctx->opt_share = int(value); break;
     case VRH_OPT_AO_GATE: VRH_CHECK(value <= 2, "vrh_ctx_set_option: AO gate is 1 (on) or 2 (off)"); ctx->opt_gate = int(value); break;
     case VRH_OPT_POP_ON_MISS: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pop on miss is 1 (on) or 2 (off)"); ctx->opt_pop = int(value); break;
@@ -156,7 +159,8 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
     case VRH_OPT_BLOCKS_PER_CU: ctx->opt_bpc = int(value); break;
     case VRH_OPT_WAVES_PER_SIMD: VRH_CHECK(value == 0 || value == 1 || value == 5 || value == 6 || value == 8, "vrh_ctx_set_option: waves per SIMD is 1, 5, 6 or 8"); ctx->opt_occ = int(value); break;
     case VRH_OPT_EXACT_MINMAX: ctx->opt_exact_minmax = value ? 1 : 0; break;
-    case VRH_OPT_XCD_QUEUES: VRH_CHECK(value <= 3, "vrh_ctx_set_option: xcd queues is 1 (strips), 2 (off) or 3 (band-interleaved)"); ctx->opt_xcd_queues = int(value); break;
+    case VRH_OPT_XCD_QUEUES: VRH_CHECK(value <= 4, "vrh_ctx_set_option: xcd queues is 1 (strips), 2 (off), 3 (band-interleaved) or 4 (cluster order)"); ctx->opt_xcd_queues = int(value); break;
+    case VRH_OPT_CLUSTER_TILES: VRH_CHECK(value <= 1024, "vrh_ctx_set_option: cluster tiles is 1..1024 (0 = auto)"); ctx->opt_cluster = int(value); break;
     default: set_error("vrh_ctx_set_option: unknown option"); return VRH_ERR_INVALID;
     }
     return VRH_OK;
@@ -1116,7 +1120,9 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     p.frame_num = frame_num;
     p.frame_rows = frame_rows;
     p.width = cam->width; p.height = cam->height;
+    p.width_f = float(cam->width); p.height_f = float(cam->height);
     p.samples = ao ? k->samples : 0; p.radius = k->radius; p.eps = k->eps;
+    p.samples_recip = ao ? ((1u << 20) + p.samples - 1u) / p.samples : 0u;
     std::memcpy(p.bg, k->bg, 16);
     if (sp)
     {
@@ -1141,9 +1147,16 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     // per frame (profiles/r02_ab/ab31_tile_order_orbit_*.log): band order hf10M AO +3.5 %, hf10M
     // primary +10 %, hf1M AO +0.3 %, but hf1M primary -2.8 % (its scene fits the MALL, and a
     // strip's primaries then keep their XCD's L2); one-frame launches keep strips (ab30)
+    // AO with frames in flight: cluster order (every XCD on its own strip, the F frames of a cluster of
+    // 8 tiles handed out back to back): against the band order, round 4, same box, 20 frames per
+    // launch (profiles/r04_ab/cluster/): hf10M +3.3 % (static camera) / +0.3 % (orbiting 0.5 deg per
+    // frame), hf1M +0.9 % / +2.3 %; clusters of 4-16 tiles alike, 240 (a whole band) no gain
     const bool band_auto = num_frames > 1 && (lc.ao || sc->info.device_bytes > (256ull << 20));
+    const bool cluster_auto = num_frames > 1 && lc.ao;
     p.xcd_queues = ctx->opt_xcd_queues == 2 ? 0u : ctx->opt_xcd_queues == 1 ? 1u
-                 : ctx->opt_xcd_queues == 3 ? 2u : (band_auto ? 2u : 1u);
+                 : ctx->opt_xcd_queues == 3 ? 2u : ctx->opt_xcd_queues == 4 ? 3u
+                 : cluster_auto ? 3u : (band_auto ? 2u : 1u);
+    p.cluster = ctx->opt_cluster ? uint32_t(ctx->opt_cluster) : 8u;
     if (shade)
     {
         p.shade.materials = k->shading->materials;
