@@ -20,7 +20,8 @@
 //                                                               bvh refs, materials and lights
 //   ref_kernels multi  <grid> <W> <H> <outdir>                  multi_hit<16> over the refs: hit count
 //                                                               and the first / last hit per pixel
-//   ref_kernels bench  <grid> <W> <H> <frames>                  AO kernel throughput (median frame)
+//   ref_kernels bench  <grid> <W> <H> <launches> [F]            AO kernel throughput (median frame,
+//                                                               F frames per launch)
 //
 // Outputs: color.bin (RGBA32F as rendered), t.bin (the depth the kernel returned, where it set one).
 #include <visionaray_hip/reference.h>      // was: #include <visionaray/bvh.h> ... <visionaray/traverse.h>
@@ -317,18 +318,26 @@ int main(int argc, char** argv)
             }
             else
             {
-                const int frames = argc > 5 ? atoi(argv[5]) : 10;
+                // bench <grid> <W> <H> <launches> [F]: median wall time per frame over `launches`
+                // synchronous launches of F frames each (F = 1: one frame() per frame, as cuda_sched is
+                // driven; F > 1: hip_sched::frames, frames in flight, distinct sampler seeds per frame)
+                const int launches = argc > 5 ? atoi(argv[5]) : 10;
+                const int F = argc > 6 ? atoi(argv[6]) : 1;
+                hip_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> rtF;
+                rtF.resize(W, H * unsigned(F));
+                std::vector<camera> cams(size_t(F), cam);
                 std::vector<double> ms;
-                for (int f = 0; f <= frames; ++f)
+                for (int l = 0; l <= launches; ++l)
                 {
                     auto t0 = std::chrono::steady_clock::now();
-                    sched.frame(kernel, sparams, unsigned(f));
+                    if (F == 1) sched.frame(kernel, sparams, unsigned(l));
+                    else sched.frames(kernel, cams, rtF, unsigned(l * F));
                     auto t1 = std::chrono::steady_clock::now();
-                    if (f > 0) ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+                    if (l > 0) ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count() / F);
                 }
                 std::sort(ms.begin(), ms.end());
-                printf("{\"mode\":\"bench\",\"kernel\":\"ao/main.cpp (reference headers)\",\"frame_ms_median\":%.4f,\"frames\":%d}\n",
-                       ms[ms.size() / 2], frames);
+                printf("{\"mode\":\"bench\",\"kernel\":\"ao/main.cpp (reference headers)\",\"frame_ms_median\":%.4f,"
+                       "\"launches\":%d,\"frames_per_launch\":%d}\n", ms[ms.size() / 2], launches, F);
                 return 0;
             }
         }

@@ -100,6 +100,29 @@ def test_colour_code_wire_equals_single_gpu_colour(ctx, group, kind, samples, sh
         assert np.array_equal(out["color"][f * n:(f + 1) * n].view(np.uint32), ref["color"].view(np.uint32)), f
 
 
+@pytest.mark.parametrize("fields", ["color", "color+prim_id"])
+@pytest.mark.parametrize("samples", [8, 5])
+def test_no_occ_kernel_through_group(ctx, group, fields, samples):
+    """An AO kernel that leaves the occlusion target out (ao_kernel(occ=False), VRH_KERNEL_NO_OCC)
+    through the group: the wire's occlusion bytes (code byte / colour re-derivation) are the group's
+    own staging data, so the gathered colour still equals the one-GPU frame."""
+    host, dev = device_scene(ctx, "hf200")
+    W, H = 320, 180
+    cam, _, _ = scenes.scene_camera("hf200", W, H)
+    basis = cam.basis(W, H)
+    f = _capi.VRH_RT_COLOR | (_capi.VRH_RT_PRIM_ID if fields == "color+prim_id" else 0)
+    dst = va.hip_buffer_rt(ctx, W, H * 2, flags=f)
+    group.render(dev, va.ao_kernel(dev, samples=samples, occ=False), dst, [basis] * 2, frame_num=4, shards=3, fields=f)
+    group.sync()
+    out = dst.download()
+    dst.close()
+    n = W * H
+    for k, ref in enumerate(single_frames(ctx, dev, va.ao_kernel(dev, samples=samples), basis, W, H, 2, 4)):
+        assert np.array_equal(out["color"][k * n:(k + 1) * n].view(np.uint32), ref["color"].view(np.uint32)), k
+        if "prim_id" in out:
+            assert np.array_equal(out["prim_id"][k * n:(k + 1) * n], ref["prim_id"]), k
+
+
 @pytest.mark.parametrize("shards,frames", [(2, 1), (3, 4), (8, 2), (135, 1)])
 def test_sharded_frames_equal_single_gpu_frames(ctx, group, shards, frames):
     """Frames in flight through the group (frame numbers 7, 8, ...), every buffer gathered."""

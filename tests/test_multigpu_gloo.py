@@ -217,3 +217,17 @@ def test_exchange_plan_pairs_every_send_with_a_receive():
                 sends = multigpu.exchange_plan(rank, world, shards)[0]
                 # per peer, the root's receives from `rank` list the same shards in the same order
                 assert [s for s, _ in sends] == [s for s, p in recvs if p == rank]
+
+
+def test_unshard_host_rejects_mismatched_wire_and_empty_width():
+    """vrh_unshard_host checks that the wire layout is the one the fields and kernel give, and that the
+    image has a width (a zero width or an empty wire layout was a division by zero)."""
+    Wd, Hd, S, F = 5, 37, 3, 2
+    w_ids = multigpu.wire_layout(FIELDS_IDS, Wd, Hd, F, S, bg=BG)
+    g = np.zeros((S, w_ids.shard_bytes), np.uint8)
+    # the same bytes read as a colour-only gather: another layout -> refused, not re-derived quietly
+    with pytest.raises(_capi.VrhError):
+        multigpu.unshard(g, w_ids, FIELDS_COLOR, Wd, Hd, S, 0, bg=BG)
+    with pytest.raises(_capi.VrhError):
+        multigpu.unshard(g, w_ids, FIELDS_IDS, 0, Hd, S, 0, bg=BG)
+    multigpu.unshard(g, w_ids, FIELDS_IDS, Wd, Hd, S, F - 1, bg=BG)      # the matching call still works

@@ -295,7 +295,13 @@ VRH_API int vrh_render_sharded(uint32_t n, vrh_group* const* groups, const vrh_s
                 rt.occ = ao ? g->work + 4 * px : nullptr;
             }
             vrh_shard sh{ s, S, 1u, 0u };
-            rc = vrh_render_batch(ctx, scenes[i], &rt, cams, num_frames, &kernels[i], &sh, frame_num);
+            // the staging AO masks are the group's own (the root re-derives the colour from them, or the
+            // code byte is packed from them): a kernel that leaves the occlusion target out
+            // (VRH_KERNEL_NO_OCC) still writes them -- it only may for <= 8 samples, and with more the
+            // colour itself crosses the wire (layout_for), so rt.occ is null then
+            vrh_kernel_desc kd = kernels[i];
+            if (kd.kind == VRH_KERNEL_AO && kd.samples <= 8) kd.flags &= ~uint32_t(VRH_KERNEL_NO_OCC);
+            rc = vrh_render_batch(ctx, scenes[i], &rt, cams, num_frames, &kd, &sh, frame_num);
             if (rc) return rc;
             if (wl.code)
                 VRH_HIP(launch_pack_code(rt.prim_id, rt.occ, base + o_code, px, ctx->stream));
@@ -407,13 +413,20 @@ VRH_API int vrh_unshard_host(const void* gathered, const vrh_wire_layout* wire, 
                              uint32_t shards, uint32_t frame, uint32_t fields, const vrh_kernel_desc* k,
                              void* color, uint32_t* prim_id, uint8_t* occ, float* t)
 {
-    VRH_CHECK(gathered && wire && k && shards >= 1, "vrh_unshard_host: bad argument");
+    VRH_CHECK(gathered && wire && k && shards >= 1 && width >= 1, "vrh_unshard_host: bad argument");
     const wire_layout wl = layout_for(fields, *k);
+    VRH_CHECK(wl.bytes_per_px() > 0, "vrh_unshard_host: these fields put nothing on the wire");
     const uint32_t rows = VRH_BAND_ROWS * plan::shard_bands(height, 0, shards);
     VRH_CHECK(wire->rows == rows, "vrh_unshard_host: wire layout of another geometry");
     const size_t frames = rows ? size_t(wire->shard_bytes / (wl.bytes_per_px() * size_t(rows) * width)) : 0;
     VRH_CHECK(frame < frames, "vrh_unshard_host: frame out of range");
     const plan::wire_offsets o = plan::offsets_for(wl, size_t(rows) * width * frames);
+    // the wire layout passed must be the one these fields and this kernel give (vrh_group_wire_layout)
+    const uint64_t none = ~0ull;
+    VRH_CHECK(wire->shard_bytes == o.shard_bytes && wire->prim_id == (wl.pid ? o.pid : none) &&
+              wire->occ == (wl.occ ? o.occ : none) && wire->t == (wl.t ? o.t : none) &&
+              wire->color == (wl.color ? o.col : none) && wire->code == (wl.code ? o.code : none),
+              "vrh_unshard_host: wire layout of other fields or another kernel");
     const uint32_t whole[4] = { 0, 0, 0, 0 };
     // the destination buffers hold this one frame: frame_params offsets them by f * W * H, so step back
     const size_t fo = size_t(frame) * width * height;

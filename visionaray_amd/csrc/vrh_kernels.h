@@ -41,10 +41,6 @@ struct render_params
     float width_f, height_f;  // (float)width, (float)height (sched_common.h:137-138 divides by them)
 
     uint32_t samples;
-    // ceil(2^20 / samples): (c * samples_recip) >> 20 == c / samples for every c < 2048 (the error
-    // c * (recip - 2^20 / samples) / 2^20 stays below 2048 / 2^20 < 1 / samples for samples <= 32),
-    // a multiply instead of a division whose reciprocal the compiler kept in a spilled VGPR
-    uint32_t samples_recip;
     float radius, eps;
     float bg[4];
     // pixel sampler pass (vrh_render_sampled): primary rays through (x + px_off, y + px_off) or, with

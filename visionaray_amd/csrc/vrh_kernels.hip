@@ -810,8 +810,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         // slot pixels and cut are recs_ / spx / cut_, cutn (this wave's, or a sibling's it helps)
         auto start_ao = [&](const float* recs_, const uint8_t* spx, const float* cut_, uint32_t cutn, uint32_t tile,
                             uint32_t par, uint32_t cand, uint32_t owner) {
-            // cand / S by the host's reciprocal (exact: cand < 64 S <= 2048, S <= 32, vrh_kernels.h)
-            const uint32_t slot = (cand * P.samples_recip) >> 20, smp = cand - slot * S;
+            const uint32_t slot = cand / S, smp = cand - slot * S;
             uint32_t x, y, orow, fr;
             tile_pixel(P, tile, spx[par * 64u + slot], x, y, orow, fr);
             r = ao_ray<COUNT>(P, recs_, slot, smp, y * P.width + x, fr, cnt);

@@ -15,7 +15,9 @@ struct vrh_ctx
     hipStream_t stream = nullptr;
     bool own_stream = false;
     int num_cus = 0;
-    hipEvent_t group_written = nullptr;   // the last render-group unshard into one of this context's targets
+    // the `written` events of this context's targets that a render group's root wrote (one per target,
+    // re-recorded by every unshard): vrh_sync waits for all of them (two groups may write two targets)
+    std::vector<hipEvent_t> group_written;
     // device counters (u64), see render_params::counters; [0..7] reset per frame
     unsigned long long* counters = nullptr;
     uint32_t* user_queues = nullptr;            // vrh_ctx_user_queues (8 heads x 64 B)
@@ -96,7 +98,13 @@ inline hipError_t mark_written(vrh_rt* rt, hipStream_t stream)
     const hipError_t e = hipEventRecord(rt->written, stream);
     if (e != hipSuccess) return e;
     rt->written_pending = true;
-    if (rt->ctx) { rt->ctx->group_written = rt->written; }
+    if (rt->ctx)
+    {
+        auto& gw = rt->ctx->group_written;
+        bool known = false;
+        for (hipEvent_t ev : gw) known |= ev == rt->written;
+        if (!known) gw.push_back(rt->written);
+    }
     return hipSuccess;
 }
 

@@ -772,7 +772,12 @@ VRH_API int vrh_rt_free(vrh_rt* rt)
     {
         if (rt->ctx) (void)hipSetDevice(rt->ctx->device);
         (void)hipEventSynchronize(rt->written);
-        if (rt->ctx && rt->ctx->group_written == rt->written) rt->ctx->group_written = nullptr;
+        if (rt->ctx)
+        {
+            auto& gw = rt->ctx->group_written;
+            for (size_t i = 0; i < gw.size(); ++i)
+                if (gw[i] == rt->written) { gw.erase(gw.begin() + long(i)); break; }
+        }
         (void)hipEventDestroy(rt->written);
     }
     delete rt;
@@ -1029,6 +1034,13 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     lc.occ = ctx->opt_occ ? ctx->opt_occ : whitted ? 5 : lc.epi ? 1 : lc.ao ? 5 : 6;
     if (sp) lc.occ = lc.ao ? 5 : 6;                    // the sampler instances exist at the defaults
     if (list) lc.occ = ao ? 5 : 6;
+    // tail sharing has instances for uncounted one-frame AO launches at 5 waves / SIMD only
+    // (vrh_kernels.hip pick_share); elsewhere the option changes nothing, not even the block size
+    if (lc.share && (lc.count || lc.epi || lc.occ != 5 || lc.sched != 0))
+    {
+        lc.share = false;
+        if (!ctx->opt_block) lc.block = 64;
+    }
     // auto: the LDS part of the stack shrinks (in steps of 4 entries) while LDS, not registers,
     // limits the waves per CU -- a deep BVH (hf10M: depth 26) then keeps the register-bound
     // occupancy and its few deepest entries go to the overflow block
@@ -1102,7 +1114,7 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     // per-tile entry cut of the 4-wide tree for AO rays (needs the gate: the tile's hits are known)
     // entries nearest-first (+3.5 % over the cut order, profiles/r02_ab/ab33_ao_cut_order*.log)
     p.ao_cut = (p.quad_ok && p.ao_gate && ctx->opt_cut != 2) ? (ctx->opt_cut == 3 ? 1u : 2u) : 0u;
-    p.ao_share = (ao_share && lc.block > 64) ? 1u : 0u;
+    p.ao_share = (lc.share && lc.block > 64) ? 1u : 0u;
     for (uint32_t f = 0; f < num_frames; ++f)
     {
         std::memcpy(p.cam[f].eye, cams[f].eye, 12); std::memcpy(p.cam[f].cam_u, cams[f].cam_u, 12);
@@ -1122,7 +1134,6 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     p.width = cam->width; p.height = cam->height;
     p.width_f = float(cam->width); p.height_f = float(cam->height);
     p.samples = ao ? k->samples : 0; p.radius = k->radius; p.eps = k->eps;
-    p.samples_recip = ao ? ((1u << 20) + p.samples - 1u) / p.samples : 0u;
     std::memcpy(p.bg, k->bg, 16);
     if (sp)
     {
@@ -1264,7 +1275,7 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
 VRH_API int vrh_sync(vrh_ctx* ctx)
 {
     VRH_CHECK(ctx, "vrh_sync: null");
-    if (ctx->group_written) VRH_HIP(hipEventSynchronize(ctx->group_written));
+    for (hipEvent_t ev : ctx->group_written) VRH_HIP(hipEventSynchronize(ev));
     VRH_HIP(hipStreamSynchronize(ctx->stream));
     return VRH_OK;
 }
