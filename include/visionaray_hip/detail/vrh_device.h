@@ -496,7 +496,7 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
         // a wave-uniform address, constant address space), the rest per lane (56 of the record's
         // 64 B: two boxes, two links).  Same bytes either way.  (Extending this to waves whose lanes
         // want 2 or 3 distinct pairs -- one scalar load each, selected per lane -- measured 2-10 %
-        // slower: profiles/r01_ab_peel/.)
+        // slower: profiles/r01/ab_peel/.)
         float4 q0, q1, q2;
         float2 q3;
         typedef const __attribute__((address_space(4))) float cfloat;

@@ -425,12 +425,242 @@ __device__ inline void fetch_quad(const float4* quads, uint32_t link, float4 (&q
     }
 }
 
-template <bool FAST, typename CullT, typename Leaf>
-__device__ inline void walk_slab(vrh_scene_view const& b, vrh::dev::ray_t const& r, float max_t, CullT const& cull_t, Leaf&& leaf)
+// ---- entry cut of any_hit calls (exact, in the reference's visiting order) ---------------------
+// An any-hit ray of a short segment (AO: max_t = the radius) only reaches leaves whose boxes come
+// within float error of its segment: its box test passes only where the box meets the segment.  So
+// for the segments of a wave, all inside a region R, every subtree whose box does not meet R is a box
+// test every one of those rays fails.  The wave keeps, in LDS, a skeleton of the BVH's top for R:
+// copies of the pair records (both child boxes, the same bits) from the root down to at most
+// UCUT_ENTRIES subtrees that meet R, where
+//   * a child whose box does not meet R becomes SKEL_NONE -- the test every contained ray fails;
+//   * a record with exactly one child meeting R is skipped into that child's record when the child's
+//     box contains both grandchildren's boxes (checked per step): a ray that fails the child's box
+//     fails both grandchildren's (the slab test is monotone in the box bounds under round-to-nearest,
+//     DESIGN.md section 4), and a ray that passes it visits them next -- with one candidate there is
+//     no near / far order to keep.
+// A contained ray then walks the skeleton from LDS exactly as it would walk those records from HBM:
+// the same box tests on the same bits, near child first, ties to child 1, far child pushed.  It
+// visits the same leaves in the same order as the walk from the root, so the hit record an any_hit
+// returns is the reference's first-found one (not only its hit / miss).  The skeleton is rebuilt
+// (wave-uniform, records through the scalar cache) when more than a quarter of the wave's segments
+// leave R; R covers every direction from the segments' origins (o +- max_t |d|) plus 5 % of max_t,
+// so the next calls of an AO loop from the same hit points reuse it.  Lanes outside R, and non-finite
+// rays, start at the root.
+// Opt-in (VRH_USER_ANYHIT_CUT=1): exact, but measured SLOWER on the AO lambda (C3, round 4,
+// profiles/r04/user/): 2.06 vs 1.93 ms per frame at 32 frames per launch, 2.33 vs 2.22 one frame per
+// launch; ao/main.cpp's own kernel 2.11 vs 1.86 / 2.43 vs 2.19.  In a user kernel the levels above the
+// cut are walked by the whole wave together (every lane at the same record: the scalar-cache fetch),
+// so the LDS skeleton saves little, while the per-call containment test and the skeleton's LDS reads
+// cost on every call.  The built-in AO kernel gains from its cut (+9 %) because its rays start AT the
+// cut entries, which an any_hit that must return the reference's first-found record cannot do.
+#ifndef VRH_USER_ANYHIT_CUT
+#define VRH_USER_ANYHIT_CUT 0
+#endif
+constexpr uint32_t UCUT_NODES = 8;               // skeleton records
+constexpr uint32_t UCUT_ENTRIES = 8;             // subtrees below the skeleton that meet R
+constexpr uint32_t SKEL_BIT = 0x40000000u;       // link to skeleton record (link & 0xFF)
+constexpr uint32_t SKEL_NONE = 0x7FFFFFFFu;      // a child every contained ray misses
+// LDS words after the block's stacks: [0, 1] BVH key, [2] records (0: none), [4..6] R lo, [7..9] R hi,
+// [10..15] reduction scratch, [16 + 16 k, 32 + 16 k) record k (the pair layout: q0 q1 q2 links)
+constexpr uint32_t UCUT_WORDS = 16u + 16u * UCUT_NODES;
+
+__device__ inline uint32_t* user_cut_area()
+{
+    extern __shared__ uint32_t vrh_user_smem[];
+    return vrh_user_smem + VRH_USER_STACK * 64u;
+}
+
+// child c of a pair record (14 words: q0 q1 q2, link0, link1): lo = w[c], w[2 + c], w[4 + c],
+// hi = w[6 + c], w[8 + c], w[10 + c]
+__device__ inline bool ucut_meets(const float (&w)[14], uint32_t c, const float* lo, const float* hi)
+{
+    return (w[c] <= hi[0]) & (w[6 + c] >= lo[0]) & (w[2 + c] <= hi[1]) & (w[8 + c] >= lo[1])
+         & (w[4 + c] <= hi[2]) & (w[10 + c] >= lo[2]);
+}
+// both child boxes of record v inside child c's box of record w
+__device__ inline bool ucut_contains(const float (&w)[14], uint32_t c, const float (&v)[14])
+{
+    bool ok = true;
+#pragma unroll
+    for (uint32_t a = 0; a < 3; ++a)
+        ok = ok & (v[2 * a] >= w[2 * a + c]) & (v[2 * a + 1] >= w[2 * a + c])
+                & (v[6 + 2 * a] <= w[6 + 2 * a + c]) & (v[6 + 2 * a + 1] <= w[6 + 2 * a + c]);
+    return ok;
+}
+__device__ inline void ucut_load(const float4* pairs, uint32_t p, float (&w)[14])
+{
+    user_cfloat* cp = (user_cfloat*)(const float*)(pairs) + 16u * (uint32_t)__builtin_amdgcn_readfirstlane((int)p);
+#pragma unroll
+    for (int k = 0; k < 14; ++k) w[k] = cp[k];
+}
+// the record to keep for the subtree under pair link p: p, or the record a chain of single-child
+// steps leads to (containment checked at every step)
+__device__ inline void ucut_compress(const float4* pairs, uint32_t p, const float* lo, const float* hi, float (&w)[14])
+{
+    ucut_load(pairs, p, w);
+#pragma unroll 1
+    for (int guard = 0; guard < 64; ++guard)
+    {
+        const bool m0 = ucut_meets(w, 0, lo, hi), m1 = ucut_meets(w, 1, lo, hi);
+        if (m0 == m1) return;
+        const uint32_t c = m0 ? 0u : 1u;
+        const uint32_t l = __float_as_uint(w[12 + c]);
+        if (l & vrh::dev::LEAF_BIT) return;
+        float v[14];
+        ucut_load(pairs, l, v);
+        if (!ucut_contains(w, c, v)) return;
+#pragma unroll
+        for (int k = 0; k < 14; ++k) w[k] = v[k];
+    }
+}
+// write record w as skeleton record k (by the first active lane); returns its inner children that
+// meet R (new entries), links rewritten: outside R -> SKEL_NONE
+__device__ inline uint32_t ucut_put(uint32_t* cw, uint32_t k, const float (&w)[14], const float* lo, const float* hi, bool writer)
+{
+    uint32_t l[2], entries = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < 2; ++c)
+    {
+        l[c] = __float_as_uint(w[12 + c]);
+        if (!ucut_meets(w, c, lo, hi)) l[c] = SKEL_NONE;
+        else if (!(l[c] & vrh::dev::LEAF_BIT)) entries += 1u;
+    }
+    if (writer)
+    {
+        float4* r = reinterpret_cast<float4*>(cw + 16u + 16u * k);
+        r[0] = make_float4(w[0], w[1], w[2], w[3]);
+        r[1] = make_float4(w[4], w[5], w[6], w[7]);
+        r[2] = make_float4(w[8], w[9], w[10], w[11]);
+        r[3] = make_float4(__uint_as_float(l[0]), __uint_as_float(l[1]), 0.0f, 0.0f);
+    }
+    return entries;
+}
+__device__ inline void ucut_sync()
+{
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+}
+
+// The link this lane's any-hit walk starts at: skeleton record 0 if its segment lies in the wave's
+// R (rebuilt here when needed), else the root.  Called by every lane that calls any_hit.
+__device__ inline uint32_t user_cut_entry(vrh_scene_view const& b, vrh::dev::ray_t const& r, float max_t, bool fast)
+{
+    using namespace vrh::dev;
+    uint32_t* cw = user_cut_area();
+    float* cf = reinterpret_cast<float*>(cw);
+    const uint32_t lane = __lane_id();
+    const uint64_t act = __ballot(true);
+    const uint32_t first = (uint32_t)__builtin_ctzll(act);
+    // the segment {o + t d : 0 <= t <= max_t}, per axis
+    const float o[3] = { r.ori.x, r.ori.y, r.ori.z }, d[3] = { r.dir.x, r.dir.y, r.dir.z };
+    float slo[3], shi[3];
+    bool seg_ok = fast;
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+    {
+        const float t = max_t * d[a];
+        slo[a] = o[a] + (t < 0.0f ? t : 0.0f);
+        shi[a] = o[a] + (t > 0.0f ? t : 0.0f);
+        seg_ok = seg_ok & __builtin_isfinite(slo[a]) & __builtin_isfinite(shi[a]);
+    }
+    const uint64_t key = (uint64_t)(uintptr_t)b.pairs;
+    auto inside = [&]() {
+        const bool have = cw[2] != 0u && cw[0] == (uint32_t)key && cw[1] == (uint32_t)(key >> 32);
+        return have & seg_ok & (slo[0] >= cf[4]) & (slo[1] >= cf[5]) & (slo[2] >= cf[6])
+                    & (shi[0] <= cf[7]) & (shi[1] <= cf[8]) & (shi[2] <= cf[9]);
+    };
+    bool in = inside();
+    const uint64_t out = __ballot(seg_ok & !in);
+    const uint32_t nout = (uint32_t)__popcll(out);
+    if (nout == 0u || 4u * nout <= (uint32_t)__popcll(act)) return in ? SKEL_BIT : b.root;
+
+    // rebuild: R = every direction from the origins of this call's finite segments, plus slack
+    if (lane == first)
+    {
+        cw[2] = 0u;
+        cf[10] = cf[11] = cf[12] = INFINITY;
+        cf[13] = cf[14] = cf[15] = -INFINITY;
+    }
+    ucut_sync();
+    if (seg_ok)
+    {
+        const float reach = max_t * __builtin_sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]) * 1.0001f + 0.05f * max_t;
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+        {
+            atomicMin(&cf[10 + a], o[a] - reach);
+            atomicMax(&cf[13 + a], o[a] + reach);
+        }
+    }
+    ucut_sync();
+    float rlo[3], rhi[3], lo[3], hi[3], mag = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+    {
+        rlo[a] = cf[10 + a];
+        rhi[a] = cf[13 + a];
+        mag = fmaxf(mag, fmaxf(fabsf(rlo[a]), fabsf(rhi[a])));
+    }
+    // R grown by a margin far above a slab test's float error: every box a contained ray passes meets it
+    const float m = 1e-4f * (1.0f + mag);
+    bool finite = true;
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+    {
+        lo[a] = rlo[a] - m;
+        hi[a] = rhi[a] + m;
+        finite = finite & __builtin_isfinite(lo[a]) & __builtin_isfinite(hi[a]);
+    }
+    // (a binary tree over n leaf-ordered primitives has fewer than n pairs: pair links stay below SKEL_BIT)
+    if (!finite || (b.root & LEAF_BIT) || b.num_prims >= SKEL_BIT) return b.root;
+    // the skeleton, breadth first: record 0 for the root, then entries expanded in order while the
+    // records and the entries below them fit
+    const float4* pairs = static_cast<const float4*>(b.pairs);
+    float w[14];
+    ucut_compress(pairs, b.root, lo, hi, w);
+    uint32_t n = 1, entries = ucut_put(cw, 0, w, lo, hi, lane == first);
+    ucut_sync();
+#pragma unroll 1
+    for (uint32_t k = 0; k < n && n < UCUT_NODES; ++k)
+    {
+#pragma unroll 1
+        for (uint32_t c = 0; c < 2u && n < UCUT_NODES; ++c)
+        {
+            const uint32_t g = (uint32_t)__builtin_amdgcn_readfirstlane((int)cw[16u + 16u * k + 12u + c]);
+            if ((g & LEAF_BIT) || (g & SKEL_BIT)) continue;            // leaf, outside R, or expanded
+            float v[14];
+            ucut_compress(pairs, g, lo, hi, v);
+            uint32_t e = 0;
+            for (uint32_t cc = 0; cc < 2u; ++cc)
+                e += (ucut_meets(v, cc, lo, hi) && !(__float_as_uint(v[12 + cc]) & LEAF_BIT)) ? 1u : 0u;
+            if (entries - 1u + e > UCUT_ENTRIES) continue;
+            ucut_put(cw, n, v, lo, hi, lane == first);
+            if (lane == first) cw[16u + 16u * k + 12u + c] = SKEL_BIT | n;
+            entries = entries - 1u + e;
+            n += 1u;
+            ucut_sync();
+        }
+    }
+    if (lane == first)
+    {
+        cw[0] = (uint32_t)key;
+        cw[1] = (uint32_t)(key >> 32);
+        cf[4] = rlo[0]; cf[5] = rlo[1]; cf[6] = rlo[2];
+        cf[7] = rhi[0]; cf[8] = rhi[1]; cf[9] = rhi[2];
+        cw[2] = n;
+    }
+    ucut_sync();
+    in = inside();
+    return in ? SKEL_BIT : b.root;
+}
+
+template <bool FAST, bool CUT = false, typename CullT, typename Leaf>
+__device__ inline void walk_slab(vrh_scene_view const& b, vrh::dev::ray_t const& r, float max_t, CullT const& cull_t, Leaf&& leaf,
+                                 uint32_t start = 0xFFFFFFFFu)
 {
     const float4* pairs = static_cast<const float4*>(b.pairs);
     vrh::dev::lds_stack st = user_stack();
-    st.push(b.root);
+    st.push(CUT ? start : b.root);
     while (!st.empty())
     {
         uint32_t link = st.pop();
@@ -439,11 +669,21 @@ __device__ inline void walk_slab(vrh_scene_view const& b, vrh::dev::ray_t const&
         {
             float4 q0, q1, q2;
             float2 q3;
-            fetch_pair(pairs, link, q0, q1, q2, q3);
+            if (CUT && (link & SKEL_BIT))
+            {
+                // a skeleton record (user_cut_entry): the pair record's own bits, from LDS
+                const float4* nr = reinterpret_cast<const float4*>(user_cut_area() + 16u + 16u * (link & 0xFFu));
+                q0 = nr[0]; q1 = nr[1]; q2 = nr[2];
+                const float4 l = nr[3];
+                q3 = make_float2(l.x, l.y);
+            }
+            else
+                fetch_pair(pairs, link, q0, q1, q2, q3);
             bool b0, b1;
             float tn0, tn1;
             vrh::dev::box_pair<FAST>(q0, q1, q2, r, cull_t(), max_t, b0, b1, tn0, tn1);
             const uint32_t l0 = __float_as_uint(q3.x), l1 = __float_as_uint(q3.y);
+            if (CUT) { b0 = b0 & (l0 != SKEL_NONE); b1 = b1 & (l1 != SKEL_NONE); }   // outside R: missed
             if (!(b0 | b1)) { at_leaf = false; break; }                               // pop
             const bool go0 = (b0 & b1) ? (tn0 < tn1) : b0;                             // ties -> child 1
             if (b0 & b1) st.push(go0 ? l1 : l0);
@@ -531,6 +771,17 @@ __device__ inline void walk(vrh_scene_view const& b, Ray const& ray, float max_t
     const bool fast = b.finite_bounds && vrh::dev::finite_ray(r);
     if constexpr (ANY && !VRH_USER_BINARY_ANYHIT)
         if (fast && b.quads && walk_quads(b, r, max_t, leaf)) return;
+    if constexpr (ANY && VRH_USER_ANYHIT_CUT)
+    {
+        // the entry cut needs the LDS area user_render provides after the stacks of its 64-thread blocks
+        if (blockDim.x * blockDim.y * blockDim.z == 64u)
+        {
+            const uint32_t start = user_cut_entry(b, r, max_t, fast);
+            if (fast) walk_slab<true, true>(b, r, max_t, cull_t, leaf, start);
+            else walk_slab<false>(b, r, max_t, cull_t, leaf);
+            return;
+        }
+    }
     if (fast) walk_slab<true>(b, r, max_t, cull_t, leaf);
     else walk_slab<false>(b, r, max_t, cull_t, leaf);
 }
@@ -1191,6 +1442,7 @@ template <typename K, uint32_t SK = VRH_SAMPLER_UNIFORM, uint32_t SN = 1, uint32
 __global__ __launch_bounds__(64) VRH_USER_OCC void user_render(K kernel, user_frames<NC> f)
 {
     const uint32_t lane = threadIdx.y * 8u + threadIdx.x;
+    if (VRH_USER_ANYHIT_CUT && lane == 0u) user_cut_area()[2] = 0u;     // no any_hit entry cut yet
     uint32_t q = xcc_id();
     for (uint32_t tried = 0; tried < 8u; ++tried, q = (q + 1u) & 7u)
     {
@@ -1218,7 +1470,7 @@ __global__ __launch_bounds__(64) VRH_USER_OCC void user_render(K kernel, user_fr
 template <typename K, uint32_t SK, uint32_t SN, uint32_t NC>
 inline hipError_t launch_user_render(hip_context& ctx, K const& kernel, user_frames<NC>& f, hipStream_t stream)
 {
-    const size_t lds = size_t(64) * VRH_USER_STACK * sizeof(uint32_t);
+    const size_t lds = (size_t(64) * VRH_USER_STACK + (VRH_USER_ANYHIT_CUT ? UCUT_WORDS : 0u)) * sizeof(uint32_t);
     auto fn = user_render<K, SK, SN, NC>;
     check(vrh_ctx_user_queues(ctx.get(), &f.queues), "vrh_ctx_user_queues");
     int dev = 0, cus = 0, per_cu = 0;

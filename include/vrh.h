@@ -222,7 +222,7 @@ enum vrh_option {
     VRH_OPT_AO_SCHEDULE = 3,     /* refilling loop of a wave: 3 = one descend-to-leaf step per
                                     iteration, the only schedule (auto: 3).  Round 1's vote loop,
                                     item-loop AO and two-pass AO were removed (never faster,
-                                    profiles/r01_ab*), and in round 2 the primary-visibility item
+                                    profiles/r01/ab*), and in round 2 the primary-visibility item
                                     loop (4, the old sphere default: 6-9 % slower than the step loop,
                                     profiles/r02_ab/ab18_sphere_schedule.log); 4 returns
                                     VRH_ERR_UNSUPPORTED                                             */

@@ -21,6 +21,7 @@
 //                                                                frames() launch equal three frame() calls
 //   user_kernels draws <grid> <W> <H> <outdir> <frame>          kernel(r, random_sampler<float>&): draws
 //                                                                0, 1, 2, 15 of the pixel's sampler as colour
+//   user_kernels anyrec <grid> <W> <H> <outdir> <frame> [radius] the AO lambda's any_hit hit records, hashed
 //   user_kernels rsao  <grid> <W> <H> <outdir> <frame>          the AO example's kernel (ao/main.cpp:183-246)
 //                                                                with standalone.h's random_sampler and
 //                                                                cosine_sample_hemisphere; depth = hit t
@@ -337,6 +338,47 @@ int main(int argc, char** argv)
             rt.download(out.data(), nullptr, t.data());
             write_file(outdir + "/color.bin", out.data(), out.size() * 4);
             write_file(outdir + "/t.bin", t.data(), t.size() * 4);
+            return 0;
+        }
+        else if (mode == "anyrec")
+        {
+            // the hit RECORDS of the AO lambda's any_hit calls, not only hit / miss: per pixel an
+            // FNV-1a hash over (hit, prim_id, t bits) of the 8 records (colour x), the number of hits
+            // (colour y) -- any_hit returns the first hit in the walk's visiting order, so a build
+            // with the entry cut (VRH_USER_ANYHIT_CUT) must give the records of the build without it
+            const unsigned frame_num = unsigned(strtoul(argv[6], nullptr, 10));
+            const float radius = argc > 7 ? float(atof(argv[7])) : 0.1f;
+            hip_bvh_ref const* begin = one.r;
+            hip_bvh_ref const* end = one.r + one.n;
+            sched.frame([=] __device__ (ray r, random_sampler<float>& samp) -> result_record<float>
+            {
+                result_record<float> result;
+                result.color = vec4(0.0f, 0.0f, 0.0f, 0.0f);
+                auto hr = closest_hit(r, begin, end);
+                if (hr.hit)
+                {
+                    hr.isect_pos = r.ori + r.dir * hr.t;
+                    vec3 n = get_normal(dnormals, hr);
+                    vec3 u, v, w = n;
+                    make_orthonormal_basis(u, v, w);
+                    uint32_t h = 2166136261u, hits = 0;
+                    auto mix = [&](uint32_t x) { for (int k = 0; k < 4; ++k) { h ^= (x >> (8 * k)) & 0xFFu; h *= 16777619u; } };
+                    for (int i = 0; i < 8; ++i)
+                    {
+                        auto sp = cosine_sample_hemisphere(samp.next(), samp.next());
+                        auto dir = normalize(sp.x * u + sp.y * v + sp.z * w);
+                        ray ao(hr.isect_pos + dir * 1E-3f, dir);
+                        auto rec = any_hit(ao, begin, end, radius);
+                        mix(rec.hit ? 1u : 0u);
+                        if (rec.hit) { mix(uint32_t(rec.prim_id)); mix(__float_as_uint(rec.t)); hits += 1u; }
+                    }
+                    result.color = vec4(__uint_as_float(h), float(hits), 1.0f, 1.0f);
+                }
+                return result;
+            }, sparams, frame_num);
+            std::vector<float> out(4 * size_t(W) * H);
+            rt.download(out.data());
+            write_file(outdir + "/color.bin", out.data(), out.size() * 4);
             return 0;
         }
         else if (mode == "bench")

@@ -66,6 +66,31 @@ def test_user_ao_kernel_shared_anyhit_matches_reference(tmp_path, golden, oracle
                                        ("color", "color_hash")])
 
 
+CUT_BIN = os.path.join(ROOT, "build", "tests", "uk_cut")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grid,W,H,frame,radius", [(200, 320, 180, 0, 0.1), (200, 320, 180, 5, 0.4),
+                                                   (708, 1920, 1080, 2, 0.1), (64, 160, 90, 1, 2.0)])
+def test_anyhit_entry_cut_returns_reference_order_records(tmp_path, grid, W, H, frame, radius):
+    """The opt-in any_hit entry cut (hip_kernels.h VRH_USER_ANYHIT_CUT=1, user_cut_entry: a skeleton of
+    the BVH's top in LDS, chains skipped only where boxes nest) walks the same leaves in the same order
+    as the walk from the root: every any_hit call of the AO lambda returns the same hit RECORD (prim id
+    and t of the first hit found), not only the same hit / miss -- against the default build."""
+    assert os.path.exists(CUT_BIN), "run __graft_entry__.build() (make -C visionaray_amd cpp_tests)"
+    outs = []
+    for b in (CUT_BIN, BIN):
+        d = tmp_path / os.path.basename(b)
+        d.mkdir()
+        subprocess.run([b, "anyrec", str(grid), str(W), str(H), str(d), str(frame), str(radius)], check=True,
+                       capture_output=True, text=True, timeout=120)
+        outs.append(np.fromfile(d / "color.bin", np.float32).reshape(-1, 4))
+    cut, ref = outs
+    assert float((ref[:, 1] > 0).mean()) > 0.01, "the case must have occluded AO rays"
+    bad = np.flatnonzero(np.any(cut.view(np.uint32) != ref.view(np.uint32), axis=1))
+    assert bad.size == 0, f"{bad.size} pixels' any_hit records differ, first {bad[:8].tolist()}"
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["mask_hf200_320x180", "mask_hf64_160x90"])
 def test_user_mask_intersector_matches_reference(tmp_path, golden, oracle_mod, case):

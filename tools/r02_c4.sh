@@ -1,6 +1,6 @@
 #!/bin/bash
 # C4 (hf10M primary + 8 AO, one GPU) before / after the round-2 AO defaults: PMC traffic and
-# memory-path passes at 8 frames per launch (as profiles/r01_c4_pmc/), then bench.py on C2, C4, C5.
+# memory-path passes at 8 frames per launch (as the round-1 memory-path passes), then bench.py on C2, C4, C5.
 # "before" = the round-1 AO settings (ao_gate off, binary any-hit records, no pop on miss).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp

@@ -8,7 +8,7 @@ OUT=${OUT:-gpurun_out/r04/user}; mkdir -p $OUT
 for rep in $(seq 1 ${REPS:-2}); do
   for F in ${FS:-1 32}; do
     L=20; [ $F -gt 1 ] && L=4
-    for b in ${BINS:-build/tests/user_kernels oracle/_ref/ref_kernels}; do
+    for b in ${BINS:-build/tests/user_kernels build/tests/uk_nocut oracle/_ref/ref_kernels oracle/_ref/ref_kernels_nocut}; do
       [ -x $b ] || continue
       case $b in
         *ref_kernels*) r=$(timeout -k 10 120 $b bench hf1M 1920 1080 $L $F) ;;

@@ -140,7 +140,7 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
     case VRH_OPT_WIDE_ANYHIT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: wide any-hit is 1 (on) or 2 (off)"); ctx->opt_wide = int(value); break;
     case VRH_OPT_DESCENT_CAP: ctx->opt_dcap = int(value); break;
     case VRH_OPT_COOP_FETCH:
-        // the cooperative quad fetch was removed in round 2 (measured slower, profiles/r01_ab_nocoop.log)
+        // the cooperative quad fetch was removed in round 2 (measured slower, profiles/r01/ab_nocoop.log)
         VRH_CHECK(value == 0 || value == 2, "vrh_ctx_set_option: cooperative fetch was removed (2 = off is accepted)");
         if (value == 1) return VRH_ERR_UNSUPPORTED;
         break;
@@ -238,7 +238,7 @@ VRH_API int vrh_scene_upload(vrh_ctx* ctx, const void* nodes_v, uint32_t num_nod
     }
 
     // -- cache-line pairing (VRH_OPT_PAIR_LAYOUT = 1; auto off: measured neutral, within 1.3 %,
-    // profiles/r01_ab_layout.log): re-lay the pair records in a depth-first
+    // profiles/r01/ab_layout.log): re-lay the pair records in a depth-first
     // preorder that puts each pair's child-0 pair right after it, so a parent and a child share a
     // 128-B line on half of the descent steps (31 % in the builder's order).  Links are renumbered;
     // the tree, the traversal order and every result are unchanged.
@@ -1027,10 +1027,10 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     // frames in flight on the step loop (primary / AO, uncounted): the BATCH instantiation
     if (lc.sched == 0 && num_frames > 1 && !lc.count && lc.epi == 0 && !hmask) lc.sched = 3;
     // shading epilogues: no VGPR cap (their lane state spills at 6 waves/SIMD; measured faster at 4,
-    // profiles/r01_shade/shade_bench.jsonl), except whitted, whose bounce surface lives in LDS (vrh_shade.h):
+    // profiles/r01/shade/shade_bench.jsonl), except whitted, whose bounce surface lives in LDS (vrh_shade.h):
     // 96 VGPRs without spills, 5 waves/SIMD, +0.7-2.1 % over 4 (profiles/r03_ab/whitted/); AO on the
     // step loop: 5 waves/SIMD (96 VGPRs, no spills: 4-6 % faster than 6 with 18 spilled VGPRs); primary
-    // visibility: 6 (profiles/r01_ab_waves/); BVH lists run at these defaults
+    // visibility: 6 (profiles/r01/ab_waves/); BVH lists run at these defaults
     lc.occ = ctx->opt_occ ? ctx->opt_occ : whitted ? 5 : lc.epi ? 1 : lc.ao ? 5 : 6;
     if (sp) lc.occ = lc.ao ? 5 : 6;                    // the sampler instances exist at the defaults
     if (list) lc.occ = ao ? 5 : 6;
@@ -1080,7 +1080,7 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     p.num_roots = sc->num_roots;
     for (uint32_t i = 0; i < sc->num_roots; ++i) p.roots[i] = sc->roots[i];
     p.step_limit = sc->info.num_nodes + sc->info.num_indices + 16u;
-    // measured: profiles/r01_ab (AO: refill at 32 free lanes), profiles/r01_ab_primary (primary
+    // measured: profiles/r01/ab (AO: refill at 32 free lanes), profiles/r01/ab_primary (primary
     // visibility: pop on a miss and a cap of 8 visits per descent step, +6 % on hf1M and +36 % on
     // hf10M; both hurt AO)
     const bool primary_step = !lc.ao && lc.epi == 0;
@@ -1096,7 +1096,7 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     p.refill_min_primary = ctx->opt_refill ? uint32_t(ctx->opt_refill)
                          : (primary_step && num_frames > 1) ? 16u : lc.epi ? refill_shade : 1u;
     p.descent_cap = ctx->opt_dcap ? uint32_t(ctx->opt_dcap) : primary_step ? 8u : 0xFFFFFFFFu;
-    // shading epilogues (simple / multi_hit / whitted) pop on a miss too: +4-7 % (profiles/r01_shade/)
+    // shading epilogues (simple / multi_hit / whitted) pop on a miss too: +4-7 % (profiles/r01/shade/)
     // AO (step loop): the tile's AO rays wait for its primaries (ao_gate), any-hit rays descend the
     // 4-wide records and primaries pop on a miss -- together +6 % on hf1M and +10 % on hf10M
     // (profiles/r02_ab/ab4_c4opts.log); each alone is within +-2 %
