@@ -505,7 +505,11 @@ def main():
                 "counted": {"distinct_16B_pieces_per_launch": round(pieces_launch),
                             "distinct_16B_pieces_per_ray": round(float(cstats["l1_requests"]) / n_rays, 3),
                             "vmem_instrs_per_ray": round(float(cstats["vmem_instrs"]) / n_rays, 3),
-                            "lines128_per_vmem_instr": round(float(cstats["l1_lines"]) / max(float(cstats["vmem_instrs"]), 1.0), 3)},
+                            "lines128_per_vmem_instr": round(float(cstats["l1_lines"]) / max(float(cstats["vmem_instrs"]), 1.0), 3),
+                            # the vector L1's 4-lane merging: accesses as the lanes sit (the model of
+                            # TCP_TOTAL_CACHE_ACCESSES) and if lanes wanting one piece sat together
+                            "group4_accesses_per_launch": round(float(cstats.get("l1_group_accesses", 0)) * frame_share),
+                            "ideal_group_accesses_per_launch": round(float(cstats.get("l1_ideal_accesses", 0)) * frame_share)},
                 "hbm_algorithmic": {
                     "bytes_per_ray": round(bytes_per_ray, 1), "box_tests_per_ray": round(n_box / n_rays, 3),
                     "prim_tests_per_ray": round(n_prim / n_rays, 3), "achieved_gbs": round(hbm_alg, 1),

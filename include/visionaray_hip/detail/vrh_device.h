@@ -255,6 +255,9 @@ struct test_counts
     // the instruction count (`vmem`); kept by the wave's first active lane, summed over lanes at the
     // end.  A divergence diagnostic -- the hardware's TCP access count is measured by PMC instead.
     uint64_t reqs, lines, vmem;
+    // the vector L1's merging (counting variant): acc4 = distinct pieces per aligned 4-lane group,
+    // summed over groups (the hardware's accesses); acc_ideal = per distinct piece ceil(lanes / 4)
+    uint64_t acc4, acc_ideal;
 };
 
 // distinct values of `key` over the active lanes (wave-uniform result)
@@ -293,17 +296,53 @@ __device__ __forceinline__ uint32_t distinct_keys_per_quarter(uint64_t key)
     return n;
 }
 
+// distinct values of `key` within each aligned 4-lane group, summed, and sum over distinct values of
+// ceil(lanes with it / 4) (wave-uniform results): the vector L1's accesses of a 16-B-per-lane load
+// as the lanes sit, and as they would if the lanes wanting one piece sat together
+__device__ __forceinline__ void group_accesses(uint64_t key, uint32_t& acc4, uint32_t& ideal)
+{
+    const uint64_t act = __ballot(true);
+    const uint32_t lane = __lane_id();
+    // this lane is the first (lowest) active lane of its group with its key
+    bool first = true;
+#pragma unroll
+    for (uint32_t k = 1; k < 4; ++k)
+    {
+        const uint32_t o = (lane & ~3u) + ((lane + k) & 3u);          // the other lanes of the group
+        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)key, (int)o), hi = (uint32_t)__shfl((int)(uint32_t)(key >> 32), (int)o);
+        const bool same = ((act >> o) & 1ull) && ((((uint64_t)hi << 32) | lo) == key);
+        first = first && !(same && o < lane);
+    }
+    acc4 = (uint32_t)__popcll(__ballot(first));
+    uint64_t rem = act;
+    uint32_t n = 0;
+    while (rem)
+    {
+        const int f = __builtin_ctzll(rem);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, f);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(key >> 32), f);
+        const uint64_t m = __ballot(key == (((uint64_t)hi << 32) | lo)) & act;
+        n += ((uint32_t)__popcll(m) + 3u) / 4u;
+        rem &= ~m;
+    }
+    ideal = n;
+}
+
 // one wave-level vector-memory instruction whose lanes access `bytes` (<= 16) at `p`: account for it
 // in the L1 model (counting variant only; called by the active lanes)
 __device__ __forceinline__ void count_vmem(test_counts& c, const void* p, uint32_t times = 1u)
 {
     const uint64_t a = (uint64_t)(uintptr_t)p;
     const uint32_t l = distinct_keys(a >> 7), q = distinct_keys_per_quarter(a >> 4);
+    uint32_t g4, gi;
+    group_accesses(a >> 4, g4, gi);
     if (__lane_id() == (uint32_t)__builtin_ctzll(__ballot(true)))
     {
         c.lines += (uint64_t)l * times;
         c.reqs += (uint64_t)q * times;
         c.vmem += times;
+        c.acc4 += (uint64_t)g4 * times;
+        c.acc_ideal += (uint64_t)gi * times;
     }
 }
 

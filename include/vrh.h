@@ -174,6 +174,12 @@ typedef struct {
      * divergence; rocprofv3's TCP_TOTAL_CACHE_ACCESSES counts the hardware's own requests (about
      * 2.2x l1_requests on the AO kernel, profiles/pmc_traffic.json) */
     uint64_t l1_lines, l1_requests, vmem_instrs;
+    /* the same instructions under the vector L1's own merging (lanes that want one 16-B piece share
+     * an access only inside an aligned group of 4 lanes; tools/micro/l1_roof.hip): l1_group_accesses
+     * = the sum over 4-lane groups of the distinct pieces in the group -- the model of
+     * TCP_TOTAL_CACHE_ACCESSES -- and l1_ideal_accesses = the sum over distinct pieces of
+     * ceil(lanes wanting it / 4), the count if the lanes wanting one piece sat together in groups */
+    uint64_t l1_group_accesses, l1_ideal_accesses;
 } vrh_frame_stats;
 
 typedef struct {
@@ -236,6 +242,13 @@ enum vrh_option {
                                     order (cluster, frame, tile: the frames in flight of a cluster
                                     back to back) (auto: 4 with frames in flight for AO, 3 with frames
                                     in flight for scenes > 256 MB, else 1)                         */
+    VRH_OPT_QUAD_REFILL = 24,    /* AO step loop, lane layout (2-bit mask): 1 = rays only to aligned 4-lane
+                                    groups whose lanes are all idle (4 consecutive rays each), 2 = a
+                                    tile's pixels in 2x2 blocks (auto: 0)                          */
+    VRH_OPT_GROUP_UNITS = 25,    /* AO frames in flight with blocks of several waves (VRH_OPT_BLOCK_THREADS)
+                                    and cluster order: the block's waves take chunks of this many
+                                    (tile, frame) units together, frames of one tile fastest, so they
+                                    share the CU's L1 (1..1024; auto: 0 = off)                     */
     VRH_OPT_CLUSTER_TILES = 23,  /* VRH_OPT_XCD_QUEUES 4: 8x8 tiles per cluster, 1..1024 (auto: 8) */
     VRH_OPT_REFILL_MIN = 8,      /* free lanes (1..64) before finished rays are retired and idle
                                     lanes refilled (auto: AO 24, 28 for scenes above 256 MB)      */

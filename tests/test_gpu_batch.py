@@ -88,7 +88,10 @@ def test_batch_spheres(ctx, n):
 
 @pytest.mark.parametrize("opts", [{"ao_schedule": 3}, {"refill_min": 1}, {"xcd_queues": 2}, {"xcd_queues": 1},
                                   {"wide_anyhit": 1}, {"xcd_queues": 4}, {"xcd_queues": 4, "cluster_tiles": 3},
-                                  {"xcd_queues": 4, "cluster_tiles": 1}, {"xcd_queues": 4, "cluster_tiles": 1024}])
+                                  {"xcd_queues": 4, "cluster_tiles": 1}, {"xcd_queues": 4, "cluster_tiles": 1024},
+                                  {"quad_refill": 3}, {"block_threads": 256, "group_units": 3},
+                                  {"block_threads": 256, "group_units": 1024},
+                                  {"block_threads": 320, "group_units": 7, "cluster_tiles": 3}])
 def test_batch_under_other_schedules(ctx, opts):
     for k, v in opts.items():
         ctx.set_option(k, v)
@@ -111,9 +114,12 @@ def test_batch_packed_shards_cluster_order(ctx, count, index, n):
     ctx.set_option("cluster_tiles", 7)
     try:
         check_batch(ctx, "hf200", 320, 180, "ao", n, shard=_capi.vrh_shard(index, count, 1, 0))
+        ctx.set_option("block_threads", 256)
+        ctx.set_option("group_units", n)       # block-shared hand-out of one tile's frames
+        check_batch(ctx, "hf200", 320, 180, "ao", n, shard=_capi.vrh_shard(index, count, 1, 0))
     finally:
-        ctx.set_option("xcd_queues", 0)
-        ctx.set_option("cluster_tiles", 0)
+        for o in ("xcd_queues", "cluster_tiles", "block_threads", "group_units"):
+            ctx.set_option(o, 0)
 
 
 def test_batch_arguments_are_checked(ctx):

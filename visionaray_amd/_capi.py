@@ -55,6 +55,8 @@ VRH_OPT_SCALAR_FETCH, VRH_OPT_PAIR_LAYOUT, VRH_OPT_AO_GATE, VRH_OPT_WAVE_TIMES =
 VRH_OPT_AO_CUT = 20
 VRH_OPT_AO_SHARE = 22
 VRH_OPT_CLUSTER_TILES = 23
+VRH_OPT_QUAD_REFILL = 24
+VRH_OPT_GROUP_UNITS = 25
 VRH_OPT_AO_STEAL = 21
 VRH_MAX_TIMED_FRAMES = 1024
 VRH_MAX_SCENE_LIST = 8
@@ -90,7 +92,8 @@ class vrh_frame_stats(C.Structure):
                 ("frames", C.c_uint32),
                 ("wave_steps", C.c_uint64), ("busy_lane_steps", C.c_uint64), ("wave_box_iters", C.c_uint64),
                 ("wave_prim_iters", C.c_uint64), ("wave_box_uniform_iters", C.c_uint64),
-                ("l1_lines", C.c_uint64), ("l1_requests", C.c_uint64), ("vmem_instrs", C.c_uint64)]
+                ("l1_lines", C.c_uint64), ("l1_requests", C.c_uint64), ("vmem_instrs", C.c_uint64),
+                ("l1_group_accesses", C.c_uint64), ("l1_ideal_accesses", C.c_uint64)]
 
 
 class vrh_scene_view(C.Structure):

@@ -163,7 +163,8 @@ class Context:
                  "descent_cap": capi.VRH_OPT_DESCENT_CAP, "pop_on_miss": capi.VRH_OPT_POP_ON_MISS,
                  "coop_fetch": capi.VRH_OPT_COOP_FETCH, "scalar_fetch": capi.VRH_OPT_SCALAR_FETCH,
                  "pair_layout": capi.VRH_OPT_PAIR_LAYOUT, "ao_gate": capi.VRH_OPT_AO_GATE, "ao_cut": capi.VRH_OPT_AO_CUT, "wave_times": capi.VRH_OPT_WAVE_TIMES,
-                 "ao_share": capi.VRH_OPT_AO_SHARE, "cluster_tiles": capi.VRH_OPT_CLUSTER_TILES}
+                 "ao_share": capi.VRH_OPT_AO_SHARE, "cluster_tiles": capi.VRH_OPT_CLUSTER_TILES,
+                 "quad_refill": capi.VRH_OPT_QUAD_REFILL, "group_units": capi.VRH_OPT_GROUP_UNITS}
         capi.check("vrh_ctx_set_option", self.handle, names.get(option, option), int(value))
 
     def last_frame_stats(self):

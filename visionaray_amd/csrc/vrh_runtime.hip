@@ -160,6 +160,8 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
     case VRH_OPT_WAVES_PER_SIMD: VRH_CHECK(value == 0 || value == 1 || value == 5 || value == 6 || value == 8, "vrh_ctx_set_option: waves per SIMD is 1, 5, 6 or 8"); ctx->opt_occ = int(value); break;
     case VRH_OPT_EXACT_MINMAX: ctx->opt_exact_minmax = value ? 1 : 0; break;
     case VRH_OPT_XCD_QUEUES: VRH_CHECK(value <= 4, "vrh_ctx_set_option: xcd queues is 1 (strips), 2 (off), 3 (band-interleaved) or 4 (cluster order)"); ctx->opt_xcd_queues = int(value); break;
+    case VRH_OPT_GROUP_UNITS: ctx->opt_group = int(value); break;
+    case VRH_OPT_QUAD_REFILL: VRH_CHECK(value <= 3, "vrh_ctx_set_option: quad refill is a 2-bit mask"); ctx->opt_quad = int(value); break;
     case VRH_OPT_CLUSTER_TILES: VRH_CHECK(value <= 1024, "vrh_ctx_set_option: cluster tiles is 1..1024 (0 = auto)"); ctx->opt_cluster = int(value); break;
     default: set_error("vrh_ctx_set_option: unknown option"); return VRH_ERR_INVALID;
     }
@@ -1168,6 +1170,11 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
                  : ctx->opt_xcd_queues == 3 ? 2u : ctx->opt_xcd_queues == 4 ? 3u
                  : cluster_auto ? 3u : (band_auto ? 2u : 1u);
     p.cluster = ctx->opt_cluster ? uint32_t(ctx->opt_cluster) : 8u;
+    p.quad_refill = uint32_t(ctx->opt_quad);
+    // block-shared hand-out: blocks of several waves, frames in flight, cluster order (the units of a
+    // chunk are one tile's frames)
+    p.group = (ctx->opt_group && lc.ao && !list && lc.block > 64 && num_frames > 1 && p.xcd_queues == 3u)
+            ? uint32_t(ctx->opt_group) : 0u;
     if (shade)
     {
         p.shade.materials = k->shading->materials;
@@ -1332,7 +1339,7 @@ VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats)
     VRH_HIP(hipEventSynchronize(ctx->ev_stop[ctx->last_slot]));
     float ms = 0.0f;
     VRH_HIP(hipEventElapsedTime(&ms, ctx->ev_start[ctx->last_slot], ctx->ev_stop[ctx->last_slot]));
-    unsigned long long c[COUNTERS_LINES + 3];
+    unsigned long long c[COUNTERS_LINES + 5];
     VRH_HIP(hipMemcpy(c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     ctx->last.kernel_ms = ms;
     ctx->last.rays = c[1];
@@ -1347,6 +1354,8 @@ VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats)
     ctx->last.l1_lines = c[COUNTERS_LINES];
     ctx->last.vmem_instrs = c[COUNTERS_LINES + 1];
     ctx->last.l1_requests = c[COUNTERS_LINES + 2];
+    ctx->last.l1_group_accesses = c[COUNTERS_LINES + 3];
+    ctx->last.l1_ideal_accesses = c[COUNTERS_LINES + 4];
     *stats = ctx->last;
     if (c[5] & 1ull) { set_error("traversal step guard tripped: corrupt BVH (rays were cut short)"); return VRH_ERR_HIP; }
     return VRH_OK;
