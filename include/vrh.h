@@ -217,7 +217,7 @@ VRH_API int vrh_ctx_get_stream(const vrh_ctx* ctx, int* hip_device, void** hip_s
 
 /* launch tuning (per context; 0 = automatic).  Results never depend on these. */
 enum vrh_option {
-    VRH_OPT_BLOCK_THREADS = 1,   /* threads per block, multiple of 64 (auto: 64)                  */
+    VRH_OPT_BLOCK_THREADS = 1,   /* threads per block, a multiple of 64 up to 256 (auto: 64)       */
     VRH_OPT_STACK_CAP = 2,       /* traversal stack entries per lane kept in LDS; entries beyond
                                     them (up to the BVH depth) go to a global overflow block, so
                                     any value is exact.  Primary / AO step loops at their default
@@ -242,13 +242,11 @@ enum vrh_option {
                                     order (cluster, frame, tile: the frames in flight of a cluster
                                     back to back) (auto: 4 with frames in flight for AO, 3 with frames
                                     in flight for scenes > 256 MB, else 1)                         */
-    VRH_OPT_QUAD_REFILL = 24,    /* AO step loop, lane layout (2-bit mask): 1 = rays only to aligned 4-lane
-                                    groups whose lanes are all idle (4 consecutive rays each), 2 = a
-                                    tile's pixels in 2x2 blocks (auto: 0)                          */
-    VRH_OPT_GROUP_UNITS = 25,    /* AO frames in flight with blocks of several waves (VRH_OPT_BLOCK_THREADS)
-                                    and cluster order: the block's waves take chunks of this many
-                                    (tile, frame) units together, frames of one tile fastest, so they
-                                    share the CU's L1 (1..1024; auto: 0 = off)                     */
+    VRH_OPT_QUAD_REFILL = 24,    /* removed in round 4 (measured slower, profiles/r04/ab/lane_layout/): AO rays
+                                    only to fully idle aligned 4-lane groups / 2x2 pixel order;
+                                    0 accepted, other values -> VRH_ERR_UNSUPPORTED                */
+    VRH_OPT_GROUP_UNITS = 25,    /* removed in round 4 (measured slower): block-shared hand-out of
+                                    one tile's frames; 0 accepted, other values -> VRH_ERR_UNSUPPORTED */
     VRH_OPT_CLUSTER_TILES = 23,  /* VRH_OPT_XCD_QUEUES 4: 8x8 tiles per cluster, 1..1024 (auto: 8) */
     VRH_OPT_REFILL_MIN = 8,      /* free lanes (1..64) before finished rays are retired and idle
                                     lanes refilled (auto: AO 24, 28 for scenes above 256 MB)      */

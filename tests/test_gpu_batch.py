@@ -89,9 +89,7 @@ def test_batch_spheres(ctx, n):
 @pytest.mark.parametrize("opts", [{"ao_schedule": 3}, {"refill_min": 1}, {"xcd_queues": 2}, {"xcd_queues": 1},
                                   {"wide_anyhit": 1}, {"xcd_queues": 4}, {"xcd_queues": 4, "cluster_tiles": 3},
                                   {"xcd_queues": 4, "cluster_tiles": 1}, {"xcd_queues": 4, "cluster_tiles": 1024},
-                                  {"quad_refill": 3}, {"block_threads": 256, "group_units": 3},
-                                  {"block_threads": 256, "group_units": 1024},
-                                  {"block_threads": 320, "group_units": 7, "cluster_tiles": 3}])
+                                  {"block_threads": 256}, {"block_threads": 192, "cluster_tiles": 3}])
 def test_batch_under_other_schedules(ctx, opts):
     for k, v in opts.items():
         ctx.set_option(k, v)
@@ -114,11 +112,8 @@ def test_batch_packed_shards_cluster_order(ctx, count, index, n):
     ctx.set_option("cluster_tiles", 7)
     try:
         check_batch(ctx, "hf200", 320, 180, "ao", n, shard=_capi.vrh_shard(index, count, 1, 0))
-        ctx.set_option("block_threads", 256)
-        ctx.set_option("group_units", n)       # block-shared hand-out of one tile's frames
-        check_batch(ctx, "hf200", 320, 180, "ao", n, shard=_capi.vrh_shard(index, count, 1, 0))
     finally:
-        for o in ("xcd_queues", "cluster_tiles", "block_threads", "group_units"):
+        for o in ("xcd_queues", "cluster_tiles"):
             ctx.set_option(o, 0)
 
 
@@ -139,3 +134,23 @@ def test_batch_arguments_are_checked(ctx):
     with pytest.raises(va.VrhError):
         va.render_batch(ctx, dev, rt, [bases[0], odd], kern)
     rt.close()
+
+
+def test_removed_hand_out_options_are_refused(ctx):
+    """Round 4's quad-coherent and block-shared hand-outs measured slower and were removed: 0 is
+    accepted, anything else is VRH_ERR_UNSUPPORTED (profiles/r04/ab/lane_layout/)."""
+    for opt in (_capi.VRH_OPT_QUAD_REFILL, _capi.VRH_OPT_GROUP_UNITS):
+        ctx.set_option(opt, 0)
+        with pytest.raises(_capi.VrhError) as e:
+            ctx.set_option(opt, 1)
+        assert e.value.code == _capi.VRH_ERR_UNSUPPORTED
+
+
+def test_block_threads_above_launch_bounds_rejected(ctx):
+    """The traversal kernels are compiled for <= 256 threads per block; a larger block is refused at
+    vrh_ctx_set_option instead of failing the launch."""
+    for bad in (320, 512, 100):
+        with pytest.raises(_capi.VrhError):
+            ctx.set_option("block_threads", bad)
+    ctx.set_option("block_threads", 256)
+    ctx.set_option("block_threads", 0)

@@ -22,9 +22,6 @@ VARIANTS = {
     "global_queue": {"xcd_queues": 2},
     "band_interleaved_queues": {"xcd_queues": 3},
     "cluster_queues": {"xcd_queues": 4, "cluster_tiles": 5},
-    "quad_refill": {"quad_refill": 1},
-    "quad_refill_2x2": {"quad_refill": 3},
-    "pixels_2x2": {"quad_refill": 2},
     "step_wide": {"ao_schedule": 3, "wide_anyhit": 1},
     "step_wide_exact": {"ao_schedule": 3, "wide_anyhit": 1, "exact_minmax": 1},
     "step_cap1": {"ao_schedule": 3, "descent_cap": 1},
@@ -53,7 +50,7 @@ VARIANTS = {
 }
 OPTIONS = ("ao_schedule", "refill_min", "wide_anyhit", "exact_minmax", "descent_cap", "xcd_queues",
            "pop_on_miss", "scalar_fetch", "waves_per_simd", "pair_layout", "ao_gate",
-           "stack_cap", "ao_cut", "cluster_tiles", "quad_refill")
+           "stack_cap", "ao_cut", "cluster_tiles")
 
 
 @pytest.fixture(params=sorted(VARIANTS))

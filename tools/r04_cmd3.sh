@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out/r04q
 VC='[{"name":"default"},{"name":"q1","quad_refill":1},{"name":"q2","quad_refill":2},{"name":"q3","quad_refill":3}]'
-V='[{"name":"default"},{"name":"q1","quad_refill":1},{"name":"q3","quad_refill":3},{"name":"b256","block_threads":256},{"name":"g256","block_threads":256,"group_units":20},{"name":"g256q3","block_threads":256,"group_units":20,"quad_refill":3},{"name":"g320","block_threads":320,"group_units":20},{"name":"g640","block_threads":640,"group_units":20}]'
+V='[{"name":"default"},{"name":"q1","quad_refill":1},{"name":"q3","quad_refill":3},{"name":"b256","block_threads":256},{"name":"g256","block_threads":256,"group_units":20},{"name":"g256q3","block_threads":256,"group_units":20,"quad_refill":3},{"name":"g192","block_threads":192,"group_units":20},{"name":"g128","block_threads":128,"group_units":20}]'
 OUT=gpurun_out/r04q K='schedules or batch' STEPS='tests' tools/r04_session.sh || exit 1
 for s in hf1M hf10M; do
   VRH_AB="$VC" timeout -k 10 300 python tools/count_variants.py $s > gpurun_out/r04q/count_$s.log 2>&1 || exit 1

@@ -75,10 +75,6 @@ struct render_params
                               // band-interleaved (band, frame) units; 3: per-XCD strips in cluster
                               // order (cluster, frame, tile); 0: one global queue
     uint32_t cluster;         // xcd_queues 3: tiles per cluster (>= 1)
-    uint32_t group;           // AO step loop, blocks of several waves: units per block-shared chunk
-                              // (group_next: the block's waves take the frames of one tile together), 0 off
-    uint32_t quad_refill;     // AO step loop: bit 0 rays to fully idle aligned 4-lane groups only,
-                              // bit 1 pixels of a tile in 2x2 blocks (tile_pixel)
     uint32_t refill_min;      // retire / refill once this many lanes are free (AO step loop)
     uint32_t refill_min_primary;   // the same for the step loop's primary-only stream
     uint32_t ao_cut;          // AO step loop: any-hit rays start at the tile's cut of the 4-wide tree

@@ -75,15 +75,8 @@ __device__ __forceinline__ bool tile_pixel(const render_params& P, uint32_t id, 
     uint32_t lb = tile / P.tiles_x;               // local band
     uint32_t tx = tile - lb * P.tiles_x;
     uint32_t band = lb * P.shard_count + P.shard_index;
-    // pixel k of the tile: row-major, or (quad_refill bit 1) 2x2 blocks -- k = 4 q + j, block q of the
-    // tile's 4x4 blocks (row-major), j its pixel -- so that 4 consecutive pixels are a 2x2 block
-    uint32_t px = lane & 7u, in_band = lane >> 3;
-    if (P.quad_refill & 2u)
-    {
-        px = ((lane >> 1) & 6u) | (lane & 1u);
-        in_band = ((lane >> 3) & 6u) | ((lane >> 1) & 1u);
-    }
-    x = tx * TILE + px;
+    x = tx * TILE + (lane & 7u);
+    uint32_t in_band = lane >> 3;
     y = band * BAND + in_band;
     out_row = f * P.frame_rows + (P.packed ? lb * BAND + in_band : y);
     // the frame's scissor box, clamped to the image on the host (cuda_sched.inl:71: x < sb.x,
@@ -325,90 +318,6 @@ __device__ __forceinline__ uint32_t next_tile(const render_params& P, tile_queue
         tq.tried += 1u;
     }
     return NONE;
-}
-
-// Block-shared hand-out (render_params::group, blocks of several waves, frames in flight): the waves
-// of one block take the frames of ONE tile together, so they trace the same nodes and triangles at
-// the same time and share the CU's vector L1 (the per-XCD queues only share the XCD's L2).  Unit t of
-// XCD queue q is, within strip q of the launch's bands, (band, cluster of P.cluster tiles, tile,
-// frame) with the frame fastest; the block takes P.group consecutive units at a time from the queue
-// (stealing from the other queues as next_tile does) into a chunk its waves drain through one 64-bit
-// LDS word { next (low 32 bits), queue << 29 | first unit (high) }: an atomic add on it hands out a
-// unit and the chunk it belongs to in one operation, so a refill (an atomic exchange by the one wave
-// that holds the lock word) can never hand out a unit twice.  Every unit of every queue is handed out
-// exactly once: a chunk's units past the end of its queue are skipped (the queue is then dry).
-__device__ __forceinline__ uint32_t gu(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
-__device__ __forceinline__ uint32_t group_units(const render_params& P, uint32_t q, uint32_t& b0)
-{
-    const uint32_t nb = P.num_tiles / P.tiles_x;
-    b0 = (uint32_t)(((uint64_t)nb * q) >> 3);
-    const uint32_t b1 = (uint32_t)(((uint64_t)nb * (q + 1u)) >> 3);
-    return (b1 - b0) * P.tiles_x * P.num_frames;
-}
-__device__ __forceinline__ uint32_t group_decode(const render_params& P, uint32_t t, uint32_t b0)
-{
-    const uint32_t tx = P.tiles_x, F = P.num_frames, C = P.cluster;
-    const uint32_t per_band = tx * F;
-    const uint32_t lb = t / per_band;
-    const uint32_t r = t - lb * per_band;
-    const uint32_t c = r / (C * F);
-    const uint32_t r2 = r - c * C * F;
-    const uint32_t j = r2 / F;                     // tile of the cluster (every tile holds F units)
-    const uint32_t f = r2 - j * F;
-    return (f << TILE_FRAME_SHIFT) | ((b0 + lb) * tx + c * C + j);
-}
-constexpr uint32_t GQ_LOCK = 2, GQ_FREE = 0u, GQ_TAKEN = 1u, GQ_DRY = 2u;
-__device__ __forceinline__ uint32_t group_next(const render_params& P, tile_queue& tq, uint32_t lane, uint32_t* gq)
-{
-    unsigned long long* word = reinterpret_cast<unsigned long long*>(gq);
-    for (;;)
-    {
-        unsigned long long w = 0ull;
-        if (lane == 0u) w = __hip_atomic_fetch_add(word, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint32_t u = gu((uint32_t)__shfl((int)(uint32_t)w, 0));
-        const uint32_t hi = gu((uint32_t)__shfl((int)(uint32_t)(w >> 32), 0));
-        if (u < P.group)
-        {
-            const uint32_t q = hi >> 29, t = (hi & 0x1FFFFFFFu) + u;
-            uint32_t b0;
-            if (t < group_units(P, q, b0)) return group_decode(P, t, b0);
-        }
-        // the chunk is used up: one wave refills it, the others wait for the lock word
-        uint32_t st = GQ_TAKEN;
-        if (lane == 0u)
-        {
-            uint32_t expect = GQ_FREE;
-            st = __hip_atomic_compare_exchange_strong(&gq[GQ_LOCK], &expect, GQ_TAKEN, __ATOMIC_ACQ_REL,
-                                                      __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) ? GQ_FREE : expect;
-        }
-        st = gu((uint32_t)__shfl((int)st, 0));
-        if (st == GQ_DRY) return NONE;
-        if (st == GQ_TAKEN)
-        {
-            // another wave refills: wait until it has published the new chunk (or found every queue dry)
-            while (gu(lds_ld(&gq[GQ_LOCK])) == GQ_TAKEN) __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        // this wave holds the lock: take P.group units from the XCD queues, stealing in turn
-        uint32_t chunk_hi = 0u;
-        bool got = false;
-        while (tq.tried < 8u)
-        {
-            uint32_t t = 0;
-            if (lane == 0) t = atomicAdd(reinterpret_cast<uint32_t*>(P.counters + 8u + 8u * tq.q), P.group);
-            t = gu((uint32_t)__shfl((int)t, 0));
-            uint32_t b0;
-            if (t < group_units(P, tq.q, b0)) { chunk_hi = (tq.q << 29) | t; got = true; break; }
-            tq.q = (tq.q + 1u) & 7u;
-            tq.tried += 1u;
-        }
-        if (lane == 0u)
-        {
-            if (got) __hip_atomic_exchange(word, (unsigned long long)chunk_hi << 32, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_store(&gq[GQ_LOCK], got ? GQ_FREE : GQ_DRY, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        if (!got) return NONE;
-    }
 }
 
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask)
@@ -872,20 +781,6 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         uint32_t* const ao_base = smem + P.stack_cap * block; // wave w's AO area: ao_base + w * AO_WAVE_WORDS
         uint32_t* const sh = ao_area + AO_SH;
         const uint32_t nwaves = block >> 6;
-        // block-shared hand-out (frames in flight, blocks of several waves): the block's chunk word
-        // and lock after the waves' AO areas
-        uint32_t* const gq = ao_base + nwaves * AO_WAVE_WORDS;
-        const bool grouped = P.group != 0u && nwaves > 1u;
-        if (grouped)
-        {
-            if (tid == 0u)
-            {
-                // an exhausted chunk: the first hand-out of every wave goes to the refill
-                *reinterpret_cast<unsigned long long*>(gq) = (unsigned long long)P.group;
-                gq[GQ_LOCK] = GQ_FREE;
-            }
-            __syncthreads();
-        }
         const bool share = SHARE && !LIST && P.ao_share && nwaves > 1u;
         bool shC = false, shD = false;                        // tile C / D published to the sibling waves
         uint32_t* const dry = ao_base + AO_SH + SH_DRY;       // wave 0's word: the block saw the queues dry
@@ -900,7 +795,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         const float4 bg = make_float4(P.bg[0], P.bg[1], P.bg[2], P.bg[3]);
         tile_queue tq = queue_init(P);
         // wave-uniform tile state
-        uint32_t tileC = grouped ? group_next(P, tq, lane, gq) : next_tile(P, tq, lane), parC = 0;
+        uint32_t tileC = next_tile(P, tq, lane), parC = 0;
         mark_dry(tileC);
         // tile timeline (counting instance only): [3 t] hand-out, [3 t + 1] primaries done, [3 t + 2] written
         auto tile_mark = [&](uint32_t id, uint32_t k) {
@@ -985,7 +880,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             {
                 tileD = tileC; parD = parC; slotsD = pubC;
                 shD = shC; shC = false;
-                tileC = grouped ? group_next(P, tq, lane, gq) : next_tile(P, tq, lane);
+                tileC = next_tile(P, tq, lane);
                 mark_dry(tileC);
                 tile_mark(tileC, 0u);
                 parC ^= 1u;
@@ -996,14 +891,6 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             //    many lanes at once
             uint64_t idle = __ballot(mode == IDLE);
             if ((uint32_t)__popcll(idle) < P.refill_min && idle != ~0ull) idle = 0ull;
-            // quad_refill bit 0: rays go only to aligned 4-lane groups whose 4 lanes are all idle, 4
-            // consecutive rays (4 samples of one hit, or a 2x2 pixel block) per group -- the vector L1
-            // merges the requests of lanes that want one 16-B piece only inside such a group
-            if (P.quad_refill & 1u)
-            {
-                const uint64_t q = idle & (idle >> 1) & (idle >> 2) & (idle >> 3) & 0x1111111111111111ull;
-                idle = q | (q << 1) | (q << 2) | (q << 3);
-            }
             // ao_gate: a tile's AO rays wait until all its primaries have finished, so the waves'
             // steps are mostly all-primary or all-AO (binary closest-hit and 4-wide any-hit descents
             // then rarely share a step); +1 % alone, +6 % (hf1M) / +10 % (hf10M) with the 4-wide
@@ -1047,7 +934,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     start_ao(recs, slot_px, cut, cutN, tileC, parC, cand, wave);
                 issC = shC ? min(avail, base + want) : issC + n;
                 if (parC) inflight1 += n; else inflight0 += n;
-                idle = __ballot(mode == IDLE) & idle;
+                idle = __ballot(mode == IDLE);
             }
             if (idle && tileC != NONE && handedC < 64u)
             {
@@ -1307,7 +1194,7 @@ bool render_spill_available(const launch_config& c)
 
 size_t render_lds_bytes(const launch_config& c)
 {
-    size_t words = size_t(c.stack_cap) * c.block + (c.ao ? size_t(c.block / 64) * dev::AO_WAVE_WORDS + 4u : 0)
+    size_t words = size_t(c.stack_cap) * c.block + (c.ao ? size_t(c.block / 64) * dev::AO_WAVE_WORDS : 0)
                  + (c.epi == 2 ? size_t(5) * c.max_hits * c.block : 0)
                  + (c.epi == 3 ? size_t(dev::WL_WORDS) * c.block : 0);
     return words * 4;

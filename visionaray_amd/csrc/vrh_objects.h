@@ -34,7 +34,7 @@ struct vrh_ctx
     vrh_frame_stats last{};
     bool have_frame = false;
     // tuning options (0 = automatic), vrh_ctx_set_option
-    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_dcap = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0, opt_pop = 0, opt_scalar = 0, opt_layout = 0, opt_gate = 0, opt_wave_times = 0, opt_cut = 0, opt_share = 0, opt_cluster = 0, opt_quad = 0, opt_group = 0;
+    int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_dcap = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0, opt_pop = 0, opt_scalar = 0, opt_layout = 0, opt_gate = 0, opt_wave_times = 0, opt_cut = 0, opt_share = 0, opt_cluster = 0;
 };
 
 struct vrh_scene

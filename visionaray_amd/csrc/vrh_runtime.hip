@@ -130,7 +130,9 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
     switch (option)
     {
     case VRH_OPT_BLOCK_THREADS:
-        VRH_CHECK(value % 64 == 0, "vrh_ctx_set_option: block threads must be a multiple of 64");
+        // the traversal kernels are compiled for at most 256 threads per block (__launch_bounds__(256, ...)):
+        // a larger block would break the register allocation's assumptions (a launch failure)
+        VRH_CHECK(value % 64 == 0 && value <= 256, "vrh_ctx_set_option: block threads must be a multiple of 64, at most 256");
         ctx->opt_block = int(value); break;
     case VRH_OPT_STACK_CAP: ctx->opt_stack = int(value); break;
     case VRH_OPT_AO_SCHEDULE:
@@ -160,8 +162,11 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
     case VRH_OPT_WAVES_PER_SIMD: VRH_CHECK(value == 0 || value == 1 || value == 5 || value == 6 || value == 8, "vrh_ctx_set_option: waves per SIMD is 1, 5, 6 or 8"); ctx->opt_occ = int(value); break;
     case VRH_OPT_EXACT_MINMAX: ctx->opt_exact_minmax = value ? 1 : 0; break;
     case VRH_OPT_XCD_QUEUES: VRH_CHECK(value <= 4, "vrh_ctx_set_option: xcd queues is 1 (strips), 2 (off), 3 (band-interleaved) or 4 (cluster order)"); ctx->opt_xcd_queues = int(value); break;
-    case VRH_OPT_GROUP_UNITS: ctx->opt_group = int(value); break;
-    case VRH_OPT_QUAD_REFILL: VRH_CHECK(value <= 3, "vrh_ctx_set_option: quad refill is a 2-bit mask"); ctx->opt_quad = int(value); break;
+    case VRH_OPT_GROUP_UNITS:
+    case VRH_OPT_QUAD_REFILL:
+        // measured in round 4 and removed (slower: profiles/r04/ab/lane_layout/); 0 is accepted
+        if (value != 0) { set_error("vrh_ctx_set_option: the quad-coherent and block-shared hand-outs were removed (they measured slower)"); return VRH_ERR_UNSUPPORTED; }
+        return VRH_OK;
     case VRH_OPT_CLUSTER_TILES: VRH_CHECK(value <= 1024, "vrh_ctx_set_option: cluster tiles is 1..1024 (0 = auto)"); ctx->opt_cluster = int(value); break;
     default: set_error("vrh_ctx_set_option: unknown option"); return VRH_ERR_INVALID;
     }
@@ -1170,11 +1175,6 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
                  : ctx->opt_xcd_queues == 3 ? 2u : ctx->opt_xcd_queues == 4 ? 3u
                  : cluster_auto ? 3u : (band_auto ? 2u : 1u);
     p.cluster = ctx->opt_cluster ? uint32_t(ctx->opt_cluster) : 8u;
-    p.quad_refill = uint32_t(ctx->opt_quad);
-    // block-shared hand-out: blocks of several waves, frames in flight, cluster order (the units of a
-    // chunk are one tile's frames)
-    p.group = (ctx->opt_group && lc.ao && !list && lc.block > 64 && num_frames > 1 && p.xcd_queues == 3u)
-            ? uint32_t(ctx->opt_group) : 0u;
     if (shade)
     {
         p.shade.materials = k->shading->materials;
