@@ -258,7 +258,10 @@ struct test_counts
     // the vector L1's merging (counting variant): acc4 = distinct pieces per aligned 4-lane group,
     // summed over groups (the hardware's accesses); acc_ideal = per distinct piece ceil(lanes / 4)
     uint64_t acc4, acc_ideal;
+    uint64_t acc_kind[5];     // acc4 by load kind (VMEM_*)
 };
+// kinds of the counted vector-memory instructions
+constexpr uint32_t VMEM_PRIM = 0, VMEM_QUAD = 1, VMEM_PAIR = 2, VMEM_NORMAL = 3, VMEM_STORE = 4;
 
 // distinct values of `key` over the active lanes (wave-uniform result)
 __device__ __forceinline__ uint32_t distinct_keys(uint64_t key)
@@ -330,7 +333,7 @@ __device__ __forceinline__ void group_accesses(uint64_t key, uint32_t& acc4, uin
 
 // one wave-level vector-memory instruction whose lanes access `bytes` (<= 16) at `p`: account for it
 // in the L1 model (counting variant only; called by the active lanes)
-__device__ __forceinline__ void count_vmem(test_counts& c, const void* p, uint32_t times = 1u)
+__device__ __forceinline__ void count_vmem(test_counts& c, const void* p, uint32_t times = 1u, uint32_t kind = VMEM_PRIM)
 {
     const uint64_t a = (uint64_t)(uintptr_t)p;
     const uint32_t l = distinct_keys(a >> 7), q = distinct_keys_per_quarter(a >> 4);
@@ -343,6 +346,7 @@ __device__ __forceinline__ void count_vmem(test_counts& c, const void* p, uint32
         c.vmem += times;
         c.acc4 += (uint64_t)g4 * times;
         c.acc_ideal += (uint64_t)gi * times;
+        c.acc_kind[kind] += (uint64_t)g4 * times;
     }
 }
 
@@ -487,7 +491,7 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
         {
             const float4* p = quads + 8u * link;
             const float4 xl = p[0], yl = p[1], zl = p[2], xh = p[3], yh = p[4], zh = p[5], lk = p[6];
-            if (COUNT) count_vmem(cnt, p, 7u);
+            if (COUNT) count_vmem(cnt, p, 7u, VMEM_QUAD);
             const uint32_t k0 = __float_as_uint(lk.x), k1 = __float_as_uint(lk.y);
             const uint32_t k2 = __float_as_uint(lk.z), k3 = __float_as_uint(lk.w);
             float d0, d1, d2, d3;
@@ -554,7 +558,7 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
             const float4* p = pairs + 4u * link;
             q0 = p[0]; q1 = p[1]; q2 = p[2];
             q3 = *reinterpret_cast<const float2*>(p + 3);
-            if (COUNT) count_vmem(cnt, p, 4u);      // one 64-B record: 4 loads, one line each
+            if (COUNT) count_vmem(cnt, p, 4u, VMEM_PAIR);      // one 64-B record: 4 loads, one line each
         }
         bool b0, b1;
         float tn0, tn1;

@@ -180,6 +180,9 @@ typedef struct {
      * TCP_TOTAL_CACHE_ACCESSES -- and l1_ideal_accesses = the sum over distinct pieces of
      * ceil(lanes wanting it / 4), the count if the lanes wanting one piece sat together in groups */
     uint64_t l1_group_accesses, l1_ideal_accesses;
+    /* l1_group_accesses by kind: primitives, 4-wide records, binary pair records, AO normals,
+     * output stores */
+    uint64_t l1_group_by_kind[5];
 } vrh_frame_stats;
 
 typedef struct {

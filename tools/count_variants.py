@@ -33,6 +33,7 @@ for v in variants:
            "vmem_instrs": s["vmem_instrs"], "group4_accesses": s["l1_group_accesses"],
            "ideal_accesses": s["l1_ideal_accesses"],
            "group4_per_instr": round(s["l1_group_accesses"] / max(1, s["vmem_instrs"]), 3),
+           "group4_by_kind": dict(zip(("prims", "quads", "pairs", "normals", "stores"), list(s["l1_group_by_kind"]))),
            "box_tests_per_ray": round(s["box_tests"] / max(1, s["rays"]), 3),
            "prim_tests_per_ray": round(s["prim_tests"] / max(1, s["rays"]), 3)}
     print(json.dumps(out), flush=True)

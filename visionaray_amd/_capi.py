@@ -93,7 +93,8 @@ class vrh_frame_stats(C.Structure):
                 ("wave_steps", C.c_uint64), ("busy_lane_steps", C.c_uint64), ("wave_box_iters", C.c_uint64),
                 ("wave_prim_iters", C.c_uint64), ("wave_box_uniform_iters", C.c_uint64),
                 ("l1_lines", C.c_uint64), ("l1_requests", C.c_uint64), ("vmem_instrs", C.c_uint64),
-                ("l1_group_accesses", C.c_uint64), ("l1_ideal_accesses", C.c_uint64)]
+                ("l1_group_accesses", C.c_uint64), ("l1_ideal_accesses", C.c_uint64),
+                ("l1_group_by_kind", C.c_uint64 * 5)]
 
 
 class vrh_scene_view(C.Structure):

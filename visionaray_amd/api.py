@@ -170,7 +170,7 @@ class Context:
     def last_frame_stats(self):
         s = capi.vrh_frame_stats()
         capi.check("vrh_last_frame_stats", self.handle, C.byref(s))
-        return {k: getattr(s, k) for k, _ in s._fields_}
+        return {k: (list(getattr(s, k)) if isinstance(getattr(s, k), C.Array) else getattr(s, k)) for k, _ in s._fields_}
 
     def wave_times(self):
         """(start, end) of every wave of the last launch in ms from the launch's first start, or
@@ -205,7 +205,7 @@ class Context:
     def accum_stats(self):
         s = capi.vrh_accum_stats()
         capi.check("vrh_get_accum_stats", self.handle, C.byref(s))
-        return {k: getattr(s, k) for k, _ in s._fields_}
+        return {k: (list(getattr(s, k)) if isinstance(getattr(s, k), C.Array) else getattr(s, k)) for k, _ in s._fields_}
 
     def close(self):
         if self.handle:

@@ -99,6 +99,8 @@ __device__ __forceinline__ void flush_totals(const render_params& P, uint32_t la
 {
     unsigned long long rr = rays_total, hh = hits_total, b = cnt.box, q = cnt.prim, uni_sum = cnt.w_uni;
     unsigned long long li = cnt.lines, rq = cnt.reqs, vm = cnt.vmem, a4 = cnt.acc4, ai = cnt.acc_ideal;
+    unsigned long long ak[5];
+    for (int k = 0; k < 5; ++k) ak[k] = cnt.acc_kind[k];
     for (int off = 32; off > 0; off >>= 1)
     {
         rr += __shfl_down(rr, off);
@@ -108,6 +110,7 @@ __device__ __forceinline__ void flush_totals(const render_params& P, uint32_t la
             b += __shfl_down(b, off); q += __shfl_down(q, off); uni_sum += __shfl_down(uni_sum, off);
             li += __shfl_down(li, off); rq += __shfl_down(rq, off); vm += __shfl_down(vm, off);
             a4 += __shfl_down(a4, off); ai += __shfl_down(ai, off);
+            for (int k = 0; k < 5; ++k) ak[k] += __shfl_down(ak[k], off);
         }
     }
     if (__ballot(cnt.aborted) != 0ull && lane == 0) atomicOr(P.counters + 5, 1ull);
@@ -131,6 +134,7 @@ __device__ __forceinline__ void flush_totals(const render_params& P, uint32_t la
             atomicAdd(P.counters + COUNTERS_LINES + 2, rq);
             atomicAdd(P.counters + COUNTERS_LINES + 3, a4);
             atomicAdd(P.counters + COUNTERS_LINES + 4, ai);
+            for (int k = 0; k < 5; ++k) atomicAdd(P.counters + COUNTERS_LINES + 5 + k, ak[k]);
         }
     }
 }
@@ -335,7 +339,7 @@ __device__ __forceinline__ ray_t ao_ray(const render_params& P, const float* rec
     f3 pos = mk3(sr[0], sr[1], sr[2]);
     const float4* np = P.normals + __float_as_uint(sr[3]);
     const float4 nn = *np;                                             // get_normal.h:26-37
-    if (COUNT) count_vmem(cnt, np);
+    if (COUNT) count_vmem(cnt, np, 1u, VMEM_NORMAL);
     f3 n = mk3(nn.x, nn.y, nn.z);
     // vector3.inl:357-367 make_orthonormal_basis(u, v, w = n)
     f3 bv = fabsf(n.x) > fabsf(n.y) ? normalize(mk3(-n.z, 0.0f, n.x)) : normalize(mk3(0.0f, n.z, -n.y));
@@ -509,10 +513,10 @@ __device__ __forceinline__ uint32_t ao_cut_build(const render_params& P, const f
 constexpr uint32_t ST_COLOR = 1u, ST_OCC = 2u, ST_PID = 4u, ST_T = 8u;
 __device__ __forceinline__ void count_stores(test_counts& cnt, const render_params& P, size_t o, uint32_t which)
 {
-    if ((which & ST_COLOR) && P.color) count_vmem(cnt, P.color + o);
-    if ((which & ST_OCC) && P.occ) count_vmem(cnt, P.occ + o);
-    if ((which & ST_PID) && P.prim_id) count_vmem(cnt, P.prim_id + o);
-    if ((which & ST_T) && P.t) count_vmem(cnt, P.t + o);
+    if ((which & ST_COLOR) && P.color) count_vmem(cnt, P.color + o, 1u, VMEM_STORE);
+    if ((which & ST_OCC) && P.occ) count_vmem(cnt, P.occ + o, 1u, VMEM_STORE);
+    if ((which & ST_PID) && P.prim_id) count_vmem(cnt, P.prim_id + o, 1u, VMEM_STORE);
+    if ((which & ST_T) && P.t) count_vmem(cnt, P.t + o, 1u, VMEM_STORE);
 }
 
 // BVH-ref lists (traverse_linear.inl:76-141): the ray's BVH `bk` is exhausted (rc < 0).  Every BVH

@@ -1339,7 +1339,7 @@ VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats)
     VRH_HIP(hipEventSynchronize(ctx->ev_stop[ctx->last_slot]));
     float ms = 0.0f;
     VRH_HIP(hipEventElapsedTime(&ms, ctx->ev_start[ctx->last_slot], ctx->ev_stop[ctx->last_slot]));
-    unsigned long long c[COUNTERS_LINES + 5];
+    unsigned long long c[COUNTERS_LINES + 10];
     VRH_HIP(hipMemcpy(c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     ctx->last.kernel_ms = ms;
     ctx->last.rays = c[1];
@@ -1356,6 +1356,7 @@ VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats)
     ctx->last.l1_requests = c[COUNTERS_LINES + 2];
     ctx->last.l1_group_accesses = c[COUNTERS_LINES + 3];
     ctx->last.l1_ideal_accesses = c[COUNTERS_LINES + 4];
+    for (int k = 0; k < 5; ++k) ctx->last.l1_group_by_kind[k] = c[COUNTERS_LINES + 5 + k];
     *stats = ctx->last;
     if (c[5] & 1ull) { set_error("traversal step guard tripped: corrupt BVH (rays were cut short)"); return VRH_ERR_HIP; }
     return VRH_OK;
