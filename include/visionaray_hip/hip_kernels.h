@@ -1433,6 +1433,13 @@ __device__ inline uint32_t xcc_id()
 #ifndef VRH_USER_WAVES
 #define VRH_USER_WAVES 0
 #endif
+// VRH_USER_CLUSTER: with several frames per launch, tiles per cluster of the hand-out order (the
+// frames of a cluster back to back); 0: frame-major strips.  ao/main.cpp's kernel, C3, 32 frames per
+// launch (profiles/r04/user/cluster_ab.log): strips 1.858 ms per frame, clusters of 8 tiles 1.765,
+// of 1 tile (a tile's frames back to back) 1.744; 4 / 16 / 64 tiles as 8
+#ifndef VRH_USER_CLUSTER
+#define VRH_USER_CLUSTER 1u
+#endif
 #if VRH_USER_WAVES
 #define VRH_USER_OCC __attribute__((amdgpu_waves_per_eu(VRH_USER_WAVES)))
 #else
@@ -1455,8 +1462,23 @@ __global__ __launch_bounds__(64) VRH_USER_OCC void user_render(K kernel, user_fr
             if (lane == 0) t = atomicAdd(f.queues + q * VRH_USER_QUEUE_STRIDE, 1u);
             t = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)t, 0));
             if (t >= n) break;
-            const uint32_t c = t / len;
-            const uint32_t tile = lo + (t - c * len);
+            uint32_t c, tile;
+            if (VRH_USER_CLUSTER > 0u && f.nframes > 1u)
+            {
+                // cluster order: the strip's tiles in clusters of VRH_USER_CLUSTER, the frames of a
+                // cluster handed out back to back (the last cluster may be narrower)
+                const uint32_t C = VRH_USER_CLUSTER, F = f.nframes;
+                const uint32_t cl = t / (C * F);
+                const uint32_t r = t - cl * C * F;
+                const uint32_t cw = min(C, len - cl * C);
+                c = r / cw;
+                tile = lo + cl * C + (r - c * cw);
+            }
+            else
+            {
+                c = t / len;
+                tile = lo + (t - c * len);
+            }
             const uint32_t ty = tile / f.tiles_x;
             const uint32_t x = f.x0 + (tile - ty * f.tiles_x) * 8u + threadIdx.x;
             const uint32_t y = f.y0 + ty * 8u + threadIdx.y;
