@@ -1427,7 +1427,8 @@ __device__ inline uint32_t xcc_id()
 }
 
 // the persistent loop: queue q hands out strip q (tiles [tiles * q / 8, tiles * (q + 1) / 8)) of
-// every frame, frame-major; every (frame, tile) is handed out exactly once by one of the 8 heads, so
+// every frame, in cluster order (VRH_USER_CLUSTER, below) or frame-major; every (frame, tile) is
+// handed out exactly once by one of the 8 heads, so
 // which XCD a wave runs on changes only speed.  Every wave leaves once all 8 queues are empty.
 // VRH_USER_WAVES: waves per SIMD the register allocation targets (0: the compiler's choice)
 #ifndef VRH_USER_WAVES
