@@ -72,6 +72,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="host threads for the CPU baseline (default: the best of a 16/64/128/256 sweep)")
     ap.add_argument("--no-verify", action="store_true", help="skip the untimed checks against the fixtures")
+    ap.add_argument("--no-user-kernel", action="store_true",
+                    help="skip the user-kernel leg (hf1M AO at N=1: hip_kernels.h device lambda, 32 frames per launch)")
     ap.add_argument("--frames-in-flight", type=int, default=32,
                     help="max frames per persistent launch (vrh_render_batch, 1..32)")
     ap.add_argument("--single-frames", type=int, default=10, help="frames of the hip_sched::frame leg (median)")
@@ -175,6 +177,33 @@ def cpu_baseline(scene, kernel, threads=None):
     return {"value": round(out["rays"] / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{scene} rows {rows[0]}-{rows[1]} of 1920x1080 ({out['rays']} rays), scalar C restatement",
             "retries": 0, "stall_s": 0.0, **info}
+
+
+def user_kernel_leg(W, H, n_rays):
+    """The same workload through a user kernel: the AO lambda of tests/cpp/user_kernels.hip (ao/main.cpp's
+    kernel with random_sampler directions, include/visionaray_hip/hip_kernels.h, compiled by hipcc) on
+    hip_sched::frames, 32 frames per launch, median over 4 launches -- the path a Visionaray program with
+    its own kernel takes.  Run after the timed region, in a child process; null when the program is absent."""
+    exe = os.path.join(ROOT, "build", "tests", "user_kernels")
+    if not os.access(exe, os.X_OK):
+        return None
+    try:
+        r = subprocess.run([exe, "bench", "708", str(W), str(H), "/tmp", "4", "32"], capture_output=True,
+                           text=True, timeout=180)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    rec = None
+    for ln in r.stdout.splitlines():
+        if ln.startswith("{") and "frame_ms_median" in ln:
+            rec = json.loads(ln)
+    if r.returncode != 0 or rec is None:
+        return {"error": f"rc {r.returncode}"}
+    ms = float(rec["frame_ms_median"])
+    # the lambda traces the built-in kernel's rays: the same primary rays, 8 AO rays per hit
+    return {"mrays": round(n_rays / (ms * 1e-3) / 1e6, 1), "frame_ms_median": ms,
+            "frames_per_launch": rec["frames_per_launch"], "launches": rec["launches"],
+            "kernel": "AO device lambda (ao/main.cpp's, random_sampler) via hip_kernels.h on hip_sched::frames",
+            "program": "build/tests/user_kernels bench 708 %d %d /tmp 4 32" % (W, H)}
 
 
 def frames_per_launch(steps, cap):
@@ -459,6 +488,9 @@ def main():
             shape = {"mode": name, "accesses_per_load": round(m["tcp_accesses_per_load"], 2),
                      "kernel_accesses_per_load": round(apl, 2), "peak": round(sp, 1),
                      "frac": round(achieved / sp, 4)}
+        user_leg = None
+        if world == 1 and args.scene == "hf1M" and kernel == "ao" and not args.no_user_kernel and not grouped:
+            user_leg = user_kernel_leg(W, H, n_rays)
         line = {
             "metric": "Mrays/s (primary + 8-sample AO)" if kernel == "ao" else "Mrays/s (primary)",
             "value": round(mrays, 3),
@@ -522,6 +554,8 @@ def main():
             "moving_camera": moving,
             "moving_camera_mrays": moving["mrays_kernel"] if moving else None,
             "cpu_baseline": cpu,
+            "user_kernel": user_leg,
+            "user_kernel_mrays": user_leg.get("mrays") if user_leg else None,
             "host_build_s": round(build_s, 3),
             "verify": verify,
         }
