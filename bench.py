@@ -19,6 +19,8 @@ Frames in flight: the K timed frames run as K / F persistent launches of F frame
 tail is paid once per launch.  `value` is K frames' rays over the wall time of the timed region.
 The hip_sched::frame path -- one synchronous launch per frame, as the reference's scheduler
 issues frames -- is measured separately over --single-frames frames (median): single_frame_*.
+single_frame_async_* is the same frame() path with asynchronous issue (VRH_OPT_ASYNC_FRAMES, the
+cuda_sched model): --single-frames back-to-back calls, one final sync, rate over the hipEvent span.
 The timed frames share the scene camera (their AO samples differ); moving_camera_* repeats the
 timed launches with the eye orbiting --moving-camera degrees per frame (default 0.5: no two frames
 share primary rays), reported beside the headline.
@@ -114,6 +116,14 @@ def cgroup_cpu_quota():
         return None
 
 
+def usable_cpus(info):
+    """CPUs this process can actually run on: the cgroup quota (rounded down, at least 1) when there is
+    one, else the affinity mask.  The baseline's worker-thread count is reported separately."""
+    q = info.get("cgroup_cpu_quota")
+    avail = info.get("cpus_available") or 1
+    return max(1, min(avail, int(q))) if q else avail
+
+
 CPU_SWEEP = (16, 64, 128, 256)
 CPU_ATTEMPT_TIMEOUT_S = 60
 
@@ -130,6 +140,8 @@ def cpu_baseline(scene, kernel, threads=None):
     samples = 8 if kernel == "ao" else 0
     info = host_info()
     info["cgroup_cpu_quota"] = cgroup_cpu_quota()
+    info["cores_note"] = ("cores = the CPUs the process may use (cgroup quota, else affinity); threads = "
+                          "the worker threads of the best sweep point")
     if os.path.exists(O.REF_BENCH_BIN):
         avail = info["cpus_available"] or 1
         counts = [threads] if threads else sorted({min(t, avail) for t in CPU_SWEEP})
@@ -159,7 +171,8 @@ def cpu_baseline(scene, kernel, threads=None):
         if not done:
             raise RuntimeError(f"every reference run stalled: {sweep}")
         best = max(done, key=lambda p: p["value"])
-        return {"value": best["value"], "unit": "Mrays/s", "cores": best["threads"], "kind": "reference",
+        return {"value": best["value"], "unit": "Mrays/s", "cores": usable_cpus(info), "threads": best["threads"],
+                "kind": "reference",
                 "sample": f"{scene} 1920x1080, {samples} AO spp, tiled_sched<basic_ray<simd::float4>> -O3 -msse4.1, "
                           f"best of a worker-thread sweep {counts}, each the median of 3 frames after 1 warm-up "
                           f"({best['rays_per_frame']} rays/frame)",
@@ -174,7 +187,8 @@ def cpu_baseline(scene, kernel, threads=None):
     t0 = time.perf_counter()
     out = O.render(sc, cam, mode=mode, rows=rows, threads=threads)
     dt = time.perf_counter() - t0
-    return {"value": round(out["rays"] / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+    return {"value": round(out["rays"] / dt / 1e6, 3), "unit": "Mrays/s", "cores": min(threads, usable_cpus(info)),
+            "threads": threads, "kind": "port",
             "sample": f"{scene} rows {rows[0]}-{rows[1]} of 1920x1080 ({out['rays']} rays), scalar C restatement",
             "retries": 0, "stall_s": 0.0, **info}
 
@@ -405,6 +419,54 @@ def main():
                   "path": "hip_sched::frame -> vrh_render + vrh_sync (one launch per frame)"}
         rt_s.close()
 
+    # ---- hip_sched::frame with asynchronous issue (VRH_OPT_ASYNC_FRAMES, cuda_sched's model:
+    # cuda_sched.inl:306-320 returns without a sync): --single-frames back-to-back frame() calls, one
+    # final sync, into one shared target and into two alternating targets (rank 0, N = 1)
+    single_async = None
+    if world == 1 and not grouped and args.single_frames > 0:
+        sched = va.hip_sched(ctx)
+        single_async = {"frames": args.single_frames,
+                        "path": "hip_sched::frame x N, end_frame without sync, then one vrh_sync: frames "
+                                "alternate between the context's two frame lanes (vrh.h VRH_OPT_ASYNC_FRAMES)"}
+        ctx.set_option("async_frames", 1)
+        try:
+            for targets in (1, 2):
+                rts_a = [va.hip_buffer_rt(ctx, W, H) for _ in range(targets)]
+                for i in range(2):                       # warm-up: both lanes, scratch targets allocated
+                    sched.frame(kern, va.make_sched_params(cam, rts_a[i % targets]), frame_num=next_frame[0])
+                    next_frame[0] += 1
+                ctx.sync()
+                ctx.stats_reset()
+                first = next_frame[0]
+                t1 = time.perf_counter()
+                for i in range(args.single_frames):
+                    sched.frame(kern, va.make_sched_params(cam, rts_a[i % targets]), frame_num=first + i)
+                ctx.sync()
+                wall = time.perf_counter() - t1
+                next_frame[0] += args.single_frames
+                am = ctx.accum_stats()
+                leg = {"targets": targets, "span_ms": round(am["span_ms"], 4), "wall_ms": round(wall * 1e3, 4),
+                       "kernel_ms_per_frame_sum": round(am["kernel_ms_total"] / args.single_frames, 4),
+                       "ms_per_frame": round(am["span_ms"] / args.single_frames, 4),
+                       "mrays_span": round(am[rays_key] / am["span_ms"] / 1e3, 3),
+                       "mrays_wall": round(am[rays_key] / wall / 1e6, 3)}
+                if not args.no_verify and targets == 1:
+                    # the shared target holds the last frame, equal to its own synchronous render
+                    last = rts_a[0].download(t=False)
+                    ctx.set_option("async_frames", 0)
+                    one = va.hip_buffer_rt(ctx, W, H)
+                    sched.frame(kern, va.make_sched_params(cam, one), frame_num=first + args.single_frames - 1)
+                    ref1 = one.download(t=False)
+                    one.close()
+                    ctx.set_option("async_frames", 1)
+                    verify["async_shared_target_holds_last_frame"] = all(
+                        np.array_equal(last[k].view(np.uint8), ref1[k].view(np.uint8)) for k in last)
+                for r in rts_a:
+                    r.close()
+                single_async["shared_target" if targets == 1 else "two_targets"] = leg
+        finally:
+            ctx.set_option("async_frames", 0)
+
     # ---- moving-camera leg (N = 1, untimed by the driver's clock): the timed launches' shape with
     # the eye orbiting --moving-camera degrees per frame, so no two frames of a launch share primary
     # rays (the timed frames share the scene camera, as the reference viewer's frames do at rest)
@@ -458,9 +520,9 @@ def main():
         # PMC of this exact configuration (tools/r02_session.sh + tools/pmc_bench.py): HBM bytes per
         # launch (`traffic`), the L1 requests the hardware counted and how busy the TD unit was
         # one committed pass per frames-per-launch value (the driver's --steps decides F)
-        pmc_name = f"pmc_traffic_F{F}_{args.scene}.json"
-        if not os.path.exists(os.path.join(ROOT, "profiles", pmc_name)):
-            pmc_name = f"pmc_traffic_F{F}.json"
+        # (most specific first: scene + kernel, scene, the C3 default)
+        pmc_name = next((n for n in (f"pmc_traffic_F{F}_{args.scene}_{kernel}.json", f"pmc_traffic_F{F}_{args.scene}.json")
+                         if os.path.exists(os.path.join(ROOT, "profiles", n))), f"pmc_traffic_F{F}.json")
         pmc = load_json(os.path.join(ROOT, "profiles", pmc_name)) or {}
         traffic, pmc_info = None, None
         from visionaray_amd.buildinfo import kernel_source_sha256
@@ -551,6 +613,8 @@ def main():
             },
             "single_frame": single,
             "single_frame_mrays": single["mrays_kernel"] if single else None,
+            "single_frame_async": single_async,
+            "single_frame_async_mrays": single_async["shared_target"]["mrays_span"] if single_async else None,
             "moving_camera": moving,
             "moving_camera_mrays": moving["mrays_kernel"] if moving else None,
             "cpu_baseline": cpu,

@@ -215,8 +215,9 @@ struct stack_t
     uint32_t stride;      // words between entries = threads per block
     uint32_t end;         // SPILL: base + LDS entries * stride (unused otherwise)
     uint32_t lim_off;     // total entries * stride (LDS + overflow; wave-uniform)
-    uint32_t* spill;      // SPILL: this block's overflow block minus LDS entries * stride (wave-uniform):
-                          // the entry at top >= end lives at spill[top] (= block[top - end + base])
+    uint32_t* spill;      // SPILL: this block's overflow block minus LDS entries * stride (wave-uniform,
+                          // computed in integer arithmetic, render_unified_kernel): the entry at
+                          // top >= end lives at spill[top] (= block[top - end + base])
     __device__ __forceinline__ void reset() { top = base; }
     // k more entries fit (lim_off is uniform, so no per-lane limit register stays live)
     __device__ __forceinline__ bool room(uint32_t k) const { return top + k * stride <= base + lim_off; }
@@ -515,8 +516,12 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
             // nearest hit entry first (ties -> lower index), the other hits pushed
             d0 = h0 ? d0 : INFINITY; d1 = h1 ? d1 : INFINITY; d2 = h2 ? d2 : INFINITY; d3 = h3 ? d3 : INFINITY;
 #if VRH_SORTED_PUSH
-            // all hit entries in distance order: a 4-element sorting network (stable for ties: the
-            // lower index stays first), the nearest descended, the others pushed farthest first
+            // all hit entries in distance order: a 4-element sorting network, the nearest descended,
+            // the others pushed farthest first.  Only the descended entry keeps the old selection's tie
+            // rule (equal distances -> the lower index); the order among the pushed entries is not
+            // stable for ties (d = [1, 1, 0, 5] pushes index 1 ahead of 0) -- harmless for this
+            // boolean any-hit walk, whose result does not depend on the visiting order, but not a
+            // first-found hit record order
             float e0 = d0, e1 = d1, e2 = d2, e3 = d3;
             uint32_t c0 = k0, c1 = k1, c2 = k2, c3 = k3;
             auto cx = [](float& a, uint32_t& ka, float& b, uint32_t& kb) {

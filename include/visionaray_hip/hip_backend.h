@@ -159,7 +159,16 @@ public:
     }
     vrh_ctx* get() const { return ctx_.get(); }
     void sync() const { hip_detail::check(vrh_sync(get()), "vrh_sync"); }
-    void set_option(uint32_t opt, int64_t value) { hip_detail::check(vrh_ctx_set_option(get(), opt, value), "vrh_ctx_set_option"); }
+    void set_option(uint32_t opt, int64_t value)
+    {
+        hip_detail::check(vrh_ctx_set_option(get(), opt, value), "vrh_ctx_set_option");
+        if (opt == VRH_OPT_ASYNC_FRAMES) async_frames_ = value != 0;
+    }
+    // cuda_sched's issue model (cuda_sched.inl:306-320): hip_sched::frame returns once the frame is
+    // issued; back-to-back frames overlap their launch tails on the context's two frame lanes, and
+    // hip_buffer_rt::download / sync() wait for them (vrh.h VRH_OPT_ASYNC_FRAMES)
+    void set_async_frames(bool on) { set_option(VRH_OPT_ASYNC_FRAMES, on ? 1 : 0); }
+    bool async_frames() const { return async_frames_; }
     vrh_frame_stats last_frame_stats() const
     {
         vrh_frame_stats s{};
@@ -175,6 +184,7 @@ public:
 
 private:
     std::shared_ptr<vrh_ctx> ctx_;
+    bool async_frames_ = false;
 };
 
 //-------------------------------------------------------------------------------------------------
@@ -464,8 +474,13 @@ public:
     }
 
     void begin_frame() {}
-    // end_frame() synchronises, so hip_sched::frame blocks like tiled_sched::frame
-    void end_frame() { ctx_->sync(); }
+    // end_frame() synchronises, so hip_sched::frame blocks like tiled_sched::frame -- unless the
+    // context issues frames asynchronously (hip_context::set_async_frames): then it returns at once,
+    // as gpu_buffer_rt::end_frame does (gpu_buffer_rt.inl:84-86), and download() waits
+    void end_frame()
+    {
+        if (!ctx_->async_frames()) ctx_->sync();
+    }
 
     ref_type ref()
     {

@@ -283,6 +283,18 @@ enum vrh_option {
                                     idle waves of the same block claim from (blocks of 4 waves):
                                     1 = on, 2 = off (auto: off -- measured 2-3 % slower on one-frame
                                     C3 / C4 launches, profiles/r03_ab/ao_share/)                    */
+    VRH_OPT_ASYNC_FRAMES = 26,   /* 1: frames are issued like cuda_sched issues them (cuda_sched.inl:306-320,
+                                    no synchronisation): they alternate between two frame lanes of
+                                    the context (HIP streams of its own), so the next frame's waves
+                                    take the CUs the previous frame's launch tail leaves idle.
+                                    Results are unchanged: a frame into a target that the other lane
+                                    still writes renders into the lane's scratch target (primary / AO
+                                    kernels, one frame, uniform / jittered sampler) and is copied in
+                                    issue order, or waits for that lane (every other case); every
+                                    entry point that works on the context stream (clears, downloads,
+                                    uploads, vrh_sync, vrh_ctx_get_stream, group renders) first waits
+                                    for every frame issued so far.  Shard renders stay on the context
+                                    stream.  0 = off (the default: frames on the context stream)    */
     VRH_OPT_PAIR_LAYOUT = 15,    /* scene upload (read by vrh_scene_upload): 1 = node pairs in
                                     depth-first preorder, a pair's child-0 pair next to it in one
                                     128-B line; 2 = the builder's order (auto: 2; 1 measured
@@ -401,6 +413,8 @@ typedef struct {
     uint32_t timed_frames;    /* renders whose kernel time is in the sums                 */
     double   kernel_ms_total, kernel_ms_min, kernel_ms_max;
     uint64_t rays, hits;
+    double   span_ms;         /* first frame's launch start to the last frame's launch end (hipEvents; frames
+                                 of overlapping asynchronous launches count once), 0 if not all timed */
 } vrh_accum_stats;
 VRH_API int vrh_stats_reset(vrh_ctx* ctx);
 VRH_API int vrh_get_accum_stats(vrh_ctx* ctx, vrh_accum_stats* out);           /* syncs */

@@ -73,3 +73,25 @@ def test_ao_share_full_frame_hf1M(ctx, golden, oracle_mod):
 def test_ao_share_option_range(ctx):
     with pytest.raises(Exception):
         ctx.set_option("ao_share", 3)
+
+
+def test_ao_share_keeps_block_size_where_no_share_instance(ctx, scene):
+    """Sharing exists only for one-frame AO launches at 5 waves / SIMD: a batched AO launch or a primary
+    launch with the option set runs the plain instance at its usual 64-thread block, and a one-frame AO
+    launch runs 4-wave blocks (the kernel selection decides, vrh_kernels.hip render_share_available)."""
+    dev, cam, _ = scene
+    basis = cam.basis(W, H)
+    ctx.set_option("ao_share", 1)
+    try:
+        rt = va.hip_buffer_rt(ctx, W, 2 * H)
+        va.render_batch(ctx, dev, rt, [basis, basis], va.ao_kernel(dev), None, frame_num=1)
+        assert ctx.last_frame_stats()["block_threads"] == 64
+        rt.close()
+        rt = va.hip_buffer_rt(ctx, W, H)
+        va.render(ctx, dev, rt, basis, va.closest_hit_kernel(dev), None)
+        assert ctx.last_frame_stats()["block_threads"] == 64
+        va.render(ctx, dev, rt, basis, va.ao_kernel(dev), None)
+        assert ctx.last_frame_stats()["block_threads"] == 256
+        rt.close()
+    finally:
+        ctx.set_option("ao_share", 0)

@@ -146,6 +146,17 @@ def test_removed_hand_out_options_are_refused(ctx):
         assert e.value.code == _capi.VRH_ERR_UNSUPPORTED
 
 
+def test_option_values_out_of_range_rejected(ctx):
+    """Negative and too large option values are refused at vrh_ctx_set_option, before they can reach a
+    kernel as wrapped uint32 values (a negative cluster size could make cluster x frames 0)."""
+    for opt, bad in (("cluster_tiles", -1), ("cluster_tiles", -2**31), ("cluster_tiles", 1025), ("refill_min", -3)):
+        with pytest.raises(_capi.VrhError) as e:
+            ctx.set_option(opt, bad)
+        assert e.value.code == _capi.VRH_ERR_INVALID
+    ctx.set_option("cluster_tiles", 0)
+    ctx.set_option("refill_min", 0)
+
+
 def test_block_threads_above_launch_bounds_rejected(ctx):
     """The traversal kernels are compiled for <= 256 threads per block; a larger block is refused at
     vrh_ctx_set_option instead of failing the launch."""

@@ -1,0 +1,68 @@
+#!/bin/bash
+# One parametrized GPU session (replaces the per-round session scripts of rounds 2-4).
+#   OUT=gpurun_out/<dir> tools/session.sh STEP [STEP ...]
+# Steps (each with its own time limit; a fault / abort / timeout ends the session):
+#   tests[:K]        pytest -m gpu (optionally -k K)          smoke       __graft_entry__.smoke()
+#   bench:<cfg>      the driver's shape (--steps 20 --warmup 5) on cfg = c3 (with the CPU baseline and
+#                    the user-kernel leg) | c4 | c2 | c5 | f32 (the no-argument command) | shards8
+#   pmc:<cfg>        TCP / HBM read / HBM write counter passes of bench:<cfg> and their summary
+#                    (tools/pmc_bench.py -> profiles/pmc_traffic_F<F>[_<scene>_<kernel>].json)
+#   mem:<cfg>        L2 hit / TD busy / TD stall passes of bench:<cfg>
+#   trace:<cfg>      rocprofv3 --kernel-trace --stats of bench:<cfg>
+#   ab:<scene>:<libs>[:<kernel>]   same-box A/B of library builds (tools/ab_builds.sh), libs comma-separated
+#   cmd:<name>:<seconds>:<command> anything else
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+OUT=${OUT:-gpurun_out/session}
+mkdir -p $OUT
+fatal() { case "$1" in 124|134|137|139) return 0;; esac; return 1; }
+step() {  # name, timeout, command...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 $t "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  tail -${TAIL:-2} $OUT/$name.log | cut -c1-400; echo "$name rc=$rc"
+  if fatal $rc; then echo "fatal exit; stopping"; exit $rc; fi
+  [ $rc = 0 ] || exit $rc
+}
+Q="--no-cpu-baseline --single-frames 0 --moving-camera 0 --no-user-kernel --no-verify"
+cfg_args() {  # cfg -> bench arguments (driver shape)
+  case $1 in
+    c3) echo "--steps 20 --warmup 5";;
+    c4) echo "--scene hf10M --steps 20 --warmup 5";;
+    c2) echo "--scene hf1M --kernel primary --steps 20 --warmup 5";;
+    c5) echo "--scene sph1M --steps 20 --warmup 5";;
+    f32) echo "";;
+    shards8) echo "--steps 20 --warmup 5 --shards 8";;
+    *) echo "unknown cfg $1" >&2; exit 2;;
+  esac
+}
+cfg_meta() {  # cfg -> scene kernel F
+  case $1 in c3) echo "hf1M ao 20";; c4) echo "hf10M ao 20";; c2) echo "hf1M primary 20";;
+             c5) echo "sph1M primary 20";; f32) echo "hf1M ao 32";; esac
+}
+for s in "$@"; do
+  kind=${s%%:*}; arg=${s#*:}; [ "$arg" = "$s" ] && arg=
+  case $kind in
+    tests) TAIL=4 step pytest_gpu${arg:+_k} 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 \
+             --timeout-method thread ${arg:+-k "$arg"};;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()";;
+    bench) extra="--no-cpu-baseline"; [ "$arg" = c3 ] && extra=""
+           step bench_$arg 600 python3 bench.py $(cfg_args $arg) $extra;;
+    pmc)   a="$(cfg_args $arg) $Q"; set -- $(cfg_meta $arg); sc=$1 kn=$2 F=$3; d=$OUT/pmc_$arg
+           step pmc_${arg}_tcp 300 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD --output-format csv -d $d/pmc_bench_tcp -o run -- python3 bench.py $a
+           step pmc_${arg}_hbm 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $d/pmc_bench_hbm -o run -- python3 bench.py $a
+           step pmc_${arg}_wr 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $d/pmc_bench_wr -o run -- python3 bench.py $a
+           name=pmc_traffic_F$F.json; [ "$arg" != c3 ] && [ "$arg" != f32 ] && name=pmc_traffic_F${F}_${sc}_${kn}.json
+           python3 tools/pmc_bench.py $d $d/$name $sc $kn $F "python3 bench.py $a" && cp $d/$name profiles/;;
+    mem)   a="$(cfg_args $arg) $Q"; d=$OUT/mem_$arg
+           step mem_${arg}_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $d/tcc -o run -- python3 bench.py $a
+           step mem_${arg}_td 300 rocprofv3 --pmc TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE --output-format csv -d $d/td -o run -- python3 bench.py $a;;
+    trace) step trace_$arg 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$arg -o run -- python3 bench.py $(cfg_args $arg) --no-cpu-baseline;;
+    ab)    IFS=: read -r sc libs kn <<< "$arg"
+           LIBS="${libs//,/ }" SCENES=$sc KERNEL=${kn:-ao} step ab_${sc}_${kn:-ao} 900 bash tools/ab_builds.sh;;
+    cmd)   IFS=: read -r name t c <<< "$arg"; step $name $t bash -c "$c";;
+    *) echo "unknown step $s"; exit 2;;
+  esac
+done
+exit 0

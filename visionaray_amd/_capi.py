@@ -57,6 +57,7 @@ VRH_OPT_AO_SHARE = 22
 VRH_OPT_CLUSTER_TILES = 23
 VRH_OPT_QUAD_REFILL = 24
 VRH_OPT_GROUP_UNITS = 25
+VRH_OPT_ASYNC_FRAMES = 26
 VRH_OPT_AO_STEAL = 21
 VRH_MAX_TIMED_FRAMES = 1024
 VRH_MAX_SCENE_LIST = 8
@@ -66,7 +67,7 @@ VRH_GROUP_ID_BYTES = 128
 class vrh_accum_stats(C.Structure):
     _fields_ = [("frames", C.c_uint32), ("timed_frames", C.c_uint32), ("kernel_ms_total", C.c_double),
                 ("kernel_ms_min", C.c_double), ("kernel_ms_max", C.c_double), ("rays", C.c_uint64),
-                ("hits", C.c_uint64)]
+                ("hits", C.c_uint64), ("span_ms", C.c_double)]
 
 
 class vrh_pixel_sampler(C.Structure):

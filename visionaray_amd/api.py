@@ -149,6 +149,7 @@ class Context:
             capi.check("vrh_ctx_create_on_stream", int(device), C.c_void_p(stream), C.byref(h))
         self.handle = h
         self.device = device
+        self.async_frames = False
 
     def sync(self):
         capi.check("vrh_sync", self.handle)
@@ -164,8 +165,13 @@ class Context:
                  "coop_fetch": capi.VRH_OPT_COOP_FETCH, "scalar_fetch": capi.VRH_OPT_SCALAR_FETCH,
                  "pair_layout": capi.VRH_OPT_PAIR_LAYOUT, "ao_gate": capi.VRH_OPT_AO_GATE, "ao_cut": capi.VRH_OPT_AO_CUT, "wave_times": capi.VRH_OPT_WAVE_TIMES,
                  "ao_share": capi.VRH_OPT_AO_SHARE, "cluster_tiles": capi.VRH_OPT_CLUSTER_TILES,
-                 "quad_refill": capi.VRH_OPT_QUAD_REFILL, "group_units": capi.VRH_OPT_GROUP_UNITS}
-        capi.check("vrh_ctx_set_option", self.handle, names.get(option, option), int(value))
+                 "quad_refill": capi.VRH_OPT_QUAD_REFILL, "group_units": capi.VRH_OPT_GROUP_UNITS,
+                 "async_frames": capi.VRH_OPT_ASYNC_FRAMES}
+        opt = names.get(option, option)
+        capi.check("vrh_ctx_set_option", self.handle, opt, int(value))
+        if opt == capi.VRH_OPT_ASYNC_FRAMES:
+            # cuda_sched's issue model: hip_sched.frame returns without waiting (end_frame no-op)
+            self.async_frames = bool(value)
 
     def last_frame_stats(self):
         s = capi.vrh_frame_stats()
@@ -346,8 +352,11 @@ class hip_buffer_rt:
         pass
 
     def end_frame(self):
-        """Blocks until the frame is done (so hip_sched::frame is synchronous like tiled_sched)."""
-        self.ctx.sync()
+        """Blocks until the frame is done (so hip_sched::frame is synchronous like tiled_sched) -- unless
+        the context issues frames asynchronously (set_option("async_frames", 1)): then, like
+        gpu_buffer_rt::end_frame (gpu_buffer_rt.inl:84-86), it returns at once and download() waits."""
+        if not self.ctx.async_frames:
+            self.ctx.sync()
 
     def device_buffers(self):
         bufs = [C.c_void_p() for _ in range(4)]
@@ -685,6 +694,9 @@ class hip_sched:
 
     frame() = rt.begin_frame() -> vrh_render -> rt.end_frame() (end_frame syncs, so frame() is
     synchronous like tiled_sched).  shard=(index, count, packed) renders only that image-tile shard.
+    With ctx.set_option("async_frames", 1) frame() returns once the frame is issued, as cuda_sched's
+    does (cuda_sched.inl:306-320): back-to-back frames overlap their launch tails on the context's two
+    frame lanes; rt.download() / ctx.sync() wait for them (VRH_OPT_ASYNC_FRAMES).
     """
 
     def __init__(self, ctx):

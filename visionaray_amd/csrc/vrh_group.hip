@@ -195,6 +195,7 @@ VRH_API int vrh_group_sync(vrh_group* g)
 {
     VRH_CHECK(g, "vrh_group_sync: null");
     VRH_HIP(hipSetDevice(g->ctx->device));
+    VRH_HIP(ctx_join(g->ctx));
     VRH_HIP(hipStreamSynchronize(g->ctx->stream));
     VRH_HIP(hipStreamSynchronize(g->stream));
     return VRH_OK;
@@ -267,6 +268,7 @@ VRH_API int vrh_render_sharded(uint32_t n, vrh_group* const* groups, const vrh_s
         vrh_group* g = groups[i];
         vrh_ctx* ctx = g->ctx;
         VRH_HIP(hipSetDevice(ctx->device));
+        VRH_HIP(ctx_join(ctx));                 // after the context's asynchronous frames
         const uint32_t si = g->next;
         g->next ^= 1u;
         slot_of[i] = si;

@@ -101,6 +101,7 @@ constexpr int COUNTERS_LINES = 80;      // [80] L1 128-B lines, [81] wave-level 
                                         // [83] 4-lane-group accesses, [84] ideal-grouping accesses (counting variant)
 constexpr int COUNTERS_TOTAL = 208;     // u64 words [208], [209]: totals
 constexpr int COUNTERS_WORDS = 256;
+constexpr int COUNTER_BLOCKS = 3;      // per context: frames on its stream + one per asynchronous frame lane
 
 struct launch_config
 {
@@ -124,6 +125,7 @@ size_t render_lds_bytes(const launch_config& c);
 hipError_t launch_render(const render_params& p, const launch_config& c, int grid, hipStream_t s);
 int render_blocks_per_cu(const launch_config& c);
 bool render_spill_available(const launch_config& c);   // an overflow-stack instance exists for c
+bool render_share_available(const launch_config& c);   // an AO tail-sharing instance exists for c
 struct unshard_params
 {
     uint32_t width, height, count, rows_per_shard;

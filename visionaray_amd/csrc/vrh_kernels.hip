@@ -572,8 +572,13 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     st.end = tid + P.stack_cap * block;
     st.lim_off = (SPILL ? P.stack_total : P.stack_cap) * block;
     // the overflow entries of lane tid start at entry stack_cap: word top - stack_cap * block of this
-    // block's overflow area, i.e. spill[top] with the pointer moved back by stack_cap * block words
-    st.spill = SPILL ? P.stack_spill + size_t(blockIdx.x) * (P.stack_total - P.stack_cap) * block - size_t(P.stack_cap) * block
+    // block's overflow area, i.e. spill[top] with the pointer moved back by stack_cap * block words.
+    // The move is done on the address as an integer: for block 0 it points before the allocation,
+    // which pointer arithmetic (an inbounds GEP) may not express; every access spill[top] with
+    // top >= stack_cap * block lands inside this block's area
+    st.spill = SPILL ? reinterpret_cast<uint32_t*>(
+                           reinterpret_cast<uintptr_t>(P.stack_spill + size_t(blockIdx.x) * (P.stack_total - P.stack_cap) * block)
+                           - uintptr_t(P.stack_cap) * block * sizeof(uint32_t))
                      : nullptr;
     uint32_t* ao_area = smem + P.stack_cap * block + wave * AO_WAVE_WORDS;
     test_counts cnt = {};
@@ -1194,6 +1199,11 @@ bool render_spill_available(const launch_config& c)
     launch_config s = c;
     s.spill = true;
     return select_variant(s) != nullptr;
+}
+
+bool render_share_available(const launch_config& c)
+{
+    return c.kind == dev::KIND_TRI ? pick_share<dev::KIND_TRI>(c) != nullptr : pick_share<dev::KIND_SPHERE>(c) != nullptr;
 }
 
 size_t render_lds_bytes(const launch_config& c)

@@ -33,7 +33,33 @@ struct vrh_ctx
     uint32_t last_slot = 0;
     vrh_frame_stats last{};
     bool have_frame = false;
+    // asynchronous frames (VRH_OPT_ASYNC_FRAMES, cuda_sched's issue model, cuda_sched.inl:306-320):
+    // frames alternate between two frame lanes (streams of their own), so frame k + 1's waves take
+    // the CUs that frame k's launch tail leaves idle.  Each lane has its own counter block and stack
+    // overflow block; a target written by the other lane is rendered into the lane's scratch target
+    // and copied in issue order (vrh_runtime.hip issue_async).  Work on `stream` joins the lanes
+    // first (ctx_join): it waits for every frame issued so far.
+    struct lane_t
+    {
+        hipStream_t stream = nullptr;
+        hipEvent_t done = nullptr;              // recorded after every frame issued on this lane
+        bool used = false;
+        unsigned long long* counters = nullptr; // COUNTERS_WORDS words of the counter allocation
+        void* spill = nullptr;
+        size_t spill_bytes = 0;
+        // scratch target (primary / AO frames into a target the other lane still writes)
+        float4* color = nullptr;
+        uint32_t* prim_id = nullptr;
+        float* t = nullptr;
+        uint8_t* occ = nullptr;
+        size_t pixels = 0;
+    } lane[2];
+    uint32_t next_lane = 0;
+    hipEvent_t main_mark = nullptr;             // position of `stream` that an async frame waits for
+    mutable uint64_t join_epoch = 0;            // incremented by every join of the lanes into `stream`
+    unsigned long long* last_counters = nullptr;    // counter block of the last frame (vrh_last_frame_stats)
     // tuning options (0 = automatic), vrh_ctx_set_option
+    int opt_async = 0;
     int opt_block = 0, opt_stack = 0, opt_sched = 0, opt_refill = 0, opt_dcap = 0, opt_bpc = 0, opt_occ = 0, opt_exact_minmax = 0, opt_xcd_queues = 0, opt_wide = 0, opt_pop = 0, opt_scalar = 0, opt_layout = 0, opt_gate = 0, opt_wave_times = 0, opt_cut = 0, opt_share = 0, opt_cluster = 0;
 };
 
@@ -85,6 +111,11 @@ struct vrh_rt
     uint32_t mh_n = 0;
     hipEvent_t written = nullptr;     // last vrh_render_sharded unshard into this target (group stream)
     bool written_pending = false;
+    // asynchronous frames: the lane that wrote this target last, and when (recorded on that lane after
+    // the frame's writes); valid while the context has not joined its lanes since (join_epoch)
+    hipEvent_t lane_written = nullptr;
+    int lane = -1;
+    uint64_t lane_epoch = 0;
 };
 
 // a render group's root wrote `rt` on `stream`: record it so the target's own context orders after
@@ -105,6 +136,23 @@ inline hipError_t mark_written(vrh_rt* rt, hipStream_t stream)
         for (hipEvent_t ev : gw) known |= ev == rt->written;
         if (!known) gw.push_back(rt->written);
     }
+    return hipSuccess;
+}
+
+// asynchronous frames: `stream` waits for every frame issued on the context's frame lanes so far
+// (no host synchronisation).  Every entry point that issues work on `stream` or synchronises it calls
+// this first, so work issued after a frame sees that frame's results.
+inline hipError_t ctx_join(const vrh_ctx* ctx)
+{
+    bool any = false;
+    for (const auto& l : ctx->lane)
+        if (l.used)
+        {
+            const hipError_t e = hipStreamWaitEvent(ctx->stream, l.done, 0);
+            if (e != hipSuccess) return e;
+            any = true;
+        }
+    if (any) ++ctx->join_epoch;
     return hipSuccess;
 }
 

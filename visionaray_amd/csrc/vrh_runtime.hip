@@ -42,7 +42,16 @@ int select_device(vrh_ctx* ctx)
 // target's context stream waits for that (an event wait, no host synchronisation)
 int rt_wait(vrh_ctx* ctx, vrh_rt* rt)
 {
+    VRH_HIP(ctx_join(ctx));
     if (rt && rt->written_pending) VRH_HIP(hipStreamWaitEvent(ctx->stream, rt->written, 0));
+    return VRH_OK;
+}
+
+// the context stream after every asynchronous frame, then the host after the stream
+int ctx_drain(vrh_ctx* ctx)
+{
+    VRH_HIP(ctx_join(ctx));
+    VRH_HIP(hipStreamSynchronize(ctx->stream));
     return VRH_OK;
 }
 
@@ -86,10 +95,13 @@ VRH_API int vrh_ctx_create_on_stream(int hip_device, void* hip_stream, vrh_ctx**
             if (e != hipSuccess) { set_error(hipGetErrorString(e)); rc = VRH_ERR_HIP; break; }
             ctx->own_stream = true;
         }
-        e = hipMalloc(&ctx->counters, COUNTERS_WORDS * sizeof(unsigned long long));
+        // one counter block for frames on the context stream, one per frame lane (asynchronous frames)
+        e = hipMalloc(&ctx->counters, COUNTER_BLOCKS * COUNTERS_WORDS * sizeof(unsigned long long));
         if (e != hipSuccess) { set_error(hipGetErrorString(e)); rc = VRH_ERR_OOM; break; }
-        e = hipMemset(ctx->counters, 0, COUNTERS_WORDS * sizeof(unsigned long long));
+        e = hipMemset(ctx->counters, 0, COUNTER_BLOCKS * COUNTERS_WORDS * sizeof(unsigned long long));
         if (e != hipSuccess) { set_error(hipGetErrorString(e)); rc = VRH_ERR_HIP; break; }
+        ctx->last_counters = ctx->counters;
+        for (int i = 0; i < 2; ++i) ctx->lane[i].counters = ctx->counters + size_t(i + 1) * COUNTERS_WORDS;
     } while (0);
     if (rc != VRH_OK) { vrh_ctx_destroy(ctx); return rc; }
     *out = ctx;
@@ -101,6 +113,12 @@ VRH_API int vrh_ctx_create(int hip_device, vrh_ctx** out) { return vrh_ctx_creat
 VRH_API int vrh_ctx_get_stream(const vrh_ctx* ctx, int* hip_device, void** hip_stream)
 {
     VRH_CHECK(ctx, "vrh_ctx_get_stream: null context");
+    // work the caller issues on the stream comes after every frame issued so far (asynchronous frames)
+    if (hip_stream && (ctx->lane[0].used || ctx->lane[1].used))
+    {
+        VRH_HIP(hipSetDevice(ctx->device));
+        VRH_HIP(ctx_join(ctx));
+    }
     if (hip_device) *hip_device = ctx->device;
     if (hip_stream) *hip_stream = ctx->stream;
     return VRH_OK;
@@ -110,7 +128,18 @@ VRH_API int vrh_ctx_destroy(vrh_ctx* ctx)
 {
     if (!ctx) return VRH_OK;
     (void)hipSetDevice(ctx->device);
+    for (auto& l : ctx->lane)
+        if (l.stream) (void)hipStreamSynchronize(l.stream);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto& l : ctx->lane)
+    {
+        if (l.spill) (void)hipFree(l.spill);
+        for (void* q : { (void*)l.color, (void*)l.prim_id, (void*)l.t, (void*)l.occ })
+            if (q) (void)hipFree(q);
+        if (l.done) (void)hipEventDestroy(l.done);
+        if (l.stream) (void)hipStreamDestroy(l.stream);
+    }
+    if (ctx->main_mark) (void)hipEventDestroy(ctx->main_mark);
     if (ctx->counters) (void)hipFree(ctx->counters);
     if (ctx->wave_times) (void)hipFree(ctx->wave_times);
     if (ctx->user_queues) (void)hipFree(ctx->user_queues);
@@ -167,7 +196,12 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
         // measured in round 4 and removed (slower: profiles/r04/ab/lane_layout/); 0 is accepted
         if (value != 0) { set_error("vrh_ctx_set_option: the quad-coherent and block-shared hand-outs were removed (they measured slower)"); return VRH_ERR_UNSUPPORTED; }
         return VRH_OK;
-    case VRH_OPT_CLUSTER_TILES: VRH_CHECK(value <= 1024, "vrh_ctx_set_option: cluster tiles is 1..1024 (0 = auto)"); ctx->opt_cluster = int(value); break;
+    case VRH_OPT_ASYNC_FRAMES: VRH_CHECK(value <= 1, "vrh_ctx_set_option: asynchronous frames is 1 (on) or 0 (off)"); ctx->opt_async = int(value); break;
+    case VRH_OPT_CLUSTER_TILES:
+        // stored as the kernel's uint32 cluster size: a negative value would wrap (cluster x frames can
+        // become 0, a division by zero in the hand-out), so the range is checked here as well
+        VRH_CHECK(value >= 0 && value <= 1024, "vrh_ctx_set_option: cluster tiles is 1..1024 (0 = auto)");
+        ctx->opt_cluster = int(value); break;
     default: set_error("vrh_ctx_set_option: unknown option"); return VRH_ERR_INVALID;
     }
     return VRH_OK;
@@ -577,7 +611,7 @@ VRH_API int vrh_scene_download_bvh(vrh_ctx* ctx, const vrh_scene* sc, void* node
     VRH_CHECK(*num_nodes >= sc->info.num_nodes, "vrh_scene_download_bvh: nodes_out too small");
     int rc = select_device(ctx);
     if (rc) return rc;
-    VRH_HIP(hipStreamSynchronize(ctx->stream));
+    if ((rc = ctx_drain(ctx))) return rc;
     VRH_HIP(hipMemcpy(nodes_out, sc->dnodes, size_t(sc->info.num_nodes) * sizeof(node32), hipMemcpyDeviceToHost));
     if (indices_out) VRH_HIP(hipMemcpy(indices_out, sc->dindices, size_t(sc->info.num_indices) * 4, hipMemcpyDeviceToHost));
     *num_nodes = sc->info.num_nodes;
@@ -775,6 +809,12 @@ VRH_API int vrh_rt_free(vrh_rt* rt)
         if (rt->mh_prim_id) (void)hipFree(rt->mh_prim_id);
         if (rt->mh_t) (void)hipFree(rt->mh_t);
     }
+    if (rt->lane_written)
+    {
+        if (rt->ctx) (void)hipSetDevice(rt->ctx->device);
+        (void)hipEventSynchronize(rt->lane_written);
+        (void)hipEventDestroy(rt->lane_written);
+    }
     if (rt->written)
     {
         if (rt->ctx) (void)hipSetDevice(rt->ctx->device);
@@ -800,6 +840,22 @@ __global__ void fill_rt_kernel(float4* color, uint32_t* pid, float* t, uint8_t* 
     if (pid) pid[i] = 0xFFFFFFFFu;
     if (t) t[i] = -1.0f;
     if (occ) occ[i] = 0;
+}
+
+// asynchronous frames: a frame rendered into a lane's scratch target lands in its target, scissor box
+// only (the pixels a frame writes), once the target's previous writer is done
+__global__ void copy_clip_kernel(float4* color, uint32_t* pid, float* t, uint8_t* occ, const float4* s_color,
+                                 const uint32_t* s_pid, const float* s_t, const uint8_t* s_occ, uint32_t width,
+                                 uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1)
+{
+    const uint32_t x = x0 + blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t y = y0 + blockIdx.y * blockDim.y + threadIdx.y;
+    if (x >= x1 || y >= y1) return;
+    const size_t i = size_t(y) * width + x;
+    if (color) color[i] = s_color[i];
+    if (pid) pid[i] = s_pid[i];
+    if (t) t[i] = s_t[i];
+    if (occ) occ[i] = s_occ[i];
 }
 } // namespace
 
@@ -1041,9 +1097,10 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     lc.occ = ctx->opt_occ ? ctx->opt_occ : whitted ? 5 : lc.epi ? 1 : lc.ao ? 5 : 6;
     if (sp) lc.occ = lc.ao ? 5 : 6;                    // the sampler instances exist at the defaults
     if (list) lc.occ = ao ? 5 : 6;
-    // tail sharing has instances for uncounted one-frame AO launches at 5 waves / SIMD only
-    // (vrh_kernels.hip pick_share); elsewhere the option changes nothing, not even the block size
-    if (lc.share && (lc.count || lc.epi || lc.occ != 5 || lc.sched != 0))
+    // tail sharing has instances for uncounted one-frame AO launches at 5 waves / SIMD only: where
+    // the kernel selection (vrh_kernels.hip pick_share, asked through render_share_available) has no
+    // SHARE instance the option changes nothing, not even the block size
+    if (lc.share && !render_share_available(lc))
     {
         lc.share = false;
         if (!ctx->opt_block) lc.block = 64;
@@ -1079,8 +1136,15 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
 
     int rc = select_device(ctx);
     if (rc) return rc;
-    rc = rt_wait(ctx, rt);
-    if (rc) return rc;
+    // asynchronous frames (VRH_OPT_ASYNC_FRAMES): whole-image frames go to a frame lane (below);
+    // shard renders (render groups record events on the context stream after their renders) and the
+    // timeline diagnostics stay on the context stream
+    const bool async = ctx->opt_async && !shard && !ctx->opt_wave_times;
+    if (!async)
+    {
+        rc = rt_wait(ctx, rt);
+        if (rc) return rc;
+    }
 
     render_params p{};
     p.pairs = sc->pairs; p.prims = sc->prims; p.normals = sc->normals; p.root = sc->roots[0];
@@ -1167,7 +1231,7 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     // strip's primaries then keep their XCD's L2); one-frame launches keep strips (ab30)
     // AO with frames in flight: cluster order (every XCD on its own strip, the F frames of a cluster of
     // 8 tiles handed out back to back): against the band order, round 4, same box, 20 frames per
-    // launch (profiles/r04_ab/cluster/): hf10M +3.3 % (static camera) / +0.3 % (orbiting 0.5 deg per
+    // launch (profiles/r04/ab/cluster_hf{1M,10M}_{static,orbit}.log): hf10M +3.3 % (static camera) / +0.3 % (orbiting 0.5 deg per
     // frame), hf1M +0.9 % / +2.3 %; clusters of 4-16 tiles alike, 240 (a whole band) no gain
     const bool band_auto = num_frames > 1 && (lc.ao || sc->info.device_bytes > (256ull << 20));
     const bool cluster_auto = num_frames > 1 && lc.ao;
@@ -1201,21 +1265,85 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     const uint64_t units = uint64_t(num_frames) * p.num_tiles;
     int grid = std::max(1, int(std::min<uint64_t>(uint64_t(ctx->num_cus) * per_cu, (units + waves_per_block - 1) / waves_per_block)));
 
+    // where the launch runs: the context stream with its counter / overflow blocks, or a frame lane
+    hipStream_t S = ctx->stream;
+    unsigned long long* ctr = ctx->counters;
+    void** spill = &ctx->spill;
+    size_t* spill_bytes = &ctx->spill_bytes;
+    vrh_ctx::lane_t* L = nullptr;
+    bool via_scratch = false;
+    float4* dst_color = p.color; uint32_t* dst_pid = p.prim_id; float* dst_t = p.t; uint8_t* dst_occ = p.occ;
+    if (async)
+    {
+        // cuda_sched issues a frame and returns (cuda_sched.inl:306-320): frames alternate between two
+        // lanes, so this frame's waves fill the CUs the previous frame's launch tail leaves idle
+        const uint32_t li = ctx->next_lane;
+        L = &ctx->lane[li];
+        if (!L->stream)
+        {
+            VRH_HIP(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking));
+            VRH_HIP(hipEventCreateWithFlags(&L->done, hipEventDisableTiming));
+        }
+        if (!ctx->main_mark) VRH_HIP(hipEventCreateWithFlags(&ctx->main_mark, hipEventDisableTiming));
+        if (!rt->lane_written) VRH_HIP(hipEventCreateWithFlags(&rt->lane_written, hipEventDisableTiming));
+        ctx->next_lane ^= 1u;
+        S = L->stream;
+        ctr = L->counters;
+        spill = &L->spill;
+        spill_bytes = &L->spill_bytes;
+        // after everything issued on the context stream before this call (clears, uploads, frames there)
+        VRH_HIP(hipEventRecord(ctx->main_mark, ctx->stream));
+        VRH_HIP(hipStreamWaitEvent(S, ctx->main_mark, 0));
+        if (rt->written_pending) VRH_HIP(hipStreamWaitEvent(S, rt->written, 0));
+        // the target's last writer is the other lane, not yet joined: write order must hold.  A primary /
+        // AO frame of one image through a sampler that does not read the target renders into this lane's
+        // scratch target now and is copied after that writer; anything else waits for it
+        const bool other_writer = rt->lane >= 0 && rt->lane != int(li) && rt->lane_epoch == ctx->join_epoch;
+        if (other_writer)
+        {
+            const bool scratch_ok = num_frames == 1 && (k->kind == VRH_KERNEL_PRIMARY || ao) && (!sp || sp->blend == 0);
+            if (scratch_ok)
+            {
+                const size_t n = size_t(rt->width) * rt->height;
+                if (n > L->pixels)
+                {
+                    VRH_HIP(hipStreamSynchronize(S));
+                    for (void** q : { (void**)&L->color, (void**)&L->prim_id, (void**)&L->t, (void**)&L->occ })
+                        if (*q) { (void)hipFree(*q); *q = nullptr; }
+                    L->pixels = 0;
+                    VRH_HIP(hipMalloc(&L->color, n * sizeof(float4)));
+                    VRH_HIP(hipMalloc(&L->prim_id, n * sizeof(uint32_t)));
+                    VRH_HIP(hipMalloc(&L->t, n * sizeof(float)));
+                    VRH_HIP(hipMalloc(&L->occ, n));
+                    L->pixels = n;
+                }
+                p.color = dst_color ? L->color : nullptr;
+                p.prim_id = dst_pid ? L->prim_id : nullptr;
+                p.t = dst_t ? L->t : nullptr;
+                p.occ = dst_occ ? L->occ : nullptr;
+                via_scratch = true;
+            }
+            else
+                VRH_HIP(hipStreamWaitEvent(S, rt->lane_written, 0));
+        }
+    }
+    p.counters = ctr;
+
     // the stack overflow blocks of the persistent grid (grown on demand; the stream is drained
     // first, so no launch still uses the old block)
     if (lc.spill)
     {
         const size_t bytes = size_t(grid) * (p.stack_total - p.stack_cap) * size_t(lc.block) * sizeof(uint32_t);
-        if (bytes > ctx->spill_bytes)
+        if (bytes > *spill_bytes)
         {
-            VRH_HIP(hipStreamSynchronize(ctx->stream));
-            if (ctx->spill) (void)hipFree(ctx->spill);
-            ctx->spill = nullptr;
-            ctx->spill_bytes = 0;
-            VRH_HIP(hipMalloc(&ctx->spill, bytes));
-            ctx->spill_bytes = bytes;
+            VRH_HIP(hipStreamSynchronize(S));
+            if (*spill) (void)hipFree(*spill);
+            *spill = nullptr;
+            *spill_bytes = 0;
+            VRH_HIP(hipMalloc(spill, bytes));
+            *spill_bytes = bytes;
         }
-        p.stack_spill = static_cast<uint32_t*>(ctx->spill);
+        p.stack_spill = static_cast<uint32_t*>(*spill);
     }
 
     // per-wave timeline of this launch (diagnostic, VRH_OPT_WAVE_TIMES)
@@ -1261,10 +1389,36 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
         ctx->ev_start.push_back(a);
         ctx->ev_stop.push_back(b);
     }
-    VRH_HIP(hipMemsetAsync(ctx->counters, 0, COUNTERS_FRAME * sizeof(unsigned long long), ctx->stream));
-    VRH_HIP(hipEventRecord(ctx->ev_start[slot], ctx->stream));
-    if (p.num_tiles > 0) VRH_HIP(launch_render(p, lc, grid, ctx->stream));
-    VRH_HIP(hipEventRecord(ctx->ev_stop[slot], ctx->stream));
+    VRH_HIP(hipMemsetAsync(ctr, 0, COUNTERS_FRAME * sizeof(unsigned long long), S));
+    VRH_HIP(hipEventRecord(ctx->ev_start[slot], S));
+    if (p.num_tiles > 0) VRH_HIP(launch_render(p, lc, grid, S));
+    VRH_HIP(hipEventRecord(ctx->ev_stop[slot], S));
+    if (async)
+    {
+        if (via_scratch)
+        {
+            // after the target's previous writer (the other lane), the scissor box of the scratch
+            // target -- every pixel a primary / AO frame writes -- goes to the target
+            VRH_HIP(hipStreamWaitEvent(S, rt->lane_written, 0));
+            const uint32_t* cl = p.cam[0].clip;
+            if (cl[2] > cl[0] && cl[3] > cl[1])
+            {
+                const dim3 blk(64, 4), grd((cl[2] - cl[0] + 63) / 64, (cl[3] - cl[1] + 3) / 4);
+                hipLaunchKernelGGL(copy_clip_kernel, grd, blk, 0, S, dst_color, dst_pid, dst_t, dst_occ,
+                                   (const float4*)p.color, (const uint32_t*)p.prim_id, (const float*)p.t,
+                                   (const uint8_t*)p.occ, rt->width, cl[0], cl[1], cl[2], cl[3]);
+                VRH_HIP(hipGetLastError());
+            }
+        }
+        VRH_HIP(hipEventRecord(rt->lane_written, S));
+        rt->lane = int(L - ctx->lane);
+        rt->lane_epoch = ctx->join_epoch;
+        VRH_HIP(hipEventRecord(L->done, S));
+        L->used = true;
+    }
+    else
+        rt->lane = -1;
+    ctx->last_counters = ctr;
     ctx->last_slot = slot;
     ctx->frames++;
 
@@ -1282,14 +1436,15 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
 VRH_API int vrh_sync(vrh_ctx* ctx)
 {
     VRH_CHECK(ctx, "vrh_sync: null");
+    VRH_HIP(hipSetDevice(ctx->device));
     for (hipEvent_t ev : ctx->group_written) VRH_HIP(hipEventSynchronize(ev));
-    VRH_HIP(hipStreamSynchronize(ctx->stream));
-    return VRH_OK;
+    return ctx_drain(ctx);
 }
 
 VRH_API int vrh_get_tile_times(vrh_ctx* ctx, uint64_t* out, uint64_t capacity, uint64_t* count)
 {
     VRH_CHECK(ctx && count, "vrh_get_tile_times: null");
+    VRH_HIP(hipSetDevice(ctx->device));
     VRH_HIP(hipStreamSynchronize(ctx->stream));
     *count = ctx->tile_times_used;
     if (out && ctx->tile_times_used)
@@ -1315,7 +1470,7 @@ VRH_API int vrh_get_wave_times(vrh_ctx* ctx, uint64_t* out, uint64_t capacity, u
     VRH_CHECK(ctx && count, "vrh_get_wave_times: null");
     int rc = select_device(ctx);
     if (rc) return rc;
-    VRH_HIP(hipStreamSynchronize(ctx->stream));
+    if ((rc = ctx_drain(ctx))) return rc;
     *count = ctx->wave_times_used;
     if (ticks_per_ms)
     {
@@ -1340,7 +1495,7 @@ VRH_API int vrh_last_frame_stats(vrh_ctx* ctx, vrh_frame_stats* stats)
     float ms = 0.0f;
     VRH_HIP(hipEventElapsedTime(&ms, ctx->ev_start[ctx->last_slot], ctx->ev_stop[ctx->last_slot]));
     unsigned long long c[COUNTERS_LINES + 10];
-    VRH_HIP(hipMemcpy(c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
+    VRH_HIP(hipMemcpy(c, ctx->last_counters, sizeof(c), hipMemcpyDeviceToHost));
     ctx->last.kernel_ms = ms;
     ctx->last.rays = c[1];
     ctx->last.hits = c[2];
@@ -1367,8 +1522,9 @@ VRH_API int vrh_stats_reset(vrh_ctx* ctx)
     VRH_CHECK(ctx, "vrh_stats_reset: null");
     int rc = select_device(ctx);
     if (rc) return rc;
-    VRH_HIP(hipStreamSynchronize(ctx->stream));
-    VRH_HIP(hipMemset(ctx->counters + COUNTERS_TOTAL, 0, 16 * sizeof(unsigned long long)));
+    if ((rc = ctx_drain(ctx))) return rc;
+    for (int b = 0; b < COUNTER_BLOCKS; ++b)
+        VRH_HIP(hipMemset(ctx->counters + size_t(b) * COUNTERS_WORDS + COUNTERS_TOTAL, 0, 16 * sizeof(unsigned long long)));
     ctx->frames = 0;
     return VRH_OK;
 }
@@ -1378,7 +1534,7 @@ VRH_API int vrh_get_accum_stats(vrh_ctx* ctx, vrh_accum_stats* out)
     VRH_CHECK(ctx && out, "vrh_get_accum_stats: null");
     int rc = select_device(ctx);
     if (rc) return rc;
-    VRH_HIP(hipStreamSynchronize(ctx->stream));
+    if ((rc = ctx_drain(ctx))) return rc;
     vrh_accum_stats a{};
     a.frames = ctx->frames;
     a.timed_frames = std::min<uint32_t>(ctx->frames, VRH_MAX_TIMED_FRAMES);
@@ -1392,10 +1548,20 @@ VRH_API int vrh_get_accum_stats(vrh_ctx* ctx, vrh_accum_stats* out)
         a.kernel_ms_max = std::max<double>(a.kernel_ms_max, ms);
     }
     if (a.timed_frames == 0) a.kernel_ms_min = 0.0;
-    unsigned long long c[2];
-    VRH_HIP(hipMemcpy(c, ctx->counters + COUNTERS_TOTAL, sizeof(c), hipMemcpyDeviceToHost));
-    a.rays = c[0];
-    a.hits = c[1];
+    // first launch's start to the last launch's end: overlapping (asynchronous) frames count once
+    if (a.frames >= 1 && a.frames <= VRH_MAX_TIMED_FRAMES)
+    {
+        float ms = 0.0f;
+        VRH_HIP(hipEventElapsedTime(&ms, ctx->ev_start[0], ctx->ev_stop[a.frames - 1]));
+        a.span_ms = ms;
+    }
+    for (int b = 0; b < COUNTER_BLOCKS; ++b)
+    {
+        unsigned long long c[2];
+        VRH_HIP(hipMemcpy(c, ctx->counters + size_t(b) * COUNTERS_WORDS + COUNTERS_TOTAL, sizeof(c), hipMemcpyDeviceToHost));
+        a.rays += c[0];
+        a.hits += c[1];
+    }
     *out = a;
     return VRH_OK;
 }
@@ -1477,6 +1643,7 @@ VRH_API int vrh_unshard(vrh_ctx* ctx, uint32_t width, uint32_t height, uint32_t 
               "vrh_unshard: re-deriving AO colour needs the gathered masks and samples <= 8");
     int rc = select_device(ctx);
     if (rc) return rc;
+    if ((rc = rt_wait(ctx, dst))) return rc;
     unshard_params u{};
     u.width = width; u.height = height; u.count = count;
     u.rows_per_shard = VRH_BAND_ROWS * vrh_shard_bands(height, 0, count);
