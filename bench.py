@@ -60,6 +60,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
 TRI_BYTES, SPHERE_BYTES, INDEX_BYTES, NODE_BYTES = 64, 48, 4, 32
 OUT_BYTES_PRIMARY = 24          # RGBA32F + u32 prim_id + f32 t per primary ray
+GROUP_TIMEOUT_MS = 60000        # N > 1: deadline of every wait on a peer rank (join, exchange, sync)
 L1_REQ_BYTES = 16               # one vector-L1 request (TCP access) = one lane's 16-B piece (tools/l1_roof.py)
 
 
@@ -259,7 +260,9 @@ def main():
     local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        import datetime
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                timeout=datetime.timedelta(milliseconds=3 * GROUP_TIMEOUT_MS))
 
     kernel = args.kernel or ("ao" if not args.scene.startswith("sph") else "primary")
 
@@ -297,7 +300,9 @@ def main():
         if rank == 0:
             uid.copy_(torch.frombuffer(bytearray(va.render_group.unique_id()), dtype=torch.uint8))
         dist.broadcast(uid, 0)
-        group = va.render_group(ctx, world, rank, bytes(uid.cpu().numpy().tobytes()))
+        # every wait on a peer has a deadline (vrh_group_join_timeout): a dead rank ends the others with an
+        # error instead of a hang
+        group = va.render_group(ctx, world, rank, bytes(uid.cpu().numpy().tobytes()), timeout_ms=GROUP_TIMEOUT_MS)
     elif grouped:
         group = va.render_group(ctx, 1, 0, va.render_group.unique_id())
     full_rts = {}
@@ -517,7 +522,7 @@ def main():
         pieces_launch = float(cstats["l1_requests"]) * frame_share    # counting variant: distinct 16-B pieces
         peak = roof.get("peak_gbs") if roof else None
         hbm_alg = bytes_per_ray * rays_launch / (k_ms_mean * 1e-3) / 1e9
-        # PMC of this exact configuration (tools/r02_session.sh + tools/pmc_bench.py): HBM bytes per
+        # PMC of this exact configuration (tools/session.sh pmc:<cfg> + tools/pmc_bench.py): HBM bytes per
         # launch (`traffic`), the L1 requests the hardware counted and how busy the TD unit was
         # one committed pass per frames-per-launch value (the driver's --steps decides F)
         # (most specific first: scene + kernel, scene, the C3 default)
@@ -633,4 +638,14 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except BaseException:
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            # a failed rank leaves at once, without the barrier or the group's teardown: the other ranks'
+            # deadlines (GROUP_TIMEOUT_MS) end them with an error instead of a hang
+            import traceback
+            traceback.print_exc()
+            sys.stderr.flush()
+            os._exit(3)
+        raise

@@ -201,45 +201,72 @@ __device__ __forceinline__ bool isect_sphere(const ray_t& r, float4 a, float& t)
 }
 
 // Per-lane stack, column-major ([entry][lane]) so a wave's pushes/pops hit 64 distinct LDS banks.
-// The top is kept as a word offset advanced by the block stride (no multiply per push/pop).
-// SPILL = true: only the first (end - base) / stride entries live in LDS; deeper entries continue,
-// in the same column layout, in a global overflow block of the launch (`spill`), so a BVH deeper
-// than the LDS part is still exact -- used where LDS, not registers, would limit the waves per CU
-// (vrh_render; the check costs 2-4 % where it is not needed, so SPILL = false has none).
+// `used` = entries in use x the block stride (a word offset from the lane's column `base`), so the
+// bounds checks compare it with wave-uniform limits only (no per-lane limit register stays live).
+// SPILL = true: only the first cap_off / stride entries live in LDS; deeper entries continue, in the
+// same column layout, in a global overflow block of the launch (`spill`), so a BVH deeper than the
+// LDS part is still exact -- used where LDS, not registers, would limit the waves per CU
+// (vrh_render; the check costs 2-4 % where it is not needed, so SPILL = false has none).  The
+// overflow block is addressed through a buffer resource (wave-uniform base in SGPRs, 32-bit per-lane
+// offset, accesses past the block dropped): no 64-bit per-lane address stays live.
 template <bool SPILL>
 struct stack_t
 {
     uint32_t* mem;        // dynamic LDS base
     uint32_t base;        // this lane's column (word offset of entry 0)
-    uint32_t top;         // word offset of the next free entry
+    uint32_t used;        // entries in use x stride
     uint32_t stride;      // words between entries = threads per block
-    uint32_t end;         // SPILL: base + LDS entries * stride (unused otherwise)
-    uint32_t lim_off;     // total entries * stride (LDS + overflow; wave-uniform)
-    uint32_t* spill;      // SPILL: this block's overflow block minus LDS entries * stride (wave-uniform,
-                          // computed in integer arithmetic, render_unified_kernel): the entry at
-                          // top >= end lives at spill[top] (= block[top - end + base])
-    __device__ __forceinline__ void reset() { top = base; }
-    // k more entries fit (lim_off is uniform, so no per-lane limit register stays live)
-    __device__ __forceinline__ bool room(uint32_t k) const { return top + k * stride <= base + lim_off; }
+    uint32_t cap_off;     // SPILL: LDS entries x stride (wave-uniform; unused otherwise)
+    uint32_t lim_off;     // total entries x stride (LDS + overflow; wave-uniform)
+    uint32_t* spill;      // SPILL: this block's overflow block (wave-uniform): the entry at used >= cap_off
+                          // lives at word base + used - cap_off of it (addressed as byte offset
+                          // 4 (base + used) from a descriptor base 4 cap_off bytes before the block, so
+                          // no per-lane base - cap_off is kept)
+    __device__ __forceinline__ void init(uint32_t* m, uint32_t column, uint32_t block_stride, uint32_t lds_entries,
+                                         uint32_t total_entries, uint32_t* overflow)
+    {
+        mem = m; base = column; used = 0u; stride = block_stride;
+        cap_off = lds_entries * block_stride;
+        lim_off = total_entries * block_stride;
+        spill = overflow;
+    }
+    __device__ __forceinline__ void reset() { used = 0u; }
+    // k more entries fit
+    __device__ __forceinline__ bool room(uint32_t k) const { return used + k * stride <= lim_off; }
+#if defined(__HIP_DEVICE_COMPILE__)
+    __device__ __forceinline__ __amdgpu_buffer_rsrc_t overflow() const
+    {
+        // gfx9 buffer descriptor word 3 (raw dwords, as composable_kernel's CK_BUFFER_RESOURCE_3RD_DWORD);
+        // the base moved back by cap_off words as an integer (a descriptor field, not a C++ pointer),
+        // no range check (num_records = max: every offset a lane forms lies in its column of the block)
+        return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(reinterpret_cast<uintptr_t>(spill) - uintptr_t(cap_off) * 4u),
+                                                 0, -1, 0x00020000);
+    }
+#endif
     __device__ __forceinline__ void push(uint32_t v)
     {
         if constexpr (SPILL)
         {
-            if (__builtin_expect(top < end, 1)) mem[top] = v;
-            else spill[top] = v;
+            if (__builtin_expect(used < cap_off, 1)) mem[base + used] = v;
+#if defined(__HIP_DEVICE_COMPILE__)
+            else __builtin_amdgcn_raw_buffer_store_b32(v, overflow(), int((base + used) * 4u), 0, 0);
+#endif
         }
         else
-            mem[top] = v;
-        top += stride;
+            mem[base + used] = v;
+        used += stride;
     }
     __device__ __forceinline__ uint32_t pop()
     {
-        top -= stride;
+        used -= stride;
+#if defined(__HIP_DEVICE_COMPILE__)
         if constexpr (SPILL)
-            if (__builtin_expect(top >= end, 0)) return spill[top];
-        return mem[top];
+            if (__builtin_expect(used >= cap_off, 0))
+                return __builtin_amdgcn_raw_buffer_load_b32(overflow(), int((base + used) * 4u), 0, 0);
+#endif
+        return mem[base + used];
     }
-    __device__ __forceinline__ bool empty() const { return top == base; }
+    __device__ __forceinline__ bool empty() const { return used == 0u; }
 };
 using lds_stack = stack_t<false>;
 
@@ -464,7 +491,9 @@ __device__ __forceinline__ bool leaf_loop(const float4* __restrict__ prims, uint
 // records instead: the same set of leaves is reached (vrh_quad.cpp), the order does not matter
 // for an any-hit result, and the nearest hit entry is descended first.  If a record's hits could
 // overflow the stack, the ray restarts on the binary records from `root` (still exact).
-template <int KIND, bool COUNT, bool FAST, bool UV = false, class MultiList = void, class Stack>
+// CAPPED = false: an instance without the descent cap (`resume` is never set, `cap` is ignored): the
+// kernels whose launches never cap a descent keep no per-lane visit counter
+template <int KIND, bool COUNT, bool FAST, bool UV = false, class MultiList = void, bool CAPPED = true, class Stack>
 __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const float4* __restrict__ prims,
                                         const float4* __restrict__ quads, uint32_t root, bool& quad,
                                         const ray_t& r, float max_t, bool any, Stack& st,
@@ -479,7 +508,7 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
     // the tree was validated at upload (no cycles, links in range), so the descent terminates;
     // the guard below only bounds the number of outer iterations per ray
     uint32_t link;
-    if (resume != NO_RESUME)
+    if (CAPPED && resume != NO_RESUME)
     {
         link = resume;
         resume = NO_RESUME;
@@ -550,7 +579,7 @@ __device__ __forceinline__ int ray_step(const float4* __restrict__ pairs, const 
     {
         // at most `cap` inner visits per call: a lane still descending keeps its node in `resume`
         // and continues next call, so one long descent does not hold the whole wave
-        if (it == 0u) { resume = link; return 0; }
+        if (CAPPED && it == 0u) { resume = link; return 0; }
         if (COUNT)
         {
             // one node for the whole wave? (counted once, by the first active lane)

@@ -218,10 +218,13 @@ public:
     }
 
     // one rank of a group spread over processes
-    hip_render_group(std::shared_ptr<hip_context> ctx, uint32_t nranks, uint32_t rank, vrh_group_id const& id)
+    // (timeout_ms: the deadline of every wait on a peer, 0 = VRH_GROUP_TIMEOUT_MS; a missed one throws
+    // hip_error with VRH_ERR_TIMEOUT after aborting the communicator, vrh_group_join_timeout)
+    hip_render_group(std::shared_ptr<hip_context> ctx, uint32_t nranks, uint32_t rank, vrh_group_id const& id,
+                     uint32_t timeout_ms = 0)
     {
         vrh_group* g = nullptr;
-        hip_detail::check(vrh_group_join(ctx->get(), nranks, rank, &id, &g), "vrh_group_join");
+        hip_detail::check(vrh_group_join_timeout(ctx->get(), nranks, rank, &id, timeout_ms, &g), "vrh_group_join");
         ctxs_.push_back(std::move(ctx));
         groups_.emplace_back(g, [](vrh_group* q) { vrh_group_free(q); });
     }

@@ -372,13 +372,7 @@ __device__ inline vrh::dev::lds_stack user_stack()
     const uint32_t nthreads = blockDim.x * blockDim.y * blockDim.z;
     const uint32_t tid = threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z);
     vrh::dev::lds_stack st;
-    st.mem = vrh_user_smem;
-    st.base = tid;
-    st.stride = nthreads;
-    st.top = tid;
-    st.end = tid + VRH_USER_STACK * nthreads;
-    st.lim_off = VRH_USER_STACK * nthreads;
-    st.spill = nullptr;          // checked_ref: the BVH fits the LDS stack
+    st.init(vrh_user_smem, tid, nthreads, VRH_USER_STACK, VRH_USER_STACK, nullptr);   // checked_ref: the BVH fits
     return st;
 }
 

@@ -50,7 +50,9 @@ enum vrh_status {
     VRH_ERR_HIP = 2,          /* HIP runtime error (message in vrh_last_error)         */
     VRH_ERR_OOM = 3,          /* device or host allocation failed                      */
     VRH_ERR_UNSUPPORTED = 4,  /* e.g. BVH deeper than the device stack supports        */
-    VRH_ERR_NO_DEVICE = 5     /* no HIP device visible                                 */
+    VRH_ERR_NO_DEVICE = 5,    /* no HIP device visible                                 */
+    VRH_ERR_TIMEOUT = 6       /* a render-group peer did not answer within the group's deadline: the
+                                 communicator was aborted (ncclCommAbort) and the group is failed */
 };
 
 /* primitive layouts accepted by vrh_scene_upload / vrh_build_bvh (reference binary layouts,
@@ -499,6 +501,22 @@ typedef struct vrh_group vrh_group;
 typedef struct { char internal[128]; } vrh_group_id;   /* = ncclUniqueId */
 VRH_API int vrh_group_get_id(vrh_group_id* id);
 VRH_API int vrh_group_join(vrh_ctx* ctx, uint32_t nranks, uint32_t rank, const vrh_group_id* id, vrh_group** out);
+/* Failure containment (the first multi-GPU run must fail with an error, not hang):
+ * the communicator of a joined group is non-blocking (ncclCommInitRankConfig, blocking = 0).  Every
+ * wait on a peer -- the join itself, the enqueue of an exchange or scene broadcast, vrh_group_sync --
+ * polls the communicator's state (ncclCommGetAsyncError) and the streams against a deadline of
+ * timeout_ms (0: VRH_GROUP_TIMEOUT_MS); on an RCCL error or at the deadline the communicator is
+ * aborted (ncclCommAbort), the group is marked failed, and the call returns VRH_ERR_TIMEOUT (or
+ * VRH_ERR_HIP for an error) with vrh_last_error set.  Every later call on a failed group returns
+ * VRH_ERR_INVALID at once; vrh_group_free releases it without waiting on the peers.  vrh_group_join
+ * = vrh_group_join_timeout with timeout_ms 0. */
+#define VRH_GROUP_TIMEOUT_MS 120000u
+VRH_API int vrh_group_join_timeout(vrh_ctx* ctx, uint32_t nranks, uint32_t rank, const vrh_group_id* id,
+                                   uint32_t timeout_ms, vrh_group** out);
+/* the deadline of a group's later waits (exchange enqueue, vrh_group_sync, scene broadcast), ms > 0 */
+VRH_API int vrh_group_set_timeout(vrh_group* group, uint32_t timeout_ms);
+/* 1 if the group failed (aborted after an error or a missed deadline), else 0 */
+VRH_API int vrh_group_failed(const vrh_group* group);
 VRH_API int vrh_group_create_local(uint32_t ndev, vrh_ctx* const* ctxs, vrh_group** out);
 VRH_API int vrh_group_info(const vrh_group* group, uint32_t* nranks, uint32_t* rank);
 VRH_API int vrh_group_sync(vrh_group* group);   /* waits for the renders AND the exchange */

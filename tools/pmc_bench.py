@@ -4,7 +4,7 @@
 
     python tools/pmc_bench.py <session dir> [out.json] [scene] [kernel] [frames per launch] [command]
 
-<session dir> holds one sub-directory per counter pass (tools/r02_session.sh: pmc_bench_tcp =
+<session dir> holds one sub-directory per counter pass (tools/session.sh pmc:<cfg>: pmc_bench_tcp =
 TCP_TOTAL_CACHE_ACCESSES_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD, pmc_bench_hbm =
 FETCH_SIZE, pmc_bench_wr = WRITE_SIZE).  Only the dispatches of the timed kernel are used: the
 frames-in-flight instantiation render_unified_kernel<..., BATCH = true> (its launches all have the

@@ -10,6 +10,10 @@
 #   mem:<cfg>        L2 hit / TD busy / TD stall passes of bench:<cfg>
 #   trace:<cfg>      rocprofv3 --kernel-trace --stats of bench:<cfg>
 #   ab:<scene>:<libs>[:<kernel>]   same-box A/B of library builds (tools/ab_builds.sh), libs comma-separated
+#   pmcuser:<lambda|ref>  trace + counter passes of a user-kernel program (32 frames per launch, C3) and
+#                    their summary (tools/pmc_user.py -> profiles/pmc_user_<lambda|ref>.json)
+#   user[:reps]      user-kernel throughput: AO lambda and ao/main.cpp's kernel, 1 and 32 frames per launch
+#   counters         rocprofv3 -L (the counters this box offers)
 #   cmd:<name>:<seconds>:<command> anything else
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
@@ -41,10 +45,11 @@ cfg_meta() {  # cfg -> scene kernel F
   case $1 in c3) echo "hf1M ao 20";; c4) echo "hf10M ao 20";; c2) echo "hf1M primary 20";;
              c5) echo "sph1M primary 20";; f32) echo "hf1M ao 32";; esac
 }
+n_tests=0
 for s in "$@"; do
   kind=${s%%:*}; arg=${s#*:}; [ "$arg" = "$s" ] && arg=
   case $kind in
-    tests) TAIL=4 step pytest_gpu${arg:+_k} 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 \
+    tests) n_tests=$((n_tests + 1)); TAIL=4 step pytest_gpu_$n_tests 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 \
              --timeout-method thread ${arg:+-k "$arg"};;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()";;
     bench) extra="--no-cpu-baseline"; [ "$arg" = c3 ] && extra=""
@@ -61,6 +66,26 @@ for s in "$@"; do
     trace) step trace_$arg 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$arg -o run -- python3 bench.py $(cfg_args $arg) --no-cpu-baseline;;
     ab)    IFS=: read -r sc libs kn <<< "$arg"
            LIBS="${libs//,/ }" SCENES=$sc KERNEL=${kn:-ao} step ab_${sc}_${kn:-ao} 900 bash tools/ab_builds.sh;;
+    pmcuser) # lambda: the restated AO lambda (bench's user leg), ref: ao/main.cpp's own kernel through the
+             # reference's headers -- both on hip_sched::frames, 32 frames per launch, C3
+           case $arg in lambda) prog="build/tests/user_kernels bench 708 1920 1080 /tmp 4 32";;
+                        ref) prog="oracle/_ref/ref_kernels bench hf1M 1920 1080 4 32";; esac
+           d=$OUT/pmcuser_$arg
+           step pmcuser_${arg}_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $d/trace -o run -- $prog
+           step pmcuser_${arg}_tcp 300 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD --output-format csv -d $d/pmc_tcp -o run -- $prog
+           step pmcuser_${arg}_hbm 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $d/pmc_hbm -o run -- $prog
+           step pmcuser_${arg}_wr 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $d/pmc_wr -o run -- $prog
+           step pmcuser_${arg}_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_SALU --output-format csv -d $d/pmc_sq -o run -- $prog
+           python3 tools/pmc_user.py $d $d/pmc_user_$arg.json "$prog" 32 $d/trace && cp $d/pmc_user_$arg.json profiles/;;
+    user)  # user-kernel throughput (C3): the restated AO lambda and ao/main.cpp's own kernel (reference
+           # headers), one frame per launch and 32 in flight, alternating, ${arg:-2} repetitions
+           for rep in $(seq 1 ${arg:-2}); do for F in 1 32; do L=20; [ $F -gt 1 ] && L=4
+             for b in build/tests/user_kernels oracle/_ref/ref_kernels; do [ -x $b ] || continue
+               case $b in *ref_kernels*) a="bench hf1M 1920 1080 $L $F";; *) a="bench 708 1920 1080 /tmp $L $F";; esac
+               TAIL=1 step user_$(basename $b)_F${F}_$rep 150 $b $a
+               echo "$(basename $b) F=$F $(grep frame_ms_median $OUT/user_$(basename $b)_F${F}_$rep.log)" >> $OUT/user.log
+             done; done; done;;
+    counters) step counters_list 120 rocprofv3 -L;;
     cmd)   IFS=: read -r name t c <<< "$arg"; step $name $t bash -c "$c";;
     *) echo "unknown step $s"; exit 2;;
   esac

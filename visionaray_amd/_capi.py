@@ -13,7 +13,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VRH_LIB") or os.path.join(_HERE, "_lib", "libvrh.so")
 
 # enums (vrh.h)
-VRH_OK, VRH_ERR_INVALID, VRH_ERR_HIP, VRH_ERR_OOM, VRH_ERR_UNSUPPORTED, VRH_ERR_NO_DEVICE = range(6)
+VRH_OK, VRH_ERR_INVALID, VRH_ERR_HIP, VRH_ERR_OOM, VRH_ERR_UNSUPPORTED, VRH_ERR_NO_DEVICE, VRH_ERR_TIMEOUT = range(7)
+VRH_GROUP_TIMEOUT_MS = 120000
 VRH_PRIM_TRI64, VRH_PRIM_SPHERE48 = 0, 1
 VRH_KERNEL_PRIMARY, VRH_KERNEL_AO, VRH_KERNEL_SIMPLE, VRH_KERNEL_MULTI_HIT, VRH_KERNEL_WHITTED = 0, 1, 2, 3, 4
 VRH_MAX_HITS = 16
@@ -196,6 +197,9 @@ SIGNATURES = {
     "vrh_build_bvh": (C.c_int, [_vp, _u32, _u32, _vp, C.POINTER(_u32), _vp, C.POINTER(_u32)]),
     "vrh_group_get_id": (C.c_int, [C.c_void_p]),
     "vrh_group_join": (C.c_int, [_vp, _u32, _u32, C.c_void_p, C.POINTER(_vp)]),
+    "vrh_group_join_timeout": (C.c_int, [_vp, _u32, _u32, C.c_void_p, _u32, C.POINTER(_vp)]),
+    "vrh_group_set_timeout": (C.c_int, [_vp, _u32]),
+    "vrh_group_failed": (C.c_int, [_vp]),
     "vrh_group_create_local": (C.c_int, [_u32, C.POINTER(_vp), C.POINTER(_vp)]),
     "vrh_group_info": (C.c_int, [_vp, C.POINTER(_u32), C.POINTER(_u32)]),
     "vrh_group_sync": (C.c_int, [_vp]),

@@ -815,13 +815,17 @@ class render_group:
     with render_sharded(members, ...).  The exchange is libvrh's (ncclSend / ncclRecv on the
     group's own stream); nothing of it goes through torch."""
 
-    def __init__(self, ctx, nranks, rank, uid):
+    def __init__(self, ctx, nranks, rank, uid, timeout_ms=0):
+        """timeout_ms: the deadline of every wait on a peer (join, exchange, sync); 0 = the library's
+        VRH_GROUP_TIMEOUT_MS.  A missed deadline aborts the communicator and raises VrhError with
+        code VRH_ERR_TIMEOUT instead of hanging (vrh_group_join_timeout)."""
         if len(uid) != GROUP_ID_BYTES:
             raise ValueError("render_group: the id is 128 bytes (vrh_group_id)")
         self.ctx = ctx
         buf = (C.c_char * GROUP_ID_BYTES).from_buffer_copy(uid)
         h = C.c_void_p()
-        capi.check("vrh_group_join", ctx.handle, nranks, rank, C.cast(buf, C.c_void_p), C.byref(h))
+        capi.check("vrh_group_join_timeout", ctx.handle, nranks, rank, C.cast(buf, C.c_void_p), int(timeout_ms),
+                   C.byref(h))
         self.handle = h
         self.nranks, self.rank = nranks, rank
 
@@ -854,6 +858,14 @@ class render_group:
 
     def sync(self):
         capi.check("vrh_group_sync", self.handle)
+
+    def set_timeout(self, timeout_ms):
+        capi.check("vrh_group_set_timeout", self.handle, int(timeout_ms))
+
+    @property
+    def failed(self):
+        """True once the group was aborted (an RCCL error or a missed deadline)."""
+        return bool(capi.lib().vrh_group_failed(self.handle)) if getattr(self, "handle", None) else False
 
     def close(self):
         if getattr(self, "handle", None):

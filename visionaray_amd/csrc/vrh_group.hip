@@ -25,9 +25,11 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 using namespace vrh;
@@ -50,6 +52,11 @@ struct vrh_group
     uint32_t next = 0;
     uint8_t* work = nullptr;               // colour-only gathers: one shard's prim ids + AO masks before packing
     size_t work_bytes = 0;
+    // failure containment (vrh.h vrh_group_join_timeout): a joined group's communicator is non-blocking
+    // and every wait on a peer has a deadline; a group that missed one or saw an RCCL error is aborted
+    bool nonblocking = false;
+    bool failed = false;
+    uint32_t timeout_ms = VRH_GROUP_TIMEOUT_MS;
 };
 
 namespace {
@@ -78,17 +85,96 @@ int group_init_common(vrh_group* g)
 using plan::wire_layout;
 using plan::layout_for;
 
+using steady = std::chrono::steady_clock;
+
+// abort the communicator (ncclCommAbort returns without the peers) and mark the group failed
+int fail_group(vrh_group* g, int code, const std::string& msg)
+{
+    if (g->comm) { (void)ncclCommAbort(g->comm); g->comm = nullptr; }
+    g->failed = true;
+    set_error(msg);
+    return code;
+}
+
+// poll between checks: spin for the first 20 ms (a finished exchange is seen within microseconds,
+// vrh_group_sync ends bench's timed region), then sleep 1 ms per check
+void poll_pause(steady::time_point t0)
+{
+    if (steady::now() - t0 < std::chrono::milliseconds(20)) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::milliseconds(1));
+}
+
+// the communicator's state until nothing is in progress (a non-blocking init, or the enqueue of a
+// group of send / receive / broadcast calls), against the group's deadline
+int wait_comm(vrh_group* g, const char* what)
+{
+    if (!g->comm) return VRH_OK;
+    const auto t0 = steady::now();
+    const auto deadline = t0 + std::chrono::milliseconds(g->timeout_ms);
+    for (;;)
+    {
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t r = ncclCommGetAsyncError(g->comm, &st);
+        if (r != ncclSuccess) return fail_group(g, VRH_ERR_HIP, std::string(what) + ": ncclCommGetAsyncError: " + ncclGetErrorString(r));
+        if (st == ncclSuccess) return VRH_OK;
+        if (st != ncclInProgress) return fail_group(g, VRH_ERR_HIP, std::string(what) + ": " + ncclGetErrorString(st));
+        if (steady::now() > deadline)
+            return fail_group(g, VRH_ERR_TIMEOUT, std::string(what) + ": no answer from a group peer within " +
+                                                  std::to_string(g->timeout_ms) + " ms (communicator aborted)");
+        poll_pause(t0);
+    }
+}
+
+// the group's streams (and the context stream, ctx_too) until idle, watching the communicator for
+// an asynchronous error, against the deadline -- in place of hipStreamSynchronize, which would wait
+// forever for a receive whose sender died
+int wait_streams(vrh_group* g, bool ctx_too, const char* what)
+{
+    VRH_HIP(hipSetDevice(g->ctx->device));
+    if (ctx_too) VRH_HIP(ctx_join(g->ctx));
+    const auto t0 = steady::now();
+    const auto deadline = t0 + std::chrono::milliseconds(g->timeout_ms);
+    for (;;)
+    {
+        bool busy = false;
+        for (hipStream_t s : { ctx_too ? g->ctx->stream : nullptr, g->stream })
+        {
+            if (!s) continue;
+            const hipError_t e = hipStreamQuery(s);
+            if (e == hipErrorNotReady) busy = true;
+            else if (e != hipSuccess) { set_error(std::string(what) + ": " + hipGetErrorString(e)); return VRH_ERR_HIP; }
+        }
+        if (!busy) return VRH_OK;
+        if (g->comm)
+        {
+            ncclResult_t st = ncclSuccess;
+            if (ncclCommGetAsyncError(g->comm, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress)
+                return fail_group(g, VRH_ERR_HIP, std::string(what) + ": " + ncclGetErrorString(st));
+        }
+        if (steady::now() > deadline)
+            return fail_group(g, VRH_ERR_TIMEOUT, std::string(what) + ": the exchange did not finish within " +
+                                                  std::to_string(g->timeout_ms) + " ms (communicator aborted)");
+        poll_pause(t0);
+    }
+}
+
+#define VRH_GROUP_OK(g, what)                                                                      \
+    do {                                                                                           \
+        if ((g)->failed) { set_error(std::string(what) + ": the render group failed earlier"); return VRH_ERR_INVALID; } \
+    } while (0)
+
 // (re)allocate a staging buffer; an exchange or render still using the old one is waited for first
 int grow(vrh_group* g, uint8_t*& p, size_t& have, size_t need)
 {
     if (have >= need) return VRH_OK;
-    VRH_HIP(hipStreamSynchronize(g->ctx->stream));
-    VRH_HIP(hipStreamSynchronize(g->stream));
+    const int rc = wait_streams(g, true, "vrh_render_sharded: staging");
+    if (rc) return rc;
     if (p) { VRH_HIP(hipFree(p)); p = nullptr; have = 0; }
     VRH_HIP(hipMalloc(&p, need));
     have = need;
     return VRH_OK;
 }
+
 
 // what a scene replica needs to know before its arrays arrive (vrh_group_broadcast_scene)
 struct scene_header
@@ -132,24 +218,62 @@ VRH_API int vrh_group_get_id(vrh_group_id* id)
     return VRH_OK;
 }
 
-VRH_API int vrh_group_join(vrh_ctx* ctx, uint32_t nranks, uint32_t rank, const vrh_group_id* id, vrh_group** out)
+VRH_API int vrh_group_join_timeout(vrh_ctx* ctx, uint32_t nranks, uint32_t rank, const vrh_group_id* id,
+                                   uint32_t timeout_ms, vrh_group** out)
 {
     VRH_CHECK(ctx && id && out && nranks >= 1 && rank < nranks, "vrh_group_join: bad argument");
     *out = nullptr;
     auto* g = new (std::nothrow) vrh_group;
     if (!g) { set_error("host allocation failed"); return VRH_ERR_OOM; }
     g->ctx = ctx; g->nranks = nranks; g->rank = rank;
+    g->timeout_ms = timeout_ms ? timeout_ms : VRH_GROUP_TIMEOUT_MS;
     int rc = group_init_common(g);
     if (rc == VRH_OK)
     {
+        // non-blocking communicator: the init returns at once (ncclInProgress) and is polled against
+        // the deadline, so a peer that never joins gives an error instead of a hang
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof(u));
-        ncclResult_t r = ncclCommInitRank(&g->comm, int(nranks), u, int(rank));
-        if (r != ncclSuccess) { set_error(std::string("vrh_group_join: ncclCommInitRank: ") + ncclGetErrorString(r)); rc = VRH_ERR_HIP; }
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        const ncclResult_t r = ncclCommInitRankConfig(&g->comm, int(nranks), u, int(rank), &cfg);
+        if (r != ncclSuccess && r != ncclInProgress)
+        {
+            set_error(std::string("vrh_group_join: ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+            rc = VRH_ERR_HIP;
+        }
+        else
+        {
+            g->nonblocking = true;
+            rc = wait_comm(g, "vrh_group_join");
+        }
     }
-    if (rc != VRH_OK) { vrh_group_free(g); return rc; }
+    if (rc != VRH_OK)
+    {
+        const std::string msg = vrh_last_error();
+        vrh_group_free(g);
+        set_error(msg);
+        return rc;
+    }
     *out = g;
     return VRH_OK;
+}
+
+VRH_API int vrh_group_join(vrh_ctx* ctx, uint32_t nranks, uint32_t rank, const vrh_group_id* id, vrh_group** out)
+{
+    return vrh_group_join_timeout(ctx, nranks, rank, id, 0u, out);
+}
+
+VRH_API int vrh_group_set_timeout(vrh_group* g, uint32_t timeout_ms)
+{
+    VRH_CHECK(g && timeout_ms > 0, "vrh_group_set_timeout: bad argument");
+    g->timeout_ms = timeout_ms;
+    return VRH_OK;
+}
+
+VRH_API int vrh_group_failed(const vrh_group* g)
+{
+    return g && g->failed ? 1 : 0;
 }
 
 VRH_API int vrh_group_create_local(uint32_t ndev, vrh_ctx* const* ctxs, vrh_group** out)
@@ -194,20 +318,27 @@ VRH_API int vrh_group_info(const vrh_group* g, uint32_t* nranks, uint32_t* rank)
 VRH_API int vrh_group_sync(vrh_group* g)
 {
     VRH_CHECK(g, "vrh_group_sync: null");
-    VRH_HIP(hipSetDevice(g->ctx->device));
-    VRH_HIP(ctx_join(g->ctx));
-    VRH_HIP(hipStreamSynchronize(g->ctx->stream));
-    VRH_HIP(hipStreamSynchronize(g->stream));
-    return VRH_OK;
+    VRH_GROUP_OK(g, "vrh_group_sync");
+    return wait_streams(g, true, "vrh_group_sync");
 }
 
 VRH_API int vrh_group_free(vrh_group* g)
 {
     if (!g) return VRH_OK;
     if (g->ctx) (void)hipSetDevice(g->ctx->device);
-    if (g->ctx) (void)hipStreamSynchronize(g->ctx->stream);
-    if (g->stream) (void)hipStreamSynchronize(g->stream);
-    if (g->comm) (void)ncclCommDestroy(g->comm);
+    if (!g->failed)
+    {
+        // the group's work first (with the deadline: a dead peer fails the group instead of hanging)
+        if (g->ctx && g->stream) (void)wait_streams(g, true, "vrh_group_free");
+        if (g->comm && g->nonblocking)
+        {
+            // a non-blocking communicator is finalized (polled like every wait) before it is destroyed
+            const ncclResult_t r = ncclCommFinalize(g->comm);
+            if (r != ncclSuccess && r != ncclInProgress) (void)fail_group(g, VRH_ERR_HIP, "vrh_group_free: ncclCommFinalize");
+            else (void)wait_comm(g, "vrh_group_free");
+        }
+    }
+    if (g->comm) (void)(g->failed ? ncclCommAbort(g->comm) : ncclCommDestroy(g->comm));
     for (auto& s : g->slot)
     {
         if (s.rendered) (void)hipEventDestroy(s.rendered);
@@ -236,6 +367,7 @@ VRH_API int vrh_render_sharded(uint32_t n, vrh_group* const* groups, const vrh_s
     for (uint32_t i = 0; i < n; ++i)
     {
         VRH_CHECK(groups[i] && scenes[i] && groups[i]->nranks == N, "vrh_render_sharded: groups of one communicator");
+        VRH_GROUP_OK(groups[i], "vrh_render_sharded");
         VRH_CHECK(scenes[i]->ctx == groups[i]->ctx, "vrh_render_sharded: scene i must live on group i's context");
         VRH_CHECK(kernels[i].kind == kernels[0].kind && kernels[i].samples == kernels[0].samples,
                   "vrh_render_sharded: one kernel for every rank");
@@ -329,7 +461,20 @@ VRH_API int vrh_render_sharded(uint32_t n, vrh_group* const* groups, const vrh_s
     }
     const ncclResult_t xe = ncclGroupEnd();
     if (xr == ncclSuccess) xr = xe;
-    if (xr != ncclSuccess) { set_error(std::string("vrh_render_sharded: exchange: ") + ncclGetErrorString(xr)); return VRH_ERR_HIP; }
+    if (xr != ncclSuccess && xr != ncclInProgress)
+    {
+        const std::string msg = std::string("vrh_render_sharded: exchange: ") + ncclGetErrorString(xr);
+        for (uint32_t i = 0; i < n; ++i) (void)fail_group(groups[i], VRH_ERR_HIP, msg);
+        return VRH_ERR_HIP;
+    }
+    // non-blocking communicators: the sends / receives are enqueued once nothing is in progress (the
+    // first exchange with a peer connects to it -- a dead peer is caught here, at the deadline)
+    for (uint32_t i = 0; i < n; ++i)
+    {
+        VRH_HIP(hipSetDevice(groups[i]->ctx->device));
+        const int rc = wait_comm(groups[i], "vrh_render_sharded: exchange");
+        if (rc) return rc;
+    }
     // 3. the root lays the bands back into image order, frame by frame
     for (uint32_t i = 0; i < n; ++i)
     {
@@ -450,6 +595,7 @@ VRH_API int vrh_group_broadcast_scene(uint32_t n, vrh_group* const* groups, cons
     for (uint32_t i = 0; i < n; ++i)
     {
         VRH_CHECK(groups[i] && groups[i]->nranks == groups[0]->nranks, "vrh_group_broadcast_scene: groups of one communicator");
+        VRH_GROUP_OK(groups[i], "vrh_group_broadcast_scene");
         out[i] = nullptr;
         if (groups[i]->rank == 0) root = int(i);
     }
@@ -492,14 +638,17 @@ VRH_API int vrh_group_broadcast_scene(uint32_t n, vrh_group* const* groups, cons
             r = ncclBroadcast(dh[i], dh[i], sizeof(scene_header), ncclUint8, 0, groups[i]->comm, groups[i]->stream);
         const ncclResult_t r2 = ncclGroupEnd();
         if (r == ncclSuccess) r = r2;
-        if (r != ncclSuccess) { set_error(std::string("vrh_group_broadcast_scene: header: ") + ncclGetErrorString(r)); rc = VRH_ERR_HIP; }
+        if (r != ncclSuccess && r != ncclInProgress) { set_error(std::string("vrh_group_broadcast_scene: header: ") + ncclGetErrorString(r)); rc = VRH_ERR_HIP; }
+        for (uint32_t i = 0; i < n && rc == VRH_OK; ++i)
+            if (hipSetDevice(groups[i]->ctx->device) == hipSuccess)
+                rc = wait_comm(groups[i], "vrh_group_broadcast_scene: header");
     }
     std::vector<scene_header> hh(n);
     for (uint32_t i = 0; i < n && rc == VRH_OK; ++i)
     {
         vrh_group* g = groups[i];
-        if (hipSetDevice(g->ctx->device) != hipSuccess || hipStreamSynchronize(g->stream) != hipSuccess ||
-            hipMemcpy(&hh[i], dh[i], sizeof(scene_header), hipMemcpyDeviceToHost) != hipSuccess)
+        rc = wait_streams(g, false, "vrh_group_broadcast_scene: header");
+        if (rc == VRH_OK && hipMemcpy(&hh[i], dh[i], sizeof(scene_header), hipMemcpyDeviceToHost) != hipSuccess)
         { set_error("vrh_group_broadcast_scene: header download"); rc = VRH_ERR_HIP; }
     }
     free_headers();
@@ -552,12 +701,18 @@ VRH_API int vrh_group_broadcast_scene(uint32_t n, vrh_group* const* groups, cons
         }
         const ncclResult_t r2 = ncclGroupEnd();
         if (r == ncclSuccess) r = r2;
-        if (r != ncclSuccess) { free_out(); set_error(std::string("vrh_group_broadcast_scene: ") + ncclGetErrorString(r)); return VRH_ERR_HIP; }
+        if (r != ncclSuccess && r != ncclInProgress) { free_out(); set_error(std::string("vrh_group_broadcast_scene: ") + ncclGetErrorString(r)); return VRH_ERR_HIP; }
+        for (uint32_t i = 0; i < n; ++i)
+        {
+            int rc2 = hipSetDevice(groups[i]->ctx->device) == hipSuccess ? wait_comm(groups[i], "vrh_group_broadcast_scene")
+                                                                         : VRH_ERR_HIP;
+            if (rc2) { const std::string m = vrh_last_error(); free_out(); set_error(m); return rc2; }
+        }
     }
     for (uint32_t i = 0; i < n; ++i)
     {
-        if (hipSetDevice(groups[i]->ctx->device) != hipSuccess || hipStreamSynchronize(groups[i]->stream) != hipSuccess)
-        { free_out(); set_error("vrh_group_broadcast_scene: sync"); return VRH_ERR_HIP; }
+        const int rc2 = wait_streams(groups[i], false, "vrh_group_broadcast_scene");
+        if (rc2) { const std::string m = vrh_last_error(); free_out(); set_error(m); return rc2; }
     }
     return VRH_OK;
 }

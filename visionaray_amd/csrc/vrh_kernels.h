@@ -41,6 +41,10 @@ struct render_params
     float width_f, height_f;  // (float)width, (float)height (sched_common.h:137-138 divides by them)
 
     uint32_t samples;
+    // ceil(2^20 / samples): (c * samples_recip) >> 20 == c / samples for every c < 64 * samples
+    // (checked for samples 1..32: the error c * (recip - 2^20 / samples) / 2^20 stays below
+    // 1 / samples), a multiply instead of a division whose reciprocal the compiler kept in a VGPR
+    uint32_t samples_recip;
     float radius, eps;
     float bg[4];
     // pixel sampler pass (vrh_render_sampled): primary rays through (x + px_off, y + px_off) or, with

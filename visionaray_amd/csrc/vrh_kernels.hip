@@ -47,6 +47,16 @@ constexpr int AO_CUT = AO_SLOT_PX + 2 * 64 / 4;         // the current tile's en
 #ifndef VRH_AO_CUT_MAX
 #define VRH_AO_CUT_MAX 8
 #endif
+// the AO kernel's lane state: 1 = max_t derived from `any` (AO rays: the radius, primaries: max())
+#ifndef VRH_AO_LEAN
+#define VRH_AO_LEAN 1
+#endif
+// 1 = the AO instances honour a descent cap (VRH_OPT_DESCENT_CAP; measured no gain on AO, round 4
+// profiles/r04/ab/cut16_dcap.log); 0 = compiled out (no `resume` / visit counter per lane)
+#ifndef VRH_AO_DCAP
+#define VRH_AO_DCAP 0
+#endif
+constexpr bool AO_CAPPED = VRH_AO_DCAP != 0;
 constexpr uint32_t CUT_MAX = VRH_AO_CUT_MAX;            // records of a cut
 constexpr int AO_SH = AO_CUT + 2 * 8 * CUT_MAX;        // two levels x entries of box lo xyz, hi xyz, link, pad
 // Tail sharing (render_params::ao_share, blocks of several waves): once the tile queues are dry, a
@@ -57,6 +67,11 @@ constexpr int AO_SH = AO_CUT + 2 * 8 * CUT_MAX;        // two levels x entries o
 // has seen the queues run dry.
 constexpr int AO_WAVE_WORDS = AO_SH + 8;
 constexpr uint32_t SH_TILE = 0, SH_PAR = 1, SH_NEXT = 2, SH_AVAIL = 3, SH_HELP = 4, SH_CUTN = 5, SH_DRY = 6;
+// the root link, read from the kernel's argument segment where it is used (a scalar load) instead of
+// being held in a register across the refill loop, where the register allocator of the 6-wave AO
+// instances copied it to a VGPR and spilled that to scratch
+__device__ __forceinline__ uint32_t kernarg_root();
+
 __device__ __forceinline__ uint32_t lds_ld(const uint32_t* p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -243,10 +258,16 @@ __device__ __forceinline__ uint32_t strip_lo(const render_params& P, uint32_t q,
     return (uint32_t)(((uint64_t)P.num_tiles * q) / nq);
 }
 
+#ifndef VRH_PRIMARY_CLUSTER
+#define VRH_PRIMARY_CLUSTER 1
+#endif
+// CLUSTER = false: an instance without the cluster order's code (its launches hand out the band order
+// for xcd_queues 3)
+template <bool CLUSTER = true>
 __device__ __forceinline__ uint32_t next_tile(const render_params& P, tile_queue& tq, uint32_t lane)
 {
     const uint32_t nq = P.xcd_queues ? 8u : 1u;
-    if (P.xcd_queues == 3u)
+    if (CLUSTER && P.xcd_queues == 3u)
     {
         // cluster order (frames in flight): queue q owns strip q of the launch's bands; a band is cut
         // into clusters of P.cluster tiles, and the units of a strip are (cluster, frame, tile) with
@@ -279,7 +300,7 @@ __device__ __forceinline__ uint32_t next_tile(const render_params& P, tile_queue
         }
         return NONE;
     }
-    if (P.xcd_queues == 2u)
+    if (P.xcd_queues == 2u || (!CLUSTER && P.xcd_queues == 3u))
     {
         // band-interleaved (frames in flight): the launch's (band, frame) units in band-major order,
         // unit u = band * num_frames + frame dealt to queue u % 8 -- all 8 XCDs sweep the image's
@@ -541,6 +562,13 @@ __device__ __forceinline__ int list_next(const render_params& P, bool any, uint3
     return -1;
 }
 
+__device__ __forceinline__ uint32_t kernarg_root()
+{
+    typedef const volatile __attribute__((address_space(4))) uint32_t karg_u32;
+    karg_u32* ka = (karg_u32*)__builtin_amdgcn_kernarg_segment_ptr();
+    return ka[offsetof(render_params, root) / 4u];
+}
+
 // One refilling loop per wave.  Primary rays (one per pixel of the wave's tile)
 // and AO rays (published as soon as their primary hit is known) are stepped by the same
 // instruction stream (ray_step); a lane that finishes a ray immediately takes the next one, so
@@ -565,28 +593,19 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     const uint32_t block = blockDim.x;
 
     stack_t<SPILL> st;
-    st.mem = smem;
-    st.base = tid;
-    st.stride = block;
-    st.top = tid;
-    st.end = tid + P.stack_cap * block;
-    st.lim_off = (SPILL ? P.stack_total : P.stack_cap) * block;
-    // the overflow entries of lane tid start at entry stack_cap: word top - stack_cap * block of this
-    // block's overflow area, i.e. spill[top] with the pointer moved back by stack_cap * block words.
-    // The move is done on the address as an integer: for block 0 it points before the allocation,
-    // which pointer arithmetic (an inbounds GEP) may not express; every access spill[top] with
-    // top >= stack_cap * block lands inside this block's area
-    st.spill = SPILL ? reinterpret_cast<uint32_t*>(
-                           reinterpret_cast<uintptr_t>(P.stack_spill + size_t(blockIdx.x) * (P.stack_total - P.stack_cap) * block)
-                           - uintptr_t(P.stack_cap) * block * sizeof(uint32_t))
-                     : nullptr;
+    // the overflow entries of this block: (stack_total - stack_cap) entries per lane, same column layout
+    st.init(smem, tid, block, P.stack_cap, SPILL ? P.stack_total : P.stack_cap,
+            SPILL ? P.stack_spill + size_t(blockIdx.x) * (P.stack_total - P.stack_cap) * block : nullptr);
     uint32_t* ao_area = smem + P.stack_cap * block + wave * AO_WAVE_WORDS;
     test_counts cnt = {};
-    uint64_t rays_total = 0, hits_total = 0;
+    // per-lane ray / hit counts of this launch (below 2^32 per lane: a launch traces < 2^32 rays)
+    uint32_t rays_total = 0, hits_total = 0;
     const hit_mask_params hml = P.hmask;          // a local copy: &P would spill the kernel arguments
     const hit_mask_params* hm = &hml;             // ray_step tests hm->mask
-    if (P.wave_times && lane == 0)      // the start is stored at once: nothing stays live across the loop
-        P.wave_times[2 * (size_t(blockIdx.x) * (blockDim.x >> 6) + wave)] = wall_clock64();
+    // the wave's (start, end) slot: the start is stored at once, the end slot kept as a wave-uniform
+    // pointer (nothing of the prologue's per-lane values stays live across the loop)
+    unsigned long long* const wt_slot = P.wave_times ? P.wave_times + 2 * (size_t(blockIdx.x) * (blockDim.x >> 6) + uu(wave)) : nullptr;
+    if (wt_slot && lane == 0) wt_slot[0] = wall_clock64();
 
     // lane state: the ray it is stepping
     constexpr uint32_t IDLE = 0, PRIMARY = 1, AORAY = 2;
@@ -604,7 +623,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
     {
         // ---- primary visibility: stream pixels, write each when its ray finishes ------------
         tile_queue tq = queue_init(P);
-        uint32_t tile = next_tile(P, tq, lane);
+        uint32_t tile = next_tile<VRH_PRIMARY_CLUSTER != 0>(P, tq, lane);
         uint32_t handed = 0;                       // pixels of `tile` handed out (wave-uniform)
         uint32_t out_o = 0;
         hit_extra hx = { 0.0f, 0.0f, 0u };
@@ -624,7 +643,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             {
                 if (handed >= 64u && tile != NONE)
                 {
-                    tile = next_tile(P, tq, lane);
+                    tile = next_tile<VRH_PRIMARY_CLUSTER != 0>(P, tq, lane);
                     handed = 0;
                 }
                 if (tile != NONE)
@@ -822,7 +841,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         // slot pixels and cut are recs_ / spx / cut_, cutn (this wave's, or a sibling's it helps)
         auto start_ao = [&](const float* recs_, const uint8_t* spx, const float* cut_, uint32_t cutn, uint32_t tile,
                             uint32_t par, uint32_t cand, uint32_t owner) {
-            const uint32_t slot = cand / S, smp = cand - slot * S;
+            // cand / S by the host's reciprocal (exact for cand < 64 S, render_params::samples_recip)
+            const uint32_t slot = (cand * P.samples_recip) >> 20, smp = cand - slot * S;
             uint32_t x, y, orow, fr;
             tile_pixel(P, tile, spx[par * 64u + slot], x, y, orow, fr);
             r = ao_ray<COUNT>(P, recs_, slot, smp, y * P.width + x, fr, cnt);
@@ -914,7 +934,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     if (P.ao_cut && issC == 0u)
                     {
                         // the tile's first AO hand-out: all its hits are published (ao_gate)
-                        cutN = ao_cut_build<COUNT>(P, recs, pubC, cut, lane, cnt);
+                        cutN = uu(ao_cut_build<COUNT>(P, recs, pubC, cut, lane, cnt));   // wave-uniform (SGPR)
                         if (cutN != NONE && cutN + 4u > P.stack_cap) cutN = NONE;
                     }
                 // once the block's queues are dry, the tile's AO rays are handed out through the LDS
@@ -956,7 +976,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                     r = primary_ray<SAMPLED>(P, fr, x, y);
                     finite = finite_ray(r);
                     best_t = FMAX; best_prim = 0; steps = 0; max_t = FMAX; any = false; quad = false;
-                    st.reset(); st.push(P.root); resume = NO_RESUME;
+                    st.reset(); st.push(LIST ? P.root : kernarg_root()); resume = NO_RESUME;
                     bk = 0; res_t = FMAX; res_prim = 0;
                     mode = PRIMARY;
                     tag = k;
@@ -1014,9 +1034,14 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             int rc = 0;
             if (busy)
             {
+                // the AO kernel's rays: any-hit AO rays up to the radius, closest-hit primaries unbounded
+                // (derived from `any` instead of a per-lane max_t).  The root link ray_step restarts a
+                // 4-wide descent at is pair 0: 4-wide records exist only for trees whose root is a pair,
+                // stored first (render_params::quad_ok checks it), so no register holds it
+                const float mt = VRH_AO_LEAN ? (any ? P.radius : FMAX) : max_t;
                 rc = (P.fast_ok && __ballot(!finite) == 0ull)
-                    ? ray_step<KIND, COUNT, true>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm)
-                    : ray_step<KIND, COUNT, false>(P.pairs, P.prims, P.quads, P.root, quad, r, max_t, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm);
+                    ? ray_step<KIND, COUNT, true, false, void, AO_CAPPED>(P.pairs, P.prims, P.quads, 0u, quad, r, mt, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm)
+                    : ray_step<KIND, COUNT, false, false, void, AO_CAPPED>(P.pairs, P.prims, P.quads, 0u, quad, r, mt, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm);
             }
             if constexpr (LIST)
                 if (busy && rc < 0) rc = list_next(P, any, bk, res_t, res_prim, best_t, best_prim, st, resume);
@@ -1082,9 +1107,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         }
     }
 
-    if (P.wave_times && lane == 0)
-        P.wave_times[2 * (size_t(blockIdx.x) * (blockDim.x >> 6) + wave) + 1] = wall_clock64();
-    flush_totals<COUNT>(P, lane, rays_total, hits_total, cnt);
+    if (wt_slot && __lane_id() == 0u) wt_slot[1] = wall_clock64();
+    flush_totals<COUNT>(P, __lane_id(), rays_total, hits_total, cnt);
 }
 
 // un-interleave gathered packed shards [count][rows_per_shard][W] into the full image (vrh_plan.h
@@ -1159,14 +1183,16 @@ static kernel_fn pick(bool ao, bool count, int occ, int sched)
     return pick_occ<KIND, 1>(ao, count, sched);
 }
 
-// the overflow-stack instances exist at the default budgets only: AO 5 waves / SIMD (triangles),
-// primary visibility 6
+// the overflow-stack instances exist at the register budgets the defaults choose from: AO 5 or 6
+// waves / SIMD (triangles), primary visibility 6 or 8
 template <int KIND>
 static kernel_fn pick_spill(bool ao, int occ, int sched)
 {
     const int s = sched == 3 ? 5 : 4;
     if (ao && KIND == dev::KIND_TRI && occ == 5) return pick_occ<KIND, 5>(true, false, s);
+    if (ao && KIND == dev::KIND_TRI && occ == 6) return pick_occ<KIND, 6>(true, false, s);
     if (!ao && occ == 6) return pick_occ<KIND, 6>(false, false, s);
+    if (!ao && occ == 8) return pick_occ<KIND, 8>(false, false, s);
     return nullptr;
 }
 

@@ -1181,7 +1181,8 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     p.quads = sc->quads;
     // 4-wide any-hit records: auto on for the AO step loop (with ao_gate), off elsewhere
     const bool wide = ctx->opt_wide == 1 || (ctx->opt_wide == 0 && ao_step);
-    p.quad_ok = (sc->quads && p.fast_ok && wide) ? 1u : 0u;
+    // (the AO kernel restarts a 4-wide descent that would overflow its stack at pair 0: the root)
+    p.quad_ok = (sc->quads && p.fast_ok && wide && sc->roots[0] == 0u) ? 1u : 0u;
     // per-tile entry cut of the 4-wide tree for AO rays (needs the gate: the tile's hits are known)
     // entries nearest-first (+3.5 % over the cut order, profiles/r02_ab/ab33_ao_cut_order*.log)
     p.ao_cut = (p.quad_ok && p.ao_gate && ctx->opt_cut != 2) ? (ctx->opt_cut == 3 ? 1u : 2u) : 0u;
@@ -1205,6 +1206,7 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     p.width = cam->width; p.height = cam->height;
     p.width_f = float(cam->width); p.height_f = float(cam->height);
     p.samples = ao ? k->samples : 0; p.radius = k->radius; p.eps = k->eps;
+    p.samples_recip = ao ? ((1u << 20) + p.samples - 1u) / p.samples : 0u;
     std::memcpy(p.bg, k->bg, 16);
     if (sp)
     {
