@@ -238,7 +238,9 @@ enum vrh_option {
                                     profiles/r02_ab/ab18_sphere_schedule.log); 4 returns
                                     VRH_ERR_UNSUPPORTED                                             */
     VRH_OPT_BLOCKS_PER_CU = 4,   /* resident blocks per CU for the persistent grid (auto: max)     */
-    VRH_OPT_WAVES_PER_SIMD = 5,  /* register budget of the unified kernel: 1 (none), 5, 6 or 8 (auto: 5 AO, 6 primary) */
+    VRH_OPT_WAVES_PER_SIMD = 5,  /* register budget of the unified kernel: 1 (none), 5, 6 or 8 (auto: AO 6
+                                    for BVHs at most 20 deep, else 5; primary visibility 8 for
+                                    triangles, 6 for spheres; shading kernels 1, whitted 5)      */
     VRH_OPT_EXACT_MINMAX = 6,    /* 1 = always use the ternary min/max slab test (auto: hardware
                                     min/max where provably identical, see vrh_device.h)           */
     VRH_OPT_XCD_QUEUES = 7,      /* tile queues: 1 = one per XCD (image strips) with stealing,
