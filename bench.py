@@ -215,10 +215,31 @@ def user_kernel_leg(W, H, n_rays):
         return {"error": f"rc {r.returncode}"}
     ms = float(rec["frame_ms_median"])
     # the lambda traces the built-in kernel's rays: the same primary rays, 8 AO rays per hit
-    return {"mrays": round(n_rays / (ms * 1e-3) / 1e6, 1), "frame_ms_median": ms,
-            "frames_per_launch": rec["frames_per_launch"], "launches": rec["launches"],
-            "kernel": "AO device lambda (ao/main.cpp's, random_sampler) via hip_kernels.h on hip_sched::frames",
-            "program": "build/tests/user_kernels bench 708 %d %d /tmp 4 32" % (W, H)}
+    leg = {"mrays": round(n_rays / (ms * 1e-3) / 1e6, 1), "frame_ms_median": ms,
+           "frames_per_launch": rec["frames_per_launch"], "launches": rec["launches"],
+           "kernel": "AO device lambda (ao/main.cpp's, random_sampler) via hip_kernels.h on hip_sched::frames",
+           "program": "build/tests/user_kernels bench 708 %d %d /tmp 4 32" % (W, H)}
+    # roofline of the user kernel, as the built-in's: the vector-L1 requests of the committed PMC pass of
+    # this program (profiles/pmc_user_lambda.json, kernel-source hash checked) x 16 B over the live launch
+    # time (median wall time of a 32-frame frames() launch: the kernel plus its launch, an upper bound)
+    pmc = load_json(os.path.join(ROOT, "profiles", "pmc_user_lambda.json")) or {}
+    roof = load_json(os.path.join(ROOT, "profiles", "l1_roof.json"))
+    from visionaray_amd.buildinfo import kernel_source_sha256
+    if (pmc.get("l1_requests_per_launch") and pmc.get("frames_per_launch") == rec["frames_per_launch"]
+            and pmc.get("kernel_source_sha256") == kernel_source_sha256() and roof):
+        launch_s = ms * 1e-3 * rec["frames_per_launch"]
+        achieved = pmc["l1_requests_per_launch"] * L1_REQ_BYTES / launch_s / 1e9
+        sq = load_json(os.path.join(ROOT, "profiles", "pmc_sq_lambda.json")) or {}
+        leg["roofline"] = {"bound": "vmem-l1", "unit": "GB/s", "achieved": round(achieved, 1), "peak": roof.get("peak_gbs"),
+                           "frac": round(achieved / roof["peak_gbs"], 4), "td_busy_frac": round(pmc["td_busy_frac"], 4),
+                           "l1_requests_per_launch": pmc["l1_requests_per_launch"],
+                           "waves_per_launch": pmc.get("waves_per_launch"),
+                           "lane_utilisation_valu": sq.get("lane_utilisation_valu"),
+                           "valu_insts_per_ray": sq.get("valu_insts_per_ray"),
+                           "source": "profiles/pmc_user_lambda.json, profiles/pmc_sq_lambda.json, profiles/l1_roof.json"}
+    else:
+        leg["roofline"] = None
+    return leg
 
 
 def frames_per_launch(steps, cap):

@@ -75,7 +75,7 @@ for s in "$@"; do
            step pmcuser_${arg}_tcp 300 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD --output-format csv -d $d/pmc_tcp -o run -- $prog
            step pmcuser_${arg}_hbm 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $d/pmc_hbm -o run -- $prog
            step pmcuser_${arg}_wr 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $d/pmc_wr -o run -- $prog
-           step pmcuser_${arg}_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_SALU --output-format csv -d $d/pmc_sq -o run -- $prog
+           step pmcuser_${arg}_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_SALU --output-format csv -d $d/pmc_sq -o run -- $prog
            python3 tools/pmc_user.py $d $d/pmc_user_$arg.json "$prog" 32 $d/trace && cp $d/pmc_user_$arg.json profiles/;;
     user)  # user-kernel throughput (C3): the restated AO lambda and ao/main.cpp's own kernel (reference
            # headers), one frame per launch and 32 in flight, alternating, ${arg:-2} repetitions
@@ -85,6 +85,20 @@ for s in "$@"; do
                TAIL=1 step user_$(basename $b)_F${F}_$rep 150 $b $a
                echo "$(basename $b) F=$F $(grep frame_ms_median $OUT/user_$(basename $b)_F${F}_$rep.log)" >> $OUT/user.log
              done; done; done;;
+    sq)    # one SQ pass (VALU lane utilisation, instructions per ray, issue / wait shares, waves):
+           # sq:<cfg> the built-in kernel of bench:<cfg> (RAYS = its rays per frame, default C3's),
+           # sq:lambda / sq:ref the user-kernel programs
+           SQC="SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_SALU"
+           d=$OUT/sq_$arg
+           case $arg in
+             lambda) step sq_$arg 300 rocprofv3 --pmc $SQC --output-format csv -d $d -o run -- build/tests/user_kernels bench 708 1920 1080 /tmp 4 32
+                     python3 tools/pmc_sq.py $d $d/pmc_sq_$arg.json "$arg" 32 13037200 user_render;;
+             ref)    step sq_$arg 300 rocprofv3 --pmc $SQC --output-format csv -d $d -o run -- oracle/_ref/ref_kernels bench hf1M 1920 1080 4 32
+                     python3 tools/pmc_sq.py $d $d/pmc_sq_$arg.json "$arg" 32 13037200 user_render;;
+             *)      a="$(cfg_args $arg) $Q"; set -- $(cfg_meta $arg)
+                     step sq_$arg 300 rocprofv3 --pmc $SQC --output-format csv -d $d -o run -- python3 bench.py $a
+                     python3 tools/pmc_sq.py $d $d/pmc_sq_$arg.json "$arg" $3 ${RAYS:-13037200};;
+           esac;;
     counters) step counters_list 120 rocprofv3 -L;;
     cmd)   IFS=: read -r name t c <<< "$arg"; step $name $t bash -c "$c";;
     *) echo "unknown step $s"; exit 2;;
