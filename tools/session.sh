@@ -79,8 +79,8 @@ for s in "$@"; do
            python3 tools/pmc_user.py $d $d/pmc_user_$arg.json "$prog" 32 $d/trace && cp $d/pmc_user_$arg.json profiles/;;
     user)  # user-kernel throughput (C3): the restated AO lambda and ao/main.cpp's own kernel (reference
            # headers), one frame per launch and 32 in flight, alternating, ${arg:-2} repetitions
-           for rep in $(seq 1 ${arg:-2}); do for F in 1 32; do L=20; [ $F -gt 1 ] && L=4
-             for b in build/tests/user_kernels oracle/_ref/ref_kernels; do [ -x $b ] || continue
+           for rep in $(seq 1 ${arg:-2}); do for F in ${FS:-1 32}; do L=20; [ $F -gt 1 ] && L=4
+             for b in ${BINS:-build/tests/user_kernels oracle/_ref/ref_kernels}; do [ -x $b ] || continue
                case $b in *ref_kernels*) a="bench hf1M 1920 1080 $L $F";; *) a="bench 708 1920 1080 /tmp $L $F";; esac
                TAIL=1 step user_$(basename $b)_F${F}_$rep 150 $b $a
                echo "$(basename $b) F=$F $(grep frame_ms_median $OUT/user_$(basename $b)_F${F}_$rep.log)" >> $OUT/user.log
@@ -92,6 +92,8 @@ for s in "$@"; do
            d=$OUT/sq_$arg
            case $arg in
              lambda) step sq_$arg 300 rocprofv3 --pmc $SQC --output-format csv -d $d -o run -- build/tests/user_kernels bench 708 1920 1080 /tmp 4 32
+                     python3 tools/pmc_sq.py $d $d/pmc_sq_$arg.json "$arg" 32 13037200 user_render;;
+             uk_*)   step sq_$arg 300 rocprofv3 --pmc $SQC --output-format csv -d $d -o run -- build/tests/$arg bench 708 1920 1080 /tmp 4 32
                      python3 tools/pmc_sq.py $d $d/pmc_sq_$arg.json "$arg" 32 13037200 user_render;;
              ref)    step sq_$arg 300 rocprofv3 --pmc $SQC --output-format csv -d $d -o run -- oracle/_ref/ref_kernels bench hf1M 1920 1080 4 32
                      python3 tools/pmc_sq.py $d $d/pmc_sq_$arg.json "$arg" 32 13037200 user_render;;
