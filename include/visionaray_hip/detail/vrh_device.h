@@ -234,12 +234,21 @@ struct stack_t
     // k more entries fit
     __device__ __forceinline__ bool room(uint32_t k) const { return used + k * stride <= lim_off; }
 #if defined(__HIP_DEVICE_COMPILE__)
+    typedef __attribute__((address_space(3))) uint32_t lds_word;
+    // the LDS byte address of the lane's entry at `used` (SPILL): one per-lane value serves the LDS access
+    // and, past the LDS part, the offset into the overflow block's buffer resource
+    __device__ __forceinline__ uint32_t entry_addr() const
+    {
+        return uint32_t(reinterpret_cast<uintptr_t>((lds_word*)mem)) + (base + used) * 4u;
+    }
     __device__ __forceinline__ __amdgpu_buffer_rsrc_t overflow() const
     {
         // gfx9 buffer descriptor word 3 (raw dwords, as composable_kernel's CK_BUFFER_RESOURCE_3RD_DWORD);
-        // the base moved back by cap_off words as an integer (a descriptor field, not a C++ pointer),
-        // no range check (num_records = max: every offset a lane forms lies in its column of the block)
-        return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(reinterpret_cast<uintptr_t>(spill) - uintptr_t(cap_off) * 4u),
+        // the base moved back by the LDS part and the LDS base address, as integers (descriptor fields, not
+        // C++ pointers), so that entry_addr() is the byte offset; no range check (num_records = max: every
+        // offset a lane forms lies in its column of the block)
+        const uintptr_t lds0 = uintptr_t(uint32_t(reinterpret_cast<uintptr_t>((lds_word*)mem)));
+        return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(reinterpret_cast<uintptr_t>(spill) - uintptr_t(cap_off) * 4u - lds0),
                                                  0, -1, 0x00020000);
     }
 #endif
@@ -247,9 +256,10 @@ struct stack_t
     {
         if constexpr (SPILL)
         {
-            if (__builtin_expect(used < cap_off, 1)) mem[base + used] = v;
 #if defined(__HIP_DEVICE_COMPILE__)
-            else __builtin_amdgcn_raw_buffer_store_b32(v, overflow(), int((base + used) * 4u), 0, 0);
+            const uint32_t a = entry_addr();
+            if (__builtin_expect(used < cap_off, 1)) *(lds_word*)uintptr_t(a) = v;
+            else __builtin_amdgcn_raw_buffer_store_b32(v, overflow(), int(a), 0, 0);
 #endif
         }
         else
@@ -261,8 +271,11 @@ struct stack_t
         used -= stride;
 #if defined(__HIP_DEVICE_COMPILE__)
         if constexpr (SPILL)
-            if (__builtin_expect(used >= cap_off, 0))
-                return __builtin_amdgcn_raw_buffer_load_b32(overflow(), int((base + used) * 4u), 0, 0);
+        {
+            const uint32_t a = entry_addr();
+            if (__builtin_expect(used >= cap_off, 0)) return __builtin_amdgcn_raw_buffer_load_b32(overflow(), int(a), 0, 0);
+            return *(lds_word*)uintptr_t(a);
+        }
 #endif
         return mem[base + used];
     }

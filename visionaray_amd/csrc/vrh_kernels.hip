@@ -67,6 +67,7 @@ constexpr int AO_SH = AO_CUT + 2 * 8 * CUT_MAX;        // two levels x entries o
 // has seen the queues run dry.
 constexpr int AO_WAVE_WORDS = AO_SH + 8;
 constexpr uint32_t SH_TILE = 0, SH_PAR = 1, SH_NEXT = 2, SH_AVAIL = 3, SH_HELP = 4, SH_CUTN = 5, SH_DRY = 6;
+constexpr uint32_t TAG_NONFINITE = 0x80000000u;   // AO kernel lane tag: the ray is not finite
 // the root link, read from the kernel's argument segment where it is used (a scalar load) instead of
 // being held in a register across the refill loop, where the register allocator of the 6-wave AO
 // instances copied it to a VGPR and spilled that to scratch
@@ -835,6 +836,9 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
         uint32_t tileD = NONE, parD = 0, slotsD = 0;
         uint32_t inflight0 = 0, inflight1 = 0;                // AO rays in flight per buffer parity
         // lane state: PRIMARY tag = pixel lane k of tile C; AORAY tag = slot | s << 6 | parity << 11 |
+        // owner wave << 12; bit 31 (TAG_NONFINITE) = the ray has a non-finite origin or inverse
+        // direction (it takes the literal slab test) -- kept in the tag rather than in a register of its
+        // own, which the 6-wave instances spilled
         // owner wave << 12 (the wave whose tile the ray belongs to: this one unless it helps a sibling)
         uint32_t tag = 0;
         // AO ray `cand` (slot-major: slot cand / S, sample cand % S) of the tile `tile` whose hit records,
@@ -848,8 +852,8 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             r = ao_ray<COUNT>(P, recs_, slot, smp, y * P.width + x, fr, cnt);
             best_t = FMAX; best_prim = 0; steps = 0; max_t = P.radius; any = true;
             bk = 0; res_t = FMAX; res_prim = 0;
-            finite = finite_ray(r);
-            quad = P.quad_ok && finite;
+            const bool fin = finite_ray(r);
+            quad = P.quad_ok && fin;
             st.reset(); resume = NO_RESUME;
             if (!LIST && (!SPILL || VRH_AO_CUT_SPILL) && VRH_AO_CUT && quad && cutn != NONE)
             {
@@ -873,7 +877,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             else
                 st.push(quad ? 0u : P.root);
             mode = AORAY;
-            tag = slot | (smp << 6) | (par << 11) | (SHARE ? owner << 12 : 0u);
+            tag = slot | (smp << 6) | (par << 11) | (SHARE ? owner << 12 : 0u) | (fin ? 0u : TAG_NONFINITE);
             rays_total += 1;
         };
         for (;;)
@@ -974,12 +978,11 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 if (mode == IDLE && k < 64u && tile_pixel(P, tileC, k, x, y, orow, fr))
                 {
                     r = primary_ray<SAMPLED>(P, fr, x, y);
-                    finite = finite_ray(r);
                     best_t = FMAX; best_prim = 0; steps = 0; max_t = FMAX; any = false; quad = false;
                     st.reset(); st.push(LIST ? P.root : kernarg_root()); resume = NO_RESUME;
                     bk = 0; res_t = FMAX; res_prim = 0;
                     mode = PRIMARY;
-                    tag = k;
+                    tag = k | (finite_ray(r) ? 0u : TAG_NONFINITE);
                     rays_total += 1;
                     started = true;
                 }
@@ -1039,7 +1042,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 // 4-wide descent at is pair 0: 4-wide records exist only for trees whose root is a pair,
                 // stored first (render_params::quad_ok checks it), so no register holds it
                 const float mt = VRH_AO_LEAN ? (any ? P.radius : FMAX) : max_t;
-                rc = (P.fast_ok && __ballot(!finite) == 0ull)
+                rc = (P.fast_ok && __ballot((tag & TAG_NONFINITE) != 0u) == 0ull)
                     ? ray_step<KIND, COUNT, true, false, void, AO_CAPPED>(P.pairs, P.prims, P.quads, 0u, quad, r, mt, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm)
                     : ray_step<KIND, COUNT, false, false, void, AO_CAPPED>(P.pairs, P.prims, P.quads, 0u, quad, r, mt, any, st, best_t, best_prim, cnt, steps, P.step_limit, resume, P.descent_cap, P.step_flags, nullptr, static_cast<const void*>(nullptr), hm);
             }
@@ -1048,7 +1051,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
             if (COUNT) count_wave(cnt, busy);
             // 5. finished AO rays: record occlusion, retire from their tile's in-flight count
             const bool ao_done = mode == AORAY && rc != 0;
-            const uint32_t own = SHARE ? tag >> 12 : wave;    // the wave whose tile the ray belongs to
+            const uint32_t own = SHARE ? (tag >> 12) & 7u : wave;    // the wave whose tile the ray belongs to
             const bool mine = own == wave;
             uint32_t* const mk = mine ? masks : ao_base + own * AO_WAVE_WORDS + AO_MASKS;
             if (ao_done && rc > 0) atomicOr(&mk[((tag >> 11) & 1u) * 64u + (tag & 63u)], 1u << ((tag >> 6) & 31u));
@@ -1074,7 +1077,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                 if (pr_done)
                 {
                     uint32_t x, y, orow;
-                    tile_pixel(P, tileC, tag, x, y, orow);
+                    tile_pixel(P, tileC, tag & 63u, x, y, orow);
                     const size_t o = (size_t)orow * P.width + x;
                     if (P.prim_id) P.prim_id[o] = hit ? best_prim : 0xFFFFFFFFu;
                     if (P.t) P.t[o] = hit ? best_t : -1.0f;
@@ -1087,7 +1090,7 @@ __global__ __launch_bounds__(256, OCC) void render_unified_kernel(render_params 
                         rec[0] = pos.x; rec[1] = pos.y; rec[2] = pos.z;
                         rec[3] = __uint_as_float(best_prim);
                         masks[parC * 64u + slot] = 0u;
-                        slot_px[parC * 64u + slot] = (uint8_t)tag;
+                        slot_px[parC * 64u + slot] = (uint8_t)(tag & 63u);
                     }
                     else
                     {

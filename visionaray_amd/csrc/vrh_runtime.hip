@@ -1092,15 +1092,14 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     // shading epilogues: no VGPR cap (their lane state spills at 6 waves/SIMD; measured faster at 4,
     // profiles/r01/shade/shade_bench.jsonl), except whitted, whose bounce surface lives in LDS (vrh_shade.h):
     // 96 VGPRs without spills, 5 waves/SIMD, +0.7-2.1 % over 4 (profiles/r03_ab/whitted/).
-    // AO on the step loop (round 5, the lean lane state: no VGPR spill at 80 VGPRs): 6 waves/SIMD with
-    // the whole stack in LDS where the BVH is at most 20 deep (hf1M: 22 waves/CU, +3 % over 5 waves,
-    // profiles/r05/occupancy/), 5 waves/SIMD with the overflow stack for deeper BVHs (hf10M: 6 waves
-    // -4.6 % with 16 LDS entries, -10 % with the whole stack); AO tail sharing (opt-in) has 5-wave
-    // instances only.  Primary visibility: 8 waves/SIMD for triangles (64 VGPRs, no spill: hf1M
-    // +6.7-11 %, hf10M +3-9 %), 6 for spheres (8 measured -1 to -4 %, profiles/r05/occupancy/); the
-    // counting variants keep 5 / 6 (at 8 they spill hundreds of VGPRs).  BVH lists run at 5 / 6
-    const bool deep = sc->info.max_depth > 20u;
-    const int occ_ao = (ctx->opt_share == 1 || deep || lc.count) ? 5 : 6;
+    // AO on the step loop (round 5, the lean lane state: no VGPR spill or scratch at 80 VGPRs, also in
+    // the overflow-stack instances): 6 waves/SIMD, the LDS stack shrunk (below) to 16 entries so that 24
+    // waves fit a CU, the rest in the overflow block -- hf1M +4.8 %, hf10M +8.7 % over 5 waves
+    // (profiles/r05/occupancy/s6_*); AO tail sharing (opt-in) has 5-wave instances only.  Primary
+    // visibility: 8 waves/SIMD for triangles (64 VGPRs, no spill: hf1M +6.7-11 %, hf10M +3-9 %), 6 for
+    // spheres (8 measured -1 to -4 %, profiles/r05/occupancy/); the counting variants keep 5 / 6 (at 8
+    // they spill hundreds of VGPRs).  BVH lists run at 5 / 6
+    const int occ_ao = (ctx->opt_share == 1 || lc.count) ? 5 : 6;
     const int occ_primary = (lc.kind == 0 && !lc.count) ? 8 : 6;
     lc.occ = ctx->opt_occ ? ctx->opt_occ : whitted ? 5 : lc.epi ? 1 : lc.ao ? occ_ao : occ_primary;
     if (sp) lc.occ = lc.ao ? 5 : 6;                    // the sampler instances exist at the defaults
@@ -1118,10 +1117,7 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     // occupancy and its few deepest entries go to the overflow block
     // (the primary / AO step loops at their default register budgets have overflow-stack instances;
     // every other kernel keeps its whole stack in LDS, as does an explicit VRH_OPT_STACK_CAP >= depth)
-    // (6-wave AO launches keep the whole stack in LDS: measured faster than shrinking it for the
-    // register-bound 24 waves/CU, profiles/r05/occupancy/)
-    const bool keep_lds_stack = lc.ao && lc.occ == 6 && !ctx->opt_stack;
-    if (!keep_lds_stack && render_spill_available(lc) && (!ctx->opt_stack || cap < total))
+    if (render_spill_available(lc) && (!ctx->opt_stack || cap < total))
     {
         lc.spill = true;
         if (!ctx->opt_stack)
