@@ -194,12 +194,10 @@ def cpu_baseline(scene, kernel, threads=None):
             "retries": 0, "stall_s": 0.0, **info}
 
 
-def user_kernel_leg(W, H, n_rays):
-    """The same workload through a user kernel: the AO lambda of tests/cpp/user_kernels.hip (ao/main.cpp's
-    kernel with random_sampler directions, include/visionaray_hip/hip_kernels.h, compiled by hipcc) on
-    hip_sched::frames, 32 frames per launch, median over 4 launches -- the path a Visionaray program with
-    its own kernel takes.  Run after the timed region, in a child process; null when the program is absent."""
-    exe = os.path.join(ROOT, "build", "tests", "user_kernels")
+def user_program_run(prog, W, H, n_rays):
+    """median frame time of tests/cpp/user_kernels.hip's `bench` mode built as build/tests/<prog>; null
+    when the program is absent"""
+    exe = os.path.join(ROOT, "build", "tests", prog)
     if not os.access(exe, os.X_OK):
         return None
     try:
@@ -215,10 +213,25 @@ def user_kernel_leg(W, H, n_rays):
         return {"error": f"rc {r.returncode}"}
     ms = float(rec["frame_ms_median"])
     # the lambda traces the built-in kernel's rays: the same primary rays, 8 AO rays per hit
-    leg = {"mrays": round(n_rays / (ms * 1e-3) / 1e6, 1), "frame_ms_median": ms,
-           "frames_per_launch": rec["frames_per_launch"], "launches": rec["launches"],
-           "kernel": "AO device lambda (ao/main.cpp's, random_sampler) via hip_kernels.h on hip_sched::frames",
-           "program": "build/tests/user_kernels bench 708 %d %d /tmp 4 32" % (W, H)}
+    return {"mrays": round(n_rays / (ms * 1e-3) / 1e6, 1), "frame_ms_median": ms,
+            "frames_per_launch": rec["frames_per_launch"], "launches": rec["launches"],
+            "program": "build/tests/%s bench 708 %d %d /tmp 4 32" % (prog, W, H)}
+
+
+def user_kernel_leg(W, H, n_rays):
+    """The same workload through a user kernel: the AO lambda of tests/cpp/user_kernels.hip (ao/main.cpp's
+    kernel with random_sampler directions, include/visionaray_hip/hip_kernels.h, compiled by hipcc) on
+    hip_sched::frames, 32 frames per launch, median over 4 launches -- the path a Visionaray program with
+    its own kernel takes.  Run after the timed region, in a child process; null when the program is absent."""
+    leg = user_program_run("user_kernels", W, H, n_rays)
+    if leg is None or "error" in leg:
+        return leg
+    leg["kernel"] = "AO device lambda (ao/main.cpp's, random_sampler) via hip_kernels.h on hip_sched::frames"
+    # the same program built with deferred any_hit calls (hip_kernels.h VRH_USER_DEFER=1: each tile's
+    # kernel runs record / trace / replay, the any_hit rays traced as one pool): the same frames
+    leg["deferred"] = user_program_run("uk_defer", W, H, n_rays)
+    rec = {"frames_per_launch": leg["frames_per_launch"]}
+    ms = leg["frame_ms_median"]
     # roofline of the user kernel, as the built-in's: the vector-L1 requests of the committed PMC pass of
     # this program (profiles/pmc_user_lambda.json, kernel-source hash checked) x 16 B over the live launch
     # time (median wall time of a 32-frame frames() launch: the kernel plus its launch, an upper bound)
@@ -646,6 +659,7 @@ def main():
             "cpu_baseline": cpu,
             "user_kernel": user_leg,
             "user_kernel_mrays": user_leg.get("mrays") if user_leg else None,
+            "user_kernel_deferred_mrays": (user_leg.get("deferred") or {}).get("mrays") if user_leg else None,
             "host_build_s": round(build_s, 3),
             "verify": verify,
         }

@@ -176,6 +176,15 @@ public:
         return s;
     }
 
+    // device memory that hipcc-compiled launches keep with the context (hip_kernels.h: the logs of
+    // VRH_USER_DEFER), allocated and grown there; freed with the context
+    struct scratch_block
+    {
+        std::shared_ptr<void> mem;
+        size_t bytes = 0;
+    };
+    scratch_block& scratch() { return *scratch_; }
+
     static std::shared_ptr<hip_context> const& default_context()
     {
         static std::shared_ptr<hip_context> d = std::make_shared<hip_context>(0);
@@ -185,6 +194,7 @@ public:
 private:
     std::shared_ptr<vrh_ctx> ctx_;
     bool async_frames_ = false;
+    std::shared_ptr<scratch_block> scratch_ = std::make_shared<scratch_block>();
 };
 
 //-------------------------------------------------------------------------------------------------

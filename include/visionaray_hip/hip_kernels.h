@@ -942,6 +942,231 @@ __device__ inline void walk_shared(vrh_scene_view const& b, vrh::dev::ray_t cons
     }
 }
 
+// ---- deferred any_hit calls (VRH_USER_DEFER=1) --------------------------------------------------
+// A user kernel runs one pixel per lane and its any_hit calls one after another, so the wave waits
+// for its slowest lane once per call (the AO lambda: eight times per tile, VALU lane utilisation 0.37
+// against the built-in kernel's 0.51).  With the option, user_render runs every tile in
+// three phases:
+//   record  the kernel runs for the tile's pixels; each any_hit call with the default intersector on
+//           a single BVH is logged (ray, max_t) into the wave's log and answered "no hit" for now;
+//           closest_hit calls run as usual and are logged with the leaf index of their result; nothing
+//           is stored into the render target;
+//   trace   the wave traces the tile's logged any_hit rays as one pool: a lane whose ray is done takes
+//           the next ray of the pool (vrh_device.h ray_step, the binary records in the reference's
+//           order -- near child first, ties to child 1, far child pushed, leaf primitives in index
+//           order -- so every ray ends on the reference's first-found hit);
+//   replay  the kernel runs again from the start with the same sampler seeds; a call that is the
+//           logged one bit for bit (the same kind, BVH, origin, direction and max_t) gets the logged
+//           answer -- its hit record rebuilt by testing the one recorded leaf primitive with the
+//           call's own intersector and update rule -- and any other call runs directly.  The colours
+//           are stored.
+// The kernel's results are those of running it once: a replayed call returns what the direct call
+// would return (the same ray, the same leaf, the same test), and a kernel whose later calls depend on
+// earlier answers simply finds them unlogged and runs them directly.  The kernel must be a pure
+// function of its ray, sampler and position -- it runs twice per pixel -- which every reference
+// kernel is; hence opt-in.  Calls with a custom intersector or update rule, multi_hit, other BVHs
+// than the tile's first and calls past VRH_USER_DEFER_SLOTS per pixel run directly.
+#ifndef VRH_USER_DEFER
+#define VRH_USER_DEFER 0
+#endif
+#ifndef VRH_USER_DEFER_SLOTS
+#define VRH_USER_DEFER_SLOTS 16
+#endif
+// the trace phase's tuning (AO lambda, C3, 32 frames per launch, rates, profiles/r05/defer/): a lane takes
+// a new ray once 32 lanes are idle (1: -0.5 %, 48: -2 %, 64: -22 %); pairs wave-uniform over the active
+// lanes through the scalar cache, no pop on miss (ray_step flags 2; 3: -4 %, 1: -7 %, 0: -2 %); no descent
+// cap (4 / 8 visits: -21 % / -14 %); the pool in call order (pixel order: -16 %); binary records only
+// (hit / miss over the 4-wide records first, then a binary re-walk of the hits: -41 %)
+constexpr uint32_t DEFER_REFILL = 32u;
+constexpr uint32_t DEFER_STEP_FLAGS = 2u;
+static_assert(!(VRH_USER_DEFER && VRH_USER_ANYHIT_SHARE), "VRH_USER_DEFER and VRH_USER_ANYHIT_SHARE are alternatives");
+constexpr uint32_t DEFER_OFF = 0u, DEFER_RECORD = 1u, DEFER_REPLAY = 2u;
+// the last word of a log entry: DTAG_ANY for an any_hit call, DTAG_PENDING until the trace phase has
+// answered it, the low bits the leaf index of the hit primitive or DTAG_NONE
+constexpr uint32_t DTAG_ANY = 0x80000000u, DTAG_PENDING = 0x40000000u, DTAG_NONE = 0x3FFFFFFFu;
+// a wave's log: VRH_USER_DEFER_SLOTS x 64 entries of 32 B ([slot][lane]: ori, dir, max_t, tag), then
+// the pool (entry indices of the pending any_hit calls, in call order)
+constexpr uint32_t DEFER_ENTRIES = VRH_USER_DEFER_SLOTS * 64u;
+constexpr size_t DEFER_WAVE_BYTES = size_t(DEFER_ENTRIES) * (32u + 4u);
+// LDS words after the stacks (and the entry-cut area): [0] phase, [1] pool size, [2] BVH set,
+// [4, 6) log base, [6, 24) the tile's BVH (vrh_scene_view), [24, 88) calls per lane so far
+constexpr uint32_t DEFER_WORDS = 88u;
+static_assert(sizeof(vrh_scene_view) <= 18u * 4u, "the LDS copy of the tile's BVH holds 18 words");
+enum defer_state : uint32_t { DEFER_RUN = 0u, DEFER_RUN_LOG = 1u, DEFER_PENDING = 2u, DEFER_LOGGED = 3u };
+#ifndef VRH_DEFER_PROF
+#define VRH_DEFER_PROF 0
+#endif
+// VRH_DEFER_PROF (diagnostic build): per block, lane 0 sums [0] record [1] trace [2] replay clock
+// cycles, [3] tiles, [4] pooled rays, [5] trace-loop iterations, [6] busy lanes summed over those
+// iterations, and writes them with DEFER_PROF_MAGIC in [7] to the first 64 B of its log at the end
+constexpr unsigned long long DEFER_PROF_MAGIC = 0x5652484445464552ull;
+
+__device__ inline uint32_t* defer_area()
+{
+    extern __shared__ uint32_t vrh_user_smem[];
+    return vrh_user_smem + VRH_USER_STACK * 64u + (VRH_USER_ANYHIT_CUT ? UCUT_WORDS : 0u);
+}
+
+__device__ inline float4* defer_log(const uint32_t* a)
+{
+    return reinterpret_cast<float4*>(uintptr_t(a[4]) | (uintptr_t(a[5]) << 32));
+}
+
+struct defer_call
+{
+    uint32_t state;     // defer_state
+    uint32_t entry;     // the call's log entry (slot * 64 + lane)
+    uint32_t li;        // DEFER_LOGGED: leaf index of the answer's primitive, or DTAG_NONE
+};
+
+__device__ inline bool same_bits(float a, float b) { return __float_as_uint(a) == __float_as_uint(b); }
+
+// what to do with a call of the current phase (any: any_hit, else closest_hit) on BVH v
+__device__ inline defer_call defer_begin(vrh_scene_view const& v, basic_ray<float> const& ray, float max_t, bool any)
+{
+    defer_call d{ DEFER_RUN, 0u, DTAG_NONE };
+    uint32_t* a = defer_area();
+    const uint32_t phase = a[0];
+    if (phase == DEFER_OFF || v.max_depth >= VRH_USER_STACK || v.num_prims >= DTAG_NONE) return d;
+    const uint32_t lane = __lane_id();
+    if (phase == DEFER_RECORD && a[2] == 0u)
+    {
+        // the tile's BVH: the first one a call names (the lowest calling lane's)
+        if (lane == (uint32_t)__builtin_ctzll(__ballot(true)))
+        {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
+            for (uint32_t k = 0; k < uint32_t(sizeof(vrh_scene_view) / 4u); ++k) a[6u + k] = w[k];
+            a[2] = 1u;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (a[2] == 0u || reinterpret_cast<const vrh_scene_view*>(a + 6)->pairs != v.pairs) return d;
+    const uint32_t c = a[24u + lane];
+    if (c >= VRH_USER_DEFER_SLOTS) return d;
+    a[24u + lane] = c + 1u;
+    d.entry = c * 64u + lane;
+    float4* ent = defer_log(a) + 2u * d.entry;
+    if (phase == DEFER_RECORD)
+    {
+        if (!any) { d.state = DEFER_RUN_LOG; return d; }
+        ent[0] = make_float4(ray.ori.x, ray.ori.y, ray.ori.z, ray.dir.x);
+        ent[1] = make_float4(ray.dir.y, ray.dir.z, max_t, __uint_as_float(DTAG_ANY | DTAG_PENDING));
+        // the pool, in call order: the lanes deferring here take consecutive places
+        const uint64_t m = __ballot(true);
+        const uint32_t n = a[1];
+        uint32_t* pool = reinterpret_cast<uint32_t*>(defer_log(a) + 2u * DEFER_ENTRIES);
+        pool[n + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u))] = d.entry;
+        __builtin_amdgcn_wave_barrier();
+        if (lane == (uint32_t)__builtin_ctzll(m)) a[1] = n + uint32_t(__popcll(m));
+        __builtin_amdgcn_wave_barrier();
+        d.state = DEFER_PENDING;
+        return d;
+    }
+    // replay: the logged call must be this one, bit for bit (reading only the tag while every answer so
+    // far equals the record phase's -- the kernel then makes the same calls -- measured 0.8-1.3 % slower)
+    const float4 e0 = ent[0], e1 = ent[1];
+    const uint32_t tag = __float_as_uint(e1.w);
+    if (same_bits(e0.x, ray.ori.x) && same_bits(e0.y, ray.ori.y) && same_bits(e0.z, ray.ori.z) && same_bits(e0.w, ray.dir.x)
+        && same_bits(e1.x, ray.dir.y) && same_bits(e1.y, ray.dir.z) && same_bits(e1.z, max_t)
+        && (tag & (DTAG_ANY | DTAG_PENDING)) == (any ? DTAG_ANY : 0u))
+    {
+        d.state = DEFER_LOGGED;
+        d.li = tag & DTAG_NONE;
+    }
+    return d;
+}
+
+// record phase: a closest_hit call ran directly and ended on leaf primitive li (DTAG_NONE: no hit)
+__device__ inline void defer_log_closest(defer_call const& d, basic_ray<float> const& ray, float max_t, uint32_t li)
+{
+    float4* ent = defer_log(defer_area()) + 2u * d.entry;
+    ent[0] = make_float4(ray.ori.x, ray.ori.y, ray.ori.z, ray.dir.x);
+    ent[1] = make_float4(ray.dir.y, ray.dir.z, max_t, __uint_as_float(li));
+}
+
+// trace phase: the pool's rays, a lane taking the next one as soon as its ray is done
+template <int KIND>
+__device__ inline void defer_trace_kind(uint32_t* a, unsigned long long* prof)
+{
+    using namespace vrh::dev;
+    const uint32_t n = a[1];
+    const vrh_scene_view& v = *reinterpret_cast<const vrh_scene_view*>(a + 6);
+    const float4* pairs = static_cast<const float4*>(v.pairs);
+    const float4* prims = static_cast<const float4*>(v.prims);
+    const uint32_t root = v.root;
+    const bool finite_scene = v.finite_bounds != 0u;
+    float4* ent = defer_log(a);
+    const uint32_t* pool = reinterpret_cast<const uint32_t*>(ent + 2u * DEFER_ENTRIES);
+    lds_stack st = user_stack();
+    constexpr uint32_t IDLE = 0xFFFFFFFFu;
+    uint32_t cur = IDLE, next = 0u;
+    ray_t r{};
+    float max_t = 0.0f, best_t = FMAX;
+    uint32_t pid = 0u, resume = NO_RESUME;  // (no descent cap: resume stays unset)
+    bool fin = true, quad = false;          // (binary records only: quad stays false)
+    hit_extra hx{ 0.0f, 0.0f, 0u };
+    test_counts cnt{};
+#if VRH_DEFER_PROF
+    uint32_t prof_it = 0u, prof_busy = 0u;
+#endif
+    for (;;)
+    {
+        const uint64_t idle = __ballot(cur == IDLE);
+        if (idle != 0ull && next < n && (uint32_t(__popcll(idle)) >= DEFER_REFILL || idle == ~0ull))
+        {
+            const uint32_t k = next + __builtin_amdgcn_mbcnt_hi(uint32_t(idle >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(idle), 0u));
+            if (cur == IDLE && k < n)
+            {
+                cur = pool[k];
+                const float4 e0 = ent[2u * cur], e1 = ent[2u * cur + 1u];
+                r = make_ray(mk3(e0.x, e0.y, e0.z), mk3(e0.w, e1.x, e1.y));
+                max_t = e1.z;
+                best_t = FMAX;
+                fin = finite_ray(r);
+                st.reset();
+                st.push(root);
+            }
+            next += uint32_t(__popcll(idle));
+        }
+        const bool busy = cur != IDLE;
+        const uint64_t active = __ballot(busy);
+        if (active == 0ull) break;
+#if VRH_DEFER_PROF
+        prof_it += 1u;
+        prof_busy += uint32_t(__popcll(active));
+#endif
+        const bool fast = finite_scene && __ballot(busy && !fin) == 0ull;
+        if (busy)
+        {
+            uint32_t steps = 0u;
+            const int res = fast ? ray_step<KIND, false, true, true, void, false>(pairs, prims, nullptr, root, quad, r, max_t, true, st,
+                                                                               best_t, pid, cnt, steps, 0xFFFFFFFFu, resume,
+                                                                               0xFFFFFFFFu, DEFER_STEP_FLAGS, &hx)
+                                 : ray_step<KIND, false, false, true, void, false>(pairs, prims, nullptr, root, quad, r, max_t, true, st,
+                                                                                best_t, pid, cnt, steps, 0xFFFFFFFFu, resume,
+                                                                                0xFFFFFFFFu, DEFER_STEP_FLAGS, &hx);
+            if (res != 0)
+            {
+                reinterpret_cast<uint32_t*>(ent + 2u * cur + 1u)[3] = DTAG_ANY | (res == 1 ? hx.li : DTAG_NONE);
+                cur = IDLE;
+            }
+        }
+    }
+#if VRH_DEFER_PROF
+    prof[4] += n;
+    prof[5] += prof_it;
+    prof[6] += prof_busy;
+#endif
+}
+
+__device__ inline void defer_trace(unsigned long long* prof)
+{
+    uint32_t* a = defer_area();
+    if (a[1] == 0u) return;
+    if (reinterpret_cast<const vrh_scene_view*>(a + 6)->prim_kind == VRH_PRIM_TRI64) defer_trace_kind<vrh::dev::KIND_TRI>(a, prof);
+    else defer_trace_kind<vrh::dev::KIND_SPHERE>(a, prof);
+}
+
 template <typename It>
 using range_value_t = typename std::decay<decltype(*std::declval<It>())>::type;
 template <typename It>
@@ -1029,6 +1254,31 @@ VRH_FUNC inline auto intersect(
             hip_detail::walk_shared<false>(b.view, r, max_t, result, leaf2);
         return result;
     }
+    // deferred calls (VRH_USER_DEFER: user_render's record / trace / replay phases): the default
+    // intersector and update rule on one primitive type, one hit record
+    constexpr bool deferrable = VRH_USER_DEFER && MultiHitMax == 1 && Traversal != detail::MultiHit
+                                && std::is_same<Intersector, default_intersector>::value && std::is_same<Cond, is_closer_t>::value;
+    hip_detail::defer_call d{ hip_detail::DEFER_RUN, 0u, hip_detail::DTAG_NONE };
+    if constexpr (deferrable)
+    {
+        d = hip_detail::defer_begin(b.view, ray, max_t, Traversal == detail::AnyHit);
+        if (d.state == hip_detail::DEFER_PENDING) return result;     // record phase: answered in the replay
+        if (d.state == hip_detail::DEFER_LOGGED)
+        {
+            if (d.li == hip_detail::DTAG_NONE) return result;
+            // the logged answer: the one primitive it names, through the walk's own leaf step
+            uint32_t flags = 0;
+            const P prim = hip_detail::leaf_primitive<P>(prims, d.li, flags);
+            auto hr = HR(isect(ray, prim), int(d.li));
+            auto closer = update_cond(hr, result, max_t);
+            if (any(closer))
+            {
+                update_if(result, hr, closer);
+                return result;
+            }
+        }
+    }
+    uint32_t won = hip_detail::DTAG_NONE;      // the leaf index of the primitive the result holds
     hip_detail::walk<Traversal == detail::AnyHit>(b.view, ray, max_t, [&]() { return hip_detail::cull_of(result); },
                      [&](uint32_t i, uint32_t& flags) -> bool
                      {
@@ -1037,9 +1287,12 @@ VRH_FUNC inline auto intersect(
                          auto closer = update_cond(hr, result, max_t);
                          if (!any(closer)) return false;
                          update_if(result, hr, closer);
+                         won = i;
                          detail::exit_traversal<Traversal> early_exit;
                          return early_exit.check(result);
                      });
+    if constexpr (deferrable)
+        if (d.state == hip_detail::DEFER_RUN_LOG) hip_detail::defer_log_closest(d, ray, max_t, won);
     return result;
 }
 
@@ -1072,7 +1325,7 @@ using prim_record = hit_record<basic_ray<float>, primitive<unsigned>>;
 using bvh_record = hit_record_bvh<prim_record>;
 
 template <bool Any, typename Isect>
-__device__ inline bvh_record traverse_bvh(basic_ray<float> const& ray, vrh_scene_view const& b, Isect& isect, float max_t)
+__device__ inline bvh_record traverse_bvh_direct(basic_ray<float> const& ray, vrh_scene_view const& b, Isect& isect, float max_t)
 {
     using HR = prim_record;
     bvh_record result;
@@ -1110,6 +1363,32 @@ __device__ inline bvh_record traverse_bvh(basic_ray<float> const& ray, vrh_scene
              return false;
          });
     return result;
+}
+
+template <bool Any, typename Isect>
+__device__ inline bvh_record traverse_bvh(basic_ray<float> const& ray, vrh_scene_view const& b, Isect& isect, float max_t)
+{
+    if constexpr (VRH_USER_DEFER && std::is_same<Isect, default_intersector>::value)
+    {
+        // deferred calls (user_render's record / trace / replay phases, above)
+        const defer_call d = defer_begin(b, ray, max_t, Any);
+        if (d.state == DEFER_PENDING) return bvh_record();        // record phase: answered in the replay
+        if (d.state == DEFER_LOGGED)
+        {
+            if (d.li == DTAG_NONE) return bvh_record();
+            // the logged answer: the one primitive it names, tested and merged as the walk's leaf does
+            const float4* prims = static_cast<const float4*>(b.prims);
+            uint32_t flags = 0;
+            prim_record hr;
+            if (b.prim_kind == VRH_PRIM_TRI64) hr = isect(ray, leaf_primitive<basic_triangle<3, float>>(prims, d.li, flags));
+            else hr = isect(ray, leaf_primitive<basic_sphere<float>>(prims, d.li, flags));
+            if (is_closer(hr, prim_record(), max_t)) return bvh_record(hr, d.li);
+        }
+        bvh_record res = traverse_bvh_direct<Any>(ray, b, isect, max_t);
+        if (d.state == DEFER_RUN_LOG) defer_log_closest(d, ray, max_t, res.hit ? res.primitive_list_index : DTAG_NONE);
+        return res;
+    }
+    return traverse_bvh_direct<Any>(ray, b, isect, max_t);
 }
 } // hip_detail
 
@@ -1277,6 +1556,7 @@ struct user_frames
     uint32_t* queues;             // vrh_ctx_user_queues: 8 heads, VRH_USER_QUEUE_STRIDE words apart
     uint32_t matrix_cam;          // sched_params with camera matrices: their inverses (column-major)
     float inv_view[16], inv_proj[16];
+    char* defer_log;              // VRH_USER_DEFER: DEFER_WAVE_BYTES per block of the grid
 };
 
 // the primary ray through image position (fx, fy) (the pixel plus the sampler's offset) of camera c:
@@ -1350,8 +1630,9 @@ struct call_with_intersector
 template <typename T, typename = void> struct has_depth : std::false_type {};
 template <typename T> struct has_depth<T, decltype((void)std::declval<T>().depth)> : std::true_type {};
 
-// pixel (x, y) of frame c of the launch
-template <typename K, uint32_t SK, uint32_t SN, uint32_t NC>
+// pixel (x, y) of frame c of the launch; STORE = false (the record phase of VRH_USER_DEFER) runs the
+// kernel without storing its results
+template <typename K, uint32_t SK, uint32_t SN, uint32_t NC, bool STORE = true>
 __device__ inline void user_pixel(K& kernel, user_frames<NC> const& f, uint32_t c, uint32_t x, uint32_t y)
 {
     const uint32_t frame_num = f.frame_num + c;
@@ -1361,9 +1642,9 @@ __device__ inline void user_pixel(K& kernel, user_frames<NC> const& f, uint32_t 
     {
         // sched_common.h:130-176 make_primary_ray_impl (uniform pixel sampler), as the built-in kernels
         auto res = invoke_kernel(kernel, user_primary_ray(f, c, (float)x, (float)y), samp, x, y, 0);
-        if (f.color) f.color[o] = make_float4(res.color.x, res.color.y, res.color.z, res.color.w);
+        if (STORE && f.color) f.color[o] = make_float4(res.color.x, res.color.y, res.color.z, res.color.w);
         if constexpr (has_depth<decltype(res)>::value)
-            if (f.t) f.t[o] = res.depth;
+            if (STORE && f.t) f.t[o] = res.depth;
     }
     else
     {
@@ -1387,9 +1668,9 @@ __device__ inline void user_pixel(K& kernel, user_frames<NC> const& f, uint32_t 
                 d = make_float4(res.color.x * a + d.x * 1.0f, res.color.y * a + d.y * 1.0f,
                                 res.color.z * a + d.z * 1.0f, res.color.w * a + d.w * 1.0f);
                 if constexpr (has_depth<decltype(res)>::value)
-                    if (f.t) f.t[o] = res.depth;
+                    if (STORE && f.t) f.t[o] = res.depth;
             }
-            if (f.color) f.color[o] = d;
+            if (STORE && f.color) f.color[o] = d;
         }
         else
         {
@@ -1406,9 +1687,9 @@ __device__ inline void user_pixel(K& kernel, user_frames<NC> const& f, uint32_t 
                     cl = make_float4(cl.x * a + d.x * b, cl.y * a + d.y * b, cl.z * a + d.z * b, cl.w * a + d.w * b);
                 }
             }
-            if (f.color) f.color[o] = cl;
+            if (STORE && f.color) f.color[o] = cl;
             if constexpr (has_depth<decltype(res)>::value)
-                if (f.t) f.t[o] = res.depth;
+                if (STORE && f.t) f.t[o] = res.depth;
         }
     }
 }
@@ -1445,6 +1726,9 @@ __global__ __launch_bounds__(64) VRH_USER_OCC void user_render(K kernel, user_fr
 {
     const uint32_t lane = threadIdx.y * 8u + threadIdx.x;
     if (VRH_USER_ANYHIT_CUT && lane == 0u) user_cut_area()[2] = 0u;     // no any_hit entry cut yet
+    if (VRH_USER_DEFER && lane == 0u) defer_area()[0] = DEFER_OFF;
+    unsigned long long prof[8] = {};         // VRH_DEFER_PROF
+    (void)prof;
     uint32_t q = xcc_id();
     for (uint32_t tried = 0; tried < 8u; ++tried, q = (q + 1u) & 7u)
     {
@@ -1477,9 +1761,86 @@ __global__ __launch_bounds__(64) VRH_USER_OCC void user_render(K kernel, user_fr
             const uint32_t ty = tile / f.tiles_x;
             const uint32_t x = f.x0 + (tile - ty * f.tiles_x) * 8u + threadIdx.x;
             const uint32_t y = f.y0 + ty * 8u + threadIdx.y;
-            if (x < f.x1 && y < f.y1) user_pixel<K, SK, SN, NC>(kernel, f, c, x, y);
+            const bool in = x < f.x1 && y < f.y1;
+            if constexpr (VRH_USER_DEFER)
+            {
+                // record, trace, replay (the deferred any_hit calls, above); one wave per block, so the
+                // barriers only order the phases' LDS and global accesses
+                uint32_t* da = defer_area();
+                da[24u + lane] = 0u;
+                if (lane == 0u)
+                {
+                    const uintptr_t log = uintptr_t(f.defer_log + size_t(blockIdx.x) * DEFER_WAVE_BYTES);
+                    da[0] = DEFER_RECORD; da[1] = 0u; da[2] = 0u;
+                    da[4] = uint32_t(log); da[5] = uint32_t(uint64_t(log) >> 32);
+                }
+                __syncthreads();
+#if VRH_DEFER_PROF
+                const uint64_t p0 = clock64();
+#endif
+                if (in) user_pixel<K, SK, SN, NC, false>(kernel, f, c, x, y);
+                __threadfence_block();
+                __syncthreads();
+#if VRH_DEFER_PROF
+                const uint64_t p1 = clock64();
+#endif
+                if (da[2] != 0u) defer_trace(prof);
+                __threadfence_block();
+                __syncthreads();
+#if VRH_DEFER_PROF
+                const uint64_t p2 = clock64();
+#endif
+                da[24u + lane] = 0u;
+                if (lane == 0u) da[0] = DEFER_REPLAY;
+                __syncthreads();
+                if (in) user_pixel<K, SK, SN, NC>(kernel, f, c, x, y);
+                __syncthreads();
+#if VRH_DEFER_PROF
+                const uint64_t p3 = clock64();
+                prof[0] += p1 - p0;
+                prof[1] += p2 - p1;
+                prof[2] += p3 - p2;
+                prof[3] += 1u;
+#endif
+            }
+            else if (in) user_pixel<K, SK, SN, NC>(kernel, f, c, x, y);
         }
     }
+#if VRH_DEFER_PROF
+    if (VRH_USER_DEFER && lane == 0u)
+    {
+        prof[7] = DEFER_PROF_MAGIC;
+        unsigned long long* o = reinterpret_cast<unsigned long long*>(f.defer_log + size_t(blockIdx.x) * DEFER_WAVE_BYTES);
+        for (int k = 0; k < 8; ++k) o[k] = prof[k];
+    }
+#endif
+}
+
+// at least `bytes` of device memory kept with the context (grown after a device sync: earlier
+// launches on the context's stream may still use the old block)
+inline char* context_scratch(hip_context& ctx, size_t bytes)
+{
+    auto& sb = ctx.scratch();
+    if (bytes > sb.bytes)
+    {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+            throw hip_error("hip_sched: device scratch: device sync", VRH_ERR_HIP);
+        sb.mem.reset();
+        sb.bytes = 0;
+        void* p = nullptr;
+        if (hipMalloc(&p, bytes) != hipSuccess) throw hip_error("hip_sched: device scratch: hipMalloc", VRH_ERR_OOM);
+        sb.mem.reset(p, [dev](void* q) {
+            int d0 = 0;
+            if (hipGetDevice(&d0) == hipSuccess && hipSetDevice(dev) == hipSuccess)
+            {
+                (void)hipFree(q);
+                (void)hipSetDevice(d0);
+            }
+        });
+        sb.bytes = bytes;
+    }
+    return static_cast<char*>(sb.mem.get());
 }
 
 // launch `kern` over f on the context's stream: the queues zeroed first, then a grid of as many
@@ -1487,7 +1848,8 @@ __global__ __launch_bounds__(64) VRH_USER_OCC void user_render(K kernel, user_fr
 template <typename K, uint32_t SK, uint32_t SN, uint32_t NC>
 inline hipError_t launch_user_render(hip_context& ctx, K const& kernel, user_frames<NC>& f, hipStream_t stream)
 {
-    const size_t lds = (size_t(64) * VRH_USER_STACK + (VRH_USER_ANYHIT_CUT ? UCUT_WORDS : 0u)) * sizeof(uint32_t);
+    const size_t lds = (size_t(64) * VRH_USER_STACK + (VRH_USER_ANYHIT_CUT ? UCUT_WORDS : 0u) + (VRH_USER_DEFER ? DEFER_WORDS : 0u))
+                       * sizeof(uint32_t);
     auto fn = user_render<K, SK, SN, NC>;
     check(vrh_ctx_user_queues(ctx.get(), &f.queues), "vrh_ctx_user_queues");
     int dev = 0, cus = 0, per_cu = 0;
@@ -1498,6 +1860,7 @@ inline hipError_t launch_user_render(hip_context& ctx, K const& kernel, user_fra
     const uint64_t work = uint64_t(f.tiles) * f.nframes;
     const uint64_t resident = uint64_t(cus > 0 ? cus : 1) * uint64_t(per_cu > 0 ? per_cu : 1);
     const uint32_t grid = uint32_t(work < resident ? work : resident);
+    if (VRH_USER_DEFER) f.defer_log = context_scratch(ctx, size_t(grid) * DEFER_WAVE_BYTES);
     if ((e = hipMemsetAsync(f.queues, 0, 8u * VRH_USER_QUEUE_STRIDE * sizeof(uint32_t), stream)) != hipSuccess) return e;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(8, 8), lds, stream, kernel, f);
     return hipGetLastError();

@@ -431,6 +431,24 @@ int main(int argc, char** argv)
             std::sort(ms.begin(), ms.end());
             printf("{\"mode\":\"bench\",\"frame_ms_median\":%.4f,\"launches\":%d,\"frames_per_launch\":%d,"
                    "\"kernel\":\"%s\"}\n", ms[ms.size() / 2], launches, F, F == 1 ? "ao lambda" : "random_sampler ao lambda");
+#if VRH_DEFER_PROF
+            {
+                // the blocks' phase counters at the head of their logs (hip_kernels.h VRH_DEFER_PROF)
+                auto& sb = hip_context::default_context()->scratch();
+                std::vector<unsigned long long> h(sb.bytes / 8);
+                (void)hipDeviceSynchronize();
+                (void)hipMemcpy(h.data(), sb.mem.get(), sb.bytes, hipMemcpyDeviceToHost);
+                unsigned long long pr[7] = {};
+                unsigned blocks = 0;
+                const size_t stride = hip_detail::DEFER_WAVE_BYTES / 8;
+                for (size_t b = 0; b + 8 <= h.size(); b += stride)
+                    if (h[b + 7] == hip_detail::DEFER_PROF_MAGIC) { ++blocks; for (int k = 0; k < 7; ++k) pr[k] += h[b + k]; }
+                printf("{\"defer_prof\":{\"blocks\":%u,\"record\":%llu,\"trace\":%llu,\"replay\":%llu,\"tiles\":%llu,"
+                       "\"pool_rays\":%llu,\"trace_iterations\":%llu,\"busy_lanes\":%llu}}\n",
+                       blocks, pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6]);
+            }
+#endif
+            fflush(stdout);
         }
         else if (mode == "frames")
         {

@@ -33,6 +33,13 @@ BG = np.array([0.1, 0.2, 0.3, 1.0], np.float32)
 needs_bin = pytest.mark.skipif(not os.path.exists(BIN), reason="oracle/_ref/ref_kernels is built in the build container")
 
 
+def _use(monkeypatch, variant):
+    """run the tests' program as the build `variant` (oracle/Makefile: ref_kernels_<variant>)"""
+    b = BIN + "_" + variant
+    assert os.path.exists(b), f"oracle/Makefile builds {os.path.basename(b)} next to ref_kernels"
+    monkeypatch.setattr(sys.modules[__name__], "BIN", b)
+
+
 def _run(tmp_path, mode, scene, W, H, *extra):
     out = tmp_path / mode
     out.mkdir()
@@ -58,14 +65,14 @@ def test_random_sampler_draws_bit_exact(tmp_path, golden, oracle_mod, case):
 @pytest.mark.gpu
 @needs_bin
 @pytest.mark.parametrize("case", ["rs_hf64_160x90_f0", "rs_hf200_320x180_f3", "rs_hf1M_f1"])
-@pytest.mark.parametrize("share", [False, True])
-def test_reference_ao_kernel_on_hip_sched(tmp_path, golden, oracle_mod, case, share, monkeypatch):
+@pytest.mark.parametrize("variant", ["direct", "share", "defer"])
+def test_reference_ao_kernel_on_hip_sched(tmp_path, golden, oracle_mod, case, variant, monkeypatch):
     """ao/main.cpp's kernel, compiled from the reference's headers by hipcc: hits, t and every pixel's
-    AO count bit-exact.  share: the build with
-    the shared any-hit walk (VRH_USER_ANYHIT_SHARE=1, oracle/_ref/ref_kernels_share)."""
-    if share:
-        assert os.path.exists(BIN + "_share"), "oracle/Makefile builds ref_kernels_share next to ref_kernels"
-        monkeypatch.setattr(sys.modules[__name__], "BIN", BIN + "_share")
+    AO count bit-exact.  share: the build with the shared any-hit walk (VRH_USER_ANYHIT_SHARE=1,
+    oracle/_ref/ref_kernels_share); defer: deferred any_hit calls (VRH_USER_DEFER=1, record / trace /
+    replay, oracle/_ref/ref_kernels_defer)."""
+    if variant != "direct":
+        _use(monkeypatch, variant)
     g = golden[case]
     ref = np.load(os.path.join(GOLDEN, case + ".npz"))
     out = _run(tmp_path, "ao", g["scene"], g["W"], g["H"], g["frame"])
@@ -89,10 +96,12 @@ GRID = {"hf64": 64, "hf200": 200, "hf1M": 708}
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["rs_hf64_160x90_f0", "rs_hf1M_f1"])
-def test_standalone_random_sampler_and_ao_kernel(tmp_path, golden, oracle_mod, case):
+@pytest.mark.parametrize("prog", ["user_kernels", "uk_defer"])
+def test_standalone_random_sampler_and_ao_kernel(tmp_path, golden, oracle_mod, case, prog):
     """Without the reference headers (hip_kernels.h + standalone.h): the restated random_sampler<float>
     draws bit-exact, the AO example's kernel with the restated cosine_sample_hemisphere on the same bar
-    as the reference-header build (every AO count exact)."""
+    as the reference-header build (every AO count exact); uk_defer: deferred any_hit calls."""
+    UK_BIN = os.path.join(ROOT, "build", "tests", prog)
     g = golden[case]
     ref = np.load(os.path.join(GOLDEN, case + ".npz"))
     d = tmp_path / "d"
@@ -117,10 +126,13 @@ def test_standalone_random_sampler_and_ao_kernel(tmp_path, golden, oracle_mod, c
                                        ("shade_cornell12_face", "shade"), ("shade_cornell12_vertex", "shade"),
                                        ("whitted_hf64_vertex", "whitted"), ("whitted_cornell12_face", "whitted"),
                                        ("whitted_hfstack32x24_face", "whitted")])
-def test_reference_shading_kernels_on_hip_sched(tmp_path, golden, case, mode):
+@pytest.mark.parametrize("variant", ["direct", "defer"])
+def test_reference_shading_kernels_on_hip_sched(tmp_path, golden, case, mode, variant, monkeypatch):
     """simple::kernel / whitted::kernel (the reference's own code, kernels.h make_kernel_params over
     device refs, materials and lights) against the reference's frames: misses bit-exact, radiance
-    within 1e-5 relative."""
+    within 1e-5 relative.  defer: the shadow rays deferred and the bounces replayed (VRH_USER_DEFER=1)."""
+    if variant != "direct":
+        _use(monkeypatch, variant)
     g = golden[case]
     extra = [g["binding"]] + ([g["bounces"], g["eps"]] if mode == "whitted" else [])
     got = _run(tmp_path, mode, g["scene"], g["W"], g["H"], *extra)["color"]
@@ -133,9 +145,13 @@ def test_reference_shading_kernels_on_hip_sched(tmp_path, golden, case, mode):
 @pytest.mark.gpu
 @needs_bin
 @pytest.mark.parametrize("case", ["multi_hfstack32x24_face", "multi_hfstack32x24_vertex", "multi_cornell12_face"])
-def test_reference_multi_hit_on_hip_sched(tmp_path, golden, case):
+@pytest.mark.parametrize("variant", ["direct", "defer"])
+def test_reference_multi_hit_on_hip_sched(tmp_path, golden, case, variant, monkeypatch):
     """multi_hit<16>(ray, refs) through the reference's traverse / insert_sorted on the device BVH: hit
-    lists bit-exact; the multi_hit example's compositing within 1e-5."""
+    lists bit-exact; the multi_hit example's compositing within 1e-5 (defer: multi_hit is never
+    deferred, the build must still give the same lists)."""
+    if variant != "direct":
+        _use(monkeypatch, variant)
     g = golden[case]
     out = _run(tmp_path, "multi", g["scene"], g["W"], g["H"], g["binding"])
     ref = np.load(os.path.join(GOLDEN, case + ".npz"))

@@ -26,6 +26,21 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 GRID = {"hf64": 64, "hf200": 200}
 
 
+DEFER_BIN = os.path.join(ROOT, "build", "tests", "uk_defer")
+VARIANTS = {"direct": None, "defer": DEFER_BIN}
+
+
+@pytest.fixture(params=list(VARIANTS))
+def ukbin(request, monkeypatch):
+    """Every user-kernel case twice: the default build, and the build with deferred any_hit calls
+    (hip_kernels.h VRH_USER_DEFER=1: record, trace the tile's any_hit rays as one pool, replay), whose
+    frames must be the same bits."""
+    b = VARIANTS[request.param] or BIN
+    assert os.path.exists(b), "run __graft_entry__.build() (make -C visionaray_amd cpp_tests)"
+    monkeypatch.setattr(sys.modules[__name__], "BIN", b)
+    return b
+
+
 def _run(tmp_path, mode, scene, W, H, *extra):
     out = tmp_path / mode
     out.mkdir()
@@ -43,7 +58,7 @@ def _check_hashes(oracle_mod, got, g, keys):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case,frame", [("hf200_320x180", 0), ("frame1_hf200_320x180", 1)])
-def test_user_ao_kernel_matches_reference(tmp_path, golden, oracle_mod, case, frame):
+def test_user_ao_kernel_matches_reference(tmp_path, golden, oracle_mod, case, frame, ukbin):
     g = golden[case]
     got = _run(tmp_path, "ao", g["scene"], g["W"], g["H"], frame)
     _check_hashes(oracle_mod, got, g, [("prim_id", "primid_hash"), ("t", "t_hash"), ("occ", "occ_hash"),
@@ -78,22 +93,26 @@ def test_anyhit_entry_cut_returns_reference_order_records(tmp_path, grid, W, H, 
     as the walk from the root: every any_hit call of the AO lambda returns the same hit RECORD (prim id
     and t of the first hit found), not only the same hit / miss -- against the default build."""
     assert os.path.exists(CUT_BIN), "run __graft_entry__.build() (make -C visionaray_amd cpp_tests)"
+    assert os.path.exists(DEFER_BIN), "run __graft_entry__.build() (make -C visionaray_amd cpp_tests)"
     outs = []
-    for b in (CUT_BIN, BIN):
+    for b in (CUT_BIN, DEFER_BIN, BIN):
         d = tmp_path / os.path.basename(b)
         d.mkdir()
         subprocess.run([b, "anyrec", str(grid), str(W), str(H), str(d), str(frame), str(radius)], check=True,
                        capture_output=True, text=True, timeout=120)
         outs.append(np.fromfile(d / "color.bin", np.float32).reshape(-1, 4))
-    cut, ref = outs
+    ref = outs[-1]
     assert float((ref[:, 1] > 0).mean()) > 0.01, "the case must have occluded AO rays"
-    bad = np.flatnonzero(np.any(cut.view(np.uint32) != ref.view(np.uint32), axis=1))
-    assert bad.size == 0, f"{bad.size} pixels' any_hit records differ, first {bad[:8].tolist()}"
+    # the deferred build (VRH_USER_DEFER=1) traces the same calls in a pool, in the same walk order:
+    # the same records too
+    for name, got in zip(("entry cut", "deferred"), outs[:2]):
+        bad = np.flatnonzero(np.any(got.view(np.uint32) != ref.view(np.uint32), axis=1))
+        assert bad.size == 0, f"{name}: {bad.size} pixels' any_hit records differ, first {bad[:8].tolist()}"
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["mask_hf200_320x180", "mask_hf64_160x90"])
-def test_user_mask_intersector_matches_reference(tmp_path, golden, oracle_mod, case):
+def test_user_mask_intersector_matches_reference(tmp_path, golden, oracle_mod, case, ukbin):
     g = golden[case]
     ref = np.load(os.path.join(GOLDEN, case + ".npz"))
     mpath = tmp_path / "mask.bin"
@@ -109,7 +128,7 @@ def test_user_mask_intersector_matches_reference(tmp_path, golden, oracle_mod, c
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["jittered", "jittered_blend", "ssaa2", "ssaa4", "ssaa8"])
-def test_user_kernel_pixel_samplers_match_reference(tmp_path, golden, kind):
+def test_user_kernel_pixel_samplers_match_reference(tmp_path, golden, kind, ukbin):
     """make_sched_params(pixel_sampler::<kind>, cam, rt) with a user kernel: the reference harness's
     sampler frames (colour blended onto the same initial target, the last sample's prim id)."""
     case = f"sampler_{kind}_hf64_ao"
@@ -127,7 +146,7 @@ def test_user_kernel_pixel_samplers_match_reference(tmp_path, golden, kind):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["matrix_uniform_hf64_ao", "matrix_ssaa4_hf64_ao"])
-def test_user_kernel_camera_matrices_match_reference(tmp_path, golden, case):
+def test_user_kernel_camera_matrices_match_reference(tmp_path, golden, case, ukbin):
     """make_sched_params(sampler, view_matrix, proj_matrix, rt) with a user kernel: the reference
     harness's matrix-camera frames (sched_common.h:152-176)."""
     g = golden[case]
@@ -145,7 +164,7 @@ def test_user_kernel_camera_matrices_match_reference(tmp_path, golden, case):
 
 
 @pytest.mark.gpu
-def test_user_kernel_with_intersector_in_sched_params(tmp_path, golden, oracle_mod):
+def test_user_kernel_with_intersector_in_sched_params(tmp_path, golden, oracle_mod, ukbin):
     """make_sched_params(sampler, cam, rt, isect) (scheduler.h:177-193): hip_sched calls the kernel as
     kernel(isect, r, x, y) (sched_common.h:786-818) -- the mask frames again."""
     case = "mask_hf200_320x180"
@@ -162,7 +181,7 @@ def test_user_kernel_with_intersector_in_sched_params(tmp_path, golden, oracle_m
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["heart_hf64_160x90", "heart_hf200_320x180"])
-def test_user_heart_intersector_matches_reference(tmp_path, golden, case):
+def test_user_heart_intersector_matches_reference(tmp_path, golden, case, ukbin):
     g = golden[case]
     ref = np.load(os.path.join(GOLDEN, case + ".npz"))
     got = _run(tmp_path, "heart", g["scene"], g["W"], g["H"])
@@ -174,7 +193,7 @@ def test_user_heart_intersector_matches_reference(tmp_path, golden, case):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["list_hf64_160x90", "list_hf200_320x180"])
-def test_user_kernel_over_bvh_list_with_scissor_matches_reference(tmp_path, golden, oracle_mod, case):
+def test_user_kernel_over_bvh_list_with_scissor_matches_reference(tmp_path, golden, oracle_mod, case, ukbin):
     """closest_hit / any_hit over a list of two BVH refs (traverse_linear.inl:76-141) in a user lambda,
     with the scissor box honoured by the user-kernel launch (cuda_sched.inl:71)."""
     g = golden[case]
@@ -185,7 +204,7 @@ def test_user_kernel_over_bvh_list_with_scissor_matches_reference(tmp_path, gold
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("scene,W,H", [("hf64", 160, 90), ("hf200", 333, 181)])
-def test_user_kernel_frames_in_flight_equal_single_frames(tmp_path, scene, W, H):
+def test_user_kernel_frames_in_flight_equal_single_frames(tmp_path, scene, W, H, ukbin):
     """hip_sched::frames with a user kernel (one persistent launch, three cameras, frame numbers
     f0 .. f0 + 2) equals three frame() calls bit for bit, and the frames differ (ragged width and
     height: partial tiles at the right and bottom edges)."""
@@ -205,5 +224,6 @@ def test_user_kernel_header_needs_hipcc(tmp_path):
 
 
 def test_user_kernel_program_is_built():
-    """build() compiled the user-kernel program for gfx950 (it travels to the GPU box with the tree)."""
-    assert os.path.exists(BIN), "run __graft_entry__.build() (make -C visionaray_amd cpp_tests)"
+    """build() compiled the user-kernel programs for gfx950 (they travel to the GPU box with the tree)."""
+    for b in (BIN, DEFER_BIN, SHARE_BIN, CUT_BIN):
+        assert os.path.exists(b), f"{b}: run __graft_entry__.build() (make -C visionaray_amd cpp_tests)"

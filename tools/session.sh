@@ -10,7 +10,7 @@
 #   mem:<cfg>        L2 hit / TD busy / TD stall passes of bench:<cfg>
 #   trace:<cfg>      rocprofv3 --kernel-trace --stats of bench:<cfg>
 #   ab:<scene>:<libs>[:<kernel>]   same-box A/B of library builds (tools/ab_builds.sh), libs comma-separated
-#   pmcuser:<lambda|ref>  trace + counter passes of a user-kernel program (32 frames per launch, C3) and
+#   pmcuser:<lambda|defer|ref>  trace + counter passes of a user-kernel program (32 frames per launch, C3) and
 #                    their summary (tools/pmc_user.py -> profiles/pmc_user_<lambda|ref>.json)
 #   user[:reps]      user-kernel throughput: AO lambda and ao/main.cpp's kernel, 1 and 32 frames per launch
 #   counters         rocprofv3 -L (the counters this box offers)
@@ -66,9 +66,11 @@ for s in "$@"; do
     trace) step trace_$arg 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$arg -o run -- python3 bench.py $(cfg_args $arg) --no-cpu-baseline;;
     ab)    IFS=: read -r sc libs kn <<< "$arg"
            LIBS="${libs//,/ }" SCENES=$sc KERNEL=${kn:-ao} step ab_${sc}_${kn:-ao} 900 bash tools/ab_builds.sh;;
-    pmcuser) # lambda: the restated AO lambda (bench's user leg), ref: ao/main.cpp's own kernel through the
-             # reference's headers -- both on hip_sched::frames, 32 frames per launch, C3
+    pmcuser) # lambda: the restated AO lambda (bench's user leg), defer: the same with deferred any_hit
+             # calls (VRH_USER_DEFER), ref: ao/main.cpp's own kernel through the reference's headers -- all on
+             # hip_sched::frames, 32 frames per launch, C3
            case $arg in lambda) prog="build/tests/user_kernels bench 708 1920 1080 /tmp 4 32";;
+                        defer) prog="build/tests/uk_defer bench 708 1920 1080 /tmp 4 32";;
                         ref) prog="oracle/_ref/ref_kernels bench hf1M 1920 1080 4 32";; esac
            d=$OUT/pmcuser_$arg
            step pmcuser_${arg}_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $d/trace -o run -- $prog
@@ -80,7 +82,7 @@ for s in "$@"; do
     user)  # user-kernel throughput (C3): the restated AO lambda and ao/main.cpp's own kernel (reference
            # headers), one frame per launch and 32 in flight, alternating, ${arg:-2} repetitions
            for rep in $(seq 1 ${arg:-2}); do for F in ${FS:-1 32}; do L=20; [ $F -gt 1 ] && L=4
-             for b in ${BINS:-build/tests/user_kernels oracle/_ref/ref_kernels}; do [ -x $b ] || continue
+             for b in ${BINS:-build/tests/user_kernels build/tests/uk_defer oracle/_ref/ref_kernels oracle/_ref/ref_kernels_defer}; do [ -x $b ] || continue
                case $b in *ref_kernels*) a="bench hf1M 1920 1080 $L $F";; *) a="bench 708 1920 1080 /tmp $L $F";; esac
                TAIL=1 step user_$(basename $b)_F${F}_$rep 150 $b $a
                echo "$(basename $b) F=$F $(grep frame_ms_median $OUT/user_$(basename $b)_F${F}_$rep.log)" >> $OUT/user.log
