@@ -970,7 +970,7 @@ __device__ inline void walk_shared(vrh_scene_view const& b, vrh::dev::ray_t cons
 #define VRH_USER_DEFER 0
 #endif
 #ifndef VRH_USER_DEFER_SLOTS
-#define VRH_USER_DEFER_SLOTS 16
+#define VRH_USER_DEFER_SLOTS 12     // logged calls per pixel (AO: 1 closest + 8 any); more run directly
 #endif
 // the trace phase's tuning (AO lambda, C3, 32 frames per launch, rates, profiles/r05/defer/): a lane takes
 // a new ray once 32 lanes are idle (1: -0.5 %, 48: -2 %, 64: -22 %); pairs wave-uniform over the active
@@ -984,13 +984,16 @@ constexpr uint32_t DEFER_OFF = 0u, DEFER_RECORD = 1u, DEFER_REPLAY = 2u;
 // the last word of a log entry: DTAG_ANY for an any_hit call, DTAG_PENDING until the trace phase has
 // answered it, the low bits the leaf index of the hit primitive or DTAG_NONE
 constexpr uint32_t DTAG_ANY = 0x80000000u, DTAG_PENDING = 0x40000000u, DTAG_NONE = 0x3FFFFFFFu;
-// a wave's log: VRH_USER_DEFER_SLOTS x 64 entries of 32 B ([slot][lane]: ori, dir, max_t, tag), then
-// the pool (entry indices of the pending any_hit calls, in call order)
+// a wave's log: VRH_USER_DEFER_SLOTS x 64 entries of 32 B ([slot][lane]: ori, dir, max_t, tag); the
+// pool (entry indices of the pending any_hit calls, in call order) is in LDS
 constexpr uint32_t DEFER_ENTRIES = VRH_USER_DEFER_SLOTS * 64u;
-constexpr size_t DEFER_WAVE_BYTES = size_t(DEFER_ENTRIES) * (32u + 4u);
+constexpr size_t DEFER_WAVE_BYTES = size_t(DEFER_ENTRIES) * 32u;
 // LDS words after the stacks (and the entry-cut area): [0] phase, [1] pool size, [2] BVH set,
-// [4, 6) log base, [6, 24) the tile's BVH (vrh_scene_view), [24, 88) calls per lane so far
-constexpr uint32_t DEFER_WORDS = 88u;
+// [4, 6) log base, [6, 24) the tile's BVH (vrh_scene_view), [24, 88) calls per lane so far, [88, ...) the pool
+// then the pool: 16-bit entry indices, DEFER_ENTRIES / 2 words (10,080 B of LDS per wave with the
+// stacks: 16 waves / CU; the pool in the global log instead: -2 %, profiles/r05/defer/)
+constexpr uint32_t DEFER_WORDS = 88u + DEFER_ENTRIES / 2u;
+static_assert(DEFER_ENTRIES <= 65536u, "16-bit pool entries");
 static_assert(sizeof(vrh_scene_view) <= 18u * 4u, "the LDS copy of the tile's BVH holds 18 words");
 enum defer_state : uint32_t { DEFER_RUN = 0u, DEFER_RUN_LOG = 1u, DEFER_PENDING = 2u, DEFER_LOGGED = 3u };
 #ifndef VRH_DEFER_PROF
@@ -1054,8 +1057,8 @@ __device__ inline defer_call defer_begin(vrh_scene_view const& v, basic_ray<floa
         // the pool, in call order: the lanes deferring here take consecutive places
         const uint64_t m = __ballot(true);
         const uint32_t n = a[1];
-        uint32_t* pool = reinterpret_cast<uint32_t*>(defer_log(a) + 2u * DEFER_ENTRIES);
-        pool[n + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u))] = d.entry;
+        const uint32_t pos = n + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+        reinterpret_cast<uint16_t*>(a + 88)[pos] = uint16_t(d.entry);
         __builtin_amdgcn_wave_barrier();
         if (lane == (uint32_t)__builtin_ctzll(m)) a[1] = n + uint32_t(__popcll(m));
         __builtin_amdgcn_wave_barrier();
@@ -1096,7 +1099,7 @@ __device__ inline void defer_trace_kind(uint32_t* a, unsigned long long* prof)
     const uint32_t root = v.root;
     const bool finite_scene = v.finite_bounds != 0u;
     float4* ent = defer_log(a);
-    const uint32_t* pool = reinterpret_cast<const uint32_t*>(ent + 2u * DEFER_ENTRIES);
+    const uint16_t* pool = reinterpret_cast<const uint16_t*>(a + 88);
     lds_stack st = user_stack();
     constexpr uint32_t IDLE = 0xFFFFFFFFu;
     uint32_t cur = IDLE, next = 0u;
@@ -1117,7 +1120,7 @@ __device__ inline void defer_trace_kind(uint32_t* a, unsigned long long* prof)
             const uint32_t k = next + __builtin_amdgcn_mbcnt_hi(uint32_t(idle >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(idle), 0u));
             if (cur == IDLE && k < n)
             {
-                cur = pool[k];
+                cur = uint32_t(pool[k]);
                 const float4 e0 = ent[2u * cur], e1 = ent[2u * cur + 1u];
                 r = make_ray(mk3(e0.x, e0.y, e0.z), mk3(e0.w, e1.x, e1.y));
                 max_t = e1.z;
