@@ -5,8 +5,9 @@ no-op, gpu_buffer_rt.inl:84-86) with the frames overlapping on the context's two
 The bar is the synchronous path's result: a sequence of frames, clears, downloads and pixel-sampler
 passes run with the option on must leave every target -- and every intermediate download -- bit for
 bit as the same sequence does one synchronous frame at a time.  That covers the write order of two
-lanes on one target (the scratch-target copy), blending samplers that read the target, scissor boxes,
-shading kernels (which wait instead of using scratch), and the joins of the context stream.
+lanes on one target (the scratch-target copy, pending until something needs it, dropped when a later
+frame supersedes it), blending samplers that read the target, scissor boxes, shading kernels (which
+wait instead of using scratch), and the joins of the context stream.
 """
 import ctypes
 import os
@@ -138,6 +139,51 @@ def test_scissor_boxes_on_a_shared_target(ctx, scene):
     boxes = [(0, 0, W, H), (13, 7, 200, 150), (100, 40, W, 170), None, (0, 90, 160, H), (31, 0, 32, H)]
     ops = [("frame", 0, "ao" if i % 2 else "primary", i, 2 + i, U, boxes[i]) for i in range(6)]
     check_sequence(ctx, scene, ops, 1)
+
+
+def test_superseded_scratch_copies(ctx, scene):
+    """A frame that goes through the scratch target leaves its copy pending: a later primary / AO frame
+    into the same target over at least the same box drops it (that frame's pixels are never seen), any
+    other frame, a download or a frame on the same lane for another target issues it first.  Mixed:
+    full frames superseding each other, a smaller box (no cover), primary after AO and back, a second
+    target in between (the lanes' scratch targets reused), a download mid-sequence."""
+    full, half = None, (0, 0, W, 90)
+    ops = [("frame", 0, "ao", 0, 1, U, full), ("frame", 0, "primary", 1, 2, U, full),
+           ("frame", 0, "ao", 2, 3, U, (20, 20, 300, 160)), ("frame", 0, "ao", 3, 4, U, full),
+           ("frame", 1, "primary", 4, 5, U, full), ("frame", 0, "primary", 5, 6, U, full),
+           ("frame", 1, "ao", 0, 7, U, full), ("frame", 0, "ao", 1, 8, U, full), ("download", 0),
+           ("frame", 0, "ao", 2, 9, U, full), ("frame", 0, "primary", 3, 10, U, half),
+           ("frame", 0, "ao", 4, 11, U, full), ("frame", 1, "ao", 5, 12, U, half), ("frame", 0, "ao", 0, 13, U, full)]
+    check_sequence(ctx, scene, ops, 2)
+
+
+def test_target_freed_with_a_pending_copy(ctx, scene):
+    """A target closed while its last frame's copy is pending: the copy is dropped (nobody can read
+    it) and the context goes on with another target."""
+    dev = scene
+    cam, _, _ = scenes.scene_camera(NAME, W, H)
+    k = va.ao_kernel(dev)
+    sched = va.hip_sched(ctx)
+    ref = va.hip_buffer_rt(ctx, W, H)
+    try:
+        sched.frame(k, va.make_sched_params(U, cam, ref), frame_num=4)
+        want = _bits(ref.download())
+    finally:
+        ref.close()
+    ctx.set_option("async_frames", 1)
+    try:
+        a = va.hip_buffer_rt(ctx, W, H)
+        for f in range(3):
+            sched.frame(k, va.make_sched_params(U, cam, a), frame_num=1 + f)
+        a.close()
+        b = va.hip_buffer_rt(ctx, W, H)
+        for f in range(3):
+            sched.frame(k, va.make_sched_params(U, cam, b), frame_num=2 + f)
+        got = _bits(b.download())
+        b.close()
+    finally:
+        ctx.set_option("async_frames", 0)
+    _same(got, want, "target after a freed target's pending copy")
 
 
 def test_blending_and_jittered_samplers(ctx, scene):

@@ -53,6 +53,12 @@ struct vrh_ctx
         float* t = nullptr;
         uint8_t* occ = nullptr;
         size_t pixels = 0;
+        // the frame in the scratch target whose copy into `pending_rt` is not issued yet: a later frame
+        // into that target writing the same fields over at least the same box drops it (only the last
+        // frame's pixels are ever seen), anything else issues it first (ctx_flush_pending)
+        vrh_rt* pending_rt = nullptr;
+        uint32_t pending_clip[4] = {};
+        bool pending_fields[4] = {};      // colour, prim id, t, occlusion
     } lane[2];
     uint32_t next_lane = 0;
     hipEvent_t main_mark = nullptr;             // position of `stream` that an async frame waits for
@@ -142,8 +148,13 @@ inline hipError_t mark_written(vrh_rt* rt, hipStream_t stream)
 // asynchronous frames: `stream` waits for every frame issued on the context's frame lanes so far
 // (no host synchronisation).  Every entry point that issues work on `stream` or synchronises it calls
 // this first, so work issued after a frame sees that frame's results.
+// issue the pending scratch copy of lane `l` (vrh_runtime.hip); l < 0: both lanes
+hipError_t ctx_flush_pending(const vrh_ctx* ctx, int l = -1);
+
 inline hipError_t ctx_join(const vrh_ctx* ctx)
 {
+    const hipError_t f = ctx_flush_pending(ctx);
+    if (f != hipSuccess) return f;
     bool any = false;
     for (const auto& l : ctx->lane)
         if (l.used)

@@ -809,6 +809,9 @@ VRH_API int vrh_rt_free(vrh_rt* rt)
         if (rt->mh_prim_id) (void)hipFree(rt->mh_prim_id);
         if (rt->mh_t) (void)hipFree(rt->mh_t);
     }
+    if (rt->ctx)
+        for (auto& l : rt->ctx->lane)
+            if (l.pending_rt == rt) l.pending_rt = nullptr;     // a frame nobody can read any more
     if (rt->lane_written)
     {
         if (rt->ctx) (void)hipSetDevice(rt->ctx->device);
@@ -858,6 +861,44 @@ __global__ void copy_clip_kernel(float4* color, uint32_t* pid, float* t, uint8_t
     if (occ) occ[i] = s_occ[i];
 }
 } // namespace
+
+} // extern "C"
+
+// Asynchronous frames into a shared target: the scratch copy of lane l's pending frame, issued on that
+// lane after the target's last writer (the other lane, unless joined since); the target's last writer
+// is then this lane.  Called before anything else may read or write the target (ctx_join: every entry
+// point that works on the context stream; vrh_render_batch for other frames) and before the lane's
+// scratch target is reused.
+hipError_t ctx_flush_pending(const vrh_ctx* cctx, int only)
+{
+    vrh_ctx* ctx = const_cast<vrh_ctx*>(cctx);
+    for (int l = 0; l < 2; ++l)
+    {
+        if (only >= 0 && l != only) continue;
+        vrh_ctx::lane_t& L = ctx->lane[l];
+        vrh_rt* rt = L.pending_rt;
+        if (!rt) continue;
+        L.pending_rt = nullptr;
+        hipError_t e;
+        if (rt->lane >= 0 && rt->lane != l && rt->lane_epoch == ctx->join_epoch)
+            if ((e = hipStreamWaitEvent(L.stream, rt->lane_written, 0)) != hipSuccess) return e;
+        const uint32_t* cl = L.pending_clip;
+        const dim3 blk(64, 4), grd((cl[2] - cl[0] + 63) / 64, (cl[3] - cl[1] + 3) / 4);
+        const bool* fl = L.pending_fields;
+        hipLaunchKernelGGL(copy_clip_kernel, grd, blk, 0, L.stream, fl[0] ? rt->color : nullptr, fl[1] ? rt->prim_id : nullptr,
+                           fl[2] ? rt->t : nullptr, fl[3] ? rt->occ : nullptr, (const float4*)L.color,
+                           (const uint32_t*)L.prim_id, (const float*)L.t, (const uint8_t*)L.occ, rt->width,
+                           cl[0], cl[1], cl[2], cl[3]);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if ((e = hipEventRecord(rt->lane_written, L.stream)) != hipSuccess) return e;
+        rt->lane = l;
+        rt->lane_epoch = ctx->join_epoch;
+        if ((e = hipEventRecord(L.done, L.stream)) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+extern "C" {
 
 // gpu_buffer_rt::clear_color_buffer (thrust::fill, gpu_buffer_rt.inl:49-76); side buffers reset to "miss"
 VRH_API int vrh_rt_clear(vrh_ctx* ctx, vrh_rt* rt, const float color[4])
@@ -1304,13 +1345,32 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
         VRH_HIP(hipEventRecord(ctx->main_mark, ctx->stream));
         VRH_HIP(hipStreamWaitEvent(S, ctx->main_mark, 0));
         if (rt->written_pending) VRH_HIP(hipStreamWaitEvent(S, rt->written, 0));
-        // the target's last writer is the other lane, not yet joined: write order must hold.  A primary /
-        // AO frame of one image through a sampler that does not read the target renders into this lane's
-        // scratch target now and is copied after that writer; anything else waits for it
+        // a primary / AO frame of one image through a sampler that does not read the target writes every
+        // field of the target at every pixel of its scissor box: it may go through the scratch target,
+        // and it supersedes a pending scratch copy into this target of no larger box (that frame's pixels
+        // would never be seen: they are dropped, not copied).  Any other pending copy into this target,
+        // and one still in this lane's scratch target, is issued first.
+        const bool scratch_ok = num_frames == 1 && (k->kind == VRH_KERNEL_PRIMARY || ao) && (!sp || sp->blend == 0);
+        const uint32_t* cl = p.cam[0].clip;
+        const bool fields[4] = { dst_color != nullptr, dst_pid != nullptr, dst_t != nullptr, dst_occ != nullptr };
+        for (uint32_t l = 0; l < 2; ++l)
+        {
+            vrh_ctx::lane_t& Q = ctx->lane[l];
+            if (!Q.pending_rt) continue;
+            const uint32_t* qc = Q.pending_clip;
+            const bool covers = Q.pending_rt == rt && scratch_ok && cl[0] <= qc[0] && cl[1] <= qc[1] && cl[2] >= qc[2]
+                                && cl[3] >= qc[3] && fields[0] == Q.pending_fields[0] && fields[1] == Q.pending_fields[1]
+                                && fields[2] == Q.pending_fields[2] && fields[3] == Q.pending_fields[3];
+            if (covers) Q.pending_rt = nullptr;
+            else if (Q.pending_rt == rt || l == li) VRH_HIP(ctx_flush_pending(ctx, int(l)));
+        }
+        // the target's last writer is the other lane, not yet joined: write order must hold.  A frame that
+        // may go through the scratch target renders there now, and its copy becomes the lane's pending
+        // copy (issued when something else needs the target, dropped when a later frame supersedes it);
+        // anything else waits for that writer
         const bool other_writer = rt->lane >= 0 && rt->lane != int(li) && rt->lane_epoch == ctx->join_epoch;
         if (other_writer)
         {
-            const bool scratch_ok = num_frames == 1 && (k->kind == VRH_KERNEL_PRIMARY || ao) && (!sp || sp->blend == 0);
             if (scratch_ok)
             {
                 const size_t n = size_t(rt->width) * rt->height;
@@ -1404,24 +1464,27 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     VRH_HIP(hipEventRecord(ctx->ev_stop[slot], S));
     if (async)
     {
+        const uint32_t* cl = p.cam[0].clip;
         if (via_scratch)
         {
-            // after the target's previous writer (the other lane), the scissor box of the scratch
-            // target -- every pixel a primary / AO frame writes -- goes to the target
-            VRH_HIP(hipStreamWaitEvent(S, rt->lane_written, 0));
-            const uint32_t* cl = p.cam[0].clip;
+            // the scissor box of the scratch target -- every pixel a primary / AO frame writes -- is this
+            // lane's pending copy into the target (ctx_flush_pending: after the target's previous writer)
             if (cl[2] > cl[0] && cl[3] > cl[1])
             {
-                const dim3 blk(64, 4), grd((cl[2] - cl[0] + 63) / 64, (cl[3] - cl[1] + 3) / 4);
-                hipLaunchKernelGGL(copy_clip_kernel, grd, blk, 0, S, dst_color, dst_pid, dst_t, dst_occ,
-                                   (const float4*)p.color, (const uint32_t*)p.prim_id, (const float*)p.t,
-                                   (const uint8_t*)p.occ, rt->width, cl[0], cl[1], cl[2], cl[3]);
-                VRH_HIP(hipGetLastError());
+                L->pending_rt = rt;
+                for (int i = 0; i < 4; ++i) L->pending_clip[i] = cl[i];
+                L->pending_fields[0] = dst_color != nullptr;
+                L->pending_fields[1] = dst_pid != nullptr;
+                L->pending_fields[2] = dst_t != nullptr;
+                L->pending_fields[3] = dst_occ != nullptr;
             }
         }
-        VRH_HIP(hipEventRecord(rt->lane_written, S));
-        rt->lane = int(L - ctx->lane);
-        rt->lane_epoch = ctx->join_epoch;
+        else
+        {
+            VRH_HIP(hipEventRecord(rt->lane_written, S));
+            rt->lane = int(L - ctx->lane);
+            rt->lane_epoch = ctx->join_epoch;
+        }
         VRH_HIP(hipEventRecord(L->done, S));
         L->used = true;
     }
