@@ -272,8 +272,9 @@ def test_user_stream_work_after_async_frames(ctx, scene):
 
 
 def test_async_option_range(ctx):
-    with pytest.raises(_capi.VrhError):
-        ctx.set_option("async_frames", 2)
+    for bad in (2, -1):
+        with pytest.raises(_capi.VrhError):
+            ctx.set_option("async_frames", bad)
     ctx.set_option("async_frames", 0)
 
 

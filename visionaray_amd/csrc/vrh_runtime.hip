@@ -196,7 +196,7 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
         // measured in round 4 and removed (slower: profiles/r04/ab/lane_layout/); 0 is accepted
         if (value != 0) { set_error("vrh_ctx_set_option: the quad-coherent and block-shared hand-outs were removed (they measured slower)"); return VRH_ERR_UNSUPPORTED; }
         return VRH_OK;
-    case VRH_OPT_ASYNC_FRAMES: VRH_CHECK(value <= 1, "vrh_ctx_set_option: asynchronous frames is 1 (on) or 0 (off)"); ctx->opt_async = int(value); break;
+    case VRH_OPT_ASYNC_FRAMES: VRH_CHECK(value == 0 || value == 1, "vrh_ctx_set_option: asynchronous frames is 1 (on) or 0 (off)"); ctx->opt_async = int(value); break;
     case VRH_OPT_CLUSTER_TILES:
         // stored as the kernel's uint32 cluster size: a negative value would wrap (cluster x frames can
         // become 0, a division by zero in the hand-out), so the range is checked here as well
