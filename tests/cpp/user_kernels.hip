@@ -381,6 +381,59 @@ int main(int argc, char** argv)
             write_file(outdir + "/color.bin", out.data(), out.size() * 4);
             return 0;
         }
+        else if (mode == "sphrec")
+        {
+            // sphrec <grid> W H outdir frame radius n: a sphere scene (vrh_gen_spheres: n spheres in
+            // [-1, 1]^3, the camera at (0, 0, 3.5) as scenes.py's sph<n>): per pixel the closest hit
+            // (prim id, t) and an FNV-1a hash over the records of 8 any_hit rays of radius `radius`
+            // from the hit point (a hemisphere about -dir) -- the sphere path of closest_hit / any_hit,
+            // and of the deferred build's trace
+            const unsigned frame_num = unsigned(strtoul(argv[6], nullptr, 10));
+            const float radius = float(atof(argv[7]));
+            const unsigned nsph = unsigned(strtoul(argv[8], nullptr, 10));
+            using sph_t = basic_sphere<float>;
+            std::vector<sph_t> sph(nsph);
+            if (vrh_gen_spheres(nsph, sph.data()) != VRH_OK) return 2;
+            auto host_sph = build<index_bvh<sph_t>>(sph.data(), sph.size());
+            hip_index_bvh<sph_t> dev_sph(host_sph);
+            hip_bvh_ref sref = checked_ref(dev_sph.ref());
+
+            const ref_list sl{ to_device(std::vector<hip_bvh_ref>{ sref }), 1u };
+            camera scam;
+            scam.perspective(45.0f * constants::degrees_to_radians<float>(), W / static_cast<float>(H), 0.001f, 1000.0f);
+            scam.look_at(vec3(0.0f, 0.0f, 3.5f), vec3(0.0f, 0.0f, 0.0f), vec3(0.0f, 1.0f, 0.0f));
+            auto sp_params = make_sched_params(pixel_sampler::uniform_type{}, scam, rt);
+            hip_bvh_ref const* begin = sl.r;
+            hip_bvh_ref const* end = sl.r + sl.n;
+            sched.frame([=] __device__ (ray r, random_sampler<float>& samp) -> result_record<float>
+            {
+                result_record<float> result;
+                result.color = vec4(0.0f, 0.0f, __uint_as_float(0xFFFFFFFFu), -1.0f);
+                auto hr = closest_hit(r, begin, end);
+                if (hr.hit)
+                {
+                    const vec3 p = r.ori + r.dir * hr.t;
+                    vec3 u, v, w = normalize(-r.dir);
+                    make_orthonormal_basis(u, v, w);
+                    uint32_t h = 2166136261u, hits = 0;
+                    auto mix = [&](uint32_t x) { for (int k = 0; k < 4; ++k) { h ^= (x >> (8 * k)) & 0xFFu; h *= 16777619u; } };
+                    for (int i = 0; i < 8; ++i)
+                    {
+                        auto sp = cosine_sample_hemisphere(samp.next(), samp.next());
+                        auto dir = normalize(sp.x * u + sp.y * v + sp.z * w);
+                        auto rec = any_hit(ray(p + dir * 1E-3f, dir), begin, end, radius);
+                        mix(rec.hit ? 1u : 0u);
+                        if (rec.hit) { mix(uint32_t(rec.prim_id)); mix(__float_as_uint(rec.t)); hits += 1u; }
+                    }
+                    result.color = vec4(__uint_as_float(h), float(hits), __uint_as_float(uint32_t(hr.prim_id)), hr.t);
+                }
+                return result;
+            }, sp_params, frame_num);
+            std::vector<float> out(4 * size_t(W) * H);
+            rt.download(out.data());
+            write_file(outdir + "/color.bin", out.data(), out.size() * 4);
+            return 0;
+        }
         else if (mode == "bench")
         {
             // user-kernel throughput, median wall time per frame over `launches` synchronous launches:

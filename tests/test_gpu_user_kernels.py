@@ -111,6 +111,33 @@ def test_anyhit_entry_cut_returns_reference_order_records(tmp_path, grid, W, H, 
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,W,H,frame,radius", [(20000, 320, 180, 3, 0.3), (8000, 160, 90, 1, 0.8)])
+def test_user_kernel_on_spheres_closest_hit_and_deferred_records(tmp_path, oracle_mod, n, W, H, frame, radius):
+    """closest_hit / any_hit over a sphere BVH (basic_sphere<float>, vrh_gen_spheres) in a user lambda:
+    every pixel's closest hit (prim id, t) equals the oracle's primary render of the same scene and
+    camera, and the deferred build (VRH_USER_DEFER=1, its trace on the sphere path) returns the direct
+    build's any_hit RECORDS for 8 rays per hit."""
+    outs = []
+    for b in (BIN, DEFER_BIN):
+        assert os.path.exists(b), "run __graft_entry__.build() (make -C visionaray_amd cpp_tests)"
+        d = tmp_path / os.path.basename(b)
+        d.mkdir()
+        subprocess.run([b, "sphrec", "64", str(W), str(H), str(d), str(frame), str(radius), str(n)], check=True,
+                       capture_output=True, text=True, timeout=120)
+        outs.append(np.fromfile(d / "color.bin", np.float32).reshape(-1, 4))
+    direct, deferred = outs
+    bad = np.flatnonzero(np.any(deferred.view(np.uint32) != direct.view(np.uint32), axis=1))
+    assert bad.size == 0, f"deferred: {bad.size} pixels differ, first {bad[:8].tolist()}"
+    pid = direct[:, 2].view(np.uint32)
+    hit = pid != 0xFFFFFFFF
+    assert hit.mean() > 0.02 and float((direct[hit, 1] > 0).mean()) > 0.01, "the case must have hits and occluded rays"
+    O = oracle_mod
+    ref = O.render(O.make_scene(f"sph{n}"), O.scene_camera(f"sph{n}", W, H), mode=O.VO_MODE_PRIMARY)
+    assert np.array_equal(pid, ref["prim_id"]), f"{int((pid != ref['prim_id']).sum())} pixels' closest hit differs from the oracle"
+    assert np.array_equal(direct[hit, 3].view(np.uint32), ref["t"][hit].view(np.uint32)), "closest-hit t"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("case", ["mask_hf200_320x180", "mask_hf64_160x90"])
 def test_user_mask_intersector_matches_reference(tmp_path, golden, oracle_mod, case, ukbin):
     g = golden[case]
