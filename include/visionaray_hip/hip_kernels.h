@@ -1724,8 +1724,35 @@ __device__ inline uint32_t xcc_id()
 #else
 #define VRH_USER_OCC
 #endif
+template <typename K, uint32_t SK, uint32_t SN, uint32_t NC>
+__device__ __forceinline__ void user_render_body(K& kernel, user_frames<NC> const& f);
+
 template <typename K, uint32_t SK = VRH_SAMPLER_UNIFORM, uint32_t SN = 1, uint32_t NC = 1>
 __global__ __launch_bounds__(64) VRH_USER_OCC void user_render(K kernel, user_frames<NC> f)
+{
+    user_render_body<K, SK, SN, NC>(kernel, f);
+}
+
+// VRH_USER_AUTO_WAVES (default on unless VRH_USER_WAVES or VRH_USER_DEFER is set): the same kernel
+// also compiled for a 5-wave register target; the launch takes it when it holds more waves per CU
+// and spills at most VRH_USER_AUTO_SCRATCH bytes per lane (the AO lambda: 104 VGPRs = 4 waves, or 96
+// with 4 spilled = 5 waves: +4.2 %, profiles/r05/user/)
+#ifndef VRH_USER_AUTO_WAVES
+#define VRH_USER_AUTO_WAVES (VRH_USER_WAVES == 0 && !VRH_USER_DEFER)
+#endif
+#ifndef VRH_USER_AUTO_SCRATCH
+#define VRH_USER_AUTO_SCRATCH 32
+#endif
+#if VRH_USER_AUTO_WAVES
+template <typename K, uint32_t SK = VRH_SAMPLER_UNIFORM, uint32_t SN = 1, uint32_t NC = 1>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void user_render_w5(K kernel, user_frames<NC> f)
+{
+    user_render_body<K, SK, SN, NC>(kernel, f);
+}
+#endif
+
+template <typename K, uint32_t SK, uint32_t SN, uint32_t NC>
+__device__ __forceinline__ void user_render_body(K& kernel, user_frames<NC> const& f)
 {
     const uint32_t lane = threadIdx.y * 8u + threadIdx.x;
     if (VRH_USER_ANYHIT_CUT && lane == 0u) user_cut_area()[2] = 0u;     // no any_hit entry cut yet
@@ -1860,6 +1887,26 @@ inline hipError_t launch_user_render(hip_context& ctx, K const& kernel, user_fra
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, lds);
     if (e != hipSuccess) return e;
+#if VRH_USER_AUTO_WAVES
+    {
+        // once per kernel: the 5-wave instance if it holds more waves and spills (almost) nothing
+        static int w5 = -1;
+        auto fn5 = user_render_w5<K, SK, SN, NC>;
+        if (w5 < 0)
+        {
+            hipFuncAttributes a{};
+            int per_cu5 = 0;
+            if ((e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(fn5))) != hipSuccess) return e;
+            if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu5, fn5, 64, lds)) != hipSuccess) return e;
+            w5 = (per_cu5 > per_cu && a.localSizeBytes <= size_t(VRH_USER_AUTO_SCRATCH)) ? per_cu5 : 0;
+        }
+        if (w5 > 0)
+        {
+            fn = fn5;
+            per_cu = w5;
+        }
+    }
+#endif
     const uint64_t work = uint64_t(f.tiles) * f.nframes;
     const uint64_t resident = uint64_t(cus > 0 ? cus : 1) * uint64_t(per_cu > 0 ? per_cu : 1);
     const uint32_t grid = uint32_t(work < resident ? work : resident);
