@@ -992,7 +992,11 @@ constexpr size_t DEFER_WAVE_BYTES = size_t(DEFER_ENTRIES) * 32u;
 // [4, 6) log base, [6, 24) the tile's BVH (vrh_scene_view), [24, 88) calls per lane so far, [88, ...) the pool
 // then the pool: 16-bit entry indices, DEFER_ENTRIES / 2 words (10,080 B of LDS per wave with the
 // stacks: 16 waves / CU; the pool in the global log instead: -2 %, profiles/r05/defer/)
-constexpr uint32_t DEFER_WORDS = 88u + DEFER_ENTRIES / 2u;
+// then one bit per entry: the trace phase found no hit (a miss leaves the entry's tag pending; only a
+// hit writes its leaf index to the log)
+constexpr uint32_t DEFER_MISS_WORDS = DEFER_ENTRIES / 32u;
+constexpr uint32_t DEFER_WORDS = 88u + DEFER_ENTRIES / 2u + DEFER_MISS_WORDS;
+__device__ inline uint32_t* defer_miss_bits(uint32_t* a) { return a + 88u + DEFER_ENTRIES / 2u; }
 static_assert(DEFER_ENTRIES <= 65536u, "16-bit pool entries");
 static_assert(sizeof(vrh_scene_view) <= 18u * 4u, "the LDS copy of the tile's BVH holds 18 words");
 enum defer_state : uint32_t { DEFER_RUN = 0u, DEFER_RUN_LOG = 1u, DEFER_PENDING = 2u, DEFER_LOGGED = 3u };
@@ -1068,7 +1072,8 @@ __device__ inline defer_call defer_begin(vrh_scene_view const& v, basic_ray<floa
     // replay: the logged call must be this one, bit for bit (reading only the tag while every answer so
     // far equals the record phase's -- the kernel then makes the same calls -- measured 0.8-1.3 % slower)
     const float4 e0 = ent[0], e1 = ent[1];
-    const uint32_t tag = __float_as_uint(e1.w);
+    uint32_t tag = __float_as_uint(e1.w);
+    if (any && (tag & DTAG_PENDING) && (defer_miss_bits(a)[d.entry >> 5] >> (d.entry & 31u) & 1u)) tag = DTAG_ANY | DTAG_NONE;
     if (same_bits(e0.x, ray.ori.x) && same_bits(e0.y, ray.ori.y) && same_bits(e0.z, ray.ori.z) && same_bits(e0.w, ray.dir.x)
         && same_bits(e1.x, ray.dir.y) && same_bits(e1.y, ray.dir.z) && same_bits(e1.z, max_t)
         && (tag & (DTAG_ANY | DTAG_PENDING)) == (any ? DTAG_ANY : 0u))
@@ -1150,7 +1155,8 @@ __device__ inline void defer_trace_kind(uint32_t* a, unsigned long long* prof)
                                                                                 0xFFFFFFFFu, DEFER_STEP_FLAGS, &hx);
             if (res != 0)
             {
-                reinterpret_cast<uint32_t*>(ent + 2u * cur + 1u)[3] = DTAG_ANY | (res == 1 ? hx.li : DTAG_NONE);
+                if (res == 1) reinterpret_cast<uint32_t*>(ent + 2u * cur + 1u)[3] = DTAG_ANY | hx.li;
+                else atomicOr(&defer_miss_bits(a)[cur >> 5], 1u << (cur & 31u));
                 cur = IDLE;
             }
         }
@@ -1798,6 +1804,7 @@ __device__ __forceinline__ void user_render_body(K& kernel, user_frames<NC> cons
                 // barriers only order the phases' LDS and global accesses
                 uint32_t* da = defer_area();
                 da[24u + lane] = 0u;
+                for (uint32_t w = lane; w < DEFER_MISS_WORDS; w += 64u) defer_miss_bits(da)[w] = 0u;
                 if (lane == 0u)
                 {
                     const uintptr_t log = uintptr_t(f.defer_log + size_t(blockIdx.x) * DEFER_WAVE_BYTES);
