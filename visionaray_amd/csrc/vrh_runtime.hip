@@ -1214,7 +1214,12 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     const uint32_t refill_shade = (lc.epi == 1 || lc.epi == 3) ? 8u : 1u;
     p.refill_min_primary = ctx->opt_refill ? uint32_t(ctx->opt_refill)
                          : (primary_step && num_frames > 1) ? 16u : lc.epi ? refill_shade : 1u;
-    p.descent_cap = ctx->opt_dcap ? uint32_t(ctx->opt_dcap) : primary_step ? 8u : 0xFFFFFFFFu;
+    // primary visibility caps a lane's descent at 8 inner visits per step; at 8 waves / SIMD (round 5,
+    // profiles/r05/sweepP2/, 20 frames per launch, min over rounds) triangle scenes the Infinity Cache
+    // holds run best at 10 (hf1M +3 %; hf10M, above 256 MB, best at 8: 10 is -3 %), spheres at 6
+    // (sph1M +1.5 %)
+    const uint32_t dcap_primary = sc->info.prim_kind == VRH_PRIM_SPHERE48 ? 6u : sc->info.device_bytes > (256ull << 20) ? 8u : 10u;
+    p.descent_cap = ctx->opt_dcap ? uint32_t(ctx->opt_dcap) : primary_step ? dcap_primary : 0xFFFFFFFFu;
     // shading epilogues (simple / multi_hit / whitted) pop on a miss too: +4-7 % (profiles/r01/shade/)
     // AO (step loop): the tile's AO rays wait for its primaries (ao_gate), any-hit rays descend the
     // 4-wide records and primaries pop on a miss -- together +6 % on hf1M and +10 % on hf10M
