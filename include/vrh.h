@@ -261,8 +261,9 @@ enum vrh_option {
                                     loop): 1 = on when the BVH passes the containment check, 2 = off
                                     (auto: on for the AO kernel, off for the shading kernels)     */
     VRH_OPT_DESCENT_CAP = 11,    /* step loop: inner visits per step before a lane's descent is
-                                    resumed in the next step (1..1024; auto: 8 for primary
-                                    visibility, unlimited for AO)                                 */
+                                    resumed in the next step (1..1024; auto for primary visibility:
+                                    6 for spheres, 10 for triangle scenes up to 256 MB, 8 above;
+                                    unlimited for AO)                                             */
     VRH_OPT_POP_ON_MISS = 12,    /* step loop: a descent that misses both children pops its stack
                                     and keeps descending in the same step: 1 = on, 2 = off (auto: on) */
     VRH_OPT_COOP_FETCH = 13,     /* removed in round 2 (the cooperative quad fetch measured slower):
