@@ -42,6 +42,9 @@ Rank 0 prints one JSON line (the contract of the task statement) with:
   * cpu_baseline: the reference's own SSE4 tiled_sched path (oracle/_ref, built from
     /root/reference by oracle/Makefile) on a bounded sample, best of a worker-thread sweep, with the
     host's core count, cgroup quota and model, and the retries / stall seconds of tiled_sched stalls.
+
+Settle: after the W warm-up steps, untimed launches of the timed shape run for --settle-ms (300 ms) of
+wall time so that the timed launches run at the GPU's sustained clocks (the line's `settle` object).
 """
 from __future__ import annotations
 
@@ -83,6 +86,9 @@ def parse():
     ap.add_argument("--moving-camera", type=float, default=0.5,
                     help="degrees of camera orbit per frame in an extra moving-camera leg after the timed region "
                          "(0: no such leg); its launches have the timed launches' shape")
+    ap.add_argument("--settle-ms", type=float, default=300.0,
+                    help="untimed launches of the timed shape for this long after the warm-up steps "
+                         "(GPU clock ramp), 0 = none")
     ap.add_argument("--gather-ids", action="store_true",
                     help="N > 1 / --shards: gather prim ids + AO masks with the colour (5 B per pixel on the wire, not 1)")
     ap.add_argument("--shards", type=int, default=0,
@@ -404,7 +410,20 @@ def main():
     for _ in range(args.warmup % F):
         run_batch(1)
     run_batch(F)
+    # settle: the GPU ramps its clocks over the first ~0.1-0.3 s of sustained work, and W warm-up steps
+    # of 0.2-1.1 ms frames are far shorter than that; untimed launches of the timed shape until
+    # --settle-ms of wall time have passed (reported in the line), so the timed launches run at the
+    # clocks every later launch runs at
+    settle_t0 = time.perf_counter()
+    settle_launches = 0
+    while (time.perf_counter() - settle_t0) * 1e3 < args.settle_ms:
+        run_batch(F)
+        settle_launches += 1
+        if settle_launches % 8 == 0:
+            sync()
     barrier()
+    settle = {"ms": round((time.perf_counter() - settle_t0) * 1e3, 1), "launches": settle_launches,
+              "frames_per_launch": F}
     ctx.stats_reset()
     barrier()
     first_timed = next_frame[0]
@@ -661,6 +680,7 @@ def main():
             "user_kernel_mrays": user_leg.get("mrays") if user_leg else None,
             "user_kernel_deferred_mrays": (user_leg.get("deferred") or {}).get("mrays") if user_leg else None,
             "host_build_s": round(build_s, 3),
+            "settle": settle,
             "verify": verify,
         }
         print(json.dumps(line), file=json_out, flush=True)
