@@ -1137,13 +1137,14 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     // the overflow-stack instances): 6 waves/SIMD, the LDS stack shrunk (below) to 16 entries so that 24
     // waves fit a CU, the rest in the overflow block -- hf1M +4.8 %, hf10M +8.7 % over 5 waves
     // (profiles/r05/occupancy/s6_*); AO tail sharing (opt-in) has 5-wave instances only.  Primary
-    // visibility: 8 waves/SIMD (64 VGPRs, no spill: hf1M +6.7-11 %, hf10M +3-9 %; spheres with the
-    // LDS stack shrunk to 20 entries so that 32 waves fit a CU: sph1M +4.8 % over 7 waves,
-    // profiles/r05/sweepS/ -- at the whole 28-entry stack in LDS only 22 fit, -1 to -4 %,
-    // profiles/r05/occupancy/); the counting variants keep 5 / 6 (at 8 they spill hundreds of
-    // VGPRs).  BVH lists run at 5 / 6
+    // visibility: 8 waves/SIMD (64 VGPRs, no spill: hf1M +6.7-11 %, hf10M +3-9 %); spheres with frames in
+    // flight too, with the LDS stack shrunk to 20 entries so that 32 waves fit a CU (sph1M +4.8 % over 7
+    // waves, profiles/r05/sweepS/ -- at the whole 28-entry stack in LDS only 22 fit, -1 to -4 %,
+    // profiles/r05/occupancy/), but one frame per launch at 7 (the occupancy-6 instance: 8 waves with the
+    // overflow stack measured -8 %, profiles/r05/s26/); the counting variants keep 5 / 6 (at 8 they
+    // spill hundreds of VGPRs).  BVH lists run at 5 / 6
     const int occ_ao = (ctx->opt_share == 1 || lc.count) ? 5 : 6;
-    const int occ_primary = !lc.count ? 8 : 6;
+    const int occ_primary = (!lc.count && (lc.kind == 0 || num_frames > 1)) ? 8 : 6;
     lc.occ = ctx->opt_occ ? ctx->opt_occ : whitted ? 5 : lc.epi ? 1 : lc.ao ? occ_ao : occ_primary;
     if (sp) lc.occ = lc.ao ? 5 : 6;                    // the sampler instances exist at the defaults
     if (list) lc.occ = ao ? 5 : 6;
