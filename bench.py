@@ -9,6 +9,10 @@ A "step" is one frame.  Inputs (BVH, primitives, normals) are resident in HBM be
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
+--gpus N > 1 without a launcher (no WORLD_SIZE): bench.py starts the N ranks itself as child processes
+before anything touches the GPU (launch_plan / spawn_ranks); with fewer GPUs than N, or WORLD_SIZE
+disagreeing with --gpus, it exits 2 with a message and prints no line.
+
 Frames: every frame has its own frame number (vrh_render's frame_num -> its own AO sample set,
 as the reference reseeds per frame, cuda_sched.inl:38-45, 79): the W warm-up frames are numbers
 1..W, the K timed frames W+1..W+K; frame 0 and frame 3 are rendered once, untimed, and checked
@@ -40,8 +44,9 @@ Rank 0 prints one JSON line (the contract of the task statement) with:
     gathers) on the microbenchmark tools/micro/l1_roof.hip (profiles/l1_roof.json).  The SURVEY
     §8d algorithmic HBM bytes are kept as roofline.hbm_algorithmic (informational);
   * cpu_baseline: the reference's own SSE4 tiled_sched path (oracle/_ref, built from
-    /root/reference by oracle/Makefile) on a bounded sample, best of a worker-thread sweep, with the
-    host's core count, cgroup quota and model, and the retries / stall seconds of tiled_sched stalls.
+    /root/reference by oracle/Makefile) on a bounded sample at threads = the CPUs the process may use
+    (cgroup quota), the median of 7 frames, with a cores/4 and cores/2 sweep and each point's spread,
+    the host's core count, quota and model, and the retries / stall seconds of tiled_sched stalls.
 
 Settle: after the W warm-up steps, untimed launches of the timed shape run for --settle-ms (300 ms) of
 wall time so that the timed launches run at the GPU's sustained clocks (the line's `settle` object).
@@ -76,7 +81,8 @@ def parse():
     ap.add_argument("--kernel", default=None, choices=["ao", "primary"], help="default: ao for triangles")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=None,
-                    help="host threads for the CPU baseline (default: the best of a 16/64/128/256 sweep)")
+                    help="host threads for the CPU baseline (default: the CPUs the process may use, with a "
+                         "cores/4, cores/2 sweep beside it)")
     ap.add_argument("--no-verify", action="store_true", help="skip the untimed checks against the fixtures")
     ap.add_argument("--no-user-kernel", action="store_true",
                     help="skip the user-kernel leg (hf1M AO at N=1: hip_kernels.h device lambda, 32 frames per launch)")
@@ -131,27 +137,37 @@ def usable_cpus(info):
     return max(1, min(avail, int(q))) if q else avail
 
 
-CPU_SWEEP = (16, 64, 128, 256)
-CPU_ATTEMPT_TIMEOUT_S = 60
+CPU_ATTEMPT_TIMEOUT_S = 90
+CPU_FRAMES = 7                  # timed frames per sweep point (median), after 1 warm-up frame
+
+
+def cpu_sweep_points(cores, threads=None):
+    """Worker-thread counts of the CPU baseline: --cpu-threads alone, else cores/4, cores/2 and cores --
+    never above the CPUs the process may use (oversubscribed points measured up to 3x apart between
+    sessions)."""
+    if threads:
+        return [threads]
+    return sorted({max(1, cores // 4), max(1, cores // 2), cores})
 
 
 def cpu_baseline(scene, kernel, threads=None):
     """Reference SSE4 tiled_sched<ray4> (oracle/_ref/vsnray_ref_bench) on a bounded sample: the same
-    scene and camera at full resolution, 1 warm-up + 3 timed frames per run.  Without --cpu-threads
-    the worker count is swept over CPU_SWEEP (capped at the CPUs this process may run on) and the
-    best is reported, with every point of the sweep.  tiled_sched can lose a worker's wake-up
-    (tiled_sched.inl:181 waits without a predicate against the notify_all at :386) and stall a frame
-    for good: a run that passes CPU_ATTEMPT_TIMEOUT_S is killed and tried once more, and the line
-    records the retries and the seconds lost to stalls."""
+    scene and camera at full resolution, 1 warm-up + CPU_FRAMES timed frames per point, the median
+    frame.  `value` is the point at threads = cores (the CPUs this process may use: the cgroup quota,
+    else the affinity mask); the sweep below it (cores/4, cores/2) and each point's min / max frame
+    rate are reported beside it.  tiled_sched can lose a worker's wake-up (tiled_sched.inl:181 waits
+    without a predicate against the notify_all at :386) and stall a frame for good: a run that passes
+    CPU_ATTEMPT_TIMEOUT_S is killed and tried once more, and the line records the retries and the
+    seconds lost to stalls."""
     from oracle import oracle as O
     samples = 8 if kernel == "ao" else 0
     info = host_info()
     info["cgroup_cpu_quota"] = cgroup_cpu_quota()
-    info["cores_note"] = ("cores = the CPUs the process may use (cgroup quota, else affinity); threads = "
-                          "the worker threads of the best sweep point")
+    cores = usable_cpus(info)
+    info["cores_note"] = ("cores = the CPUs the process may use (cgroup quota, else affinity); value = the "
+                          "sweep point at threads = cores")
     if os.path.exists(O.REF_BENCH_BIN):
-        avail = info["cpus_available"] or 1
-        counts = [threads] if threads else sorted({min(t, avail) for t in CPU_SWEEP})
+        counts = cpu_sweep_points(cores, threads)
         sweep, retries, stall_s = [], 0, 0.0
         for n in counts:
             print(f"cpu baseline: reference tiled_sched, {n} threads ...", file=sys.stderr, flush=True)
@@ -159,7 +175,7 @@ def cpu_baseline(scene, kernel, threads=None):
             for attempt in range(2):
                 t0 = time.perf_counter()
                 try:
-                    r = O.ref_bench(scene, n, 3, 1920, 1080, samples, timeout=CPU_ATTEMPT_TIMEOUT_S)
+                    r = O.ref_bench(scene, n, CPU_FRAMES, 1920, 1080, samples, timeout=CPU_ATTEMPT_TIMEOUT_S)
                 except subprocess.TimeoutExpired:
                     lost = time.perf_counter() - t0
                     print(f"cpu baseline: {n} threads stalled ({lost:.0f} s, tiled_sched lost wake-up)",
@@ -168,8 +184,14 @@ def cpu_baseline(scene, kernel, threads=None):
                     if attempt == 0:
                         point["retries"] += 1
                     continue
+                rpf = r["rays_per_frame"]
                 point["value"] = round(r["mrays_per_s"], 3)
-                point["rays_per_frame"] = r["rays_per_frame"]
+                point["rays_per_frame"] = rpf
+                if r.get("min_s"):
+                    # frame-rate spread of the point: slowest and fastest of its timed frames
+                    point["min"] = round(rpf / r["max_s"] / 1e6, 3)
+                    point["max"] = round(rpf / r["min_s"] / 1e6, 3)
+                    point["spread"] = round((r["max_s"] - r["min_s"]) / r["median_s"], 4)
                 break
             retries += point["retries"]
             stall_s += point["stall_s"]
@@ -177,13 +199,14 @@ def cpu_baseline(scene, kernel, threads=None):
         done = [p for p in sweep if p["value"] is not None]
         if not done:
             raise RuntimeError(f"every reference run stalled: {sweep}")
-        best = max(done, key=lambda p: p["value"])
-        return {"value": best["value"], "unit": "Mrays/s", "cores": usable_cpus(info), "threads": best["threads"],
+        at = next((p for p in done if p["threads"] == (threads or cores)), None) or max(done, key=lambda p: p["threads"])
+        return {"value": at["value"], "unit": "Mrays/s", "cores": cores, "threads": at["threads"],
                 "kind": "reference",
                 "sample": f"{scene} 1920x1080, {samples} AO spp, tiled_sched<basic_ray<simd::float4>> -O3 -msse4.1, "
-                          f"best of a worker-thread sweep {counts}, each the median of 3 frames after 1 warm-up "
-                          f"({best['rays_per_frame']} rays/frame)",
-                "sweep": sweep, "retries": retries, "stall_s": round(stall_s, 1), **info}
+                          f"{at['threads']} worker threads, the median of {CPU_FRAMES} frames after 1 warm-up "
+                          f"({at['rays_per_frame']} rays/frame); sweep {counts} beside it",
+                "sweep": sweep, "best_of_sweep": max(p["value"] for p in done),
+                "retries": retries, "stall_s": round(stall_s, 1), **info}
     # fallback: the plain-C restatement (scalar, OpenMP rows) on 1/8 of the image rows
     threads = threads or min(16, info["cpus_available"] or 1)
     sc = O.make_scene(scene)
@@ -275,8 +298,101 @@ def load_json(path):
         return None
 
 
+LAUNCH_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+
+
+def launch_plan(gpus, env, device_count):
+    """What this process does for --gpus `gpus` under environment `env` on a node with `device_count`
+    GPUs (counted without initialising the GPU): ("run", None) -- this process is one rank (N = 1, or a
+    rank started by torch.distributed.run / by this launcher); ("spawn", [env of rank 0..N-1]) -- no
+    launcher ran: start the N ranks as child processes (nothing here has touched the GPU); or ("error",
+    message) -- a run that would measure something other than N GPUs (more ranks than GPUs, WORLD_SIZE
+    and --gpus disagreeing), which must never print a line."""
+    if gpus < 1:
+        return "error", f"--gpus {gpus}: at least one GPU"
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            return "error", (f"WORLD_SIZE={world} but --gpus {gpus}: the line would report {world} GPUs for a "
+                             f"{gpus}-GPU run; launch with --nproc-per-node {gpus}")
+        local = int(env.get("LOCAL_RANK", env.get("RANK", "0")))
+        if world > 1 and local >= device_count:
+            return "error", (f"rank with LOCAL_RANK={local} of {world} ranks, but this node has {device_count} "
+                             f"GPU(s): one process per GPU is required (ranks may not share a GPU)")
+        return "run", None
+    if gpus == 1:
+        return "run", None
+    if device_count < gpus:
+        return "error", (f"--gpus {gpus}, but this node has {device_count} GPU(s): refusing to measure fewer "
+                         f"GPUs than asked (one process per GPU)")
+    port = int(env.get("MASTER_PORT", "0")) or free_port()
+    envs = []
+    for r in range(gpus):
+        e = dict(env)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(gpus), "LOCAL_WORLD_SIZE": str(gpus),
+                  "MASTER_ADDR": env.get("MASTER_ADDR", "127.0.0.1"), "MASTER_PORT": str(port)})
+        envs.append(e)
+    return "spawn", envs
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(envs, argv, grace_s=None):
+    """Start one child process per rank (this process never touches the GPU and does not exec), rank 0's
+    stdout (the JSON line) passed through; the others' stdout goes to stderr.  When a rank fails, the
+    rest end through their group deadlines (GROUP_TIMEOUT_MS); whatever still runs `grace_s` later is
+    killed by its own process group.  Returns the first non-zero exit status (0 when every rank passed)."""
+    import signal
+    grace_s = grace_s if grace_s is not None else 3 * GROUP_TIMEOUT_MS / 1e3 + 30
+    procs = []
+    for r, e in enumerate(envs):
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv, env=e,
+                                      stdout=None if r == 0 else sys.stderr.fileno(), start_new_session=True))
+    first_bad, t_fail = 0, None
+    while True:
+        live = [p for p in procs if p.poll() is None]
+        for p in procs:
+            if p.returncode not in (None, 0) and not first_bad:
+                first_bad, t_fail = p.returncode, time.monotonic()
+                print(f"bench launcher: rank {procs.index(p)} exited with {p.returncode}; waiting up to "
+                      f"{grace_s:.0f} s for the other ranks", file=sys.stderr, flush=True)
+        if not live:
+            break
+        if t_fail is not None and time.monotonic() - t_fail > grace_s:
+            for p in live:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except OSError:
+                    pass
+            for p in live:
+                p.wait()
+            break
+        time.sleep(0.05)
+    return first_bad if first_bad else (1 if any(p.returncode for p in procs) else 0)
+
+
+def device_count():
+    """GPUs of this node without initialising the GPU (torch.cuda.device_count does not, on this image)."""
+    import torch
+    return torch.cuda.device_count()
+
+
 def main():
     args = parse()
+    action, info = launch_plan(args.gpus, os.environ, device_count() if args.gpus > 1 or
+                               int(os.environ.get("WORLD_SIZE", "1")) > 1 else 1)
+    if action == "error":
+        print(f"bench.py: error: {info}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if action == "spawn":
+        print(f"bench launcher: starting {len(info)} ranks (no WORLD_SIZE in the environment)", file=sys.stderr,
+              flush=True)
+        sys.exit(spawn_ranks(info, sys.argv[1:]))
     # the JSON line is the only thing on stdout: native libraries (RCCL prints a version banner at
     # communicator init) write to fd 1 directly, so fd 1 becomes stderr and the line goes to a dup
     json_out = os.fdopen(os.dup(1), "w")
@@ -285,8 +401,6 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}; using WORLD_SIZE", file=sys.stderr)
 
     # torch first: its HIP runtime (and RCCL) is then the one libvrh.so binds to (one per process)
     import numpy as np
@@ -296,8 +410,6 @@ def main():
     import visionaray_amd as va
     from visionaray_amd import _capi, scenes
 
-    ndev = torch.cuda.device_count()
-    local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     if world > 1:
         import datetime

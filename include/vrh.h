@@ -223,7 +223,7 @@ VRH_API int vrh_ctx_get_stream(const vrh_ctx* ctx, int* hip_device, void** hip_s
 /* launch tuning (per context; 0 = automatic).  Results never depend on these. */
 enum vrh_option {
     VRH_OPT_BLOCK_THREADS = 1,   /* threads per block, a multiple of 64 up to 256 (auto: 64)       */
-    VRH_OPT_STACK_CAP = 2,       /* traversal stack entries per lane kept in LDS; entries beyond
+    VRH_OPT_STACK_CAP = 2,       /* traversal stack entries per lane kept in LDS (1..640); entries beyond
                                     them (up to the BVH depth) go to a global overflow block, so
                                     any value is exact.  Primary / AO step loops at their default
                                     register budgets only; other kernels keep the whole stack in
@@ -237,10 +237,13 @@ enum vrh_option {
                                     loop (4, the old sphere default: 6-9 % slower than the step loop,
                                     profiles/r02_ab/ab18_sphere_schedule.log); 4 returns
                                     VRH_ERR_UNSUPPORTED                                             */
-    VRH_OPT_BLOCKS_PER_CU = 4,   /* resident blocks per CU for the persistent grid (auto: max)     */
-    VRH_OPT_WAVES_PER_SIMD = 5,  /* register budget of the unified kernel: 1 (none), 5, 6 or 8 (auto: AO 6
-                                    for BVHs at most 20 deep, else 5; primary visibility 8 for
-                                    triangles, 6 for spheres; shading kernels 1, whitted 5)      */
+    VRH_OPT_BLOCKS_PER_CU = 4,   /* resident blocks per CU for the persistent grid, 1..32 (auto: max) */
+    VRH_OPT_WAVES_PER_SIMD = 5,  /* register budget of the unified kernel: 1 (none), 5, 6 or 8 (auto:
+                                    AO 6, 5 for test-counting launches and with AO tail sharing;
+                                    primary visibility 8 for triangles and for sphere launches of
+                                    several frames, 6 for one-frame sphere launches and counting;
+                                    pixel-sampler passes and BVH lists AO 5 / primary 6; shading
+                                    kernels 1, whitted 5)                                          */
     VRH_OPT_EXACT_MINMAX = 6,    /* 1 = always use the ternary min/max slab test (auto: hardware
                                     min/max where provably identical, see vrh_device.h)           */
     VRH_OPT_XCD_QUEUES = 7,      /* tile queues: 1 = one per XCD (image strips) with stealing,
@@ -305,6 +308,9 @@ enum vrh_option {
                                     128-B line; 2 = the builder's order (auto: 2; 1 measured
                                     neutral)                                                      */
 };
+/* every value is checked against its option's range (the comments above) before it is narrowed:
+ * out of range -> VRH_ERR_INVALID, a removed setting -> VRH_ERR_UNSUPPORTED, unknown option ->
+ * VRH_ERR_INVALID */
 VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value);
 
 /* scene upload: copies the host arrays (reference layouts) into device memory the scene owns.

@@ -742,9 +742,9 @@ static int run_bench(scene_desc const& d, aligned_vector<P>& prims, std::vector<
     double med = times[times.size() / 2];
     printf("{\"kind\":\"reference\",\"path\":\"tiled_sched<basic_ray<simd::float4>> -O3 -msse4.1\",\"scene\":\"%s\","
            "\"W\":%d,\"H\":%d,\"samples\":%d,\"threads\":%d,\"frames\":%d,\"rays_per_frame\":%llu,"
-           "\"median_s\":%.6f,\"mrays_per_s\":%.3f}\n",
+           "\"median_s\":%.6f,\"min_s\":%.6f,\"max_s\":%.6f,\"mrays_per_s\":%.3f}\n",
            d.name.c_str(), W, H, samples, threads, frames, (unsigned long long)rays_per_frame, med,
-           rays_per_frame / med / 1e6);
+           times.front(), times.back(), rays_per_frame / med / 1e6);
     return 0;
 }
 

@@ -157,6 +157,37 @@ def test_option_values_out_of_range_rejected(ctx):
     ctx.set_option("refill_min", 0)
 
 
+# every option with its accepted range (vrh_runtime.hip k_option_ranges) and the values inside it that
+# are refused as removed / unsupported
+OPTION_RANGES = {
+    "block_threads": (0, 256), "stack_cap": (0, 640), "blocks_per_cu": (0, 32), "refill_min": (0, 64),
+    "descent_cap": (0, 1024), "cluster_tiles": (0, 1024), "wide_anyhit": (0, 2), "pop_on_miss": (0, 2),
+    "scalar_fetch": (0, 2), "pair_layout": (0, 2), "ao_gate": (0, 2), "ao_share": (0, 2), "ao_cut": (0, 3),
+    "xcd_queues": (0, 4), "wave_times": (0, 2), "exact_minmax": (0, 1), "async_frames": (0, 1),
+    "waves_per_simd": (0, 8), "ao_schedule": (0, 4), "coop_fetch": (0, 2), "quad_refill": (0, 1),
+    "group_units": (0, 1), _capi.VRH_OPT_AO_STEAL: (0, 2),
+}
+
+
+@pytest.mark.parametrize("opt", list(OPTION_RANGES), ids=str)
+def test_every_option_range_checked(ctx, opt):
+    """Each vrh_ctx_set_option value is checked against its option's own range on the int64 before it
+    is narrowed: negatives (-1, INT32_MIN, INT64_MIN), one below and one above the range and 2^32 (which
+    would wrap to 0) are VRH_ERR_INVALID; both edges of the range are accepted (or refused as
+    removed / not a valid setting -- never wrapped)."""
+    lo, hi = OPTION_RANGES[opt]
+    for bad in {-1, -2**31, -2**63, lo - 1, hi + 1, 2**32, 2**31}:
+        with pytest.raises(_capi.VrhError) as e:
+            ctx.set_option(opt, bad)
+        assert e.value.code == _capi.VRH_ERR_INVALID, (opt, bad)
+    for edge in (lo, hi):
+        try:
+            ctx.set_option(opt, edge)
+        except _capi.VrhError as e:          # e.g. waves_per_simd 8 is fine, ao_schedule 4 was removed
+            assert e.code in (_capi.VRH_ERR_UNSUPPORTED, _capi.VRH_ERR_INVALID), (opt, edge)
+    ctx.set_option(opt, 0)                   # back to automatic
+
+
 def test_block_threads_above_launch_bounds_rejected(ctx):
     """The traversal kernels are compiled for <= 256 threads per block; a larger block is refused at
     vrh_ctx_set_option instead of failing the launch."""

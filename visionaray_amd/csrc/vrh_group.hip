@@ -96,12 +96,14 @@ int fail_group(vrh_group* g, int code, const std::string& msg)
     return code;
 }
 
-// poll between checks: spin for the first 20 ms (a finished exchange is seen within microseconds,
-// vrh_group_sync ends bench's timed region), then sleep 1 ms per check
+// poll between checks: yield (no sleep) for the first 2 s, so a finished exchange is seen within
+// microseconds whatever the launch length (vrh_group_sync ends bench's timed region; a grouped C4
+// launch is ~20-40 ms); past 2 s -- a slow or dead peer, not a timed wait -- sleep 50 us per check,
+// an overshoot under 0.01 % of the wait
 void poll_pause(steady::time_point t0)
 {
-    if (steady::now() - t0 < std::chrono::milliseconds(20)) std::this_thread::yield();
-    else std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    if (steady::now() - t0 < std::chrono::seconds(2)) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(50));
 }
 
 // the communicator's state until nothing is in progress (a non-blocking init, or the enqueue of a
@@ -142,7 +144,8 @@ int wait_streams(vrh_group* g, bool ctx_too, const char* what)
             if (!s) continue;
             const hipError_t e = hipStreamQuery(s);
             if (e == hipErrorNotReady) busy = true;
-            else if (e != hipSuccess) { set_error(std::string(what) + ": " + hipGetErrorString(e)); return VRH_ERR_HIP; }
+            else if (e != hipSuccess)      // a device error: the group's exchanges cannot complete
+                return fail_group(g, VRH_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
         }
         if (!busy) return VRH_OK;
         if (g->comm)

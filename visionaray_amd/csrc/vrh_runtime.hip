@@ -152,56 +152,88 @@ VRH_API int vrh_ctx_destroy(vrh_ctx* ctx)
     return VRH_OK;
 }
 
+// the accepted range of every option (0 = automatic wherever a range starts at 0); checked on the
+// int64 value before it is narrowed, so a negative or huge value is refused, never wrapped
+struct option_range { uint32_t option; int64_t lo, hi; const char* what; };
+constexpr option_range k_option_ranges[] = {
+    { VRH_OPT_BLOCK_THREADS, 0, 256, "block threads is 0 (auto) or a multiple of 64 up to 256" },
+    { VRH_OPT_STACK_CAP, 0, 640, "stack cap is 0 (auto) or 1..640 LDS entries per lane" },
+    { VRH_OPT_AO_SCHEDULE, 0, 4, "schedule is 0 (auto) or 3 (step loop)" },
+    { VRH_OPT_BLOCKS_PER_CU, 0, 32, "blocks per CU is 0 (auto) or 1..32" },
+    { VRH_OPT_WAVES_PER_SIMD, 0, 8, "waves per SIMD is 0 (auto), 1, 5, 6 or 8" },
+    { VRH_OPT_EXACT_MINMAX, 0, 1, "exact min/max is 0 (auto) or 1 (on)" },
+    { VRH_OPT_XCD_QUEUES, 0, 4, "xcd queues is 0 (auto), 1 (strips), 2 (off), 3 (band-interleaved) or 4 (cluster order)" },
+    { VRH_OPT_REFILL_MIN, 0, 64, "refill threshold is 0 (auto) or 1..64" },
+    { VRH_OPT_WIDE_ANYHIT, 0, 2, "wide any-hit is 0 (auto), 1 (on) or 2 (off)" },
+    { VRH_OPT_DESCENT_CAP, 0, 1024, "descent cap is 0 (auto) or 1..1024" },
+    { VRH_OPT_POP_ON_MISS, 0, 2, "pop on miss is 0 (auto), 1 (on) or 2 (off)" },
+    { VRH_OPT_COOP_FETCH, 0, 2, "cooperative fetch was removed (0 / 2 = off is accepted)" },
+    { VRH_OPT_SCALAR_FETCH, 0, 2, "scalar fetch is 0 (auto), 1 (on) or 2 (off)" },
+    { VRH_OPT_PAIR_LAYOUT, 0, 2, "pair layout is 0 (auto), 1 (line pairing) or 2 (builder order)" },
+    { VRH_OPT_AO_GATE, 0, 2, "AO gate is 0 (auto), 1 (on) or 2 (off)" },
+    { VRH_OPT_WAVE_TIMES, 0, 2, "wave times is 0 (off), 1 (on) or 2 (on + tile times of counting one-frame AO launches)" },
+    { VRH_OPT_AO_CUT, 0, 3, "AO cut is 0 (auto), 1 (on, entries nearest-first), 2 (off) or 3 (on, entries in cut order)" },
+    { VRH_OPT_AO_STEAL, 0, 2, "AO tail stash was removed (0 / 2 = off is accepted)" },
+    { VRH_OPT_AO_SHARE, 0, 2, "AO tail sharing is 0 (auto), 1 (on) or 2 (off)" },
+    { VRH_OPT_CLUSTER_TILES, 0, 1024, "cluster tiles is 0 (auto) or 1..1024" },
+    { VRH_OPT_QUAD_REFILL, 0, 1, "the quad-coherent hand-out was removed (0 is accepted)" },
+    { VRH_OPT_GROUP_UNITS, 0, 1, "the block-shared hand-out was removed (0 is accepted)" },
+    { VRH_OPT_ASYNC_FRAMES, 0, 1, "asynchronous frames is 1 (on) or 0 (off)" },
+};
+
 VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
 {
     VRH_CHECK(ctx, "vrh_ctx_set_option: null");
-    VRH_CHECK(value >= 0 && value <= 1024, "vrh_ctx_set_option: value out of range");
+    const option_range* range = nullptr;
+    for (const option_range& r : k_option_ranges)
+        if (r.option == option) range = &r;
+    if (!range) { set_error("vrh_ctx_set_option: unknown option"); return VRH_ERR_INVALID; }
+    VRH_CHECK(value >= range->lo && value <= range->hi,
+              std::string("vrh_ctx_set_option: value ") + std::to_string(value) + " out of range: " + range->what);
+    const int v = int(value);
     switch (option)
     {
     case VRH_OPT_BLOCK_THREADS:
         // the traversal kernels are compiled for at most 256 threads per block (__launch_bounds__(256, ...)):
         // a larger block would break the register allocation's assumptions (a launch failure)
-        VRH_CHECK(value % 64 == 0 && value <= 256, "vrh_ctx_set_option: block threads must be a multiple of 64, at most 256");
-        ctx->opt_block = int(value); break;
-    case VRH_OPT_STACK_CAP: ctx->opt_stack = int(value); break;
+        VRH_CHECK(v % 64 == 0, std::string("vrh_ctx_set_option: ") + range->what);
+        ctx->opt_block = v; break;
+    case VRH_OPT_STACK_CAP: ctx->opt_stack = v; break;
     case VRH_OPT_AO_SCHEDULE:
         // the item loop (4) was removed in round 2: the step loop measured faster for every kernel
-        if (value == 4) { set_error("vrh_ctx_set_option: the item-loop schedule was removed (the step loop is faster, profiles/r02_ab/ab18_sphere_schedule.log)"); return VRH_ERR_UNSUPPORTED; }
-        VRH_CHECK(value == 0 || value == 3, "vrh_ctx_set_option: schedule is 3 (step loop)"); ctx->opt_sched = int(value); break;
-    case VRH_OPT_WIDE_ANYHIT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: wide any-hit is 1 (on) or 2 (off)"); ctx->opt_wide = int(value); break;
-    case VRH_OPT_DESCENT_CAP: ctx->opt_dcap = int(value); break;
+        if (v == 4) { set_error("vrh_ctx_set_option: the item-loop schedule was removed (the step loop is faster, profiles/r02_ab/ab18_sphere_schedule.log)"); return VRH_ERR_UNSUPPORTED; }
+        VRH_CHECK(v == 0 || v == 3, std::string("vrh_ctx_set_option: ") + range->what); ctx->opt_sched = v; break;
+    case VRH_OPT_WIDE_ANYHIT: ctx->opt_wide = v; break;
+    case VRH_OPT_DESCENT_CAP: ctx->opt_dcap = v; break;
     case VRH_OPT_COOP_FETCH:
         // the cooperative quad fetch was removed in round 2 (measured slower, profiles/r01/ab_nocoop.log)
-        VRH_CHECK(value == 0 || value == 2, "vrh_ctx_set_option: cooperative fetch was removed (2 = off is accepted)");
-        if (value == 1) return VRH_ERR_UNSUPPORTED;
+        if (v == 1) { set_error("vrh_ctx_set_option: the cooperative fetch was removed (it measured slower)"); return VRH_ERR_UNSUPPORTED; }
         break;
-    case VRH_OPT_WAVE_TIMES: VRH_CHECK(value <= 2, "vrh_ctx_set_option: wave times is 1 (on), 2 (on + tile times of counting one-frame AO launches) or 0 (off)"); ctx->opt_wave_times = int(value); break;
-    case VRH_OPT_AO_CUT: VRH_CHECK(value <= 3, "vrh_ctx_set_option: AO cut is 1 (on, entries nearest-first), 2 (off) or 3 (on, entries in cut order)"); ctx->opt_cut = int(value); break;
+    case VRH_OPT_WAVE_TIMES: ctx->opt_wave_times = v; break;
+    case VRH_OPT_AO_CUT: ctx->opt_cut = v; break;
     case VRH_OPT_AO_STEAL:
         // the AO tail stash was removed in round 3 (measured slower)
-        if (value == 1) { set_error("vrh_ctx_set_option: the AO tail stash was removed (it measured slower)"); return VRH_ERR_UNSUPPORTED; }
-        return VRH_OK;
-    case VRH_OPT_AO_SHARE: VRH_CHECK(value <= 2, "vrh_ctx_set_option: AO tail sharing is 1 (on) or 2 (off)"); ctx->opt_share = int(value); break;
-    case VRH_OPT_AO_GATE: VRH_CHECK(value <= 2, "vrh_ctx_set_option: AO gate is 1 (on) or 2 (off)"); ctx->opt_gate = int(value); break;
-    case VRH_OPT_POP_ON_MISS: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pop on miss is 1 (on) or 2 (off)"); ctx->opt_pop = int(value); break;
-    case VRH_OPT_PAIR_LAYOUT: VRH_CHECK(value <= 2, "vrh_ctx_set_option: pair layout is 1 (line pairing) or 2 (builder order)"); ctx->opt_layout = int(value); break;
-    case VRH_OPT_SCALAR_FETCH: VRH_CHECK(value <= 2, "vrh_ctx_set_option: scalar fetch is 1 (on) or 2 (off)"); ctx->opt_scalar = int(value); break;
-    case VRH_OPT_REFILL_MIN: VRH_CHECK(value <= 64, "vrh_ctx_set_option: refill threshold is 1..64"); ctx->opt_refill = int(value); break;
-    case VRH_OPT_BLOCKS_PER_CU: ctx->opt_bpc = int(value); break;
-    case VRH_OPT_WAVES_PER_SIMD: VRH_CHECK(value == 0 || value == 1 || value == 5 || value == 6 || value == 8, "vrh_ctx_set_option: waves per SIMD is 1, 5, 6 or 8"); ctx->opt_occ = int(value); break;
-    case VRH_OPT_EXACT_MINMAX: ctx->opt_exact_minmax = value ? 1 : 0; break;
-    case VRH_OPT_XCD_QUEUES: VRH_CHECK(value <= 4, "vrh_ctx_set_option: xcd queues is 1 (strips), 2 (off), 3 (band-interleaved) or 4 (cluster order)"); ctx->opt_xcd_queues = int(value); break;
+        if (v == 1) { set_error("vrh_ctx_set_option: the AO tail stash was removed (it measured slower)"); return VRH_ERR_UNSUPPORTED; }
+        break;
+    case VRH_OPT_AO_SHARE: ctx->opt_share = v; break;
+    case VRH_OPT_AO_GATE: ctx->opt_gate = v; break;
+    case VRH_OPT_POP_ON_MISS: ctx->opt_pop = v; break;
+    case VRH_OPT_PAIR_LAYOUT: ctx->opt_layout = v; break;
+    case VRH_OPT_SCALAR_FETCH: ctx->opt_scalar = v; break;
+    case VRH_OPT_REFILL_MIN: ctx->opt_refill = v; break;
+    case VRH_OPT_BLOCKS_PER_CU: ctx->opt_bpc = v; break;
+    case VRH_OPT_WAVES_PER_SIMD:
+        VRH_CHECK(v == 0 || v == 1 || v == 5 || v == 6 || v == 8, std::string("vrh_ctx_set_option: ") + range->what);
+        ctx->opt_occ = v; break;
+    case VRH_OPT_EXACT_MINMAX: ctx->opt_exact_minmax = v; break;
+    case VRH_OPT_XCD_QUEUES: ctx->opt_xcd_queues = v; break;
     case VRH_OPT_GROUP_UNITS:
     case VRH_OPT_QUAD_REFILL:
         // measured in round 4 and removed (slower: profiles/r04/ab/lane_layout/); 0 is accepted
-        if (value != 0) { set_error("vrh_ctx_set_option: the quad-coherent and block-shared hand-outs were removed (they measured slower)"); return VRH_ERR_UNSUPPORTED; }
-        return VRH_OK;
-    case VRH_OPT_ASYNC_FRAMES: VRH_CHECK(value == 0 || value == 1, "vrh_ctx_set_option: asynchronous frames is 1 (on) or 0 (off)"); ctx->opt_async = int(value); break;
-    case VRH_OPT_CLUSTER_TILES:
-        // stored as the kernel's uint32 cluster size: a negative value would wrap (cluster x frames can
-        // become 0, a division by zero in the hand-out), so the range is checked here as well
-        VRH_CHECK(value >= 0 && value <= 1024, "vrh_ctx_set_option: cluster tiles is 1..1024 (0 = auto)");
-        ctx->opt_cluster = int(value); break;
+        if (v != 0) { set_error("vrh_ctx_set_option: the quad-coherent and block-shared hand-outs were removed (they measured slower)"); return VRH_ERR_UNSUPPORTED; }
+        break;
+    case VRH_OPT_ASYNC_FRAMES: ctx->opt_async = v; break;
+    case VRH_OPT_CLUSTER_TILES: ctx->opt_cluster = v; break;
     default: set_error("vrh_ctx_set_option: unknown option"); return VRH_ERR_INVALID;
     }
     return VRH_OK;
