@@ -704,6 +704,16 @@ def main():
                 pmc_info = {"l1_requests_per_launch": pmc["l1_requests_per_launch"],
                             "td_busy_frac": round(pmc["td_busy_frac"], 4),
                             "source": f"profiles/{pmc_name}: " + pmc.get("command", "")}
+                # the load-count model: time follows the wave-level vector loads at a
+                # near-constant TD cost per load -- SQ_INSTS_VMEM_RD per ray and TD busy cycles per load
+                cpl = pmc.get("counters_per_launch") or {}
+                if cpl.get("SQ_INSTS_VMEM_RD") and cpl.get("TD_TD_BUSY_sum"):
+                    loads = cpl["SQ_INSTS_VMEM_RD"]
+                    pmc_info["wave_loads_per_launch"] = round(loads)
+                    pmc_info["wave_loads_per_frame"] = round(loads / F)
+                    pmc_info["wave_loads_per_ray"] = round(loads / rays_launch, 4)
+                    pmc_info["td_cycles_per_load"] = round(cpl["TD_TD_BUSY_sum"] / loads, 3)
+                    pmc_info["l1_requests_per_load"] = round(pmc["l1_requests_per_launch"] / loads, 3)
         # achieved: the hardware-counted L1 requests (TCP_TOTAL_CACHE_ACCESSES) of a committed PMC pass
         # of this exact configuration, over the live hipEvent time; without one it is not reported
         achieved = (pmc_info["l1_requests_per_launch"] * L1_REQ_BYTES / (k_ms_mean * 1e-3) / 1e9) if pmc_info else None

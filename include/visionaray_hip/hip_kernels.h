@@ -54,6 +54,7 @@
 #include "detail/vrh_libm.h"
 
 #include <array>
+#include <atomic>
 #include <cassert>
 #include <cfloat>
 #include <cstring>
@@ -67,6 +68,9 @@
 // 16 KB of LDS, which held a CU to 10 resident waves (2.5 per SIMD) -- 32 lets the registers bound
 // it (4 waves per SIMD for the AO kernel)
 #define VRH_USER_STACK 32
+#endif
+#ifndef VRH_USER_DEFER
+#define VRH_USER_DEFER 0          // deferred any_hit calls (below), opt-in
 #endif
 
 namespace visionaray
@@ -336,15 +340,76 @@ VRH_FUNC inline vector<3, T> cosine_sample_hemisphere(T u1, T u2)
 
 namespace hip_detail
 {
+// The BVH arrays a user kernel walks are reached through pointers it reads from device memory (the
+// hip_bvh_ref range): the compiler cannot tell their address space and emits FLAT loads, which count
+// against both vmcnt and lgkmcnt -- every wait for an LDS stack pop then also waits for the record
+// fetches in flight, and a triangle's 48 B came out as five loads around one such wait.  They are
+// global memory (vrh_scene_view, hipMalloc), so the fetches below say so: global_load_dwordx4.
+#ifndef VRH_USER_GLOBAL_LOADS
+#define VRH_USER_GLOBAL_LOADS 1
+#endif
+// (component by component: a whole-struct copy binds the global lvalue to float4's copy constructor,
+// a generic reference, and the load is FLAT again)
+typedef __attribute__((address_space(1))) const float4 global_float4;
+typedef __attribute__((address_space(1))) const float2 global_float2;
+__device__ __forceinline__ float4 gld4(const float4* p)
+{
+#if VRH_USER_GLOBAL_LOADS && defined(__HIP_DEVICE_COMPILE__)
+    global_float4* g = (global_float4*)p;
+    return make_float4(g->x, g->y, g->z, g->w);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ float2 gld2(const float2* p)
+{
+#if VRH_USER_GLOBAL_LOADS && defined(__HIP_DEVICE_COMPILE__)
+    global_float2* g = (global_float2*)p;
+    return make_float2(g->x, g->y);
+#else
+    return *p;
+#endif
+}
+
+// A BVH ref's view (vrh_scene_view, 72 B) is read at every closest_hit / any_hit call.  The ref lives
+// in device memory the kernel never writes (a bvh_ref array, ao/main.cpp:171-178), at an address
+// every lane of the wave shares: read it then through the scalar cache (s_load) instead of one
+// vector load per field and call.  A ref in private or LDS memory (a local copy) is read as usual.
+__device__ inline vrh_scene_view uniform_view(vrh_scene_view const& v)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint64_t a = reinterpret_cast<uint64_t>(&v);
+    const uint64_t af = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(a)))))
+                      | (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(a >> 32))))) << 32);
+    const void* pf = reinterpret_cast<const void*>(af);
+    if (__ballot(a != af) == 0ull && (af & 3u) == 0u && !__builtin_amdgcn_is_private(pf) && !__builtin_amdgcn_is_shared(pf))
+    {
+        typedef const __attribute__((address_space(4))) uint32_t cword;
+        cword* cw = (cword*)(pf);
+        vrh_scene_view r;
+        uint32_t* w = reinterpret_cast<uint32_t*>(&r);
+#pragma unroll
+        for (uint32_t k = 0; k < uint32_t(sizeof(vrh_scene_view) / 4u); ++k) w[k] = cw[k];
+        return r;
+    }
+#endif
+    return v;
+}
+
 // the leaf primitive i of the device layout, rebuilt as a primitive object of type P (the
 // reference's basic_triangle<3,float> / basic_sphere<float>, or standalone.h's of the same layout)
 template <typename P>
-__device__ inline P leaf_primitive(const float4* prims, uint32_t i, uint32_t& flags)
+__host__ __device__ inline P leaf_primitive(const float4* prims, uint32_t i, uint32_t& flags)
 {
     P p;
+#if defined(__HIP_DEVICE_COMPILE__)
+    auto ld = [](const float4* q) { return gld4(q); };
+#else
+    auto ld = [](const float4* q) { return *q; };
+#endif
     if constexpr (is_sphere<P>::value)
     {
-        const float4 a = prims[2u * i], b = prims[2u * i + 1u];
+        const float4 a = ld(prims + 2u * i), b = ld(prims + 2u * i + 1u);
         p.center = decltype(p.center)(a.x, a.y, a.z);
         p.radius = a.w;
         p.prim_id = __float_as_uint(b.x);
@@ -353,7 +418,14 @@ __device__ inline P leaf_primitive(const float4* prims, uint32_t i, uint32_t& fl
     }
     else
     {
-        const float4 a = prims[3u * i], b = prims[3u * i + 1u], c = prims[3u * i + 2u];
+        const float4 a = ld(prims + 3u * i), b = ld(prims + 3u * i + 1u), c = ld(prims + 3u * i + 2u);
+#if defined(__HIP_DEVICE_COMPILE__)
+        // the third 16 B as ONE load: its fields are read at different places (e2.z and the flags by the
+        // test, prim / geom ids only for a hit), and the compiler would otherwise split it into a dword
+        // load now and another after the test -- a per-lane gather costs the TD about the same for 4 B
+        // as for 16 B (profiles/l1_roof.json)
+        asm volatile("" :: "v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w));
+#endif
         p.v1 = decltype(p.v1)(a.x, a.y, a.z);
         p.e1 = decltype(p.e1)(a.w, b.x, b.y);
         p.e2 = decltype(p.e2)(b.z, b.w, c.x);
@@ -397,8 +469,8 @@ __device__ inline void fetch_pair(const float4* pairs, uint32_t link, float4& q0
     else
     {
         const float4* p = pairs + 4u * link;
-        q0 = p[0]; q1 = p[1]; q2 = p[2];
-        q3 = *reinterpret_cast<const float2*>(p + 3);
+        q0 = gld4(p); q1 = gld4(p + 1); q2 = gld4(p + 2);
+        q3 = gld2(reinterpret_cast<const float2*>(p + 3));
     }
 }
 
@@ -415,7 +487,7 @@ __device__ inline void fetch_quad(const float4* quads, uint32_t link, float4 (&q
     {
         const float4* p = quads + 8u * link;
 #pragma unroll
-        for (int k = 0; k < 7; ++k) q[k] = p[k];
+        for (int k = 0; k < 7; ++k) q[k] = gld4(p + k);
     }
 }
 
@@ -942,6 +1014,201 @@ __device__ inline void walk_shared(vrh_scene_view const& b, vrh::dev::ray_t cons
     }
 }
 
+// ---- ordered cooperative any_hit (VRH_USER_ANYHIT_ORDERED, the default) --------------------------
+// A user kernel calls any_hit from one lane per pixel; each call runs until its slowest lane is done.
+// Here the lanes that entered the call together share the work AND keep the reference's answer: the
+// record of the FIRST accepted primitive in the ray's own depth-first order (near child first, ties to
+// child 1, leaf primitives in index order; intersect.inl:66-130 with exit_traversal<AnyHit>).
+//   * Every place in a ray's walk has a key: the bits of the branches taken at the pairs where both
+//     children were hit (0 = the near child, 1 = the far one), MSB first, with an end marker.  Keys of
+//     disjoint subtrees compare as integers in the order the walk visits them.
+//   * A lane whose ray is done (or that never had one) takes the BOTTOM entry of a lane holding two or
+//     more -- or one, while that lane is inside a descent -- with the donor's ray and the entry's key:
+//     the bottom entry is the last work of that segment of the walk, so every segment stays a
+//     contiguous stretch of the ray's order.
+//   * Before an any-hit ray's first accepted primitive its box tests compare against constants (max_t),
+//     so the leaves a segment reaches and the order it reaches them in do not depend on who walks it.
+//   * A lane that accepts a primitive records (key, primitive) for the ray (LDS atomicMin of the key in
+//     the owner's column) and ends its segment; a lane whose next work is later than the ray's best key
+//     drops it.  When no lane has work left, the smallest key is the reference's first hit.
+// The owner then rebuilds its record by testing that one primitive with its own ray and intersector
+// (the test every lane ran is the same arithmetic).  Default intersector and update rule, one BVH of
+// at most 2^25 primitives, depth <= VRH_USER_STACK - 4, one-wave blocks of user_render; otherwise the
+// walk above.  Descents are cut after OCA_VISITS pair visits per step so that work can move between
+// lanes.
+// Opt-in (VRH_USER_ANYHIT_ORDERED=1): exact (every any_hit record of the parity suite equals the
+// per-lane walk's), but SLOWER.  A schedule simulation of C3's AO calls (tools/sim/oca_sim.c, 3,200
+// calls of sampled tiles, scalar fetches of wave-uniform records modelled) puts its wave-level vector
+// loads at only 0.89 of the per-lane walk's with 4 visits per step (0.96 with whole descents; a
+// perfectly packed wave would need 0.57): the calls' tails have little left to share.  And its lane
+// state costs registers: the AO lambda needs 143 VGPRs (3 waves / SIMD) or spills 200 B at 5 waves, so
+// C3 ran 2.01 ms per frame against 1.75 (profiles/r06/oca/).
+#ifndef VRH_USER_ANYHIT_ORDERED
+#define VRH_USER_ANYHIT_ORDERED 0
+#endif
+#ifndef VRH_OCA_VISITS
+#define VRH_OCA_VISITS 4
+#endif
+constexpr uint32_t OCA_RING = VRH_USER_STACK - 2u;       // stack ring; the column's last two words: best key, prim
+constexpr uint32_t OCA_LVL_SHIFT = 25u;                  // entry = link | level << 25
+constexpr uint32_t OCA_LINK_MASK = vrh::dev::LEAF_BIT | ((1u << OCA_LVL_SHIFT) - 1u);
+constexpr uint32_t OCA_NOKEY = 0xFFFFFFFFu, OCA_NONE = 0xFFFFFFFFu, OCA_IDLE = 0xFFFFFFFFu;
+static_assert(VRH_USER_STACK >= 16u, "the ordered any_hit walk moves 14 words through a lane's stack column");
+
+// the key of `len` path bits (len <= 30): the bits left-aligned, then a one
+__device__ __forceinline__ uint32_t oca_key(uint32_t path, uint32_t len)
+{
+    return uint32_t((uint64_t(path) << (32u - len)) | (1ull << (31u - len)));
+}
+
+// every active lane calls with the same BVH, which the walk can take (wave-uniform answer)
+__device__ __forceinline__ bool oca_wave_usable(vrh_scene_view const& b)
+{
+    const uint64_t pa = reinterpret_cast<uint64_t>(b.pairs);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane(int(uint32_t(pa)));
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane(int(uint32_t(pa >> 32)));
+    const bool ok = VRH_USER_ANYHIT_ORDERED && b.max_depth + 4u <= VRH_USER_STACK && b.num_prims < (1u << OCA_LVL_SHIFT)
+                  && blockDim.x * blockDim.y * blockDim.z == 64u && pa == ((uint64_t(hi) << 32) | lo);
+    return __ballot(!ok) == 0ull;
+}
+
+// test(ray, max_t, i, flags) -> bool: primitive i accepted for that ray (the walk's own leaf test);
+// returns the leaf index of this lane's ray's first hit in the reference order, or OCA_NONE
+template <bool FAST, typename Test>
+__device__ inline uint32_t walk_ordered(vrh_scene_view const& b, vrh::dev::ray_t const& r0, float max_t0, Test&& test)
+{
+    using namespace vrh::dev;
+    extern __shared__ uint32_t vrh_user_smem[];
+    constexpr uint32_t N = 64u;                            // one-wave blocks (oca_usable)
+    const float4* pairs = static_cast<const float4*>(b.pairs);
+    const uint32_t lane = __lane_id();
+    uint32_t* col = vrh_user_smem + lane;                  // this lane's column: word k at col[k * N]
+    auto slot = [&](uint32_t k) -> uint32_t& { return col[(k % OCA_RING) * N]; };
+    col[OCA_RING * N] = OCA_NOKEY;                          // this lane's ray: best key, its primitive
+    col[(OCA_RING + 1u) * N] = OCA_NONE;
+    uint32_t task = lane;                                   // whose ray this lane walks (OCA_IDLE: none)
+    ray_t tr = r0;
+    float tmax = max_t0;
+    uint32_t path = 0u, plen = 0u;                          // key of the current place
+    uint32_t cur = b.root;                                  // node to continue from (OCA_NONE: pop)
+    uint32_t bot = 0u, top = 0u;                            // live ring entries [bot, top)
+    __builtin_amdgcn_wave_barrier();
+    for (;;)
+    {
+        // 1. work later in its ray's order than the ray's best hit is dropped; no work left: idle
+        if (task != OCA_IDLE)
+        {
+            uint32_t pos = OCA_NOKEY;
+            if (cur != OCA_NONE) pos = oca_key(path, plen);
+            else if (top != bot)
+            {
+                const uint32_t lv = (slot(top - 1u) >> OCA_LVL_SHIFT) & 31u;
+                pos = oca_key(((path >> (plen - lv)) << 1) | 1u, lv + 1u);
+            }
+            else task = OCA_IDLE;
+            if (task != OCA_IDLE && vrh_user_smem[task + OCA_RING * N] < pos) task = OCA_IDLE;
+        }
+        const uint64_t busy = __ballot(task != OCA_IDLE);
+        if (busy == 0ull) break;
+        // 2. idle lanes take bottom entries (k-th idle <- k-th donor), through the idle lane's column
+        const uint64_t idle = __ballot(task == OCA_IDLE);
+        const uint64_t donors = __ballot(task != OCA_IDLE && (top - bot >= 2u || (cur != OCA_NONE && top != bot)));
+        if (idle != 0ull && donors != 0ull)
+        {
+            const uint32_t n = min((uint32_t)__popcll(idle), (uint32_t)__popcll(donors));
+            const uint32_t dr = (uint32_t)__popcll(donors & ((1ull << lane) - 1ull));
+            if (((donors >> lane) & 1ull) && dr < n)
+            {
+                const uint32_t e = slot(bot++);
+                const uint32_t lv = (e >> OCA_LVL_SHIFT) & 31u;
+                uint32_t* c = vrh_user_smem + nth_bit(idle, dr);
+                c[0] = __float_as_uint(tr.ori.x); c[N] = __float_as_uint(tr.ori.y); c[2 * N] = __float_as_uint(tr.ori.z);
+                c[3 * N] = __float_as_uint(tr.dir.x); c[4 * N] = __float_as_uint(tr.dir.y); c[5 * N] = __float_as_uint(tr.dir.z);
+                c[6 * N] = __float_as_uint(tr.inv.x); c[7 * N] = __float_as_uint(tr.inv.y); c[8 * N] = __float_as_uint(tr.inv.z);
+                c[9 * N] = __float_as_uint(tmax); c[10 * N] = task; c[11 * N] = e & OCA_LINK_MASK;
+                c[12 * N] = ((path >> (plen - lv)) << 1) | 1u; c[13 * N] = lv + 1u;
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            const uint32_t ir = (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+            if (((idle >> lane) & 1ull) && ir < n)
+            {
+                tr.ori = mk3(__uint_as_float(col[0]), __uint_as_float(col[N]), __uint_as_float(col[2 * N]));
+                tr.dir = mk3(__uint_as_float(col[3 * N]), __uint_as_float(col[4 * N]), __uint_as_float(col[5 * N]));
+                tr.inv = mk3(__uint_as_float(col[6 * N]), __uint_as_float(col[7 * N]), __uint_as_float(col[8 * N]));
+                tmax = __uint_as_float(col[9 * N]);
+                task = col[10 * N];
+                cur = col[11 * N];
+                path = col[12 * N];
+                plen = col[13 * N];
+                bot = top = 0u;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        // 3. at most VRH_OCA_VISITS pair visits, or the leaf reached
+        bool hit = false;
+        uint32_t key = 0u, won = OCA_NONE;
+        if (task != OCA_IDLE)
+        {
+            uint32_t link = cur;
+            cur = OCA_NONE;
+            if (link == OCA_NONE)
+            {
+                const uint32_t e = slot(--top);
+                const uint32_t lv = (e >> OCA_LVL_SHIFT) & 31u;
+                link = e & OCA_LINK_MASK;
+                path = ((path >> (plen - lv)) << 1) | 1u;
+                plen = lv + 1u;
+            }
+            bool at_leaf = true;
+            for (uint32_t k = 0;; ++k)
+            {
+                if (link & LEAF_BIT) break;
+                if (k == VRH_OCA_VISITS) { cur = link; at_leaf = false; break; }
+                float4 q0, q1, q2;
+                float2 q3;
+                fetch_pair(pairs, link, q0, q1, q2, q3);
+                bool b0, b1;
+                float tn0, tn1;
+                box_pair<FAST>(q0, q1, q2, tr, FMAX, tmax, b0, b1, tn0, tn1);
+                const uint32_t l0 = __float_as_uint(q3.x), l1 = __float_as_uint(q3.y);
+                if (!(b0 | b1)) { at_leaf = false; break; }
+                const bool go0 = (b0 & b1) ? (tn0 < tn1) : b0;                 // ties -> child 1
+                if (b0 & b1)
+                {
+                    slot(top++) = (go0 ? l1 : l0) | (plen << OCA_LVL_SHIFT);
+                    path <<= 1;                                                  // the near side: 0
+                    plen += 1u;
+                }
+                link = go0 ? l0 : l1;
+            }
+            if (at_leaf)
+                for (uint32_t i = link & ~LEAF_BIT;; ++i)
+                {
+                    uint32_t flags = 0;
+                    if (test(tr, tmax, i, flags)) { hit = true; won = i; key = oca_key(path, plen); break; }
+                    if (flags & END_BIT) break;
+                }
+            if (hit)
+            {
+                atomicMin(&vrh_user_smem[task + OCA_RING * N], key);
+                cur = OCA_NONE; bot = top = 0u;
+            }
+        }
+        // 4. the ray's primitive: written by the lane whose key won (keys of distinct leaves differ)
+        if (__ballot(hit) != 0ull)
+        {
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            if (hit && vrh_user_smem[task + OCA_RING * N] == key) vrh_user_smem[task + (OCA_RING + 1u) * N] = won;
+            __builtin_amdgcn_wave_barrier();
+            if (hit) task = OCA_IDLE;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    return col[OCA_RING * N] == OCA_NOKEY ? OCA_NONE : col[(OCA_RING + 1u) * N];
+}
+
 // ---- deferred any_hit calls (VRH_USER_DEFER=1) --------------------------------------------------
 // A user kernel runs one pixel per lane and its any_hit calls one after another, so the wave waits
 // for its slowest lane once per call (the AO lambda: eight times per tile, VALU lane utilisation 0.37
@@ -994,9 +1261,13 @@ constexpr size_t DEFER_WAVE_BYTES = size_t(DEFER_ENTRIES) * 32u;
 // stacks: 16 waves / CU; the pool in the global log instead: -2 %, profiles/r05/defer/)
 // then one bit per entry: the trace phase found no hit (a miss leaves the entry's tag pending; only a
 // hit writes its leaf index to the log)
+// then 64 words: each lane's number of logged calls in the record phase.  The replay trusts a log entry
+// only below that count: a kernel whose answers change its path can make more calls in the replay than
+// it logged, and the slots past the count hold entries of an earlier tile
 constexpr uint32_t DEFER_MISS_WORDS = DEFER_ENTRIES / 32u;
-constexpr uint32_t DEFER_WORDS = 88u + DEFER_ENTRIES / 2u + DEFER_MISS_WORDS;
+constexpr uint32_t DEFER_WORDS = 88u + DEFER_ENTRIES / 2u + DEFER_MISS_WORDS + 64u;
 __device__ inline uint32_t* defer_miss_bits(uint32_t* a) { return a + 88u + DEFER_ENTRIES / 2u; }
+__device__ inline uint32_t* defer_logged_calls(uint32_t* a) { return a + 88u + DEFER_ENTRIES / 2u + DEFER_MISS_WORDS; }
 static_assert(DEFER_ENTRIES <= 65536u, "16-bit pool entries");
 static_assert(sizeof(vrh_scene_view) <= 18u * 4u, "the LDS copy of the tile's BVH holds 18 words");
 enum defer_state : uint32_t { DEFER_RUN = 0u, DEFER_RUN_LOG = 1u, DEFER_PENDING = 2u, DEFER_LOGGED = 3u };
@@ -1050,6 +1321,7 @@ __device__ inline defer_call defer_begin(vrh_scene_view const& v, basic_ray<floa
     if (a[2] == 0u || reinterpret_cast<const vrh_scene_view*>(a + 6)->pairs != v.pairs) return d;
     const uint32_t c = a[24u + lane];
     if (c >= VRH_USER_DEFER_SLOTS) return d;
+    if (phase == DEFER_REPLAY && c >= defer_logged_calls(a)[lane]) return d;   // not logged this tile: run it
     a[24u + lane] = c + 1u;
     d.entry = c * 64u + lane;
     float4* ent = defer_log(a) + 2u * d.entry;
@@ -1239,12 +1511,13 @@ VRH_FUNC inline auto intersect(
     using HR = hit_record_bvh<basic_ray<float>, hip_bvh_ref_t<P>, decltype(isect(ray, std::declval<P>()))>;
     using RT = typename detail::traversal_result<HR, Traversal, MultiHitMax>::type;
     RT result;
-    const float4* prims = static_cast<const float4*>(b.view.prims);
+    const vrh_scene_view view = hip_detail::uniform_view(b.view);
+    const float4* prims = static_cast<const float4*>(view.prims);
     if constexpr (Traversal == detail::AnyHit && VRH_USER_ANYHIT_SHARE)
     {
         // the shared any-hit walk (hip_detail::walk_shared): the same leaf step on the ray being
         // traversed, into the record of this visit
-        if (b.view.max_depth >= VRH_USER_STACK) return result;
+        if (view.max_depth >= VRH_USER_STACK) return result;
         const vrh::dev::ray_t r = hip_detail::dev_ray(ray);
         auto leaf2 = [&](vrh::dev::ray_t const& tr, float tmax, uint32_t i, uint32_t& flags, RT& rec) -> bool
         {
@@ -1257,11 +1530,40 @@ VRH_FUNC inline auto intersect(
             detail::exit_traversal<Traversal> early_exit;
             return early_exit.check(rec);
         };
-        if (b.view.finite_bounds && __ballot(!vrh::dev::finite_ray(r)) == 0ull)
-            hip_detail::walk_shared<true>(b.view, r, max_t, result, leaf2);
+        if (view.finite_bounds && __ballot(!vrh::dev::finite_ray(r)) == 0ull)
+            hip_detail::walk_shared<true>(view, r, max_t, result, leaf2);
         else
-            hip_detail::walk_shared<false>(b.view, r, max_t, result, leaf2);
+            hip_detail::walk_shared<false>(view, r, max_t, result, leaf2);
         return result;
+    }
+    // the ordered cooperative walk (hip_detail::walk_ordered): default intersector and update rule
+    constexpr bool orderable = VRH_USER_ANYHIT_ORDERED && Traversal == detail::AnyHit && MultiHitMax == 1
+                               && std::is_same<Intersector, default_intersector>::value && std::is_same<Cond, is_closer_t>::value;
+    if constexpr (orderable)
+    {
+        if (view.max_depth >= VRH_USER_STACK) return result;
+        if (hip_detail::oca_wave_usable(view))
+        {
+            const vrh::dev::ray_t r = hip_detail::dev_ray(ray);
+            auto test = [&](vrh::dev::ray_t const& tr, float tmax, uint32_t i, uint32_t& flags) -> bool
+            {
+                const basic_ray<float> ray2(vector<3, float>(tr.ori.x, tr.ori.y, tr.ori.z), vector<3, float>(tr.dir.x, tr.dir.y, tr.dir.z));
+                const P prim = hip_detail::leaf_primitive<P>(prims, i, flags);
+                return any(update_cond(HR(isect(ray2, prim), int(i)), RT(), tmax));
+            };
+            const uint32_t w = (view.finite_bounds && __ballot(!vrh::dev::finite_ray(r)) == 0ull)
+                             ? hip_detail::walk_ordered<true>(view, r, max_t, test) : hip_detail::walk_ordered<false>(view, r, max_t, test);
+            if (w != hip_detail::OCA_NONE)
+            {
+                // the owner's own leaf step on the primitive its ray's walk accepts first
+                uint32_t flags = 0;
+                const P prim = hip_detail::leaf_primitive<P>(prims, w, flags);
+                auto hr = HR(isect(ray, prim), int(w));
+                auto closer = update_cond(hr, result, max_t);
+                if (any(closer)) update_if(result, hr, closer);
+            }
+            return result;
+        }
     }
     // deferred calls (VRH_USER_DEFER: user_render's record / trace / replay phases): the default
     // intersector and update rule on one primitive type, one hit record
@@ -1270,7 +1572,7 @@ VRH_FUNC inline auto intersect(
     hip_detail::defer_call d{ hip_detail::DEFER_RUN, 0u, hip_detail::DTAG_NONE };
     if constexpr (deferrable)
     {
-        d = hip_detail::defer_begin(b.view, ray, max_t, Traversal == detail::AnyHit);
+        d = hip_detail::defer_begin(view, ray, max_t, Traversal == detail::AnyHit);
         if (d.state == hip_detail::DEFER_PENDING) return result;     // record phase: answered in the replay
         if (d.state == hip_detail::DEFER_LOGGED)
         {
@@ -1288,7 +1590,7 @@ VRH_FUNC inline auto intersect(
         }
     }
     uint32_t won = hip_detail::DTAG_NONE;      // the leaf index of the primitive the result holds
-    hip_detail::walk<Traversal == detail::AnyHit>(b.view, ray, max_t, [&]() { return hip_detail::cull_of(result); },
+    hip_detail::walk<Traversal == detail::AnyHit>(view, ray, max_t, [&]() { return hip_detail::cull_of(result); },
                      [&](uint32_t i, uint32_t& flags) -> bool
                      {
                          const P prim = hip_detail::leaf_primitive<P>(prims, i, flags);
@@ -1357,6 +1659,34 @@ __device__ inline bvh_record traverse_bvh_direct(basic_ray<float> const& ray, vr
         else walk_shared<false>(b, r, max_t, result, leaf2);
         return result;
     }
+    if constexpr (Any && VRH_USER_ANYHIT_ORDERED && std::is_same<Isect, default_intersector>::value)
+    {
+        // the ordered cooperative walk (walk_ordered): the reference's first hit, lanes sharing the work
+        if (b.max_depth >= VRH_USER_STACK) return result;
+        if (oca_wave_usable(b))
+        {
+            const vrh::dev::ray_t r = dev_ray(ray);
+            auto test = [&](vrh::dev::ray_t const& tr, float tmax, uint32_t i, uint32_t& flags) -> bool
+            {
+                const basic_ray<float> ray2(vec3(tr.ori.x, tr.ori.y, tr.ori.z), vec3(tr.dir.x, tr.dir.y, tr.dir.z));
+                HR hr;
+                if (b.prim_kind == VRH_PRIM_TRI64) hr = isect(ray2, leaf_primitive<basic_triangle<3, float>>(prims, i, flags));
+                else hr = isect(ray2, leaf_primitive<basic_sphere<float>>(prims, i, flags));
+                return is_closer(hr, HR(), tmax);
+            };
+            const uint32_t w = (b.finite_bounds && __ballot(!vrh::dev::finite_ray(r)) == 0ull)
+                             ? walk_ordered<true>(b, r, max_t, test) : walk_ordered<false>(b, r, max_t, test);
+            if (w != OCA_NONE)
+            {
+                uint32_t flags = 0;
+                HR hr;
+                if (b.prim_kind == VRH_PRIM_TRI64) hr = isect(ray, leaf_primitive<basic_triangle<3, float>>(prims, w, flags));
+                else hr = isect(ray, leaf_primitive<basic_sphere<float>>(prims, w, flags));
+                if (is_closer(hr, static_cast<HR const&>(result), max_t)) result = bvh_record(hr, w);
+            }
+            return result;
+        }
+    }
     // the leaf: every primitive in index order, is_closer / update_if (intersect.inl:103-128)
     walk<Any>(b, ray, max_t, [&]() { return result.t; },
          [&](uint32_t i, uint32_t& flags) -> bool
@@ -1410,7 +1740,7 @@ __device__ inline hip_detail::bvh_record closest_hit(basic_ray<float> const& ray
     hip_detail::bvh_record result;
     for (It it = begin; it != end; ++it)
     {
-        auto hr = hip_detail::traverse_bvh<false>(ray, it->view, isect, FLT_MAX);
+        auto hr = hip_detail::traverse_bvh<false>(ray, hip_detail::uniform_view(it->view), isect, FLT_MAX);
         if (is_closer(hr, result, FLT_MAX)) result = hr;
     }
     return result;
@@ -1422,7 +1752,7 @@ __device__ inline hip_detail::bvh_record any_hit(basic_ray<float> const& ray, It
     hip_detail::bvh_record result;
     for (It it = begin; it != end; ++it)
     {
-        auto hr = hip_detail::traverse_bvh<true>(ray, it->view, isect, max_t);
+        auto hr = hip_detail::traverse_bvh<true>(ray, hip_detail::uniform_view(it->view), isect, max_t);
         if (is_closer(hr, result, max_t)) result = hr;
         if (result.hit) return result;
     }
@@ -1742,12 +2072,17 @@ __global__ __launch_bounds__(64) VRH_USER_OCC void user_render(K kernel, user_fr
 // VRH_USER_AUTO_WAVES (default on unless VRH_USER_WAVES or VRH_USER_DEFER is set): the same kernel
 // also compiled for a 5-wave register target; the launch takes it when it holds more waves per CU
 // and spills at most VRH_USER_AUTO_SCRATCH bytes per lane (the AO lambda: 104 VGPRs = 4 waves, or 96
-// with 4 spilled = 5 waves: +4.2 %, profiles/r05/user/)
+// with 4 spilled = 5 waves: +4.2 %, profiles/r05/user/; round 6: 64 B, below)
 #ifndef VRH_USER_AUTO_WAVES
 #define VRH_USER_AUTO_WAVES (VRH_USER_WAVES == 0 && !VRH_USER_DEFER)
 #endif
 #ifndef VRH_USER_AUTO_SCRATCH
-#define VRH_USER_AUTO_SCRATCH 32
+// round 6: the AO lambda with global loads is 96 VGPRs + 48 B of scratch at 5 waves against 114 VGPRs
+// at 4: 1.750 vs 1.821 ms per frame (profiles/r06/user_loads/), so up to 64 B
+#define VRH_USER_AUTO_SCRATCH 64
+#endif
+#ifndef VRH_USER_MAX_DEVICES
+#define VRH_USER_MAX_DEVICES 64     // device ordinals the per-device launch choices are cached for
 #endif
 #if VRH_USER_AUTO_WAVES
 template <typename K, uint32_t SK = VRH_SAMPLER_UNIFORM, uint32_t SN = 1, uint32_t NC = 1>
@@ -1827,6 +2162,7 @@ __device__ __forceinline__ void user_render_body(K& kernel, user_frames<NC> cons
 #if VRH_DEFER_PROF
                 const uint64_t p2 = clock64();
 #endif
+                defer_logged_calls(da)[lane] = da[24u + lane];
                 da[24u + lane] = 0u;
                 if (lane == 0u) da[0] = DEFER_REPLAY;
                 __syncthreads();
@@ -1896,21 +2232,26 @@ inline hipError_t launch_user_render(hip_context& ctx, K const& kernel, user_fra
     if (e != hipSuccess) return e;
 #if VRH_USER_AUTO_WAVES
     {
-        // once per kernel: the 5-wave instance if it holds more waves and spills (almost) nothing
-        static int w5 = -1;
+        // once per kernel and device: the 5-wave instance if it holds more waves and spills (almost)
+        // nothing.  The answer is cached per device ordinal (devices of different architectures get
+        // their own), in atomics: 0 = not asked yet, 1 = keep the default instance, n + 1 = the 5-wave
+        // instance at n blocks per CU.  Two threads asking at once compute the same answer.
+        static std::atomic<int> w5_cache[VRH_USER_MAX_DEVICES];
         auto fn5 = user_render_w5<K, SK, SN, NC>;
-        if (w5 < 0)
+        int w5 = (dev >= 0 && dev < VRH_USER_MAX_DEVICES) ? w5_cache[dev].load(std::memory_order_acquire) : 0;
+        if (w5 == 0)
         {
             hipFuncAttributes a{};
             int per_cu5 = 0;
             if ((e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(fn5))) != hipSuccess) return e;
             if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu5, fn5, 64, lds)) != hipSuccess) return e;
-            w5 = (per_cu5 > per_cu && a.localSizeBytes <= size_t(VRH_USER_AUTO_SCRATCH)) ? per_cu5 : 0;
+            w5 = (per_cu5 > per_cu && a.localSizeBytes <= size_t(VRH_USER_AUTO_SCRATCH)) ? per_cu5 + 1 : 1;
+            if (dev >= 0 && dev < VRH_USER_MAX_DEVICES) w5_cache[dev].store(w5, std::memory_order_release);
         }
-        if (w5 > 0)
+        if (w5 > 1)
         {
             fn = fn5;
-            per_cu = w5;
+            per_cu = w5 - 1;
         }
     }
 #endif

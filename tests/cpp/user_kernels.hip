@@ -22,6 +22,7 @@
 //   user_kernels draws <grid> <W> <H> <outdir> <frame>          kernel(r, random_sampler<float>&): draws
 //                                                                0, 1, 2, 15 of the pixel's sampler as colour
 //   user_kernels anyrec <grid> <W> <H> <outdir> <frame> [radius] the AO lambda's any_hit hit records, hashed
+//   user_kernels chain <grid> <W> <H> <outdir> <frame> [radius] any_hit calls that depend on earlier answers
 //   user_kernels rsao  <grid> <W> <H> <outdir> <frame>          the AO example's kernel (ao/main.cpp:183-246)
 //                                                                with standalone.h's random_sampler and
 //                                                                cosine_sample_hemisphere; depth = hit t
@@ -373,6 +374,61 @@ int main(int argc, char** argv)
                         if (rec.hit) { mix(uint32_t(rec.prim_id)); mix(__float_as_uint(rec.t)); hits += 1u; }
                     }
                     result.color = vec4(__uint_as_float(h), float(hits), 1.0f, 1.0f);
+                }
+                return result;
+            }, sparams, frame_num);
+            std::vector<float> out(4 * size_t(W) * H);
+            rt.download(out.data());
+            write_file(outdir + "/color.bin", out.data(), out.size() * 4);
+            return 0;
+        }
+        else if (mode == "chain")
+        {
+            // chain <grid> W H outdir frame radius: a kernel whose calls depend on earlier answers -- per
+            // AO sample an any_hit; when it hits, two more any_hit calls (a shorter and a reflected ray).
+            // Under VRH_USER_DEFER the record phase sees every first call answered "no hit" (pending) and
+            // logs one call per sample; the replay, with the real answers, makes up to three: the calls
+            // past the record phase's count must run directly, not read the log slots an earlier tile
+            // left.  The frame (a hash of every record, the number of calls) must equal the
+            // direct build's.
+            const unsigned frame_num = unsigned(strtoul(argv[6], nullptr, 10));
+            const float radius = argc > 7 ? float(atof(argv[7])) : 0.1f;
+            hip_bvh_ref const* begin = one.r;
+            hip_bvh_ref const* end = one.r + one.n;
+            sched.frame([=] __device__ (ray r, random_sampler<float>& samp) -> result_record<float>
+            {
+                result_record<float> result;
+                result.color = vec4(0.0f, 0.0f, 0.0f, 0.0f);
+                auto hr = closest_hit(r, begin, end);
+                if (hr.hit)
+                {
+                    hr.isect_pos = r.ori + r.dir * hr.t;
+                    vec3 n = get_normal(dnormals, hr);
+                    vec3 u, v, w = n;
+                    make_orthonormal_basis(u, v, w);
+                    uint32_t h = 2166136261u, calls = 0;
+                    auto mix = [&](uint32_t x) { for (int k = 0; k < 4; ++k) { h ^= (x >> (8 * k)) & 0xFFu; h *= 16777619u; } };
+                    auto rec_mix = [&](decltype(hr) const& rec) {
+                        mix(rec.hit ? 1u : 0u);
+                        if (rec.hit) { mix(uint32_t(rec.prim_id)); mix(__float_as_uint(rec.t)); }
+                    };
+                    for (int i = 0; i < 4; ++i)
+                    {
+                        auto sp = cosine_sample_hemisphere(samp.next(), samp.next());
+                        auto dir = normalize(sp.x * u + sp.y * v + sp.z * w);
+                        ray ao(hr.isect_pos + dir * 1E-3f, dir);
+                        auto rec = any_hit(ao, begin, end, radius);
+                        rec_mix(rec);
+                        calls += 1u;
+                        if (rec.hit)
+                        {
+                            rec_mix(any_hit(ao, begin, end, rec.t * 0.5f));
+                            auto refl = normalize(dir - n * (2.0f * dot(dir, n)));
+                            rec_mix(any_hit(ray(hr.isect_pos + n * 1E-3f, normalize(refl + n)), begin, end, radius));
+                            calls += 2u;
+                        }
+                    }
+                    result.color = vec4(__uint_as_float(h), float(calls), 1.0f, 1.0f);
                 }
                 return result;
             }, sparams, frame_num);

@@ -82,6 +82,7 @@ def test_user_ao_kernel_shared_anyhit_matches_reference(tmp_path, golden, oracle
 
 
 CUT_BIN = os.path.join(ROOT, "build", "tests", "uk_cut")
+OCA_BIN = os.path.join(ROOT, "build", "tests", "uk_oca")
 
 
 @pytest.mark.gpu
@@ -91,11 +92,13 @@ def test_anyhit_entry_cut_returns_reference_order_records(tmp_path, grid, W, H, 
     """The opt-in any_hit entry cut (hip_kernels.h VRH_USER_ANYHIT_CUT=1, user_cut_entry: a skeleton of
     the BVH's top in LDS, chains skipped only where boxes nest) walks the same leaves in the same order
     as the walk from the root: every any_hit call of the AO lambda returns the same hit RECORD (prim id
-    and t of the first hit found), not only the same hit / miss -- against the default build."""
-    assert os.path.exists(CUT_BIN), "run __graft_entry__.build() (make -C visionaray_amd cpp_tests)"
-    assert os.path.exists(DEFER_BIN), "run __graft_entry__.build() (make -C visionaray_amd cpp_tests)"
+    and t of the first hit found), not only the same hit / miss -- against the default build.  So do
+    the deferred build and the ordered cooperative walk (VRH_USER_ANYHIT_ORDERED=1: lanes share the
+    calls' work, every segment keyed by its place in the ray's walk order)."""
+    for b in (CUT_BIN, DEFER_BIN, OCA_BIN):
+        assert os.path.exists(b), "run __graft_entry__.build() (make -C visionaray_amd cpp_tests)"
     outs = []
-    for b in (CUT_BIN, DEFER_BIN, BIN):
+    for b in (CUT_BIN, DEFER_BIN, OCA_BIN, BIN):
         d = tmp_path / os.path.basename(b)
         d.mkdir()
         subprocess.run([b, "anyrec", str(grid), str(W), str(H), str(d), str(frame), str(radius)], check=True,
@@ -105,9 +108,32 @@ def test_anyhit_entry_cut_returns_reference_order_records(tmp_path, grid, W, H, 
     assert float((ref[:, 1] > 0).mean()) > 0.01, "the case must have occluded AO rays"
     # the deferred build (VRH_USER_DEFER=1) traces the same calls in a pool, in the same walk order:
     # the same records too
-    for name, got in zip(("entry cut", "deferred"), outs[:2]):
+    for name, got in zip(("entry cut", "deferred", "ordered cooperative walk"), outs[:3]):
         bad = np.flatnonzero(np.any(got.view(np.uint32) != ref.view(np.uint32), axis=1))
         assert bad.size == 0, f"{name}: {bad.size} pixels' any_hit records differ, first {bad[:8].tolist()}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grid,W,H,frame,radius", [(200, 320, 180, 0, 0.1), (708, 1920, 1080, 4, 0.1),
+                                                   (64, 160, 90, 2, 0.5)])
+def test_deferred_replay_with_more_calls_than_recorded(tmp_path, grid, W, H, frame, radius):
+    """A kernel whose later any_hit calls depend on earlier answers (the `chain` mode: a hit adds two
+    more calls): the record phase of VRH_USER_DEFER sees only the first call per sample (answered "no
+    hit" until the trace), the replay makes up to three.  The calls past each lane's recorded count run
+    directly -- the log slots there belong to an earlier tile -- so every record equals the direct build's."""
+    outs = []
+    for b in (BIN, DEFER_BIN):
+        assert os.path.exists(b), "run __graft_entry__.build() (make -C visionaray_amd cpp_tests)"
+        d = tmp_path / os.path.basename(b)
+        d.mkdir()
+        subprocess.run([b, "chain", str(grid), str(W), str(H), str(d), str(frame), str(radius)], check=True,
+                       capture_output=True, text=True, timeout=120)
+        outs.append(np.fromfile(d / "color.bin", np.float32).reshape(-1, 4))
+    direct, deferred = outs
+    calls = direct[:, 1]
+    assert float((calls > 4).mean()) > 0.01, "the case must have pixels whose replay makes extra calls"
+    bad = np.flatnonzero(np.any(deferred.view(np.uint32) != direct.view(np.uint32), axis=1))
+    assert bad.size == 0, f"deferred: {bad.size} pixels differ, first {bad[:8].tolist()}"
 
 
 @pytest.mark.gpu
@@ -252,5 +278,5 @@ def test_user_kernel_header_needs_hipcc(tmp_path):
 
 def test_user_kernel_program_is_built():
     """build() compiled the user-kernel programs for gfx950 (they travel to the GPU box with the tree)."""
-    for b in (BIN, DEFER_BIN, SHARE_BIN, CUT_BIN):
+    for b in (BIN, DEFER_BIN, SHARE_BIN, CUT_BIN, OCA_BIN):
         assert os.path.exists(b), f"{b}: run __graft_entry__.build() (make -C visionaray_amd cpp_tests)"

@@ -30,7 +30,9 @@ dev = va.hip_index_bvh(ctx, host, scenes.normals_for(prims))
 cam, W, H = scenes.scene_camera(scene)
 basis = cam.basis(W, H)
 kern = va.ao_kernel(dev) if kind == "ao" else va.closest_hit_kernel(dev)
-out = {"scene": scene, "kind": kind, "frames": frames, "frames_in_flight": F, "per_n": {}}
+from visionaray_amd.buildinfo import kernel_source_sha256  # noqa: E402
+out = {"scene": scene, "kind": kind, "frames": frames, "frames_in_flight": F, "per_n": {},
+       "kernel_source_sha256": kernel_source_sha256()}
 base = None
 for n in (1, 2, 4, 8):
     rows = _capi.VRH_BAND_ROWS * va.shard_bands(H, 0, n)

@@ -1661,11 +1661,22 @@ VRH_API int vrh_get_accum_stats(vrh_ctx* ctx, vrh_accum_stats* out)
     }
     if (a.timed_frames == 0) a.kernel_ms_min = 0.0;
     // first launch's start to the last launch's end: overlapping (asynchronous) frames count once
+    // (asynchronous frames alternate between two frame lanes: the second-to-last frame can end after the
+    // last one, and the second frame can start before the first -- the span runs from the earliest of
+    // the first two starts to the latest of the last two ends, all measured from the first start)
     if (a.frames >= 1 && a.frames <= VRH_MAX_TIMED_FRAMES)
     {
-        float ms = 0.0f;
-        VRH_HIP(hipEventElapsedTime(&ms, ctx->ev_start[0], ctx->ev_stop[a.frames - 1]));
-        a.span_ms = ms;
+        float end = 0.0f, begin = 0.0f;
+        VRH_HIP(hipEventElapsedTime(&end, ctx->ev_start[0], ctx->ev_stop[a.frames - 1]));
+        if (a.frames >= 2)
+        {
+            float e2 = 0.0f, s2 = 0.0f;
+            VRH_HIP(hipEventElapsedTime(&e2, ctx->ev_start[0], ctx->ev_stop[a.frames - 2]));
+            VRH_HIP(hipEventElapsedTime(&s2, ctx->ev_start[0], ctx->ev_start[1]));
+            end = std::max(end, e2);
+            begin = std::min(begin, s2);
+        }
+        a.span_ms = double(end) - double(begin);
     }
     for (int b = 0; b < COUNTER_BLOCKS; ++b)
     {
