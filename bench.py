@@ -45,7 +45,7 @@ Rank 0 prints one JSON line (the contract of the task statement) with:
     §8d algorithmic HBM bytes are kept as roofline.hbm_algorithmic (informational);
   * cpu_baseline: the reference's own SSE4 tiled_sched path (oracle/_ref, built from
     /root/reference by oracle/Makefile) on a bounded sample at threads = the CPUs the process may use
-    (cgroup quota), the median of 7 frames, with a cores/4 and cores/2 sweep and each point's spread,
+    (cgroup quota) at most: the best of a cores/4, cores/2, cores - 1, cores sweep, 2 runs per point of 7 frames each,
     the host's core count, quota and model, and the retries / stall seconds of tiled_sched stalls.
 
 Settle: after the W warm-up steps, untimed launches of the timed shape run for --settle-ms (300 ms) of
@@ -81,8 +81,8 @@ def parse():
     ap.add_argument("--kernel", default=None, choices=["ao", "primary"], help="default: ao for triangles")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=None,
-                    help="host threads for the CPU baseline (default: the CPUs the process may use, with a "
-                         "cores/4, cores/2 sweep beside it)")
+                    help="host threads for the CPU baseline (default: the best of a cores/4, cores/2, cores - 1, "
+                         "cores sweep, cores = the CPUs the process may use)")
     ap.add_argument("--no-verify", action="store_true", help="skip the untimed checks against the fixtures")
     ap.add_argument("--no-user-kernel", action="store_true",
                     help="skip the user-kernel leg (hf1M AO at N=1: hip_kernels.h device lambda, 32 frames per launch)")
@@ -141,21 +141,28 @@ CPU_ATTEMPT_TIMEOUT_S = 90
 CPU_FRAMES = 7                  # timed frames per sweep point (median), after 1 warm-up frame
 
 
+CPU_RUNS = 2                    # runs per sweep point; the faster one counts (a run can only be slowed)
+
+
 def cpu_sweep_points(cores, threads=None):
-    """Worker-thread counts of the CPU baseline: --cpu-threads alone, else cores/4, cores/2 and cores --
-    never above the CPUs the process may use (oversubscribed points measured up to 3x apart between
-    sessions)."""
+    """Worker-thread counts of the CPU baseline: --cpu-threads alone, else cores/4, cores/2, cores - 1
+    and cores -- never above the CPUs the process may use (oversubscribed points measured up to 3x
+    apart between sessions)."""
     if threads:
         return [threads]
-    return sorted({max(1, cores // 4), max(1, cores // 2), cores})
+    return sorted({max(1, cores // 4), max(1, cores // 2), max(1, cores - 1), cores})
 
 
 def cpu_baseline(scene, kernel, threads=None):
     """Reference SSE4 tiled_sched<ray4> (oracle/_ref/vsnray_ref_bench) on a bounded sample: the same
-    scene and camera at full resolution, 1 warm-up + CPU_FRAMES timed frames per point, the median
-    frame.  `value` is the point at threads = cores (the CPUs this process may use: the cgroup quota,
-    else the affinity mask); the sweep below it (cores/4, cores/2) and each point's min / max frame
-    rate are reported beside it.  tiled_sched can lose a worker's wake-up (tiled_sched.inl:181 waits
+    scene and camera at full resolution, 1 warm-up + CPU_FRAMES timed frames per run, the median
+    frame; CPU_RUNS runs per point, the faster counts.  Points: cores/4, cores/2, cores - 1 and cores
+    (the CPUs this process may use: the cgroup quota, else the affinity mask), never more.  `value` is
+    the best point.  At threads = cores the workers alone fill the quota, so any other thread of the
+    container (the Python parent, the HIP runtime) makes CFS throttle all of them: round 6 measured
+    93.4 and 75.1 Mrays/s there in two sessions while 8 threads gave 43.21 / 43.13 (profiles/r06/cpu/),
+    hence cores - 1 beside it and the best of the sweep as `value`.  Each point's min / max frame rate
+    is reported.  tiled_sched can lose a worker's wake-up (tiled_sched.inl:181 waits
     without a predicate against the notify_all at :386) and stall a frame for good: a run that passes
     CPU_ATTEMPT_TIMEOUT_S is killed and tried once more, and the line records the retries and the
     seconds lost to stalls."""
@@ -164,48 +171,53 @@ def cpu_baseline(scene, kernel, threads=None):
     info = host_info()
     info["cgroup_cpu_quota"] = cgroup_cpu_quota()
     cores = usable_cpus(info)
-    info["cores_note"] = ("cores = the CPUs the process may use (cgroup quota, else affinity); value = the "
-                          "sweep point at threads = cores")
+    info["cores_note"] = ("cores = the CPUs the process may use (cgroup quota, else affinity); value = the best "
+                          "sweep point, threads = its worker threads (never above cores)")
     if os.path.exists(O.REF_BENCH_BIN):
         counts = cpu_sweep_points(cores, threads)
         sweep, retries, stall_s = [], 0, 0.0
         for n in counts:
             print(f"cpu baseline: reference tiled_sched, {n} threads ...", file=sys.stderr, flush=True)
-            point = {"threads": n, "value": None, "retries": 0, "stall_s": 0.0}
-            for attempt in range(2):
-                t0 = time.perf_counter()
-                try:
-                    r = O.ref_bench(scene, n, CPU_FRAMES, 1920, 1080, samples, timeout=CPU_ATTEMPT_TIMEOUT_S)
-                except subprocess.TimeoutExpired:
-                    lost = time.perf_counter() - t0
-                    print(f"cpu baseline: {n} threads stalled ({lost:.0f} s, tiled_sched lost wake-up)",
-                          file=sys.stderr, flush=True)
-                    point["stall_s"] = round(point["stall_s"] + lost, 1)
-                    if attempt == 0:
-                        point["retries"] += 1
-                    continue
-                rpf = r["rays_per_frame"]
-                point["value"] = round(r["mrays_per_s"], 3)
-                point["rays_per_frame"] = rpf
-                if r.get("min_s"):
-                    # frame-rate spread of the point: slowest and fastest of its timed frames
-                    point["min"] = round(rpf / r["max_s"] / 1e6, 3)
-                    point["max"] = round(rpf / r["min_s"] / 1e6, 3)
-                    point["spread"] = round((r["max_s"] - r["min_s"]) / r["median_s"], 4)
-                break
+            point = {"threads": n, "value": None, "runs": [], "retries": 0, "stall_s": 0.0}
+            for run in range(CPU_RUNS):
+                for attempt in range(2):
+                    t0 = time.perf_counter()
+                    try:
+                        r = O.ref_bench(scene, n, CPU_FRAMES, 1920, 1080, samples, timeout=CPU_ATTEMPT_TIMEOUT_S)
+                    except subprocess.TimeoutExpired:
+                        lost = time.perf_counter() - t0
+                        print(f"cpu baseline: {n} threads stalled ({lost:.0f} s, tiled_sched lost wake-up)",
+                              file=sys.stderr, flush=True)
+                        point["stall_s"] = round(point["stall_s"] + lost, 1)
+                        if attempt == 0:
+                            point["retries"] += 1
+                        continue
+                    rpf = r["rays_per_frame"]
+                    point["runs"].append(round(r["mrays_per_s"], 3))
+                    if point["value"] is None or r["mrays_per_s"] > point["value"]:
+                        point["value"] = round(r["mrays_per_s"], 3)
+                        point["rays_per_frame"] = rpf
+                        if r.get("min_s"):
+                            # frame-rate spread of the run: slowest and fastest of its timed frames
+                            point["min"] = round(rpf / r["max_s"] / 1e6, 3)
+                            point["max"] = round(rpf / r["min_s"] / 1e6, 3)
+                            point["spread"] = round((r["max_s"] - r["min_s"]) / r["median_s"], 4)
+                    break
             retries += point["retries"]
             stall_s += point["stall_s"]
             sweep.append(point)
         done = [p for p in sweep if p["value"] is not None]
         if not done:
             raise RuntimeError(f"every reference run stalled: {sweep}")
-        at = next((p for p in done if p["threads"] == (threads or cores)), None) or max(done, key=lambda p: p["threads"])
+        at = max(done, key=lambda p: p["value"])
+        at_cores = next((p["value"] for p in done if p["threads"] == cores), None)
         return {"value": at["value"], "unit": "Mrays/s", "cores": cores, "threads": at["threads"],
                 "kind": "reference",
                 "sample": f"{scene} 1920x1080, {samples} AO spp, tiled_sched<basic_ray<simd::float4>> -O3 -msse4.1, "
-                          f"{at['threads']} worker threads, the median of {CPU_FRAMES} frames after 1 warm-up "
-                          f"({at['rays_per_frame']} rays/frame); sweep {counts} beside it",
-                "sweep": sweep, "best_of_sweep": max(p["value"] for p in done),
+                          f"best of a worker-thread sweep {counts} within the {cores} CPUs the process may use "
+                          f"(the faster of {CPU_RUNS} runs per point, each the median of {CPU_FRAMES} frames after 1 "
+                          f"warm-up; {at['rays_per_frame']} rays/frame)",
+                "sweep": sweep, "value_at_threads_eq_cores": at_cores,
                 "retries": retries, "stall_s": round(stall_s, 1), **info}
     # fallback: the plain-C restatement (scalar, OpenMP rows) on 1/8 of the image rows
     threads = threads or min(16, info["cpus_available"] or 1)

@@ -1261,13 +1261,13 @@ constexpr size_t DEFER_WAVE_BYTES = size_t(DEFER_ENTRIES) * 32u;
 // stacks: 16 waves / CU; the pool in the global log instead: -2 %, profiles/r05/defer/)
 // then one bit per entry: the trace phase found no hit (a miss leaves the entry's tag pending; only a
 // hit writes its leaf index to the log)
-// then 64 words: each lane's number of logged calls in the record phase.  The replay trusts a log entry
-// only below that count: a kernel whose answers change its path can make more calls in the replay than
-// it logged, and the slots past the count hold entries of an earlier tile
+// The per-lane call word [24 + lane] counts the calls so far in its low 16 bits; in the replay its high
+// 16 bits hold the number of calls the record phase logged.  The replay trusts a log entry only below
+// that count: a kernel whose answers change its path can make more calls in the replay than it logged,
+// and the slots past the count hold entries of an earlier tile
 constexpr uint32_t DEFER_MISS_WORDS = DEFER_ENTRIES / 32u;
-constexpr uint32_t DEFER_WORDS = 88u + DEFER_ENTRIES / 2u + DEFER_MISS_WORDS + 64u;
+constexpr uint32_t DEFER_WORDS = 88u + DEFER_ENTRIES / 2u + DEFER_MISS_WORDS;
 __device__ inline uint32_t* defer_miss_bits(uint32_t* a) { return a + 88u + DEFER_ENTRIES / 2u; }
-__device__ inline uint32_t* defer_logged_calls(uint32_t* a) { return a + 88u + DEFER_ENTRIES / 2u + DEFER_MISS_WORDS; }
 static_assert(DEFER_ENTRIES <= 65536u, "16-bit pool entries");
 static_assert(sizeof(vrh_scene_view) <= 18u * 4u, "the LDS copy of the tile's BVH holds 18 words");
 enum defer_state : uint32_t { DEFER_RUN = 0u, DEFER_RUN_LOG = 1u, DEFER_PENDING = 2u, DEFER_LOGGED = 3u };
@@ -1319,10 +1319,11 @@ __device__ inline defer_call defer_begin(vrh_scene_view const& v, basic_ray<floa
         __builtin_amdgcn_wave_barrier();
     }
     if (a[2] == 0u || reinterpret_cast<const vrh_scene_view*>(a + 6)->pairs != v.pairs) return d;
-    const uint32_t c = a[24u + lane];
+    const uint32_t cw = a[24u + lane];
+    const uint32_t c = cw & 0xFFFFu;
     if (c >= VRH_USER_DEFER_SLOTS) return d;
-    if (phase == DEFER_REPLAY && c >= defer_logged_calls(a)[lane]) return d;   // not logged this tile: run it
-    a[24u + lane] = c + 1u;
+    if (phase == DEFER_REPLAY && c >= (cw >> 16)) return d;      // not logged in this tile's record phase: run it
+    a[24u + lane] = cw + 1u;
     d.entry = c * 64u + lane;
     float4* ent = defer_log(a) + 2u * d.entry;
     if (phase == DEFER_RECORD)
@@ -2045,6 +2046,12 @@ __device__ inline uint32_t xcc_id()
 // handed out exactly once by one of the 8 heads, so
 // which XCD a wave runs on changes only speed.  Every wave leaves once all 8 queues are empty.
 // VRH_USER_WAVES: waves per SIMD the register allocation targets (0: the compiler's choice)
+#if VRH_USER_DEFER && !defined(VRH_USER_WAVES)
+// the deferred build's LDS (8 KB of stacks + 2.2 KB of log state per wave) holds a CU to 15 waves, so
+// it targets 4 waves per SIMD: without the target the AO lambda drifted to 130-134 VGPRs (3 waves) on
+// small source changes -- 1.92 vs 1.65 ms per frame (profiles/r06/defer_regs/)
+#define VRH_USER_WAVES 4
+#endif
 #ifndef VRH_USER_WAVES
 #define VRH_USER_WAVES 0
 #endif
@@ -2162,8 +2169,7 @@ __device__ __forceinline__ void user_render_body(K& kernel, user_frames<NC> cons
 #if VRH_DEFER_PROF
                 const uint64_t p2 = clock64();
 #endif
-                defer_logged_calls(da)[lane] = da[24u + lane];
-                da[24u + lane] = 0u;
+                da[24u + lane] = (da[24u + lane] & 0xFFFFu) << 16;     // logged calls, and the count from 0
                 if (lane == 0u) da[0] = DEFER_REPLAY;
                 __syncthreads();
                 if (in) user_pixel<K, SK, SN, NC>(kernel, f, c, x, y);
