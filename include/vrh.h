@@ -292,10 +292,12 @@ enum vrh_option {
                                     1 = on, 2 = off (auto: off -- measured 2-3 % slower on one-frame
                                     C3 / C4 launches, profiles/r03_ab/ao_share/)                    */
     VRH_OPT_ASYNC_FRAMES = 26,   /* 1: frames are issued like cuda_sched issues them (cuda_sched.inl:306-320,
-                                    no synchronisation): they alternate between two frame lanes of
-                                    the context (HIP streams of its own), so the next frame's waves
-                                    take the CUs the previous frame's launch tail leaves idle.
-                                    Results are unchanged: a frame into a target that the other lane
+                                    no synchronisation): they go round robin over the frame lanes of
+                                    the context (HIP streams of its own; 3 lanes, or 2..4 given as
+                                    the value), so the next frames' waves take the CUs the earlier
+                                    frames' launch tails leave idle (changing the lane count first
+                                    waits, on the device, for every frame issued so far).
+                                    Results are unchanged: a frame into a target that another lane
                                     still writes renders into the lane's scratch target (primary / AO
                                     kernels, one frame, uniform / jittered sampler) and is copied in
                                     issue order, or waits for that lane (every other case); every

@@ -1,11 +1,11 @@
 """GPU: asynchronous frames (VRH_OPT_ASYNC_FRAMES) -- cuda_sched's issue model
 (cuda_sched.inl:306-320: frame() returns once the kernel is issued; gpu_buffer_rt::end_frame is a
-no-op, gpu_buffer_rt.inl:84-86) with the frames overlapping on the context's two frame lanes.
+no-op, gpu_buffer_rt.inl:84-86) with the frames overlapping on the context's frame lanes (2-4).
 
 The bar is the synchronous path's result: a sequence of frames, clears, downloads and pixel-sampler
 passes run with the option on must leave every target -- and every intermediate download -- bit for
-bit as the same sequence does one synchronous frame at a time.  That covers the write order of two
-lanes on one target (the scratch-target copy, pending until something needs it, dropped when a later
+bit as the same sequence does one synchronous frame at a time.  That covers the write order of 2, 3
+and 4 lanes on one target (the scratch-target copy, pending until something needs it, dropped when a later
 frame supersedes it), blending samplers that read the target, scissor boxes, shading kernels (which
 wait instead of using scratch), and the joins of the context stream.
 """
@@ -53,10 +53,21 @@ def _shading(ctx, dev):
     return va.shading(ctx, mats, lights)
 
 
+LANES = [2]     # frame lanes of the asynchronous run (the `lanes` fixture sets it per test)
+
+
+@pytest.fixture(params=[2, 3, 4], autouse=True)
+def lanes(request):
+    """Every sequence with 2, 3 and 4 frame lanes (VRH_OPT_ASYNC_FRAMES = the lane count): the write
+    order of any number of lanes on one target must give the synchronous bits."""
+    LANES[0] = request.param
+    return request.param
+
+
 def run_sequence(ctx, dev, ops, n_targets, async_on):
     """Run `ops` with asynchronous frames on or off; return every target's final contents and the
     downloads the sequence asked for on the way."""
-    ctx.set_option("async_frames", 1 if async_on else 0)
+    ctx.set_option("async_frames", LANES[0] if async_on else 0)
     cams = frame_cameras(NAME, W, H, 6)
     sh = _shading(ctx, dev)
     kernels = {"ao": va.ao_kernel(dev), "primary": va.closest_hit_kernel(dev),
@@ -272,10 +283,12 @@ def test_user_stream_work_after_async_frames(ctx, scene):
 
 
 def test_async_option_range(ctx):
-    for bad in (2, -1):
+    """0 = off, 1 = on with the default lanes, 2..4 = that many lanes; anything else is refused."""
+    for bad in (5, -1, 2**32):
         with pytest.raises(_capi.VrhError):
             ctx.set_option("async_frames", bad)
-    ctx.set_option("async_frames", 0)
+    for ok in (1, 2, 3, 4, 0):
+        ctx.set_option("async_frames", ok)
 
 
 def test_full_frame_hf1M_async_shared_target(ctx, golden, oracle_mod):

@@ -163,7 +163,7 @@ OPTION_RANGES = {
     "block_threads": (0, 256), "stack_cap": (0, 640), "blocks_per_cu": (0, 32), "refill_min": (0, 64),
     "descent_cap": (0, 1024), "cluster_tiles": (0, 1024), "wide_anyhit": (0, 2), "pop_on_miss": (0, 2),
     "scalar_fetch": (0, 2), "pair_layout": (0, 2), "ao_gate": (0, 2), "ao_share": (0, 2), "ao_cut": (0, 3),
-    "xcd_queues": (0, 4), "wave_times": (0, 2), "exact_minmax": (0, 1), "async_frames": (0, 1),
+    "xcd_queues": (0, 4), "wave_times": (0, 2), "exact_minmax": (0, 1), "async_frames": (0, 4),
     "waves_per_simd": (0, 8), "ao_schedule": (0, 4), "coop_fetch": (0, 2), "quad_refill": (0, 1),
     "group_units": (0, 1), _capi.VRH_OPT_AO_STEAL: (0, 2),
 }

@@ -27,7 +27,7 @@ cam, W, H = scenes.scene_camera(scene)
 basis = cam.basis(W, H)
 kern = va.ao_kernel(dev)
 rt = va.hip_buffer_rt(ctx, W, H * F)
-out = {"scene": scene, "depth": int(host.depth), "frames_per_launch": F, "launches": launches, "caps": {}}
+out = {"scene": scene, "depth": int(host.max_depth), "frames_per_launch": F, "launches": launches, "caps": {}}
 fn = 1
 for cap in caps:
     ctx.set_option("stack_cap", cap)

@@ -105,7 +105,11 @@ constexpr int COUNTERS_LINES = 80;      // [80] L1 128-B lines, [81] wave-level 
                                         // [83] 4-lane-group accesses, [84] ideal-grouping accesses (counting variant)
 constexpr int COUNTERS_TOTAL = 208;     // u64 words [208], [209]: totals
 constexpr int COUNTERS_WORDS = 256;
-constexpr int COUNTER_BLOCKS = 3;      // per context: frames on its stream + one per asynchronous frame lane
+constexpr int VRH_MAX_FRAME_LANES = 4;  // asynchronous frames: frame lanes of a context, at most
+#ifndef VRH_DEFAULT_FRAME_LANES
+#define VRH_DEFAULT_FRAME_LANES 3       // VRH_OPT_ASYNC_FRAMES = 1
+#endif
+constexpr int COUNTER_BLOCKS = 1 + VRH_MAX_FRAME_LANES;   // per context: frames on its stream + one per frame lane
 
 struct launch_config
 {

@@ -34,8 +34,8 @@ struct vrh_ctx
     vrh_frame_stats last{};
     bool have_frame = false;
     // asynchronous frames (VRH_OPT_ASYNC_FRAMES, cuda_sched's issue model, cuda_sched.inl:306-320):
-    // frames alternate between two frame lanes (streams of their own), so frame k + 1's waves take
-    // the CUs that frame k's launch tail leaves idle.  Each lane has its own counter block and stack
+    // frames go round robin over `num_lanes` frame lanes (streams of their own; 2-4, VRH_OPT_ASYNC_FRAMES),
+    // so frame k + 1's waves take the CUs that frame k's launch tail leaves idle.  Each lane has its own counter block and stack
     // overflow block; a target written by the other lane is rendered into the lane's scratch target
     // and copied in issue order (vrh_runtime.hip issue_async).  Work on `stream` joins the lanes
     // first (ctx_join): it waits for every frame issued so far.
@@ -59,8 +59,9 @@ struct vrh_ctx
         vrh_rt* pending_rt = nullptr;
         uint32_t pending_clip[4] = {};
         bool pending_fields[4] = {};      // colour, prim id, t, occlusion
-    } lane[2];
+    } lane[vrh::VRH_MAX_FRAME_LANES];
     uint32_t next_lane = 0;
+    uint32_t num_lanes = 2;                     // frame lanes in use (VRH_OPT_ASYNC_FRAMES)
     hipEvent_t main_mark = nullptr;             // position of `stream` that an async frame waits for
     mutable uint64_t join_epoch = 0;            // incremented by every join of the lanes into `stream`
     unsigned long long* last_counters = nullptr;    // counter block of the last frame (vrh_last_frame_stats)
@@ -148,7 +149,7 @@ inline hipError_t mark_written(vrh_rt* rt, hipStream_t stream)
 // asynchronous frames: `stream` waits for every frame issued on the context's frame lanes so far
 // (no host synchronisation).  Every entry point that issues work on `stream` or synchronises it calls
 // this first, so work issued after a frame sees that frame's results.
-// issue the pending scratch copy of lane `l` (vrh_runtime.hip); l < 0: both lanes
+// issue the pending scratch copy of lane `l` (vrh_runtime.hip); l < 0: every lane
 hipError_t ctx_flush_pending(const vrh_ctx* ctx, int l = -1);
 
 inline hipError_t ctx_join(const vrh_ctx* ctx)

@@ -101,7 +101,7 @@ VRH_API int vrh_ctx_create_on_stream(int hip_device, void* hip_stream, vrh_ctx**
         e = hipMemset(ctx->counters, 0, COUNTER_BLOCKS * COUNTERS_WORDS * sizeof(unsigned long long));
         if (e != hipSuccess) { set_error(hipGetErrorString(e)); rc = VRH_ERR_HIP; break; }
         ctx->last_counters = ctx->counters;
-        for (int i = 0; i < 2; ++i) ctx->lane[i].counters = ctx->counters + size_t(i + 1) * COUNTERS_WORDS;
+        for (int i = 0; i < VRH_MAX_FRAME_LANES; ++i) ctx->lane[i].counters = ctx->counters + size_t(i + 1) * COUNTERS_WORDS;
     } while (0);
     if (rc != VRH_OK) { vrh_ctx_destroy(ctx); return rc; }
     *out = ctx;
@@ -114,7 +114,9 @@ VRH_API int vrh_ctx_get_stream(const vrh_ctx* ctx, int* hip_device, void** hip_s
 {
     VRH_CHECK(ctx, "vrh_ctx_get_stream: null context");
     // work the caller issues on the stream comes after every frame issued so far (asynchronous frames)
-    if (hip_stream && (ctx->lane[0].used || ctx->lane[1].used))
+    bool lanes_used = false;
+    for (const auto& l : ctx->lane) lanes_used |= l.used;
+    if (hip_stream && lanes_used)
     {
         VRH_HIP(hipSetDevice(ctx->device));
         VRH_HIP(ctx_join(ctx));
@@ -178,7 +180,7 @@ constexpr option_range k_option_ranges[] = {
     { VRH_OPT_CLUSTER_TILES, 0, 1024, "cluster tiles is 0 (auto) or 1..1024" },
     { VRH_OPT_QUAD_REFILL, 0, 1, "the quad-coherent hand-out was removed (0 is accepted)" },
     { VRH_OPT_GROUP_UNITS, 0, 1, "the block-shared hand-out was removed (0 is accepted)" },
-    { VRH_OPT_ASYNC_FRAMES, 0, 1, "asynchronous frames is 1 (on) or 0 (off)" },
+    { VRH_OPT_ASYNC_FRAMES, 0, VRH_MAX_FRAME_LANES, "asynchronous frames is 0 (off), 1 (on, the default number of frame lanes) or 2..4 (on, that many frame lanes)" },
 };
 
 VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
@@ -232,7 +234,20 @@ VRH_API int vrh_ctx_set_option(vrh_ctx* ctx, uint32_t option, int64_t value)
         // measured in round 4 and removed (slower: profiles/r04/ab/lane_layout/); 0 is accepted
         if (v != 0) { set_error("vrh_ctx_set_option: the quad-coherent and block-shared hand-outs were removed (they measured slower)"); return VRH_ERR_UNSUPPORTED; }
         break;
-    case VRH_OPT_ASYNC_FRAMES: ctx->opt_async = v; break;
+    case VRH_OPT_ASYNC_FRAMES:
+    {
+        // a different lane count: every frame issued so far is joined into the context stream first
+        const uint32_t lanes = v == 1 ? uint32_t(VRH_DEFAULT_FRAME_LANES) : v > 1 ? uint32_t(v) : ctx->num_lanes;
+        if (lanes != ctx->num_lanes)
+        {
+            VRH_HIP(hipSetDevice(ctx->device));
+            VRH_HIP(ctx_join(ctx));
+            ctx->num_lanes = lanes;
+            ctx->next_lane = 0;
+        }
+        ctx->opt_async = v ? 1 : 0;
+        break;
+    }
     case VRH_OPT_CLUSTER_TILES: ctx->opt_cluster = v; break;
     default: set_error("vrh_ctx_set_option: unknown option"); return VRH_ERR_INVALID;
     }
@@ -904,7 +919,7 @@ __global__ void copy_clip_kernel(float4* color, uint32_t* pid, float* t, uint8_t
 hipError_t ctx_flush_pending(const vrh_ctx* cctx, int only)
 {
     vrh_ctx* ctx = const_cast<vrh_ctx*>(cctx);
-    for (int l = 0; l < 2; ++l)
+    for (int l = 0; l < VRH_MAX_FRAME_LANES; ++l)
     {
         if (only >= 0 && l != only) continue;
         vrh_ctx::lane_t& L = ctx->lane[l];
@@ -1365,8 +1380,8 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
     float4* dst_color = p.color; uint32_t* dst_pid = p.prim_id; float* dst_t = p.t; uint8_t* dst_occ = p.occ;
     if (async)
     {
-        // cuda_sched issues a frame and returns (cuda_sched.inl:306-320): frames alternate between two
-        // lanes, so this frame's waves fill the CUs the previous frame's launch tail leaves idle
+        // cuda_sched issues a frame and returns (cuda_sched.inl:306-320): frames go round robin over the
+        // frame lanes, so this frame's waves fill the CUs the earlier frames' launch tails leave idle
         const uint32_t li = ctx->next_lane;
         L = &ctx->lane[li];
         if (!L->stream)
@@ -1376,7 +1391,7 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
         }
         if (!ctx->main_mark) VRH_HIP(hipEventCreateWithFlags(&ctx->main_mark, hipEventDisableTiming));
         if (!rt->lane_written) VRH_HIP(hipEventCreateWithFlags(&rt->lane_written, hipEventDisableTiming));
-        ctx->next_lane ^= 1u;
+        ctx->next_lane = (ctx->next_lane + 1u) % ctx->num_lanes;
         S = L->stream;
         ctr = L->counters;
         spill = &L->spill;
@@ -1393,7 +1408,7 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
         const bool scratch_ok = num_frames == 1 && (k->kind == VRH_KERNEL_PRIMARY || ao) && (!sp || sp->blend == 0);
         const uint32_t* cl = p.cam[0].clip;
         const bool fields[4] = { dst_color != nullptr, dst_pid != nullptr, dst_t != nullptr, dst_occ != nullptr };
-        for (uint32_t l = 0; l < 2; ++l)
+        for (uint32_t l = 0; l < uint32_t(VRH_MAX_FRAME_LANES); ++l)
         {
             vrh_ctx::lane_t& Q = ctx->lane[l];
             if (!Q.pending_rt) continue;
@@ -1661,20 +1676,20 @@ VRH_API int vrh_get_accum_stats(vrh_ctx* ctx, vrh_accum_stats* out)
     }
     if (a.timed_frames == 0) a.kernel_ms_min = 0.0;
     // first launch's start to the last launch's end: overlapping (asynchronous) frames count once
-    // (asynchronous frames alternate between two frame lanes: the second-to-last frame can end after the
-    // last one, and the second frame can start before the first -- the span runs from the earliest of
-    // the first two starts to the latest of the last two ends, all measured from the first start)
+    // (asynchronous frames go round robin over the frame lanes: one of the last frames can end after the
+    // last one, and a later frame can start before the first -- the span runs from the earliest start of
+    // the first VRH_MAX_FRAME_LANES frames to the latest end of the last ones, measured from the first start)
     if (a.frames >= 1 && a.frames <= VRH_MAX_TIMED_FRAMES)
     {
-        float end = 0.0f, begin = 0.0f;
-        VRH_HIP(hipEventElapsedTime(&end, ctx->ev_start[0], ctx->ev_stop[a.frames - 1]));
-        if (a.frames >= 2)
+        float end = -1e30f, begin = 0.0f;
+        const uint32_t w = std::min<uint32_t>(a.frames, uint32_t(VRH_MAX_FRAME_LANES));
+        for (uint32_t i = 0; i < w; ++i)
         {
-            float e2 = 0.0f, s2 = 0.0f;
-            VRH_HIP(hipEventElapsedTime(&e2, ctx->ev_start[0], ctx->ev_stop[a.frames - 2]));
-            VRH_HIP(hipEventElapsedTime(&s2, ctx->ev_start[0], ctx->ev_start[1]));
-            end = std::max(end, e2);
-            begin = std::min(begin, s2);
+            float e = 0.0f, s = 0.0f;
+            VRH_HIP(hipEventElapsedTime(&e, ctx->ev_start[0], ctx->ev_stop[a.frames - 1 - i]));
+            VRH_HIP(hipEventElapsedTime(&s, ctx->ev_start[0], ctx->ev_start[i]));
+            end = std::max(end, e);
+            begin = std::min(begin, s);
         }
         a.span_ms = double(end) - double(begin);
     }
