@@ -293,7 +293,7 @@ enum vrh_option {
                                     C3 / C4 launches, profiles/r03_ab/ao_share/)                    */
     VRH_OPT_ASYNC_FRAMES = 26,   /* 1: frames are issued like cuda_sched issues them (cuda_sched.inl:306-320,
                                     no synchronisation): they go round robin over the frame lanes of
-                                    the context (HIP streams of its own; 3 lanes, or 2..4 given as
+                                    the context (HIP streams of its own; 2 lanes, or 2..4 given as
                                     the value), so the next frames' waves take the CUs the earlier
                                     frames' launch tails leave idle (changing the lane count first
                                     waits, on the device, for every frame issued so far).

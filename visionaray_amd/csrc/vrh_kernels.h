@@ -107,7 +107,11 @@ constexpr int COUNTERS_TOTAL = 208;     // u64 words [208], [209]: totals
 constexpr int COUNTERS_WORDS = 256;
 constexpr int VRH_MAX_FRAME_LANES = 4;  // asynchronous frames: frame lanes of a context, at most
 #ifndef VRH_DEFAULT_FRAME_LANES
-#define VRH_DEFAULT_FRAME_LANES 3       // VRH_OPT_ASYNC_FRAMES = 1
+// VRH_OPT_ASYNC_FRAMES = 1.  Measured (round 6, tools/async_lanes_ab.py, ten frames into one target,
+// profiles/r06/async_lanes/): 3 lanes 8-10 % slower than 2 on C2 / C3 / C4 / C5, 4 lanes within -1..+1 %
+// of 2.  Why 3 loses is not established (the process has 4 hardware queues, GPU_MAX_HW_QUEUES, for the
+// context stream and the lanes); 2 stays the default, 3 and 4 are selectable and tested
+#define VRH_DEFAULT_FRAME_LANES 2
 #endif
 constexpr int COUNTER_BLOCKS = 1 + VRH_MAX_FRAME_LANES;   // per context: frames on its stream + one per frame lane
 
