@@ -165,7 +165,7 @@ public:
         if (opt == VRH_OPT_ASYNC_FRAMES) async_frames_ = value != 0;
     }
     // cuda_sched's issue model (cuda_sched.inl:306-320): hip_sched::frame returns once the frame is
-    // issued; back-to-back frames overlap their launch tails on the context's two frame lanes, and
+    // issued; back-to-back frames overlap their launch tails on the context's frame lanes, and
     // hip_buffer_rt::download / sync() wait for them (vrh.h VRH_OPT_ASYNC_FRAMES)
     void set_async_frames(bool on) { set_option(VRH_OPT_ASYNC_FRAMES, on ? 1 : 0); }
     bool async_frames() const { return async_frames_; }
