@@ -282,6 +282,38 @@ def test_user_stream_work_after_async_frames(ctx, scene):
     assert np.array_equal(got, want)
 
 
+def test_lane_count_changed_between_frames(ctx, scene, lanes):
+    """Changing the number of frame lanes while frames are in flight first joins every lane: frames
+    issued on 4 lanes, then on 2, then on 3, into one shared target and a second target, leave the
+    synchronous run's bits."""
+    if lanes != 2:
+        pytest.skip("one run is enough: the lane counts are switched inside the test")
+    dev = scene
+    cams = frame_cameras(NAME, W, H, 6)
+    k = va.ao_kernel(dev)
+    sched = va.hip_sched(ctx)
+    plan = [(4, 0), (4, 1), (4, 0), (2, 0), (2, 1), (3, 0), (3, 0), (3, 1), (4, 0)]
+
+    def run(async_on):
+        rts = [va.hip_buffer_rt(ctx, W, H) for _ in range(2)]
+        try:
+            for i, (n, ti) in enumerate(plan):
+                ctx.set_option("async_frames", n if async_on else 0)
+                base_cam, _, _ = scenes.scene_camera(NAME, W, H)
+                sp = va.make_sched_params(U, base_cam, rts[ti])
+                sp.cam = _basis_camera(cams[i % 6])
+                sched.frame(k, sp, frame_num=20 + i)
+            return [_bits(rt.download()) for rt in rts]
+        finally:
+            ctx.set_option("async_frames", 0)
+            for rt in rts:
+                rt.close()
+
+    want, got = run(False), run(True)
+    for i, (a, b) in enumerate(zip(got, want)):
+        _same(a, b, f"target {i}")
+
+
 def test_async_option_range(ctx):
     """0 = off, 1 = on with the default lanes, 2..4 = that many lanes; anything else is refused."""
     for bad in (5, -1, 2**32):
