@@ -45,7 +45,7 @@ Rank 0 prints one JSON line (the contract of the task statement) with:
     §8d algorithmic HBM bytes are kept as roofline.hbm_algorithmic (informational);
   * cpu_baseline: the reference's own SSE4 tiled_sched path (oracle/_ref, built from
     /root/reference by oracle/Makefile) on a bounded sample at threads = the CPUs the process may use
-    (cgroup quota) at most: the best of a cores/4, cores/2, cores - 1, cores sweep, 2 runs per point of 7 frames each,
+    (cgroup quota) at most: the best of a cores/4, cores/2, cores - 1, cores sweep, 3 runs per point of 7 frames each,
     the host's core count, quota and model, and the retries / stall seconds of tiled_sched stalls.
 
 Settle: after the W warm-up steps, untimed launches of the timed shape run for --settle-ms (300 ms) of
@@ -141,7 +141,7 @@ CPU_ATTEMPT_TIMEOUT_S = 90
 CPU_FRAMES = 7                  # timed frames per sweep point (median), after 1 warm-up frame
 
 
-CPU_RUNS = 2                    # runs per sweep point; the faster one counts (a run can only be slowed)
+CPU_RUNS = 3                    # runs per sweep point; the fastest one counts (a run can only be slowed)
 
 
 def cpu_sweep_points(cores, threads=None):
@@ -582,7 +582,7 @@ def main():
     single = None
     if world == 1 and args.single_frames > 0:
         rt_s = va.hip_buffer_rt(ctx, W, H)
-        sched = va.hip_sched(ctx)
+        sched = va.hip_sched(ctx, async_frames=False)       # frame() returns when the frame is done
         sp = va.make_sched_params(va.pixel_sampler.uniform_type, cam, rt_s)
         k_ms, wall_ms, rays = [], [], []
         sched.frame(kern, sp, frame_num=next_frame[0])     # warm-up of this launch shape
@@ -606,7 +606,7 @@ def main():
     # final sync, into one shared target and into two alternating targets (rank 0, N = 1)
     single_async = None
     if world == 1 and not grouped and args.single_frames > 0:
-        sched = va.hip_sched(ctx)
+        sched = va.hip_sched(ctx)                            # hip_sched's default: cuda_sched's issue model
         single_async = {"frames": args.single_frames,
                         "path": "hip_sched::frame x N, end_frame without sync, then one vrh_sync: frames "
                                 "alternate between the context's two frame lanes (vrh.h VRH_OPT_ASYNC_FRAMES)"}

@@ -740,9 +740,15 @@ template <typename R>
 class hip_sched
 {
 public:
-    explicit hip_sched(std::shared_ptr<hip_context> ctx = hip_context::default_context())
+    // cuda_sched's issue model by default (cuda_sched.inl:306-320: frame() enqueues and returns,
+    // gpu_buffer_rt::end_frame is a no-op, gpu_buffer_rt.inl:84-86): the scheduler turns on its
+    // context's asynchronous frames (VRH_OPT_ASYNC_FRAMES), so back-to-back frame() calls overlap their
+    // launch tails and hip_buffer_rt::download / hip_context::sync wait for them; async_frames = false
+    // keeps a frame() that returns only when the frame is done (tiled_sched's behaviour)
+    explicit hip_sched(std::shared_ptr<hip_context> ctx = hip_context::default_context(), bool async_frames = true)
         : ctx_(std::move(ctx))
     {
+        ctx_->set_async_frames(async_frames);
     }
 
     // multi-GPU: frames sharded over a render group; `shards` image-tile shards

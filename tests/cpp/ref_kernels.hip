@@ -332,6 +332,7 @@ int main(int argc, char** argv)
                     auto t0 = std::chrono::steady_clock::now();
                     if (F == 1) sched.frame(kernel, sparams, unsigned(l));
                     else sched.frames(kernel, cams, rtF, unsigned(l * F));
+                    hip_context::default_context()->sync();  // frame() only issues the launch (cuda_sched's model)
                     auto t1 = std::chrono::steady_clock::now();
                     if (l > 0) ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count() / F);
                 }

@@ -55,7 +55,7 @@ def main():
         "whitted_face_4": va.whitted_kernel(dev, sh, bg=bg, ambient=amb, num_bounces=4, epsilon=1e-3),
         "multi_hit_16": va.multi_hit_kernel(dev, sh, max_hits=16),
     }
-    sched = va.hip_sched(ctx)
+    sched = va.hip_sched(ctx, async_frames=False)      # timed: frame() returns when the frame is done
     sp = va.make_sched_params(va.pixel_sampler.uniform_type, cam, rt)
     F = a.frames_per_launch
     if F > 1:

@@ -692,15 +692,18 @@ def whitted_kernel(bvh, shade, binding=normals_per_face_binding, bg=(0.0, 0.0, 0
 class hip_sched:
     """hip_sched<R>: drop-in for cuda_sched<R> (cuda_sched.h:25-40).
 
-    frame() = rt.begin_frame() -> vrh_render -> rt.end_frame() (end_frame syncs, so frame() is
-    synchronous like tiled_sched).  shard=(index, count, packed) renders only that image-tile shard.
-    With ctx.set_option("async_frames", 1) frame() returns once the frame is issued, as cuda_sched's
-    does (cuda_sched.inl:306-320): back-to-back frames overlap their launch tails on the context's two
-    frame lanes; rt.download() / ctx.sync() wait for them (VRH_OPT_ASYNC_FRAMES).
+    frame() = rt.begin_frame() -> vrh_render -> rt.end_frame().  By default the scheduler issues frames
+    as cuda_sched does (cuda_sched.inl:306-320: frame() enqueues and returns, gpu_buffer_rt::end_frame
+    is a no-op, gpu_buffer_rt.inl:84-86): it turns on its context's asynchronous frames, back-to-back
+    frames overlap their launch tails on the context's frame lanes, and rt.download() / ctx.sync() wait
+    for them (VRH_OPT_ASYNC_FRAMES).  hip_sched(ctx, async_frames=False) keeps frame() synchronous (it
+    returns when the frame is done, like tiled_sched).  shard=(index, count, packed) renders only that
+    image-tile shard.
     """
 
-    def __init__(self, ctx):
+    def __init__(self, ctx, async_frames=True):
         self.ctx = ctx
+        ctx.set_option("async_frames", 1 if async_frames else 0)
 
     def frame(self, kernel, sparams, frame_num=0, shard=None, sync=True):
         if not isinstance(kernel, _builtin_kernel):

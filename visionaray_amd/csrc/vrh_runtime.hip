@@ -91,7 +91,10 @@ VRH_API int vrh_ctx_create_on_stream(int hip_device, void* hip_stream, vrh_ctx**
         if (hip_stream) ctx->stream = static_cast<hipStream_t>(hip_stream);
         else
         {
-            e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+            // a blocking stream (round 6): like the default stream cuda_sched launches on
+            // (cuda_sched.inl:306-320), it is ordered against work on the NULL stream -- a program that
+            // reads a target with a plain hipMemcpy after an asynchronous frame() sees the frame
+            e = hipStreamCreateWithFlags(&ctx->stream, hipStreamDefault);
             if (e != hipSuccess) { set_error(hipGetErrorString(e)); rc = VRH_ERR_HIP; break; }
             ctx->own_stream = true;
         }
@@ -1386,7 +1389,7 @@ int render_batch_impl(vrh_ctx* ctx, const vrh_scene* sc, vrh_rt* rt, const vrh_c
         L = &ctx->lane[li];
         if (!L->stream)
         {
-            VRH_HIP(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking));
+            VRH_HIP(hipStreamCreateWithFlags(&L->stream, hipStreamDefault));    // blocking: see vrh_ctx_create
             VRH_HIP(hipEventCreateWithFlags(&L->done, hipEventDisableTiming));
         }
         if (!ctx->main_mark) VRH_HIP(hipEventCreateWithFlags(&ctx->main_mark, hipEventDisableTiming));
