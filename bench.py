@@ -156,7 +156,7 @@ def cpu_sweep_points(cores, threads=None):
 def cpu_baseline(scene, kernel, threads=None):
     """Reference SSE4 tiled_sched<ray4> (oracle/_ref/vsnray_ref_bench) on a bounded sample: the same
     scene and camera at full resolution, 1 warm-up + CPU_FRAMES timed frames per run, the median
-    frame; CPU_RUNS runs per point, the faster counts.  Points: cores/4, cores/2, cores - 1 and cores
+    frame; CPU_RUNS runs per point, the fastest counts.  Points: cores/4, cores/2, cores - 1 and cores
     (the CPUs this process may use: the cgroup quota, else the affinity mask), never more.  `value` is
     the best point.  At threads = cores the workers alone fill the quota, so any other thread of the
     container (the Python parent, the HIP runtime) makes CFS throttle all of them: round 6 measured
@@ -215,7 +215,7 @@ def cpu_baseline(scene, kernel, threads=None):
                 "kind": "reference",
                 "sample": f"{scene} 1920x1080, {samples} AO spp, tiled_sched<basic_ray<simd::float4>> -O3 -msse4.1, "
                           f"best of a worker-thread sweep {counts} within the {cores} CPUs the process may use "
-                          f"(the faster of {CPU_RUNS} runs per point, each the median of {CPU_FRAMES} frames after 1 "
+                          f"(the fastest of {CPU_RUNS} runs per point, each the median of {CPU_FRAMES} frames after 1 "
                           f"warm-up; {at['rays_per_frame']} rays/frame)",
                 "sweep": sweep, "value_at_threads_eq_cores": at_cores,
                 "retries": retries, "stall_s": round(stall_s, 1), **info}
