@@ -1702,20 +1702,27 @@ __device__ inline bvh_record traverse_bvh_direct(basic_ray<float> const& ray, vr
             return result;
         }
     }
-    // the leaf: every primitive in index order, is_closer / update_if (intersect.inl:103-128)
-    walk<Any>(b, ray, max_t, [&]() { return result.t; },
-         [&](uint32_t i, uint32_t& flags) -> bool
-         {
-             HR hr;
-             if (b.prim_kind == VRH_PRIM_TRI64) hr = isect(ray, leaf_primitive<basic_triangle<3, float>>(prims, i, flags));
-             else hr = isect(ray, leaf_primitive<basic_sphere<float>>(prims, i, flags));
-             if (is_closer(hr, static_cast<HR const&>(result), max_t))
+    // the leaf: every primitive in index order, is_closer / update_if (intersect.inl:103-128).  One walk
+    // per primitive type, chosen by the (wave-uniform) scene kind, so the leaf step of the walk tests
+    // one type of primitive (C3, AO lambda: 1.699 vs 1.721 ms per frame with the kind tested per
+    // primitive, 2.045 vs 2.108 at one frame per launch, profiles/r06/user_walk/kind_walks.log)
+    auto walk_prims = [&](auto prim_tag)
+    {
+        using P = decltype(prim_tag);
+        walk<Any>(b, ray, max_t, [&]() { return result.t; },
+             [&](uint32_t i, uint32_t& flags) -> bool
              {
-                 result = bvh_record(hr, i);
-                 if (Any) return true;                     // exit_traversal.h:49-56
-             }
-             return false;
-         });
+                 const HR hr = isect(ray, leaf_primitive<P>(prims, i, flags));
+                 if (is_closer(hr, static_cast<HR const&>(result), max_t))
+                 {
+                     result = bvh_record(hr, i);
+                     if (Any) return true;                     // exit_traversal.h:49-56
+                 }
+                 return false;
+             });
+    };
+    if (b.prim_kind == VRH_PRIM_TRI64) walk_prims(basic_triangle<3, float>());
+    else walk_prims(basic_sphere<float>());
     return result;
 }
 
