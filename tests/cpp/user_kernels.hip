@@ -592,17 +592,19 @@ int main(int argc, char** argv)
                 }
                 return result;
             };
-            std::vector<camera> cams(3, cam);
-            cams[1].look_at(vec3(0.0f, 1.0f, 1.4f), vec3(0.0f), vec3(0.0f, 1.0f, 0.0f));
-            cams[2].look_at(vec3(0.0f, 1.1f, 1.4f), vec3(0.0f), vec3(0.0f, 1.0f, 0.0f));
+            // [nframes]: frames per launch (default 3), the eye raised by 0.1 per frame
+            const size_t NF = argc > 7 ? size_t(strtoul(argv[7], nullptr, 10)) : 3u;
+            std::vector<camera> cams(NF, cam);
+            for (size_t f = 1; f < NF; ++f)
+                cams[f].look_at(vec3(0.0f, 0.9f + 0.1f * float(f), 1.4f), vec3(0.0f), vec3(0.0f, 1.0f, 0.0f));
             hip_buffer_rt<PF_RGBA32F, PF_UNSPECIFIED> rt3;
-            rt3.resize(W, 3 * H);
+            rt3.resize(W, unsigned(NF) * H);
             sched.frames(k, cams, rt3, frame_num);
             const size_t n = size_t(W) * H;
-            std::vector<float> c3(12 * n), t3(3 * n), c1(4 * n), t1(n);
+            std::vector<float> c3(4 * NF * n), t3(NF * n), c1(4 * n), t1(n);
             rt3.download(c3.data(), nullptr, t3.data());
             bool ok = true, distinct = false;
-            for (size_t f = 0; f < 3; ++f)
+            for (size_t f = 0; f < NF; ++f)
             {
                 auto sp = make_sched_params(pixel_sampler::uniform_type{}, cams[f], rt);
                 sched.frame(k, sp, frame_num + unsigned(f));

@@ -256,12 +256,13 @@ def test_user_kernel_over_bvh_list_with_scissor_matches_reference(tmp_path, gold
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("scene,W,H", [("hf64", 160, 90), ("hf200", 333, 181)])
-def test_user_kernel_frames_in_flight_equal_single_frames(tmp_path, scene, W, H, ukbin):
-    """hip_sched::frames with a user kernel (one persistent launch, three cameras, frame numbers
-    f0 .. f0 + 2) equals three frame() calls bit for bit, and the frames differ (ragged width and
+@pytest.mark.parametrize("scene,W,H,nf", [("hf64", 160, 90, 3), ("hf200", 333, 181, 3), ("hf64", 160, 90, 8),
+                                          ("hf200", 333, 181, 32)])
+def test_user_kernel_frames_in_flight_equal_single_frames(tmp_path, scene, W, H, nf, ukbin):
+    """hip_sched::frames with a user kernel (one persistent launch, nf cameras, frame numbers
+    f0 .. f0 + nf - 1) equals nf frame() calls bit for bit, and the frames differ (ragged width and
     height: partial tiles at the right and bottom edges)."""
-    r = subprocess.run([BIN, "frames", str(GRID[scene]), str(W), str(H), str(tmp_path), "7"],
+    r = subprocess.run([BIN, "frames", str(GRID[scene]), str(W), str(H), str(tmp_path), "7", str(nf)],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert '"frames_ok":true' in r.stdout and '"distinct":true' in r.stdout
