@@ -396,6 +396,21 @@ __device__ inline vrh_scene_view uniform_view(vrh_scene_view const& v)
     return v;
 }
 
+// p as held by the wave's first active lane, and whether every active lane holds the same p: the
+// opt-in walks that keep one BVH's state for the whole wave (the shared any_hit walk, whose lanes take
+// over each other's subtrees; the entry cut's skeleton) need every lane on the same BVH.  (The scalar
+// fetches of wave-uniform records need no such check: a load through a divergent pointer is compiled
+// as a vector load -- tests/cpp/user_kernels.hip divbvh)
+template <typename T>
+__device__ __forceinline__ const T* first_lane_ptr(const T* p, bool& uniform)
+{
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint64_t af = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(a)))))
+                      | (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(a >> 32))))) << 32);
+    uniform = __ballot(a != af) == 0ull;
+    return reinterpret_cast<const T*>(af);
+}
+
 // the leaf primitive i of the device layout, rebuilt as a primitive object of type P (the
 // reference's basic_triangle<3,float> / basic_sphere<float>, or standalone.h's of the same layout)
 template <typename P>
@@ -629,6 +644,9 @@ __device__ inline uint32_t user_cut_entry(vrh_scene_view const& b, vrh::dev::ray
         shi[a] = o[a] + (t > 0.0f ? t : 0.0f);
         seg_ok = seg_ok & __builtin_isfinite(slo[a]) & __builtin_isfinite(shi[a]);
     }
+    bool same_bvh = false;
+    (void)first_lane_ptr(b.pairs, same_bvh);
+    if (!same_bvh) return b.root;                    // the skeleton is one BVH's: lanes on others start at the root
     const uint64_t key = (uint64_t)(uintptr_t)b.pairs;
     auto inside = [&]() {
         const bool have = cw[2] != 0u && cw[0] == (uint32_t)key && cw[1] == (uint32_t)(key >> 32);
@@ -1531,25 +1549,31 @@ VRH_FUNC inline auto intersect(
     if constexpr (Traversal == detail::AnyHit && VRH_USER_ANYHIT_SHARE)
     {
         // the shared any-hit walk (hip_detail::walk_shared): the same leaf step on the ray being
-        // traversed, into the record of this visit
-        if (view.max_depth >= VRH_USER_STACK) return result;
-        const vrh::dev::ray_t r = hip_detail::dev_ray(ray);
-        auto leaf2 = [&](vrh::dev::ray_t const& tr, float tmax, uint32_t i, uint32_t& flags, RT& rec) -> bool
+        // traversed, into the record of this visit -- when every lane of the wave walks the same BVH
+        // (a lane takes over another lane's subtrees); otherwise each lane walks its own below
+        bool same_bvh = false;
+        (void)hip_detail::first_lane_ptr(view.pairs, same_bvh);
+        if (same_bvh)
         {
-            const basic_ray<float> ray2(vector<3, float>(tr.ori.x, tr.ori.y, tr.ori.z), vector<3, float>(tr.dir.x, tr.dir.y, tr.dir.z));
-            const P prim = hip_detail::leaf_primitive<P>(prims, i, flags);
-            auto hr = HR(isect(ray2, prim), int(i));
-            auto closer = update_cond(hr, rec, tmax);
-            if (!any(closer)) return false;
-            update_if(rec, hr, closer);
-            detail::exit_traversal<Traversal> early_exit;
-            return early_exit.check(rec);
-        };
-        if (view.finite_bounds && __ballot(!vrh::dev::finite_ray(r)) == 0ull)
-            hip_detail::walk_shared<true>(view, r, max_t, result, leaf2);
-        else
-            hip_detail::walk_shared<false>(view, r, max_t, result, leaf2);
-        return result;
+            if (view.max_depth >= VRH_USER_STACK) return result;
+            const vrh::dev::ray_t r = hip_detail::dev_ray(ray);
+            auto leaf2 = [&](vrh::dev::ray_t const& tr, float tmax, uint32_t i, uint32_t& flags, RT& rec) -> bool
+            {
+                const basic_ray<float> ray2(vector<3, float>(tr.ori.x, tr.ori.y, tr.ori.z), vector<3, float>(tr.dir.x, tr.dir.y, tr.dir.z));
+                const P prim = hip_detail::leaf_primitive<P>(prims, i, flags);
+                auto hr = HR(isect(ray2, prim), int(i));
+                auto closer = update_cond(hr, rec, tmax);
+                if (!any(closer)) return false;
+                update_if(rec, hr, closer);
+                detail::exit_traversal<Traversal> early_exit;
+                return early_exit.check(rec);
+            };
+            if (view.finite_bounds && __ballot(!vrh::dev::finite_ray(r)) == 0ull)
+                hip_detail::walk_shared<true>(view, r, max_t, result, leaf2);
+            else
+                hip_detail::walk_shared<false>(view, r, max_t, result, leaf2);
+            return result;
+        }
     }
     // the ordered cooperative walk (hip_detail::walk_ordered): default intersector and update rule
     constexpr bool orderable = VRH_USER_ANYHIT_ORDERED && Traversal == detail::AnyHit && MultiHitMax == 1
@@ -1658,21 +1682,27 @@ __device__ inline bvh_record traverse_bvh_direct(basic_ray<float> const& ray, vr
     const float4* prims = static_cast<const float4*>(b.prims);
     if constexpr (Any && VRH_USER_ANYHIT_SHARE)
     {
-        if (b.max_depth >= VRH_USER_STACK) return result;
-        const vrh::dev::ray_t r = dev_ray(ray);
-        auto leaf2 = [&](vrh::dev::ray_t const& tr, float tmax, uint32_t i, uint32_t& flags, bvh_record& rec) -> bool
+        // lanes take over each other's subtrees: only when the wave walks one BVH
+        bool same_bvh = false;
+        (void)first_lane_ptr(b.pairs, same_bvh);
+        if (same_bvh)
         {
-            const basic_ray<float> ray2(vec3(tr.ori.x, tr.ori.y, tr.ori.z), vec3(tr.dir.x, tr.dir.y, tr.dir.z));
-            HR hr;
-            if (b.prim_kind == VRH_PRIM_TRI64) hr = isect(ray2, leaf_primitive<basic_triangle<3, float>>(prims, i, flags));
-            else hr = isect(ray2, leaf_primitive<basic_sphere<float>>(prims, i, flags));
-            if (!is_closer(hr, static_cast<HR const&>(rec), tmax)) return false;
-            rec = bvh_record(hr, i);
-            return true;                                      // exit_traversal.h:49-56
-        };
-        if (b.finite_bounds && __ballot(!vrh::dev::finite_ray(r)) == 0ull) walk_shared<true>(b, r, max_t, result, leaf2);
-        else walk_shared<false>(b, r, max_t, result, leaf2);
-        return result;
+            if (b.max_depth >= VRH_USER_STACK) return result;
+            const vrh::dev::ray_t r = dev_ray(ray);
+            auto leaf2 = [&](vrh::dev::ray_t const& tr, float tmax, uint32_t i, uint32_t& flags, bvh_record& rec) -> bool
+            {
+                const basic_ray<float> ray2(vec3(tr.ori.x, tr.ori.y, tr.ori.z), vec3(tr.dir.x, tr.dir.y, tr.dir.z));
+                HR hr;
+                if (b.prim_kind == VRH_PRIM_TRI64) hr = isect(ray2, leaf_primitive<basic_triangle<3, float>>(prims, i, flags));
+                else hr = isect(ray2, leaf_primitive<basic_sphere<float>>(prims, i, flags));
+                if (!is_closer(hr, static_cast<HR const&>(rec), tmax)) return false;
+                rec = bvh_record(hr, i);
+                return true;                                      // exit_traversal.h:49-56
+            };
+            if (b.finite_bounds && __ballot(!vrh::dev::finite_ray(r)) == 0ull) walk_shared<true>(b, r, max_t, result, leaf2);
+            else walk_shared<false>(b, r, max_t, result, leaf2);
+            return result;
+        }
     }
     if constexpr (Any && VRH_USER_ANYHIT_ORDERED && std::is_same<Isect, default_intersector>::value)
     {

@@ -705,6 +705,69 @@ int main(int argc, char** argv)
             rt.clear_color_buffer();
             sched.frame(ao_kernel(two, dnormals, default_intersector{}, W, frame_num), sparams, frame_num);
         }
+        else if (mode == "divbvh")
+        {
+            // lanes of one wave walking DIFFERENT BVHs in the same closest_hit / any_hit call (the BVH
+            // chosen per pixel, (x ^ y) & 1, of the triangles split by prim_id parity) against the same
+            // choice made after wave-uniform calls on both BVHs: equal bit for bit
+            const unsigned frame_num = argc > 6 ? unsigned(strtoul(argv[6], nullptr, 10)) : 0u;
+            std::vector<tri_t> part[2];
+            for (auto const& t : tris) part[t.prim_id % 2u].push_back(t);
+            auto h0 = build<index_bvh<tri_t>>(part[0].data(), part[0].size());
+            auto h1 = build<index_bvh<tri_t>>(part[1].data(), part[1].size());
+            hip_index_bvh<tri_t> d0(h0), d1(h1);
+            hip_bvh_ref const* two = to_device(std::vector<hip_bvh_ref>{ checked_ref(d0.ref()), checked_ref(d1.ref()) });
+            auto body = [=] __device__ (ray r, unsigned x, unsigned y, bool divergent) -> result_record<float>
+            {
+                const unsigned sel = (x ^ y) & 1u;
+                auto pick = [&](auto&& call) {
+                    if (divergent) return call(two + sel);
+                    auto a = call(two);
+                    auto b = call(two + 1);
+                    return sel ? b : a;
+                };
+                result_record<float> result;
+                result.color = vec4(__uint_as_float(0xFFFFFFFFu), -1.0f, 0.0f, 1.0f);
+                auto hr = pick([&](hip_bvh_ref const* p) { return closest_hit(r, p, p + 1); });
+                result.hit = hr.hit;
+                if (!hr.hit) return result;
+                hr.isect_pos = r.ori + r.dir * hr.t;
+                vec3 n = get_normal(dnormals, hr);
+                vec3 uu, vv, w = n;
+                make_orthonormal_basis(uu, vv, w);
+                unsigned mask = 0, recs = 0x811C9DC5u;
+                for (unsigned smp = 0; smp < 8; ++smp)
+                {
+                    vec3 s = hip_ao_sample(y * W + x, smp, frame_num);
+                    auto dir = normalize(s.x * uu + s.y * vv + s.z * w);
+                    ray ao(hr.isect_pos + dir * 1E-3f, dir);
+                    auto ar = pick([&](hip_bvh_ref const* p) { return any_hit(ao, p, p + 1, 0.1f); });
+                    if (ar.hit) mask |= 1u << smp;
+                    recs = (recs ^ (ar.hit ? unsigned(ar.prim_id) : 0xFFFFFFFFu)) * 16777619u;
+                }
+                // x, y, z: the primary record and the AO hit / miss bits; w: the any_hit records
+                result.color = vec4(__uint_as_float(unsigned(hr.prim_id)), hr.t, __uint_as_float(mask), __uint_as_float(recs));
+                return result;
+            };
+            std::vector<float> a(4 * size_t(W) * H), b(4 * size_t(W) * H);
+            sched.frame([=] __device__ (ray r, unsigned x, unsigned y) { return body(r, x, y, true); }, sparams, frame_num);
+            rt.download(a.data());
+            sched.frame([=] __device__ (ray r, unsigned x, unsigned y) { return body(r, x, y, false); }, sparams, frame_num);
+            rt.download(b.data());
+            size_t hits = 0;
+            bool same_hits = true;
+            for (size_t p = 0; p < size_t(W) * H; ++p)
+            {
+                uint32_t bits;
+                memcpy(&bits, &b[4 * p], 4);
+                hits += bits != 0xFFFFFFFFu;
+                same_hits = same_hits && std::memcmp(&a[4 * p], &b[4 * p], 12) == 0;
+            }
+            const bool same = std::memcmp(a.data(), b.data(), a.size() * 4) == 0;
+            printf("{\"mode\":\"divbvh\",\"same\":%s,\"same_hits\":%s,\"hits\":%zu}\n", same ? "true" : "false",
+                   same_hits ? "true" : "false", hits);
+            return same_hits && hits > 0 ? 0 : 1;
+        }
         else if (mode == "heart")
         {
             heart_intersector isect;

@@ -268,6 +268,34 @@ def test_user_kernel_frames_in_flight_equal_single_frames(tmp_path, scene, W, H,
     assert '"frames_ok":true' in r.stdout and '"distinct":true' in r.stdout
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene,W,H,frame", [("hf64", 160, 90, 0), ("hf200", 333, 181, 3)])
+def test_user_kernel_lanes_on_different_bvhs(tmp_path, scene, W, H, frame, ukbin):
+    """closest_hit / any_hit calls in which the lanes of a wave walk different BVHs (chosen per pixel)
+    give the records the same calls give when every lane walks the same BVH: the scalar-cache fetches
+    of wave-uniform records must not take one lane's BVH for another's (their roots share an index)."""
+    r = subprocess.run([BIN, "divbvh", str(GRID[scene]), str(W), str(H), str(tmp_path), str(frame)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert '"same":true' in r.stdout and '"same_hits":true' in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("binary", ["uk_share", "uk_oca", "uk_cut"])
+def test_any_hit_variants_with_lanes_on_different_bvhs(tmp_path, binary):
+    """The opt-in any_hit walks with the lanes of a wave on different BVHs: the shared walk (whose
+    lanes take over each other's subtrees) falls back to per-lane walks and keeps every hit / miss
+    answer (which hit it reports may differ by design); the ordered walk and the entry cut keep the
+    records too."""
+    b = os.path.join(ROOT, "build", "tests", binary)
+    assert os.path.exists(b), "make -C visionaray_amd cpp_tests"
+    r = subprocess.run([b, "divbvh", "200", "333", "181", str(tmp_path), "3"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert '"same_hits":true' in r.stdout
+    if binary != "uk_share":
+        assert '"same":true' in r.stdout
+
+
 def test_user_kernel_header_needs_hipcc(tmp_path):
     """hip_kernels.h is device code: a host compiler gets a clear error, not a silent host path."""
     src = tmp_path / "host.cpp"
