@@ -26,6 +26,7 @@
 
 #include "../vrh.h"
 
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <cstring>
@@ -67,6 +68,20 @@ namespace hip_detail
 inline void check(int rc, const char* what)
 {
     if (rc != VRH_OK) throw hip_error(what, rc);
+}
+
+// the deepest BVH this process has taken a ref of (hip_index_bvh::ref): a user-kernel launch
+// (visionaray_hip/hip_kernels.h) gives its threads the short LDS stack while every such BVH fits it
+inline std::atomic<uint32_t>& user_ref_depth()
+{
+    static std::atomic<uint32_t> d{ 0u };
+    return d;
+}
+inline void note_ref_depth(uint32_t depth)
+{
+    auto& d = user_ref_depth();
+    uint32_t cur = d.load(std::memory_order_relaxed);
+    while (depth > cur && !d.compare_exchange_weak(cur, depth, std::memory_order_release, std::memory_order_relaxed)) {}
 }
 
 template <typename T, typename = void> struct is_sphere : std::false_type {};
@@ -364,6 +379,7 @@ public:
     {
         hip_bvh_ref_t<Primitive> r{};
         hip_detail::check(vrh_scene_get_view(handle(), 0, &r.view), "vrh_scene_get_view");
+        hip_detail::note_ref_depth(r.view.max_depth);
         return r;
     }
 

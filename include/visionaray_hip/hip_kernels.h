@@ -72,6 +72,20 @@
 #ifndef VRH_USER_DEFER
 #define VRH_USER_DEFER 0          // deferred any_hit calls (below), opt-in
 #endif
+#ifndef VRH_USER_LDS_STACK
+// the stack entries per thread a launch gives in LDS while every BVH the program has taken a ref of
+// (hip_index_bvh::ref) is shallower than that; VRH_USER_STACK entries once one is deeper.  LDS bounded
+// the waves per CU: 64 lanes x 32 entries are 8 KB per one-wave block, and a CU held fewer than 20;
+// with 24 entries (6 KB) a CU holds 26 and the registers bound it (C3, the AO lambda: 1.698 -> 1.549
+// ms per frame at 6 waves / SIMD, ao/main.cpp's kernel 1.662 -> 1.490; profiles/r06/user_lds/).  The
+// opt-in walks below that keep their own state in the stack columns always take the whole stack.
+#if VRH_USER_DEFER || VRH_USER_ANYHIT_CUT || VRH_USER_ANYHIT_SHARE || VRH_USER_ANYHIT_ORDERED
+#define VRH_USER_LDS_STACK VRH_USER_STACK
+#else
+#define VRH_USER_LDS_STACK 24
+#endif
+#endif
+static_assert(VRH_USER_LDS_STACK >= 1 && VRH_USER_LDS_STACK <= VRH_USER_STACK, "VRH_USER_LDS_STACK: 1 .. VRH_USER_STACK");
 
 namespace visionaray
 {
@@ -451,15 +465,25 @@ __host__ __device__ inline P leaf_primitive(const float4* prims, uint32_t i, uin
     return p;
 }
 
-// the per-thread traversal stack: a column of the block's dynamic LDS (hip_sched's user-kernel
-// launch provides VRH_USER_STACK entries per thread)
+// the per-thread traversal stack: a column of the block's dynamic LDS.  With VRH_USER_LDS_STACK <
+// VRH_USER_STACK the launch gives either many entries per thread (USER_STACK_SIZED); the first LDS
+// word then holds that count (user_render writes it) and the columns start after it
+constexpr bool USER_STACK_SIZED = VRH_USER_LDS_STACK < VRH_USER_STACK;
+constexpr uint32_t USER_LDS_HEADER = USER_STACK_SIZED ? 1u : 0u;
+__device__ inline uint32_t user_stack_entries()
+{
+    extern __shared__ uint32_t vrh_user_smem[];
+    if constexpr (USER_STACK_SIZED) return (uint32_t)__builtin_amdgcn_readfirstlane((int)vrh_user_smem[0]);
+    return VRH_USER_STACK;
+}
 __device__ inline vrh::dev::lds_stack user_stack()
 {
     extern __shared__ uint32_t vrh_user_smem[];
     const uint32_t nthreads = blockDim.x * blockDim.y * blockDim.z;
     const uint32_t tid = threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z);
     vrh::dev::lds_stack st;
-    st.init(vrh_user_smem, tid, nthreads, VRH_USER_STACK, VRH_USER_STACK, nullptr);   // checked_ref: the BVH fits
+    const uint32_t n = user_stack_entries();
+    st.init(vrh_user_smem + USER_LDS_HEADER, tid, nthreads, n, n, nullptr);   // walk(): the BVH fits
     return st;
 }
 
@@ -750,7 +774,7 @@ __device__ inline void walk_slab(vrh_scene_view const& b, vrh::dev::ray_t const&
 {
     using vrh::dev::LEAF_BIT;
     const float4* pairs = static_cast<const float4*>(b.pairs);
-    vrh::dev::lds_stack st = user_stack();
+    auto st = user_stack();
     // the pair record `link`: which children are hit (b0, b1), and whether child 0 is the near one
     auto step = [&](uint32_t link, bool& b0, bool& b1, uint32_t& l0, uint32_t& l1, bool& go0)
     {
@@ -809,7 +833,7 @@ __device__ inline bool walk_quads(vrh_scene_view const& b, vrh::dev::ray_t const
 {
     using vrh::dev::QUAD_NONE;
     const float4* quads = static_cast<const float4*>(b.quads);
-    vrh::dev::lds_stack st = user_stack();
+    auto st = user_stack();
     st.push(0u);
     while (!st.empty())
     {
@@ -864,7 +888,7 @@ __device__ inline bool walk_quads(vrh_scene_view const& b, vrh::dev::ray_t const
 template <bool ANY = false, typename Ray, typename CullT, typename Leaf>
 __device__ inline void walk(vrh_scene_view const& b, Ray const& ray, float max_t, CullT const& cull_t, Leaf&& leaf)
 {
-    if (b.max_depth >= VRH_USER_STACK) return;
+    if (b.max_depth >= user_stack_entries()) return;
     const vrh::dev::ray_t r = dev_ray(ray);
     const bool fast = b.finite_bounds && vrh::dev::finite_ray(r);
     if constexpr (ANY && !VRH_USER_BINARY_ANYHIT)
@@ -1410,7 +1434,7 @@ __device__ inline void defer_trace_kind(uint32_t* a, unsigned long long* prof)
     const bool finite_scene = v.finite_bounds != 0u;
     float4* ent = defer_log(a);
     const uint16_t* pool = reinterpret_cast<const uint16_t*>(a + 88);
-    lds_stack st = user_stack();
+    auto st = user_stack();
     constexpr uint32_t IDLE = 0xFFFFFFFFu;
     uint32_t cur = IDLE, next = 0u;
     ray_t r{};
@@ -1948,6 +1972,7 @@ struct user_frames
     uint32_t matrix_cam;          // sched_params with camera matrices: their inverses (column-major)
     float inv_view[16], inv_proj[16];
     char* defer_log;              // VRH_USER_DEFER: DEFER_WAVE_BYTES per block of the grid
+    uint32_t stack_entries;       // LDS stack entries per thread of this launch (USER_STACK_SIZED)
 };
 
 // the primary ray through image position (fx, fy) (the pixel plus the sampler's offset) of camera c:
@@ -2139,6 +2164,12 @@ __global__ __launch_bounds__(64) VRH_USER_OCC void user_render(K kernel, user_fr
 // at 4: 1.750 vs 1.821 ms per frame (profiles/r06/user_loads/), so up to 64 B
 #define VRH_USER_AUTO_SCRATCH 64
 #endif
+#ifndef VRH_USER_AUTO_SCRATCH6
+// the 6-wave instance may spill more: with 24 LDS stack entries the AO lambda at 6 waves (80 VGPRs +
+// 108 B of scratch) ran 1.542 ms per frame against 1.607 at 5 (96 + 28 B), ao/main.cpp's kernel at 6
+// (80 + 216 B) 1.495 against 1.588 at 5 (96 + 20 B) (profiles/r06/user_lds/)
+#define VRH_USER_AUTO_SCRATCH6 256
+#endif
 #ifndef VRH_USER_MAX_DEVICES
 #define VRH_USER_MAX_DEVICES 64     // device ordinals the per-device launch choices are cached for
 #endif
@@ -2148,12 +2179,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void us
 {
     user_render_body<K, SK, SN, NC>(kernel, f);
 }
+template <typename K, uint32_t SK = VRH_SAMPLER_UNIFORM, uint32_t SN = 1, uint32_t NC = 1>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void user_render_w6(K kernel, user_frames<NC> f)
+{
+    user_render_body<K, SK, SN, NC>(kernel, f);
+}
 #endif
 
 template <typename K, uint32_t SK, uint32_t SN, uint32_t NC>
 __device__ __forceinline__ void user_render_body(K& kernel, user_frames<NC> const& f)
 {
     const uint32_t lane = threadIdx.y * 8u + threadIdx.x;
+    if constexpr (USER_STACK_SIZED)
+    {
+        extern __shared__ uint32_t vrh_user_smem[];
+        if (lane == 0u) vrh_user_smem[0] = f.stack_entries;        // the stack entries this launch gives
+        __syncthreads();
+    }
     if (VRH_USER_ANYHIT_CUT && lane == 0u) user_cut_area()[2] = 0u;     // no any_hit entry cut yet
     if (VRH_USER_DEFER && lane == 0u) defer_area()[0] = DEFER_OFF;
     unsigned long long prof[8] = {};         // VRH_DEFER_PROF
@@ -2278,8 +2320,13 @@ inline char* context_scratch(hip_context& ctx, size_t bytes)
 template <typename K, uint32_t SK, uint32_t SN, uint32_t NC>
 inline hipError_t launch_user_render(hip_context& ctx, K const& kernel, user_frames<NC>& f, hipStream_t stream)
 {
-    const size_t lds = (size_t(64) * VRH_USER_STACK + (VRH_USER_ANYHIT_CUT ? UCUT_WORDS : 0u) + (VRH_USER_DEFER ? DEFER_WORDS : 0u))
-                       * sizeof(uint32_t);
+    static_assert(!USER_STACK_SIZED || !(VRH_USER_DEFER || VRH_USER_ANYHIT_CUT || VRH_USER_ANYHIT_SHARE || VRH_USER_ANYHIT_ORDERED),
+                  "the deferred calls, the entry cut and the shared / ordered any_hit walks keep their state in whole LDS stack columns");
+    // the short stack while every BVH the program has taken a ref of fits it, else the whole stack
+    f.stack_entries = (USER_STACK_SIZED && user_ref_depth().load(std::memory_order_acquire) < VRH_USER_LDS_STACK) ? VRH_USER_LDS_STACK
+                                                                                                               : VRH_USER_STACK;
+    const size_t lds = (size_t(64) * f.stack_entries + USER_LDS_HEADER + (VRH_USER_ANYHIT_CUT ? UCUT_WORDS : 0u)
+                        + (VRH_USER_DEFER ? DEFER_WORDS : 0u)) * sizeof(uint32_t);
     auto fn = user_render<K, SK, SN, NC>;
     check(vrh_ctx_user_queues(ctx.get(), &f.queues), "vrh_ctx_user_queues");
     int dev = 0, cus = 0, per_cu = 0;
@@ -2289,27 +2336,37 @@ inline hipError_t launch_user_render(hip_context& ctx, K const& kernel, user_fra
     if (e != hipSuccess) return e;
 #if VRH_USER_AUTO_WAVES
     {
-        // once per kernel and device: the 5-wave instance if it holds more waves and spills (almost)
-        // nothing.  The answer is cached per device ordinal (devices of different architectures get
-        // their own), in atomics: 0 = not asked yet, 1 = keep the default instance, n + 1 = the 5-wave
-        // instance at n blocks per CU.  Two threads asking at once compute the same answer.
-        static std::atomic<int> w5_cache[VRH_USER_MAX_DEVICES];
+        // once per kernel and device: the instance for 5 or 6 waves / SIMD when it holds more waves per CU
+        // and spills at most VRH_USER_AUTO_SCRATCH (5) / VRH_USER_AUTO_SCRATCH6 (6) bytes per lane, the
+        // one with more waves first.  The answer is cached per device ordinal (devices of different
+        // architectures get their own), in atomics: 0 = not asked yet, else (waves << 8) | blocks per CU
+        // of the chosen instance.  Two threads asking at once compute the same answer.
+        static std::atomic<int> wave_cache[VRH_USER_MAX_DEVICES][2];     // [device][whole stack]
         auto fn5 = user_render_w5<K, SK, SN, NC>;
-        int w5 = (dev >= 0 && dev < VRH_USER_MAX_DEVICES) ? w5_cache[dev].load(std::memory_order_acquire) : 0;
-        if (w5 == 0)
+        auto fn6 = user_render_w6<K, SK, SN, NC>;
+        const int whole = f.stack_entries == VRH_USER_STACK ? 1 : 0;
+        int pick = (dev >= 0 && dev < VRH_USER_MAX_DEVICES) ? wave_cache[dev][whole].load(std::memory_order_acquire) : 0;
+        if (pick == 0)
         {
-            hipFuncAttributes a{};
-            int per_cu5 = 0;
-            if ((e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(fn5))) != hipSuccess) return e;
-            if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu5, fn5, 64, lds)) != hipSuccess) return e;
-            w5 = (per_cu5 > per_cu && a.localSizeBytes <= size_t(VRH_USER_AUTO_SCRATCH)) ? per_cu5 + 1 : 1;
-            if (dev >= 0 && dev < VRH_USER_MAX_DEVICES) w5_cache[dev].store(w5, std::memory_order_release);
+            pick = (1 << 8) | per_cu;
+            const std::pair<decltype(fn), int> cand[2] = { { fn6, VRH_USER_AUTO_SCRATCH6 }, { fn5, VRH_USER_AUTO_SCRATCH } };
+            for (int k = 0; k < 2; ++k)
+            {
+                hipFuncAttributes a{};
+                int n = 0;
+                if ((e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(cand[k].first))) != hipSuccess) return e;
+                if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, cand[k].first, 64, lds)) != hipSuccess) return e;
+                if (n > per_cu && a.localSizeBytes <= size_t(cand[k].second))
+                {
+                    pick = ((6 - k) << 8) | n;
+                    break;
+                }
+            }
+            if (dev >= 0 && dev < VRH_USER_MAX_DEVICES) wave_cache[dev][whole].store(pick, std::memory_order_release);
         }
-        if (w5 > 1)
-        {
-            fn = fn5;
-            per_cu = w5 - 1;
-        }
+        if ((pick >> 8) == 6) fn = fn6;
+        else if ((pick >> 8) == 5) fn = fn5;
+        per_cu = pick & 0xFF;
     }
 #endif
     const uint64_t work = uint64_t(f.tiles) * f.nframes;

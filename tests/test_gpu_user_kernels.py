@@ -137,12 +137,14 @@ def test_deferred_replay_with_more_calls_than_recorded(tmp_path, grid, W, H, fra
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,W,H,frame,radius", [(20000, 320, 180, 3, 0.3), (8000, 160, 90, 1, 0.8)])
+@pytest.mark.parametrize("n,W,H,frame,radius", [(20000, 320, 180, 3, 0.3), (8000, 160, 90, 1, 0.8),
+                                                 (1000000, 96, 54, 2, 0.05)])
 def test_user_kernel_on_spheres_closest_hit_and_deferred_records(tmp_path, oracle_mod, n, W, H, frame, radius):
     """closest_hit / any_hit over a sphere BVH (basic_sphere<float>, vrh_gen_spheres) in a user lambda:
     every pixel's closest hit (prim id, t) equals the oracle's primary render of the same scene and
     camera, and the deferred build (VRH_USER_DEFER=1, its trace on the sphere path) returns the direct
-    build's any_hit RECORDS for 8 rays per hit."""
+    build's any_hit RECORDS for 8 rays per hit.  1M spheres: a BVH 26 levels deep, deeper than the
+    short LDS stack (VRH_USER_LDS_STACK), so the launch gives the whole stack."""
     outs = []
     for b in (BIN, DEFER_BIN):
         assert os.path.exists(b), "run __graft_entry__.build() (make -C visionaray_amd cpp_tests)"
