@@ -32,8 +32,9 @@
 // index order), with the primitive test handed to the intersector, so the default intersector gives
 // the built-in kernels' bits.
 //
-// Device lambdas capture by value ([=]): they run on the GPU.  The traversal stack lives in LDS
-// (VRH_USER_STACK entries per thread); BVHs deeper than that are rejected by hip_bvh_ref checks.
+// Device lambdas capture by value ([=]): they run on the GPU.  The traversal stack lives in LDS (at most
+// VRH_USER_STACK entries per thread, VRH_USER_LDS_STACK while every BVH the program has taken a ref of
+// is shallower; below); BVHs deeper than VRH_USER_STACK are rejected by checked_ref.
 #pragma once
 
 #if !defined(__HIP__)
