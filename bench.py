@@ -274,16 +274,19 @@ def user_kernel_leg(W, H, n_rays):
     rec = {"frames_per_launch": leg["frames_per_launch"]}
     ms = leg["frame_ms_median"]
     # roofline of the user kernel, as the built-in's: the vector-L1 requests of the committed PMC pass of
-    # this program (profiles/pmc_user_lambda.json, kernel-source hash checked) x 16 B over the live launch
-    # time (median wall time of a 32-frame frames() launch: the kernel plus its launch, an upper bound)
+    # this program (profiles/pmc_user_lambda.json; the hash of libvrh's and the user-kernel headers'
+    # sources checked) x 16 B over the live launch time (median wall time of a 32-frame frames() launch:
+    # the kernel plus its launch, an upper bound)
     pmc = load_json(os.path.join(ROOT, "profiles", "pmc_user_lambda.json")) or {}
     roof = load_json(os.path.join(ROOT, "profiles", "l1_roof.json"))
-    from visionaray_amd.buildinfo import kernel_source_sha256
+    from visionaray_amd.buildinfo import user_kernel_source_sha256
     if (pmc.get("l1_requests_per_launch") and pmc.get("frames_per_launch") == rec["frames_per_launch"]
-            and pmc.get("kernel_source_sha256") == kernel_source_sha256() and roof):
+            and pmc.get("user_kernel_source_sha256") == user_kernel_source_sha256() and roof):
         launch_s = ms * 1e-3 * rec["frames_per_launch"]
         achieved = pmc["l1_requests_per_launch"] * L1_REQ_BYTES / launch_s / 1e9
         sq = load_json(os.path.join(ROOT, "profiles", "pmc_sq_lambda.json")) or {}
+        if sq.get("user_kernel_source_sha256") != user_kernel_source_sha256():
+            sq = {}
         leg["roofline"] = {"bound": "vmem-l1", "unit": "GB/s", "achieved": round(achieved, 1), "peak": roof.get("peak_gbs"),
                            "frac": round(achieved / roof["peak_gbs"], 4), "td_busy_frac": round(pmc["td_busy_frac"], 4),
                            "l1_requests_per_launch": pmc["l1_requests_per_launch"],

@@ -183,3 +183,17 @@ def test_kernel_source_hash_identifies_the_build(tmp_path):
         assert buildinfo.kernel_source_sha256() != h
     finally:
         buildinfo.kernel_sources = orig
+
+
+def test_user_kernel_source_hash_covers_the_user_kernel_headers():
+    """The user-kernel PMC passes (profiles/pmc_user_*.json, pmc_sq_lambda.json) are reported only for
+    the sources they were measured on: libvrh's kernel sources plus the device headers the user programs
+    are compiled from and the bench's user-kernel program."""
+    import os
+    from visionaray_amd import buildinfo
+    files = buildinfo.user_kernel_sources()
+    assert all(os.path.exists(p) for p in files)
+    for name in ("hip_kernels.h", "hip_backend.h", "vrh_device.h", "user_kernels.hip", "vrh_kernels.hip"):
+        assert any(os.path.basename(p) == name for p in files), name
+    h = buildinfo.user_kernel_source_sha256()
+    assert len(h) == 64 and h != buildinfo.kernel_source_sha256()

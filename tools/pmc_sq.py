@@ -46,8 +46,9 @@ def main():
            "wait_inst_share": c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"],
            "waves_per_launch": c["SQ_WAVES"]}
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    from visionaray_amd.buildinfo import kernel_source_sha256
+    from visionaray_amd.buildinfo import kernel_source_sha256, user_kernel_source_sha256
     res["kernel_source_sha256"] = kernel_source_sha256()
+    res["user_kernel_source_sha256"] = user_kernel_source_sha256()
     with open(out, "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
     print(json.dumps({k: v for k, v in res.items() if k != "counters_per_launch"}))

@@ -61,8 +61,9 @@ def main():
             name = name or n
     res = {"program": prog, "frames_per_launch": fpl, "kernel_name": name, "counters_per_launch": c}
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    from visionaray_amd.buildinfo import kernel_source_sha256
+    from visionaray_amd.buildinfo import kernel_source_sha256, user_kernel_source_sha256
     res["kernel_source_sha256"] = kernel_source_sha256()
+    res["user_kernel_source_sha256"] = user_kernel_source_sha256()
     ms = trace_ms(tdir) if tdir else None
     res["trace_ms_per_launch"] = ms
     if "TCP_TOTAL_CACHE_ACCESSES_sum" in c:

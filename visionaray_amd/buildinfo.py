@@ -17,10 +17,26 @@ def kernel_sources():
                     os.path.join(_ROOT, "include", "visionaray_hip", "detail", "vrh_device.h")]
 
 
-def kernel_source_sha256():
+def _sha256(files):
     h = hashlib.sha256()
-    for p in kernel_sources():
+    for p in files:
         h.update(os.path.relpath(p, _ROOT).encode())
         with open(p, "rb") as f:
             h.update(f.read())
     return h.hexdigest()
+
+
+def kernel_source_sha256():
+    return _sha256(kernel_sources())
+
+
+def user_kernel_sources():
+    """The user-kernel programs' sources on top of libvrh's: the device headers they are compiled from
+    (include/visionaray_hip) and the test program the bench's user leg runs."""
+    return (kernel_sources() + sorted(glob.glob(os.path.join(_ROOT, "include", "visionaray_hip", "*.h"))
+                                      + glob.glob(os.path.join(_ROOT, "include", "visionaray_hip", "detail", "*.h")))
+            + [os.path.join(_ROOT, "tests", "cpp", "user_kernels.hip")])
+
+
+def user_kernel_source_sha256():
+    return _sha256(user_kernel_sources())
