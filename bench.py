@@ -256,6 +256,9 @@ def user_program_run(prog, W, H, n_rays):
     # the lambda traces the built-in kernel's rays: the same primary rays, 8 AO rays per hit
     return {"mrays": round(n_rays / (ms * 1e-3) / 1e6, 1), "frame_ms_median": ms,
             "frames_per_launch": rec["frames_per_launch"], "launches": rec["launches"],
+            # the instance the launch took (register target: 0 = the compiler's own), its one-wave blocks
+            # per CU and the LDS stack entries per thread (hip_kernels.h launch_user_render)
+            "launch": rec.get("launch"),
             "program": "build/tests/%s bench 708 %d %d /tmp 4 32" % (prog, W, H)}
 
 

@@ -2316,6 +2316,22 @@ inline char* context_scratch(hip_context& ctx, size_t bytes)
     return static_cast<char*>(sb.mem.get());
 }
 
+// what the calling thread's last user-kernel launch chose: the instance's register target (0: the
+// compiler's own allocation, else 5 or 6 waves per SIMD), its one-wave blocks per CU, the LDS stack
+// entries per thread and the grid (the bench line reports them)
+struct user_launch_info
+{
+    int waves_target = 0;
+    int blocks_per_cu = 0;
+    uint32_t stack_entries = 0;
+    uint32_t grid = 0;
+};
+inline user_launch_info& last_user_launch()
+{
+    static thread_local user_launch_info info;
+    return info;
+}
+
 // launch `kern` over f on the context's stream: the queues zeroed first, then a grid of as many
 // one-wave blocks as the GPU holds at once (the kernel's own occupancy), at most one per tile
 template <typename K, uint32_t SK, uint32_t SN, uint32_t NC>
@@ -2368,11 +2384,17 @@ inline hipError_t launch_user_render(hip_context& ctx, K const& kernel, user_fra
         if ((pick >> 8) == 6) fn = fn6;
         else if ((pick >> 8) == 5) fn = fn5;
         per_cu = pick & 0xFF;
+        last_user_launch().waves_target = (pick >> 8) > 1 ? (pick >> 8) : 0;
     }
 #endif
     const uint64_t work = uint64_t(f.tiles) * f.nframes;
     const uint64_t resident = uint64_t(cus > 0 ? cus : 1) * uint64_t(per_cu > 0 ? per_cu : 1);
     const uint32_t grid = uint32_t(work < resident ? work : resident);
+    auto& info = last_user_launch();
+    if (!VRH_USER_AUTO_WAVES) info.waves_target = VRH_USER_WAVES;
+    info.blocks_per_cu = per_cu;
+    info.stack_entries = f.stack_entries;
+    info.grid = grid;
     if (VRH_USER_DEFER) f.defer_log = context_scratch(ctx, size_t(grid) * DEFER_WAVE_BYTES);
     if ((e = hipMemsetAsync(f.queues, 0, 8u * VRH_USER_QUEUE_STRIDE * sizeof(uint32_t), stream)) != hipSuccess) return e;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(8, 8), lds, stream, kernel, f);

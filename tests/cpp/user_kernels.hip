@@ -539,8 +539,11 @@ int main(int argc, char** argv)
                 if (l > 0) ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count() / F);
             }
             std::sort(ms.begin(), ms.end());
+            const auto& li = visionaray::hip_detail::last_user_launch();
             printf("{\"mode\":\"bench\",\"frame_ms_median\":%.4f,\"launches\":%d,\"frames_per_launch\":%d,"
-                   "\"kernel\":\"%s\"}\n", ms[ms.size() / 2], launches, F, F == 1 ? "ao lambda" : "random_sampler ao lambda");
+                   "\"kernel\":\"%s\",\"launch\":{\"waves_target\":%d,\"blocks_per_cu\":%d,\"stack_entries\":%u,\"grid\":%u}}\n",
+                   ms[ms.size() / 2], launches, F, F == 1 ? "ao lambda" : "random_sampler ao lambda",
+                   li.waves_target, li.blocks_per_cu, li.stack_entries, li.grid);
 #if VRH_DEFER_PROF
             {
                 // the blocks' phase counters at the head of their logs (hip_kernels.h VRH_DEFER_PROF)
