@@ -2339,9 +2339,15 @@ inline hipError_t launch_user_render(hip_context& ctx, K const& kernel, user_fra
 {
     static_assert(!USER_STACK_SIZED || !(VRH_USER_DEFER || VRH_USER_ANYHIT_CUT || VRH_USER_ANYHIT_SHARE || VRH_USER_ANYHIT_ORDERED),
                   "the deferred calls, the entry cut and the shared / ordered any_hit walks keep their state in whole LDS stack columns");
-    // the short stack while every BVH the program has taken a ref of fits it, else the whole stack
-    f.stack_entries = (USER_STACK_SIZED && user_ref_depth().load(std::memory_order_acquire) < VRH_USER_LDS_STACK) ? VRH_USER_LDS_STACK
-                                                                                                               : VRH_USER_STACK;
+    // the stack the deepest BVH the program has taken a ref of needs, at least VRH_USER_LDS_STACK and at
+    // most VRH_USER_STACK entries per thread: fewer entries, fewer bytes of LDS per block, more blocks
+    if (USER_STACK_SIZED)
+    {
+        const uint32_t need = user_ref_depth().load(std::memory_order_acquire) + 1u;
+        f.stack_entries = need < VRH_USER_LDS_STACK ? VRH_USER_LDS_STACK : need > VRH_USER_STACK ? VRH_USER_STACK : need;
+    }
+    else
+        f.stack_entries = VRH_USER_STACK;
     const size_t lds = (size_t(64) * f.stack_entries + USER_LDS_HEADER + (VRH_USER_ANYHIT_CUT ? UCUT_WORDS : 0u)
                         + (VRH_USER_DEFER ? DEFER_WORDS : 0u)) * sizeof(uint32_t);
     auto fn = user_render<K, SK, SN, NC>;
@@ -2358,11 +2364,11 @@ inline hipError_t launch_user_render(hip_context& ctx, K const& kernel, user_fra
         // one with more waves first.  The answer is cached per device ordinal (devices of different
         // architectures get their own), in atomics: 0 = not asked yet, else (waves << 8) | blocks per CU
         // of the chosen instance.  Two threads asking at once compute the same answer.
-        static std::atomic<int> wave_cache[VRH_USER_MAX_DEVICES][2];     // [device][whole stack]
+        static std::atomic<int> wave_cache[VRH_USER_MAX_DEVICES][VRH_USER_STACK + 1];     // [device][stack entries]
         auto fn5 = user_render_w5<K, SK, SN, NC>;
         auto fn6 = user_render_w6<K, SK, SN, NC>;
-        const int whole = f.stack_entries == VRH_USER_STACK ? 1 : 0;
-        int pick = (dev >= 0 && dev < VRH_USER_MAX_DEVICES) ? wave_cache[dev][whole].load(std::memory_order_acquire) : 0;
+        const uint32_t se = f.stack_entries;
+        int pick = (dev >= 0 && dev < VRH_USER_MAX_DEVICES) ? wave_cache[dev][se].load(std::memory_order_acquire) : 0;
         if (pick == 0)
         {
             pick = (1 << 8) | per_cu;
@@ -2379,7 +2385,7 @@ inline hipError_t launch_user_render(hip_context& ctx, K const& kernel, user_fra
                     break;
                 }
             }
-            if (dev >= 0 && dev < VRH_USER_MAX_DEVICES) wave_cache[dev][whole].store(pick, std::memory_order_release);
+            if (dev >= 0 && dev < VRH_USER_MAX_DEVICES) wave_cache[dev][se].store(pick, std::memory_order_release);
         }
         if ((pick >> 8) == 6) fn = fn6;
         else if ((pick >> 8) == 5) fn = fn5;
