@@ -75,11 +75,12 @@
 #endif
 #ifndef VRH_USER_LDS_STACK
 // the stack entries per thread a launch gives in LDS while every BVH the program has taken a ref of
-// (hip_index_bvh::ref) is shallower than that; VRH_USER_STACK entries once one is deeper.  LDS bounded
-// the waves per CU: 64 lanes x 32 entries are 8 KB per one-wave block, and a CU held fewer than 20;
-// with 24 entries (6 KB) a CU holds 26 and the registers bound it (C3, the AO lambda: 1.698 -> 1.549
-// ms per frame at 6 waves / SIMD, ao/main.cpp's kernel 1.662 -> 1.490; profiles/r06/user_lds/).  The
-// opt-in walks below that keep their own state in the stack columns always take the whole stack.
+// (hip_index_bvh::ref) is shallower than that; once one is deeper, the depth + 1 it needs (at most
+// VRH_USER_STACK).  LDS bounded the waves per CU: 64 lanes x 32 entries are 8 KB per one-wave block,
+// and a CU held fewer than 20; with 24 entries (6 KB) a CU holds 26 and the registers bound it (C3,
+// the AO lambda: 1.698 -> 1.549 ms per frame at 6 waves / SIMD, ao/main.cpp's kernel 1.662 -> 1.490;
+// profiles/r06/user_lds/).  The opt-in walks below that keep their own state in the stack columns
+// always take the whole stack.
 #if VRH_USER_DEFER || VRH_USER_ANYHIT_CUT || VRH_USER_ANYHIT_SHARE || VRH_USER_ANYHIT_ORDERED
 #define VRH_USER_LDS_STACK VRH_USER_STACK
 #else
