@@ -13,6 +13,7 @@ tests/cpp/user_kernels.hip (built by visionaray_amd/Makefile `cpp_tests`) render
   * list  -- the AO kernel over a list of two BVH refs with a scissor box (fixtures: list_*);
   * isect -- the mask case with the intersector passed in the sched params (kernel(isect, r, x, y)).
 """
+import json
 import os
 import subprocess
 import sys
@@ -311,3 +312,15 @@ def test_user_kernel_program_is_built():
     """build() compiled the user-kernel programs for gfx950 (they travel to the GPU box with the tree)."""
     for b in (BIN, DEFER_BIN, SHARE_BIN, CUT_BIN, OCA_BIN):
         assert os.path.exists(b), f"{b}: run __graft_entry__.build() (make -C visionaray_amd cpp_tests)"
+
+
+@pytest.mark.gpu
+def test_user_kernel_launch_takes_short_stacks_and_six_waves():
+    """The AO lambda's launch on hf1M (a BVH 20 levels deep): 24 LDS stack entries per thread and the
+    6-wave instance, 24 one-wave blocks per CU (hip_kernels.h launch_user_render; the bench line's
+    user_kernel.launch) -- LDS, not registers, had held the user kernels under 5 waves per SIMD."""
+    r = subprocess.run([BIN, "bench", "708", "1920", "1080", "/tmp", "1", "32"], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rec = next(json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{") and "frame_ms_median" in ln)
+    assert rec["launch"]["stack_entries"] == 24
+    assert rec["launch"]["waves_target"] == 6 and rec["launch"]["blocks_per_cu"] == 24
