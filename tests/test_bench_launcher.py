@@ -87,3 +87,24 @@ def test_spawn_ranks_propagates_a_failing_rank(tmp_path):
     finally:
         bench.__file__ = orig
     assert rc == 5
+
+
+def test_user_program_leg_reports_the_launch_choice(tmp_path, monkeypatch):
+    """bench.py's user-kernel leg (user_program_run) takes the program's median frame time and passes
+    its launch choice (register target, blocks per CU, LDS stack entries) into the line; a failing or
+    absent program gives an error / null, never a number."""
+    tests_dir = tmp_path / "build" / "tests"
+    tests_dir.mkdir(parents=True)
+    prog = tests_dir / "fake_uk"
+    prog.write_text("#!/bin/sh\necho '{\"mode\":\"bench\",\"frame_ms_median\":1.5,\"launches\":4,\"frames_per_launch\":32,"
+                    "\"launch\":{\"waves_target\":6,\"blocks_per_cu\":24,\"stack_entries\":24,\"grid\":6144}}'\n")
+    prog.chmod(0o755)
+    bad = tests_dir / "bad_uk"
+    bad.write_text("#!/bin/sh\nexit 3\n")
+    bad.chmod(0o755)
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    leg = bench.user_program_run("fake_uk", 1920, 1080, 15_000_000)
+    assert leg["mrays"] == 10000.0 and leg["frame_ms_median"] == 1.5
+    assert leg["launch"] == {"waves_target": 6, "blocks_per_cu": 24, "stack_entries": 24, "grid": 6144}
+    assert "error" in bench.user_program_run("bad_uk", 1920, 1080, 15_000_000)
+    assert bench.user_program_run("absent_uk", 1920, 1080, 15_000_000) is None
